@@ -1,0 +1,268 @@
+"""langstream_amd.ops -- the compute path.
+
+Every function dispatches on the device of its inputs:
+
+* GPU tensors -> the hand-written gfx950 HIP kernels in ``ops/csrc`` (module
+  ``_hip_ops``, built in-tree by ``langstream_amd._build``).  If the extension is
+  missing on a GPU we raise -- there is NO silent eager fallback on the GPU.
+* CPU tensors -> ``ops.reference`` (plain fp32 PyTorch), used by the CPU test
+  suite and the CPU plumbing pipeline.
+
+Plain dense GEMMs are not here: they go to hipBLASLt through ``torch.matmul`` /
+``torch.nn.functional.linear`` (allowed for library GEMMs); everything fused or
+attention-shaped is ours.
+"""
+from __future__ import annotations
+
+import importlib.machinery
+import importlib.util
+import os
+import sys
+from typing import Optional, Sequence
+
+import torch
+
+from . import reference as ref
+
+KV_BLOCK = 64
+PREFILL_ROWS = 128  # query rows per prefill-attention workgroup (see attention_prefill.hip)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_SO = os.path.join(_HERE, "_hip_ops.so")
+_ext = None
+_ext_err: Optional[BaseException] = None
+
+
+def _load():
+    global _ext, _ext_err
+    if _ext is not None or _ext_err is not None:
+        return _ext
+    try:
+        if not os.path.exists(_SO):
+            raise ImportError(f"{_SO} not built (run python -m langstream_amd._build)")
+        loader = importlib.machinery.ExtensionFileLoader("_hip_ops", _SO)
+        spec = importlib.util.spec_from_file_location("_hip_ops", _SO, loader=loader)
+        mod = importlib.util.module_from_spec(spec)
+        loader.exec_module(mod)
+        sys.modules["langstream_amd.ops._hip_ops"] = mod
+        _ext = mod
+    except BaseException as e:  # noqa: BLE001 - remember and re-raise on GPU use
+        _ext_err = e
+    return _ext
+
+
+def hip_available() -> bool:
+    return _load() is not None
+
+
+def hip() :
+    """The native module; raises loudly when it cannot be loaded."""
+    m = _load()
+    if m is None:
+        raise RuntimeError(f"langstream_amd HIP kernels unavailable: {_ext_err!r}")
+    return m
+
+
+def _gpu(*ts) -> bool:
+    return any(isinstance(t, torch.Tensor) and t.is_cuda for t in ts)
+
+
+# ---------------------------------------------------------------- norms
+def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    if _gpu(x):
+        out = torch.empty_like(x) if out is None else out
+        hip().rmsnorm(out, x, w, eps)
+        return out
+    r = ref.rmsnorm(x, w, eps)
+    if out is not None:
+        out.copy_(r)
+        return out
+    return r
+
+
+def fused_add_rmsnorm(x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor, eps: float) -> None:
+    """In place: residual += x ; x = rmsnorm(residual) * w."""
+    if _gpu(x):
+        hip().fused_add_rmsnorm(x, residual, w, eps)
+    else:
+        ref.fused_add_rmsnorm(x, residual, w, eps)
+
+
+def layernorm(x, g, b, eps, bias=None, residual=None, out=None):
+    if _gpu(x):
+        out = torch.empty_like(x) if out is None else out
+        hip().layernorm(out, x, bias, residual, g, b, eps)
+        return out
+    r = ref.layernorm(x, bias, residual, g, b, eps)
+    if out is not None:
+        out.copy_(r)
+        return out
+    return r
+
+
+def embed_layernorm(ids, pos_ids, type_ids, wte, wpe, wtt, g, b, eps):
+    if _gpu(wte):
+        out = torch.empty(ids.numel(), wte.shape[1], dtype=wte.dtype, device=wte.device)
+        hip().embed_layernorm(out, ids, pos_ids, type_ids, wte, wpe, wtt, g, b, eps)
+        return out
+    return ref.embed_layernorm(ids, pos_ids, type_ids, wte, wpe, wtt, g, b, eps)
+
+
+# ---------------------------------------------------------------- activations
+def silu_and_mul(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    if _gpu(x):
+        F = x.shape[-1] // 2
+        out = torch.empty(*x.shape[:-1], F, dtype=x.dtype, device=x.device) if out is None else out
+        hip().silu_and_mul(out, x)
+        return out
+    return ref.silu_and_mul(x)
+
+
+def bias_gelu_(x: torch.Tensor, bias: Optional[torch.Tensor]) -> torch.Tensor:
+    if _gpu(x):
+        hip().bias_gelu(x, bias)
+        return x
+    x.copy_(ref.bias_gelu(x, bias))
+    return x
+
+
+# ---------------------------------------------------------------- rope / kv cache
+def rope_and_cache(qkv, pos, cos_sin, slots, k_cache, v_cache, Hq: int, Hkv: int, apply_rope: bool = True):
+    if _gpu(qkv):
+        hip().rope_and_cache(qkv, pos, cos_sin, slots, k_cache, v_cache, Hq, Hkv, apply_rope)
+    else:
+        ref.rope_and_cache(qkv, pos, cos_sin, slots, k_cache, v_cache, Hq, Hkv, apply_rope)
+
+
+# ---------------------------------------------------------------- attention
+def decode_splits(max_ctx: int, batch_kv_pairs: int, n_cu: int = 256) -> tuple[int, int]:
+    """Split-KV plan for decode: enough workgroups to fill the chip (>= 2 per CU)
+    without splitting short contexts."""
+    nblk = max(1, (max_ctx + KV_BLOCK - 1) // KV_BLOCK)
+    want = max(1, (2 * n_cu + batch_kv_pairs - 1) // max(1, batch_kv_pairs))
+    nsplit = max(1, min(want, nblk // 4 if nblk >= 8 else 1, 32))
+    bps = (nblk + nsplit - 1) // nsplit
+    nsplit = (nblk + bps - 1) // bps
+    return nsplit, bps
+
+
+def paged_decode_attention(q, k_cache, v_cache, block_tables, ctx_lens, scale, out=None,
+                           nsplit: int = 1, blocks_per_split: int = 1 << 30, workspace=None):
+    """q: [B, Hq*D] (may be a strided view into the QKV buffer); returns [B, Hq*D]."""
+    B = ctx_lens.shape[0]
+    D = k_cache.shape[3]
+    Hq = q.shape[-1] // D if q.dim() == 2 else q.shape[1]
+    if _gpu(q):
+        out = torch.empty(B, Hq * D, dtype=q.dtype, device=q.device) if out is None else out
+        if nsplit > 1:
+            assert workspace is not None and workspace.numel() >= B * Hq * nsplit * (D + 2)
+        ws = workspace if workspace is not None else out.new_empty(0, dtype=torch.float32)
+        hip().paged_decode_attention(out, q, k_cache, v_cache, block_tables, ctx_lens, scale, nsplit,
+                                     min(blocks_per_split, block_tables.shape[1]), ws)
+        return out
+    r = ref.paged_decode_attention(q.reshape(B, Hq, D), k_cache, v_cache, block_tables, ctx_lens, scale)
+    return r.reshape(B, Hq * D)
+
+
+def prefill_tiles(q_lens: Sequence[int], G: int, prefix_lens: Sequence[int] | None = None) -> torch.Tensor:
+    """Work list for the prefill kernel: (seq, first row), rows = token*G + g, heaviest first."""
+    tiles = []
+    for s, ql in enumerate(q_lens):
+        rows = ql * G
+        pre = prefix_lens[s] if prefix_lens is not None else 0
+        for r0 in range(0, rows, PREFILL_ROWS):
+            last = min(r0 + PREFILL_ROWS, rows) - 1
+            tiles.append((pre + last // G, s, r0))
+    tiles.sort(key=lambda t: -t[0])
+    t = torch.tensor([(s, r0) for _, s, r0 in tiles], dtype=torch.int32)
+    return t.reshape(-1, 2)
+
+
+def paged_prefill_attention(q, k_cache, v_cache, block_tables, q_start, q_len, ctx_len, tiles, Hq, scale,
+                            out=None):
+    T = q.shape[0]
+    D = k_cache.shape[3]
+    if _gpu(q):
+        out = torch.empty(T, Hq * D, dtype=q.dtype, device=q.device) if out is None else out
+        hip().paged_prefill_attention(out, q, k_cache, v_cache, block_tables, q_start, q_len, ctx_len, tiles,
+                                      Hq, scale)
+        return out
+    return ref.paged_prefill_attention(q, k_cache, v_cache, block_tables, q_start, q_len, ctx_len, Hq, scale)
+
+
+def varlen_encoder_attention(qkv, q_start, q_len, tiles, Hq, Hkv, scale, out=None):
+    T = qkv.shape[0]
+    D = qkv.shape[1] // (Hq + 2 * Hkv)
+    if _gpu(qkv):
+        out = torch.empty(T, Hq * D, dtype=qkv.dtype, device=qkv.device) if out is None else out
+        hip().varlen_encoder_attention(out, qkv, q_start, q_len, tiles, Hq, Hkv, scale)
+        return out
+    return ref.varlen_encoder_attention(qkv, q_start, q_len, Hq, Hkv, scale)
+
+
+# ---------------------------------------------------------------- sampling
+def sample(logits, temperature, top_k, top_p, seeds, steps, n_top: int = 0):
+    """Returns (tokens int32 [B], logprobs f32 [B], top_ids [B,n]|None, top_lps [B,n]|None)."""
+    B = logits.shape[0]
+    if _gpu(logits):
+        dev = logits.device
+        tok = torch.empty(B, dtype=torch.int32, device=dev)
+        lp = torch.empty(B, dtype=torch.float32, device=dev)
+        ti = torch.empty(B * max(n_top, 1), dtype=torch.int32, device=dev)
+        tl = torch.empty(B * max(n_top, 1), dtype=torch.float32, device=dev)
+        hip().sample_tokens(logits, temperature, top_k, top_p, seeds, steps, tok, lp, ti, tl, n_top)
+        if n_top:
+            return tok, lp, ti.view(B, n_top), tl.view(B, n_top)
+        return tok, lp, None, None
+    gens = []
+    for r in range(B):
+        g = torch.Generator()
+        g.manual_seed(int(seeds[r]) * 1_000_003 + int(steps[r]))
+        gens.append(g)
+    tok, lp = ref.sample(logits, temperature, top_k, top_p, gens)
+    if n_top:
+        logp = torch.log_softmax(logits.float(), -1)
+        v, i = torch.topk(logp, n_top, dim=-1)
+        return tok, lp, i.int(), v
+    return tok, lp, None, None
+
+
+def apply_logit_deltas(logits, rows, toks, delta):
+    if _gpu(logits):
+        hip().apply_logit_deltas(logits, rows, toks, delta)
+    else:
+        for r, t, d in zip(rows.tolist(), toks.tolist(), delta.tolist()):
+            if 0 <= t < logits.shape[1]:
+                logits[r, t] += d
+
+
+# ---------------------------------------------------------------- embeddings / vectors
+def pool_embeddings(x, start, length, mode: int, normalize: bool, out_dtype=torch.float32):
+    if _gpu(x):
+        out = torch.empty(start.numel(), x.shape[1], dtype=out_dtype, device=x.device)
+        hip().pool_embeddings(out, x, start, length, mode, normalize)
+        return out
+    return ref.pool_embeddings(x, start, length, mode, normalize).to(out_dtype)
+
+
+def l2_normalize_rows(x):
+    if _gpu(x):
+        out = torch.empty_like(x)
+        hip().l2_normalize_rows(out, x)
+        return out
+    return torch.nn.functional.normalize(x.float(), dim=-1, eps=1e-12).to(x.dtype)
+
+
+def knn_topk(X, Q, k: int):
+    """Top-k rows of X by dot product with each query row.  Returns (scores f32 [Q,k], idx int32 [Q,k])."""
+    if _gpu(X):
+        Qn, N = Q.shape[0], X.shape[0]
+        nchunks = (N + 1023) // 1024
+        dev = X.device
+        out_s = torch.empty(Qn, k, dtype=torch.float32, device=dev)
+        out_i = torch.empty(Qn, k, dtype=torch.int32, device=dev)
+        ws_s = torch.empty(max(1, Qn * nchunks * k), dtype=torch.float32, device=dev)
+        ws_i = torch.empty(max(1, Qn * nchunks * k), dtype=torch.int32, device=dev)
+        hip().knn_topk(X, Q, k, out_s, out_i, ws_s, ws_i)
+        return out_s, out_i
+    return ref.knn_topk(X, Q, k)

@@ -1,0 +1,252 @@
+// Paged GQA decode attention on MFMA (gfx950, mfma_f32_16x16x32_bf16).
+//
+// One query token per sequence.  Work unit = one (sequence, kv-head) pair; its G
+// query heads (G = Hq/Hkv <= 16) are the 16 MFMA "rows" (padded with zero rows).
+//
+// Layout trick (no LDS, no transposes): with the V cache stored transposed
+// ([NB, Hkv, D, BS]) and the scores computed SWAPPED (S^T = K * Q^T), every MFMA
+// operand of both products is one 16-B contiguous global load per lane and the
+// softmax statistics stay lane-local:
+//   S^T tile kt=(2*kg+e):  A = K rows, lane i=l&15 loads key 32kg + 8(i>>2) + 4e + (i&3)
+//                          B = Q^T (registers), acc[r] = S[key 32kg+8h+4e+r][qrow l&15]
+//   O^T tile dt:           A = V^T rows d=16dt+i, keys 32kg+8h..+7 (16 B)
+//                          B = P^T: element j of lane-group h is key 32kg+8h+j, which is
+//                          exactly acc(kt=2kg+(j>>2))[j&3] of the same lane.
+// The K-row permutation above is what makes the P^T fragment lane-local.
+//
+// Grid: (B*Hkv, S splits).  4 waves per workgroup stride over the split's KV blocks
+// and are merged through LDS; with S > 1 a second kernel merges the splits.
+#include <torch/extension.h>
+#include <ATen/hip/HIPContext.h>
+#include "common.h"
+
+namespace {
+
+constexpr int BS = 64;  // tokens per KV block (engine-wide constant)
+constexpr float LOG2E = 1.4426950408889634f;
+
+template <int D>
+__global__ void __launch_bounds__(256) decode_attn_kernel(
+    bf16* __restrict__ out, const bf16* __restrict__ q, int64_t q_stride, const bf16* __restrict__ kc,
+    const bf16* __restrict__ vc, const int32_t* __restrict__ block_tables, int max_blocks,
+    const int32_t* __restrict__ ctx_lens, int Hkv, int G, int NB, float scale_log2, int blocks_per_split,
+    float* __restrict__ part_o, float* __restrict__ part_ml) {
+  constexpr int KS = D / 32;  // k-steps over the head dim
+  constexpr int DT = D / 16;  // 16-wide output tiles over the head dim
+  __shared__ float sh_o[4][16][D + 4];
+  __shared__ float sh_m[4][16], sh_l[4][16];
+
+  const int pair = blockIdx.x;
+  const int b = pair / Hkv, kvh = pair - b * Hkv;
+  const int split = blockIdx.y, nsplit = gridDim.y;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int i16 = lane & 15, h = lane >> 4;
+
+  const int ctx = ctx_lens[b];
+  int nblk = (ctx + BS - 1) / BS;
+  nblk = min(nblk, max_blocks);
+  const int bstart = split * blocks_per_split;
+  const int bend = min(nblk, bstart + blocks_per_split);
+
+  // Q^T fragments (B operand): lane holds Q[head kvh*G + i16][32ks + 8h .. +7]
+  bf16x8 qf[KS];
+  const bool qrow_valid = i16 < G;
+  const bf16* qp = q + (int64_t)b * q_stride + (int64_t)(kvh * G + (qrow_valid ? i16 : 0)) * D + 8 * h;
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    uint4 v = qrow_valid ? ld16(qp + 32 * ks) : make_uint4(0, 0, 0, 0);
+    qf[ks] = __builtin_bit_cast(bf16x8, v);
+  }
+
+  f32x4 o[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m = -1e30f, l = 0.f;
+
+  const int32_t* bt = block_tables + (int64_t)b * max_blocks;
+  for (int bi = bstart + wid; bi < bend; bi += 4) {
+    const int blk = min(max(bt[bi], 0), NB - 1);
+    const bf16* kb = kc + ((int64_t)blk * Hkv + kvh) * BS * D;
+    const bf16* vb = vc + ((int64_t)blk * Hkv + kvh) * D * BS;
+    // ---- S^T = K Q^T for the 64 keys of this block (4 tiles of 16 keys)
+    f32x4 s[4];
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) {
+      const int kg = kt >> 1, e = kt & 1;
+      const int key = 32 * kg + 8 * (i16 >> 2) + 4 * e + (i16 & 3);
+      const bf16* kr = kb + key * D + 8 * h;
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const bf16x8 a = __builtin_bit_cast(bf16x8, ld16(kr + 32 * ks));
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, qf[ks], acc, 0, 0, 0);
+      }
+      s[kt] = acc;
+    }
+    // ---- online softmax (row = qrow = lane&15; this lane holds 16 of the 64 keys)
+    const int kbase = bi * BS;
+    float mx = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = kbase + 32 * (kt >> 1) + 8 * h + 4 * (kt & 1) + r;
+        float v = s[kt][r] * scale_log2;
+        v = key < ctx ? v : -INFINITY;
+        s[kt][r] = v;
+        mx = fmaxf(mx, v);
+      }
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mnew = fmaxf(m, mx);
+    const float alpha = exp2f(m - mnew);
+    float psum = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float p = exp2f(s[kt][r] - mnew);
+        s[kt][r] = p;
+        psum += p;
+      }
+    }
+    psum += __shfl_xor(psum, 16, 64);
+    psum += __shfl_xor(psum, 32, 64);
+    l = l * alpha + psum;
+    m = mnew;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) o[dt] *= alpha;
+    // ---- O^T += V^T P^T
+#pragma unroll
+    for (int kg = 0; kg < 2; ++kg) {
+      bf16x8 pf;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        pf[j] = (bf16)s[2 * kg][j];
+        pf[4 + j] = (bf16)s[2 * kg + 1][j];
+      }
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) {
+        const bf16x8 a = __builtin_bit_cast(bf16x8, ld16(vb + (16 * dt + i16) * BS + 32 * kg + 8 * h));
+        o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, pf, o[dt], 0, 0, 0);
+      }
+    }
+  }
+
+  // ---- merge the 4 waves through LDS.  o[dt][r] = O[qrow i16][d = 16dt + 4h + r]
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) sh_o[wid][i16][16 * dt + 4 * h + r] = o[dt][r];
+  if (h == 0) {
+    sh_m[wid][i16] = m;
+    sh_l[wid][i16] = l;
+  }
+  __syncthreads();
+  // 256 threads: thread -> (qrow, d-chunk of D/16)
+  const int row = threadIdx.x >> 4;   // 0..15
+  const int dc = threadIdx.x & 15;    // chunk of D/16 elements
+  constexpr int CH = D / 16;
+  if (row < G) {
+    float mw[4], mstar = -1e30f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) { mw[w] = sh_m[w][row]; mstar = fmaxf(mstar, mw[w]); }
+    float lt = 0.f, f[4];
+#pragma unroll
+    for (int w = 0; w < 4; ++w) { f[w] = exp2f(mw[w] - mstar); lt += sh_l[w][row] * f[w]; }
+    float acc[CH];
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      float a = 0.f;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) a += sh_o[w][row][dc * CH + c] * f[w];
+      acc[c] = a;
+    }
+    const int head = kvh * G + row;
+    if (nsplit == 1) {
+      const float inv = lt > 0.f ? 1.f / lt : 0.f;
+      bf16* op = out + ((int64_t)b * Hkv * G + head) * D + dc * CH;
+#pragma unroll
+      for (int c = 0; c < CH; ++c) op[c] = (bf16)(acc[c] * inv);
+    } else {
+      const int64_t pi = (((int64_t)b * Hkv * G + head) * nsplit + split);
+      float* po = part_o + pi * D + dc * CH;
+#pragma unroll
+      for (int c = 0; c < CH; ++c) po[c] = acc[c];
+      if (dc == 0) {
+        part_ml[pi * 2] = mstar;
+        part_ml[pi * 2 + 1] = lt;
+      }
+    }
+  }
+}
+
+template <int D>
+__global__ void __launch_bounds__(256) decode_merge_kernel(bf16* __restrict__ out, const float* __restrict__ part_o,
+                                                           const float* __restrict__ part_ml, int nsplit, int nrows) {
+  // one wave per (b, head) row; lanes over d
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= nrows) return;
+  const float* ml = part_ml + (int64_t)row * nsplit * 2;
+  float mstar = -1e30f;
+  for (int s = 0; s < nsplit; ++s) mstar = fmaxf(mstar, ml[2 * s]);
+  float lt = 0.f;
+  for (int s = 0; s < nsplit; ++s) lt += ml[2 * s + 1] * exp2f(ml[2 * s] - mstar);
+  const float inv = lt > 0.f ? 1.f / lt : 0.f;
+  for (int d = lane; d < D; d += 64) {
+    float a = 0.f;
+    for (int s = 0; s < nsplit; ++s) a += part_o[((int64_t)row * nsplit + s) * D + d] * exp2f(ml[2 * s] - mstar);
+    out[(int64_t)row * D + d] = (bf16)(a * inv);
+  }
+}
+
+}  // namespace
+
+// q: [B, Hq*D] view (row stride q_stride elements), out: [B, Hq, D] contiguous.
+// workspace: f32 tensor with >= B*Hq*nsplit*(D+2) elements when nsplit > 1.
+void paged_decode_attention(at::Tensor out, at::Tensor q, at::Tensor k_cache, at::Tensor v_cache,
+                            at::Tensor block_tables, at::Tensor ctx_lens, double scale, int64_t nsplit,
+                            int64_t blocks_per_split, at::Tensor workspace) {
+  TORCH_CHECK(q.is_cuda() && q.scalar_type() == at::kBFloat16 && out.scalar_type() == at::kBFloat16);
+  TORCH_CHECK(out.is_contiguous() && q.stride(-1) == 1);
+  TORCH_CHECK(k_cache.dim() == 4 && v_cache.dim() == 4);
+  const int Hkv = k_cache.size(1), D = k_cache.size(3);
+  TORCH_CHECK(k_cache.size(2) == BS && v_cache.size(3) == BS && v_cache.size(2) == D, "KV block size must be 64");
+  const int B = ctx_lens.numel();
+  TORCH_CHECK(out.numel() % ((int64_t)B * D) == 0);
+  const int Hq = out.numel() / ((int64_t)B * D);
+  TORCH_CHECK(Hq % Hkv == 0);
+  const int G = Hq / Hkv;
+  TORCH_CHECK(G <= 16, "GQA group too large for the 16-row MFMA tile");
+  TORCH_CHECK(block_tables.scalar_type() == at::kInt && block_tables.is_contiguous() && block_tables.size(0) == B);
+  TORCH_CHECK(ctx_lens.scalar_type() == at::kInt && ctx_lens.is_contiguous());
+  TORCH_CHECK(nsplit >= 1 && blocks_per_split >= 1);
+  const int64_t q_stride = q.dim() >= 2 ? q.stride(0) : (int64_t)Hq * D;
+  TORCH_CHECK(q_stride % 8 == 0);
+  if (B == 0) return;
+  float* po = nullptr;
+  float* pml = nullptr;
+  if (nsplit > 1) {
+    TORCH_CHECK(workspace.scalar_type() == at::kFloat && workspace.numel() >= (int64_t)B * Hq * nsplit * (D + 2));
+    po = workspace.data_ptr<float>();
+    pml = po + (int64_t)B * Hq * nsplit * D;
+  }
+  auto stream = at::hip::getCurrentHIPStream();
+  dim3 grid(B * Hkv, nsplit);
+  const float sl2 = (float)scale * LOG2E;
+#define LAUNCH(DD)                                                                                               \
+  decode_attn_kernel<DD><<<grid, 256, 0, stream>>>((bf16*)out.data_ptr(), (const bf16*)q.data_ptr(), q_stride, \
+                                                   (const bf16*)k_cache.data_ptr(), (const bf16*)v_cache.data_ptr(), \
+                                                   block_tables.data_ptr<int32_t>(), (int)block_tables.size(1),  \
+                                                   ctx_lens.data_ptr<int32_t>(), Hkv, G, (int)k_cache.size(0),    \
+                                                   sl2, (int)blocks_per_split, po, pml);                          \
+  if (nsplit > 1)                                                                                                \
+    decode_merge_kernel<DD><<<(B * Hq + 3) / 4, 256, 0, stream>>>((bf16*)out.data_ptr(), po, pml, (int)nsplit,   \
+                                                                  B * Hq)
+  if (D == 128) { LAUNCH(128); }
+  else if (D == 64) { LAUNCH(64); }
+  else TORCH_CHECK(false, "unsupported head dim ", D);
+#undef LAUNCH
+}

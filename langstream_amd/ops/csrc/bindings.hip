@@ -1,0 +1,48 @@
+// Python bindings for the langstream_amd HIP kernels (module `_hip_ops`).
+#include <torch/extension.h>
+
+void rmsnorm(at::Tensor out, at::Tensor x, at::Tensor w, double eps);
+void fused_add_rmsnorm(at::Tensor x, at::Tensor residual, at::Tensor w, double eps);
+void layernorm(at::Tensor out, at::Tensor x, c10::optional<at::Tensor> bias, c10::optional<at::Tensor> residual,
+               at::Tensor g, at::Tensor b, double eps);
+void embed_layernorm(at::Tensor out, at::Tensor ids, at::Tensor pos_ids, c10::optional<at::Tensor> type_ids,
+                     at::Tensor wte, at::Tensor wpe, at::Tensor wtt, at::Tensor g, at::Tensor b, double eps);
+void silu_and_mul(at::Tensor out, at::Tensor x);
+void bias_gelu(at::Tensor x, c10::optional<at::Tensor> bias);
+void rope_and_cache(at::Tensor qkv, at::Tensor pos, at::Tensor cos_sin, at::Tensor slots, at::Tensor k_cache,
+                    at::Tensor v_cache, int64_t Hq, int64_t Hkv, bool apply_rope);
+void paged_decode_attention(at::Tensor out, at::Tensor q, at::Tensor k_cache, at::Tensor v_cache,
+                            at::Tensor block_tables, at::Tensor ctx_lens, double scale, int64_t nsplit,
+                            int64_t blocks_per_split, at::Tensor workspace);
+void paged_prefill_attention(at::Tensor out, at::Tensor q, at::Tensor k_cache, at::Tensor v_cache,
+                             at::Tensor block_tables, at::Tensor q_start, at::Tensor q_len, at::Tensor ctx_len,
+                             at::Tensor tiles, int64_t Hq, double scale);
+void varlen_encoder_attention(at::Tensor out, at::Tensor qkv, at::Tensor q_start, at::Tensor q_len,
+                              at::Tensor tiles, int64_t Hq, int64_t Hkv, double scale);
+void sample_tokens(at::Tensor logits, at::Tensor temperature, at::Tensor top_k, at::Tensor top_p, at::Tensor seeds,
+                   at::Tensor steps, at::Tensor out_tok, at::Tensor out_lp, at::Tensor top_ids, at::Tensor top_lps,
+                   int64_t n_top);
+void apply_logit_deltas(at::Tensor logits, at::Tensor rows, at::Tensor toks, at::Tensor delta);
+void pool_embeddings(at::Tensor out, at::Tensor x, at::Tensor start, at::Tensor len, int64_t mode, bool normalize);
+void l2_normalize_rows(at::Tensor out, at::Tensor x);
+void knn_topk(at::Tensor X, at::Tensor Q, int64_t K, at::Tensor out_s, at::Tensor out_i, at::Tensor ws_s,
+              at::Tensor ws_i);
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "langstream_amd CDNA4 (gfx950) kernels";
+  m.def("rmsnorm", &rmsnorm);
+  m.def("fused_add_rmsnorm", &fused_add_rmsnorm);
+  m.def("layernorm", &layernorm);
+  m.def("embed_layernorm", &embed_layernorm);
+  m.def("silu_and_mul", &silu_and_mul);
+  m.def("bias_gelu", &bias_gelu);
+  m.def("rope_and_cache", &rope_and_cache);
+  m.def("paged_decode_attention", &paged_decode_attention);
+  m.def("paged_prefill_attention", &paged_prefill_attention);
+  m.def("varlen_encoder_attention", &varlen_encoder_attention);
+  m.def("sample_tokens", &sample_tokens);
+  m.def("apply_logit_deltas", &apply_logit_deltas);
+  m.def("pool_embeddings", &pool_embeddings);
+  m.def("l2_normalize_rows", &l2_normalize_rows);
+  m.def("knn_topk", &knn_topk);
+}

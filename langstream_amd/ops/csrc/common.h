@@ -1,0 +1,81 @@
+// Shared helpers for the langstream_amd CDNA4 (gfx950) kernels.
+//
+// Conventions used by every kernel in this directory:
+//  * bf16 tensors are handled as `__bf16` (clang native type); f32->bf16 uses the
+//    plain cast, which hipcc lowers to v_cvt_pk_bf16_f32 on gfx950 (NaN-safe).
+//  * memory-bound kernels move 16 B per lane (8 x bf16) per access (guide G13).
+//  * wave = 64 lanes; reductions use __shfl_xor over 64 lanes.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define LS_WAVE 64
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ float bf2f(bf16 x) { return (float)x; }
+__device__ __forceinline__ bf16 f2bf(float x) { return (bf16)x; }
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Block-wide sum for blockDim.x <= 1024 (multiple of 64).  `red` must hold
+// blockDim.x/64 floats of LDS.  Result is broadcast to every thread.
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  v = wave_sum(v);
+  __syncthreads();
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  float t = 0.f;
+  for (int i = 0; i < nw; ++i) t += red[i];
+  return t;
+}
+
+__device__ __forceinline__ float block_max(float v, float* red) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  v = wave_max(v);
+  __syncthreads();
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  float t = -INFINITY;
+  for (int i = 0; i < nw; ++i) t = fmaxf(t, red[i]);
+  return t;
+}
+
+__device__ __forceinline__ uint4 ld16(const void* p) { return *reinterpret_cast<const uint4*>(p); }
+__device__ __forceinline__ void st16(void* p, uint4 v) { *reinterpret_cast<uint4*>(p) = v; }
+
+__device__ __forceinline__ void unpack8(uint4 v, float* f) {
+  const bf16x8 b = __builtin_bit_cast(bf16x8, v);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) f[i] = (float)b[i];
+}
+
+__device__ __forceinline__ uint4 pack8(const float* f) {
+  bf16x8 b;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) b[i] = (bf16)f[i];
+  return __builtin_bit_cast(uint4, b);
+}
+
+// XCD-aware bijective remap of a linear workgroup id (guide §5 "XCD swizzle
+// must be bijective"): consecutive logical tiles land on the same XCD so they
+// share that XCD's L2.  Speed only -- never relied on for correctness.
+__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
+  const int q = nwg / 8, r = nwg % 8, xcd = orig % 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
+}

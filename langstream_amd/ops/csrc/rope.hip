@@ -1,0 +1,125 @@
+// RoPE + paged-KV cache write, fused (one pass over the QKV projection output).
+//
+// qkv      : [T, (Hq + 2*Hkv) * D] bf16, rotated IN PLACE for the q and k heads
+// pos      : [T] int32 absolute positions
+// cos_sin  : [max_pos, D] f32 table; cols [0, D/2) = cos, [D/2, D) = sin (host-built,
+//            includes any rope scaling; no device trig -- guide App. B "element-wise")
+// slots    : [T] int64 cache slot = block * BS + offset (-1 = do not cache)
+// k_cache  : [NB, Hkv, BS, D]   (token-major rows: 256-B contiguous per token & head)
+// v_cache  : [NB, Hkv, D, BS]   (TRANSPOSED: keys contiguous, so attention reads V^T
+//            MFMA fragments with one 16-B load per lane -- see attention kernels)
+//
+// A workgroup handles 64 consecutive tokens.  Phase 1 rotates q/k (16-B vectors,
+// HF "rotate_half" convention) and stores rotated K rows.  Phase 2 stages V for one
+// kv head at a time in LDS and writes it transposed with lane == token, so a wave's
+// 2-B stores for one head-dim d land on consecutive cache addresses.
+#include <torch/extension.h>
+#include <ATen/hip/HIPContext.h>
+#include "common.h"
+
+namespace {
+
+constexpr int TOK = 64;
+
+template <int D>
+__global__ void __launch_bounds__(256) rope_cache_kernel(bf16* __restrict__ qkv, const int32_t* __restrict__ pos,
+                                                         const float* __restrict__ cos_sin,
+                                                         const int64_t* __restrict__ slots, bf16* __restrict__ kc,
+                                                         bf16* __restrict__ vc, int64_t T, int Hq, int Hkv, int BS,
+                                                         int max_pos, int apply_rope, int64_t nslots) {
+  __shared__ __attribute__((aligned(16))) bf16 vt[TOK][D + 8];
+  const int64_t t0 = (int64_t)blockIdx.x * TOK;
+  const int ntok = (int)min((int64_t)TOK, T - t0);
+  const int row_elems = (Hq + 2 * Hkv) * D;
+  constexpr int HALF = D / 2;
+  constexpr int VPH = HALF / 8;  // 16-B vectors per half head
+  // ---- phase 1: rotate q and k heads, write k to the cache
+  const int tasks = ntok * (Hq + Hkv) * VPH;
+  for (int i = threadIdx.x; i < tasks; i += blockDim.x) {
+    const int tl = i / ((Hq + Hkv) * VPH);
+    const int rem = i - tl * (Hq + Hkv) * VPH;
+    const int h = rem / VPH, c = rem - h * VPH;
+    const int64_t t = t0 + tl;
+    bf16* base = qkv + t * row_elems + h * D;  // k heads follow q heads contiguously
+    float a[8], b[8];
+    unpack8(ld16(base + c * 8), a);
+    unpack8(ld16(base + HALF + c * 8), b);
+    if (apply_rope) {
+      const int p = min(max(pos[t], 0), max_pos - 1);
+      const float* cs = cos_sin + (int64_t)p * D;
+      float co[8], si[8];
+      *reinterpret_cast<float4*>(co) = *reinterpret_cast<const float4*>(cs + c * 8);
+      *reinterpret_cast<float4*>(co + 4) = *reinterpret_cast<const float4*>(cs + c * 8 + 4);
+      *reinterpret_cast<float4*>(si) = *reinterpret_cast<const float4*>(cs + HALF + c * 8);
+      *reinterpret_cast<float4*>(si + 4) = *reinterpret_cast<const float4*>(cs + HALF + c * 8 + 4);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float x1 = a[j], x2 = b[j];
+        a[j] = x1 * co[j] - x2 * si[j];
+        b[j] = x2 * co[j] + x1 * si[j];
+      }
+    }
+    const uint4 pa = pack8(a), pb = pack8(b);
+    st16(base + c * 8, pa);
+    st16(base + HALF + c * 8, pb);
+    if (h >= Hq) {
+      const int64_t s = slots[t];
+      if (s >= 0 && s < nslots) {
+        const int64_t blk = s / BS, off = s - blk * BS;
+        bf16* kd = kc + ((blk * Hkv + (h - Hq)) * BS + off) * D;
+        st16(kd + c * 8, pa);
+        st16(kd + HALF + c * 8, pb);
+      }
+    }
+  }
+  // ---- phase 2: V, transposed through LDS
+  const int lane_tok = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  int64_t my_slot = lane_tok < ntok ? slots[t0 + lane_tok] : -1;
+  if (my_slot >= nslots) my_slot = -1;
+  for (int hv = 0; hv < Hkv; ++hv) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < ntok * (D / 8); i += blockDim.x) {
+      const int tl = i / (D / 8), c = i - tl * (D / 8);
+      const bf16* src = qkv + (t0 + tl) * row_elems + (Hq + Hkv + hv) * D + c * 8;
+      *reinterpret_cast<uint4*>(&vt[tl][c * 8]) = ld16(src);
+    }
+    __syncthreads();
+    if (my_slot >= 0) {
+      const int64_t blk = my_slot / BS, off = my_slot - blk * BS;
+      bf16* vd = vc + ((blk * Hkv + hv) * (int64_t)D) * BS + off;
+      for (int d = wid; d < D; d += 4) vd[(int64_t)d * BS] = vt[lane_tok][d];
+    }
+  }
+}
+
+}  // namespace
+
+void rope_and_cache(at::Tensor qkv, at::Tensor pos, at::Tensor cos_sin, at::Tensor slots, at::Tensor k_cache,
+                    at::Tensor v_cache, int64_t Hq, int64_t Hkv, bool apply_rope) {
+  TORCH_CHECK(qkv.is_cuda() && qkv.scalar_type() == at::kBFloat16 && qkv.is_contiguous());
+  TORCH_CHECK(pos.scalar_type() == at::kInt && slots.scalar_type() == at::kLong);
+  TORCH_CHECK(cos_sin.scalar_type() == at::kFloat && cos_sin.is_contiguous());
+  TORCH_CHECK(k_cache.scalar_type() == at::kBFloat16 && v_cache.scalar_type() == at::kBFloat16);
+  TORCH_CHECK(k_cache.dim() == 4 && v_cache.dim() == 4);
+  const int D = k_cache.size(3);
+  const int BS = k_cache.size(2);
+  TORCH_CHECK(k_cache.size(1) == Hkv && v_cache.size(1) == Hkv && v_cache.size(2) == D && v_cache.size(3) == BS);
+  TORCH_CHECK(qkv.size(-1) == (Hq + 2 * Hkv) * D);
+  const int64_t T = qkv.numel() / qkv.size(-1);
+  TORCH_CHECK(pos.numel() == T && slots.numel() == T);
+  TORCH_CHECK(cos_sin.size(1) == D);
+  if (T == 0) return;
+  auto stream = at::hip::getCurrentHIPStream();
+  const int grid = (int)((T + TOK - 1) / TOK);
+#define LAUNCH(DD)                                                                                          \
+  rope_cache_kernel<DD><<<grid, 256, 0, stream>>>((bf16*)qkv.data_ptr(), pos.data_ptr<int32_t>(),          \
+                                                  cos_sin.data_ptr<float>(), slots.data_ptr<int64_t>(),     \
+                                                  (bf16*)k_cache.data_ptr(), (bf16*)v_cache.data_ptr(), T,  \
+                                                  (int)Hq, (int)Hkv, BS, (int)cos_sin.size(0), apply_rope ? 1 : 0, \
+                                                  (int64_t)k_cache.size(0) * BS)
+  if (D == 128) LAUNCH(128);
+  else if (D == 64) LAUNCH(64);
+  else TORCH_CHECK(false, "unsupported head dim ", D);
+#undef LAUNCH
+}

@@ -1,0 +1,273 @@
+// Token sampling + log-probs for the decode loop (one workgroup of 1024 threads per
+// sequence row; rows of 128K logits are streamed 16 B per lane, 2-3 passes, L2-hot).
+//
+// Per row r (all params are device tensors so the launch is graph-capturable):
+//   temperature[r] <= 0  -> greedy argmax
+//   otherwise            -> Gumbel-max sampling from softmax(logits / T), optionally
+//                           restricted by top_k[r] (>0) and top_p[r] (<1).  The cut is
+//                           found with a 2048-bin LDS histogram of (logit - max)/T over
+//                           [-32, 0] nats; the cutoff bin is kept whole (documented
+//                           approximation: ties within 1/64 nat).
+// Outputs: token[r] (int32), logprob[r] = log softmax(logits)[token] at T = 1 (what
+// OpenAI-style `logprobs` and FLARE consume), and optionally the top-n alternatives.
+//
+// apply_penalties: logits[row, tok] -= presence*(cnt>0) + frequency*cnt ; += bias
+// (sparse triples; host builds them only for rows that use penalties / logit_bias).
+#include <torch/extension.h>
+#include <ATen/hip/HIPContext.h>
+#include "common.h"
+
+namespace {
+
+constexpr int NBINS = 2048;
+constexpr float RANGE = 32.f;
+
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+  return z ^ (z >> 31);
+}
+
+__device__ __forceinline__ float uniform01(uint64_t seed, uint64_t idx) {
+  const uint64_t z = mix64(seed ^ mix64(idx + 0x9e3779b97f4a7c15ULL));
+  // 24 random bits -> (0, 1)
+  return ((float)(z >> 40) + 0.5f) * (1.0f / 16777216.0f);
+}
+
+template <typename T>
+__device__ __forceinline__ float ldf(const T* p) { return (float)(*p); }
+
+struct ArgMax {
+  float v;
+  int i;
+};
+__device__ __forceinline__ ArgMax amax(ArgMax a, ArgMax b) {
+  return (b.v > a.v || (b.v == a.v && b.i < a.i)) ? b : a;
+}
+__device__ __forceinline__ ArgMax wave_argmax(ArgMax a) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    ArgMax b{__shfl_xor(a.v, o, 64), __shfl_xor(a.i, o, 64)};
+    a = amax(a, b);
+  }
+  return a;
+}
+
+template <typename T>
+__global__ void __launch_bounds__(1024) sample_kernel(const T* __restrict__ logits, int64_t row_stride, int V,
+                                                      const float* __restrict__ temperature,
+                                                      const int32_t* __restrict__ top_k,
+                                                      const float* __restrict__ top_p,
+                                                      const int64_t* __restrict__ seeds,
+                                                      const int64_t* __restrict__ steps,
+                                                      int32_t* __restrict__ out_tok, float* __restrict__ out_lp,
+                                                      int n_top, int32_t* __restrict__ top_ids,
+                                                      float* __restrict__ top_lps) {
+  __shared__ float red_f[16];
+  __shared__ int red_i[16];
+  __shared__ float hist_mass[NBINS];
+  __shared__ int hist_cnt[NBINS];
+  __shared__ int cut_bin;
+  const int row = blockIdx.x;
+  const T* lr = logits + (int64_t)row * row_stride;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const float temp = temperature[row];
+  const bool greedy = !(temp > 0.f);
+  const float invT = greedy ? 1.f : 1.f / temp;
+
+  // ---- pass 1: max, argmax, sum exp (T = 1)
+  ArgMax best{-INFINITY, 0x7fffffff};
+  float mloc = -INFINITY, sloc = 0.f;
+  for (int i = tid; i < V; i += blockDim.x) {
+    const float x = ldf(lr + i);
+    if (x > best.v) best = ArgMax{x, i};
+    if (x > mloc) {
+      sloc = sloc * __expf(mloc - x) + 1.f;
+      mloc = x;
+    } else {
+      sloc += __expf(x - mloc);
+    }
+  }
+  best = wave_argmax(best);
+  // combine (m, s) across the wave
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float mo = __shfl_xor(mloc, o, 64), so = __shfl_xor(sloc, o, 64);
+    const float mn = fmaxf(mloc, mo);
+    sloc = (mloc == -INFINITY ? 0.f : sloc * __expf(mloc - mn)) + (mo == -INFINITY ? 0.f : so * __expf(mo - mn));
+    mloc = mn;
+  }
+  __shared__ float red_m[16], red_s[16];
+  if (lane == 0) {
+    red_f[wid] = best.v;
+    red_i[wid] = best.i;
+    red_m[wid] = mloc;
+    red_s[wid] = sloc;
+  }
+  __syncthreads();
+  const int nw = blockDim.x >> 6;
+  ArgMax gbest{-INFINITY, 0x7fffffff};
+  float gm = -INFINITY;
+  for (int w = 0; w < nw; ++w) {
+    gbest = amax(gbest, ArgMax{red_f[w], red_i[w]});
+    gm = fmaxf(gm, red_m[w]);
+  }
+  float gs = 0.f;
+  for (int w = 0; w < nw; ++w) gs += red_m[w] == -INFINITY ? 0.f : red_s[w] * __expf(red_m[w] - gm);
+  const float logZ = gm + __logf(gs);
+
+  int token = gbest.i;
+  if (!greedy) {
+    const int k = top_k[row];
+    const float p = top_p[row];
+    const bool restrict_ = (k > 0 && k < V) || (p > 0.f && p < 1.f);
+    float thresh = -INFINITY;  // in (x - max)/T units
+    if (restrict_) {
+      // ---- pass 2: histogram of scaled logits
+      for (int b = tid; b < NBINS; b += blockDim.x) {
+        hist_mass[b] = 0.f;
+        hist_cnt[b] = 0;
+      }
+      __syncthreads();
+      for (int i = tid; i < V; i += blockDim.x) {
+        const float z = (ldf(lr + i) - gm) * invT;
+        if (z >= -RANGE) {
+          const int b = min(NBINS - 1, (int)((z + RANGE) * (NBINS / RANGE)));
+          atomicAdd(&hist_mass[b], __expf(z));
+          atomicAdd(&hist_cnt[b], 1);
+        }
+      }
+      __syncthreads();
+      if (tid == 0) {
+        float tot = 0.f;
+        for (int b = 0; b < NBINS; ++b) tot += hist_mass[b];
+        float acc = 0.f;
+        int cnt = 0, cb = 0;
+        for (int b = NBINS - 1; b >= 0; --b) {
+          acc += hist_mass[b];
+          cnt += hist_cnt[b];
+          cb = b;
+          if ((k > 0 && cnt >= k) || (p > 0.f && p < 1.f && acc >= p * tot)) break;
+        }
+        cut_bin = cb;
+      }
+      __syncthreads();
+      thresh = cut_bin * (RANGE / NBINS) - RANGE;
+    }
+    // ---- pass 3: Gumbel-max among the kept tokens
+    const uint64_t seed = (uint64_t)seeds[row] * 0x2545F4914F6CDD1DULL + (uint64_t)steps[row];
+    ArgMax g{-INFINITY, 0x7fffffff};
+    for (int i = tid; i < V; i += blockDim.x) {
+      const float z = (ldf(lr + i) - gm) * invT;
+      if (restrict_) {
+        const int b = z >= -RANGE ? min(NBINS - 1, (int)((z + RANGE) * (NBINS / RANGE))) : -1;
+        if (b < cut_bin) continue;
+      }
+      const float u = uniform01(seed, (uint64_t)i);
+      const float gz = z - __logf(-__logf(u));
+      if (gz > g.v) g = ArgMax{gz, i};
+    }
+    (void)thresh;
+    g = wave_argmax(g);
+    __syncthreads();
+    if (lane == 0) {
+      red_f[wid] = g.v;
+      red_i[wid] = g.i;
+    }
+    __syncthreads();
+    ArgMax gg{-INFINITY, 0x7fffffff};
+    for (int w = 0; w < nw; ++w) gg = amax(gg, ArgMax{red_f[w], red_i[w]});
+    token = gg.i < V ? gg.i : gbest.i;
+  }
+  if (tid == 0) {
+    out_tok[row] = token;
+    out_lp[row] = ldf(lr + token) - logZ;
+  }
+  // ---- optional top-n alternatives (n_top small): repeated block argmax excluding picks
+  if (n_top > 0) {
+    __shared__ int picked[32];
+    for (int n = 0; n < n_top; ++n) {
+      ArgMax bb{-INFINITY, 0x7fffffff};
+      for (int i = tid; i < V; i += blockDim.x) {
+        bool skip = false;
+        for (int j = 0; j < n; ++j) skip |= (picked[j] == i);
+        if (skip) continue;
+        const float x = ldf(lr + i);
+        if (x > bb.v) bb = ArgMax{x, i};
+      }
+      bb = wave_argmax(bb);
+      __syncthreads();
+      if (lane == 0) {
+        red_f[wid] = bb.v;
+        red_i[wid] = bb.i;
+      }
+      __syncthreads();
+      if (tid == 0) {
+        ArgMax t{-INFINITY, 0x7fffffff};
+        for (int w = 0; w < nw; ++w) t = amax(t, ArgMax{red_f[w], red_i[w]});
+        const int id = t.i < V ? t.i : 0;
+        picked[n] = id;
+        top_ids[row * n_top + n] = id;
+        top_lps[row * n_top + n] = ldf(lr + id) - logZ;
+      }
+      __syncthreads();
+    }
+  }
+}
+
+template <typename T>
+__global__ void penalty_kernel(T* __restrict__ logits, int64_t row_stride, int V, const int32_t* __restrict__ rows,
+                               const int32_t* __restrict__ toks, const float* __restrict__ delta, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int t = toks[i];
+  if (t < 0 || t >= V) return;
+  T* p = logits + (int64_t)rows[i] * row_stride + t;
+  *p = (T)((float)(*p) + delta[i]);
+}
+
+}  // namespace
+
+void sample_tokens(at::Tensor logits, at::Tensor temperature, at::Tensor top_k, at::Tensor top_p, at::Tensor seeds,
+                   at::Tensor steps, at::Tensor out_tok, at::Tensor out_lp, at::Tensor top_ids, at::Tensor top_lps,
+                   int64_t n_top) {
+  TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1);
+  const int B = logits.size(0), V = logits.size(1);
+  TORCH_CHECK(temperature.scalar_type() == at::kFloat && top_p.scalar_type() == at::kFloat);
+  TORCH_CHECK(top_k.scalar_type() == at::kInt && seeds.scalar_type() == at::kLong && steps.scalar_type() == at::kLong);
+  TORCH_CHECK(out_tok.scalar_type() == at::kInt && out_lp.scalar_type() == at::kFloat);
+  TORCH_CHECK(temperature.numel() >= B && top_k.numel() >= B && top_p.numel() >= B && seeds.numel() >= B &&
+              steps.numel() >= B && out_tok.numel() >= B && out_lp.numel() >= B);
+  TORCH_CHECK(n_top >= 0 && n_top <= 32);
+  if (n_top > 0) TORCH_CHECK(top_ids.numel() >= B * n_top && top_lps.numel() >= B * n_top);
+  if (B == 0) return;
+  auto stream = at::hip::getCurrentHIPStream();
+#define LAUNCH(TT)                                                                                              \
+  sample_kernel<TT><<<B, 1024, 0, stream>>>(                                                                    \
+      (const TT*)logits.data_ptr(), logits.stride(0), V, temperature.data_ptr<float>(), top_k.data_ptr<int32_t>(), \
+      top_p.data_ptr<float>(), seeds.data_ptr<int64_t>(), steps.data_ptr<int64_t>(), out_tok.data_ptr<int32_t>(), \
+      out_lp.data_ptr<float>(), (int)n_top, n_top > 0 ? top_ids.data_ptr<int32_t>() : nullptr,                  \
+      n_top > 0 ? top_lps.data_ptr<float>() : nullptr)
+  if (logits.scalar_type() == at::kFloat) LAUNCH(float);
+  else if (logits.scalar_type() == at::kBFloat16) LAUNCH(bf16);
+  else TORCH_CHECK(false, "logits must be f32 or bf16");
+#undef LAUNCH
+}
+
+void apply_logit_deltas(at::Tensor logits, at::Tensor rows, at::Tensor toks, at::Tensor delta) {
+  TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1);
+  TORCH_CHECK(rows.scalar_type() == at::kInt && toks.scalar_type() == at::kInt && delta.scalar_type() == at::kFloat);
+  const int n = rows.numel();
+  TORCH_CHECK(toks.numel() == n && delta.numel() == n);
+  if (n == 0) return;
+  auto stream = at::hip::getCurrentHIPStream();
+  const int V = logits.size(1);
+  if (logits.scalar_type() == at::kFloat)
+    penalty_kernel<float><<<(n + 255) / 256, 256, 0, stream>>>(logits.data_ptr<float>(), logits.stride(0), V,
+                                                               rows.data_ptr<int32_t>(), toks.data_ptr<int32_t>(),
+                                                               delta.data_ptr<float>(), n);
+  else
+    penalty_kernel<bf16><<<(n + 255) / 256, 256, 0, stream>>>((bf16*)logits.data_ptr(), logits.stride(0), V,
+                                                              rows.data_ptr<int32_t>(), toks.data_ptr<int32_t>(),
+                                                              delta.data_ptr<float>(), n);
+}

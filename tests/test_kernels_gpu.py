@@ -1,0 +1,283 @@
+"""Numerics of every HIP kernel against the plain-PyTorch fp32 reference (ops.reference).
+
+All tests here need a real gfx950 GPU and the in-tree ``_hip_ops.so``; the ops layer
+raises (never falls back) when the extension is missing, so a pass here means the
+native kernels ran.
+"""
+import math
+
+import pytest
+import torch
+
+from langstream_amd import ops
+from langstream_amd.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _close(a, b, atol, rtol=0.0, msg=""):
+    a, b = a.float().cpu(), b.float().cpu()
+    err = (a - b).abs()
+    tol = atol + rtol * b.abs()
+    bad = err > tol
+    assert not bad.any(), f"{msg} max err {err.max().item():.4g} at {bad.nonzero()[:5].tolist()}"
+
+
+def test_extension_loaded():
+    assert ops.hip_available(), "native _hip_ops.so must load on the GPU box"
+
+
+@pytest.mark.parametrize("H", [384, 4096, 8192])
+def test_rmsnorm(H):
+    torch.manual_seed(0)
+    x = torch.randn(37, H, device=DEV, dtype=torch.bfloat16)
+    w = torch.randn(H, device=DEV, dtype=torch.bfloat16)
+    _close(ops.rmsnorm(x, w, 1e-5), ref.rmsnorm(x.cpu(), w.cpu(), 1e-5), 0.05, 0.02)
+
+
+def test_fused_add_rmsnorm():
+    torch.manual_seed(1)
+    x = torch.randn(19, 4096, device=DEV, dtype=torch.bfloat16)
+    r = torch.randn(19, 4096, device=DEV, dtype=torch.bfloat16)
+    w = torch.randn(4096, device=DEV, dtype=torch.bfloat16)
+    xc, rc = x.cpu().clone(), r.cpu().clone()
+    ops.fused_add_rmsnorm(x, r, w, 1e-5)
+    ref.fused_add_rmsnorm(xc, rc, w.cpu(), 1e-5)
+    _close(r, rc, 0.02, 0.01, "residual")
+    _close(x, xc, 0.05, 0.02, "normed")
+
+
+def test_layernorm_bias_residual():
+    torch.manual_seed(2)
+    x = torch.randn(50, 384, device=DEV, dtype=torch.bfloat16)
+    res = torch.randn_like(x)
+    bias, g, b = (torch.randn(384, device=DEV, dtype=torch.bfloat16) for _ in range(3))
+    got = ops.layernorm(x, g, b, 1e-12, bias=bias, residual=res)
+    exp = ref.layernorm(x.cpu(), bias.cpu(), res.cpu(), g.cpu(), b.cpu(), 1e-12)
+    _close(got, exp, 0.05, 0.02)
+
+
+def test_embed_layernorm():
+    torch.manual_seed(3)
+    V, P, H = 1000, 512, 384
+    wte = torch.randn(V, H, device=DEV, dtype=torch.bfloat16)
+    wpe = torch.randn(P, H, device=DEV, dtype=torch.bfloat16)
+    wtt = torch.randn(2, H, device=DEV, dtype=torch.bfloat16)
+    g, b = torch.randn(H, device=DEV, dtype=torch.bfloat16), torch.randn(H, device=DEV, dtype=torch.bfloat16)
+    ids = torch.randint(0, V, (77,), device=DEV, dtype=torch.int32)
+    pos = torch.randint(0, P, (77,), device=DEV, dtype=torch.int32)
+    tt = torch.randint(0, 2, (77,), device=DEV, dtype=torch.int32)
+    got = ops.embed_layernorm(ids, pos, tt, wte, wpe, wtt, g, b, 1e-12)
+    exp = ref.embed_layernorm(ids.cpu(), pos.cpu(), tt.cpu(), wte.cpu(), wpe.cpu(), wtt.cpu(), g.cpu(), b.cpu(), 1e-12)
+    _close(got, exp, 0.05, 0.02)
+
+
+def test_silu_mul_and_gelu():
+    torch.manual_seed(4)
+    x = torch.randn(33, 2 * 1536, device=DEV, dtype=torch.bfloat16)
+    _close(ops.silu_and_mul(x), ref.silu_and_mul(x.cpu()), 0.02, 0.02)
+    y = torch.randn(33, 1536, device=DEV, dtype=torch.bfloat16)
+    bias = torch.randn(1536, device=DEV, dtype=torch.bfloat16)
+    exp = ref.bias_gelu(y.cpu(), bias.cpu())
+    _close(ops.bias_gelu_(y, bias), exp, 0.02, 0.02)
+
+
+def _alloc_cache(nb, Hkv, D, dev):
+    return (torch.zeros(nb, Hkv, ops.KV_BLOCK, D, device=dev, dtype=torch.bfloat16),
+            torch.zeros(nb, Hkv, D, ops.KV_BLOCK, device=dev, dtype=torch.bfloat16))
+
+
+def test_rope_and_cache():
+    torch.manual_seed(5)
+    Hq, Hkv, D, T = 8, 2, 128, 150
+    qkv = torch.randn(T, (Hq + 2 * Hkv) * D, device=DEV, dtype=torch.bfloat16)
+    pos = torch.arange(T, device=DEV, dtype=torch.int32) + 7
+    cs = ref.rope_cos_sin(4096, D, 500000.0, device=DEV)
+    perm = torch.randperm(8 * ops.KV_BLOCK)[:T]
+    slots = perm.to(DEV, torch.int64)
+    slots[3] = -1
+    kc, vc = _alloc_cache(8, Hkv, D, DEV)
+    kr, vr = _alloc_cache(8, Hkv, D, "cpu")
+    qkv_c = qkv.cpu().clone()
+    ops.rope_and_cache(qkv, pos, cs, slots, kc, vc, Hq, Hkv)
+    ref.rope_and_cache(qkv_c, pos.cpu(), cs.cpu(), slots.cpu(), kr, vr, Hq, Hkv)
+    _close(qkv, qkv_c, 0.03, 0.01, "qkv")
+    _close(kc, kr, 0.03, 0.01, "k cache")
+    _close(vc, vr, 0.0, 0.0, "v cache")
+
+
+def _random_paged(B, ctx, Hkv, D, dev, seed=0):
+    torch.manual_seed(seed)
+    nblk = [(c + ops.KV_BLOCK - 1) // ops.KV_BLOCK for c in ctx]
+    NB = sum(nblk) + 3
+    kc = torch.randn(NB, Hkv, ops.KV_BLOCK, D, device=dev, dtype=torch.bfloat16)
+    vc = torch.randn(NB, Hkv, D, ops.KV_BLOCK, device=dev, dtype=torch.bfloat16)
+    perm = torch.randperm(NB)
+    maxb = max(nblk)
+    bt = torch.zeros(B, maxb, dtype=torch.int32)
+    k = 0
+    for b in range(B):
+        for i in range(nblk[b]):
+            bt[b, i] = perm[k]
+            k += 1
+    return kc, vc, bt.to(dev)
+
+
+@pytest.mark.parametrize("G", [4, 8])
+@pytest.mark.parametrize("nsplit", [1, 3])
+def test_paged_decode_attention(G, nsplit):
+    Hkv, D = 2, 128
+    Hq = Hkv * G
+    ctx = [1, 63, 64, 65, 300, 777]
+    B = len(ctx)
+    kc, vc, bt = _random_paged(B, ctx, Hkv, D, DEV, seed=G)
+    qkv = torch.randn(B, (Hq + 2 * Hkv) * D, device=DEV, dtype=torch.bfloat16)
+    q = qkv[:, : Hq * D]
+    cl = torch.tensor(ctx, dtype=torch.int32, device=DEV)
+    scale = 1 / math.sqrt(D)
+    maxb = bt.shape[1]
+    bps = (maxb + nsplit - 1) // nsplit
+    ws = torch.empty(B * Hq * nsplit * (D + 2), device=DEV, dtype=torch.float32)
+    got = ops.paged_decode_attention(q, kc, vc, bt, cl, scale, nsplit=nsplit, blocks_per_split=bps, workspace=ws)
+    exp = ref.paged_decode_attention(q.cpu().reshape(B, Hq, D), kc.cpu(), vc.cpu(), bt.cpu(), cl.cpu(), scale)
+    _close(got, exp.reshape(B, Hq * D), 0.03, 0.03)
+
+
+@pytest.mark.parametrize("G", [1, 4, 8])
+def test_paged_prefill_attention(G):
+    Hkv, D = 2, 128
+    Hq = Hkv * G
+    q_lens = [1, 17, 64, 130, 200]
+    prefix = [0, 5, 64, 0, 300]
+    ctx = [a + b for a, b in zip(q_lens, prefix)]
+    B = len(q_lens)
+    kc, vc, bt = _random_paged(B, ctx, Hkv, D, DEV, seed=10 + G)
+    T = sum(q_lens)
+    q = torch.randn(T, (Hq + 2 * Hkv) * D, device=DEV, dtype=torch.bfloat16)
+    starts = [0]
+    for n in q_lens[:-1]:
+        starts.append(starts[-1] + n)
+    qs = torch.tensor(starts, dtype=torch.int32, device=DEV)
+    ql = torch.tensor(q_lens, dtype=torch.int32, device=DEV)
+    cl = torch.tensor(ctx, dtype=torch.int32, device=DEV)
+    tiles = ops.prefill_tiles(q_lens, G, prefix).to(DEV)
+    scale = 1 / math.sqrt(D)
+    got = ops.paged_prefill_attention(q, kc, vc, bt, qs, ql, cl, tiles, Hq, scale)
+    exp = ref.paged_prefill_attention(q.cpu(), kc.cpu(), vc.cpu(), bt.cpu(), qs.cpu(), ql.cpu(), cl.cpu(), Hq, scale)
+    _close(got, exp, 0.03, 0.03)
+
+
+@pytest.mark.parametrize("D,H", [(32, 12), (64, 4)])
+def test_encoder_attention(D, H):
+    torch.manual_seed(20)
+    lens = [3, 64, 65, 200, 512]
+    T = sum(lens)
+    qkv = torch.randn(T, 3 * H * D, device=DEV, dtype=torch.bfloat16)
+    starts = [0]
+    for n in lens[:-1]:
+        starts.append(starts[-1] + n)
+    qs = torch.tensor(starts, dtype=torch.int32, device=DEV)
+    ql = torch.tensor(lens, dtype=torch.int32, device=DEV)
+    tiles = ops.prefill_tiles(lens, 1).to(DEV)
+    scale = 1 / math.sqrt(D)
+    got = ops.varlen_encoder_attention(qkv, qs, ql, tiles, H, H, scale)
+    exp = ref.varlen_encoder_attention(qkv.cpu(), qs.cpu(), ql.cpu(), H, H, scale)
+    _close(got, exp, 0.03, 0.03)
+
+
+def test_sampling_greedy_and_logprobs():
+    torch.manual_seed(30)
+    B, V = 7, 128256
+    logits = torch.randn(B, V, device=DEV) * 3
+    temp = torch.zeros(B, device=DEV)
+    topk = torch.zeros(B, dtype=torch.int32, device=DEV)
+    topp = torch.ones(B, device=DEV)
+    seeds = torch.arange(B, device=DEV, dtype=torch.int64)
+    steps = torch.zeros(B, device=DEV, dtype=torch.int64)
+    tok, lp, ti, tl = ops.sample(logits, temp, topk, topp, seeds, steps, n_top=3)
+    assert torch.equal(tok.cpu().long(), logits.argmax(-1).cpu())
+    exp_lp = torch.log_softmax(logits.float(), -1).gather(1, tok.long()[:, None])[:, 0]
+    _close(lp, exp_lp, 1e-3, 1e-4)
+    v, i = torch.topk(torch.log_softmax(logits.float(), -1), 3, -1)
+    assert torch.equal(ti.cpu().long(), i.cpu())
+    _close(tl, v, 1e-3, 1e-4)
+
+
+def test_sampling_distribution_topk():
+    # temperature sampling restricted to top-k: samples must stay inside the top-k set and
+    # roughly follow the renormalised softmax
+    torch.manual_seed(31)
+    B, V = 4096, 1000
+    base = torch.randn(V) * 2
+    logits = base.to(DEV).repeat(B, 1)
+    temp = torch.full((B,), 0.8, device=DEV)
+    topk = torch.full((B,), 5, dtype=torch.int32, device=DEV)
+    topp = torch.ones(B, device=DEV)
+    seeds = torch.arange(B, device=DEV, dtype=torch.int64)
+    steps = torch.zeros(B, device=DEV, dtype=torch.int64)
+    tok, _, _, _ = ops.sample(logits, temp, topk, topp, seeds, steps)
+    allowed = set(torch.topk(base, 5).indices.tolist())
+    got = tok.cpu().tolist()
+    assert set(got) <= allowed
+    p = torch.softmax(base[list(sorted(allowed))] / 0.8, 0)
+    freq = torch.tensor([got.count(t) for t in sorted(allowed)], dtype=torch.float32) / B
+    assert (freq - p).abs().max() < 0.05
+
+
+def test_sampling_top_p():
+    torch.manual_seed(32)
+    B, V = 2048, 500
+    base = torch.randn(V) * 3
+    logits = base.to(DEV).repeat(B, 1)
+    temp = torch.ones(B, device=DEV)
+    topk = torch.zeros(B, dtype=torch.int32, device=DEV)
+    topp = torch.full((B,), 0.5, device=DEV)
+    seeds = torch.arange(B, device=DEV, dtype=torch.int64) + 99
+    steps = torch.ones(B, device=DEV, dtype=torch.int64)
+    tok, _, _, _ = ops.sample(logits, temp, topk, topp, seeds, steps)
+    probs = torch.softmax(base, 0)
+    sp, si = torch.sort(probs, descending=True)
+    keep = set(si[: int(((torch.cumsum(sp, 0) - sp) < 0.5).sum()) + 1].tolist())
+    assert set(tok.cpu().tolist()) <= keep
+
+
+def test_penalties():
+    logits = torch.zeros(2, 10, device=DEV)
+    rows = torch.tensor([0, 1, 1], dtype=torch.int32, device=DEV)
+    toks = torch.tensor([3, 4, 9], dtype=torch.int32, device=DEV)
+    d = torch.tensor([-1.0, 2.0, 0.5], device=DEV)
+    ops.apply_logit_deltas(logits, rows, toks, d)
+    assert logits[0, 3].item() == -1.0 and logits[1, 4].item() == 2.0 and logits[1, 9].item() == 0.5
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_pooling(mode):
+    torch.manual_seed(40)
+    lens = [1, 7, 100]
+    x = torch.randn(sum(lens), 384, device=DEV, dtype=torch.bfloat16)
+    st = torch.tensor([0, 1, 8], dtype=torch.int32, device=DEV)
+    ln = torch.tensor(lens, dtype=torch.int32, device=DEV)
+    got = ops.pool_embeddings(x, st, ln, mode, True)
+    exp = ref.pool_embeddings(x.cpu(), st.cpu(), ln.cpu(), mode, True)
+    _close(got, exp, 2e-3, 1e-2)
+
+
+@pytest.mark.parametrize("N,Qn,k", [(5000, 3, 20), (1024, 20, 5), (10, 2, 20), (70000, 40, 64)])
+def test_knn_topk(N, Qn, k):
+    torch.manual_seed(50)
+    X = torch.nn.functional.normalize(torch.randn(N, 384), dim=-1).to(DEV, torch.bfloat16)
+    Q = torch.nn.functional.normalize(torch.randn(Qn, 384), dim=-1).to(DEV, torch.bfloat16)
+    s, i = ops.knn_topk(X, Q, k)
+    es, ei = ref.knn_topk(X.cpu(), Q.cpu(), k)
+    # scores must match the reference ranking (ties between near-equal scores may reorder)
+    valid = es > -1e30
+    _close(torch.where(valid, s.cpu(), torch.zeros_like(s.cpu())), torch.where(valid, es, torch.zeros_like(es)), 2e-3)
+    # every returned index must have the score we report
+    for q in range(Qn):
+        for j in range(k):
+            if i[q, j] >= 0:
+                sc = (X[i[q, j].long()].float() @ Q[q].float()).item()
+                assert abs(sc - s[q, j].item()) < 2e-3
+            else:
+                assert not valid[q, j]
