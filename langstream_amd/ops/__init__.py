@@ -135,14 +135,13 @@ def rope_and_cache(qkv, pos, cos_sin, slots, k_cache, v_cache, Hq: int, Hkv: int
 
 
 # ---------------------------------------------------------------- attention
-def decode_splits(max_ctx: int, batch_kv_pairs: int, n_cu: int = 256) -> tuple[int, int]:
-    """Split-KV plan for decode: enough workgroups to fill the chip (>= 2 per CU)
-    without splitting short contexts."""
-    nblk = max(1, (max_ctx + KV_BLOCK - 1) // KV_BLOCK)
-    want = max(1, (2 * n_cu + batch_kv_pairs - 1) // max(1, batch_kv_pairs))
-    nsplit = max(1, min(want, nblk // 4 if nblk >= 8 else 1, 32))
-    bps = (nblk + nsplit - 1) // nsplit
-    nsplit = (nblk + bps - 1) // bps
+def decode_splits(max_blocks: int, blocks_per_split: int = 8) -> tuple[int, int]:
+    """Split-KV plan for decode: each workgroup covers at most `blocks_per_split` KV
+    blocks (512 keys); the grid is sized for `max_blocks`, and workgroups past a
+    sequence's own context exit at once (the merge reads only the splits that exist),
+    so one captured graph serves every context length."""
+    bps = max(1, blocks_per_split)
+    nsplit = max(1, (max_blocks + bps - 1) // bps)
     return nsplit, bps
 
 

@@ -47,6 +47,10 @@ __global__ void __launch_bounds__(256) decode_attn_kernel(
   nblk = min(nblk, max_blocks);
   const int bstart = split * blocks_per_split;
   const int bend = min(nblk, bstart + blocks_per_split);
+  // splits past this sequence's context exit at once; the merge kernel only reads
+  // the ceil(nblk / blocks_per_split) splits that exist (graph-friendly: the grid is
+  // sized for the longest context the graph may see).
+  if (split > 0 && bstart >= nblk) return;
 
   // Q^T fragments (B operand): lane holds Q[head kvh*G + i16][32ks + 8h .. +7]
   bf16x8 qf[KS];
@@ -184,12 +188,16 @@ __global__ void __launch_bounds__(256) decode_attn_kernel(
 
 template <int D>
 __global__ void __launch_bounds__(256) decode_merge_kernel(bf16* __restrict__ out, const float* __restrict__ part_o,
-                                                           const float* __restrict__ part_ml, int nsplit, int nrows) {
+                                                           const float* __restrict__ part_ml, int nsplit_grid, int nrows,
+                                                           const int32_t* __restrict__ ctx_lens, int Hq,
+                                                           int blocks_per_split, int max_blocks) {
   // one wave per (b, head) row; lanes over d
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= nrows) return;
-  const float* ml = part_ml + (int64_t)row * nsplit * 2;
+  const int nblk = min((ctx_lens[row / Hq] + BS - 1) / BS, max_blocks);
+  const int nsplit = max(1, min(nsplit_grid, (nblk + blocks_per_split - 1) / blocks_per_split));
+  const float* ml = part_ml + (int64_t)row * nsplit_grid * 2;
   float mstar = -1e30f;
   for (int s = 0; s < nsplit; ++s) mstar = fmaxf(mstar, ml[2 * s]);
   float lt = 0.f;
@@ -197,7 +205,7 @@ __global__ void __launch_bounds__(256) decode_merge_kernel(bf16* __restrict__ ou
   const float inv = lt > 0.f ? 1.f / lt : 0.f;
   for (int d = lane; d < D; d += 64) {
     float a = 0.f;
-    for (int s = 0; s < nsplit; ++s) a += part_o[((int64_t)row * nsplit + s) * D + d] * exp2f(ml[2 * s] - mstar);
+    for (int s = 0; s < nsplit; ++s) a += part_o[((int64_t)row * nsplit_grid + s) * D + d] * exp2f(ml[2 * s] - mstar);
     out[(int64_t)row * D + d] = (bf16)(a * inv);
   }
 }
@@ -244,7 +252,8 @@ void paged_decode_attention(at::Tensor out, at::Tensor q, at::Tensor k_cache, at
                                                    sl2, (int)blocks_per_split, po, pml);                          \
   if (nsplit > 1)                                                                                                \
     decode_merge_kernel<DD><<<(B * Hq + 3) / 4, 256, 0, stream>>>((bf16*)out.data_ptr(), po, pml, (int)nsplit,   \
-                                                                  B * Hq)
+                                                                  B * Hq, ctx_lens.data_ptr<int32_t>(), Hq,       \
+                                                                  (int)blocks_per_split, (int)block_tables.size(1))
   if (D == 128) { LAUNCH(128); }
   else if (D == 64) { LAUNCH(64); }
   else TORCH_CHECK(false, "unsupported head dim ", D);

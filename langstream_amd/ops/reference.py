@@ -130,6 +130,9 @@ def paged_decode_attention(q, k_cache, v_cache, block_tables, ctx_lens, scale):
     outs = []
     for b in range(B):
         n = int(ctx_lens[b])
+        if n == 0:
+            outs.append(torch.zeros_like(qv[b: b + 1]))
+            continue
         K, V = gather_kv(k_cache, v_cache, block_tables[b], n)
         outs.append(attention(qv[b: b + 1], K, V, scale, causal_offset=None))
     return torch.cat(outs, 0)
