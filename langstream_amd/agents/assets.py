@@ -1,0 +1,87 @@
+"""Asset managers used at application setup / cleanup (API/runner/assets/AssetManager.java:
+initialize, assetExists, deployAsset, deleteAssetIfExists)."""
+from __future__ import annotations
+
+import logging
+from typing import Any, Dict
+
+log = logging.getLogger(__name__)
+
+
+class AssetManager:
+    def __init__(self, asset):
+        self.asset = asset
+        self.cfg: Dict[str, Any] = asset.config
+
+    def asset_exists(self) -> bool:
+        return False
+
+    def deploy_asset(self) -> None:
+        pass
+
+    def delete_asset_if_exists(self) -> None:
+        pass
+
+
+class JdbcTableManager(AssetManager):
+    def _ds(self):
+        from .vector.datasources import SqliteDataSource
+        return SqliteDataSource.shared(self.cfg["datasource"])
+
+    def asset_exists(self) -> bool:
+        ds = self._ds()
+        with ds.lock:
+            r = ds.conn.execute("SELECT name FROM sqlite_master WHERE type='table' AND lower(name)=lower(?)",
+                                [self.cfg["table-name"]]).fetchone()
+        return r is not None
+
+    def deploy_asset(self) -> None:
+        ds = self._ds()
+        with ds.lock:
+            for stmt in self.cfg.get("create-statements") or []:
+                ds.conn.execute(stmt)
+            ds.conn.commit()
+
+    def delete_asset_if_exists(self) -> None:
+        ds = self._ds()
+        stmts = self.cfg.get("delete-statements") or [f"DROP TABLE IF EXISTS {self.cfg['table-name']}"]
+        with ds.lock:
+            for stmt in stmts:
+                ds.conn.execute(stmt)
+            ds.conn.commit()
+
+
+class VectorCollectionManager(AssetManager):
+    def asset_exists(self) -> bool:
+        from ..engine.vector_store import VectorStoreRegistry
+        return VectorStoreRegistry.exists(self.cfg["collection-name"])
+
+    def deploy_asset(self) -> None:
+        from ..engine.vector_store import VectorStoreRegistry
+        dim = int(self.cfg.get("dimension") or self.cfg.get("dimensions") or 384)
+        VectorStoreRegistry.get(self.cfg["collection-name"], dim)
+
+    def delete_asset_if_exists(self) -> None:
+        from ..engine.vector_store import VectorStoreRegistry
+        VectorStoreRegistry.drop(self.cfg["collection-name"])
+
+
+class UnavailableAssetManager(AssetManager):
+    def asset_exists(self) -> bool:
+        raise RuntimeError(f"asset type {self.asset.asset_type} needs its database client and network access, which "
+                           f"are not available in this build")
+
+    deploy_asset = asset_exists
+    delete_asset_if_exists = asset_exists
+
+
+class AssetManagerRegistry:
+    _types = {"jdbc-table": JdbcTableManager, "vector-collection": VectorCollectionManager}
+
+    @classmethod
+    def register(cls, asset_type: str, factory) -> None:
+        cls._types[asset_type] = factory
+
+    @classmethod
+    def create(cls, asset) -> AssetManager:
+        return cls._types.get(asset.asset_type, UnavailableAssetManager)(asset)

@@ -1,0 +1,518 @@
+"""Expression language for ``compute`` / ``when`` / ``fields`` / ``dispatch`` etc.
+
+A Jakarta-EL/JSTL-compatible subset (parity: CMN/jstl/JstlEvaluator.java:30-305,
+CMN/jstl/JstlFunctions.java:49-537, CMN/jstl/predicate/JstlPredicate.java):
+literals (numbers, 'str', "str", true/false/null), property access ``a.b``,
+``a['b']``, ``a[0]``, arithmetic ``+ - * / div % mod``, comparisons
+(``== != < > <= >= eq ne lt gt le ge``), logic (``&& || ! and or not``), ``empty``,
+ternary ``? :``, string concatenation ``+=``, and the ``fn:`` function library.
+Expressions may be wrapped in ``${...}``.  Compiled ASTs are cached.
+"""
+from __future__ import annotations
+
+import base64
+import datetime as _dt
+import functools
+import json
+import math
+import random
+import re
+import time
+import uuid
+from decimal import Decimal
+from typing import Any, Callable, Dict, List, Optional
+
+# ---------------------------------------------------------------- lexer
+_TOKEN = re.compile(r"""
+    (?P<ws>\s+)
+  | (?P<num>\d+\.\d*(?:[eE][+-]?\d+)?|\.\d+(?:[eE][+-]?\d+)?|\d+(?:[eE][+-]?\d+)?)
+  | (?P<str>'(?:[^'\\]|\\.)*'|"(?:[^"\\]|\\.)*")
+  | (?P<op>\+=|==|!=|<=|>=|&&|\|\||[-+*/%<>!?:.,()\[\]])
+  | (?P<name>[A-Za-z_][A-Za-z0-9_]*)
+""", re.VERBOSE)
+
+_WORD_OPS = {"and": "&&", "or": "||", "not": "!", "eq": "==", "ne": "!=", "lt": "<", "gt": ">", "le": "<=",
+             "ge": ">=", "div": "/", "mod": "%"}
+
+
+def _unescape(s: str) -> str:
+    body = s[1:-1]
+    return re.sub(r"\\(.)", lambda m: {"n": "\n", "t": "\t", "r": "\r"}.get(m.group(1), m.group(1)), body)
+
+
+def tokenize(src: str) -> List[tuple]:
+    out = []
+    pos = 0
+    while pos < len(src):
+        m = _TOKEN.match(src, pos)
+        if not m:
+            raise ValueError(f"Invalid expression at {pos}: {src!r}")
+        pos = m.end()
+        kind = m.lastgroup
+        text = m.group(kind)
+        if kind == "ws":
+            continue
+        if kind == "num":
+            out.append(("num", float(text) if any(c in text for c in ".eE") else int(text)))
+        elif kind == "str":
+            out.append(("str", _unescape(text)))
+        elif kind == "name":
+            if text in _WORD_OPS:
+                out.append(("op", _WORD_OPS[text]))
+            elif text in ("true", "false"):
+                out.append(("lit", text == "true"))
+            elif text == "null":
+                out.append(("lit", None))
+            elif text == "empty":
+                out.append(("op", "empty"))
+            else:
+                out.append(("name", text))
+        else:
+            out.append(("op", text))
+    out.append(("eof", None))
+    return out
+
+
+# ---------------------------------------------------------------- parser (Pratt)
+_BP = {"?": 1, "||": 2, "&&": 3, "==": 4, "!=": 4, "<": 5, ">": 5, "<=": 5, ">=": 5, "+": 6, "-": 6, "+=": 6,
+       "*": 7, "/": 7, "%": 7}
+
+
+class _Parser:
+    def __init__(self, toks):
+        self.t = toks
+        self.i = 0
+
+    def peek(self):
+        return self.t[self.i]
+
+    def next(self):
+        tok = self.t[self.i]
+        self.i += 1
+        return tok
+
+    def expect(self, op):
+        tok = self.next()
+        if tok != ("op", op):
+            raise ValueError(f"expected {op!r}, got {tok[1]!r}")
+
+    def parse(self, rbp=0):
+        left = self.nud(self.next())
+        while True:
+            tok = self.peek()
+            if tok[0] != "op" or tok[1] not in _BP or _BP[tok[1]] <= rbp:
+                break
+            self.next()
+            op = tok[1]
+            if op == "?":
+                a = self.parse(0)
+                self.expect(":")
+                b = self.parse(0)
+                left = ("?", left, a, b)
+            else:
+                left = ("bin", op, left, self.parse(_BP[op]))
+        return left
+
+    def nud(self, tok):
+        kind, v = tok
+        if kind in ("num", "str", "lit"):
+            return self.postfix(("lit", v))
+        if kind == "op" and v == "(":
+            e = self.parse(0)
+            self.expect(")")
+            return self.postfix(e)
+        if kind == "op" and v == "!":
+            return ("not", self.parse(8))
+        if kind == "op" and v == "-":
+            return ("neg", self.parse(8))
+        if kind == "op" and v == "empty":
+            return ("empty", self.parse(8))
+        if kind == "name":
+            # namespaced function fn:name(...)
+            if self.peek() == ("op", ":") and self.t[self.i + 1][0] == "name" and self.t[self.i + 2] == ("op", "("):
+                self.next()
+                fname = self.next()[1]
+                self.expect("(")
+                args = []
+                if self.peek() != ("op", ")"):
+                    while True:
+                        args.append(self.parse(0))
+                        if self.peek() == ("op", ","):
+                            self.next()
+                            continue
+                        break
+                self.expect(")")
+                return self.postfix(("call", v, fname, args))
+            return self.postfix(("var", v))
+        raise ValueError(f"unexpected token {v!r}")
+
+    def postfix(self, e):
+        while True:
+            tok = self.peek()
+            if tok == ("op", "."):
+                self.next()
+                name = self.next()
+                if name[0] not in ("name", "lit"):
+                    raise ValueError("expected property name after '.'")
+                prop = name[1] if name[0] == "name" else str(name[1]).lower()
+                e = ("get", e, ("lit", prop))
+            elif tok == ("op", "["):
+                self.next()
+                idx = self.parse(0)
+                self.expect("]")
+                e = ("get", e, idx)
+            else:
+                return e
+
+
+@functools.lru_cache(maxsize=4096)
+def compile_expression(expr: str):
+    s = expr.strip()
+    if s.startswith("${") and s.endswith("}"):
+        s = s[2:-1]
+    p = _Parser(tokenize(s))
+    ast = p.parse(0)
+    if p.peek()[0] != "eof":
+        raise ValueError(f"unexpected trailing input in expression {expr!r}")
+    return ast
+
+
+# ---------------------------------------------------------------- evaluation
+def _num(v):
+    if isinstance(v, bool):
+        return int(v)
+    if v is None:
+        return 0
+    if isinstance(v, (int, float, Decimal)):
+        return v
+    if isinstance(v, str):
+        try:
+            return int(v)
+        except ValueError:
+            return float(v)
+    raise ValueError(f"cannot coerce {v!r} to a number")
+
+
+def _is_empty(v) -> bool:
+    return v is None or (isinstance(v, (str, list, dict, tuple, set)) and len(v) == 0)
+
+
+def _truthy(v) -> bool:
+    if isinstance(v, str):
+        return v.strip().lower() == "true"
+    return bool(v)
+
+
+def _cmp_coerce(a, b):
+    if isinstance(a, str) and isinstance(b, (int, float)) and not isinstance(b, bool):
+        try:
+            return _num(a), b
+        except ValueError:
+            return a, str(b)
+    if isinstance(b, str) and isinstance(a, (int, float)) and not isinstance(a, bool):
+        try:
+            return a, _num(b)
+        except ValueError:
+            return str(a), b
+    return a, b
+
+
+def _get(obj, key):
+    if obj is None:
+        return None
+    if isinstance(obj, dict):
+        return obj.get(key)
+    if isinstance(obj, (list, tuple)):
+        try:
+            return obj[int(key)]
+        except (IndexError, ValueError, TypeError):
+            return None
+    if isinstance(obj, str) and isinstance(key, str):
+        # JSON-string values are transparently parsed (recordToMutableRecord behaviour)
+        try:
+            parsed = json.loads(obj)
+            if isinstance(parsed, dict):
+                return parsed.get(key)
+        except ValueError:
+            return None
+        return None
+    return getattr(obj, str(key), None)
+
+
+def evaluate(ast, ctx: Dict[str, Any]) -> Any:
+    t = ast[0]
+    if t == "lit":
+        return ast[1]
+    if t == "var":
+        return ctx.get(ast[1])
+    if t == "get":
+        return _get(evaluate(ast[1], ctx), evaluate(ast[2], ctx))
+    if t == "not":
+        return not _truthy(evaluate(ast[1], ctx))
+    if t == "neg":
+        return -_num(evaluate(ast[1], ctx))
+    if t == "empty":
+        return _is_empty(evaluate(ast[1], ctx))
+    if t == "?":
+        return evaluate(ast[2], ctx) if _truthy(evaluate(ast[1], ctx)) else evaluate(ast[3], ctx)
+    if t == "call":
+        fn = FUNCTIONS.get(ast[2])
+        if fn is None:
+            raise ValueError(f"Unknown function {ast[1]}:{ast[2]}")
+        if ast[2] == "filter":
+            return _fn_filter(evaluate(ast[3][0], ctx), evaluate(ast[3][1], ctx), ctx)
+        return fn(*[evaluate(a, ctx) for a in ast[3]])
+    if t == "bin":
+        op = ast[1]
+        if op == "&&":
+            return _truthy(evaluate(ast[2], ctx)) and _truthy(evaluate(ast[3], ctx))
+        if op == "||":
+            return _truthy(evaluate(ast[2], ctx)) or _truthy(evaluate(ast[3], ctx))
+        a, b = evaluate(ast[2], ctx), evaluate(ast[3], ctx)
+        if op == "+=":
+            return _fn_tostring(a) + _fn_tostring(b)
+        if op == "==":
+            a, b = _cmp_coerce(a, b)
+            return a == b
+        if op == "!=":
+            a, b = _cmp_coerce(a, b)
+            return a != b
+        if op in ("<", ">", "<=", ">="):
+            a, b = _cmp_coerce(a, b)
+            if a is None or b is None:
+                return False
+            return {"<": a < b, ">": a > b, "<=": a <= b, ">=": a >= b}[op]
+        if op == "+":
+            return _num(a) + _num(b)
+        if op == "-":
+            return _num(a) - _num(b)
+        if op == "*":
+            return _num(a) * _num(b)
+        if op == "/":
+            return _num(a) / _num(b)
+        if op == "%":
+            return _num(a) % _num(b)
+    raise ValueError(f"bad ast node {t}")
+
+
+def eval_expression(expr: str, ctx: Dict[str, Any]) -> Any:
+    return evaluate(compile_expression(expr), ctx)
+
+
+def eval_predicate(expr: Optional[str], ctx: Dict[str, Any]) -> bool:
+    if expr is None or (isinstance(expr, str) and not expr.strip()):
+        return True
+    return _truthy(eval_expression(expr, ctx))
+
+
+# ---------------------------------------------------------------- fn: library
+def _fn_tostring(v) -> str:
+    if v is None:
+        return ""
+    if isinstance(v, bytes):
+        return v.decode("utf-8", errors="replace")
+    if isinstance(v, bool):
+        return "true" if v else "false"
+    if isinstance(v, (dict, list)):
+        return json.dumps(v)
+    if isinstance(v, float) and v.is_integer():
+        return repr(v)
+    return str(v)
+
+
+def _fn_to_json(v):
+    return json.dumps(v)
+
+
+def _fn_from_json(v):
+    if v is None:
+        return None
+    if isinstance(v, bytes):
+        v = v.decode()
+    return json.loads(v) if isinstance(v, str) else v
+
+
+def _fn_length(v):
+    if v is None:
+        return 0
+    return len(v) if isinstance(v, (str, list, dict, tuple)) else len(_fn_tostring(v))
+
+
+def _fn_to_list_of_float(v):
+    if v is None:
+        return None
+    if isinstance(v, str):
+        v = json.loads(v)
+    return [float(x) for x in v]
+
+
+def _to_int(v):
+    if v is None:
+        return None
+    if isinstance(v, bool):
+        return int(v)
+    if isinstance(v, str):
+        return int(float(v)) if v.strip() else None
+    return int(v)
+
+
+def _to_double(v):
+    if v is None:
+        return None
+    return float(v)
+
+
+def _fn_split(v, sep):
+    if v is None:
+        return None
+    s = _fn_tostring(v)
+    if s == "":
+        return []
+    return re.split(_fn_tostring(sep), s)
+
+
+def _fn_concat(*args):
+    return "".join(_fn_tostring(a) for a in args)
+
+
+def _fn_replace(v, regex, repl):
+    if v is None:
+        return None
+    return re.sub(_fn_tostring(regex), _fn_tostring(repl).replace("$", "\\"), _fn_tostring(v))
+
+
+def _fn_contains(v, s):
+    if v is None or s is None:
+        return False
+    if isinstance(v, (list, tuple, dict)):
+        return s in v
+    return _fn_tostring(s) in _fn_tostring(v)
+
+
+def _fn_coalesce(v, d):
+    return d if v is None else v
+
+
+def _fn_unpack(v, fields):
+    if v is None:
+        return None
+    vals = ([] if v == "" else v.split(",")) if isinstance(v, str) else list(v)
+    heads = _fn_tostring(fields).split(",")
+    return {h: (vals[i] if i < len(vals) else None) for i, h in enumerate(heads)}
+
+
+def _fn_list_add(lst, item):
+    return list(lst or []) + [item]
+
+
+def _fn_add_all(a, b):
+    return list(a or []) + list(b or [])
+
+
+def _fn_list_of(*args):
+    return list(args)
+
+
+def _fn_map_of(*args):
+    if len(args) % 2:
+        raise ValueError("fn:mapOf needs an even number of arguments")
+    return {_fn_tostring(args[i]): args[i + 1] for i in range(0, len(args), 2)}
+
+
+def _fn_map_put(m, k, v):
+    d = dict(m or {})
+    d[_fn_tostring(k)] = v
+    return d
+
+
+def _fn_map_remove(m, k):
+    d = dict(m or {})
+    d.pop(_fn_tostring(k), None)
+    return d
+
+
+def _fn_map_to_list_of_structs(m, fields):
+    if m is None:
+        raise ValueError("listOf doesn't allow a null value")
+    if isinstance(m, str):
+        m = json.loads(m)
+    return [{f: m.get(f) for f in fields.split(",")}]
+
+
+def _fn_list_to_list_of_structs(lst, field):
+    if lst is None:
+        raise ValueError("listOf doesn't allow a null value")
+    return [{field: x} for x in lst]
+
+
+def _to_millis(v) -> int:
+    if isinstance(v, (int, float)):
+        return int(v)
+    if isinstance(v, _dt.datetime):
+        return int(v.timestamp() * 1000)
+    if isinstance(v, str):
+        s = v.replace("Z", "+00:00")
+        d = _dt.datetime.fromisoformat(s)
+        if d.tzinfo is None:
+            d = d.replace(tzinfo=_dt.timezone.utc)
+        return int(d.timestamp() * 1000)
+    raise ValueError(f"cannot coerce {v!r} to a timestamp")
+
+
+_UNIT_MS = {"days": 86400000, "hours": 3600000, "minutes": 60000, "seconds": 1000, "millis": 1}
+
+
+def _fn_timestamp_add(v, delta, unit):
+    if v is None or unit is None:
+        raise ValueError("timestampAdd requires input and unit")
+    unit = _fn_tostring(unit)
+    ms = _to_millis(v)
+    d = int(delta)
+    if unit in ("years", "months"):
+        t = _dt.datetime.fromtimestamp(ms / 1000, tz=_dt.timezone.utc)
+        months = d * (12 if unit == "years" else 1)
+        y, mth = divmod(t.month - 1 + months, 12)
+        t = t.replace(year=t.year + y, month=mth + 1)
+        return int(t.timestamp() * 1000)
+    if unit == "nanos":
+        return ms + d // 1_000_000
+    if unit not in _UNIT_MS:
+        raise ValueError(f"Invalid unit: {unit}. Should be one of [years, months, days, hours, minutes, seconds, "
+                         f"millis]")
+    return ms + d * _UNIT_MS[unit]
+
+
+def _fn_filter(lst, expr, ctx):
+    if lst is None:
+        return None
+    out = []
+    for o in lst:
+        if o is None:
+            continue
+        c = dict(ctx)
+        c["record"] = o
+        if eval_predicate(expr, c):
+            out.append(o)
+    return out
+
+
+FUNCTIONS: Dict[str, Callable] = {
+    "length": _fn_length, "toJson": _fn_to_json, "fromJson": _fn_from_json, "toListOfFloat": _fn_to_list_of_float,
+    "uppercase": lambda v: None if v is None else _fn_tostring(v).upper(),
+    "lowercase": lambda v: None if v is None else _fn_tostring(v).lower(),
+    "contains": _fn_contains, "trim": lambda v: None if v is None else _fn_tostring(v).strip(),
+    "concat": _fn_concat, "concat3": _fn_concat, "coalesce": _fn_coalesce, "replace": _fn_replace,
+    "str": _fn_tostring, "toString": _fn_tostring, "toDouble": _to_double, "toInt": _to_int, "toLong": _to_int,
+    "toBigDecimal": lambda v, scale=None: None if v is None else (
+        Decimal(_fn_tostring(v)) if scale is None else Decimal(int(v)).scaleb(-int(scale))),
+    "decimalFromUnscaled": lambda v, scale: Decimal(int(v)).scaleb(-int(scale)),
+    "decimalFromNumber": lambda v: Decimal(str(v)),
+    "split": _fn_split, "unpack": _fn_unpack, "listOf": _fn_list_of, "emptyList": lambda: [],
+    "listAdd": _fn_list_add, "addAll": _fn_add_all, "mapOf": _fn_map_of, "emptyMap": lambda: {},
+    "mapPut": _fn_map_put, "mapRemove": _fn_map_remove, "mapToListOfStructs": _fn_map_to_list_of_structs,
+    "listToListOfStructs": _fn_list_to_list_of_structs, "filter": _fn_filter,
+    "now": lambda: int(time.time() * 1000), "uuid": lambda: str(uuid.uuid4()),
+    "random": lambda mx: random.randrange(int(mx)),
+    "timestampAdd": _fn_timestamp_add, "dateadd": _fn_timestamp_add,
+    "toSQLTimestamp": lambda v: _dt.datetime.fromtimestamp(_to_millis(v) / 1000, tz=_dt.timezone.utc).isoformat(),
+}

@@ -1,0 +1,137 @@
+"""MutableRecord: the working form of a record inside the GenAI toolkit.
+
+Parity: CMN/MutableRecord.java:58-563 -- key/value objects (JSON strings are parsed to
+maps when possible: ``recordToMutableRecord(record, attemptJsonConversion=true)``),
+properties (= headers as strings), input/output topic, event time, drop flag;
+``set_result_field`` targets value / key / value.x / key.x / properties.x /
+destinationTopic / messageKey (:309-360); the expression-language context exposes
+key, value, messageKey, topicName, destinationTopic, eventTime, properties, record.
+"""
+from __future__ import annotations
+
+import copy
+import json
+from typing import Any, Dict, List, Optional
+
+from ...api.record import Header, Record, SimpleRecord
+
+
+def attempt_json(v: Any) -> Any:
+    if isinstance(v, bytes):
+        try:
+            v = v.decode("utf-8")
+        except UnicodeDecodeError:
+            return v
+    if isinstance(v, str):
+        s = v.strip()
+        if s[:1] in ("{", "["):
+            try:
+                return json.loads(s)
+            except ValueError:
+                return v
+    return v
+
+
+def safe_clone(v: Any) -> Any:
+    if isinstance(v, (dict, list)):
+        return copy.deepcopy(v)
+    return v
+
+
+class MutableRecord:
+    __slots__ = ("key", "value", "properties", "input_topic", "output_topic", "event_time", "drop",
+                 "message_key", "record_object", "source")
+
+    def __init__(self, key=None, value=None, properties=None, input_topic=None, event_time=None, source=None):
+        self.key = key
+        self.value = value
+        self.properties: Dict[str, str] = dict(properties or {})
+        self.input_topic = input_topic
+        self.output_topic: Optional[str] = None
+        self.event_time = event_time
+        self.drop = False
+        self.message_key = None
+        self.record_object = None
+        self.source = source
+
+    @staticmethod
+    def from_record(r: Record, attempt_json_conversion: bool = True) -> "MutableRecord":
+        props = {}
+        for h in r.headers():
+            if h.key is not None and h.value is not None:
+                props[h.key] = h.value_as_string()
+        k, v = r.key(), r.value()
+        if attempt_json_conversion:
+            k, v = attempt_json(k), attempt_json(v)
+        m = MutableRecord(safe_clone(k), safe_clone(v), props, r.origin(), r.timestamp(), r)
+        return m
+
+    def copy(self) -> "MutableRecord":
+        m = MutableRecord(safe_clone(self.key), safe_clone(self.value), dict(self.properties), self.input_topic,
+                          self.event_time, self.source)
+        m.output_topic = self.output_topic
+        m.drop = self.drop
+        m.message_key = self.message_key
+        return m
+
+    def to_record(self) -> Optional[Record]:
+        if self.drop:
+            return None
+        headers = [Header(k, v) for k, v in self.properties.items()]
+        key = self.message_key if self.message_key is not None else self.key
+        r = SimpleRecord(key, self.value, self.input_topic, self.event_time, headers)
+        if self.output_topic is not None:
+            r._source_ref = {"destination_topic": self.output_topic}
+        return r
+
+    def el_context(self) -> Dict[str, Any]:
+        return {"key": self.key, "value": self.value, "messageKey": self.message_key or self.key,
+                "topicName": self.input_topic, "destinationTopic": self.output_topic, "eventTime": self.event_time,
+                "properties": self.properties, "header": self.properties,
+                "record": self.record_object if self.record_object is not None else
+                {"key": self.key, "value": self.value}}
+
+    def json_context(self) -> Dict[str, Any]:
+        """Context for mustache templates (JsonRecord: key, value, origin, timestamp, properties)."""
+        return {"key": self.key, "value": self.value, "origin": self.input_topic, "timestamp": self.event_time,
+                "properties": self.properties, "messageKey": self.message_key or self.key}
+
+    def set_result_field(self, content: Any, field: Optional[str]) -> None:
+        if field is None or field == "value":
+            self.value = content
+        elif field == "key":
+            self.key = content
+        elif field == "destinationTopic":
+            self.output_topic = str(content)
+        elif field == "messageKey":
+            self.message_key = str(content)
+        elif field.startswith("properties."):
+            self.properties[field[len("properties."):]] = content if isinstance(content, str) else (
+                json.dumps(content) if isinstance(content, (dict, list)) else str(content))
+        elif field.startswith("value."):
+            name = field[len("value."):]
+            if not isinstance(self.value, dict):
+                if self.value is None or self.value == "":
+                    self.value = {}
+                else:
+                    raise ValueError("Cannot set a value field without a schema on a non-map value")
+            _set_path(self.value, name, content)
+        elif field.startswith("key."):
+            name = field[len("key."):]
+            if not isinstance(self.key, dict):
+                if self.key is None:
+                    self.key = {}
+                else:
+                    raise ValueError("Cannot set a key field without a schema on a non-map key")
+            _set_path(self.key, name, content)
+        else:
+            raise ValueError(f"Cannot set field {field}: it does not refer to any part of the message")
+
+    def get_field(self, field: str) -> Any:
+        from .el import eval_expression
+        return eval_expression(field, self.el_context())
+
+
+def _set_path(d: dict, name: str, content: Any) -> None:
+    # like the reference, "value.a.b" sets the flat key "a.b" (no nesting)
+    d[name] = content

@@ -1,0 +1,338 @@
+"""AI service providers for the GenAI toolkit.
+
+Parity: AIA/ai/langstream/ai/agents/services/ServiceProviderRegistry.java:49-67 (dispatch on
+the config key), OpenAICompletionService.java:122-498 (chat/text completions, streaming
+chunk coalescing :256-306, embeddings), OllamaProvider.java:165-328, HuggingFaceProvider.java,
+VertexAIProvider.java, BedrockServiceProvider.java.
+
+MI355X-native: the ``local`` key (``local-gpu-configuration`` resource) binds the
+in-process GPU engines (``engine/llm_engine.py``, ``engine/embedder.py``); remote
+providers stay available over HTTP for parity (they need network access).
+"""
+from __future__ import annotations
+
+import json
+import logging
+import threading
+import uuid
+from concurrent.futures import Future
+from dataclasses import dataclass, field
+from typing import Any, Callable, Dict, List, Optional
+
+log = logging.getLogger(__name__)
+
+ChunkConsumer = Callable[[str, int, str, bool], None]  # (answer_id, index, content, last)
+
+
+@dataclass
+class ChatMessage:
+    role: str
+    content: str
+
+    def to_dict(self) -> dict:
+        return {"role": self.role, "content": self.content}
+
+
+@dataclass
+class CompletionResult:
+    content: str
+    answer_id: str = ""
+    finish_reason: Optional[str] = None
+    tokens: List[str] = field(default_factory=list)
+    logprobs: List[float] = field(default_factory=list)
+    prompt_tokens: int = 0
+    completion_tokens: int = 0
+
+
+class ChunkCoalescer:
+    """Start at 1 chunk per message, double up to ``min_chunks_per_message``: low latency
+    for the first message, fewer topic messages afterwards (OpenAICompletionService.java:256-306)."""
+
+    def __init__(self, consumer: Optional[ChunkConsumer], min_chunks_per_message: int, answer_id: str):
+        self.consumer = consumer
+        self.min_chunks = max(1, int(min_chunks_per_message or 1))
+        self.answer_id = answer_id
+        self.current = 1
+        self.buffer: List[str] = []
+        self.n = 0
+        self.index = 0
+        self.lock = threading.Lock()
+
+    def accept(self, delta: str, last: bool) -> None:
+        with self.lock:
+            if delta:
+                self.buffer.append(delta)
+                self.n += 1
+            if self.n >= self.current or last:
+                self.current = min(self.current * 2, self.min_chunks)
+                text = "".join(self.buffer)
+                self.buffer.clear()
+                self.n = 0
+                self.index += 1
+                idx = self.index
+            else:
+                return
+        if self.consumer is not None:
+            self.consumer(self.answer_id, idx, text, last)
+
+
+class CompletionsService:
+    def get_chat_completions(self, messages: List[ChatMessage], consumer: Optional[ChunkConsumer],
+                             options: Dict[str, Any]) -> Future:
+        raise NotImplementedError
+
+    def get_text_completions(self, prompts: List[str], consumer: Optional[ChunkConsumer],
+                             options: Dict[str, Any]) -> Future:
+        raise NotImplementedError
+
+
+class EmbeddingsService:
+    def compute_embeddings(self, texts: List[str]) -> Future:
+        raise NotImplementedError
+
+
+# ---------------------------------------------------------------- local GPU
+def llama3_chat_prompt(messages: List[ChatMessage]) -> str:
+    out = ["<|begin_of_text|>"]
+    for m in messages:
+        out.append(f"<|start_header_id|>{m.role}<|end_header_id|>\n\n{m.content}<|eot_id|>")
+    out.append("<|start_header_id|>assistant<|end_header_id|>\n\n")
+    return "".join(out)
+
+
+def _sampling_from_options(options: Dict[str, Any], tok):
+    from ...engine.llm_engine import SamplingParams
+    stop = options.get("stop") or []
+    if isinstance(stop, str):
+        stop = [stop]
+    lb = options.get("logit-bias") or options.get("logit_bias")
+    temperature = options.get("temperature")
+    return SamplingParams(
+        max_tokens=int(options.get("max-tokens") or options.get("max_tokens") or 256),
+        temperature=1.0 if temperature is None else float(temperature),
+        top_p=float(options.get("top-p") or options.get("top_p") or 1.0),
+        top_k=int(options.get("top-k") or options.get("top_k") or 0),
+        seed=options.get("seed"),
+        stop=list(stop),
+        presence_penalty=float(options.get("presence-penalty") or 0.0),
+        frequency_penalty=float(options.get("frequency-penalty") or 0.0),
+        logit_bias={int(k): float(v) for k, v in lb.items()} if isinstance(lb, dict) else None,
+        logprobs=int(options.get("logprobs") or 0) if options.get("logprobs") not in (True, False) else (
+            1 if options.get("logprobs") else 0),
+        ignore_eos=bool(options.get("ignore-eos", False)),
+    )
+
+
+class LocalCompletionsService(CompletionsService):
+    """Chat / text completions on the in-process continuous-batching GPU engine."""
+
+    def __init__(self, engine, tokenizer, model_name: str = "local"):
+        self.engine = engine
+        self.tok = tokenizer
+        self.model_name = model_name
+
+    def _submit(self, prompt_text: str, consumer, options, want_logprobs: bool) -> Future:
+        fut: Future = Future()
+        answer_id = f"chatcmpl-{uuid.uuid4().hex[:24]}"
+        coalescer = ChunkCoalescer(consumer, int(options.get("min-chunks-per-message", 20)), answer_id)
+        stream = bool(options.get("stream", True)) and consumer is not None
+        params = _sampling_from_options(options, self.tok)
+        if want_logprobs and params.logprobs == 0:
+            params.logprobs = 1
+        ids = self.tok.encode(prompt_text, add_bos=False)
+        toks: List[str] = []
+        lps: List[float] = []
+
+        def on_token(ev) -> None:
+            if ev.token_id >= 0:
+                if want_logprobs:
+                    toks.append(self.tok.decode([ev.token_id]))
+                    lps.append(ev.logprob)
+                if stream:
+                    coalescer.accept(ev.text, ev.finished)
+            elif stream and ev.finished:
+                coalescer.accept("", True)
+            if ev.finished:
+                req = holder.get("req")
+                text = req.text if req is not None else ""
+                if ev.finish_reason == "error":
+                    fut.set_exception(RuntimeError("generation failed"))
+                else:
+                    fut.set_result(CompletionResult(text, answer_id, ev.finish_reason, toks, lps,
+                                                    len(ids), len(req.output_ids) if req else 0))
+
+        holder: Dict[str, Any] = {}
+        holder["req"] = self.engine.submit(ids, params, on_token)
+        return fut
+
+    def get_chat_completions(self, messages, consumer, options) -> Future:
+        return self._submit(llama3_chat_prompt(messages), consumer, options, False)
+
+    def get_text_completions(self, prompts, consumer, options) -> Future:
+        return self._submit("\n".join(prompts), consumer, options, bool(options.get("logprobs")))
+
+
+class LocalEmbeddingsService(EmbeddingsService):
+    def __init__(self, engine):
+        self.engine = engine
+
+    def compute_embeddings(self, texts: List[str]) -> Future:
+        return self.engine.embed_async(texts)
+
+
+# ---------------------------------------------------------------- remote (HTTP) providers
+def _http_json(url: str, payload: dict, headers: Dict[str, str], timeout: float = 120.0) -> dict:
+    import requests
+    r = requests.post(url, json=payload, headers=headers, timeout=timeout)
+    r.raise_for_status()
+    return r.json()
+
+
+def _run_async(fn) -> Future:
+    fut: Future = Future()
+
+    def run():
+        try:
+            fut.set_result(fn())
+        except BaseException as e:  # noqa: BLE001
+            fut.set_exception(e)
+
+    threading.Thread(target=run, daemon=True).start()
+    return fut
+
+
+class OpenAIService(CompletionsService, EmbeddingsService):
+    """OpenAI / Azure OpenAI REST (streaming SSE for chat)."""
+
+    def __init__(self, cfg: Dict[str, Any], model: Optional[str] = None):
+        self.cfg = cfg
+        self.model = model
+        self.url = (cfg.get("url") or "https://api.openai.com/v1").rstrip("/")
+        self.key = cfg.get("access-key")
+        self.provider = cfg.get("provider", "openai")
+
+    def _headers(self):
+        if self.provider == "azure":
+            return {"api-key": self.key or ""}
+        return {"Authorization": f"Bearer {self.key}"}
+
+    def _endpoint(self, kind: str, model: str) -> str:
+        if self.provider == "azure":
+            return f"{self.url}/openai/deployments/{model}/{kind}?api-version=2023-05-15"
+        return f"{self.url}/{kind}"
+
+    def compute_embeddings(self, texts):
+        model = self.model or "text-embedding-ada-002"
+        return _run_async(lambda: [d["embedding"] for d in _http_json(
+            self._endpoint("embeddings", model), {"model": model, "input": texts}, self._headers())["data"]])
+
+    def get_chat_completions(self, messages, consumer, options):
+        model = options.get("model") or self.model
+
+        def run():
+            import requests
+            payload = {"model": model, "messages": [m.to_dict() for m in messages], "stream": True}
+            for k in ("max-tokens", "temperature", "top-p", "presence-penalty", "frequency-penalty", "stop", "user"):
+                if options.get(k) is not None:
+                    payload[k.replace("-", "_")] = options[k]
+            aid = f"chatcmpl-{uuid.uuid4().hex[:24]}"
+            co = ChunkCoalescer(consumer, int(options.get("min-chunks-per-message", 20)), aid)
+            parts = []
+            with requests.post(self._endpoint("chat/completions", model), json=payload, headers=self._headers(),
+                               stream=True, timeout=300) as r:
+                r.raise_for_status()
+                for line in r.iter_lines():
+                    if not line or not line.startswith(b"data:"):
+                        continue
+                    data = line[5:].strip()
+                    if data == b"[DONE]":
+                        break
+                    ev = json.loads(data)
+                    ch = (ev.get("choices") or [{}])[0]
+                    d = (ch.get("delta") or {}).get("content") or ""
+                    parts.append(d)
+                    co.accept(d, ch.get("finish_reason") is not None)
+            return CompletionResult("".join(parts), aid)
+
+        return _run_async(run)
+
+    def get_text_completions(self, prompts, consumer, options):
+        model = options.get("model") or self.model
+
+        def run():
+            payload = {"model": model, "prompt": prompts, "max_tokens": options.get("max-tokens", 256)}
+            if options.get("logprobs"):
+                payload["logprobs"] = 1
+            res = _http_json(self._endpoint("completions", model), payload, self._headers())
+            ch = res["choices"][0]
+            lp = ch.get("logprobs") or {}
+            return CompletionResult(ch.get("text", ""), res.get("id", ""), ch.get("finish_reason"),
+                                    lp.get("tokens") or [], lp.get("token_logprobs") or [])
+
+        return _run_async(run)
+
+
+class OllamaService(CompletionsService, EmbeddingsService):
+    """Ollama: /api/generate line-JSON stream (messages joined into one prompt),
+    /api/embeddings one request per text (OllamaProvider.java:165-328)."""
+
+    def __init__(self, cfg: Dict[str, Any], model: Optional[str] = None):
+        self.url = cfg.get("url", "http://localhost:11434").rstrip("/")
+        self.model = model
+
+    def compute_embeddings(self, texts):
+        return _run_async(lambda: [_http_json(f"{self.url}/api/embeddings", {"model": self.model, "prompt": t},
+                                              {})["embedding"] for t in texts])
+
+    def _generate(self, prompt, consumer, options):
+        def run():
+            import requests
+            aid = f"ollama-{uuid.uuid4().hex[:16]}"
+            co = ChunkCoalescer(consumer, int(options.get("min-chunks-per-message", 20)), aid)
+            parts = []
+            with requests.post(f"{self.url}/api/generate", json={"model": options.get("model") or self.model,
+                                                                  "prompt": prompt, "stream": True},
+                               stream=True, timeout=300) as r:
+                r.raise_for_status()
+                for line in r.iter_lines():
+                    if not line:
+                        continue
+                    ev = json.loads(line)
+                    parts.append(ev.get("response", ""))
+                    co.accept(ev.get("response", ""), bool(ev.get("done")))
+            return CompletionResult("".join(parts), aid)
+
+        return _run_async(run)
+
+    def get_chat_completions(self, messages, consumer, options):
+        return self._generate("\n".join(m.content for m in messages), consumer, options)
+
+    def get_text_completions(self, prompts, consumer, options):
+        return self._generate("\n".join(prompts), consumer, options)
+
+
+class HuggingFaceAPIService(EmbeddingsService, CompletionsService):
+    """HF inference REST (``provider: api``); ``provider: local`` maps to the GPU encoder."""
+
+    def __init__(self, cfg: Dict[str, Any], model: Optional[str] = None):
+        self.cfg = cfg
+        self.model = model
+        self.url = cfg.get("inference-url", "https://api-inference.huggingface.co/pipeline/feature-extraction")
+
+    def compute_embeddings(self, texts):
+        headers = {"Authorization": f"Bearer {self.cfg.get('access-key', '')}"}
+        return _run_async(lambda: _http_json(f"{self.url}/{self.model}", {"inputs": texts}, headers))
+
+
+class UnavailableService(CompletionsService, EmbeddingsService):
+    def __init__(self, name: str, why: str):
+        self.name, self.why = name, why
+
+    def _fail(self, *a, **k):
+        f: Future = Future()
+        f.set_exception(RuntimeError(f"{self.name} service unavailable: {self.why}"))
+        return f
+
+    compute_embeddings = _fail
+    get_chat_completions = _fail
+    get_text_completions = _fail

@@ -1,0 +1,500 @@
+"""GenAI toolkit steps (parity: AIA/com/datastax/oss/streaming/ai/*.java, step factory
+util/TransformFunctionUtil.java:166-224, configuration defaults
+CORE/agents/ai/steps/*Configuration.java).
+
+Synchronous host steps: drop-fields, merge-key-value, unwrap-key-value, cast, flatten,
+drop, compute.  Asynchronous steps (return a Future): compute-ai-embeddings (batched
+through OrderedAsyncBatchExecutor onto the GPU encoder), query (datasource),
+ai-chat-completions / ai-text-completions (GPU LLM engine; streamed chunks are written
+to ``stream-to-topic`` with stream-id / stream-index / stream-last-message).
+Every step honours ``when`` (JSTL predicate; false -> the record passes unchanged).
+"""
+from __future__ import annotations
+
+import datetime as _dt
+import json
+import logging
+import threading
+from concurrent.futures import Future
+from typing import Any, Callable, Dict, List, Optional
+
+from ...api.util import OrderedAsyncBatchExecutor
+from .el import eval_expression, eval_predicate
+from .mustache import compile_template
+from .mutable import MutableRecord
+
+log = logging.getLogger(__name__)
+
+
+def _done(v=None) -> Future:
+    f: Future = Future()
+    f.set_result(v)
+    return f
+
+
+class Step:
+    is_async = False
+
+    def __init__(self, cfg: Dict[str, Any]):
+        self.cfg = cfg
+        self.when = cfg.get("when")
+
+    def applies(self, rec: MutableRecord) -> bool:
+        return eval_predicate(self.when, rec.el_context()) if self.when else True
+
+    def start(self) -> None:
+        pass
+
+    def close(self) -> None:
+        pass
+
+    def process(self, rec: MutableRecord) -> None:
+        raise NotImplementedError
+
+    def process_async(self, rec: MutableRecord) -> Future:
+        try:
+            self.process(rec)
+            return _done()
+        except Exception as e:  # noqa: BLE001
+            f: Future = Future()
+            f.set_exception(e)
+            return f
+
+
+# ---------------------------------------------------------------- host transforms
+class DropFieldsStep(Step):
+    def process(self, rec):
+        fields = self.cfg.get("fields") or []
+        part = self.cfg.get("part")
+        for target in (("value",) if part == "value" else ("key",) if part == "key" else ("key", "value")):
+            obj = getattr(rec, target)
+            if isinstance(obj, dict):
+                for f in fields:
+                    obj.pop(f, None)
+
+
+class MergeKeyValueStep(Step):
+    def process(self, rec):
+        if isinstance(rec.key, dict) and isinstance(rec.value, dict):
+            merged = dict(rec.key)
+            merged.update(rec.value)
+            rec.value = merged
+        elif isinstance(rec.key, dict) and rec.value is None:
+            rec.value = dict(rec.key)
+
+
+class UnwrapKeyValueStep(Step):
+    def process(self, rec):
+        if bool(self.cfg.get("unwrapKey", self.cfg.get("unwrap-key", False))):
+            rec.value = rec.key
+        rec.key = None
+
+
+_CASTS: Dict[str, Callable[[Any], Any]] = {
+    "string": lambda v: v if isinstance(v, str) else (json.dumps(v) if isinstance(v, (dict, list)) else (
+        "true" if v is True else "false" if v is False else str(v))),
+    "boolean": lambda v: v if isinstance(v, bool) else str(v).strip().lower() == "true",
+    "int8": lambda v: int(float(v)), "int16": lambda v: int(float(v)), "int32": lambda v: int(float(v)),
+    "int64": lambda v: int(float(v)), "float": lambda v: float(v), "double": lambda v: float(v),
+    "bytes": lambda v: v if isinstance(v, bytes) else str(v).encode(),
+}
+
+
+class CastStep(Step):
+    def process(self, rec):
+        st = str(self.cfg.get("schema-type", "string")).lower()
+        fn = _CASTS.get(st)
+        if fn is None:
+            raise ValueError(f"Unsupported schema-type {st}")
+        part = self.cfg.get("part")
+        if part in (None, "key") and rec.key is not None:
+            rec.key = fn(rec.key)
+        if part in (None, "value") and rec.value is not None:
+            rec.value = fn(rec.value)
+
+
+def _flatten(d: dict, delim: str, prefix: str = "") -> dict:
+    out = {}
+    for k, v in d.items():
+        key = f"{prefix}{delim}{k}" if prefix else str(k)
+        if isinstance(v, dict):
+            out.update(_flatten(v, delim, key))
+        else:
+            out[key] = v
+    return out
+
+
+class FlattenStep(Step):
+    def process(self, rec):
+        delim = self.cfg.get("delimiter", "_")
+        part = self.cfg.get("part")
+        if part in (None, "key") and isinstance(rec.key, dict):
+            rec.key = _flatten(rec.key, delim)
+        if part in (None, "value") and isinstance(rec.value, dict):
+            rec.value = _flatten(rec.value, delim)
+
+
+class DropStep(Step):
+    def process(self, rec):
+        rec.drop = True
+
+
+_COMPUTE_TYPES = {
+    "STRING": lambda v: None if v is None else _CASTS["string"](v),
+    "INT8": lambda v: None if v is None else int(v), "INT16": lambda v: None if v is None else int(v),
+    "INT32": lambda v: None if v is None else int(v), "INT64": lambda v: None if v is None else int(v),
+    "FLOAT": lambda v: None if v is None else float(v), "DOUBLE": lambda v: None if v is None else float(v),
+    "BOOLEAN": lambda v: None if v is None else _CASTS["boolean"](v),
+    "BYTES": lambda v: None if v is None else _CASTS["bytes"](v),
+    "DATE": lambda v: None if v is None else _to_date(v), "TIME": lambda v: v,
+    "TIMESTAMP": lambda v: None if v is None else _to_ts(v), "INSTANT": lambda v: None if v is None else _to_ts(v),
+    "LOCAL_DATE": lambda v: None if v is None else _to_date(v), "LOCAL_TIME": lambda v: v,
+    "LOCAL_DATE_TIME": lambda v: None if v is None else _to_ts(v), "DATETIME": lambda v: None if v is None else
+    _to_ts(v), "DECIMAL": lambda v: v, "ARRAY": lambda v: v, "MAP": lambda v: v,
+}
+
+
+def _to_ts(v):
+    if isinstance(v, (int, float)):
+        return _dt.datetime.fromtimestamp(v / 1000, tz=_dt.timezone.utc).isoformat()
+    return str(v)
+
+
+def _to_date(v):
+    if isinstance(v, (int, float)):
+        return _dt.datetime.fromtimestamp(v / 1000, tz=_dt.timezone.utc).date().isoformat()
+    return str(v)[:10]
+
+
+class ComputeStep(Step):
+    def __init__(self, cfg):
+        super().__init__(cfg)
+        self.fields = []
+        for f in cfg.get("fields") or []:
+            name = f.get("name")
+            if not name:
+                raise ValueError("compute field name is required")
+            t = str(f.get("type") or "").upper() or None
+            if t and t not in _COMPUTE_TYPES:
+                raise ValueError(f"Unsupported compute type {t}")
+            self.fields.append((name, f.get("expression"), t, bool(f.get("optional", True))))
+
+    def process(self, rec):
+        ctx = rec.el_context()
+        results = []
+        for name, expr, t, optional in self.fields:
+            v = eval_expression(expr, ctx) if expr is not None else None
+            if t is not None:
+                v = _COMPUTE_TYPES[t](v)
+            if v is None and not optional:
+                raise ValueError(f"Field {name} is not optional but the expression evaluated to null")
+            results.append((name, v))
+        for name, v in results:
+            if name in ("value", "key", "destinationTopic", "messageKey") or name.startswith(
+                    ("value.", "key.", "properties.")):
+                if name.startswith("value.") and not isinstance(rec.value, dict) and rec.value is not None:
+                    rec.value = {}
+                rec.set_result_field(v, name)
+            elif name == "topicName":
+                rec.input_topic = str(v)
+            else:
+                raise ValueError(f"Invalid compute field name {name}")
+
+
+# ---------------------------------------------------------------- async AI / data steps
+class _LoopOver:
+    """Shared ``loop-over`` handling: process each element of a list field."""
+
+    @staticmethod
+    def items(rec: MutableRecord, field: Optional[str]):
+        if not field:
+            return None
+        v = eval_expression(field, rec.el_context())
+        if v is None:
+            return []
+        if not isinstance(v, list):
+            raise ValueError(f"loop-over field {field} is not a list")
+        return v
+
+
+class ComputeAIEmbeddingsStep(Step):
+    """Mustache text -> batched embeddings -> ``embeddings-field``
+    (ComputeAIEmbeddingsStep.java:66-250).  Batches of ``batch-size`` are hashed by
+    record key into ``concurrency`` ordered buckets; a bad record fails its batch."""
+    is_async = True
+
+    def __init__(self, cfg, service):
+        super().__init__(cfg)
+        self.service = service
+        self.template = compile_template(cfg.get("text") or "")
+        self.field = cfg.get("embeddings-field")
+        if not self.field:
+            raise ValueError("embeddings-field is required")
+        self.loop_over = cfg.get("loop-over")
+        self.executor = OrderedAsyncBatchExecutor(
+            int(cfg.get("batch-size", 10)), self._process_batch, int(cfg.get("flush-interval", 0)),
+            int(cfg.get("concurrency", 4)), lambda item: hash(str(item[0].key)))
+
+    def start(self):
+        self.executor.start()
+
+    def close(self):
+        self.executor.stop()
+
+    def process_async(self, rec: MutableRecord) -> Future:
+        fut: Future = Future()
+        try:
+            items = _LoopOver.items(rec, self.loop_over)
+            if items is not None:
+                texts = []
+                for it in items:
+                    c = rec.json_context()
+                    c["record"] = it
+                    texts.append(self.template.render(c))
+                if not texts:
+                    fut.set_result(None)
+                    return fut
+                f2 = self.service.compute_embeddings(texts)
+
+                def done(f):
+                    try:
+                        embs = f.result()
+                        for it, e in zip(items, embs):
+                            if isinstance(it, dict):
+                                it[self.field.split(".")[-1] if self.field.startswith("record.") else self.field] = e
+                        rec.set_result_field(items, self.loop_over)
+                        fut.set_result(None)
+                    except BaseException as ex:  # noqa: BLE001
+                        fut.set_exception(ex)
+
+                f2.add_done_callback(done)
+                return fut
+            text = self.template.render(rec.json_context())
+        except Exception as e:  # noqa: BLE001
+            fut.set_exception(e)
+            return fut
+        self.executor.add((rec, text, fut))
+        return fut
+
+    def _process_batch(self, batch, batch_fut: Future) -> None:
+        texts = [t for _, t, _ in batch]
+        try:
+            f = self.service.compute_embeddings(texts)
+        except Exception as e:  # noqa: BLE001
+            for _, _, fut in batch:
+                fut.set_exception(e)
+            batch_fut.set_exception(e)
+            return
+
+        def done(ff: Future):
+            err = ff.exception()
+            if err is not None:
+                for _, _, fut in batch:
+                    fut.set_exception(err)
+                batch_fut.set_exception(err)
+                return
+            embs = ff.result()
+            for (rec, _, fut), e in zip(batch, embs):
+                try:
+                    rec.set_result_field(e if isinstance(e, list) else list(e), self.field)
+                    fut.set_result(None)
+                except Exception as ex:  # noqa: BLE001
+                    fut.set_exception(ex)
+            batch_fut.set_result(None)
+
+        f.add_done_callback(done)
+
+
+class QueryStep(Step):
+    """fields (JSTL) -> positional params -> datasource.fetch_data / execute_statement
+    (QueryStep.java:54-222); ``loop-over``, ``only-first``, ``output-field``,
+    ``mode: query|execute``, ``generated-keys``."""
+    is_async = True
+
+    def __init__(self, cfg, datasource):
+        super().__init__(cfg)
+        self.ds = datasource
+        self.query = cfg.get("query")
+        self.fields = cfg.get("fields") or []
+        self.output_field = cfg.get("output-field")
+        self.only_first = bool(cfg.get("only-first", False))
+        self.loop_over = cfg.get("loop-over")
+        self.mode = cfg.get("mode", "query")
+        self.generated_keys = cfg.get("generated-keys") or []
+        if self.mode not in ("query", "execute"):
+            raise ValueError("mode must be query or execute")
+        if not self.output_field and self.mode == "query":
+            raise ValueError("output-field is required")
+
+    def _params(self, ctx) -> list:
+        return [eval_expression(f, ctx) for f in self.fields]
+
+    def _run_one(self, ctx):
+        params = self._params(ctx)
+        if self.mode == "execute":
+            return self.ds.execute_statement(self.query, self.generated_keys, params)
+        rows = self.ds.fetch_data(self.query, params)
+        if self.only_first:
+            return rows[0] if rows else None
+        return rows
+
+    def process_async(self, rec) -> Future:
+        fut: Future = Future()
+
+        def run():
+            try:
+                items = _LoopOver.items(rec, self.loop_over)
+                if items is not None:
+                    res = []
+                    for it in items:
+                        c = rec.el_context()
+                        c["record"] = it
+                        res.append(self._run_one(c))
+                    rec.set_result_field(res, self.output_field)
+                else:
+                    r = self._run_one(rec.el_context())
+                    if self.output_field:
+                        rec.set_result_field(r, self.output_field)
+                fut.set_result(None)
+            except BaseException as e:  # noqa: BLE001
+                fut.set_exception(e)
+
+        if getattr(self.ds, "is_async_friendly", False):
+            run()
+        else:
+            threading.Thread(target=run, daemon=True).start()
+        return fut
+
+
+class ChatCompletionsStep(Step):
+    """ai-chat-completions (ChatCompletionsStep.java:77-196)."""
+    is_async = True
+
+    def __init__(self, cfg, service, stream_consumer_factory):
+        super().__init__(cfg)
+        self.service = service
+        self.messages = [(m.get("role", "user"), compile_template(m.get("content") or ""))
+                         for m in cfg.get("messages") or []]
+        if not self.messages:
+            raise ValueError("messages is required")
+        self.field = cfg.get("completion-field")
+        self.stream_field = cfg.get("stream-response-completion-field")
+        self.log_field = cfg.get("log-field")
+        self.stream_to = cfg.get("stream-to-topic")
+        self.factory = stream_consumer_factory
+        self.stream_consumer = None
+        self.options = {k: cfg.get(k) for k in ("model", "max-tokens", "temperature", "top-p", "logit-bias", "user",
+                                                 "stop", "presence-penalty", "frequency-penalty", "seed", "top-k",
+                                                 "ignore-eos") if cfg.get(k) is not None}
+        self.options.update(cfg.get("options") or {})
+        self.options["min-chunks-per-message"] = int(cfg.get("min-chunks-per-message", 20))
+        self.options["stream"] = bool(cfg.get("stream", True))
+
+    def start(self):
+        if self.stream_to:
+            self.stream_consumer = self.factory(self.stream_to)
+
+    def close(self):
+        if self.stream_consumer is not None:
+            self.stream_consumer.close()
+
+    def _apply(self, rec: MutableRecord, content: str, streaming: bool) -> None:
+        field = self.field
+        if streaming and self.stream_field:
+            field = self.stream_field
+        rec.set_result_field(content, field)
+
+    def _chunk_consumer(self, rec):
+        if self.stream_consumer is None:
+            return None
+
+        def consume(answer_id, index, content, last):
+            c = rec.copy()
+            c.properties["stream-id"] = answer_id
+            c.properties["stream-index"] = str(index)
+            c.properties["stream-last-message"] = "true" if last else "false"
+            self._apply(c, content, True)
+            self.stream_consumer.stream_answer_chunk(index, content, last, c)
+
+        return consume
+
+    def _render_messages(self, rec):
+        from .services import ChatMessage
+        ctx = rec.json_context()
+        return [ChatMessage(role, t.render(ctx)) for role, t in self.messages]
+
+    def process_async(self, rec) -> Future:
+        fut: Future = Future()
+        try:
+            messages = self._render_messages(rec)
+            inner = self.service.get_chat_completions(messages, self._chunk_consumer(rec), dict(self.options))
+        except Exception as e:  # noqa: BLE001
+            fut.set_exception(e)
+            return fut
+
+        def done(f):
+            try:
+                res = f.result()
+                self._apply(rec, res.content, False)
+                if self.log_field:
+                    rec.set_result_field(json.dumps({"model": self.options.get("model"), "options": self.options,
+                                                     "messages": [m.to_dict() for m in messages]}), self.log_field)
+                fut.set_result(None)
+            except BaseException as e:  # noqa: BLE001
+                fut.set_exception(e)
+
+        inner.add_done_callback(done)
+        return fut
+
+
+class TextCompletionsStep(ChatCompletionsStep):
+    """ai-text-completions (TextCompletionsStep.java:95-199): prompt[] templates,
+    ``logprobs`` + ``logprobs-field = {tokens[], logprobs[]}`` (consumed by FLARE)."""
+
+    def __init__(self, cfg, service, stream_consumer_factory):
+        cfg = dict(cfg)
+        cfg.setdefault("messages", [{"role": "user", "content": p} for p in (cfg.get("prompt") or [])])
+        Step.__init__(self, cfg)
+        self.service = service
+        self.prompts = [compile_template(p) for p in cfg.get("prompt") or []]
+        if not self.prompts:
+            raise ValueError("prompt is required")
+        self.field = cfg.get("completion-field")
+        self.stream_field = cfg.get("stream-response-completion-field")
+        self.log_field = cfg.get("log-field")
+        self.stream_to = cfg.get("stream-to-topic")
+        self.factory = stream_consumer_factory
+        self.stream_consumer = None
+        self.logprobs_field = cfg.get("logprobs-field")
+        self.options = {k: cfg.get(k) for k in ("model", "max-tokens", "temperature", "top-p", "logit-bias", "user",
+                                                 "stop", "presence-penalty", "frequency-penalty", "logprobs", "seed",
+                                                 "top-k", "ignore-eos") if cfg.get(k) is not None}
+        self.options.update(cfg.get("options") or {})
+        self.options["min-chunks-per-message"] = int(cfg.get("min-chunks-per-message", 20))
+        self.options["stream"] = bool(cfg.get("stream", True))
+
+    def process_async(self, rec) -> Future:
+        fut: Future = Future()
+        try:
+            ctx = rec.json_context()
+            prompts = [t.render(ctx) for t in self.prompts]
+            inner = self.service.get_text_completions(prompts, self._chunk_consumer(rec), dict(self.options))
+        except Exception as e:  # noqa: BLE001
+            fut.set_exception(e)
+            return fut
+
+        def done(f):
+            try:
+                res = f.result()
+                self._apply(rec, res.content, False)
+                if self.logprobs_field:
+                    rec.set_result_field({"tokens": res.tokens, "logprobs": res.logprobs}, self.logprobs_field)
+                if self.log_field:
+                    rec.set_result_field(json.dumps({"model": self.options.get("model"), "options": self.options,
+                                                     "prompt": prompts}), self.log_field)
+                fut.set_result(None)
+            except BaseException as e:  # noqa: BLE001
+                fut.set_exception(e)
+
+        inner.add_done_callback(done)
+        return fut

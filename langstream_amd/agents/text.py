@@ -1,0 +1,327 @@
+"""Text-processing agents (TXT/*): text-extractor, language-detector, text-normaliser,
+document-to-json, text-splitter.
+
+* text-splitter: recursive character splitter (TXT/RecursiveCharacterTextSplitter.java:22-86,
+  TXT/TextSplitter.java merge/overlap logic, TXT/TextSplitterAgent.java:30-124): separators
+  ["\\n\\n","\\n"," ",""], chunk_size 200, chunk_overlap 100, keep_separator false,
+  length_function cl100k_base (native C++ BPE counter) or length; one record per chunk
+  with the ORIGINAL key and headers chunk_id / chunk_text_length / chunk_num_tokens /
+  text_num_chunks.
+* text-extractor: Tika AutoDetect in the reference; here: plain text, HTML, XML, JSON,
+  DOCX/PPTX/XLSX/ODT (zip + XML), RTF, and PDF text streams (uncompressed / Flate).
+* language-detector: stop-word profile scoring (Tika LanguageIdentifier in the
+  reference) -> header ``language`` (configurable), ``allowedLanguages`` filter.
+"""
+from __future__ import annotations
+
+import html
+import html.parser
+import io
+import json
+import re
+import zipfile
+import zlib
+from typing import Any, Callable, Dict, List, Optional
+
+from ..api.agent import SingleRecordAgentProcessor
+from ..api.record import Header, SimpleRecord
+from ..runtime.registry import register_agent
+
+
+def to_text(v: Any) -> str:
+    if v is None:
+        return ""
+    if isinstance(v, bytes):
+        return v.decode("utf-8", errors="replace")
+    if isinstance(v, str):
+        return v
+    if isinstance(v, (dict, list)):
+        return json.dumps(v)
+    return str(v)
+
+
+# ---------------------------------------------------------------- splitter
+class RecursiveCharacterTextSplitter:
+    def __init__(self, separators: Optional[List[str]] = None, keep_separator: bool = False, chunk_size: int = 200,
+                 chunk_overlap: int = 100, length_function: Callable[[str], int] = len):
+        if chunk_overlap > chunk_size:
+            raise ValueError(f"Got a larger chunk overlap ({chunk_overlap}) than chunk size ({chunk_size}), "
+                             f"should be smaller.")
+        self.separators = separators if separators is not None else ["\n\n", "\n", " ", ""]
+        self.keep_separator = keep_separator
+        self.chunk_size = chunk_size
+        self.chunk_overlap = chunk_overlap
+        self.length = length_function
+
+    @staticmethod
+    def _split_regex(text: str, sep: str, keep: bool) -> List[str]:
+        if sep:
+            if keep:
+                ms = list(re.finditer(f"({sep})", text))
+                if not ms:
+                    splits = [text]
+                else:
+                    splits = []
+                    if ms[0].start() != 0:
+                        splits.append(text[: ms[0].start()])
+                    for i, m in enumerate(ms):
+                        end = ms[i + 1].start() if i + 1 < len(ms) else len(text)
+                        splits.append(m.group() + text[m.end(): end])
+            else:
+                splits = re.split(sep, text)
+        else:
+            splits = list(text)
+        return [s for s in splits if s]
+
+    def _join(self, docs: List[str], sep: str) -> Optional[str]:
+        t = sep.join(docs).strip()
+        return t or None
+
+    def _merge(self, splits: List[str], sep: str) -> List[str]:
+        docs: List[str] = []
+        cur: List[str] = []
+        total = 0
+        sep_len = self.length(sep)
+        for d in splits:
+            ln = self.length(d)
+            if total + ln + (sep_len if cur else 0) > self.chunk_size:
+                if cur:
+                    doc = self._join(cur, sep)
+                    if doc is not None:
+                        docs.append(doc)
+                    while total > self.chunk_overlap or (
+                            total + ln + (sep_len if cur else 0) > self.chunk_size and total > 0):
+                        total -= self.length(cur[0]) + (sep_len if len(cur) > 1 else 0)
+                        cur.pop(0)
+            cur.append(d)
+            total += ln + (sep_len if len(cur) > 1 else 0)
+        doc = self._join(cur, sep)
+        if doc is not None:
+            docs.append(doc)
+        return docs
+
+    def _split(self, text: str, separators: List[str]) -> List[str]:
+        final: List[str] = []
+        separator = separators[-1]
+        new_seps: List[str] = []
+        for i, s in enumerate(separators):
+            if s == "":
+                separator = s
+                break
+            if re.search(s, text):
+                separator = s
+                new_seps = separators[i + 1:]
+                break
+        splits = self._split_regex(text, separator, self.keep_separator)
+        good: List[str] = []
+        sep_use = "" if self.keep_separator else separator
+        for s in splits:
+            if self.length(s) < self.chunk_size:
+                good.append(s)
+            else:
+                if good:
+                    final.extend(self._merge(good, sep_use))
+                    good = []
+                if not new_seps:
+                    final.append(s)
+                else:
+                    final.extend(self._split(s, new_seps))
+        if good:
+            final.extend(self._merge(good, sep_use))
+        return final
+
+    def split_text(self, text: str) -> List[str]:
+        return self._split(text, self.separators)
+
+
+@register_agent("text-splitter")
+class TextSplitterAgent(SingleRecordAgentProcessor):
+    def init(self, configuration: Dict[str, Any]) -> None:
+        st = str(configuration.get("splitter_type", "RecursiveCharacterTextSplitter"))
+        if st != "RecursiveCharacterTextSplitter":
+            raise ValueError(f"Unknown splitter type: {st}, only RecursiveCharacterTextSplitter is supported")
+        lf = str(configuration.get("length_function", "cl100k_base"))
+        if lf == "length":
+            self.length = len
+        else:
+            from ..tokenizers import cl100k_counter
+            self.length = cl100k_counter()
+        self.splitter = RecursiveCharacterTextSplitter(
+            configuration.get("separators", ["\n\n", "\n", " ", ""]),
+            str(configuration.get("keep_separator", "false")).lower() == "true",
+            int(configuration.get("chunk_size", 200)), int(configuration.get("chunk_overlap", 100)), self.length)
+
+    def process_record(self, record):
+        chunks = self.splitter.split_text(to_text(record.value()))
+        n = len(chunks)
+        out = []
+        for i, c in enumerate(chunks):
+            hs = list(record.headers()) + [Header("chunk_id", str(i)), Header("chunk_text_length", str(len(c))),
+                                           Header("chunk_num_tokens", str(self.length(c))),
+                                           Header("text_num_chunks", str(n))]
+            out.append(SimpleRecord.copy_from(record, key=record.key(), value=c, headers=hs))
+        return out
+
+
+# ---------------------------------------------------------------- normaliser / document-to-json
+@register_agent("text-normaliser")
+class TextNormaliserAgent(SingleRecordAgentProcessor):
+    def init(self, configuration):
+        self.lower = str(configuration.get("make-lowercase", "true")).lower() == "true"
+        self.trim = str(configuration.get("trim-spaces", "true")).lower() == "true"
+
+    def process_record(self, record):
+        t = to_text(record.value())
+        if self.lower:
+            t = t.lower()
+        if self.trim:
+            t = re.sub(r"[ \t]+", " ", t)
+            t = re.sub(r"\n\s*\n+", "\n\n", t).strip()
+        return [SimpleRecord.copy_from(record, value=t)]
+
+
+@register_agent("document-to-json")
+class DocumentToJsonAgent(SingleRecordAgentProcessor):
+    def init(self, configuration):
+        self.field = configuration.get("text-field", "text")
+        self.copy_props = str(configuration.get("copy-properties", "true")).lower() == "true"
+
+    def process_record(self, record):
+        out = {self.field: to_text(record.value())}
+        if self.copy_props:
+            for h in record.headers():
+                out[h.key] = h.value_as_string()
+        return [SimpleRecord.copy_from(record, value=out)]
+
+
+# ---------------------------------------------------------------- extraction
+class _HTMLText(html.parser.HTMLParser):
+    SKIP = {"script", "style", "head", "noscript"}
+    BLOCK = {"p", "div", "br", "li", "h1", "h2", "h3", "h4", "h5", "h6", "tr", "section", "article", "pre"}
+
+    def __init__(self):
+        super().__init__(convert_charrefs=True)
+        self.parts: List[str] = []
+        self.skip = 0
+
+    def handle_starttag(self, tag, attrs):
+        if tag in self.SKIP:
+            self.skip += 1
+        elif tag in self.BLOCK:
+            self.parts.append("\n")
+
+    def handle_endtag(self, tag):
+        if tag in self.SKIP and self.skip:
+            self.skip -= 1
+        elif tag in self.BLOCK:
+            self.parts.append("\n")
+
+    def handle_data(self, data):
+        if not self.skip:
+            self.parts.append(data)
+
+
+def html_to_text(s: str) -> str:
+    p = _HTMLText()
+    p.feed(s)
+    t = "".join(p.parts)
+    t = re.sub(r"[ \t\r]+", " ", t)
+    return re.sub(r"\n\s*\n+", "\n\n", t).strip()
+
+
+def _xml_text(data: bytes) -> str:
+    s = data.decode("utf-8", errors="replace")
+    s = re.sub(r"</w:p>|</a:p>|</text:p>|<w:br/>", "\n", s)
+    s = re.sub(r"<[^>]+>", "", s)
+    return html.unescape(s)
+
+
+def _pdf_text(data: bytes) -> str:
+    out = []
+    for m in re.finditer(rb"stream\r?\n(.*?)\r?\nendstream", data, re.S):
+        raw = m.group(1)
+        try:
+            raw = zlib.decompress(raw)
+        except zlib.error:
+            pass
+        for tm in re.finditer(rb"\[(.*?)\]\s*TJ|\((.*?)\)\s*Tj", raw, re.S):
+            if tm.group(1) is not None:
+                out.append(b"".join(re.findall(rb"\((.*?)\)", tm.group(1))).decode("latin-1"))
+            else:
+                out.append(tm.group(2).decode("latin-1"))
+        out.append("\n")
+    return re.sub(r"\n+", "\n", "".join(out)).strip()
+
+
+def extract_text(data: Any) -> str:
+    if isinstance(data, str):
+        s = data.lstrip()
+        if s[:1] == "<" and re.search(r"<(html|body|p|div)\b", s[:2000], re.I):
+            return html_to_text(data)
+        return data
+    if not isinstance(data, (bytes, bytearray)):
+        return to_text(data)
+    b = bytes(data)
+    if b[:4] == b"%PDF":
+        return _pdf_text(b)
+    if b[:2] == b"PK":
+        try:
+            with zipfile.ZipFile(io.BytesIO(b)) as z:
+                names = z.namelist()
+                parts = [n for n in names if n in ("word/document.xml", "content.xml")]
+                parts += sorted(n for n in names if re.match(r"ppt/slides/slide\d+\.xml", n))
+                parts += [n for n in names if n == "xl/sharedStrings.xml"]
+                return "\n".join(_xml_text(z.read(n)) for n in parts).strip()
+        except zipfile.BadZipFile:
+            pass
+    if b[:5] == b"{\\rtf":
+        s = b.decode("latin-1")
+        s = re.sub(r"\\[a-z]+-?\d* ?|[{}]", "", s)
+        return s.strip()
+    s = b.decode("utf-8", errors="replace")
+    return extract_text(s)
+
+
+@register_agent("text-extractor")
+class TextExtractorAgent(SingleRecordAgentProcessor):
+    def process_record(self, record):
+        return [SimpleRecord.copy_from(record, value=extract_text(record.value()))]
+
+
+# ---------------------------------------------------------------- language detection
+_STOPWORDS = {
+    "en": "the and of to in is that it for was on are with as be this by have not at from or but".split(),
+    "it": "il di che e la per un in non una sono del della si con le da al lo ma".split(),
+    "fr": "le de la et les des un une du en est que pas pour dans qui sur au avec".split(),
+    "de": "der die und das ist nicht ein eine zu den von mit sich des auf für im dem".split(),
+    "es": "el la de que y en los se del las un por con no una para es al lo como".split(),
+    "pt": "o a de que e do da em um para com não uma os no se na por mais as dos".split(),
+    "nl": "de het een en van in is dat op te zijn niet met voor die aan er".split(),
+}
+
+
+def detect_language(text: str) -> str:
+    words = re.findall(r"[a-zàâäéèêëïîôöùûüçñßáíóúãõ]+", text.lower())
+    if not words:
+        return "unknown"
+    best, score = "unknown", 0.0
+    for lang, sw in _STOPWORDS.items():
+        s = set(sw)
+        sc = sum(1 for w in words if w in s) / len(words)
+        if sc > score:
+            best, score = lang, sc
+    return best if score > 0.02 else "unknown"
+
+
+@register_agent("language-detector")
+class LanguageDetectorAgent(SingleRecordAgentProcessor):
+    def init(self, configuration):
+        self.prop = configuration.get("property", "language")
+        al = configuration.get("allowedLanguages") or []
+        self.allowed = set(al if isinstance(al, list) else [a.strip() for a in str(al).split(",") if a.strip()])
+
+    def process_record(self, record):
+        lang = detect_language(to_text(record.value()))
+        if self.allowed and lang not in self.allowed:
+            return []
+        return [SimpleRecord.with_headers(record, [Header(self.prop, lang)])]

@@ -1,0 +1,156 @@
+"""Vector agents: ``query-vector-db`` (PROCESSOR) and ``vector-db-sink`` (SINK).
+
+Parity: VEC/QueryVectorDBAgent.java:27-93 (a QueryStep over a vector datasource),
+VEC/VectorDBSinkAgent.java:25-56 (``VectorDatabaseWriter.upsert`` per record; a null
+value deletes), VEC/jdbc/JdbcWriter.java:33-208 (prepared UPDATE, then INSERT when no
+row matched; DELETE on null value).
+"""
+from __future__ import annotations
+
+import json
+import logging
+import threading
+from concurrent.futures import Future
+from typing import Any, Dict, List
+
+from ...api.agent import AgentProcessor, AgentSink, completed, failed
+from ...api.record import SourceRecordAndResult
+from ...engine.vector_store import VectorStoreRegistry
+from ...runtime.registry import register_agent
+from ..genai.el import eval_expression
+from ..genai.mutable import MutableRecord
+from ..genai.steps import QueryStep
+from .datasources import LocalVectorDataSource, SqliteDataSource, datasource_for
+
+
+@register_agent("query-vector-db")
+class QueryVectorDBAgent(AgentProcessor):
+    def init(self, configuration: Dict[str, Any]) -> None:
+        self.cfg = dict(configuration)
+        self.step = QueryStep(self.cfg, datasource_for(self.cfg.get("datasource")))
+
+    def process(self, records, sink) -> None:
+        for r in records:
+            mr = MutableRecord.from_record(r)
+            if not self.step.applies(mr):
+                sink(SourceRecordAndResult(r, [r], None))
+                continue
+            fut = self.step.process_async(mr)
+
+            def done(f, r=r, mr=mr):
+                if f.exception() is not None:
+                    sink(SourceRecordAndResult(r, None, f.exception()))
+                else:
+                    out = mr.to_record()
+                    self.processed(1, 1)
+                    sink(SourceRecordAndResult(r, [out] if out is not None else [], None))
+
+            fut.add_done_callback(done)
+
+
+class _LocalWriter:
+    """fields: id / vector / anything else -> metadata; collection-name."""
+
+    def __init__(self, cfg: Dict[str, Any]):
+        self.collection = cfg.get("collection-name") or (cfg.get("datasource") or {}).get("collection-name") \
+            or "default"
+        self.fields = cfg.get("fields") or []
+        names = {f.get("name") for f in self.fields}
+        if "vector" not in names:
+            raise ValueError("vector-db-sink (local): a field named 'vector' is required")
+
+    def upsert(self, mr: MutableRecord) -> None:
+        ctx = mr.el_context()
+        vals = {f["name"]: eval_expression(f["expression"], ctx) for f in self.fields}
+        rid = vals.pop("id", None)
+        if rid is None:
+            rid = mr.key if mr.key is not None else json.dumps(mr.value, sort_keys=True)[:256]
+        if isinstance(rid, (dict, list)):
+            rid = json.dumps(rid, sort_keys=True)
+        vec = vals.pop("vector")
+        if mr.value is None or vec is None:
+            if VectorStoreRegistry.exists(self.collection):
+                VectorStoreRegistry.get(self.collection).delete([rid])
+            return
+        if isinstance(vec, str):
+            vec = json.loads(vec)
+        VectorStoreRegistry.get(self.collection, len(vec)).upsert([rid], [vec], [vals])
+
+
+class _JdbcWriter:
+    def __init__(self, cfg: Dict[str, Any]):
+        self.ds: SqliteDataSource = SqliteDataSource.shared(cfg["datasource"])
+        self.table = cfg.get("table-name") or cfg.get("table")
+        if not self.table:
+            raise ValueError("vector-db-sink (jdbc): table-name is required")
+        self.fields = cfg.get("fields") or []
+        self.pk = [f["name"] for f in self.fields if f.get("primary-key")]
+        self.cols = [f["name"] for f in self.fields if not f.get("primary-key")]
+        if not self.pk:
+            raise ValueError("vector-db-sink (jdbc): at least one primary-key field is required")
+
+    def upsert(self, mr: MutableRecord) -> None:
+        ctx = mr.el_context()
+        vals = {f["name"]: eval_expression(f["expression"], ctx) for f in self.fields}
+        enc = lambda v: json.dumps(v) if isinstance(v, (list, dict)) else v  # noqa: E731
+        ds = self.ds
+        with ds.lock:
+            where = " AND ".join(f"{c} = ?" for c in self.pk)
+            pkv = [enc(vals[c]) for c in self.pk]
+            if mr.value is None:
+                rowids = [r[0] for r in ds.conn.execute(f"SELECT rowid FROM {self.table} WHERE {where}", pkv)]
+                ds.conn.execute(f"DELETE FROM {self.table} WHERE {where}", pkv)
+                ds.conn.commit()
+                self._mirror_delete(rowids)
+                return
+            sets = ", ".join(f"{c} = ?" for c in self.cols)
+            cur = ds.conn.execute(f"UPDATE {self.table} SET {sets} WHERE {where}",
+                                  [enc(vals[c]) for c in self.cols] + pkv) if self.cols else None
+            if cur is None or cur.rowcount == 0:
+                allc = self.pk + self.cols
+                ds.conn.execute(f"INSERT INTO {self.table} ({', '.join(allc)}) VALUES ({', '.join('?' * len(allc))})",
+                                [enc(vals[c]) for c in allc])
+            ds.conn.commit()
+            rowid = ds.conn.execute(f"SELECT rowid FROM {self.table} WHERE {where}", pkv).fetchone()[0]
+        self._mirror_upsert(rowid, vals)
+
+    def _mirror_upsert(self, rowid, vals) -> None:
+        for (table, col), name in list(self.ds.vector_cols.items()):
+            if table == self.table.lower():
+                for k, v in vals.items():
+                    if k.lower() == col and isinstance(v, list):
+                        VectorStoreRegistry.get(name, len(v)).upsert([rowid], [v])
+
+    def _mirror_delete(self, rowids) -> None:
+        for (table, col), name in list(self.ds.vector_cols.items()):
+            if table == self.table.lower() and VectorStoreRegistry.exists(name):
+                VectorStoreRegistry.get(name).delete(rowids)
+
+
+@register_agent("vector-db-sink")
+class VectorDBSinkAgent(AgentSink):
+    def init(self, configuration: Dict[str, Any]) -> None:
+        self.cfg = dict(configuration)
+        ds = self.cfg.get("datasource") or {}
+        svc = ds.get("service", "local")
+        if svc in ("local", "local-gpu"):
+            self.writer = _LocalWriter(self.cfg)
+        elif svc in ("jdbc", "sqlite"):
+            self.writer = _JdbcWriter(self.cfg)
+        else:
+            from .datasources import UnavailableDataSource
+            self.writer = None
+            self._unavailable = UnavailableDataSource(svc)
+
+    def write(self, record) -> Future:
+        self.processed(1, 0)
+        if self.writer is None:
+            try:
+                self._unavailable.execute_statement("", [], [])
+            except Exception as e:  # noqa: BLE001
+                return failed(e)
+        try:
+            self.writer.upsert(MutableRecord.from_record(record))
+            return completed(None)
+        except Exception as e:  # noqa: BLE001
+            return failed(e)

@@ -1,0 +1,272 @@
+"""Datasources for ``query`` / ``query-vector-db`` and writers for ``vector-db-sink``.
+
+Parity: F6/F9 (AIA/.../datasource/*, VEC/*): QueryStepDataSource.fetchData(query, params)
+/ executeStatement(query, generatedKeys, params) and VectorDatabaseWriter.upsert(record).
+
+MI355X-native services:
+* ``local`` / ``local-gpu``: HBM vector collections (engine/vector_store.py) with a JSON
+  query language -- ``{"collection-name": "docs", "vector": ?, "top-k": 5,
+  "filter": {"field": ?}, "include-vector": false}`` (``?`` = positional params).
+* ``jdbc`` / ``sqlite``: SQL on SQLite (stdlib) with a ``cosine_similarity`` UDF; the
+  RAG pattern ``... ORDER BY cosine_similarity(<vector col>, ?) DESC LIMIT k`` is
+  executed as a GPU kNN over an HBM mirror of the vector column (the reference
+  example ``EX/docker-chatbot/chatbot.yaml:36`` runs exactly this query on HerdDB).
+* cassandra / astra / astra-vector-db / milvus / opensearch / pinecone / solr: their
+  client libraries are not part of this image -> a datasource that fails loudly.
+"""
+from __future__ import annotations
+
+import json
+import logging
+import math
+import re
+import sqlite3
+import threading
+from typing import Any, Dict, List, Optional, Sequence
+
+from ...engine.vector_store import VectorStoreRegistry
+
+log = logging.getLogger(__name__)
+
+
+class DataSource:
+    is_async_friendly = False
+
+    def fetch_data(self, query: str, params: List[Any]) -> List[Dict[str, Any]]:
+        raise NotImplementedError
+
+    def execute_statement(self, query: str, generated_keys: Sequence[str], params: List[Any]) -> Dict[str, Any]:
+        raise NotImplementedError
+
+    def close(self) -> None:
+        pass
+
+
+def _bind_json(query: str, params: List[Any]) -> Any:
+    """Replace bare ``?`` placeholders (outside strings) with JSON-encoded params."""
+    out, i, pi, in_str = [], 0, 0, None
+    while i < len(query):
+        c = query[i]
+        if in_str:
+            out.append(c)
+            if c == "\\":
+                out.append(query[i + 1])
+                i += 1
+            elif c == in_str:
+                in_str = None
+        elif c in ('"', "'"):
+            in_str = c
+            out.append(c)
+        elif c == "?":
+            if pi >= len(params):
+                raise ValueError("not enough parameters for query")
+            out.append(json.dumps(params[pi]))
+            pi += 1
+        else:
+            out.append(c)
+        i += 1
+    return json.loads("".join(out))
+
+
+class LocalVectorDataSource(DataSource):
+    is_async_friendly = True
+
+    def __init__(self, cfg: Dict[str, Any]):
+        self.cfg = cfg
+        self.default_collection = cfg.get("collection-name") or cfg.get("collection") or "default"
+
+    def _store(self, name: Optional[str], dim: Optional[int] = None):
+        return VectorStoreRegistry.get(name or self.default_collection, dim)
+
+    def fetch_data(self, query, params):
+        q = _bind_json(query, params) if isinstance(query, str) else query
+        coll = q.get("collection-name") or q.get("collection")
+        vec = q.get("vector")
+        if vec is None:
+            raise ValueError("local vector query needs a 'vector'")
+        k = int(q.get("top-k", q.get("topK", q.get("limit", 10))))
+        flt = q.get("filter") or {}
+        if not VectorStoreRegistry.exists(coll or self.default_collection):
+            return []
+        store = self._store(coll)
+        over = k if not flt else min(64, max(k * 4, k))
+        rows = store.search([vec], over, with_vectors=bool(q.get("include-vector", False)))[0]
+        if flt:
+            rows = [r for r in rows if all(r.get(f) == v for f, v in flt.items())]
+        rows = rows[:k]
+        if q.get("include-vector"):
+            for r in rows:
+                r["vector"] = r.get("vector")
+        return rows
+
+    def execute_statement(self, query, generated_keys, params):
+        q = _bind_json(query, params) if isinstance(query, str) else query
+        action = q.get("action", "upsert")
+        coll = q.get("collection-name") or q.get("collection")
+        if action == "delete":
+            n = self._store(coll).delete([q["id"]]) if VectorStoreRegistry.exists(coll or
+                                                                               self.default_collection) else 0
+            return {"deleted": n}
+        vec = q["vector"]
+        store = self._store(coll, len(vec))
+        store.upsert([q["id"]], [vec], [q.get("metadata") or {}])
+        return {"id": q["id"]}
+
+
+def _cosine(a, b) -> Optional[float]:
+    if a is None or b is None:
+        return None
+    if isinstance(a, str):
+        a = json.loads(a)
+    if isinstance(b, str):
+        b = json.loads(b)
+    num = sum(x * y for x, y in zip(a, b))
+    da = math.sqrt(sum(x * x for x in a))
+    db = math.sqrt(sum(y * y for y in b))
+    return num / (da * db) if da and db else 0.0
+
+
+_KNN = re.compile(
+    r"^\s*select\s+(?P<cols>.+?)\s+from\s+(?P<table>[\w.]+)\s*(?P<where>where\s+.+?)?\s*order\s+by\s+"
+    r"cosine_similarity\s*\(\s*(?P<col>\w+)\s*,\s*(?:cast\s*\(\s*)?\?(?:\s+as\s+[\w\s]+\))?\s*\)\s+desc\s+"
+    r"limit\s+(?P<k>\d+)\s*;?\s*$", re.I | re.S)
+
+_dbs: Dict[str, "SqliteDataSource"] = {}
+_dbs_lock = threading.Lock()
+
+
+class SqliteDataSource(DataSource):
+    """JDBC-compatible SQL on SQLite with GPU kNN for cosine-similarity ORDER BY."""
+
+    def __init__(self, cfg: Dict[str, Any]):
+        url = str(cfg.get("url") or cfg.get("path") or "memory")
+        m = re.match(r"^jdbc:sqlite:(.+)$", url)
+        self.path = m.group(1) if m else None
+        self.name = url
+        if self.path is None:
+            # any other JDBC url (e.g. herddb) -> a process-wide in-memory database per url
+            self.conn = sqlite3.connect(f"file:{re.sub(r'[^A-Za-z0-9]', '_', url)}?mode=memory&cache=shared",
+                                        uri=True, check_same_thread=False)
+        else:
+            self.conn = sqlite3.connect(self.path, check_same_thread=False)
+        self.conn.create_function("cosine_similarity", 2, _cosine, deterministic=True)
+        self.conn.row_factory = sqlite3.Row
+        self.lock = threading.RLock()
+        self.vector_cols: Dict[tuple, str] = {}  # (table, column) -> store name
+
+    @staticmethod
+    def shared(cfg: Dict[str, Any]) -> "SqliteDataSource":
+        key = str(cfg.get("url") or cfg.get("path") or "memory")
+        with _dbs_lock:
+            ds = _dbs.get(key)
+            if ds is None:
+                ds = SqliteDataSource(cfg)
+                _dbs[key] = ds
+            return ds
+
+    def _store_name(self, table: str, col: str) -> str:
+        return f"sqlite:{self.name}:{table.lower()}:{col.lower()}"
+
+    def _sql_param(self, p):
+        if isinstance(p, (list, dict)):
+            return json.dumps(p)
+        return p
+
+    def fetch_data(self, query, params):
+        m = _KNN.match(query)
+        if m and not m.group("where"):
+            table, col, k = m.group("table"), m.group("col"), int(m.group("k"))
+            name = self._store_name(table, col)
+            vec = params[-1]
+            if isinstance(vec, str):
+                vec = json.loads(vec)
+            self._ensure_mirror(table, col, len(vec))
+            store = VectorStoreRegistry.get(name)
+            hits = store.search([vec], min(k, 64))[0] if len(store) else []
+            if not hits:
+                return []
+            ids = [h["id"] for h in hits]
+            with self.lock:
+                cur = self.conn.execute(
+                    f"SELECT {m.group('cols')}, rowid AS __rowid FROM {table} WHERE rowid IN "
+                    f"({','.join('?' * len(ids))})", ids)
+                rows = {r["__rowid"]: {k2: r[k2] for k2 in r.keys() if k2 != "__rowid"} for r in cur.fetchall()}
+            return [_decode_row(rows[i]) for i in ids if i in rows]
+        with self.lock:
+            cur = self.conn.execute(query, [self._sql_param(p) for p in params])
+            return [_decode_row({k: r[k] for k in r.keys()}) for r in cur.fetchall()]
+
+    def execute_statement(self, query, generated_keys, params):
+        with self.lock:
+            cur = self.conn.execute(query, [self._sql_param(p) for p in params])
+            self.conn.commit()
+            res = {"count": cur.rowcount}
+            if generated_keys:
+                res["generated-keys"] = {generated_keys[0]: cur.lastrowid}
+            self._invalidate_mirrors_for(query)
+            return res
+
+    # --- HBM mirror of vector columns
+    def _ensure_mirror(self, table: str, col: str, dim: int) -> None:
+        key = (table.lower(), col.lower())
+        if key in self.vector_cols:
+            return
+        name = self._store_name(table, col)
+        store = VectorStoreRegistry.get(name, dim)
+        with self.lock:
+            rows = self.conn.execute(f"SELECT rowid, {col} FROM {table}").fetchall()
+        ids, vecs = [], []
+        for r in rows:
+            v = r[1]
+            if v is None:
+                continue
+            v = json.loads(v) if isinstance(v, str) else v
+            if len(v) == dim:
+                ids.append(r[0])
+                vecs.append(v)
+        if ids:
+            store.upsert(ids, vecs)
+        self.vector_cols[key] = name
+
+    def _invalidate_mirrors_for(self, query: str) -> None:
+        ql = query.lower()
+        for (table, col), name in list(self.vector_cols.items()):
+            if re.search(rf"\b{re.escape(table)}\b", ql):
+                VectorStoreRegistry.drop(name)
+                self.vector_cols.pop((table, col), None)
+
+
+def _decode_row(r: Dict[str, Any]) -> Dict[str, Any]:
+    out = {}
+    for k, v in r.items():
+        if isinstance(v, str) and v[:1] == "[" and v[-1:] == "]":
+            try:
+                v = json.loads(v)
+            except ValueError:
+                pass
+        out[k] = v
+    return out
+
+
+class UnavailableDataSource(DataSource):
+    def __init__(self, service: str):
+        self.service = service
+
+    def _fail(self, *a, **k):
+        raise RuntimeError(f"datasource service '{self.service}' needs its client library and network access, "
+                           f"which are not available in this build; use service 'local' (GPU vector store) or "
+                           f"'jdbc' (SQLite + GPU kNN)")
+
+    fetch_data = _fail
+    execute_statement = _fail
+
+
+def datasource_for(cfg: Optional[Dict[str, Any]]) -> DataSource:
+    if cfg is None:
+        raise ValueError("datasource is required")
+    svc = cfg.get("service", "local")
+    if svc in ("local", "local-gpu"):
+        return LocalVectorDataSource(cfg)
+    if svc in ("jdbc", "sqlite"):
+        return SqliteDataSource.shared(cfg)
+    return UnavailableDataSource(svc)

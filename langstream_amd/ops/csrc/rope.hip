@@ -9,17 +9,20 @@
 // v_cache  : [NB, Hkv, D, BS]   (TRANSPOSED: keys contiguous, so attention reads V^T
 //            MFMA fragments with one 16-B load per lane -- see attention kernels)
 //
-// A workgroup handles 64 consecutive tokens.  Phase 1 rotates q/k (16-B vectors,
-// HF "rotate_half" convention) and stores rotated K rows.  Phase 2 stages V for one
-// kv head at a time in LDS and writes it transposed with lane == token, so a wave's
-// 2-B stores for one head-dim d land on consecutive cache addresses.
+// Grid: x = tiles of TOK tokens, y = head groups.  y < nq: rotate HG query heads;
+// nq <= y < nq+nk: rotate HG key heads and store them to the K cache; the last Hkv
+// y-slices write one kv head of V transposed, with lane == token inside a tile so a
+// wave's 2-B stores for one head-dim row land on consecutive cache addresses.
+// Many small workgroups: a decode step (T = batch) still spreads over
+// (T/16) x (Hq/8 + Hkv/8 + Hkv) workgroups instead of one.
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
 #include "common.h"
 
 namespace {
 
-constexpr int TOK = 64;
+constexpr int TOK = 16;  // tokens per workgroup tile
+constexpr int HG = 8;    // heads per rotate workgroup
 
 template <int D>
 __global__ void __launch_bounds__(256) rope_cache_kernel(bf16* __restrict__ qkv, const int32_t* __restrict__ pos,
@@ -27,70 +30,71 @@ __global__ void __launch_bounds__(256) rope_cache_kernel(bf16* __restrict__ qkv,
                                                          const int64_t* __restrict__ slots, bf16* __restrict__ kc,
                                                          bf16* __restrict__ vc, int64_t T, int Hq, int Hkv, int BS,
                                                          int max_pos, int apply_rope, int64_t nslots) {
-  __shared__ __attribute__((aligned(16))) bf16 vt[TOK][D + 8];
+  constexpr int HALF = D / 2;
+  constexpr int VPH = HALF / 8;  // 16-B vectors per half head
   const int64_t t0 = (int64_t)blockIdx.x * TOK;
   const int ntok = (int)min((int64_t)TOK, T - t0);
   const int row_elems = (Hq + 2 * Hkv) * D;
-  constexpr int HALF = D / 2;
-  constexpr int VPH = HALF / 8;  // 16-B vectors per half head
-  // ---- phase 1: rotate q and k heads, write k to the cache
-  const int tasks = ntok * (Hq + Hkv) * VPH;
-  for (int i = threadIdx.x; i < tasks; i += blockDim.x) {
-    const int tl = i / ((Hq + Hkv) * VPH);
-    const int rem = i - tl * (Hq + Hkv) * VPH;
-    const int h = rem / VPH, c = rem - h * VPH;
-    const int64_t t = t0 + tl;
-    bf16* base = qkv + t * row_elems + h * D;  // k heads follow q heads contiguously
-    float a[8], b[8];
-    unpack8(ld16(base + c * 8), a);
-    unpack8(ld16(base + HALF + c * 8), b);
-    if (apply_rope) {
-      const int p = min(max(pos[t], 0), max_pos - 1);
-      const float* cs = cos_sin + (int64_t)p * D;
-      float co[8], si[8];
-      *reinterpret_cast<float4*>(co) = *reinterpret_cast<const float4*>(cs + c * 8);
-      *reinterpret_cast<float4*>(co + 4) = *reinterpret_cast<const float4*>(cs + c * 8 + 4);
-      *reinterpret_cast<float4*>(si) = *reinterpret_cast<const float4*>(cs + HALF + c * 8);
-      *reinterpret_cast<float4*>(si + 4) = *reinterpret_cast<const float4*>(cs + HALF + c * 8 + 4);
+  const int nq = (Hq + HG - 1) / HG, nk = (Hkv + HG - 1) / HG;
+  const int y = blockIdx.y;
+  if (y < nq + nk) {
+    // ---- rotate a group of q (or k) heads for the tile's tokens
+    const bool is_k = y >= nq;
+    const int h0 = is_k ? Hq + (y - nq) * HG : y * HG;
+    const int hend = is_k ? Hq + Hkv : Hq;
+    const int nh = min(HG, hend - h0);
+    const int tasks = ntok * nh * VPH;
+    for (int i = threadIdx.x; i < tasks; i += blockDim.x) {
+      const int tl = i / (nh * VPH);
+      const int rem = i - tl * nh * VPH;
+      const int h = h0 + rem / VPH, c = rem % VPH;
+      const int64_t t = t0 + tl;
+      bf16* base = qkv + t * row_elems + h * D;
+      float a[8], b[8];
+      unpack8(ld16(base + c * 8), a);
+      unpack8(ld16(base + HALF + c * 8), b);
+      if (apply_rope) {
+        const int p = min(max(pos[t], 0), max_pos - 1);
+        const float* cs = cos_sin + (int64_t)p * D;
+        float co[8], si[8];
+        *reinterpret_cast<float4*>(co) = *reinterpret_cast<const float4*>(cs + c * 8);
+        *reinterpret_cast<float4*>(co + 4) = *reinterpret_cast<const float4*>(cs + c * 8 + 4);
+        *reinterpret_cast<float4*>(si) = *reinterpret_cast<const float4*>(cs + HALF + c * 8);
+        *reinterpret_cast<float4*>(si + 4) = *reinterpret_cast<const float4*>(cs + HALF + c * 8 + 4);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float x1 = a[j], x2 = b[j];
-        a[j] = x1 * co[j] - x2 * si[j];
-        b[j] = x2 * co[j] + x1 * si[j];
+        for (int j = 0; j < 8; ++j) {
+          const float x1 = a[j], x2 = b[j];
+          a[j] = x1 * co[j] - x2 * si[j];
+          b[j] = x2 * co[j] + x1 * si[j];
+        }
+      }
+      const uint4 pa = pack8(a), pb = pack8(b);
+      st16(base + c * 8, pa);
+      st16(base + HALF + c * 8, pb);
+      if (is_k) {
+        const int64_t s = slots[t];
+        if (s >= 0 && s < nslots) {
+          const int64_t blk = s / BS, off = s - blk * BS;
+          bf16* kd = kc + ((blk * Hkv + (h - Hq)) * BS + off) * D;
+          st16(kd + c * 8, pa);
+          st16(kd + HALF + c * 8, pb);
+        }
       }
     }
-    const uint4 pa = pack8(a), pb = pack8(b);
-    st16(base + c * 8, pa);
-    st16(base + HALF + c * 8, pb);
-    if (h >= Hq) {
-      const int64_t s = slots[t];
-      if (s >= 0 && s < nslots) {
-        const int64_t blk = s / BS, off = s - blk * BS;
-        bf16* kd = kc + ((blk * Hkv + (h - Hq)) * BS + off) * D;
-        st16(kd + c * 8, pa);
-        st16(kd + HALF + c * 8, pb);
-      }
-    }
+    return;
   }
-  // ---- phase 2: V, transposed through LDS
-  const int lane_tok = threadIdx.x & 63;
-  const int wid = threadIdx.x >> 6;
-  int64_t my_slot = lane_tok < ntok ? slots[t0 + lane_tok] : -1;
-  if (my_slot >= nslots) my_slot = -1;
-  for (int hv = 0; hv < Hkv; ++hv) {
-    __syncthreads();
-    for (int i = threadIdx.x; i < ntok * (D / 8); i += blockDim.x) {
-      const int tl = i / (D / 8), c = i - tl * (D / 8);
-      const bf16* src = qkv + (t0 + tl) * row_elems + (Hq + Hkv + hv) * D + c * 8;
-      *reinterpret_cast<uint4*>(&vt[tl][c * 8]) = ld16(src);
-    }
-    __syncthreads();
-    if (my_slot >= 0) {
-      const int64_t blk = my_slot / BS, off = my_slot - blk * BS;
-      bf16* vd = vc + ((blk * Hkv + hv) * (int64_t)D) * BS + off;
-      for (int d = wid; d < D; d += 4) vd[(int64_t)d * BS] = vt[lane_tok][d];
-    }
-  }
+  // ---- V of one kv head, transposed into the cache.  thread -> (token lane, d-row)
+  const int hv = y - nq - nk;
+  const int tl = threadIdx.x % TOK;
+  const int dr = threadIdx.x / TOK;  // 0..15
+  if (tl >= ntok) return;
+  const int64_t t = t0 + tl;
+  const int64_t s = slots[t];
+  if (s < 0 || s >= nslots) return;
+  const int64_t blk = s / BS, off = s - blk * BS;
+  const bf16* src = qkv + t * row_elems + (Hq + Hkv + hv) * D;
+  bf16* vd = vc + ((blk * Hkv + hv) * (int64_t)D) * BS + off;
+  for (int d = dr; d < D; d += 256 / TOK) vd[(int64_t)d * BS] = src[d];
 }
 
 }  // namespace
@@ -111,7 +115,8 @@ void rope_and_cache(at::Tensor qkv, at::Tensor pos, at::Tensor cos_sin, at::Tens
   TORCH_CHECK(cos_sin.size(1) == D);
   if (T == 0) return;
   auto stream = at::hip::getCurrentHIPStream();
-  const int grid = (int)((T + TOK - 1) / TOK);
+  const int nq = (int)((Hq + HG - 1) / HG), nk = (int)((Hkv + HG - 1) / HG);
+  dim3 grid((unsigned)((T + TOK - 1) / TOK), nq + nk + (int)Hkv);
 #define LAUNCH(DD)                                                                                          \
   rope_cache_kernel<DD><<<grid, 256, 0, stream>>>((bf16*)qkv.data_ptr(), pos.data_ptr<int32_t>(),          \
                                                   cos_sin.data_ptr<float>(), slots.data_ptr<int64_t>(),     \

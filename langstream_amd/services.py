@@ -1,0 +1,186 @@
+"""Process-wide registry of AI services and GPU engines shared by every agent.
+
+One MI355X process hosts at most one engine per model: all chat/text-completion agents
+using ``llama-3-8b`` share one continuous-batching LLMEngine (so their requests batch
+together on the GPU), all embedding agents share one EmbeddingEngine per encoder, and
+vector collections live in one HBM store registry.  The device is ``cuda:$LOCAL_RANK``
+(one process per GPU) or CPU when no GPU is present.
+
+Configuration (``local-gpu-configuration`` resource):
+  chat-model (llama-3-8b), embeddings-model (bge-small-en), device, max-batch (256),
+  max-model-len (4096), max-prefill-tokens (16384), kv-fraction (0.55), use-graphs (true),
+  weights-path / embeddings-weights-path (optional safetensors with our packed layout).
+"""
+from __future__ import annotations
+
+import logging
+import os
+import re
+import threading
+from typing import Any, Dict, Optional
+
+log = logging.getLogger(__name__)
+
+
+def _norm_model(name: Optional[str]) -> str:
+    if not name:
+        return ""
+    n = name.split("/")[-1].lower()
+    n = re.sub(r"^meta-", "", n)
+    n = n.replace("_", "-")
+    aliases = {
+        "llama-3-8b-instruct": "llama-3-8b", "llama-3-8b": "llama-3-8b", "meta-llama-3-8b-instruct": "llama-3-8b",
+        "llama-3.1-8b-instruct": "llama-3.1-8b", "llama-3-70b-instruct": "llama-3-70b",
+        "meta-llama-3-70b-instruct": "llama-3-70b", "bge-small-en-v1.5": "bge-small-en-v1.5",
+        "multilingual-e5-small": "multilingual-e5-small", "all-minilm-l6-v2": "all-MiniLM-L6-v2",
+    }
+    return aliases.get(n, n)
+
+
+def default_device() -> str:
+    import torch
+    if torch.cuda.is_available():
+        return f"cuda:{int(os.environ.get('LOCAL_RANK', '0')) % max(1, torch.cuda.device_count())}"
+    return "cpu"
+
+
+class ServiceRegistry:
+    _default: Optional["ServiceRegistry"] = None
+    _dlock = threading.Lock()
+
+    def __init__(self, overrides: Optional[Dict[str, Any]] = None):
+        self.overrides = dict(overrides or {})
+        self._llms: Dict[str, Any] = {}
+        self._embedders: Dict[str, Any] = {}
+        self._lock = threading.RLock()
+        self.tp = None  # set by the TP launcher for the chat agent
+
+    @classmethod
+    def default(cls) -> "ServiceRegistry":
+        with cls._dlock:
+            if cls._default is None:
+                cls._default = ServiceRegistry()
+            return cls._default
+
+    @classmethod
+    def set_default(cls, reg: "ServiceRegistry") -> None:
+        with cls._dlock:
+            cls._default = reg
+
+    # ------------------------------------------------------------------ engines
+    def _local_cfg(self, cfg: Optional[Dict[str, Any]]) -> Dict[str, Any]:
+        c = dict(cfg or {})
+        c.update(self.overrides)
+        return c
+
+    def llm_engine(self, model: Optional[str], cfg: Optional[Dict[str, Any]] = None):
+        import torch
+        from .engine.llm_engine import LLMEngine
+        from .models.llama import LlamaModel, PRESETS
+        from .tokenizers import BPETokenizer
+        c = self._local_cfg(cfg)
+        name = _norm_model(c.get("force-chat-model") or model) or _norm_model(c.get("chat-model")) or "llama-3-8b"
+        if name not in PRESETS:
+            name = _norm_model(c.get("chat-model")) or "llama-3-8b"
+        with self._lock:
+            eng = self._llms.get(name)
+            if eng is not None:
+                return eng
+            device = c.get("device") or default_device()
+            mcfg = PRESETS[name]
+            dtype = torch.bfloat16 if device.startswith("cuda") else torch.float32
+            log.info("starting LLM engine %s on %s", name, device)
+            model_ = LlamaModel(mcfg, device=device, dtype=dtype, tp=self.tp)
+            if c.get("weights-path"):
+                from .models.loader import load_packed
+                model_.load_state_dict(load_packed(c["weights-path"], device))
+            tok = BPETokenizer.synthetic(mcfg.vocab_size) if not c.get("tokenizer-path") else (
+                BPETokenizer.from_hf_json(c["tokenizer-path"]))
+            eng = LLMEngine(model_, tok, max_model_len=int(c.get("max-model-len", 4096)),
+                            max_batch=int(c.get("max-batch", 256)),
+                            max_prefill_tokens=int(c.get("max-prefill-tokens", 16384)),
+                            kv_fraction=float(c.get("kv-fraction", 0.55)),
+                            use_graphs=str(c.get("use-graphs", "true")).lower() == "true",
+                            num_blocks=c.get("num-blocks"))
+            if eng.use_graphs and str(c.get("capture-graphs", "true")).lower() == "true":
+                eng.capture_graphs()
+            eng.start()
+            self._llms[name] = eng
+            return eng
+
+    def embedding_engine(self, model: Optional[str], cfg: Optional[Dict[str, Any]] = None):
+        import torch
+        from .engine.embedder import EmbeddingEngine
+        from .models.bert import BertEncoder, PRESETS
+        from .tokenizers import WordPieceTokenizer
+        c = self._local_cfg(cfg)
+        name = _norm_model(c.get("force-embeddings-model") or model) or _norm_model(c.get("embeddings-model"))
+        if name not in PRESETS:
+            name = _norm_model(c.get("embeddings-model")) or "bge-small-en"
+            if name not in PRESETS:
+                name = "bge-small-en"
+        with self._lock:
+            eng = self._embedders.get(name)
+            if eng is not None:
+                return eng
+            device = c.get("device") or default_device()
+            dtype = torch.bfloat16 if device.startswith("cuda") else torch.float32
+            enc = BertEncoder(PRESETS[name], device=device, dtype=dtype)
+            if c.get("embeddings-weights-path"):
+                from .models.loader import load_packed
+                enc.load_state_dict(load_packed(c["embeddings-weights-path"], device))
+            tok = WordPieceTokenizer.from_vocab_file(c["vocab-path"]) if c.get("vocab-path") else \
+                WordPieceTokenizer.synthetic(PRESETS[name].vocab_size)
+            eng = EmbeddingEngine(enc, tok, max_batch_tokens=int(c.get("max-batch-tokens", 32768)))
+            eng.start()
+            self._embedders[name] = eng
+            return eng
+
+    # ------------------------------------------------------------------ services by agent config
+    def completions_service(self, agent_cfg: Dict[str, Any], model: Optional[str]):
+        from .agents.genai import services as s
+        if "local" in agent_cfg:
+            eng = self.llm_engine(model, agent_cfg["local"])
+            return s.LocalCompletionsService(eng, eng.tok, model or "local")
+        if "openai" in agent_cfg:
+            oc = agent_cfg["openai"]
+            if oc.get("provider") == "local":
+                eng = self.llm_engine(model, oc)
+                return s.LocalCompletionsService(eng, eng.tok, model or "local")
+            return s.OpenAIService(oc, model)
+        if "ollama" in agent_cfg:
+            return s.OllamaService(agent_cfg["ollama"], model)
+        for k in ("vertex", "bedrock", "huggingface"):
+            if k in agent_cfg:
+                return s.UnavailableService(k, "remote completions need network access to the provider")
+        raise ValueError("no AI service configured for completions")
+
+    def embeddings_service(self, agent_cfg: Dict[str, Any], model: Optional[str]):
+        from .agents.genai import services as s
+        if "local" in agent_cfg:
+            return s.LocalEmbeddingsService(self.embedding_engine(model, agent_cfg["local"]))
+        if "huggingface" in agent_cfg:
+            hc = agent_cfg["huggingface"]
+            if hc.get("provider", "local") == "local":
+                return s.LocalEmbeddingsService(self.embedding_engine(model, hc))
+            return s.HuggingFaceAPIService(hc, model)
+        if "openai" in agent_cfg:
+            oc = agent_cfg["openai"]
+            if oc.get("provider") == "local":
+                return s.LocalEmbeddingsService(self.embedding_engine(model, oc))
+            return s.OpenAIService(oc, model)
+        if "ollama" in agent_cfg:
+            return s.OllamaService(agent_cfg["ollama"], model)
+        for k in ("vertex", "bedrock"):
+            if k in agent_cfg:
+                return s.UnavailableService(k, "remote embeddings need network access to the provider")
+        raise ValueError("no AI service configured for embeddings")
+
+    def shutdown(self) -> None:
+        with self._lock:
+            for e in self._llms.values():
+                e.stop()
+            for e in self._embedders.values():
+                e.stop()
+            self._llms.clear()
+            self._embedders.clear()

@@ -148,7 +148,7 @@ def _synthetic_bpe(vocab_size: int, num_merges: int, bos: str, eos: tuple) -> BP
         if t not in vocab:
             vocab[t] = len(vocab)
     n_special = max(0, vocab_size - len(vocab))
-    names = [bos, *eos]
+    names = [bos, *eos, "<|start_header_id|>", "<|end_header_id|>"]
     specials = {}
     for i in range(n_special):
         name = names[i] if i < len(names) else f"<|reserved_special_token_{i}|>"
