@@ -325,6 +325,10 @@ class QueryStep(Step):
             raise ValueError("mode must be query or execute")
         if not self.output_field and self.mode == "query":
             raise ValueError("output-field is required")
+        self._batcher = None
+        if self.mode == "query" and not self.loop_over and hasattr(self.ds, "fetch_data_batch"):
+            from ...api.util import MicroBatcher
+            self._batcher = MicroBatcher(lambda ps: self.ds.fetch_data_batch(self.query, ps), 64, "query-batcher")
 
     def _params(self, ctx) -> list:
         return [eval_expression(f, ctx) for f in self.fields]
@@ -340,6 +344,24 @@ class QueryStep(Step):
 
     def process_async(self, rec) -> Future:
         fut: Future = Future()
+        if self._batcher is not None:
+            try:
+                inner = self._batcher.submit(self._params(rec.el_context()))
+            except Exception as e:  # noqa: BLE001
+                fut.set_exception(e)
+                return fut
+
+            def done(f):
+                try:
+                    rows = f.result()
+                    r = (rows[0] if rows else None) if self.only_first else rows
+                    rec.set_result_field(r, self.output_field)
+                    fut.set_result(None)
+                except BaseException as e:  # noqa: BLE001
+                    fut.set_exception(e)
+
+            inner.add_done_callback(done)
+            return fut
 
         def run():
             try:

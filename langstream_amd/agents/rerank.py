@@ -54,26 +54,57 @@ def bm25_scores(texts: List[str], query: str, k1: float, b: float) -> List[float
     return out
 
 
+def _java_split(t: str) -> List[str]:
+    d = t.split()
+    return [""] + d if t[:1].isspace() else (d if d else [""] if t == "" else d)
+
+
 def mmr(docs: List[Any], texts: List[str], embs: np.ndarray, query: str, max_: int, lam: float, k1: float,
         b: float) -> List[Any]:
+    """Vectorised MMR: same scores as :func:`bm25_scores` + mean-cosine diversity, with
+    the term-frequency matrix and the pairwise cosine matrix computed once."""
+    n = len(docs)
+    if n == 0:
+        return []
     norms = np.linalg.norm(embs, axis=1)
     safe = np.where(norms == 0, 1.0, norms)
     unit = embs / safe[:, None]
     cos = unit @ unit.T
     cos[norms == 0, :] = 0
     cos[:, norms == 0] = 0
-    remaining = list(range(len(docs)))
+    toks = [t.split() if t.strip() else [] for t in texts]
+    toks = [([""] + d if t[:1].isspace() else d) for t, d in zip(texts, toks)]
+    q = query.split()
+    if query[:1].isspace():
+        q = [""] + q
+    qc = Counter(q)
+    terms = list(qc)
+    qw = np.array([qc[t] for t in terms], dtype=np.float64)
+    tf = np.zeros((n, len(terms)), dtype=np.float64)
+    for i, d in enumerate(toks):
+        c = Counter(d)
+        for j, t in enumerate(terms):
+            tf[i, j] = c.get(t, 0)
+    dl = np.array([len(d) for d in toks], dtype=np.float64)
+    remaining = np.ones(n, dtype=bool)
     selected: List[int] = []
-    while remaining and len(selected) < max_:
-        rel = bm25_scores([texts[i] for i in remaining], query, k1, b)
-        best, best_score = None, -math.inf
-        for j, i in enumerate(remaining):
-            div = float(cos[i, selected].mean()) if selected else 0.0
-            sc = lam * rel[j] - (1 - lam) * div
-            if sc > best_score:
-                best, best_score = i, sc
+    div_sum = np.zeros(n, dtype=np.float64)
+    while remaining.any() and len(selected) < max_:
+        idx = np.nonzero(remaining)[0]
+        N = len(idx)
+        avgdl = dl[idx].mean()
+        df = (tf[idx] > 0).sum(0)
+        idf = np.log((N - df + 0.5) / (df + 0.5) + 1.0)
+        denom = tf[idx] + k1 * (1 - b + b * (dl[idx] / avgdl if avgdl else 1.0))[:, None]
+        with np.errstate(divide="ignore", invalid="ignore"):
+            part = np.where(denom > 0, tf[idx] * (k1 + 1) / denom, 0.0)
+        rel = (part * idf[None, :] * qw[None, :]).sum(1)
+        div = div_sum[idx] / len(selected) if selected else np.zeros(N)
+        score = lam * rel - (1 - lam) * div
+        best = int(idx[int(np.argmax(score))])
         selected.append(best)
-        remaining.remove(best)
+        remaining[best] = False
+        div_sum += cos[:, best]
     return [docs[i] for i in selected]
 
 

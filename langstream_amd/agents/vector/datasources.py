@@ -79,25 +79,34 @@ class LocalVectorDataSource(DataSource):
         return VectorStoreRegistry.get(name or self.default_collection, dim)
 
     def fetch_data(self, query, params):
-        q = _bind_json(query, params) if isinstance(query, str) else query
-        coll = q.get("collection-name") or q.get("collection")
-        vec = q.get("vector")
-        if vec is None:
-            raise ValueError("local vector query needs a 'vector'")
-        k = int(q.get("top-k", q.get("topK", q.get("limit", 10))))
-        flt = q.get("filter") or {}
-        if not VectorStoreRegistry.exists(coll or self.default_collection):
-            return []
-        store = self._store(coll)
-        over = k if not flt else min(64, max(k * 4, k))
-        rows = store.search([vec], over, with_vectors=bool(q.get("include-vector", False)))[0]
-        if flt:
-            rows = [r for r in rows if all(r.get(f) == v for f, v in flt.items())]
-        rows = rows[:k]
-        if q.get("include-vector"):
-            for r in rows:
-                r["vector"] = r.get("vector")
-        return rows
+        return self.fetch_data_batch(query, [params])[0]
+
+    def fetch_data_batch(self, query, params_list):
+        """Many queries of the same shape -> ONE kNN kernel launch per collection."""
+        parsed = [_bind_json(query, p) if isinstance(query, str) else query for p in params_list]
+        out: List[Any] = [None] * len(parsed)
+        groups: Dict[tuple, List[int]] = {}
+        for i, q in enumerate(parsed):
+            if q.get("vector") is None:
+                raise ValueError("local vector query needs a 'vector'")
+            coll = q.get("collection-name") or q.get("collection") or self.default_collection
+            k = int(q.get("top-k", q.get("topK", q.get("limit", 10))))
+            flt = q.get("filter") or {}
+            key = (coll, k, json.dumps(flt, sort_keys=True), bool(q.get("include-vector", False)))
+            groups.setdefault(key, []).append(i)
+        for (coll, k, flt_s, inc), idxs in groups.items():
+            if not VectorStoreRegistry.exists(coll):
+                for i in idxs:
+                    out[i] = []
+                continue
+            flt = json.loads(flt_s)
+            over = k if not flt else min(64, max(k * 4, k))
+            res = self._store(coll).search([parsed[i]["vector"] for i in idxs], over, with_vectors=inc)
+            for i, rows in zip(idxs, res):
+                if flt:
+                    rows = [r for r in rows if all(r.get(f) == v for f, v in flt.items())]
+                out[i] = rows[:k]
+        return out
 
     def execute_statement(self, query, generated_keys, params):
         q = _bind_json(query, params) if isinstance(query, str) else query

@@ -284,3 +284,42 @@ class _Bucket:
             log.exception("batch processor raised")
             if not fut.done():
                 fut.set_exception(e)
+
+
+class MicroBatcher(Generic[T]):
+    """Opportunistic batching without added latency: a worker thread takes the first
+    queued item and everything else already queued (up to ``max_batch``), runs
+    ``fn(items) -> results`` once, and resolves each item's Future.  Under load calls
+    coalesce into large batches (one GPU launch); when idle an item runs alone at once."""
+
+    def __init__(self, fn: Callable[[List[T]], List[Any]], max_batch: int = 64, name: str = "micro-batcher"):
+        import queue as _q
+        self.fn = fn
+        self.max_batch = max(1, max_batch)
+        self._q: "_q.Queue" = _q.Queue()
+        self._thread = threading.Thread(target=self._run, name=name, daemon=True)
+        self._thread.start()
+
+    def submit(self, item: T) -> Future:
+        f: Future = Future()
+        self._q.put((item, f))
+        return f
+
+    def _run(self) -> None:
+        import queue as _q
+        while True:
+            first = self._q.get()
+            batch = [first]
+            while len(batch) < self.max_batch:
+                try:
+                    batch.append(self._q.get_nowait())
+                except _q.Empty:
+                    break
+            try:
+                res = self.fn([b[0] for b in batch])
+                for (_, f), r in zip(batch, res):
+                    f.set_result(r)
+            except BaseException as e:  # noqa: BLE001
+                for _, f in batch:
+                    if not f.done():
+                        f.set_exception(e)

@@ -102,22 +102,28 @@ class TPInfo:
 
 @dataclass
 class AttnMeta:
-    """Per-step attention metadata (device tensors)."""
-    is_prefill: bool
-    positions: torch.Tensor          # [T] int32
-    slots: torch.Tensor              # [T] int64
-    block_tables: torch.Tensor       # [B, max_blocks] int32
-    # prefill
-    q_start: Optional[torch.Tensor] = None   # [B] int32
-    q_len: Optional[torch.Tensor] = None     # [B] int32
-    ctx_len: Optional[torch.Tensor] = None   # [B] int32
-    tiles: Optional[torch.Tensor] = None     # [ntiles, 2] int32
-    last_token_idx: Optional[torch.Tensor] = None  # [B] int64 rows whose logits we need
-    # decode
-    ctx_lens: Optional[torch.Tensor] = None  # [B] int32
+    """Per-step attention metadata (device tensors).
+
+    A step packs ``num_decode`` decode tokens (rows [0, num_decode), one per running
+    sequence) followed by prefill chunks (rows [num_decode, T)); either part may be
+    empty.  Decode rows use the paged decode kernel, prefill rows the paged prefill
+    kernel (``q_start`` is the ABSOLUTE first row of each prefill sequence)."""
+    positions: torch.Tensor                      # [T] int32
+    slots: torch.Tensor                          # [T] int64
+    num_decode: int = 0
+    # decode part
+    d_block_tables: Optional[torch.Tensor] = None  # [nd, max_blocks] int32
+    d_ctx_lens: Optional[torch.Tensor] = None      # [nd] int32
     nsplit: int = 1
     blocks_per_split: int = 1 << 30
     workspace: Optional[torch.Tensor] = None
+    # prefill part
+    num_prefill_tokens: int = 0
+    p_block_tables: Optional[torch.Tensor] = None  # [np, max_blocks] int32
+    q_start: Optional[torch.Tensor] = None         # [np] int32 (absolute rows)
+    q_len: Optional[torch.Tensor] = None           # [np] int32
+    ctx_len: Optional[torch.Tensor] = None         # [np] int32
+    tiles: Optional[torch.Tensor] = None           # [ntiles, 2] int32
 
 
 class LlamaLayer:
@@ -210,13 +216,19 @@ class LlamaModel:
             qkv = F.linear(x, layer.qkv_w)
             ops.rope_and_cache(qkv, meta.positions, self.cos_sin, meta.slots, kc, vc, self.hq, self.hkv)
             q = qkv[:, : self.hq * D]
-            if meta.is_prefill:
-                attn = ops.paged_prefill_attention(q, kc, vc, meta.block_tables, meta.q_start, meta.q_len,
-                                                   meta.ctx_len, meta.tiles, self.hq, self.scale)
-            else:
-                attn = ops.paged_decode_attention(q, kc, vc, meta.block_tables, meta.ctx_lens, self.scale,
+            nd = meta.num_decode
+            if meta.num_prefill_tokens == 0:
+                attn = ops.paged_decode_attention(q, kc, vc, meta.d_block_tables, meta.d_ctx_lens, self.scale,
                                                   nsplit=meta.nsplit, blocks_per_split=meta.blocks_per_split,
                                                   workspace=meta.workspace)
+            else:
+                attn = torch.empty(q.shape[0], self.hq * D, dtype=q.dtype, device=q.device)
+                if nd:
+                    ops.paged_decode_attention(q[:nd], kc, vc, meta.d_block_tables, meta.d_ctx_lens, self.scale,
+                                               out=attn[:nd], nsplit=meta.nsplit,
+                                               blocks_per_split=meta.blocks_per_split, workspace=meta.workspace)
+                ops.paged_prefill_attention(q, kc, vc, meta.p_block_tables, meta.q_start, meta.q_len, meta.ctx_len,
+                                            meta.tiles, self.hq, self.scale, out=attn)
             o = F.linear(attn, layer.o_w)
             self.tp.all_reduce(o)
             ops.fused_add_rmsnorm(o, residual, layer.post_norm, eps)

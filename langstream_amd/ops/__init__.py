@@ -160,7 +160,11 @@ def paged_decode_attention(q, k_cache, v_cache, block_tables, ctx_lens, scale, o
                                      min(blocks_per_split, block_tables.shape[1]), ws)
         return out
     r = ref.paged_decode_attention(q.reshape(B, Hq, D), k_cache, v_cache, block_tables, ctx_lens, scale)
-    return r.reshape(B, Hq * D)
+    r = r.reshape(B, Hq * D)
+    if out is not None:
+        out.copy_(r)
+        return out
+    return r
 
 
 def prefill_tiles(q_lens: Sequence[int], G: int, prefix_lens: Sequence[int] | None = None) -> torch.Tensor:
@@ -186,7 +190,12 @@ def paged_prefill_attention(q, k_cache, v_cache, block_tables, q_start, q_len, c
         hip().paged_prefill_attention(out, q, k_cache, v_cache, block_tables, q_start, q_len, ctx_len, tiles,
                                       Hq, scale)
         return out
-    return ref.paged_prefill_attention(q, k_cache, v_cache, block_tables, q_start, q_len, ctx_len, Hq, scale)
+    r = ref.paged_prefill_attention(q, k_cache, v_cache, block_tables, q_start, q_len, ctx_len, Hq, scale)
+    if out is None:
+        return r
+    for s, n in zip(q_start.tolist(), q_len.tolist()):
+        out[s: s + n] = r[s: s + n]
+    return out
 
 
 def varlen_encoder_attention(qkv, q_start, q_len, tiles, Hq, Hkv, scale, out=None):

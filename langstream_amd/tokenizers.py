@@ -141,6 +141,7 @@ def _unicode_to_bytes() -> dict:
 
 @functools.lru_cache(maxsize=8)
 def _synthetic_bpe(vocab_size: int, num_merges: int, bos: str, eos: tuple) -> BPETokenizer:
+    num_merges = max(0, min(num_merges, vocab_size - 256 - 16))  # leave room for special tokens
     merges = lib().train_bpe(builtin_corpus(), num_merges, 2)
     vocab = {bytes([b]): b for b in range(256)}
     for a, b in merges:
