@@ -74,6 +74,19 @@ class MutableRecord:
         m.message_key = self.message_key
         return m
 
+    def shallow_copy(self) -> "MutableRecord":
+        """Copy sharing nested objects: only the top-level key/value maps and the
+        properties are duplicated, enough for set_result_field on the copy (used for
+        every streamed answer chunk, where a deep copy of embeddings-laden values
+        would dominate the cost)."""
+        m = MutableRecord(dict(self.key) if isinstance(self.key, dict) else self.key,
+                          dict(self.value) if isinstance(self.value, dict) else self.value,
+                          dict(self.properties), self.input_topic, self.event_time, self.source)
+        m.output_topic = self.output_topic
+        m.drop = self.drop
+        m.message_key = self.message_key
+        return m
+
     def to_record(self) -> Optional[Record]:
         if self.drop:
             return None

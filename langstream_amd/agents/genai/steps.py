@@ -431,7 +431,7 @@ class ChatCompletionsStep(Step):
             return None
 
         def consume(answer_id, index, content, last):
-            c = rec.copy()
+            c = rec.shallow_copy()
             c.properties["stream-id"] = answer_id
             c.properties["stream-index"] = str(index)
             c.properties["stream-last-message"] = "true" if last else "false"

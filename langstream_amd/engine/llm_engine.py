@@ -27,6 +27,7 @@ engine:
 from __future__ import annotations
 
 import itertools
+import os
 import logging
 import queue
 import threading
@@ -238,8 +239,28 @@ class LLMEngine:
 
     # ------------------------------------------------------------------ loop
     def _loop(self) -> None:
+        import sys
+        # the engine thread shares the GIL with agent threads: a short switch interval
+        # bounds how long host bookkeeping elsewhere can delay the next GPU launch
+        sys.setswitchinterval(min(sys.getswitchinterval(), 0.001))
         if self.is_gpu:
             torch.cuda.set_device(self.device)
+        prof_path = os.environ.get("LANGSTREAM_PROFILE_ENGINE")
+        if prof_path:
+            import cProfile
+            import pstats
+            pr = cProfile.Profile()
+            pr.enable()
+            try:
+                self._loop_body()
+            finally:
+                pr.disable()
+                with open(prof_path, "w") as f:
+                    pstats.Stats(pr, stream=f).sort_stats("cumulative").print_stats(60)
+            return
+        self._loop_body()
+
+    def _loop_body(self) -> None:
         while not self._stop.is_set():
             if not self.has_work():
                 self._wake.wait(0.05)
