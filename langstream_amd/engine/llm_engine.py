@@ -10,9 +10,13 @@ engine:
 * unified steps: every step carries one decode token per running sequence plus, when
   prompts are waiting, chunked-prefill tokens (``max_prefill_tokens`` per step), so new
   requests never stall the sequences already decoding;
+* the scheduler describes a step in a fixed-layout pinned "arena" through numpy views
+  (``engine/arena.py``); the native ``StepExecutor`` runs the whole step -- upload,
+  token feedback, forward, logit deltas, sampling, download -- in ONE GIL-released
+  call, so the agent threads sharing the interpreter cannot stall the GPU;
 * pure-decode steps replay a HIP graph captured per batch-size bucket (one graph serves
   every context length: the split-KV grid is sized for ``max_model_len``); mixed steps
-  run eagerly;
+  run eagerly from C++;
 * one-step lookahead: the next step's input tokens are gathered ON DEVICE from the
   previous step's sampled tokens, so step N+1 is launched before step N's tokens are
   copied back -- host bookkeeping (detokenisation, streaming callbacks, scheduling)
@@ -21,14 +25,14 @@ engine:
 * sampling on device (temperature / top-k / top-p / seed / penalties / logit-bias,
   log-probs of the sampled token + top-n alternatives for FLARE);
 * recompute-preemption when KV blocks run out;
-* tensor parallel: rank 0 schedules and broadcasts each step over RCCL, all ranks run
-  the sharded forward (all-reduce inside), rank 0 samples.
+* tensor parallel: rank 0 schedules; its executor broadcasts the device arena over
+  RCCL and the other ranks' executors (``worker_loop``, pure C++) mirror every step.
 """
 from __future__ import annotations
 
 import itertools
-import os
 import logging
+import os
 import queue
 import threading
 import time
@@ -40,11 +44,15 @@ import torch
 import torch.distributed as dist
 
 from .. import ops
-from ..models.llama import AttnMeta, LlamaModel
+from ..models.llama import LlamaModel
 from ..native import lib
+from .arena import (H_BUCKET, H_KIND, H_ND, H_NDELTA, H_NGATHER, H_NPS, H_NROWS, H_NTILES, H_NTOP, H_ROWS_ALL,
+                    H_T, KIND_STEP, ArenaLayout, NativeStepExecutor, PyStepExecutor)
 
 log = logging.getLogger(__name__)
 BLOCK = ops.KV_BLOCK
+NSLOTS = 3          # arena ring: one being filled, one in flight, one being retired
+MAX_DELTAS = 1 << 16
 
 
 @dataclass
@@ -109,6 +117,20 @@ class Request:
         return self.prompt_ids + self.output_ids
 
     @property
+    def num_tokens(self) -> int:
+        return len(self.prompt_ids) + len(self.output_ids)
+
+    def token_at(self, i: int) -> int:
+        n = len(self.prompt_ids)
+        return self.prompt_ids[i] if i < n else self.output_ids[i - n]
+
+    def tokens(self, s: int, e: int) -> List[int]:
+        n = len(self.prompt_ids)
+        if e <= n:
+            return self.prompt_ids[s:e]
+        return (self.prompt_ids[s:] if s < n else []) + self.output_ids[max(0, s - n): e - n]
+
+    @property
     def total_len(self) -> int:
         return len(self.prompt_ids) + self.num_launched
 
@@ -123,16 +145,9 @@ class Request:
 @dataclass
 class _InFlight:
     reqs: List[Request]
-    tok: torch.Tensor            # device int32 [n]
-    lp: torch.Tensor             # device f32 [n]
-    top_ids: Optional[torch.Tensor]
-    top_lps: Optional[torch.Tensor]
-    host_tok: torch.Tensor       # pinned copies
-    host_lp: torch.Tensor
-    host_ti: Optional[torch.Tensor]
-    host_tl: Optional[torch.Tensor]
-    event: Optional[object]
-    step_id: int = 0
+    slot: int
+    n_top: int
+    step_id: int
 
 
 class LLMEngine:
@@ -173,6 +188,19 @@ class LLMEngine:
             self.kv_caches.append((kc, vc))
         self.allocator = lib().BlockAllocator(self.num_blocks)
         self.nsplit, self.bps = ops.decode_splits(self.max_blocks_per_seq)
+        # ---- step arena + executor
+        G = model.hq // model.hkv
+        max_tokens = max_prefill_tokens + max_batch
+        max_tiles = (max_prefill_tokens * G + ops.PREFILL_ROWS - 1) // ops.PREFILL_ROWS + max_batch + 1
+        self.layout = ArenaLayout.build(max_tokens, max_batch, self.max_blocks_per_seq, max_tiles, MAX_DELTAS)
+        if self.is_gpu:
+            self.exec = NativeStepExecutor(model, self.kv_caches, self.layout, NSLOTS, self.nsplit, self.bps,
+                                           self.use_graphs, self.device)
+        else:
+            self.exec = PyStepExecutor(model, self.kv_caches, self.layout, NSLOTS, self.nsplit, self.bps,
+                                       self.device, self.tp.group, self.tp.world)
+        self._slot = 0
+        self._G = G
         self._ids = itertools.count(1)
         self._inbox: "queue.Queue[Request]" = queue.Queue()
         self.waiting: List[Request] = []
@@ -188,10 +216,10 @@ class LLMEngine:
         self.buckets = sorted(set(graph_buckets or [b for b in (1, 2, 4, 8, 16, 24, 32, 48, 64, 96, 128, 160, 192,
                                                                  224, 256, 320, 384, 448, 512) if b <= max_batch]
                                   + [max_batch]))
-        self._graphs: Dict[int, dict] = {}
         self._eos = set(self.cfg.eos_token_ids)
         if tokenizer is not None and getattr(tokenizer, "eos_ids", None):
             self._eos |= set(tokenizer.eos_ids)
+        self._eos_list = sorted(self._eos)
         self._tok_bytes: Optional[List[bytes]] = None
 
     # ------------------------------------------------------------------ public api
@@ -232,10 +260,26 @@ class LLMEngine:
             self._thread.join(timeout=30)
             self._thread = None
         if self.tp.world > 1 and self.tp.rank == 0:
-            self._tp_send_header(kind=3, n=0, t=0)  # tell workers to exit
+            self._flush()
+            self.exec.shutdown()  # tell the workers to leave worker_loop()
 
     def has_work(self) -> bool:
         return bool(self.waiting or self.running or not self._inbox.empty() or self._inflight is not None)
+
+    def capture_graphs(self, sizes: Optional[Sequence[int]] = None) -> None:
+        """Capture decode graphs up front (every TP rank captures in lock-step)."""
+        if not self.use_graphs:
+            return
+        self._flush()
+        for b in sizes or self.buckets:
+            self.exec.capture(b)
+
+    def worker_loop(self) -> None:
+        """Non-zero TP ranks: mirror rank 0's steps until it stops."""
+        assert self.tp.world > 1 and self.tp.rank != 0
+        if self.is_gpu:
+            torch.cuda.set_device(self.device)
+        self.exec.worker_loop()
 
     # ------------------------------------------------------------------ loop
     def _loop(self) -> None:
@@ -349,7 +393,7 @@ class LLMEngine:
             if r.finished:
                 self.waiting.pop(0)
                 continue
-            total = len(r.all_ids)
+            total = r.num_tokens
             remaining = total - r.num_computed
             n = min(remaining, budget)
             need = self._blocks_needed(r, r.num_computed + n)
@@ -397,266 +441,170 @@ class LLMEngine:
     def _launch(self, decode: List[Request], chunks) -> _InFlight:
         nd = len(decode)
         npf = sum(n for _, n in chunks)
+        T = nd + npf
+        sample_reqs = list(decode) + [r for r, n in chunks if r.num_computed + n >= r.num_tokens]
+        nrows = len(sample_reqs)
+        n_top = min(max((r.params.logprobs for r in sample_reqs), default=0), 20)
+        B = 0
+        if npf == 0 and self.use_graphs and nd <= self.buckets[-1] and n_top == 0:
+            B = self._bucket(nd)
+            if not self.exec.has_graph(B):
+                self._flush()  # capture reuses the token-feedback buffer
+                self.exec.capture(B)
         prev = self._inflight
-        # ---- decode rows (host arrays)
-        ids_np = np.zeros(nd + npf, dtype=np.int32)
-        pos_np = np.zeros(nd + npf, dtype=np.int32)
-        slot_np = np.full(nd + npf, -1, dtype=np.int64)
-        gather_dst, gather_src = [], []
+        self._slot = slot = (self._slot + 1) % NSLOTS
+        self.exec.wait_in(slot)
+        a = self.exec.inputs[slot]
+        ids, pos, slots = a["ids"], a["pos"], a["slots"]
+        # ---- decode rows: one token each, input = previous sample (host or on-device feedback)
+        ng = 0
+        gdst, gsrc = a["gdst"], a["gsrc"]
+        dbt, dctx = a["dbt"], a["dctx"]
         for j, r in enumerate(decode):
             p = r.num_computed
             if r.pending_row >= 0:
                 assert prev is not None and r.pending_step == prev.step_id, "lost in-flight token"
-                gather_dst.append(j)
-                gather_src.append(r.pending_row)
+                gdst[ng] = j
+                gsrc[ng] = r.pending_row
+                ng += 1
+                ids[j] = 0
             else:
-                ids_np[j] = r.all_ids[p]
-            pos_np[j] = p
-            slot_np[j] = r.blocks[p // BLOCK] * BLOCK + p % BLOCK
-        # ---- prefill rows
-        sample_reqs = list(decode)
-        last_rows = []
-        q_start, q_len, ctx_len, prefix = [], [], [], []
+                ids[j] = r.token_at(p)
+            pos[j] = p
+            blk = r.blocks
+            slots[j] = blk[p // BLOCK] * BLOCK + p % BLOCK
+            dbt[j, : len(blk)] = blk
+            dctx[j] = p + 1
+        if B > nd:  # graph padding rows: no KV write, empty context, greedy
+            ids[nd:B] = 0
+            pos[nd:B] = 0
+            slots[nd:B] = -1
+            dctx[nd:B] = 0
+        # ---- prefill chunks
         t = nd
-        for r, n in chunks:
+        last_rows = []
+        q_len, prefix = [], []
+        pbt = a["pbt"]
+        for k, (r, n) in enumerate(chunks):
             s = r.num_computed
-            ids = r.all_ids[s: s + n]
-            ids_np[t: t + n] = ids
-            pos_np[t: t + n] = np.arange(s, s + n, dtype=np.int32)
+            ids[t: t + n] = r.tokens(s, s + n)
+            pp = np.arange(s, s + n, dtype=np.int64)
+            pos[t: t + n] = pp
             blk = np.asarray(r.blocks, dtype=np.int64)
-            pp = np.arange(s, s + n)
-            slot_np[t: t + n] = blk[pp // BLOCK] * BLOCK + pp % BLOCK
-            q_start.append(t)
+            slots[t: t + n] = blk[pp // BLOCK] * BLOCK + pp % BLOCK
+            pbt[k, : len(blk)] = blk
+            a["q_start"][k] = t
+            a["ctx_len"][k] = s + n
             q_len.append(n)
-            ctx_len.append(s + n)
             prefix.append(s)
             t += n
-            if s + n >= len(r.all_ids):
+            if s + n >= r.num_tokens:
                 last_rows.append(t - 1)
-                sample_reqs.append(r)
-        maxb = self.max_blocks_per_seq
-        host = {"ids": ids_np, "pos": pos_np, "slots": slot_np}
-        if nd:
-            dbt = np.zeros((nd, maxb), dtype=np.int32)
-            ctx = np.zeros(nd, dtype=np.int32)
-            for j, r in enumerate(decode):
-                dbt[j, : len(r.blocks)] = r.blocks
-                ctx[j] = r.num_computed + 1
-            host["dbt"], host["ctx"] = dbt, ctx
+        ntiles = 0
         if chunks:
-            pbt = np.zeros((len(chunks), max(len(r.blocks) for r, _ in chunks)), dtype=np.int32)
-            for j, (r, _) in enumerate(chunks):
-                pbt[j, : len(r.blocks)] = r.blocks
-            host.update(pbt=pbt, q_start=np.asarray(q_start, np.int32), q_len=np.asarray(q_len, np.int32),
-                        ctx_len=np.asarray(ctx_len, np.int32),
-                        tiles=ops.prefill_tiles(q_len, self.model.hq // self.model.hkv, prefix).numpy())
+            a["q_len"][: len(chunks)] = q_len
+            ntiles = ops.prefill_tiles_np(q_len, self._G, prefix, out=a["tiles"])
+        rows_all = nrows == T
+        if not rows_all:
+            a["rows"][:nd] = np.arange(nd)
+            a["rows"][nd:nrows] = last_rows
+        # ---- sampling parameters (+ graph padding rows) and logit deltas
+        nsr = max(nrows, B)
+        temp, top_p, top_k, seeds, steps = a["temp"], a["top_p"], a["top_k"], a["seeds"], a["steps"]
+        for j, r in enumerate(sample_reqs):
+            p = r.params
+            temp[j] = p.temperature
+            top_p[j] = p.top_p
+            top_k[j] = p.top_k
+            seeds[j] = r.seed
+            steps[j] = r.num_launched  # index of the token being sampled
+        if nsr > nrows:
+            temp[nrows:nsr] = 0.0
+            top_p[nrows:nsr] = 1.0
+            top_k[nrows:nsr] = 0
+            seeds[nrows:nsr] = 0
+            steps[nrows:nsr] = 0
+        ndelta = self._write_deltas(a["deltas"], sample_reqs)
+        # ---- header
+        h = a["hdr"]
+        h[:] = 0
+        h[H_KIND] = KIND_STEP
+        h[H_T] = T
+        h[H_ND] = nd
+        h[H_NPS] = len(chunks)
+        h[H_NTILES] = ntiles
+        h[H_NROWS] = nrows
+        h[H_NGATHER] = ng
+        h[H_NDELTA] = ndelta
+        h[H_NTOP] = n_top
+        h[H_BUCKET] = B
+        h[H_ROWS_ALL] = 1 if rows_all else 0
         # ---- advance host state (KV of these tokens is being written by this step)
         for r in decode:
             r.num_computed += 1
         for r, n in chunks:
             r.num_computed += n
-            if r.num_computed >= len(r.all_ids) and r not in self.running:
+            if r.num_computed >= r.num_tokens and r not in self.running:
                 self.running.append(r)
-        for r in sample_reqs:
+        self._step_id += 1
+        for j, r in enumerate(sample_reqs):
             r.num_launched += 1
-        gd = torch.tensor(gather_dst, dtype=torch.long) if gather_dst else None
-        gs = torch.tensor(gather_src, dtype=torch.long) if gather_src else None
+            r.pending_row = j
+            r.pending_step = self._step_id
         # ---- run
-        if npf == 0 and self.use_graphs and nd <= self.buckets[-1]:
-            logits = self._decode_graph(nd, host, gd, gs, prev)
+        self.exec.launch(slot, slot)
+        if B:
             self.stats["decode_steps"] += 1
             self.stats["graph_steps"] += 1
         else:
-            logits = self._forward_eager(host, nd, npf, last_rows, gd, gs, prev)
-            self.stats["mixed_steps" if nd else "prefill_steps"] += 1
+            self.stats["mixed_steps" if nd and npf else ("prefill_steps" if npf else "decode_steps")] += 1
         self.stats["prefill_tokens"] += npf
         self.stats["decode_tokens"] += nd
-        self._step_id += 1
-        if not sample_reqs:
-            e = torch.empty(0, dtype=torch.int32)
-            return _InFlight([], e, e, None, None, e, e, None, None, None, self._step_id)
-        for j, r in enumerate(sample_reqs):
-            r.pending_row = j
-            r.pending_step = self._step_id
-        st = self._sample(logits, sample_reqs)
-        st.step_id = self._step_id
-        return st
+        return _InFlight(sample_reqs, slot, n_top, self._step_id)
 
-    def _ids_with_gather(self, ids_dev: torch.Tensor, gd, gs, prev) -> None:
-        if gd is not None:
-            ids_dev[gd.to(self.device, non_blocking=True)] = prev.tok[gs.to(self.device, non_blocking=True)]
-
-    def _forward_eager(self, host, nd, npf, last_rows, gd, gs, prev) -> torch.Tensor:
-        dev = self.device
-        d = {k: torch.from_numpy(v).to(dev, non_blocking=True) for k, v in host.items()}
-        self._ids_with_gather(d["ids"], gd, gs, prev)
-        if self.tp.world > 1:
-            self._tp_send_step(dict(host, last=np.asarray(last_rows, np.int64)), d["ids"])
-        return self._eager_core(d, nd, npf, last_rows)
-
-    def _eager_core(self, d, nd, npf, last_rows) -> torch.Tensor:
-        D = self.cfg.head_dim
-        ws = None
-        if nd:
-            ws = torch.empty(max(1, nd * self.model.hq * self.nsplit * (D + 2)), dtype=torch.float32,
-                             device=self.device)
-        meta = AttnMeta(positions=d["pos"], slots=d["slots"], num_decode=nd,
-                        d_block_tables=d.get("dbt"), d_ctx_lens=d.get("ctx"), nsplit=self.nsplit,
-                        blocks_per_split=self.bps, workspace=ws, num_prefill_tokens=npf,
-                        p_block_tables=d.get("pbt"), q_start=d.get("q_start"), q_len=d.get("q_len"),
-                        ctx_len=d.get("ctx_len"), tiles=d.get("tiles"))
-        hidden = self.model.forward(d["ids"], meta, self.kv_caches)
-        rows = list(range(nd)) + list(last_rows)
-        if len(rows) == hidden.shape[0]:
-            sel = hidden
-        else:
-            sel = hidden.index_select(0, torch.tensor(rows, dtype=torch.long).to(self.device, non_blocking=True))
-        return self.model.logits(sel)
-
-    # -- graphs
-    def _alloc_decode_buffers(self, B: int) -> dict:
-        dev = self.device
-        D = self.cfg.head_dim
-        return {
-            "ids": torch.zeros(B, dtype=torch.int32, device=dev),
-            "pos": torch.zeros(B, dtype=torch.int32, device=dev),
-            "slots": torch.full((B,), -1, dtype=torch.int64, device=dev),
-            "dbt": torch.zeros(B, self.max_blocks_per_seq, dtype=torch.int32, device=dev),
-            "ctx": torch.zeros(B, dtype=torch.int32, device=dev),
-            "ws": torch.empty(max(1, B * self.model.hq * self.nsplit * (D + 2)), dtype=torch.float32, device=dev),
-        }
-
-    def _decode_forward(self, buf: dict) -> torch.Tensor:
-        meta = AttnMeta(positions=buf["pos"], slots=buf["slots"], num_decode=buf["ids"].shape[0],
-                        d_block_tables=buf["dbt"], d_ctx_lens=buf["ctx"], nsplit=self.nsplit,
-                        blocks_per_split=self.bps, workspace=buf["ws"])
-        hidden = self.model.forward(buf["ids"], meta, self.kv_caches)
-        return self.model.logits(hidden)
-
-    def _get_graph(self, B: int) -> dict:
-        g = self._graphs.get(B)
-        if g is not None:
-            return g
-        buf = self._alloc_decode_buffers(B)
-        g = {"buf": buf, "graph": None, "out": None}
-        if self.use_graphs:
-            s = torch.cuda.Stream(self.device)
-            s.wait_stream(torch.cuda.current_stream(self.device))
-            with torch.cuda.stream(s):
-                for _ in range(2):  # warm up (allocator, hipBLASLt heuristics)
-                    self._decode_forward(buf)
-            torch.cuda.current_stream(self.device).wait_stream(s)
-            graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(graph, pool=self._graph_pool()):
-                out = self._decode_forward(buf)
-            g["graph"], g["out"] = graph, out
-        self._graphs[B] = g
-        return g
-
-    def _graph_pool(self):
-        if not hasattr(self, "_pool"):
-            self._pool = torch.cuda.graph_pool_handle()
-        return self._pool
-
-    def capture_graphs(self, sizes: Optional[Sequence[int]] = None) -> None:
-        for b in sizes or self.buckets:
-            if self.tp.world > 1:
-                self._tp_send_header(kind=4, n=b, t=0)  # every rank captures the same bucket together
-            self._get_graph(b)
-
-    def _decode_graph(self, nd: int, host, gd, gs, prev) -> torch.Tensor:
-        B = self._bucket(nd)
-        g = self._get_graph(B)
-        buf = g["buf"]
-        pad = B - nd
-        ids = host["ids"]
-        pos, slots, ctx, dbt = host["pos"], host["slots"], host["ctx"], host["dbt"]
-        if pad:
-            ids = np.concatenate([ids, np.zeros(pad, np.int32)])
-            pos = np.concatenate([pos, np.zeros(pad, np.int32)])
-            slots = np.concatenate([slots, np.full(pad, -1, np.int64)])
-            ctx = np.concatenate([ctx, np.zeros(pad, np.int32)])
-            dbt = np.concatenate([dbt, np.zeros((pad, dbt.shape[1]), np.int32)])
-        buf["ids"].copy_(torch.from_numpy(ids), non_blocking=True)
-        buf["pos"].copy_(torch.from_numpy(pos), non_blocking=True)
-        buf["slots"].copy_(torch.from_numpy(slots), non_blocking=True)
-        buf["ctx"].copy_(torch.from_numpy(ctx), non_blocking=True)
-        buf["dbt"].copy_(torch.from_numpy(dbt), non_blocking=True)
-        self._ids_with_gather(buf["ids"], gd, gs, prev)
-        if self.tp.world > 1:
-            self._tp_send_decode(B, buf)
-        if g["graph"] is not None:
-            g["graph"].replay()
-            return g["out"][:nd]
-        return self._decode_forward(buf)[:nd]
-
-    # ------------------------------------------------------------------ sampling / retire
-    def _sample(self, logits: torch.Tensor, reqs: List[Request]) -> _InFlight:
-        n = len(reqs)
-        dev = logits.device
-        rows, toks, deltas = [], [], []
+    def _write_deltas(self, out: np.ndarray, reqs: List[Request]) -> int:
+        """(row, token, delta) triples: presence/frequency penalties, logit bias, and
+        EOS suppression until min_tokens."""
+        n = 0
+        cap = out.shape[0]
+        fview = out.view(np.float32)
         for j, r in enumerate(reqs):
             p = r.params
+            items = []
             if p.needs_history:
                 counts: Dict[int, int] = {}
                 for t in r.output_ids:
                     counts[t] = counts.get(t, 0) + 1
-                for t, c in counts.items():
-                    rows.append(j)
-                    toks.append(t)
-                    deltas.append(-(p.presence_penalty + p.frequency_penalty * c))
+                items += [(t, -(p.presence_penalty + p.frequency_penalty * c)) for t, c in counts.items()]
             if p.logit_bias:
-                for t, b in p.logit_bias.items():
-                    rows.append(j)
-                    toks.append(int(t))
-                    deltas.append(float(b))
-            if r.num_launched - 1 < p.min_tokens and not p.ignore_eos:
-                for t in self._eos:
-                    rows.append(j)
-                    toks.append(t)
-                    deltas.append(-1e9)
-        if rows:
-            logits = logits.clone()
-            ops.apply_logit_deltas(logits, torch.tensor(rows, dtype=torch.int32).to(dev),
-                                   torch.tensor(toks, dtype=torch.int32).to(dev),
-                                   torch.tensor(deltas, dtype=torch.float32).to(dev))
-        params = np.empty((n, 3), dtype=np.float32)
-        ints = np.empty((n, 3), dtype=np.int64)
-        for j, r in enumerate(reqs):
-            p = r.params
-            params[j] = (p.temperature, p.top_p, 0.0)
-            ints[j] = (p.top_k, r.seed, r.num_launched - 1)
-        pd = torch.from_numpy(params).to(dev, non_blocking=True)
-        idv = torch.from_numpy(ints).to(dev, non_blocking=True)
-        n_top = min(max(r.params.logprobs for r in reqs), 20)
-        tok, lp, ti, tl = ops.sample(logits, pd[:, 0].contiguous(), idv[:, 0].to(torch.int32), pd[:, 1].contiguous(),
-                                     idv[:, 1].contiguous(), idv[:, 2].contiguous(), n_top=n_top)
-        if self.is_gpu:
-            ht = torch.empty(n, dtype=torch.int32, pin_memory=True)
-            hl = torch.empty(n, dtype=torch.float32, pin_memory=True)
-            ht.copy_(tok, non_blocking=True)
-            hl.copy_(lp, non_blocking=True)
-            hti = htl = None
-            if ti is not None:
-                hti = torch.empty(ti.shape, dtype=torch.int32, pin_memory=True)
-                htl = torch.empty(tl.shape, dtype=torch.float32, pin_memory=True)
-                hti.copy_(ti, non_blocking=True)
-                htl.copy_(tl, non_blocking=True)
-            ev = torch.cuda.Event()
-            ev.record()
-        else:
-            ht, hl, hti, htl, ev = tok, lp, ti, tl, None
-        return _InFlight(reqs, tok, lp, ti, tl, ht, hl, hti, htl, ev)
+                items += [(int(t), float(b)) for t, b in p.logit_bias.items()]
+            if r.num_launched < p.min_tokens and not p.ignore_eos:
+                items += [(t, -1e9) for t in self._eos_list]
+            for t, d in items:
+                if n >= cap:
+                    log.warning("logit delta capacity (%d) exceeded; dropping the rest", cap)
+                    return n
+                out[n, 0] = j
+                out[n, 1] = t
+                fview[n, 2] = d
+                n += 1
+        return n
 
+    # ------------------------------------------------------------------ retire
     def _retire(self, st: _InFlight) -> None:
         t0 = time.perf_counter()
-        if st.event is not None:
-            st.event.synchronize()
+        self.exec.wait_out(st.slot)
         self.stats["wait_ms"] += (time.perf_counter() - t0) * 1000
-        tok_h = st.host_tok.tolist()
-        lp_h = st.host_lp.tolist()
-        ti_h = st.host_ti.tolist() if st.host_ti is not None else None
-        tl_h = st.host_tl.tolist() if st.host_tl is not None else None
+        n = len(st.reqs)
+        if n == 0:
+            return
+        o = self.exec.outputs[st.slot]
+        tok_h = o["tok"][:n].tolist()
+        lp_h = o["lp"][:n].tolist()
+        ti_h = tl_h = None
+        if st.n_top:
+            ti_h = o["ti"][: n * st.n_top].reshape(n, st.n_top).tolist()
+            tl_h = o["tl"][: n * st.n_top].reshape(n, st.n_top).tolist()
         now = time.perf_counter()
         for j, r in enumerate(st.reqs):
             if r.pending_step == st.step_id:
@@ -676,7 +624,7 @@ class LLMEngine:
                 reason = "stop"
             elif len(r.output_ids) >= p.max_tokens:
                 reason = "length"
-            elif len(r.all_ids) >= self.max_model_len:
+            elif r.num_tokens >= self.max_model_len:
                 reason = "length"
             delta = self._detok(r, t, final=reason is not None) if (r.callback is not None or p.stop) else ""
             if p.stop and reason is None:
@@ -746,79 +694,3 @@ class LLMEngine:
         if r in self.waiting:
             self.waiting.remove(r)
         self._release(r)
-
-    # ------------------------------------------------------------------ tensor parallel plumbing
-    # Rank 0 broadcasts a fixed 4-int header then the step's tensors; workers mirror it.
-    def _tp_send_header(self, kind: int, n: int, t: int, extra: int = 0) -> None:
-        h = torch.tensor([kind, n, t, extra], dtype=torch.int64, device=self.device)
-        dist.broadcast(h, src=self._tp_src(), group=self.tp.group)
-
-    def _tp_src(self) -> int:
-        return dist.get_global_rank(self.tp.group, 0) if self.tp.group is not None else 0
-
-    def _bcast(self, t: torch.Tensor) -> None:
-        dist.broadcast(t, src=self._tp_src(), group=self.tp.group)
-
-    _STEP_KEYS = ("pos", "slots", "dbt", "ctx", "pbt", "q_start", "q_len", "ctx_len", "tiles", "last")
-
-    def _tp_send_step(self, host: dict, ids_dev: torch.Tensor) -> None:
-        nd = host["dbt"].shape[0] if "dbt" in host else 0
-        T = host["ids"].shape[0]
-        self._tp_send_header(1, nd, T)
-        shapes = []
-        for k in self._STEP_KEYS:
-            a = host.get(k)
-            shapes += list(a.shape) + [0] * (2 - a.ndim) if a is not None else [-1, -1]
-        self._bcast(torch.tensor(shapes, dtype=torch.int64, device=self.device))
-        self._bcast(ids_dev)
-        for k in self._STEP_KEYS:
-            if host.get(k) is not None:
-                self._bcast(torch.from_numpy(np.ascontiguousarray(host[k])).to(self.device))
-
-    def _tp_send_decode(self, B: int, buf: dict) -> None:
-        self._tp_send_header(2, B, 0)
-        for k in ("ids", "pos", "slots", "ctx", "dbt"):
-            self._bcast(buf[k])
-
-    def worker_loop(self) -> None:
-        """Non-zero TP ranks: mirror rank 0's steps until told to stop."""
-        assert self.tp.world > 1 and self.tp.rank != 0
-        dev = self.device
-        dtypes = {"pos": torch.int32, "slots": torch.int64, "dbt": torch.int32, "ctx": torch.int32,
-                  "pbt": torch.int32, "q_start": torch.int32, "q_len": torch.int32, "ctx_len": torch.int32,
-                  "tiles": torch.int32, "last": torch.int64}
-        while True:
-            h = torch.empty(4, dtype=torch.int64, device=dev)
-            self._bcast(h)
-            kind, n, t, _ = (int(x) for x in h.tolist())
-            if kind == 3:
-                return
-            if kind == 4:
-                self._get_graph(n)
-                continue
-            if kind == 1:
-                shp = torch.empty(2 * len(self._STEP_KEYS), dtype=torch.int64, device=dev)
-                self._bcast(shp)
-                shp = shp.tolist()
-                ids = torch.empty(t, dtype=torch.int32, device=dev)
-                self._bcast(ids)
-                d = {"ids": ids}
-                for i, k in enumerate(self._STEP_KEYS):
-                    a, b = shp[2 * i], shp[2 * i + 1]
-                    if a < 0:
-                        continue
-                    x = torch.empty((a, b) if b else (a,), dtype=dtypes[k], device=dev)
-                    self._bcast(x)
-                    d[k] = x
-                npf = t - n
-                last_rows = d.pop("last").tolist() if "last" in d else []
-                self._eager_core(d, n, npf, last_rows)
-            elif kind == 2:
-                g = self._get_graph(n)
-                buf = g["buf"]
-                for k in ("ids", "pos", "slots", "ctx", "dbt"):
-                    self._bcast(buf[k])
-                if g["graph"] is not None:
-                    g["graph"].replay()
-                else:
-                    self._decode_forward(buf)

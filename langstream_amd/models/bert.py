@@ -105,6 +105,15 @@ class BertEncoder:
         """ids/pos: [T] int32 (packed), starts/lens: [B] int32 -> pooled [B, H]."""
         cfg = self.cfg
         nh = cfg.num_heads
+        mode = 0 if cfg.pooling == "cls" else 1
+        if self.device.type == "cuda" and ops.hip_available() and out_dtype in (torch.float32, self.dtype):
+            # native executor (ops/csrc/runner.hip): whole encoder with the GIL released
+            if getattr(self, "_runner", None) is None:
+                self._runner = ops.hip().BertRunner(
+                    self.wte, self.wpe, self.wtt, self.emb_g, self.emb_b,
+                    [[getattr(l, n) for n in BertLayer.NAMES] for l in self.layers], nh, cfg.ln_eps, self.scale,
+                    mode, cfg.normalize)
+            return self._runner.forward(ids, pos, starts, lens, tiles, out_dtype == torch.float32)
         x = ops.embed_layernorm(ids, pos, None, self.wte, self.wpe, self.wtt, self.emb_g, self.emb_b, cfg.ln_eps)
         for l in self.layers:
             qkv = F.linear(x, l.qkv_w, l.qkv_b)
@@ -115,7 +124,6 @@ class BertEncoder:
             ops.bias_gelu_(h, l.ff1_b)
             o2 = F.linear(h, l.ff2_w)
             x = ops.layernorm(o2, l.ln2_g, l.ln2_b, cfg.ln_eps, bias=l.ff2_b, residual=x)
-        mode = 0 if cfg.pooling == "cls" else 1
         return ops.pool_embeddings(x, starts, lens, mode, cfg.normalize, out_dtype=out_dtype)
 
     def pack(self, token_lists: List[List[int]]):

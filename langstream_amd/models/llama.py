@@ -241,6 +241,47 @@ class LlamaModel:
             x = d
         return x
 
+    def _native_runner(self, kv_caches: list):
+        """The C++ step executor (``ops/csrc/runner.hip``), built once per KV-cache set.
+        It issues the whole forward with the GIL released: a Python-driven forward
+        re-acquires the GIL after every op and stalls behind busy agent threads."""
+        key = id(kv_caches)
+        r = getattr(self, "_runner", None)
+        if r is not None and r[0] == key:
+            return r[1]
+        L = self.layers
+        pg = None
+        if self.tp.world > 1:
+            pg = self.tp.group if self.tp.group is not None else dist.group.WORLD
+        runner = ops.hip().LlamaRunner(
+            self.embed, [l.qkv_w for l in L], [l.o_w for l in L], [l.gate_up_w for l in L],
+            [l.down_w for l in L], [l.in_norm for l in L], [l.post_norm for l in L], self.final_norm,
+            self.lm_head, [kv[0] for kv in kv_caches], [kv[1] for kv in kv_caches], self.cos_sin, self.hq,
+            self.hkv, self.cfg.head_dim, self.cfg.rms_eps, self.scale, self.cfg.vocab_size, self.vocab_start, pg)
+        self._runner = (key, runner, kv_caches)
+        return runner
+
+    def forward_logits(self, ids: torch.Tensor, meta: AttnMeta, kv_caches: list,
+                       rows: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Forward + LM head for ``rows`` (all rows if None) -> f32 [N, V].  On the GPU
+        the native executor runs it; elsewhere the Python path (same math)."""
+        if self.device.type == "cuda" and ops.hip_available():
+            ws = meta.workspace
+            bps = meta.blocks_per_split
+            if meta.num_decode:
+                bps = min(bps, meta.d_block_tables.shape[1])
+                if meta.nsplit > 1:
+                    need = meta.num_decode * self.hq * meta.nsplit * (self.cfg.head_dim + 2)
+                    assert ws is not None and ws.numel() >= need, "decode workspace too small"
+            return self._native_runner(kv_caches).forward(
+                ids, meta.positions, meta.slots, meta.num_decode, meta.d_block_tables, meta.d_ctx_lens,
+                meta.nsplit, bps, ws, meta.num_prefill_tokens, meta.p_block_tables, meta.q_start, meta.q_len,
+                meta.ctx_len, meta.tiles, rows)
+        hidden = self.forward(ids, meta, kv_caches)
+        if rows is not None:
+            hidden = hidden.index_select(0, rows)
+        return self.logits(hidden)
+
     def logits(self, hidden: torch.Tensor) -> torch.Tensor:
         """[N, H] -> f32 [N, V] (vocab-parallel matmul + all-gather under TP)."""
         lg = F.linear(hidden, self.lm_head).float()

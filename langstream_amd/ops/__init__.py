@@ -181,6 +181,27 @@ def prefill_tiles(q_lens: Sequence[int], G: int, prefix_lens: Sequence[int] | No
     return t.reshape(-1, 2)
 
 
+def prefill_tiles_np(q_lens, G: int, prefix_lens, out=None):
+    """numpy twin of :func:`prefill_tiles` (no torch calls: used by the engine's
+    scheduler, which must not hand the GIL around).  Writes into ``out`` when given
+    and returns the number of tiles."""
+    import numpy as np
+    q_lens = np.asarray(q_lens, dtype=np.int64)
+    prefix = np.asarray(prefix_lens, dtype=np.int64)
+    rows = q_lens * G
+    n_per = (rows + PREFILL_ROWS - 1) // PREFILL_ROWS
+    seq = np.repeat(np.arange(len(q_lens)), n_per)
+    first = np.concatenate([np.arange(n) for n in n_per]) * PREFILL_ROWS if len(seq) else np.zeros(0, np.int64)
+    last = np.minimum(first + PREFILL_ROWS, rows[seq]) - 1
+    work = prefix[seq] + last // G
+    order = np.argsort(-work, kind="stable")
+    tiles = np.stack([seq[order], first[order]], axis=1).astype(np.int32)
+    if out is None:
+        return tiles
+    out[: len(tiles)] = tiles
+    return len(tiles)
+
+
 def paged_prefill_attention(q, k_cache, v_cache, block_tables, q_start, q_len, ctx_len, tiles, Hq, scale,
                             out=None):
     T = q.shape[0]

@@ -27,6 +27,7 @@ void pool_embeddings(at::Tensor out, at::Tensor x, at::Tensor start, at::Tensor 
 void l2_normalize_rows(at::Tensor out, at::Tensor x);
 void knn_topk(at::Tensor X, at::Tensor Q, int64_t K, at::Tensor out_s, at::Tensor out_i, at::Tensor ws_s,
               at::Tensor ws_i);
+void bind_runners(pybind11::module_& m);
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "langstream_amd CDNA4 (gfx950) kernels";
@@ -45,4 +46,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("pool_embeddings", &pool_embeddings);
   m.def("l2_normalize_rows", &l2_normalize_rows);
   m.def("knn_topk", &knn_topk);
+  bind_runners(m);
 }

@@ -1,0 +1,563 @@
+// Native model step executors: the whole Llama / BERT forward -- and for the LLM engine
+// the whole step (input upload, token feedback, forward, sampling, result download) --
+// issued from C++ with the GIL released.
+//
+// Why: in the streaming runtime the GPU engines share the Python GIL with agent
+// threads.  Every torch op called from Python releases and re-acquires the GIL, and
+// with busy agent threads each re-acquire waits up to the interpreter switch interval
+// -- measured 1.6-1.8 s of host time per mixed prefill step on MI355X with a
+// Python-driven forward, and still ~30 ms per decode step for the ~40 small ops of
+// input upload + sampling (cProfile, engine thread).  Here a step is ONE call.
+//
+// LlamaRunner: packed weights per layer (qkv / o / gate_up / down, two norms), paged
+//   KV caches, RoPE table; forward() handles decode rows, prefill rows or both in one
+//   step; optional tensor parallelism through a c10d ProcessGroup (RCCL all-reduce
+//   after o_proj and down_proj, all-gather of the vocab-sharded logits).
+// BertRunner: packed-varlen encoder + pooling.
+// StepExecutor: owns a ring of pinned host "arenas" (fixed layout, filled by the
+//   Python scheduler through numpy views), one device arena, the token feedback buffer
+//   and per-bucket HIP graphs.  launch(): one H2D copy of the arena, (TP: one RCCL
+//   broadcast of it to the other ranks), on-device feedback of the previous step's
+//   sampled tokens into this step's decode rows, forward, logit deltas, sampling, one
+//   D2H copy into a pinned result slot, event.  Decode-only steps replay a captured
+//   graph of gather+forward+deltas+sample; the counts those kernels need are read
+//   from the device copy of the arena header, so one graph serves every step of its
+//   bucket.  Non-zero TP ranks run worker_loop() entirely in C++.
+#include <torch/extension.h>
+#include <ATen/hip/HIPContext.h>
+#include <ATen/hip/HIPGraph.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
+#include <torch/csrc/distributed/c10d/ProcessGroup.hpp>
+
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+namespace py = pybind11;
+
+void rmsnorm(at::Tensor out, at::Tensor x, at::Tensor w, double eps);
+void fused_add_rmsnorm(at::Tensor x, at::Tensor residual, at::Tensor w, double eps);
+void layernorm(at::Tensor out, at::Tensor x, c10::optional<at::Tensor> bias, c10::optional<at::Tensor> residual,
+               at::Tensor g, at::Tensor b, double eps);
+void embed_layernorm(at::Tensor out, at::Tensor ids, at::Tensor pos_ids, c10::optional<at::Tensor> type_ids,
+                     at::Tensor wte, at::Tensor wpe, at::Tensor wtt, at::Tensor g, at::Tensor b, double eps);
+void silu_and_mul(at::Tensor out, at::Tensor x);
+void bias_gelu(at::Tensor x, c10::optional<at::Tensor> bias);
+void rope_and_cache(at::Tensor qkv, at::Tensor pos, at::Tensor cos_sin, at::Tensor slots, at::Tensor k_cache,
+                    at::Tensor v_cache, int64_t Hq, int64_t Hkv, bool apply_rope);
+void paged_decode_attention(at::Tensor out, at::Tensor q, at::Tensor k_cache, at::Tensor v_cache,
+                            at::Tensor block_tables, at::Tensor ctx_lens, double scale, int64_t nsplit,
+                            int64_t blocks_per_split, at::Tensor workspace);
+void paged_prefill_attention(at::Tensor out, at::Tensor q, at::Tensor k_cache, at::Tensor v_cache,
+                             at::Tensor block_tables, at::Tensor q_start, at::Tensor q_len, at::Tensor ctx_len,
+                             at::Tensor tiles, int64_t Hq, double scale);
+void varlen_encoder_attention(at::Tensor out, at::Tensor qkv, at::Tensor q_start, at::Tensor q_len,
+                              at::Tensor tiles, int64_t Hq, int64_t Hkv, double scale);
+void pool_embeddings(at::Tensor out, at::Tensor x, at::Tensor start, at::Tensor len, int64_t mode, bool normalize);
+void sample_tokens(at::Tensor logits, at::Tensor temperature, at::Tensor top_k, at::Tensor top_p, at::Tensor seeds,
+                   at::Tensor steps, at::Tensor out_tok, at::Tensor out_lp, at::Tensor top_ids, at::Tensor top_lps,
+                   int64_t n_top);
+
+#define HIP_OK(x)                                                                  \
+  do {                                                                             \
+    hipError_t e_ = (x);                                                           \
+    TORCH_CHECK(e_ == hipSuccess, #x " failed: ", hipGetErrorString(e_));          \
+  } while (0)
+
+namespace {
+
+// ---------------------------------------------------------------------------- Llama
+class LlamaRunner {
+ public:
+  LlamaRunner(at::Tensor embed, std::vector<at::Tensor> qkv_w, std::vector<at::Tensor> o_w,
+              std::vector<at::Tensor> gate_up_w, std::vector<at::Tensor> down_w, std::vector<at::Tensor> in_norm,
+              std::vector<at::Tensor> post_norm, at::Tensor final_norm, at::Tensor lm_head,
+              std::vector<at::Tensor> k_caches, std::vector<at::Tensor> v_caches, at::Tensor cos_sin, int64_t hq,
+              int64_t hkv, int64_t head_dim, double eps, double scale, int64_t vocab_size, int64_t vocab_start,
+              py::object process_group)
+      : embed_(embed), qkv_w_(qkv_w), o_w_(o_w), gate_up_w_(gate_up_w), down_w_(down_w), in_norm_(in_norm),
+        post_norm_(post_norm), final_norm_(final_norm), lm_head_(lm_head), kc_(k_caches), vc_(v_caches),
+        cos_sin_(cos_sin), hq_(hq), hkv_(hkv), d_(head_dim), eps_(eps), scale_(scale), vocab_(vocab_size),
+        vocab_start_(vocab_start) {
+    const size_t L = qkv_w_.size();
+    TORCH_CHECK(L > 0 && o_w_.size() == L && gate_up_w_.size() == L && down_w_.size() == L &&
+                in_norm_.size() == L && post_norm_.size() == L && kc_.size() == L && vc_.size() == L,
+                "inconsistent layer lists");
+    if (!process_group.is_none()) pg_ = py::cast<c10::intrusive_ptr<::c10d::ProcessGroup>>(process_group);
+  }
+
+  // f32 logits [rows or T, vocab]; decode rows are [0, num_decode), prefill rows after.
+  at::Tensor forward_impl(const at::Tensor& ids, const at::Tensor& pos, const at::Tensor& slots, int64_t num_decode,
+                          const at::Tensor& d_bt, const at::Tensor& d_ctx, int64_t nsplit, int64_t bps,
+                          const at::Tensor& ws, int64_t num_prefill, const at::Tensor& p_bt, const at::Tensor& q_start,
+                          const at::Tensor& q_len, const at::Tensor& ctx_len, const at::Tensor& tiles,
+                          const c10::optional<at::Tensor>& rows) {
+    const int64_t T = ids.size(0);
+    at::Tensor h = embed(ids);
+    at::Tensor residual = h;
+    at::Tensor x = at::empty_like(h);
+    rmsnorm(x, h, in_norm_[0], eps_);
+    const int64_t L = qkv_w_.size();
+    for (int64_t l = 0; l < L; ++l) {
+      at::Tensor qkv = at::linear(x, qkv_w_[l]);
+      rope_and_cache(qkv, pos, cos_sin_, slots, kc_[l], vc_[l], hq_, hkv_, true);
+      at::Tensor q = qkv.narrow(1, 0, hq_ * d_);
+      at::Tensor attn = at::empty({T, hq_ * d_}, qkv.options());
+      if (num_decode > 0)
+        paged_decode_attention(attn.narrow(0, 0, num_decode), q.narrow(0, 0, num_decode), kc_[l], vc_[l], d_bt,
+                               d_ctx, scale_, nsplit, bps, ws);
+      if (num_prefill > 0)
+        paged_prefill_attention(attn, q, kc_[l], vc_[l], p_bt, q_start, q_len, ctx_len, tiles, hq_, scale_);
+      at::Tensor o = at::linear(attn, o_w_[l]);
+      all_reduce(o);
+      fused_add_rmsnorm(o, residual, post_norm_[l], eps_);
+      at::Tensor gu = at::linear(o, gate_up_w_[l]);
+      at::Tensor a = at::empty({T, gu.size(1) / 2}, gu.options());
+      silu_and_mul(a, gu);
+      at::Tensor dn = at::linear(a, down_w_[l]);
+      all_reduce(dn);
+      fused_add_rmsnorm(dn, residual, l + 1 < L ? in_norm_[l + 1] : final_norm_, eps_);
+      x = dn;
+    }
+    at::Tensor sel = rows.has_value() ? x.index_select(0, *rows) : x;
+    at::Tensor lg = at::linear(sel, lm_head_).to(at::kFloat);
+    if (pg_) {
+      const int64_t world = pg_->getSize();
+      std::vector<at::Tensor> parts;
+      for (int64_t i = 0; i < world; ++i) parts.push_back(at::empty_like(lg));
+      std::vector<std::vector<at::Tensor>> outs{parts};
+      std::vector<at::Tensor> ins{lg.contiguous()};
+      pg_->allgather(outs, ins)->wait();
+      lg = at::cat(parts, 1);
+    }
+    if (lg.size(1) != vocab_) lg = lg.narrow(1, 0, vocab_).contiguous();
+    return lg;
+  }
+
+  at::Tensor forward(at::Tensor ids, at::Tensor pos, at::Tensor slots, int64_t num_decode,
+                     c10::optional<at::Tensor> d_bt, c10::optional<at::Tensor> d_ctx, int64_t nsplit, int64_t bps,
+                     c10::optional<at::Tensor> ws, int64_t num_prefill, c10::optional<at::Tensor> p_bt,
+                     c10::optional<at::Tensor> q_start, c10::optional<at::Tensor> q_len,
+                     c10::optional<at::Tensor> ctx_len, c10::optional<at::Tensor> tiles,
+                     c10::optional<at::Tensor> rows) {
+    at::Tensor none = at::empty({0}, ids.options().dtype(at::kInt));
+    auto get = [&](const c10::optional<at::Tensor>& t) { return t.has_value() ? *t : none; };
+    at::Tensor ws_t = ws.has_value() ? *ws : at::empty({0}, ids.options().dtype(at::kFloat));
+    TORCH_CHECK(num_decode == 0 || (d_bt.has_value() && d_ctx.has_value()), "decode rows need block tables");
+    TORCH_CHECK(num_prefill == 0 || (p_bt.has_value() && q_start.has_value() && q_len.has_value() &&
+                                     ctx_len.has_value() && tiles.has_value()), "prefill rows need metadata");
+    return forward_impl(ids, pos, slots, num_decode, get(d_bt), get(d_ctx), nsplit, bps, ws_t, num_prefill,
+                        get(p_bt), get(q_start), get(q_len), get(ctx_len), get(tiles), rows);
+  }
+
+  int64_t hq() const { return hq_; }
+  int64_t head_dim() const { return d_; }
+  int64_t vocab() const { return vocab_; }
+  c10::intrusive_ptr<::c10d::ProcessGroup> pg() const { return pg_; }
+
+ private:
+  at::Tensor embed(const at::Tensor& ids) {
+    at::Tensor idl = ids.to(at::kLong);
+    if (!pg_) return at::embedding(embed_, idl);
+    const int64_t vpr = embed_.size(0);
+    at::Tensor local = idl - vocab_start_;
+    at::Tensor mask = (local < 0).logical_or(local >= vpr);
+    at::Tensor h = at::embedding(embed_, local.clamp(0, vpr - 1));
+    h.masked_fill_(mask.unsqueeze(1), 0);
+    all_reduce(h);
+    return h;
+  }
+
+  void all_reduce(at::Tensor& t) {
+    if (!pg_) return;
+    std::vector<at::Tensor> v{t};
+    pg_->allreduce(v)->wait();
+  }
+
+  at::Tensor embed_;
+  std::vector<at::Tensor> qkv_w_, o_w_, gate_up_w_, down_w_, in_norm_, post_norm_;
+  at::Tensor final_norm_, lm_head_;
+  std::vector<at::Tensor> kc_, vc_;
+  at::Tensor cos_sin_;
+  int64_t hq_, hkv_, d_;
+  double eps_, scale_;
+  int64_t vocab_, vocab_start_;
+  c10::intrusive_ptr<::c10d::ProcessGroup> pg_;
+};
+
+// ---------------------------------------------------------------------------- BERT
+class BertRunner {
+ public:
+  BertRunner(at::Tensor wte, at::Tensor wpe, at::Tensor wtt, at::Tensor emb_g, at::Tensor emb_b,
+             std::vector<std::vector<at::Tensor>> layers, int64_t heads, double eps, double scale, int64_t pooling,
+             bool normalize)
+      : wte_(wte), wpe_(wpe), wtt_(wtt), emb_g_(emb_g), emb_b_(emb_b), layers_(layers), heads_(heads), eps_(eps),
+        scale_(scale), pooling_(pooling), normalize_(normalize) {
+    for (auto& l : layers_) TORCH_CHECK(l.size() == 12, "bert layer needs 12 tensors");
+  }
+
+  at::Tensor forward(at::Tensor ids, at::Tensor pos, at::Tensor starts, at::Tensor lens, at::Tensor tiles,
+                     bool out_f32) {
+    const int64_t T = ids.size(0), H = wte_.size(1);
+    at::Tensor x = at::empty({T, H}, wte_.options());
+    embed_layernorm(x, ids, pos, c10::nullopt, wte_, wpe_, wtt_, emb_g_, emb_b_, eps_);
+    for (auto& l : layers_) {
+      // qkv_w, qkv_b, o_w, o_b, ln1_g, ln1_b, ff1_w, ff1_b, ff2_w, ff2_b, ln2_g, ln2_b
+      at::Tensor qkv = at::linear(x, l[0], l[1]);
+      at::Tensor a = at::empty({T, H}, x.options());
+      varlen_encoder_attention(a, qkv, starts, lens, tiles, heads_, heads_, scale_);
+      at::Tensor o = at::linear(a, l[2]);
+      at::Tensor x1 = at::empty_like(x);
+      layernorm(x1, o, l[3], x, l[4], l[5], eps_);
+      at::Tensor hdn = at::linear(x1, l[6]);
+      bias_gelu(hdn, l[7]);
+      at::Tensor o2 = at::linear(hdn, l[8]);
+      at::Tensor x2 = at::empty_like(x);
+      layernorm(x2, o2, l[9], x1, l[10], l[11], eps_);
+      x = x2;
+    }
+    at::Tensor out = at::empty({starts.size(0), H}, x.options().dtype(out_f32 ? at::kFloat : x.scalar_type()));
+    pool_embeddings(out, x, starts, lens, pooling_, normalize_);
+    return out;
+  }
+
+ private:
+  at::Tensor wte_, wpe_, wtt_, emb_g_, emb_b_;
+  std::vector<std::vector<at::Tensor>> layers_;
+  int64_t heads_;
+  double eps_, scale_;
+  int64_t pooling_;
+  bool normalize_;
+};
+
+// ---------------------------------------------------------------------------- step executor
+// Arena header (int32 words); must match langstream_amd/engine/arena.py.
+enum Hdr : int {
+  H_KIND = 0,     // 1 step, 3 stop, 4 capture bucket H_BUCKET
+  H_T = 1,        // tokens in the step
+  H_ND = 2,       // decode rows [0, nd)
+  H_NPS = 3,      // prefill sequences
+  H_NTILES = 4,   // prefill attention tiles
+  H_NROWS = 5,    // rows to sample
+  H_NGATHER = 6,  // decode rows whose input token is the previous step's sample
+  H_NDELTA = 7,   // logit deltas (penalties / bias / min-tokens)
+  H_NTOP = 8,     // top logprobs per row
+  H_BUCKET = 9,   // >0: decode-only step replayed from the bucket's graph
+  H_ROWS_ALL = 10 // 1: sample every row (rows == arange(T))
+};
+
+// ids[gdst[i]] = tok_prev[gsrc[i]] for i < hdr[H_NGATHER]; count read on the device.
+__global__ void gather_feedback_kernel(int32_t* __restrict__ ids, const int64_t* __restrict__ gdst,
+                                       const int64_t* __restrict__ gsrc, const int32_t* __restrict__ tok_prev,
+                                       const int32_t* __restrict__ hdr, int cap) {
+  const int n = min(hdr[H_NGATHER], cap);
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+    ids[gdst[i]] = tok_prev[gsrc[i]];
+}
+
+// logits[row, tok] += val for each (row, tok, val) triple, count read on the device.
+__global__ void logit_delta_kernel(float* __restrict__ logits, int64_t ld, int V, int nrows,
+                                   const int32_t* __restrict__ trip, const int32_t* __restrict__ hdr, int cap) {
+  const int n = min(hdr[H_NDELTA], cap);
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const int r = trip[3 * i], t = trip[3 * i + 1];
+    const float v = __int_as_float(trip[3 * i + 2]);
+    if (r >= 0 && r < nrows && t >= 0 && t < V) atomicAdd(&logits[(int64_t)r * ld + t], v);
+  }
+}
+
+constexpr int kMaxTop = 32;
+
+class StepExecutor {
+ public:
+  StepExecutor(std::shared_ptr<LlamaRunner> runner, std::map<std::string, int64_t> off, int64_t arena_bytes,
+               int64_t fixed_bytes, int64_t max_tokens, int64_t max_seqs, int64_t max_blocks, int64_t max_tiles,
+               int64_t max_deltas, int64_t nslots, int64_t nsplit, int64_t bps, bool use_graphs, int64_t device)
+      : r_(std::move(runner)), off_(std::move(off)), arena_bytes_(arena_bytes), fixed_bytes_(fixed_bytes),
+        maxT_(max_tokens), maxS_(max_seqs), maxB_(max_blocks), maxTiles_(max_tiles), maxD_(max_deltas),
+        nsplit_(nsplit), bps_(bps), use_graphs_(use_graphs) {
+    static const char* need[] = {"hdr", "ids", "pos", "slots", "dbt", "dctx", "pbt", "q_start", "q_len", "ctx_len",
+                                 "tiles", "rows", "gdst", "gsrc", "temp", "top_p", "top_k", "seeds", "steps",
+                                 "deltas"};
+    for (const char* k : need) TORCH_CHECK(off_.count(k), "arena layout lacks ", k);
+    auto dev = at::TensorOptions().device(at::kCUDA, device);
+    auto pin = at::TensorOptions().dtype(at::kByte).pinned_memory(true);
+    for (int64_t i = 0; i < nslots; ++i) {
+      host_.push_back(at::zeros({arena_bytes_}, pin));
+      out_.push_back(at::zeros({out_bytes()}, pin));
+      hipEvent_t a, b;
+      HIP_OK(hipEventCreateWithFlags(&a, hipEventDisableTiming));
+      HIP_OK(hipEventCreateWithFlags(&b, hipEventDisableTiming));
+      in_ev_.push_back(a);
+      out_ev_.push_back(b);
+      in_used_.push_back(false);
+    }
+    arena_ = at::zeros({arena_bytes_}, dev.dtype(at::kByte));
+    hdr_small_ = at::zeros({16}, at::TensorOptions().dtype(at::kInt).pinned_memory(true));
+    tok_ = at::zeros({maxS_}, dev.dtype(at::kInt));
+    lp_ = at::zeros({maxS_}, dev.dtype(at::kFloat));
+    ti_ = at::zeros({maxS_ * kMaxTop}, dev.dtype(at::kInt));
+    tl_ = at::zeros({maxS_ * kMaxTop}, dev.dtype(at::kFloat));
+    ws_ = at::empty({std::max<int64_t>(1, maxS_ * r_->hq() * nsplit_ * (r_->head_dim() + 2))},
+                    dev.dtype(at::kFloat));
+    pool_ = at::cuda::graph_pool_handle();
+  }
+
+  ~StepExecutor() {
+    for (auto e : in_ev_) (void)hipEventDestroy(e);
+    for (auto e : out_ev_) (void)hipEventDestroy(e);
+  }
+
+  int64_t out_bytes() const { return maxS_ * 8 + maxS_ * kMaxTop * 8; }
+  at::Tensor host_slot(int64_t i) { return host_.at(i); }
+  at::Tensor out_slot(int64_t i) { return out_.at(i); }
+  bool has_graph(int64_t B) const { return graphs_.count(B) > 0; }
+
+  // Block until the H2D copy that last read host slot i has finished (slot reusable).
+  void wait_in(int64_t i) {
+    if (in_used_.at(i)) HIP_OK(hipEventSynchronize(in_ev_[i]));
+  }
+  // Block until the results of the step that wrote out slot i are on the host.
+  void wait_out(int64_t i) { HIP_OK(hipEventSynchronize(out_ev_.at(i))); }
+
+  // Rank 0: run the step described by host slot `slot`; results land in out slot `oslot`.
+  void launch(int64_t slot, int64_t oslot) {
+    const int32_t* hdr = reinterpret_cast<const int32_t*>(host_.at(slot).data_ptr());
+    TORCH_CHECK(hdr[H_KIND] == 1, "launch expects a step header");
+    validate(hdr);
+    upload(slot);
+    run(hdr);
+    download(hdr, oslot);
+  }
+
+  // All ranks (rank 0 announces it to the workers): capture the decode graph for bucket B.
+  void capture(int64_t B) {
+    if (graphs_.count(B)) return;
+    if (r_->pg()) {
+      int32_t* hdr = reinterpret_cast<int32_t*>(hdr_small_.data_ptr());
+      for (int i = 0; i < 16; ++i) hdr[i] = 0;
+      hdr[H_KIND] = 4;
+      hdr[H_BUCKET] = (int32_t)B;
+      announce(hdr);
+    }
+    do_capture(B);
+  }
+
+  void shutdown() {
+    if (!r_->pg()) return;
+    int32_t* hdr = reinterpret_cast<int32_t*>(hdr_small_.data_ptr());
+    for (int i = 0; i < 16; ++i) hdr[i] = 0;
+    hdr[H_KIND] = 3;
+    announce(hdr);
+    HIP_OK(hipStreamSynchronize(stream()));
+  }
+
+  // Non-zero TP ranks: mirror rank 0's steps until told to stop.
+  void worker_loop() {
+    TORCH_CHECK(r_->pg(), "worker_loop needs a process group");
+    int32_t* hdr = reinterpret_cast<int32_t*>(hdr_small_.data_ptr());
+    while (true) {
+      broadcast_arena();
+      HIP_OK(hipMemcpyAsync(hdr, arena_.data_ptr(), 16 * sizeof(int32_t), hipMemcpyDeviceToHost, stream()));
+      HIP_OK(hipStreamSynchronize(stream()));
+      const int kind = hdr[H_KIND];
+      if (kind == 3) return;
+      if (kind == 4) {
+        do_capture(hdr[H_BUCKET]);
+      } else if (kind == 1) {
+        validate(hdr);
+        run(hdr);
+      } else {
+        TORCH_CHECK(false, "bad step kind ", kind);
+      }
+    }
+  }
+
+ private:
+  hipStream_t stream() const { return at::hip::getCurrentHIPStream().stream(); }
+
+  template <typename T>
+  at::Tensor view(const char* name, int64_t n, at::ScalarType st) {
+    return arena_.narrow(0, off_.at(name), n * (int64_t)sizeof(T)).view(st);
+  }
+
+  void validate(const int32_t* h) const {
+    TORCH_CHECK(h[H_T] >= 0 && h[H_T] <= maxT_, "step tokens out of range: ", h[H_T]);
+    TORCH_CHECK(h[H_ND] >= 0 && h[H_ND] <= h[H_T] && h[H_ND] <= maxS_, "decode rows out of range");
+    TORCH_CHECK(h[H_NPS] >= 0 && h[H_NPS] <= maxS_ && h[H_NTILES] >= 0 && h[H_NTILES] <= maxTiles_);
+    TORCH_CHECK(h[H_NROWS] >= 0 && h[H_NROWS] <= maxS_ && h[H_NGATHER] >= 0 && h[H_NGATHER] <= maxS_);
+    TORCH_CHECK(h[H_NDELTA] >= 0 && h[H_NDELTA] <= maxD_ && h[H_NTOP] >= 0 && h[H_NTOP] <= kMaxTop);
+    TORCH_CHECK(h[H_BUCKET] >= 0 && h[H_BUCKET] <= maxS_);
+    if (h[H_BUCKET] > 0)
+      TORCH_CHECK(h[H_T] == h[H_ND] && h[H_ND] <= h[H_BUCKET] && h[H_NPS] == 0 && h[H_NTOP] == 0,
+                  "graph steps are decode-only");
+    TORCH_CHECK(h[H_NPS] == 0 || h[H_T] > h[H_ND], "prefill sequences without prefill tokens");
+  }
+
+  void upload(int64_t slot) {
+    const int32_t* hdr = reinterpret_cast<const int32_t*>(host_[slot].data_ptr());
+    const int64_t bytes = r_->pg() ? arena_bytes_ : fixed_bytes_ + 12 * (int64_t)hdr[H_NDELTA];
+    HIP_OK(hipMemcpyAsync(arena_.data_ptr(), host_[slot].data_ptr(), bytes, hipMemcpyHostToDevice, stream()));
+    HIP_OK(hipEventRecord(in_ev_[slot], stream()));
+    in_used_[slot] = true;
+    if (r_->pg()) broadcast_arena();
+  }
+
+  void announce(const int32_t* hdr) {
+    HIP_OK(hipMemcpyAsync(arena_.data_ptr(), hdr, 16 * sizeof(int32_t), hipMemcpyHostToDevice, stream()));
+    broadcast_arena();
+  }
+
+  void broadcast_arena() {
+    std::vector<at::Tensor> t{arena_};
+    c10d::BroadcastOptions o;
+    o.rootRank = 0;
+    r_->pg()->broadcast(t, o)->wait();
+  }
+
+  // The step body shared by eager launches and graph capture.
+  void body(int64_t T, int64_t nd, int64_t nps, int64_t ntiles, int64_t nrows, bool rows_all, int64_t ntop) {
+    const int32_t* dh = reinterpret_cast<const int32_t*>(arena_.data_ptr());
+    at::Tensor ids = view<int32_t>("ids", T, at::kInt);
+    gather_feedback_kernel<<<(int)std::max<int64_t>(1, (maxS_ + 255) / 256), 256, 0, stream()>>>(
+        ids.data_ptr<int32_t>(), reinterpret_cast<const int64_t*>((char*)arena_.data_ptr() + off_.at("gdst")),
+        reinterpret_cast<const int64_t*>((char*)arena_.data_ptr() + off_.at("gsrc")), tok_.data_ptr<int32_t>(), dh,
+        (int)maxS_);
+    at::Tensor pos = view<int32_t>("pos", T, at::kInt);
+    at::Tensor slots = view<int64_t>("slots", T, at::kLong);
+    at::Tensor dbt = view<int32_t>("dbt", std::max<int64_t>(nd, 1) * maxB_, at::kInt).view({-1, maxB_});
+    at::Tensor dctx = view<int32_t>("dctx", std::max<int64_t>(nd, 1), at::kInt);
+    at::Tensor pbt = view<int32_t>("pbt", std::max<int64_t>(nps, 1) * maxB_, at::kInt).view({-1, maxB_});
+    at::Tensor qs = view<int32_t>("q_start", std::max<int64_t>(nps, 1), at::kInt);
+    at::Tensor ql = view<int32_t>("q_len", std::max<int64_t>(nps, 1), at::kInt);
+    at::Tensor cl = view<int32_t>("ctx_len", std::max<int64_t>(nps, 1), at::kInt);
+    at::Tensor tiles = view<int32_t>("tiles", std::max<int64_t>(ntiles, 1) * 2, at::kInt).view({-1, 2});
+    c10::optional<at::Tensor> rows;
+    if (!rows_all) rows = view<int64_t>("rows", nrows, at::kLong);
+    at::Tensor logits = r_->forward_impl(ids, pos, slots, nd, dbt, dctx, nsplit_, std::min(bps_, maxB_), ws_,
+                                         T - nd, pbt, qs, ql, cl, tiles, rows);
+    last_logits_ = logits;
+    if (nrows == 0) return;
+    const int V = (int)logits.size(1);
+    logit_delta_kernel<<<(int)std::max<int64_t>(1, std::min<int64_t>((maxD_ + 255) / 256, 1024)), 256, 0,
+                         stream()>>>(logits.data_ptr<float>(), logits.stride(0), V, (int)logits.size(0),
+                                     reinterpret_cast<const int32_t*>((char*)arena_.data_ptr() + off_.at("deltas")),
+                                     dh, (int)maxD_);
+    at::Tensor lg = logits.narrow(0, 0, nrows);
+    sample_tokens(lg, view<float>("temp", nrows, at::kFloat), view<int32_t>("top_k", nrows, at::kInt),
+                  view<float>("top_p", nrows, at::kFloat), view<int64_t>("seeds", nrows, at::kLong),
+                  view<int64_t>("steps", nrows, at::kLong), tok_, lp_, ti_, tl_, ntop);
+  }
+
+  void run(const int32_t* h) {
+    const int64_t B = h[H_BUCKET];
+    if (B > 0) {
+      auto it = graphs_.find(B);
+      TORCH_CHECK(it != graphs_.end(), "decode graph for bucket ", B, " was not captured");
+      if (it->second) {
+        it->second->replay();
+        return;
+      }
+    }
+    body(h[H_T], h[H_ND], h[H_NPS], h[H_NTILES], h[H_NROWS], h[H_ROWS_ALL] != 0, h[H_NTOP]);
+  }
+
+  void download(const int32_t* h, int64_t oslot) {
+    const int64_t n = h[H_NROWS], ntop = h[H_NTOP];
+    char* o = (char*)out_.at(oslot).data_ptr();
+    if (n > 0) {
+      HIP_OK(hipMemcpyAsync(o, tok_.data_ptr(), n * 4, hipMemcpyDeviceToHost, stream()));
+      HIP_OK(hipMemcpyAsync(o + maxS_ * 4, lp_.data_ptr(), n * 4, hipMemcpyDeviceToHost, stream()));
+      if (ntop > 0) {
+        HIP_OK(hipMemcpyAsync(o + maxS_ * 8, ti_.data_ptr(), n * ntop * 4, hipMemcpyDeviceToHost, stream()));
+        HIP_OK(hipMemcpyAsync(o + maxS_ * 8 + maxS_ * kMaxTop * 4, tl_.data_ptr(), n * ntop * 4,
+                              hipMemcpyDeviceToHost, stream()));
+      }
+    }
+    HIP_OK(hipEventRecord(out_ev_[oslot], stream()));
+  }
+
+  // Neutral inputs for graph warm-up: no KV writes (slot -1), empty contexts, no feedback.
+  void neutralise(int64_t B) {
+    char* base = (char*)arena_.data_ptr();
+    hipStream_t s = stream();
+    HIP_OK(hipMemsetAsync(base + off_.at("hdr"), 0, 16 * 4, s));
+    HIP_OK(hipMemsetAsync(base + off_.at("ids"), 0, B * 4, s));
+    HIP_OK(hipMemsetAsync(base + off_.at("pos"), 0, B * 4, s));
+    HIP_OK(hipMemsetAsync(base + off_.at("slots"), 0xFF, B * 8, s));
+    HIP_OK(hipMemsetAsync(base + off_.at("dbt"), 0, B * maxB_ * 4, s));
+    HIP_OK(hipMemsetAsync(base + off_.at("dctx"), 0, B * 4, s));
+    HIP_OK(hipMemsetAsync(base + off_.at("temp"), 0, B * 4, s));
+    HIP_OK(hipMemsetAsync(base + off_.at("top_k"), 0, B * 4, s));
+    HIP_OK(hipMemsetAsync(base + off_.at("seeds"), 0, B * 8, s));
+    HIP_OK(hipMemsetAsync(base + off_.at("steps"), 0, B * 8, s));
+    std::vector<float> ones(B, 1.0f);
+    HIP_OK(hipMemcpy(base + off_.at("top_p"), ones.data(), B * 4, hipMemcpyHostToDevice));
+  }
+
+  void do_capture(int64_t B) {
+    TORCH_CHECK(B > 0 && B <= maxS_, "bad graph bucket ", B);
+    if (graphs_.count(B)) return;
+    if (!use_graphs_) {
+      graphs_.emplace(B, nullptr);
+      return;
+    }
+    auto cur = at::hip::getCurrentHIPStreamMasqueradingAsCUDA();
+    neutralise(B);
+    HIP_OK(hipStreamSynchronize(cur.stream()));
+    auto side = at::hip::getStreamFromPoolMasqueradingAsCUDA();
+    auto g = std::make_unique<at::cuda::CUDAGraph>();
+    {
+      at::hip::HIPStreamGuardMasqueradingAsCUDA guard(side);
+      for (int i = 0; i < 2; ++i) body(B, B, 0, 0, B, true, 0);  // allocator + hipBLASLt warm-up
+      HIP_OK(hipStreamSynchronize(side.stream()));
+      g->capture_begin(pool_);
+      body(B, B, 0, 0, B, true, 0);
+      g->capture_end();
+    }
+    HIP_OK(hipStreamSynchronize(side.stream()));
+    graph_logits_[B] = last_logits_;
+    graphs_.emplace(B, std::move(g));
+  }
+
+  std::shared_ptr<LlamaRunner> r_;
+  std::map<std::string, int64_t> off_;
+  int64_t arena_bytes_, fixed_bytes_, maxT_, maxS_, maxB_, maxTiles_, maxD_, nsplit_, bps_;
+  bool use_graphs_;
+  std::vector<at::Tensor> host_, out_;
+  std::vector<hipEvent_t> in_ev_, out_ev_;
+  std::vector<bool> in_used_;
+  at::Tensor arena_, hdr_small_, tok_, lp_, ti_, tl_, ws_, last_logits_;
+  std::map<int64_t, std::unique_ptr<at::cuda::CUDAGraph>> graphs_;
+  std::map<int64_t, at::Tensor> graph_logits_;
+  at::cuda::MempoolId_t pool_;
+};
+
+}  // namespace
+
+void bind_runners(py::module_& m) {
+  py::class_<LlamaRunner, std::shared_ptr<LlamaRunner>>(m, "LlamaRunner")
+      .def(py::init<at::Tensor, std::vector<at::Tensor>, std::vector<at::Tensor>, std::vector<at::Tensor>,
+                    std::vector<at::Tensor>, std::vector<at::Tensor>, std::vector<at::Tensor>, at::Tensor, at::Tensor,
+                    std::vector<at::Tensor>, std::vector<at::Tensor>, at::Tensor, int64_t, int64_t, int64_t, double,
+                    double, int64_t, int64_t, py::object>())
+      .def("forward", &LlamaRunner::forward, py::call_guard<py::gil_scoped_release>());
+  py::class_<BertRunner>(m, "BertRunner")
+      .def(py::init<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor, std::vector<std::vector<at::Tensor>>,
+                    int64_t, double, double, int64_t, bool>())
+      .def("forward", &BertRunner::forward, py::call_guard<py::gil_scoped_release>());
+  py::class_<StepExecutor>(m, "StepExecutor")
+      .def(py::init<std::shared_ptr<LlamaRunner>, std::map<std::string, int64_t>, int64_t, int64_t, int64_t,
+                    int64_t, int64_t, int64_t, int64_t, int64_t, int64_t, int64_t, bool, int64_t>())
+      .def("host_slot", &StepExecutor::host_slot)
+      .def("out_slot", &StepExecutor::out_slot)
+      .def("has_graph", &StepExecutor::has_graph)
+      .def("wait_in", &StepExecutor::wait_in, py::call_guard<py::gil_scoped_release>())
+      .def("wait_out", &StepExecutor::wait_out, py::call_guard<py::gil_scoped_release>())
+      .def("launch", &StepExecutor::launch, py::call_guard<py::gil_scoped_release>())
+      .def("capture", &StepExecutor::capture, py::call_guard<py::gil_scoped_release>())
+      .def("shutdown", &StepExecutor::shutdown, py::call_guard<py::gil_scoped_release>())
+      .def("worker_loop", &StepExecutor::worker_loop, py::call_guard<py::gil_scoped_release>());
+}

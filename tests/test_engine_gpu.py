@@ -22,24 +22,77 @@ def _cpu_copy(model: LlamaModel) -> LlamaModel:
     return cpu
 
 
+def _first_token_tops(e: LLMEngine, prompts, n_top=20):
+    """First sampled token of each prompt with its top-n (id, logprob) alternatives."""
+    events = {}
+    reqs = [e.submit(p, SamplingParams(max_tokens=1, temperature=0.0, ignore_eos=True, logprobs=n_top),
+                     callback=lambda ev, i=i: events.setdefault(i, ev)) for i, p in enumerate(prompts)]
+    while not all(r.finished for r in reqs):
+        e.step()
+    e._flush()
+    return [events[i] for i in range(len(prompts))]
+
+
 def test_llama_prefill_logits_match_cpu():
     cfg = PRESETS["llama-small"]
     gpu = LlamaModel(cfg, device="cuda")
     cpu = _cpu_copy(gpu)
     prompts = [list(range(5, 5 + n)) for n in (7, 70, 130)]
-    e_g = LLMEngine(gpu, None, num_blocks=64, max_model_len=1024, use_graphs=False)
-    e_c = LLMEngine(cpu, None, num_blocks=64, max_model_len=1024)
-    logits = []
-    for e in (e_g, e_c):
-        reqs = [e.submit(p, SamplingParams(max_tokens=1, temperature=0.0, ignore_eos=True)) for p in prompts]
-        e._drain_inbox()
-        batch = e._schedule_prefill()
-        captured = {}
-        orig = e._sample_and_emit
-        e._sample_and_emit = lambda lg, rs, c=captured, o=orig: (c.setdefault("lg", lg.clone()), o(lg, rs))
-        e._run_prefill(batch)
-        logits.append(captured["lg"])
-    assert _cos(logits[0], logits[1]) > 0.995
+    eg = _first_token_tops(LLMEngine(gpu, None, num_blocks=64, max_model_len=1024), prompts)
+    ec = _first_token_tops(LLMEngine(cpu, None, num_blocks=64, max_model_len=1024), prompts)
+    for g, c in zip(eg, ec):
+        cmap = dict(c.top)
+        # bf16 vs fp32: the GPU's argmax is (near-)argmax on the CPU, same max log-prob
+        assert g.token_id in cmap and cmap[g.token_id] >= c.top[0][1] - 0.05
+        assert abs(g.top[0][1] - c.top[0][1]) < 0.05
+        assert len(set(t for t, _ in g.top) & set(cmap)) >= 10
+
+
+def test_native_runner_matches_python_forward():
+    """The C++ LlamaRunner and the Python op-by-op forward issue the same kernels:
+    logits must agree to bf16 rounding on a two-sequence prefill."""
+    cfg = PRESETS["llama-small"]
+    model = LlamaModel(cfg, device="cuda")
+    kv = [(torch.zeros(16, model.hkv, 64, cfg.head_dim, device="cuda", dtype=model.dtype),
+           torch.zeros(16, model.hkv, cfg.head_dim, 64, device="cuda", dtype=model.dtype))
+          for _ in range(cfg.num_layers)]
+    lens = [70, 100]
+    T = sum(lens)
+    ids = torch.randint(5, 1000, (T,), dtype=torch.int32, device="cuda")
+    pos = torch.cat([torch.arange(n, dtype=torch.int32) for n in lens]).cuda()
+    bt = torch.tensor([[0, 1, 0, 0], [2, 3, 0, 0]], dtype=torch.int32, device="cuda")
+    slots = torch.cat([bt[s].long()[torch.arange(n) // 64].cpu() * 64 + torch.arange(n) % 64
+                       for s, n in enumerate(lens)]).cuda()
+    G = model.hq // model.hkv
+    meta = AttnMeta(positions=pos, slots=slots, num_decode=0, num_prefill_tokens=T, p_block_tables=bt,
+                    q_start=torch.tensor([0, 70], dtype=torch.int32, device="cuda"),
+                    q_len=torch.tensor(lens, dtype=torch.int32, device="cuda"),
+                    ctx_len=torch.tensor(lens, dtype=torch.int32, device="cuda"),
+                    tiles=ops.prefill_tiles(lens, G).cuda())
+    rows = torch.tensor([69, 169], dtype=torch.long, device="cuda")
+    a = model.forward_logits(ids, meta, kv, rows).float().cpu()
+    b = model.logits(model.forward(ids, meta, kv).index_select(0, rows)).float().cpu()
+    for i in range(2):
+        assert _cos(a[i], b[i]) > 0.999
+
+
+def test_native_executor_matches_python_executor():
+    """Whole-step native executor (arena upload, feedback gather, graphs, sampling)
+    against the Python executor driving the same model on the same GPU."""
+    from langstream_amd.engine.arena import PyStepExecutor
+    from langstream_amd.engine.llm_engine import NSLOTS
+    cfg = PRESETS["llama-small"]
+    model = LlamaModel(cfg, device="cuda")
+    prompts = [list(range(3, 3 + n)) for n in (5, 33, 64, 65, 200)]
+    sp = SamplingParams(max_tokens=10, temperature=0.0, ignore_eos=True)
+    e1 = LLMEngine(model, None, num_blocks=128, max_model_len=1024, max_batch=8)
+    out1 = [r.output_ids for r in e1.generate(prompts, sp)]
+    assert e1.stats["graph_steps"] > 0
+    e2 = LLMEngine(model, None, num_blocks=128, max_model_len=1024, max_batch=8, use_graphs=False)
+    e2.exec = PyStepExecutor(model, e2.kv_caches, e2.layout, NSLOTS, e2.nsplit, e2.bps, e2.device)
+    out2 = [r.output_ids for r in e2.generate(prompts, sp)]
+    for a, b in zip(out1, out2):
+        assert a[:4] == b[:4]
 
 
 def test_llama_graph_decode_matches_eager():
