@@ -226,6 +226,8 @@ def main():
     for _ in range(args.warmup):
         run_step(args.batch)
     barrier()
+    from langstream_amd.utils import threads as _threads
+    cpu0 = _threads.snapshot()
     t0 = time.time()
     all_lats = []
     for _ in range(args.steps):
@@ -233,6 +235,8 @@ def main():
         all_lats.extend(lats)
     barrier()
     elapsed = time.time() - t0
+    if os.environ.get("LANGSTREAM_THREAD_CPU"):
+        print(json.dumps({"thread_cpu_s": _threads.diff(cpu0, _threads.snapshot())}), file=sys.stderr, flush=True)
     p50 = statistics.median(all_lats) if all_lats else 0.0
     if world > 1:
         t = torch.tensor([elapsed, p50], dtype=torch.float64, device=device if use_gpu else "cpu")

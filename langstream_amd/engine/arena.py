@@ -122,6 +122,8 @@ class PyStepExecutor:
         self._av = layout.views(self._arena)
         self._tok = np.zeros(layout.max_seqs, np.int32)
         self._graphs = set()
+        self._ws = torch.empty(max(1, layout.max_seqs * model.hq * nsplit * (model.cfg.head_dim + 2)),
+                               dtype=torch.float32, device=device)
 
     def wait_in(self, i: int) -> None:
         pass
@@ -184,7 +186,7 @@ class PyStepExecutor:
         tt = lambda x: torch.from_numpy(np.ascontiguousarray(x)).to(dev)  # noqa: E731
         meta = AttnMeta(positions=tt(a["pos"][:T]), slots=tt(a["slots"][:T]), num_decode=nd,
                         d_block_tables=tt(a["dbt"][:nd]) if nd else None, d_ctx_lens=tt(a["dctx"][:nd]) if nd else None,
-                        nsplit=self.nsplit, blocks_per_split=self.bps, num_prefill_tokens=T - nd,
+                        nsplit=self.nsplit, blocks_per_split=self.bps, workspace=self._ws, num_prefill_tokens=T - nd,
                         p_block_tables=tt(a["pbt"][:nps]) if nps else None,
                         q_start=tt(a["q_start"][:nps]) if nps else None, q_len=tt(a["q_len"][:nps]) if nps else None,
                         ctx_len=tt(a["ctx_len"][:nps]) if nps else None,
