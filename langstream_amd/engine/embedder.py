@@ -18,6 +18,7 @@ from typing import List, Optional, Sequence
 import torch
 
 from ..models.bert import BertEncoder
+from ..utils.gpu import on_aux, to_host
 
 log = logging.getLogger(__name__)
 
@@ -46,8 +47,11 @@ class EmbeddingEngine:
         return out.tolist() if isinstance(out, torch.Tensor) else out
 
     def embed_tensor(self, texts: Sequence[str]) -> torch.Tensor:
+        """Device tensor, produced on the device's auxiliary stream (consume it there,
+        e.g. VectorStore.upsert, or synchronise)."""
         toks = self.tok.encode_batch(list(texts), max_len=self.max_len)
-        return self.encoder.encode_tokens(toks)
+        with on_aux(self.encoder.device):
+            return self.encoder.encode_tokens(toks)
 
     def _embed_batch(self, texts: List[str]):
         res = []
@@ -60,8 +64,9 @@ class EmbeddingEngine:
                     break
                 toks.append(t)
                 ntok += len(t)
-            emb = self.encoder.encode_tokens(toks)
-            res.append(emb.cpu())
+            with on_aux(self.encoder.device):  # do not queue behind the LLM engine's steps
+                emb = self.encoder.encode_tokens(toks)
+                res.append(to_host(emb)[0])
             self.stats["batches"] += 1
             self.stats["texts"] += len(toks)
             self.stats["tokens"] += ntok

@@ -212,7 +212,7 @@ class LLMEngine:
         self._step_id = 0
         self.stats = {"prefill_steps": 0, "decode_steps": 0, "mixed_steps": 0, "prefill_tokens": 0,
                       "decode_tokens": 0, "preemptions": 0, "requests": 0, "finished": 0, "graph_steps": 0,
-                      "host_ms": 0.0, "wait_ms": 0.0}
+                      "host_ms": 0.0, "wait_ms": 0.0, "launch_ms": 0.0, "retire_ms": 0.0}
         self.buckets = sorted(set(graph_buckets or [b for b in (1, 2, 4, 8, 16, 24, 32, 48, 64, 96, 128, 160, 192,
                                                                  224, 256, 320, 384, 448, 512) if b <= max_batch]
                                   + [max_batch]))
@@ -345,7 +345,9 @@ class LLMEngine:
         prev, self._inflight = self._inflight, launched
         self.stats["host_ms"] += (time.perf_counter() - t0) * 1000
         if prev is not None:
+            t1 = time.perf_counter()
             self._retire(prev)
+            self.stats["retire_ms"] += (time.perf_counter() - t1) * 1000
         if not self.lookahead:
             self._flush()
 
@@ -552,7 +554,9 @@ class LLMEngine:
             r.pending_row = j
             r.pending_step = self._step_id
         # ---- run
+        t0 = time.perf_counter()
         self.exec.launch(slot, slot)
+        self.stats["launch_ms"] += (time.perf_counter() - t0) * 1000
         if B:
             self.stats["decode_steps"] += 1
             self.stats["graph_steps"] += 1

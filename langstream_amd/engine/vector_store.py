@@ -18,6 +18,7 @@ from typing import Any, Dict, List, Optional, Sequence
 import torch
 
 from .. import ops
+from ..utils.gpu import on_aux, to_host
 
 
 class VectorStore:
@@ -26,7 +27,8 @@ class VectorStore:
         self.name = name
         self.device = torch.device(device)
         self.dtype = dtype
-        self._vecs = torch.zeros(max(16, capacity), dim, device=self.device, dtype=dtype)
+        with on_aux(self.device):  # every GPU op of the store runs on the auxiliary stream
+            self._vecs = torch.zeros(max(16, capacity), dim, device=self.device, dtype=dtype)
         self._n = 0
         self._ids: List[Any] = []
         self._meta: List[Dict[str, Any]] = []
@@ -56,6 +58,10 @@ class VectorStore:
         return torch.nn.functional.normalize(t, dim=-1, eps=1e-12).to(self.dtype)
 
     def upsert(self, ids: Sequence[Any], vectors, metadata: Optional[Sequence[Dict[str, Any]]] = None) -> None:
+        with on_aux(self.device):
+            self._upsert(ids, vectors, metadata)
+
+    def _upsert(self, ids, vectors, metadata) -> None:
         vecs = self._normalize(vectors)
         with self._lock:
             metadata = metadata or [{} for _ in ids]
@@ -76,6 +82,10 @@ class VectorStore:
             self._vecs[torch.tensor(rows, device=self.device, dtype=torch.long)] = vecs
 
     def delete(self, ids: Sequence[Any]) -> int:
+        with on_aux(self.device):
+            return self._delete(ids)
+
+    def _delete(self, ids: Sequence[Any]) -> int:
         removed = 0
         with self._lock:
             for k in ids:
@@ -102,11 +112,18 @@ class VectorStore:
     def vector(self, key: Any) -> Optional[List[float]]:
         with self._lock:
             r = self._row.get(key)
-            return None if r is None else self._vecs[r].float().cpu().tolist()
+            if r is None:
+                return None
+            with on_aux(self.device):
+                return to_host(self._vecs[r].float())[0].tolist()
 
     def search(self, queries, k: int = 10, with_vectors: bool = False) -> List[List[Dict[str, Any]]]:
         """queries: [Q, dim] (list or tensor).  Returns per query a list of
         {"id", "similarity", **metadata} sorted by decreasing cosine similarity."""
+        with on_aux(self.device):
+            return self._search(queries, k, with_vectors)
+
+    def _search(self, queries, k: int, with_vectors: bool) -> List[List[Dict[str, Any]]]:
         q = self._normalize(queries)
         with self._lock:
             n = self._n
@@ -114,12 +131,12 @@ class VectorStore:
                 return [[] for _ in range(q.shape[0])]
             kk = max(1, min(k, 64, n))
             s, idx = ops.knn_topk(self._vecs[:n], q.contiguous(), kk)
-            s, idx = s.cpu().tolist(), idx.cpu().tolist()
+            s, idx = (t.tolist() for t in to_host(s, idx))
             vec_rows = None
             if with_vectors:
                 flat = sorted({i for row in idx for i in row if i >= 0})
                 if flat:
-                    vv = self._vecs[torch.tensor(flat, device=self.device)].float().cpu().tolist()
+                    vv = to_host(self._vecs[torch.tensor(flat, device=self.device)].float())[0].tolist()
                     vec_rows = dict(zip(flat, vv))
             out = []
             for qi in range(len(idx)):

@@ -84,6 +84,8 @@ class BertEncoder:
             self.emb_b = torch.zeros(H, device=self.device, dtype=dtype)
             self.layers = [BertLayer(cfg, self.device, dtype) for _ in range(cfg.num_layers)]
         self.scale = 1.0 / math.sqrt(cfg.head_dim)
+        if self.device.type == "cuda":  # weights are read from the auxiliary stream
+            torch.cuda.current_stream(self.device).synchronize()
 
     def state_dict(self) -> dict:
         sd = {"wte": self.wte, "wpe": self.wpe, "wtt": self.wtt, "emb_g": self.emb_g, "emb_b": self.emb_b}

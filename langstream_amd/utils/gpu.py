@@ -1,0 +1,61 @@
+"""GPU helpers shared by the auxiliary (non-LLM) GPU services.
+
+The LLM engine keeps the default HIP stream of its device busy with back-to-back
+steps (lookahead keeps two queued).  Latency-sensitive side work -- query embeddings,
+vector-store kNN, upserts -- must not queue behind those steps, so it runs on ONE
+high-priority auxiliary stream per device and overlaps the LLM's kernels on the
+remaining CUs.  Results come back through pinned buffers and a *blocking* event, so
+the waiting thread sleeps instead of spinning a core.
+"""
+from __future__ import annotations
+
+import contextlib
+import threading
+from typing import Dict, List, Optional
+
+import torch
+
+_lock = threading.Lock()
+_aux: Dict[int, "torch.cuda.Stream"] = {}
+
+
+def aux_stream(device) -> Optional["torch.cuda.Stream"]:
+    device = torch.device(device)
+    if device.type != "cuda":
+        return None
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    with _lock:
+        s = _aux.get(idx)
+        if s is None:
+            lo, hi = torch.cuda.Stream.priority_range()
+            s = torch.cuda.Stream(device=idx, priority=min(lo, hi))
+            # everything enqueued on the device so far (weights, setup) happens-before
+            s.wait_stream(torch.cuda.current_stream(idx))
+            _aux[idx] = s
+    return s
+
+
+@contextlib.contextmanager
+def on_aux(device):
+    s = aux_stream(device)
+    if s is None:
+        yield None
+        return
+    with torch.cuda.stream(s):
+        yield s
+
+
+def to_host(*tensors: torch.Tensor) -> List[torch.Tensor]:
+    """D2H copies of the given device tensors (enqueued on the current stream) into
+    pinned buffers; waits with a blocking event.  CPU tensors pass through."""
+    if not tensors or not tensors[0].is_cuda:
+        return list(tensors)
+    outs = []
+    for t in tensors:
+        h = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+        h.copy_(t, non_blocking=True)
+        outs.append(h)
+    ev = torch.cuda.Event(blocking=True)
+    ev.record()
+    ev.synchronize()
+    return outs
