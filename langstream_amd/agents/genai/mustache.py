@@ -18,8 +18,11 @@ _TAG = re.compile(r"\{\{\{\s*(.+?)\s*\}\}\}|\{\{\s*([#^/&!]?)\s*(.*?)\s*\}\}", r
 _ESC = {"&": "&amp;", "'": "&#39;", '"': "&quot;", "<": "&lt;", ">": "&gt;", "`": "&#x60;", "=": "&#x3D;"}
 
 
+_ESC_TABLE = str.maketrans(_ESC)
+
+
 def _escape(s: str) -> str:
-    return "".join(_ESC.get(c, c) for c in s)
+    return s.translate(_ESC_TABLE)
 
 
 def _to_str(v: Any) -> str:

@@ -33,8 +33,15 @@ def attempt_json(v: Any) -> Any:
 
 
 def safe_clone(v: Any) -> Any:
-    if isinstance(v, (dict, list)):
-        return copy.deepcopy(v)
+    """Copy the top level of a map/list value.  Enough for isolation: every mutation a
+    step performs replaces a top-level entry (``set_result_field`` writes flat keys,
+    drop-fields / merge / flatten / cast build new containers), so nested objects --
+    e.g. retrieved documents with 384-float vectors -- are shared, never written.
+    A deep copy per step dominated the per-record host cost of the RAG pipeline."""
+    if isinstance(v, dict):
+        return dict(v)
+    if isinstance(v, list):
+        return list(v)
     return v
 
 

@@ -259,10 +259,11 @@ class ComputeAIEmbeddingsStep(Step):
                 def done(f):
                     try:
                         embs = f.result()
-                        for it, e in zip(items, embs):
-                            if isinstance(it, dict):
-                                it[self.field.split(".")[-1] if self.field.startswith("record.") else self.field] = e
-                        rec.set_result_field(items, self.loop_over)
+                        key = self.field.split(".")[-1] if self.field.startswith("record.") else self.field
+                        # new item maps: nested objects are shared with the source record
+                        new_items = [dict(it, **{key: e}) if isinstance(it, dict) else it
+                                     for it, e in zip(items, embs)]
+                        rec.set_result_field(new_items, self.loop_over)
                         fut.set_result(None)
                     except BaseException as ex:  # noqa: BLE001
                         fut.set_exception(ex)

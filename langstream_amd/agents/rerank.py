@@ -131,7 +131,7 @@ class ReRankAgent(SingleRecordAgentProcessor):
         self.b = float(configuration.get("b", 0.75))
 
     def process_record(self, record):
-        mr = MutableRecord.from_record(record).copy()
+        mr = MutableRecord.from_record(record)
         ctx = mr.el_context()
         docs = eval_expression(self.field, ctx) or []
         query = eval_expression(self.query_field, ctx) if self.query_field else None

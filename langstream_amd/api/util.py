@@ -307,7 +307,10 @@ class MicroBatcher(Generic[T]):
 
     def _run(self) -> None:
         import queue as _q
+        from ..utils.profiling import ThreadProfiler
+        prof = ThreadProfiler(self._thread.name)
         while True:
+            prof.tick()
             first = self._q.get()
             batch = [first]
             while len(batch) < self.max_batch:

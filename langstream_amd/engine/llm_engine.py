@@ -289,23 +289,13 @@ class LLMEngine:
         sys.setswitchinterval(min(sys.getswitchinterval(), 0.001))
         if self.is_gpu:
             torch.cuda.set_device(self.device)
-        prof_path = os.environ.get("LANGSTREAM_PROFILE_ENGINE")
-        if prof_path:
-            import cProfile
-            import pstats
-            pr = cProfile.Profile()
-            pr.enable()
-            try:
-                self._loop_body()
-            finally:
-                pr.disable()
-                with open(prof_path, "w") as f:
-                    pstats.Stats(pr, stream=f).sort_stats("cumulative").print_stats(60)
-            return
         self._loop_body()
 
     def _loop_body(self) -> None:
+        from ..utils.profiling import ThreadProfiler
+        prof = ThreadProfiler("llm-engine")
         while not self._stop.is_set():
+            prof.tick()
             if not self.has_work():
                 self._wake.wait(0.05)
                 self._wake.clear()
