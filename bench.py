@@ -255,7 +255,8 @@ def main():
                        "seq_len": 4096, "max_new_tokens": args.max_tokens, "corpus_docs_per_gpu": args.corpus,
                        "top_k": 20, "rerank": 5, "parallelism": f"dp{world}"},
             "setup_s": round(setup_s, 1),
-            "engine": {k: v for k, v in llm.stats.items()},
+            "engine": dict(llm.stats, exec_ms=dict(zip(("upload", "enqueue", "download", "wait"),
+                                                       (round(x, 1) for x in llm.exec.timings())))),
         }), flush=True)
     runner.stop(timeout=10)
     services.shutdown()

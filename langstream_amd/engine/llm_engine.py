@@ -148,6 +148,7 @@ class _InFlight:
     slot: int
     n_top: int
     step_id: int
+    ready: bool = False          # results already waited for (by the next exec.step)
 
 
 class LLMEngine:
@@ -444,8 +445,8 @@ class LLMEngine:
                 self._flush()  # capture reuses the token-feedback buffer
                 self.exec.capture(B)
         prev = self._inflight
+        # free: the previous exec.step() waited for this slot's last upload
         self._slot = slot = (self._slot + 1) % NSLOTS
-        self.exec.wait_in(slot)
         a = self.exec.inputs[slot]
         ids, pos, slots = a["ids"], a["pos"], a["slots"]
         # ---- decode rows: one token each, input = previous sample (host or on-device feedback)
@@ -545,7 +546,11 @@ class LLMEngine:
             r.pending_step = self._step_id
         # ---- run
         t0 = time.perf_counter()
-        self.exec.launch(slot, slot)
+        # one GIL-released call: launch this step, wait for the previous step's results,
+        # and for the next arena slot to be reusable
+        self.exec.step(slot, prev.slot if prev is not None else -1, (slot + 1) % NSLOTS)
+        if prev is not None:
+            prev.ready = True
         self.stats["launch_ms"] += (time.perf_counter() - t0) * 1000
         if B:
             self.stats["decode_steps"] += 1
@@ -586,9 +591,10 @@ class LLMEngine:
 
     # ------------------------------------------------------------------ retire
     def _retire(self, st: _InFlight) -> None:
-        t0 = time.perf_counter()
-        self.exec.wait_out(st.slot)
-        self.stats["wait_ms"] += (time.perf_counter() - t0) * 1000
+        if not st.ready:
+            t0 = time.perf_counter()
+            self.exec.wait_out(st.slot)
+            self.stats["wait_ms"] += (time.perf_counter() - t0) * 1000
         n = len(st.reqs)
         if n == 0:
             return

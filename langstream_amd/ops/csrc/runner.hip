@@ -30,6 +30,7 @@
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 #include <torch/csrc/distributed/c10d/ProcessGroup.hpp>
 
+#include <chrono>
 #include <map>
 #include <memory>
 #include <string>
@@ -269,6 +270,7 @@ __global__ void logit_delta_kernel(float* __restrict__ logits, int64_t ld, int V
 }
 
 constexpr int kMaxTop = 32;
+using clk = std::chrono::steady_clock;
 
 class StepExecutor {
  public:
@@ -322,14 +324,36 @@ class StepExecutor {
   // Block until the results of the step that wrote out slot i are on the host.
   void wait_out(int64_t i) { HIP_OK(hipEventSynchronize(out_ev_.at(i))); }
 
+  // One scheduler round trip in a single GIL-released call: launch the step in host
+  // slot `slot` (results -> out slot `slot`), then block until the previous step's
+  // results (out slot `prev`, -1: none) are on the host, then until host slot `next`
+  // is free for the scheduler to fill.
+  void step(int64_t slot, int64_t prev, int64_t next) {
+    launch(slot, slot);
+    auto t0 = clk::now();
+    if (prev >= 0) wait_out(prev);
+    auto t1 = clk::now();
+    if (next >= 0) wait_in(next);
+    t_wait_ += std::chrono::duration<double, std::milli>(t1 - t0).count();
+  }
+
+  // {upload, run (enqueue forward/graph), download, wait} milliseconds, cumulative.
+  std::vector<double> timings() const { return {t_up_, t_run_, t_down_, t_wait_}; }
+
   // Rank 0: run the step described by host slot `slot`; results land in out slot `oslot`.
   void launch(int64_t slot, int64_t oslot) {
     const int32_t* hdr = reinterpret_cast<const int32_t*>(host_.at(slot).data_ptr());
     TORCH_CHECK(hdr[H_KIND] == 1, "launch expects a step header");
     validate(hdr);
+    auto t0 = clk::now();
     upload(slot);
+    auto t1 = clk::now();
     run(hdr);
+    auto t2 = clk::now();
+    t_up_ += std::chrono::duration<double, std::milli>(t1 - t0).count();
+    t_run_ += std::chrono::duration<double, std::milli>(t2 - t1).count();
     download(hdr, oslot);
+    t_down_ += std::chrono::duration<double, std::milli>(clk::now() - t2).count();
   }
 
   // All ranks (rank 0 announces it to the workers): capture the decode graph for bucket B.
@@ -533,6 +557,7 @@ class StepExecutor {
   std::map<int64_t, std::unique_ptr<at::cuda::CUDAGraph>> graphs_;
   std::map<int64_t, at::Tensor> graph_logits_;
   at::cuda::MempoolId_t pool_;
+  double t_up_ = 0, t_run_ = 0, t_down_ = 0, t_wait_ = 0;
 };
 
 }  // namespace
@@ -557,6 +582,8 @@ void bind_runners(py::module_& m) {
       .def("wait_in", &StepExecutor::wait_in, py::call_guard<py::gil_scoped_release>())
       .def("wait_out", &StepExecutor::wait_out, py::call_guard<py::gil_scoped_release>())
       .def("launch", &StepExecutor::launch, py::call_guard<py::gil_scoped_release>())
+      .def("step", &StepExecutor::step, py::call_guard<py::gil_scoped_release>())
+      .def("timings", &StepExecutor::timings)
       .def("capture", &StepExecutor::capture, py::call_guard<py::gil_scoped_release>())
       .def("shutdown", &StepExecutor::shutdown, py::call_guard<py::gil_scoped_release>())
       .def("worker_loop", &StepExecutor::worker_loop, py::call_guard<py::gil_scoped_release>());
