@@ -22,6 +22,7 @@
 #include <cstdint>
 #include <mutex>
 #include <queue>
+#include <set>
 #include <shared_mutex>
 #include <string>
 #include <thread>
@@ -184,32 +185,41 @@ class ByteBPE {
     } else {
       tiktoken_ = true;
     }
+    std::set<size_t> lens;
     for (auto& s : specials) {
       specials_[s.first] = s.second;
       if ((int)id2tok_.size() <= s.second) id2tok_.resize(s.second + 1);
       id2tok_[s.second] = s.first;
       special_ids_.insert(s.second);
+      if (!s.first.empty()) {
+        special_first_[(unsigned char)s.first[0]] = true;
+        lens.insert(s.first.size());
+      }
     }
+    special_lens_.assign(lens.rbegin(), lens.rend());  // longest match first
   }
 
+  // Special tokens are matched in one left-to-right scan: only positions whose byte can
+  // start a special are probed, with one hash lookup per distinct special length (Llama-3
+  // vocabularies carry ~250 reserved specials; synthetic ones >100k).
   std::vector<int> encode(const std::string& text, bool allow_special) {
     std::vector<int> out;
     if (allow_special && !specials_.empty()) {
-      size_t i = 0;
-      while (i < text.size()) {
-        size_t best = std::string::npos, blen = 0;
-        int bid = -1;
-        for (auto& kv : specials_) {
-          size_t p = text.find(kv.first, i);
-          if (p != std::string::npos && (p < best || (p == best && kv.first.size() > blen))) {
-            best = p; blen = kv.first.size(); bid = kv.second;
-          }
+      size_t start = 0;
+      for (size_t i = 0; i < text.size(); ++i) {
+        if (!special_first_[(unsigned char)text[i]]) continue;
+        for (size_t L : special_lens_) {
+          if (i + L > text.size()) continue;
+          auto it = specials_.find(text.substr(i, L));
+          if (it == specials_.end()) continue;
+          if (i > start) encode_ordinary(text.substr(start, i - start), out);
+          out.push_back(it->second);
+          start = i + L;
+          i = start - 1;
+          break;
         }
-        if (best == std::string::npos) { encode_ordinary(text.substr(i), out); break; }
-        encode_ordinary(text.substr(i, best - i), out);
-        out.push_back(bid);
-        i = best + blen;
       }
+      if (start < text.size()) encode_ordinary(text.substr(start), out);
     } else {
       encode_ordinary(text, out);
     }
@@ -319,6 +329,8 @@ class ByteBPE {
   std::unordered_map<std::pair<int, int>, std::pair<int, int>, PairHash> pair_rank_;
   std::unordered_map<std::string, int> specials_;
   std::unordered_set<int> special_ids_;
+  bool special_first_[256] = {};
+  std::vector<size_t> special_lens_;
   int byte_id_[256];
   bool tiktoken_ = true;
   std::unordered_map<std::string, std::vector<int>> cache_;
@@ -570,10 +582,11 @@ void bind_tokenizer(py::module_& m) {
   py::class_<ByteBPE>(m, "ByteBPE")
       .def(py::init<const std::vector<std::pair<py::bytes, int>>&, const std::vector<std::pair<py::bytes, py::bytes>>&,
                     const std::vector<std::pair<std::string, int>>&>())
-      .def("encode", &ByteBPE::encode, py::arg("text"), py::arg("allow_special") = true)
+      .def("encode", &ByteBPE::encode, py::arg("text"), py::arg("allow_special") = true,
+           py::call_guard<py::gil_scoped_release>())
       .def("encode_batch", &ByteBPE::encode_batch, py::arg("texts"), py::arg("allow_special") = true,
            py::arg("threads") = 4)
-      .def("count", &ByteBPE::count)
+      .def("count", &ByteBPE::count, py::call_guard<py::gil_scoped_release>())
       .def("decode_bytes", &ByteBPE::decode_bytes, py::arg("ids"), py::arg("skip_special") = false)
       .def("vocab_size", &ByteBPE::vocab_size)
       .def("token_to_id", &ByteBPE::token_to_id)
@@ -582,7 +595,7 @@ void bind_tokenizer(py::module_& m) {
       .def(py::init<const std::vector<std::string>&, bool, bool, const std::string&, int>(), py::arg("vocab"),
            py::arg("lower") = true, py::arg("strip_accents") = true, py::arg("unk") = "[UNK]",
            py::arg("max_chars") = 100)
-      .def("encode", &WordPiece::encode)
+      .def("encode", &WordPiece::encode, py::call_guard<py::gil_scoped_release>())
       .def("encode_batch", &WordPiece::encode_batch, py::arg("texts"), py::arg("threads") = 4)
       .def("basic_tokens", &WordPiece::basic_tokens)
       .def("decode", &WordPiece::decode)
