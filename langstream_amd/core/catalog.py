@@ -86,8 +86,8 @@ _SPECS = [
     AgentSpec(("http-request",), P, required=("url",)),
     AgentSpec(("langserve-invoke",), P, required=("url",)),
     AgentSpec(("webcrawler-source",), S, disk_fn=_webcrawler_disks),
-    AgentSpec(("s3-source",), S, required=("bucketName",)),
-    AgentSpec(("azure-blob-storage-source",), S, required=("container",)),
+    AgentSpec(("s3-source",), S),
+    AgentSpec(("azure-blob-storage-source",), S, required=("endpoint",)),
     AgentSpec(("camel-source",), S, required=("component-uri",)),
     AgentSpec(("python-source",), S, required=("className",)),
     AgentSpec(("python-processor", "python-function"), P, required=("className",)),
