@@ -1,0 +1,283 @@
+"""Gateway authentication providers (``API/gateway/*``).
+
+``authenticate(ctx) -> AuthResult(authenticated, reason, principal_values)``.
+
+* ``http``   (``HttpAuthenticationProvider.java``): GET ``base-url + path-template``
+  (``{tenant}`` substituted) with ``Authorization: Bearer <credentials>`` plus
+  configured ``headers``; success iff the status is in ``accepted-statuses``
+  (200, 201).  No principal values.
+* ``jwt``    (``JwtAuthenticationProvider.java``): HS256/384/512 with ``secret-key`` or
+  RS256/384/512 with ``public-key`` (PEM) or a JWKS fetched from the token's ``jku``
+  / ``jwks-uri`` (host must be in ``jwks-hosts-allowlist``); ``exp``/``nbf`` checked;
+  optional ``audience`` checked against ``audience-claim`` (aud); principal values are
+  the string claims, ``subject`` = ``auth-claim`` (sub).  RSA verification is done with
+  plain modular exponentiation (no crypto library is available offline).
+* ``github`` (``GitHubAuthenticationProvider.java``): GET https://api.github.com/user with
+  the token; principal values ``login``, ``id``, ``name``, ``email``.
+* ``google`` (``GoogleAuthenticationProvider.java``): Google ID token = RS256 JWT whose
+  ``aud`` must equal ``clientId``, verified against Google's JWKS; principal values
+  ``subject``, ``email``, ``name``, ``locale``.
+* test mode (``test-credentials`` + ``allow-test-mode``): principal values derived from
+  sha256(credentials) exactly like ``GatewayRequestHandler.getPrincipalValues``.
+"""
+from __future__ import annotations
+
+import base64
+import hashlib
+import hmac
+import json
+import time
+import urllib.parse
+from dataclasses import dataclass, field
+from typing import Any, Callable, Dict, List, Optional
+
+
+@dataclass
+class AuthResult:
+    authenticated: bool
+    reason: Optional[str] = None
+    principal_values: Dict[str, str] = field(default_factory=dict)
+
+
+def _cfg(c: Dict[str, Any], *names, default=None):
+    for n in names:
+        if c.get(n) is not None:
+            return c[n]
+    return default
+
+
+def _b64url(s: str) -> bytes:
+    return base64.urlsafe_b64decode(s + "=" * (-len(s) % 4))
+
+
+def java_string_hash(s: str) -> int:
+    h = 0
+    for ch in s:
+        h = (31 * h + ord(ch)) & 0xFFFFFFFF
+    return h - (1 << 32) if h >= 1 << 31 else h
+
+
+def test_principal_values(credentials: str) -> Dict[str, str]:
+    subject = hashlib.sha256((credentials or "").encode()).hexdigest()
+    return {"subject": subject, "email": f"{subject}@locahost", "name": subject, "login": subject,
+            "id": str(java_string_hash(subject))}
+
+
+# ---------------------------------------------------------------- RSA (PKCS#1 v1.5) verify
+_DIGEST_INFO = {
+    "SHA256": bytes.fromhex("3031300d060960864801650304020105000420"),
+    "SHA384": bytes.fromhex("3041300d060960864801650304020205000430"),
+    "SHA512": bytes.fromhex("3051300d060960864801650304020305000440"),
+}
+
+
+def rsa_pkcs1_verify(n: int, e: int, msg: bytes, sig: bytes, hash_name: str) -> bool:
+    k = (n.bit_length() + 7) // 8
+    if len(sig) != k:
+        return False
+    m = pow(int.from_bytes(sig, "big"), e, n).to_bytes(k, "big")
+    digest = hashlib.new(hash_name.lower(), msg).digest()
+    t = _DIGEST_INFO[hash_name] + digest
+    expected = b"\x00\x01" + b"\xff" * (k - len(t) - 3) + b"\x00" + t
+    return hmac.compare_digest(m, expected)
+
+
+def _der_read(b: bytes, i: int):
+    tag = b[i]
+    ln = b[i + 1]
+    i += 2
+    if ln & 0x80:
+        nb = ln & 0x7F
+        ln = int.from_bytes(b[i: i + nb], "big")
+        i += nb
+    return tag, b[i: i + ln], i + ln
+
+
+def rsa_from_pem(pem: str):
+    """SubjectPublicKeyInfo or PKCS#1 RSAPublicKey PEM -> (n, e)."""
+    body = "".join(l for l in pem.strip().splitlines() if not l.startswith("-----"))
+    der = base64.b64decode(body)
+    tag, seq, _ = _der_read(der, 0)
+    tag1, first, nxt = _der_read(seq, 0)
+    if tag1 == 0x30:  # SPKI: AlgorithmIdentifier, BIT STRING(RSAPublicKey)
+        _, bits, _ = _der_read(seq, nxt)
+        _, rsa, _ = _der_read(bits[1:], 0)
+        _, nb, j = _der_read(rsa, 0)
+        _, eb, _ = _der_read(rsa, j)
+    else:
+        nb = first
+        _, eb, _ = _der_read(seq, nxt)
+    return int.from_bytes(nb, "big"), int.from_bytes(eb, "big")
+
+
+def rsa_from_jwk(jwk: dict):
+    return int.from_bytes(_b64url(jwk["n"]), "big"), int.from_bytes(_b64url(jwk["e"]), "big")
+
+
+# ---------------------------------------------------------------- JWT
+class JwtError(Exception):
+    pass
+
+
+def decode_jwt(token: str, *, secret: Optional[bytes] = None, rsa_key=None,
+               jwks_fetch: Optional[Callable[[dict], Optional[tuple]]] = None, leeway: int = 0) -> dict:
+    try:
+        h64, p64, s64 = token.split(".")
+        header = json.loads(_b64url(h64))
+        payload = json.loads(_b64url(p64))
+        sig = _b64url(s64)
+    except Exception as e:  # noqa: BLE001
+        raise JwtError(f"malformed token: {e}") from e
+    alg = header.get("alg", "")
+    signing_input = f"{h64}.{p64}".encode()
+    if alg.startswith("HS"):
+        if secret is None:
+            raise JwtError("HMAC token but no secret-key configured")
+        mac = hmac.new(secret, signing_input, getattr(hashlib, "sha" + alg[2:])).digest()
+        if not hmac.compare_digest(mac, sig):
+            raise JwtError("bad signature")
+    elif alg.startswith("RS"):
+        key = rsa_key
+        if key is None and jwks_fetch is not None:
+            key = jwks_fetch(header)
+        if key is None:
+            raise JwtError("RSA token but no public key available")
+        if not rsa_pkcs1_verify(key[0], key[1], signing_input, sig, "SHA" + alg[2:]):
+            raise JwtError("bad signature")
+    else:
+        raise JwtError(f"unsupported alg {alg}")
+    now = time.time()
+    if "exp" in payload and now > float(payload["exp"]) + leeway:
+        raise JwtError("token expired")
+    if "nbf" in payload and now + leeway < float(payload["nbf"]):
+        raise JwtError("token not yet valid")
+    return payload
+
+
+def encode_jwt_hs256(payload: dict, secret: bytes) -> str:
+    """Helper for tests and the CLI (`gateway` commands with a shared secret)."""
+    enc = lambda b: base64.urlsafe_b64encode(b).rstrip(b"=").decode()  # noqa: E731
+    h = enc(json.dumps({"alg": "HS256", "typ": "JWT"}).encode())
+    p = enc(json.dumps(payload).encode())
+    sig = hmac.new(secret, f"{h}.{p}".encode(), hashlib.sha256).digest()
+    return f"{h}.{p}.{enc(sig)}"
+
+
+# ---------------------------------------------------------------- providers
+class AuthProvider:
+    def __init__(self, configuration: Dict[str, Any]):
+        self.cfg = dict(configuration or {})
+
+    def authenticate(self, ctx) -> AuthResult:
+        raise NotImplementedError
+
+
+class HttpAuthProvider(AuthProvider):
+    def authenticate(self, ctx) -> AuthResult:
+        import requests
+        path = str(_cfg(self.cfg, "path-template", "pathTemplate", default="")).replace("{tenant}", ctx.tenant)
+        url = str(_cfg(self.cfg, "base-url", "baseUrl", default="")) + path
+        headers = dict(_cfg(self.cfg, "headers", default={}) or {})
+        headers["Authorization"] = "Bearer " + (ctx.credentials or "")
+        accepted = [int(x) for x in _cfg(self.cfg, "accepted-statuses", "acceptedStatuses", default=[200, 201])]
+        try:
+            r = requests.get(url, headers=headers, timeout=30)
+        except Exception as e:  # noqa: BLE001
+            return AuthResult(False, str(e))
+        if r.status_code in accepted:
+            return AuthResult(True)
+        return AuthResult(False, f"Http authentication failed: {r.status_code}")
+
+
+class JwtAuthProvider(AuthProvider):
+    def __init__(self, configuration):
+        super().__init__(configuration)
+        sk = _cfg(self.cfg, "secret-key", "secretKey")
+        self.secret = None
+        if sk:
+            s = str(sk)
+            self.secret = base64.b64decode(s[len("base64:"):]) if s.startswith("base64:") else s.encode()
+        pk = _cfg(self.cfg, "public-key", "publicKey")
+        self.rsa = rsa_from_pem(str(pk)) if pk else None
+        self.jwks_uri = _cfg(self.cfg, "jwks-uri", "jwksUri")
+        allow = _cfg(self.cfg, "jwks-hosts-allowlist", "jwksHostsAllowlist", default="")
+        self.jwks_hosts = [h.strip() for h in str(allow).split(",") if h.strip()]
+        self.auth_claim = _cfg(self.cfg, "auth-claim", "authClaim", default="sub")
+        self.audience = _cfg(self.cfg, "audience")
+        self.audience_claim = _cfg(self.cfg, "audience-claim", "audienceClaim", default="aud")
+        self._jwks_cache: Dict[str, dict] = {}
+
+    def _jwks(self, header: dict) -> Optional[tuple]:
+        uri = header.get("jku") or self.jwks_uri
+        if not uri:
+            return None
+        host = urllib.parse.urlparse(uri).hostname or ""
+        if self.jwks_hosts and not any(host == h or uri.startswith(h) for h in self.jwks_hosts):
+            raise JwtError(f"jwks host {host} not allowed")
+        keys = self._jwks_cache.get(uri)
+        if keys is None:
+            import requests
+            keys = requests.get(uri, timeout=30).json()
+            self._jwks_cache[uri] = keys
+        for k in keys.get("keys", []):
+            if header.get("kid") in (None, k.get("kid")) and k.get("kty") == "RSA":
+                return rsa_from_jwk(k)
+        return None
+
+    def authenticate(self, ctx) -> AuthResult:
+        try:
+            claims = decode_jwt(ctx.credentials or "", secret=self.secret, rsa_key=self.rsa, jwks_fetch=self._jwks)
+        except JwtError as e:
+            return AuthResult(False, str(e))
+        if self.audience is not None:
+            aud = claims.get(self.audience_claim)
+            auds = aud if isinstance(aud, list) else [aud]
+            if self.audience not in auds:
+                return AuthResult(False, "audience mismatch")
+        values = {k: str(v) for k, v in claims.items() if isinstance(v, (str, int, float, bool))}
+        if self.auth_claim in claims:
+            values["subject"] = str(claims[self.auth_claim])
+        return AuthResult(True, None, values)
+
+
+class GitHubAuthProvider(AuthProvider):
+    def authenticate(self, ctx) -> AuthResult:
+        import requests
+        try:
+            r = requests.get("https://api.github.com/user", timeout=30,
+                             headers={"Authorization": f"Bearer {ctx.credentials}",
+                                      "Accept": "application/vnd.github+json"})
+        except Exception as e:  # noqa: BLE001
+            return AuthResult(False, str(e))
+        if r.status_code != 200:
+            return AuthResult(False, f"GitHub authentication failed: {r.status_code}")
+        u = r.json()
+        return AuthResult(True, None, {k: str(u.get(k)) for k in ("login", "id", "name", "email") if u.get(k)})
+
+
+class GoogleAuthProvider(JwtAuthProvider):
+    GOOGLE_JWKS = "https://www.googleapis.com/oauth2/v3/certs"
+
+    def __init__(self, configuration):
+        super().__init__(configuration)
+        self.jwks_uri = self.jwks_uri or self.GOOGLE_JWKS
+        self.audience = _cfg(self.cfg, "clientId", "client-id")
+
+    def authenticate(self, ctx) -> AuthResult:
+        res = super().authenticate(ctx)
+        if res.authenticated:
+            pv = res.principal_values
+            res.principal_values = {k: pv[k] for k in ("subject", "email", "name", "locale") if k in pv}
+        return res
+
+
+PROVIDERS: Dict[str, Callable[[Dict[str, Any]], AuthProvider]] = {
+    "http": HttpAuthProvider, "jwt": JwtAuthProvider, "github": GitHubAuthProvider, "google": GoogleAuthProvider,
+}
+
+
+def load_provider(name: str, configuration: Dict[str, Any]) -> AuthProvider:
+    f = PROVIDERS.get(name)
+    if f is None:
+        raise ValueError(f"unknown gateway authentication provider {name}; known: {sorted(PROVIDERS)}")
+    return f(configuration)
