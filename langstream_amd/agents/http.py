@@ -72,7 +72,7 @@ class HttpRequestAgent(AgentProcessor):
         self.http = None
 
     def start(self) -> None:
-        self.pool = ThreadPoolExecutor(max_workers=8, thread_name_prefix="http-request")
+        self.pool = ThreadPoolExecutor(max_workers=8, thread_name_prefix=f"agent-{self.agent_id()}-http")
         self.http = _session(self.allow_redirects, self.handle_cookies)
 
     def close(self) -> None:
@@ -166,7 +166,7 @@ class LangServeInvokeAgent(AgentProcessor):
         self.producer = None
 
     def start(self) -> None:
-        self.pool = ThreadPoolExecutor(max_workers=8, thread_name_prefix="langserve")
+        self.pool = ThreadPoolExecutor(max_workers=8, thread_name_prefix=f"agent-{self.agent_id()}-langserve")
         self.http = _session(self.allow_redirects, self.handle_cookies)
         if self.stream_to_topic:
             prov = self.context.topic_connection_provider

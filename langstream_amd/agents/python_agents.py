@@ -134,7 +134,7 @@ class _PythonAgentMixin:
 class PythonProcessor(_PythonAgentMixin, AgentProcessor):
     def init(self, configuration):
         self._load_user(configuration)
-        self.pool = ThreadPoolExecutor(max_workers=1, thread_name_prefix="py-processor")
+        self.pool = ThreadPoolExecutor(max_workers=1, thread_name_prefix=f"agent-{self.agent_id()}-py")
 
     def start(self):
         self._start_user()

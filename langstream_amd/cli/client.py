@@ -1,0 +1,122 @@
+"""Admin client for the control plane REST API (SURVEY §2.7 G7,
+``langstream-admin-client/.../AdminClient.java``): tenants, applications (multipart
+deploy / update with app zip + instance + secrets), logs, code download, archetypes.
+Retries idempotent calls on connection errors / 5xx with backoff."""
+from __future__ import annotations
+
+import io
+import json
+import os
+import time
+import zipfile
+from typing import Any, Dict, Iterator, Optional
+
+
+def zip_directory(path: str) -> bytes:
+    buf = io.BytesIO()
+    with zipfile.ZipFile(buf, "w", zipfile.ZIP_DEFLATED) as z:
+        for root, dirs, files in os.walk(path):
+            dirs[:] = sorted(d for d in dirs if d not in ("__pycache__", ".git"))
+            for fn in sorted(files):
+                full = os.path.join(root, fn)
+                z.write(full, os.path.relpath(full, path))
+    return buf.getvalue()
+
+
+class AdminClientError(Exception):
+    def __init__(self, status: int, text: str):
+        super().__init__(f"HTTP {status}: {text}")
+        self.status = status
+
+
+class AdminClient:
+    def __init__(self, web_service_url: str, tenant: str = "default", token: Optional[str] = None,
+                 retries: int = 3, timeout: float = 120.0):
+        import requests
+        self.url = web_service_url.rstrip("/")
+        self.tenant = tenant
+        self.retries = retries
+        self.timeout = timeout
+        self.http = requests.Session()
+        if token:
+            self.http.headers["Authorization"] = f"Bearer {token}"
+
+    def _call(self, method: str, path: str, idempotent: bool = True, **kw):
+        import requests
+        last = None
+        for i in range(self.retries if idempotent else 1):
+            try:
+                r = self.http.request(method, self.url + path, timeout=self.timeout, **kw)
+            except requests.ConnectionError as e:
+                last = e
+                time.sleep(0.5 * (2 ** i))
+                continue
+            if r.status_code >= 500 and idempotent and i + 1 < self.retries:
+                time.sleep(0.5 * (2 ** i))
+                continue
+            if r.status_code >= 400:
+                raise AdminClientError(r.status_code, r.text)
+            return r
+        raise last  # type: ignore[misc]
+
+    # tenants
+    def tenants(self) -> Dict[str, Any]:
+        return self._call("GET", "/api/tenants").json()
+
+    def tenant_put(self, name: str, config: Optional[dict] = None) -> Dict[str, Any]:
+        return self._call("PUT", f"/api/tenants/{name}", json=config or {}).json()
+
+    def tenant_get(self, name: str) -> Dict[str, Any]:
+        return self._call("GET", f"/api/tenants/{name}").json()
+
+    def tenant_delete(self, name: str) -> None:
+        self._call("DELETE", f"/api/tenants/{name}")
+
+    # applications
+    def _files(self, app: Optional[str], instance: Optional[str], secrets: Optional[str]):
+        files = {}
+        if app:
+            data = zip_directory(app) if os.path.isdir(app) else open(app, "rb").read()
+            files["app"] = ("app.zip", data, "application/zip")
+        for name, p in (("instance", instance), ("secrets", secrets)):
+            if p:
+                files[name] = (name + ".yaml", open(p).read() if os.path.exists(p) else p, "text/yaml")
+        return files
+
+    def deploy(self, app_id: str, app: Optional[str], instance: Optional[str] = None, secrets: Optional[str] = None,
+               dry_run: bool = False) -> Dict[str, Any]:
+        return self._call("POST", f"/api/applications/{self.tenant}/{app_id}", idempotent=False,
+                          params={"dry-run": str(dry_run).lower()},
+                          files=self._files(app, instance, secrets)).json()
+
+    def update(self, app_id: str, app: Optional[str], instance: Optional[str] = None,
+               secrets: Optional[str] = None) -> Dict[str, Any]:
+        return self._call("PATCH", f"/api/applications/{self.tenant}/{app_id}", idempotent=False,
+                          files=self._files(app, instance, secrets)).json()
+
+    def get(self, app_id: str, stats: bool = False) -> Dict[str, Any]:
+        return self._call("GET", f"/api/applications/{self.tenant}/{app_id}",
+                          params={"stats": str(stats).lower()}).json()
+
+    def list(self):
+        return self._call("GET", f"/api/applications/{self.tenant}").json()
+
+    def delete(self, app_id: str, force: bool = False) -> None:
+        self._call("DELETE", f"/api/applications/{self.tenant}/{app_id}", params={"force": str(force).lower()})
+
+    def logs(self, app_id: str, follow: bool = False) -> Iterator[Dict[str, Any]]:
+        r = self._call("GET", f"/api/applications/{self.tenant}/{app_id}/logs",
+                       params={"follow": str(follow).lower()}, stream=True)
+        for line in r.iter_lines():
+            if line:
+                yield json.loads(line)
+
+    def download(self, app_id: str) -> bytes:
+        return self._call("GET", f"/api/applications/{self.tenant}/{app_id}/code").content
+
+    def archetypes(self):
+        return self._call("GET", f"/api/archetypes/{self.tenant}").json()
+
+    def archetype_deploy(self, archetype: str, app_id: str, params: Dict[str, Any]) -> Dict[str, Any]:
+        return self._call("POST", f"/api/archetypes/{self.tenant}/{archetype}/applications/{app_id}",
+                          idempotent=False, json=params).json()

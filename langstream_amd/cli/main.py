@@ -1,0 +1,475 @@
+"""``langstream`` command line (``langstream-cli/.../commands/**``).
+
+    python -m langstream_amd.cli <group> <command> ...
+
+Groups:
+* ``profiles``  list | get | create | update | delete | set-current  (~/.langstream/config.yaml:
+  webServiceUrl, apiGatewayUrl, tenant, token)
+* ``tenants``   list | get | put | delete
+* ``apps``      deploy | update | get | list | delete | logs | download | diagram
+* ``gateway``   produce | consume | chat  (WebSocket client; chat re-assembles streamed
+  answers from ``stream-id`` / ``stream-index`` / ``stream-last-message`` headers,
+  ``ChatGatewayCmd.java:45-120``)
+* ``run``       the ``docker run`` equivalent (``LocalRunApplicationCmd.java``): control
+  plane (8090), gateway (8091) and agent control API (8790) in-process, the app
+  deployed on memory topics and the local GPU services
+* ``archetypes`` list | get | deploy
+* ``python``    load-pip-requirements | run-tests
+* ``code-download`` (k8s init container: fetch + unzip the app code archive)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import threading
+import time
+from typing import Any, Dict, List, Optional
+
+CONFIG = os.path.expanduser(os.environ.get("LANGSTREAM_CLI_CONFIG", "~/.langstream/config.yaml"))
+DEFAULT_PROFILE = {"webServiceUrl": "http://localhost:8090", "apiGatewayUrl": "ws://localhost:8091",
+                   "tenant": "default", "token": None}
+
+
+# ---------------------------------------------------------------- profiles
+def load_config() -> Dict[str, Any]:
+    import yaml
+    if os.path.exists(CONFIG):
+        with open(CONFIG) as f:
+            c = yaml.safe_load(f) or {}
+    else:
+        c = {}
+    c.setdefault("profiles", {})
+    c.setdefault("currentProfile", "default")
+    return c
+
+
+def save_config(c: Dict[str, Any]) -> None:
+    import yaml
+    os.makedirs(os.path.dirname(CONFIG), exist_ok=True)
+    with open(CONFIG, "w") as f:
+        yaml.safe_dump(c, f)
+
+
+def current_profile(args) -> Dict[str, Any]:
+    c = load_config()
+    name = getattr(args, "profile", None) or c.get("currentProfile", "default")
+    p = dict(DEFAULT_PROFILE)
+    p.update(c["profiles"].get(name) or {})
+    if getattr(args, "tenant", None):
+        p["tenant"] = args.tenant
+    return p
+
+
+def _client(args):
+    from .client import AdminClient
+    p = current_profile(args)
+    return AdminClient(p["webServiceUrl"], p["tenant"], p.get("token"))
+
+
+def _print(obj, fmt: str = "json") -> None:
+    if fmt == "yaml":
+        import yaml
+        print(yaml.safe_dump(obj, sort_keys=False))
+    else:
+        print(json.dumps(obj, indent=2, default=str))
+
+
+# ---------------------------------------------------------------- apps
+def cmd_profiles(args) -> int:
+    c = load_config()
+    if args.cmd == "list":
+        _print({"current": c["currentProfile"], "profiles": c["profiles"]})
+    elif args.cmd == "get":
+        _print(c["profiles"].get(args.name) or {})
+    elif args.cmd in ("create", "update"):
+        p = c["profiles"].get(args.name, {}) if args.cmd == "update" else {}
+        for k, a in (("webServiceUrl", args.web_service_url), ("apiGatewayUrl", args.api_gateway_url),
+                     ("tenant", args.tenant_name), ("token", args.token)):
+            if a is not None:
+                p[k] = a
+        c["profiles"][args.name] = p
+        if args.set_current:
+            c["currentProfile"] = args.name
+        save_config(c)
+    elif args.cmd == "delete":
+        c["profiles"].pop(args.name, None)
+        save_config(c)
+    elif args.cmd == "set-current":
+        c["currentProfile"] = args.name
+        save_config(c)
+    return 0
+
+
+def cmd_tenants(args) -> int:
+    cl = _client(args)
+    if args.cmd == "list":
+        _print(cl.tenants())
+    elif args.cmd == "get":
+        _print(cl.tenant_get(args.name))
+    elif args.cmd == "put":
+        _print(cl.tenant_put(args.name, {"max-total-resource-units": args.max_units} if args.max_units else {}))
+    elif args.cmd == "delete":
+        cl.tenant_delete(args.name)
+    return 0
+
+
+def mermaid(app_dir: str, instance: Optional[str] = None, secrets: Optional[str] = None) -> str:
+    """Mermaid flowchart of the execution plan (topics as stadiums, agents as boxes)."""
+    from ..core.deployer import ApplicationDeployer
+    from ..core.parser import build_from_directory
+    info = build_from_directory(app_dir, instance, secrets)
+    plan = ApplicationDeployer().create_implementation("app", info.application)
+    lines = ["flowchart LR"]
+    ids = {}
+
+    def nid(s):
+        return ids.setdefault(s, f"n{len(ids)}")
+
+    for t in plan.topics:
+        lines.append(f'  {nid("topic:" + t)}(["{t}"])')
+    for node in plan.agents.values():
+        steps = [p["agentId"] for p in node.configuration.get("processors", [])] if \
+            node.agent_type == "composite-agent" else [node.id]
+        label = "<br/>".join(steps)
+        lines.append(f'  {nid("agent:" + node.id)}["{label}<br/><i>{node.agent_type}</i>"]')
+        if node.input is not None:
+            lines.append(f'  {nid("topic:" + node.input.name)} --> {nid("agent:" + node.id)}')
+        if node.output is not None:
+            lines.append(f'  {nid("agent:" + node.id)} --> {nid("topic:" + node.output.name)}')
+    return "\n".join(lines)
+
+
+def cmd_apps(args) -> int:
+    if args.cmd == "diagram":
+        print(mermaid(args.app, args.instance, args.secrets))
+        return 0
+    cl = _client(args)
+    if args.cmd == "deploy":
+        _print(cl.deploy(args.name, args.app, args.instance, args.secrets, args.dry_run), args.output)
+    elif args.cmd == "update":
+        _print(cl.update(args.name, args.app, args.instance, args.secrets), args.output)
+    elif args.cmd == "get":
+        _print(cl.get(args.name, stats=True), args.output)
+    elif args.cmd == "list":
+        _print(cl.list(), args.output)
+    elif args.cmd == "delete":
+        cl.delete(args.name, args.force)
+    elif args.cmd == "logs":
+        for rec in cl.logs(args.name, follow=args.follow):
+            print(f"[{rec.get('replica')}] {rec.get('level')} {rec.get('message')}")
+    elif args.cmd == "download":
+        data = cl.download(args.name)
+        out = args.output_file or f"{args.name}.zip"
+        with open(out, "wb") as f:
+            f.write(data)
+        print(out)
+    return 0
+
+
+# ---------------------------------------------------------------- gateway
+def _gw_url(args, kind: str, gateway: str) -> str:
+    import urllib.parse
+    p = current_profile(args)
+    q = [(f"param:{k}", v) for k, v in (kv.split("=", 1) for kv in args.param or [])]
+    if getattr(args, "position", None):
+        q.append(("option:position", args.position))
+    if args.credentials:
+        q.append(("credentials", args.credentials))
+    if args.test_credentials:
+        q.append(("test-credentials", args.test_credentials))
+    base = p["apiGatewayUrl"].rstrip("/")
+    return f"{base}/v1/{kind}/{p['tenant']}/{args.application}/{gateway}" + (
+        "?" + urllib.parse.urlencode(q) if q else "")
+
+
+def cmd_gateway(args) -> int:
+    import asyncio
+    import aiohttp
+
+    async def produce():
+        async with aiohttp.ClientSession() as s, s.ws_connect(_gw_url(args, "produce", args.gateway)) as ws:
+            msg = {"key": args.key, "value": args.value,
+                   "headers": dict(kv.split("=", 1) for kv in args.header or [])}
+            await ws.send_str(json.dumps(msg))
+            print((await ws.receive()).data)
+
+    async def consume():
+        n = 0
+        async with aiohttp.ClientSession() as s, s.ws_connect(_gw_url(args, "consume", args.gateway)) as ws:
+            async for m in ws:
+                print(m.data, flush=True)
+                n += 1
+                if args.num_messages and n >= args.num_messages:
+                    return
+
+    async def chat():
+        loop = asyncio.get_running_loop()
+        async with aiohttp.ClientSession() as s, s.ws_connect(_gw_url(args, "chat", args.gateway)) as ws:
+            done = asyncio.Event()
+            parts: Dict[str, Dict[int, str]] = {}
+
+            async def reader():
+                async for m in ws:
+                    d = json.loads(m.data)
+                    if "record" not in d:
+                        continue
+                    rec = d["record"]
+                    h = rec.get("headers") or {}
+                    sid = h.get("stream-id")
+                    if sid is None:
+                        print(f"\n< {rec.get('value')}", flush=True)
+                        done.set()
+                        continue
+                    parts.setdefault(sid, {})[int(h.get("stream-index", 0))] = rec.get("value") or ""
+                    print(rec.get("value") or "", end="", flush=True)
+                    if h.get("stream-last-message") == "true":
+                        print(flush=True)
+                        done.set()
+            task = asyncio.ensure_future(reader())
+            while True:
+                line = await loop.run_in_executor(None, sys.stdin.readline)
+                if not line:
+                    break
+                line = line.strip()
+                if not line:
+                    continue
+                done.clear()
+                await ws.send_str(json.dumps({"value": line}))
+                await asyncio.wait_for(done.wait(), timeout=600)
+            task.cancel()
+
+    fn = {"produce": produce, "consume": consume, "chat": chat}[args.cmd]
+    asyncio.new_event_loop().run_until_complete(fn())
+    return 0
+
+
+# ---------------------------------------------------------------- local run (docker run)
+def cmd_run(args) -> int:
+    import logging
+    logging.basicConfig(level=logging.INFO, format="%(asctime)s %(levelname)s %(threadName)s %(message)s")
+    from ..core.store import InMemoryApplicationStore
+    from ..gateway.server import GatewayServer, GatewayService
+    from ..runtime.pod import AgentAPIServer
+    from ..webservice.server import ControlPlane, WebServiceServer
+    from .client import zip_directory
+    store = InMemoryApplicationStore()
+    cp = ControlPlane(store)
+    store.put_tenant(args.tenant)
+    instance = open(args.instance).read() if args.instance else None
+    secrets = open(args.secrets).read() if args.secrets else None
+    res = cp.deploy(args.tenant, args.name, zip_directory(args.app), instance, secrets, dry_run=args.dry_run)
+    if args.dry_run:
+        _print(res, "yaml")
+        return 0
+    ws = WebServiceServer(cp, host=args.host, port=args.web_port).start()
+    gw = GatewayServer(GatewayService(store), host=args.host, port=args.gateway_port).start()
+    sa = store.get(args.tenant, args.name)
+    api = AgentAPIServer(sa.runner.runners if sa.runner else [], host=args.host, port=args.agents_port).start()
+    print(f"application {args.name} running: webservice {ws.url}  gateway {gw.url.replace('http', 'ws')}  "
+          f"agents http://{args.host}:{api.port}", flush=True)
+    stop = threading.Event()
+    try:
+        import signal
+        signal.signal(signal.SIGTERM, lambda *_: stop.set())
+    except ValueError:
+        pass
+    try:
+        while not stop.is_set():
+            stop.wait(1.0)
+            if sa.runner is not None and sa.runner.errors:
+                print(f"agent failure: {sa.runner.errors[0]!r}", file=sys.stderr)
+                return 1
+    except KeyboardInterrupt:
+        pass
+    finally:
+        api.stop()
+        gw.stop()
+        ws.stop()
+        cp.delete(args.tenant, args.name, force=True)
+    return 0
+
+
+def cmd_archetypes(args) -> int:
+    cl = _client(args)
+    if args.cmd == "list":
+        _print(cl.archetypes())
+    elif args.cmd == "get":
+        _print(next((a for a in cl.archetypes() if a["id"] == args.id), {}))
+    elif args.cmd == "deploy":
+        params = json.loads(args.parameters) if args.parameters else {}
+        _print(cl.archetype_deploy(args.id, args.name, params))
+    return 0
+
+
+def cmd_python(args) -> int:
+    pydir = os.path.join(args.app, "python")
+    if args.cmd == "load-pip-requirements":
+        req = os.path.join(pydir, "requirements.txt")
+        if not os.path.exists(req):
+            print("no python/requirements.txt")
+            return 0
+        import importlib.util
+        missing = []
+        for line in open(req):
+            name = line.split("#")[0].strip().split("==")[0].split(">=")[0].strip()
+            if name and importlib.util.find_spec(name.replace("-", "_")) is None:
+                missing.append(name)
+        os.makedirs(os.path.join(pydir, "lib"), exist_ok=True)
+        if missing:
+            print("not installed (no package index available in this environment): " + ", ".join(missing))
+            return 1
+        print("all requirements importable")
+        return 0
+    if args.cmd == "run-tests":
+        import subprocess
+        env = dict(os.environ, PYTHONPATH=os.pathsep.join([pydir, os.path.join(pydir, "lib"),
+                                                           os.environ.get("PYTHONPATH", "")]))
+        return subprocess.call([sys.executable, "-m", "pytest", pydir, "-q"], env=env)
+    return 2
+
+
+def cmd_code_download(args) -> int:
+    import io
+    import zipfile
+    from .client import AdminClient
+    url = args.web_service_url or os.environ.get("LANGSTREAM_WEBSERVICE_URL", "http://langstream-control-plane:8090")
+    data = AdminClient(url, args.tenant).download(args.application)
+    with zipfile.ZipFile(io.BytesIO(data)) as z:
+        z.extractall(args.target)
+    return 0
+
+
+# ---------------------------------------------------------------- parser
+def build_parser() -> argparse.ArgumentParser:
+    ap = argparse.ArgumentParser(prog="langstream", description="LangStream (MI355X-native) command line")
+    ap.add_argument("--profile")
+    ap.add_argument("--tenant")
+    sub = ap.add_subparsers(dest="group", required=True)
+
+    p = sub.add_parser("profiles")
+    ps = p.add_subparsers(dest="cmd", required=True)
+    ps.add_parser("list")
+    for c in ("get", "delete", "set-current"):
+        ps.add_parser(c).add_argument("name")
+    for c in ("create", "update"):
+        x = ps.add_parser(c)
+        x.add_argument("name")
+        x.add_argument("--web-service-url")
+        x.add_argument("--api-gateway-url")
+        x.add_argument("--tenant", dest="tenant_name")
+        x.add_argument("--token")
+        x.add_argument("--set-current", action="store_true")
+    p.set_defaults(fn=cmd_profiles)
+
+    t = sub.add_parser("tenants")
+    ts = t.add_subparsers(dest="cmd", required=True)
+    ts.add_parser("list")
+    for c in ("get", "delete"):
+        ts.add_parser(c).add_argument("name")
+    x = ts.add_parser("put")
+    x.add_argument("name")
+    x.add_argument("--max-units", type=int)
+    t.set_defaults(fn=cmd_tenants)
+
+    a = sub.add_parser("apps")
+    asub = a.add_subparsers(dest="cmd", required=True)
+    for c in ("deploy", "update"):
+        x = asub.add_parser(c)
+        x.add_argument("name")
+        x.add_argument("-app", "--app", required=(c == "deploy"))
+        x.add_argument("-i", "--instance")
+        x.add_argument("-s", "--secrets")
+        x.add_argument("--dry-run", action="store_true")
+        x.add_argument("-o", "--output", default="json", choices=["json", "yaml"])
+    for c in ("get",):
+        x = asub.add_parser(c)
+        x.add_argument("name")
+        x.add_argument("-o", "--output", default="json", choices=["json", "yaml"])
+    x = asub.add_parser("list")
+    x.add_argument("-o", "--output", default="json", choices=["json", "yaml"])
+    x = asub.add_parser("delete")
+    x.add_argument("name")
+    x.add_argument("--force", action="store_true")
+    x = asub.add_parser("logs")
+    x.add_argument("name")
+    x.add_argument("-f", "--follow", action="store_true")
+    x = asub.add_parser("download")
+    x.add_argument("name")
+    x.add_argument("-o", "--output-file")
+    x = asub.add_parser("diagram")
+    x.add_argument("-app", "--app", required=True)
+    x.add_argument("-i", "--instance")
+    x.add_argument("-s", "--secrets")
+    a.set_defaults(fn=cmd_apps)
+
+    g = sub.add_parser("gateway")
+    gs = g.add_subparsers(dest="cmd", required=True)
+    for c in ("produce", "consume", "chat"):
+        x = gs.add_parser(c)
+        x.add_argument("application")
+        x.add_argument("gateway")
+        x.add_argument("-p", "--param", action="append")
+        x.add_argument("-c", "--credentials")
+        x.add_argument("--test-credentials")
+        if c == "produce":
+            x.add_argument("-v", "--value")
+            x.add_argument("-k", "--key")
+            x.add_argument("--header", action="append")
+        if c == "consume":
+            x.add_argument("--position")
+            x.add_argument("-n", "--num-messages", type=int, default=0)
+        if c == "chat":
+            x.add_argument("--position")
+    g.set_defaults(fn=cmd_gateway)
+
+    r = sub.add_parser("run", help="run an application locally (the `docker run` equivalent)")
+    r.add_argument("name")
+    r.add_argument("-app", "--app", required=True)
+    r.add_argument("-i", "--instance")
+    r.add_argument("-s", "--secrets")
+    r.add_argument("--dry-run", action="store_true")
+    r.add_argument("--host", default="127.0.0.1")
+    r.add_argument("--web-port", type=int, default=8090)
+    r.add_argument("--gateway-port", type=int, default=8091)
+    r.add_argument("--agents-port", type=int, default=8790)
+    r.set_defaults(fn=cmd_run, tenant="default")
+
+    ar = sub.add_parser("archetypes")
+    ars = ar.add_subparsers(dest="cmd", required=True)
+    ars.add_parser("list")
+    ars.add_parser("get").add_argument("id")
+    x = ars.add_parser("deploy")
+    x.add_argument("id")
+    x.add_argument("name")
+    x.add_argument("-p", "--parameters", help="JSON object of archetype parameters")
+    ar.set_defaults(fn=cmd_archetypes)
+
+    py = sub.add_parser("python")
+    pys = py.add_subparsers(dest="cmd", required=True)
+    for c in ("load-pip-requirements", "run-tests"):
+        pys.add_parser(c).add_argument("-app", "--app", required=True)
+    py.set_defaults(fn=cmd_python)
+
+    cd = sub.add_parser("code-download")
+    cd.add_argument("--tenant", default="default")
+    cd.add_argument("--application", required=True)
+    cd.add_argument("--code-archive-id")
+    cd.add_argument("--target", required=True)
+    cd.add_argument("--web-service-url")
+    cd.set_defaults(fn=cmd_code_download)
+    return ap
+
+
+def main(argv: Optional[List[str]] = None) -> int:
+    args = build_parser().parse_args(argv)
+    try:
+        return args.fn(args) or 0
+    except Exception as e:  # noqa: BLE001
+        print(f"error: {e}", file=sys.stderr)
+        return 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,153 @@
+"""Kubernetes compute-cluster runtime: plan -> manifests.
+
+Parity: ``K8SRT/KubernetesClusterRuntime.java:93-380`` (one Secret with the
+RuntimePodConfiguration + one ``Agent`` custom resource per plan agent),
+``DEPL/agents/AgentResourcesFactory.java:98-586`` (StatefulSet with replicas =
+parallelism (max 8), parallel pod management, code-download init containers, the
+``agent-runtime`` container on ports 8080 (http) / 8000 (service), probes on
+``/metrics``, CPU = size x 0.5, memory = size x 512M, PVCs for agent disks, headless
+Service) and the CRD shapes of ``helm/crds``.
+
+MI355X deployment additions: each replica is one process per GPU -- the container
+requests ``amd.com/gpu: 1`` when the agent uses a GPU service (embeddings / completions /
+vector store) and the pod sets ``HIP_VISIBLE_DEVICES`` through the device plugin; a
+tensor-parallel chat agent (``tp`` > 1 in its resource) requests ``tp`` GPUs on one node
+and runs ``torchrun --nproc-per-node tp``.
+
+Manifests are returned as plain dicts (``kubectl apply -f -`` ready once dumped to
+YAML); ``apply_manifests`` shells out to kubectl when it exists.
+"""
+from __future__ import annotations
+
+import base64
+import json
+import shutil
+import subprocess
+from typing import Any, Dict, List, Optional
+
+from .planner import AgentNode, ExecutionPlan
+
+MAX_REPLICAS = 8
+GPU_AGENT_TYPES = ("ai-tools", "compute-ai-embeddings", "ai-chat-completions", "ai-text-completions",
+                   "query-vector-db", "vector-db-sink", "re-rank", "composite-agent")
+DEFAULT_IMAGE = "langstream-amd/runtime:latest"
+
+
+def _uses_gpu(node: AgentNode) -> bool:
+    if node.agent_type in ("ai-tools", "composite-agent"):
+        txt = json.dumps(node.configuration)
+        return any(t in txt for t in ("compute-ai-embeddings", "ai-chat-completions", "ai-text-completions",
+                                      "query", "vector"))
+    return node.agent_type in GPU_AGENT_TYPES
+
+
+def _name(s: str) -> str:
+    return "".join(c if c.isalnum() or c == "-" else "-" for c in s.lower()).strip("-")[:63]
+
+
+def agent_pod_configuration(plan: ExecutionPlan, node: AgentNode, tenant: str) -> Dict[str, Any]:
+    inst = plan.application.instance
+    sc = inst.streaming_cluster if inst is not None else None
+    inp: Dict[str, Any] = {}
+    if node.input is not None:
+        inp["topic"] = node.input.name
+        if node.input.deadletter is not None:
+            inp["deadLetterTopicProducer"] = {"topic": node.input.deadletter.name}
+    return {
+        "input": inp,
+        "output": {"topic": node.output.name} if node.output is not None else {},
+        "agent": {"componentType": node.component_type.value, "tenant": tenant, "agentId": node.id,
+                  "applicationId": plan.application_id, "agentType": node.agent_type,
+                  "configuration": node.configuration,
+                  "errorHandlerConfiguration": {"retries": node.errors.retries or 0,
+                                                "onFailure": node.errors.on_failure or "fail"},
+                  "agentsWithDisk": sorted(node.disks)},
+        "streamingCluster": {"type": sc.type, "configuration": sc.configuration} if sc else None,
+    }
+
+
+def render_manifests(plan: ExecutionPlan, tenant: str, code_archive_id: Optional[str] = None,
+                     image: str = DEFAULT_IMAGE, namespace_prefix: str = "langstream-") -> List[Dict[str, Any]]:
+    ns = f"{namespace_prefix}{tenant}"
+    out: List[Dict[str, Any]] = []
+    app = _name(plan.application_id)
+    for node in plan.agents.values():
+        agent = _name(f"{plan.application_id}-{node.id}")
+        size = int(node.resources.size or 1)
+        replicas = max(1, min(MAX_REPLICAS, int(node.resources.parallelism or 1)))
+        tp = int(getattr(node.resources, "tp", 1) or 1)
+        secret_name = f"{agent}-config"
+        pod_cfg = agent_pod_configuration(plan, node, tenant)
+        out.append({"apiVersion": "v1", "kind": "Secret", "metadata": {"name": secret_name, "namespace": ns},
+                    "data": {"app-config": base64.b64encode(json.dumps(pod_cfg).encode()).decode()}})
+        out.append({"apiVersion": "langstream.ai/v1alpha1", "kind": "Agent",
+                    "metadata": {"name": agent, "namespace": ns, "labels": {"app.kubernetes.io/name": app}},
+                    "spec": {"agentId": node.id, "applicationId": plan.application_id, "tenant": tenant,
+                             "agentConfigSecretRef": secret_name, "codeArchiveId": code_archive_id,
+                             "resources": {"parallelism": replicas, "size": size},
+                             "options": {"disks": [{"agentId": k, "size": v.size, "type": v.type}
+                                                   for k, v in node.disks.items()]}}})
+        gpus = tp if _uses_gpu(node) else 0
+        limits = {"cpu": f"{size * 0.5:g}", "memory": f"{size * 512}M"}
+        if gpus:
+            limits["amd.com/gpu"] = str(gpus)
+        cmd = ["python", "-m", "langstream_amd.runtime.pod", "/app-config/config"]
+        if tp > 1:
+            cmd = ["torchrun", "--nnodes=1", f"--nproc-per-node={tp}", "--master-addr=127.0.0.1", "-m",
+                   "langstream_amd.runtime.pod", "/app-config/config"]
+        container = {
+            "name": "agent-runtime", "image": image, "command": cmd,
+            "ports": [{"name": "http", "containerPort": 8080}, {"name": "service", "containerPort": 8000}],
+            "env": [{"name": "LANGSTREAM_AGENT_RUNNER_POD_CONFIGURATION", "value": "/app-config/config"},
+                    {"name": "LANGSTREAM_AGENT_RUNNER_CODE_PATH", "value": "/app-code-download"},
+                    {"name": "HSA_ENABLE_IPC_MODE_LEGACY", "value": "0"}],
+            "resources": {"requests": dict(limits), "limits": limits},
+            "livenessProbe": {"httpGet": {"path": "/metrics", "port": 8080}, "initialDelaySeconds": 10,
+                              "periodSeconds": 30, "timeoutSeconds": 5},
+            "readinessProbe": {"httpGet": {"path": "/metrics", "port": 8080}, "initialDelaySeconds": 10,
+                               "periodSeconds": 30, "timeoutSeconds": 5},
+            "volumeMounts": [{"name": "app-config", "mountPath": "/app-config"},
+                             {"name": "code-download", "mountPath": "/app-code-download"}]
+                            + [{"name": _name(f"{k}-disk"), "mountPath": f"/persistent-state/{k}"} for k in node.disks],
+        }
+        init = [{"name": "code-download", "image": image,
+                 "command": ["python", "-m", "langstream_amd.cli", "code-download", "--tenant", tenant,
+                             "--application", plan.application_id, "--code-archive-id", str(code_archive_id),
+                             "--target", "/app-code-download"],
+                 "volumeMounts": [{"name": "code-download", "mountPath": "/app-code-download"}]}]
+        out.append({
+            "apiVersion": "apps/v1", "kind": "StatefulSet",
+            "metadata": {"name": agent, "namespace": ns,
+                         "labels": {"app": agent, "langstream-application": app, "langstream-agent": node.id}},
+            "spec": {"replicas": replicas, "podManagementPolicy": "Parallel", "serviceName": agent,
+                     "selector": {"matchLabels": {"app": agent}},
+                     "template": {"metadata": {"labels": {"app": agent}},
+                                  "spec": {"initContainers": init, "containers": [container],
+                                           "terminationGracePeriodSeconds": 60,
+                                           "volumes": [{"name": "app-config", "secret": {
+                                               "secretName": secret_name,
+                                               "items": [{"key": "app-config", "path": "config"}]}},
+                                               {"name": "code-download", "emptyDir": {}}]}},
+                     "volumeClaimTemplates": [
+                         {"metadata": {"name": _name(f"{k}-disk")},
+                          "spec": {"accessModes": ["ReadWriteOnce"],
+                                   "resources": {"requests": {"storage": v.size or "256M"}},
+                                   **({"storageClassName": v.type} if v.type and v.type != "default" else {})}}
+                         for k, v in node.disks.items()]}})
+        out.append({"apiVersion": "v1", "kind": "Service", "metadata": {"name": agent, "namespace": ns},
+                    "spec": {"clusterIP": "None", "selector": {"app": agent},
+                             "ports": [{"name": "http", "port": 8080}, {"name": "service", "port": 8000}]}})
+    return out
+
+
+def to_yaml(manifests: List[Dict[str, Any]]) -> str:
+    import yaml
+    return yaml.safe_dump_all(manifests, sort_keys=False)
+
+
+def apply_manifests(manifests: List[Dict[str, Any]]) -> bool:
+    kubectl = shutil.which("kubectl")
+    if kubectl is None:
+        return False
+    subprocess.run([kubectl, "apply", "-f", "-"], input=to_yaml(manifests).encode(), check=True)
+    return True

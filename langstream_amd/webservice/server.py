@@ -1,0 +1,466 @@
+"""Control plane REST API (``WS/application/ApplicationResource.java:79-546``,
+``ApplicationService.java:65-385``, ``WS/common/TenantResource.java``, ``WS/archetype/*``).
+
+Endpoints:
+* ``/api/tenants`` GET (all) | ``/api/tenants/{tenant}`` GET / PUT / POST / DELETE;
+* ``/api/applications/{tenant}`` GET (list);
+* ``/api/applications/{tenant}/{id}`` POST (deploy, multipart ``app`` zip + ``instance``
+  + ``secrets`` text parts, ``?dry-run=true`` returns the execution plan only), PATCH
+  (update: same parts; unchanged python code keeps its code archive id -- digest
+  check, ``ModelBuilder.java:275-349``), DELETE (``?force=``), GET (``?stats=true`` adds
+  live agent status);
+* ``/api/applications/{tenant}/{id}/logs`` NDJSON stream of the app's agent logs;
+* ``/api/applications/{tenant}/{id}/code`` (zip download) and ``/code/info``;
+* ``/api/archetypes/{tenant}`` list, ``/api/archetypes/{tenant}/{id}`` get,
+  ``/api/archetypes/{tenant}/{id}/applications/{app}`` POST (deploy from archetype with
+  JSON parameters).
+
+Deploy = parse (``core.parser``) -> resolve placeholders + plan (validation, the tenant
+resource-unit limit Σ size×parallelism, ``ApplicationService.java:95-125``) -> store ->
+start on the compute cluster: ``local``/``none``/``docker`` run in-process
+(``LocalApplicationRunner``, the docker-run path); ``kubernetes`` renders the Agent
+custom resources + StatefulSets (``core.k8s``) into the store (and applies them with
+kubectl when ``apply`` is configured).  Optional bearer-token auth (HS256 JWT).
+"""
+from __future__ import annotations
+
+import asyncio
+import collections
+import hashlib
+import io
+import json
+import logging
+import os
+import shutil
+import tempfile
+import threading
+import time
+import zipfile
+from typing import Any, Dict, List, Optional
+
+from ..core.parser import build_application_instance, build_from_archetype, directory_digest, read_app_directory
+from ..core.store import ApplicationStore, InMemoryApplicationStore, StoredApplication
+
+log = logging.getLogger(__name__)
+
+
+class _AppLogBuffer(logging.Handler):
+    """Collects log records emitted by one application's agent threads."""
+
+    def __init__(self, maxlen: int = 5000):
+        super().__init__()
+        self.records: "collections.deque" = collections.deque(maxlen=maxlen)
+        self.threads: set = set()
+        self.seq = 0
+        self.cv = threading.Condition()
+
+    def emit(self, record: logging.LogRecord) -> None:
+        # agent threads and their worker pools are named "agent-<agent id>..."
+        if not any(record.threadName.startswith(p) for p in self.threads):
+            return
+        with self.cv:
+            self.seq += 1
+            self.records.append((self.seq, {"timestamp": int(record.created * 1000), "level": record.levelname,
+                                             "replica": record.threadName, "message": self.format(record)}))
+            self.cv.notify_all()
+
+    def wait_new(self, last: int, timeout: float) -> None:
+        with self.cv:
+            if self.seq <= last:
+                self.cv.wait(timeout)
+
+
+class ControlPlane:
+    """Application lifecycle independent of HTTP (also used by the CLI's local mode)."""
+
+    def __init__(self, store: Optional[ApplicationStore] = None, code_dir: Optional[str] = None,
+                 services=None, max_units_per_tenant: int = 0):
+        self.store = store or InMemoryApplicationStore()
+        self.code_dir = code_dir or tempfile.mkdtemp(prefix="langstream-code-")
+        os.makedirs(self.code_dir, exist_ok=True)
+        self.services = services
+        self.max_units = max_units_per_tenant
+        self._logs: Dict[tuple, _AppLogBuffer] = {}
+        self.archetypes_dir: Optional[str] = None
+
+    # ---------------------------------------------------------------- helpers
+    @staticmethod
+    def unzip(data: bytes, dest: str) -> Dict[str, str]:
+        with zipfile.ZipFile(io.BytesIO(data)) as z:
+            for n in z.namelist():
+                p = os.path.normpath(os.path.join(dest, n))
+                if not p.startswith(os.path.abspath(dest)):
+                    raise ValueError(f"bad path in archive: {n}")
+            z.extractall(dest)
+        # the app may be at the root or inside a single top-level directory
+        root = dest
+        entries = [e for e in os.listdir(dest) if not e.startswith(".")]
+        if not any(e.endswith(".yaml") for e in entries) and len(entries) == 1 and \
+                os.path.isdir(os.path.join(dest, entries[0])):
+            root = os.path.join(dest, entries[0])
+        return {"__root__": root, **read_app_directory(root)}
+
+    def _units(self, plan) -> int:
+        return sum(int(n.resources.size or 1) * int(n.resources.parallelism or 1) for n in plan.agents.values())
+
+    def _tenant_units(self, tenant: str, exclude: Optional[str] = None) -> int:
+        from ..core.deployer import ApplicationDeployer
+        tot = 0
+        for a in self.store.list(tenant):
+            if a.application_id == exclude:
+                continue
+            try:
+                tot += self._units(ApplicationDeployer().create_implementation(a.application_id, a.application))
+            except Exception:  # noqa: BLE001
+                pass
+        return tot
+
+    # ---------------------------------------------------------------- lifecycle
+    def deploy(self, tenant: str, app_id: str, app_zip: Optional[bytes], instance: Optional[str],
+               secrets: Optional[str], dry_run: bool = False, update: bool = False,
+               files: Optional[Dict[str, str]] = None) -> Dict[str, Any]:
+        from ..core.deployer import ApplicationDeployer
+        if self.store.get_tenant(tenant) is None:
+            raise KeyError(f"tenant {tenant} not found")
+        existing = self.store.get(tenant, app_id)
+        if update and existing is None:
+            raise KeyError(f"application {app_id} not found")
+        if not update and existing is not None and not dry_run:
+            raise FileExistsError(f"application {app_id} already exists")
+        code_root, digest, archive = None, None, None
+        if app_zip is not None:
+            tmp = tempfile.mkdtemp(prefix="app-", dir=self.code_dir)
+            files = self.unzip(app_zip, tmp)
+            code_root = files.pop("__root__")
+            digest = directory_digest(os.path.join(code_root, "python"))
+            archive = hashlib.sha256(app_zip).hexdigest()[:32]
+        elif files is None:
+            if existing is None:
+                raise ValueError("missing application archive")
+            files = existing.files
+        instance = instance if instance is not None else (existing.instance if existing else None)
+        secrets = secrets if secrets is not None else (existing.secrets if existing else None)
+        info = build_application_instance(files, instance, secrets)
+        plan = ApplicationDeployer().create_implementation(app_id, info.application)
+        units = self._units(plan)
+        if self.max_units and self._tenant_units(tenant, exclude=app_id) + units > self.max_units:
+            raise PermissionError(f"Not enough resources to deploy application {app_id}: tenant limit "
+                                  f"{self.max_units} units")
+        if dry_run:
+            return {"application": plan.to_dict(), "dry-run": True}
+        if update and existing is not None and existing.code_archive_id and digest is not None:
+            old = os.path.join(self.code_dir, existing.code_archive_id)
+            if directory_digest(os.path.join(old, "python")) == digest:
+                archive = existing.code_archive_id  # python code unchanged: keep the archive
+        if code_root is not None:
+            dst = os.path.join(self.code_dir, archive)
+            if not os.path.exists(dst):
+                shutil.move(code_root, dst)
+            with open(os.path.join(self.code_dir, archive + ".zip"), "wb") as f:
+                f.write(app_zip)
+        if existing is not None and existing.runner is not None:
+            existing.runner.stop(10)
+        sa = StoredApplication(app_id, tenant, info.application, dict(files), instance, secrets,
+                               archive or (existing.code_archive_id if existing else None), "DEPLOYING")
+        if existing is not None:
+            sa.created_at = existing.created_at
+        self.store.put(sa)
+        self._start(sa, plan)
+        return self.describe(tenant, app_id)
+
+    def _start(self, sa: StoredApplication, plan) -> None:
+        cc = sa.application.instance.compute_cluster.type if sa.application.instance and \
+            sa.application.instance.compute_cluster else "local"
+        if cc == "kubernetes":
+            from ..core.k8s import render_manifests
+            sa.manifests = render_manifests(plan, sa.tenant, sa.code_archive_id)
+            sa.status = "DEPLOYED"
+            self.store.put(sa)
+            return
+        from ..runtime.local import LocalApplicationRunner
+        code = os.path.join(self.code_dir, sa.code_archive_id) if sa.code_archive_id else ""
+        runner = LocalApplicationRunner(sa.application, application_id=sa.application_id, tenant=sa.tenant,
+                                        code_directory=code, services=self.services)
+        buf = _AppLogBuffer()
+        buf.setFormatter(logging.Formatter("%(name)s %(message)s"))
+        logging.getLogger().addHandler(buf)
+        self._logs[(sa.tenant, sa.application_id)] = buf
+        try:
+            runner.start(wait=30)
+            buf.threads = {f"agent-{n.id}" for n in plan.agents.values()}
+            sa.runner = runner
+            sa.status = "DEPLOYED"
+        except Exception as e:  # noqa: BLE001
+            log.exception("deploy failed")
+            sa.status = "ERROR_DEPLOYING"
+            sa.error = str(e)
+        self.store.put(sa)
+
+    def delete(self, tenant: str, app_id: str, force: bool = False) -> None:
+        sa = self.store.get(tenant, app_id)
+        if sa is None:
+            raise KeyError(f"application {app_id} not found")
+        if sa.runner is not None:
+            sa.runner.stop(10)
+            try:
+                from ..core.deployer import ApplicationDeployer
+                ApplicationDeployer().cleanup(tenant, sa.runner.plan)
+            except Exception:  # noqa: BLE001
+                if not force:
+                    log.warning("cleanup of %s failed", app_id)
+        buf = self._logs.pop((tenant, app_id), None)
+        if buf is not None:
+            logging.getLogger().removeHandler(buf)
+        self.store.delete(tenant, app_id)
+
+    def describe(self, tenant: str, app_id: str, stats: bool = False) -> Dict[str, Any]:
+        sa = self.store.get(tenant, app_id)
+        if sa is None:
+            raise KeyError(f"application {app_id} not found")
+        from ..core.deployer import ApplicationDeployer
+        plan = ApplicationDeployer().create_implementation(app_id, sa.application)
+        out = sa.summary()
+        out["application"] = plan.to_dict()
+        out["status"]["status"]["reason"] = getattr(sa, "error", None)
+        agents = {}
+        if sa.runner is not None and stats:
+            agents = sa.runner.agent_info()
+        out["status"]["agents"] = agents
+        if getattr(sa, "manifests", None):
+            out["manifests"] = sa.manifests
+        return out
+
+    def logs(self, tenant: str, app_id: str):
+        return self._logs.get((tenant, app_id))
+
+    # ---------------------------------------------------------------- archetypes
+    def list_archetypes(self) -> List[Dict[str, Any]]:
+        import yaml
+        out = []
+        if not self.archetypes_dir or not os.path.isdir(self.archetypes_dir):
+            return out
+        for d in sorted(os.listdir(self.archetypes_dir)):
+            p = os.path.join(self.archetypes_dir, d, "archetype.yaml")
+            if os.path.exists(p):
+                with open(p) as f:
+                    spec = (yaml.safe_load(f) or {}).get("archetype") or {}
+                out.append({"id": d, "title": spec.get("title"), "labels": spec.get("labels"),
+                            "description": spec.get("description"), "sections": spec.get("sections")})
+        return out
+
+    def deploy_archetype(self, tenant: str, archetype: str, app_id: str, params: Dict[str, Any]) -> Dict[str, Any]:
+        d = os.path.join(self.archetypes_dir or "", archetype)
+        if not os.path.isdir(d):
+            raise KeyError(f"archetype {archetype} not found")
+        info = build_from_archetype(d, params)
+        files = read_app_directory(d)
+        files.pop("archetype.yaml", None)
+        import yaml
+        inst = yaml.safe_dump({"instance": {"globals": dict(info.application.instance.globals)
+                                            if info.application.instance else {}}})
+        sec = yaml.safe_dump({"secrets": [{"id": s.id, "data": s.data}
+                                          for s in (info.application.secrets.secrets.values()
+                                                    if info.application.secrets else [])]})
+        return self.deploy(tenant, app_id, None, inst, sec, files=files)
+
+
+# ---------------------------------------------------------------- HTTP layer
+class WebServiceServer:
+    def __init__(self, cp: ControlPlane, host: str = "127.0.0.1", port: int = 8090,
+                 auth_secret: Optional[str] = None):
+        self.cp = cp
+        self.host, self.port = host, port
+        self.auth_secret = auth_secret
+        self._loop = None
+        self._thread = None
+        self._started = threading.Event()
+
+    def make_app(self):
+        from aiohttp import web
+
+        @web.middleware
+        async def auth_mw(request, handler):
+            if self.auth_secret and request.path.startswith("/api/"):
+                from ..gateway.auth import JwtError, decode_jwt
+                h = request.headers.get("Authorization", "")
+                try:
+                    decode_jwt(h[len("Bearer "):] if h.startswith("Bearer ") else "",
+                               secret=self.auth_secret.encode())
+                except JwtError as e:
+                    raise web.HTTPUnauthorized(text=str(e))
+            try:
+                return await handler(request)
+            except KeyError as e:
+                raise web.HTTPNotFound(text=str(e).strip("'"))
+            except FileExistsError as e:
+                raise web.HTTPConflict(text=str(e))
+            except PermissionError as e:
+                raise web.HTTPForbidden(text=str(e))
+            except ValueError as e:
+                raise web.HTTPBadRequest(text=str(e))
+
+        app = web.Application(middlewares=[auth_mw], client_max_size=256 * 1024 * 1024)
+        r = app.router
+        r.add_get("/api/tenants", self.tenants)
+        r.add_route("*", "/api/tenants/{tenant}", self.tenant)
+        r.add_get("/api/applications/{tenant}", self.list_apps)
+        r.add_route("*", "/api/applications/{tenant}/{id}", self.app)
+        r.add_get("/api/applications/{tenant}/{id}/logs", self.app_logs)
+        r.add_get("/api/applications/{tenant}/{id}/code", self.app_code)
+        r.add_get("/api/applications/{tenant}/{id}/code/info", self.app_code_info)
+        r.add_get("/api/archetypes/{tenant}", self.archetypes)
+        r.add_get("/api/archetypes/{tenant}/{id}", self.archetype)
+        r.add_post("/api/archetypes/{tenant}/{id}/applications/{app}", self.archetype_deploy)
+        r.add_get("/management/health", lambda req: web.json_response({"status": "UP"}))
+        return app
+
+    async def _off(self, fn, *a, **kw):
+        return await asyncio.get_running_loop().run_in_executor(None, lambda: fn(*a, **kw))
+
+    async def tenants(self, request):
+        from aiohttp import web
+        return web.json_response(self.cp.store.list_tenants())
+
+    async def tenant(self, request):
+        from aiohttp import web
+        t = request.match_info["tenant"]
+        if request.method == "GET":
+            v = self.cp.store.get_tenant(t)
+            if v is None:
+                raise KeyError(f"tenant {t} not found")
+            return web.json_response(v)
+        if request.method in ("PUT", "POST"):
+            body = await request.json() if request.can_read_body else {}
+            self.cp.store.put_tenant(t, body or {})
+            return web.json_response(self.cp.store.get_tenant(t))
+        if request.method == "DELETE":
+            if not self.cp.store.delete_tenant(t):
+                raise KeyError(f"tenant {t} not found")
+            return web.json_response({})
+        raise web.HTTPMethodNotAllowed(request.method, ["GET", "PUT", "POST", "DELETE"])
+
+    async def list_apps(self, request):
+        from aiohttp import web
+        return web.json_response([a.summary() for a in self.cp.store.list(request.match_info["tenant"])])
+
+    async def _parts(self, request) -> Dict[str, Any]:
+        out: Dict[str, Any] = {}
+        if not request.content_type.startswith("multipart/"):
+            return out
+        reader = await request.multipart()
+        async for part in reader:
+            data = await part.read()
+            out[part.name] = data if part.name == "app" else data.decode()
+        return out
+
+    async def app(self, request):
+        from aiohttp import web
+        t, i = request.match_info["tenant"], request.match_info["id"]
+        q = request.query
+        if request.method == "GET":
+            return web.json_response(await self._off(self.cp.describe, t, i, q.get("stats") == "true"),
+                                     dumps=lambda o: json.dumps(o, default=str))
+        if request.method in ("POST", "PATCH"):
+            parts = await self._parts(request)
+            res = await self._off(self.cp.deploy, t, i, parts.get("app"), parts.get("instance"),
+                                  parts.get("secrets"), q.get("dry-run") == "true", request.method == "PATCH")
+            return web.json_response(res, dumps=lambda o: json.dumps(o, default=str))
+        if request.method == "DELETE":
+            await self._off(self.cp.delete, t, i, q.get("force") == "true")
+            return web.json_response({})
+        raise web.HTTPMethodNotAllowed(request.method, ["GET", "POST", "PATCH", "DELETE"])
+
+    async def app_logs(self, request):
+        from aiohttp import web
+        t, i = request.match_info["tenant"], request.match_info["id"]
+        if self.cp.store.get(t, i) is None:
+            raise KeyError(f"application {i} not found")
+        buf = self.cp.logs(t, i)
+        resp = web.StreamResponse(headers={"Content-Type": "application/x-ndjson"})
+        await resp.prepare(request)
+        if buf is None:
+            await resp.write_eof()
+            return resp
+        follow = request.query.get("follow", "true") != "false"
+        last = 0
+        loop = asyncio.get_running_loop()
+        while True:
+            with buf.cv:
+                batch = [r for s, r in buf.records if s > last]
+                last = buf.seq
+            for r in batch:
+                await resp.write((json.dumps(r) + "\n").encode())
+            if not follow:
+                break
+            await loop.run_in_executor(None, buf.wait_new, last, 1.0)
+        await resp.write_eof()
+        return resp
+
+    async def app_code(self, request):
+        from aiohttp import web
+        sa = self.cp.store.get(request.match_info["tenant"], request.match_info["id"])
+        if sa is None or not sa.code_archive_id:
+            raise KeyError("code not found")
+        return web.FileResponse(os.path.join(self.cp.code_dir, sa.code_archive_id + ".zip"))
+
+    async def app_code_info(self, request):
+        from aiohttp import web
+        sa = self.cp.store.get(request.match_info["tenant"], request.match_info["id"])
+        if sa is None:
+            raise KeyError("application not found")
+        d = os.path.join(self.cp.code_dir, sa.code_archive_id or "")
+        return web.json_response({"code-archive-id": sa.code_archive_id,
+                                  "python-digest": directory_digest(os.path.join(d, "python")) if sa.code_archive_id
+                                  else None})
+
+    async def archetypes(self, request):
+        from aiohttp import web
+        return web.json_response(self.cp.list_archetypes())
+
+    async def archetype(self, request):
+        from aiohttp import web
+        for a in self.cp.list_archetypes():
+            if a["id"] == request.match_info["id"]:
+                return web.json_response(a)
+        raise KeyError("archetype not found")
+
+    async def archetype_deploy(self, request):
+        from aiohttp import web
+        params = await request.json() if request.can_read_body else {}
+        res = await self._off(self.cp.deploy_archetype, request.match_info["tenant"], request.match_info["id"],
+                              request.match_info["app"], params or {})
+        return web.json_response(res, dumps=lambda o: json.dumps(o, default=str))
+
+    def start(self) -> "WebServiceServer":
+        def run():
+            from aiohttp import web
+            self._loop = asyncio.new_event_loop()
+            asyncio.set_event_loop(self._loop)
+            self._runner = web.AppRunner(self.make_app())
+            self._loop.run_until_complete(self._runner.setup())
+            site = web.TCPSite(self._runner, self.host, self.port)
+            self._loop.run_until_complete(site.start())
+            if self.port == 0:
+                self.port = site._server.sockets[0].getsockname()[1]
+            self._started.set()
+            self._loop.run_forever()
+
+        self._thread = threading.Thread(target=run, daemon=True, name="webservice")
+        self._thread.start()
+        self._started.wait(30)
+        return self
+
+    def stop(self) -> None:
+        if self._loop is None:
+            return
+        fut = asyncio.run_coroutine_threadsafe(self._runner.cleanup(), self._loop)
+        try:
+            fut.result(10)
+        except Exception:  # noqa: BLE001
+            pass
+        self._loop.call_soon_threadsafe(self._loop.stop)
+        self._thread.join(10)
+
+    @property
+    def url(self) -> str:
+        return f"http://{self.host}:{self.port}"
