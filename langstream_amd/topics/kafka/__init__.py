@@ -1,0 +1,206 @@
+"""Kafka streaming runtime on the in-tree protocol client.
+
+Parity:
+* planner/runtime config (``KafkaStreamingClusterRuntime.java:41-88``,
+  ``KafkaTopic.java:62-138``): topics get ``partitions`` (default 1) and the
+  ``replication-factor`` option (default 1); consumers use
+  ``group.id = langstream-agent-<agentId>`` (shared by every replica -> consumer-group
+  data parallelism) and ``auto.offset.reset = earliest``; ``consumer.*`` / ``producer.*``
+  / ``admin`` configuration pass through; ``bootstrap.servers`` from the streaming
+  cluster's ``admin`` block (or top-level).
+* consumer (``KafkaConsumerWrapper.java``): poll -> records; out-of-order commit
+  tracking advancing only the contiguous prefix per partition; a failed commit is
+  raised by the next read().
+* producer (``KafkaProducerWrapper.java:58-270``): key/value/header serialisation by
+  Python type -- str -> UTF-8, bytes as is, dict/list -> JSON, bool/int/float -> their
+  string form; the consumer deserialises UTF-8 back to str (bytes when not UTF-8).
+* reader (``KafkaReaderWrapper.java``): assign-all, latest / earliest / absolute
+  (``{partition: offset}`` JSON, base64 in the gateway API).
+* admin (``KafkaTopicConnectionsRuntime.java:166-291``): create-if-not-exists topics
+  on deploy, delete topics with deletion-mode ``delete``.
+"""
+from __future__ import annotations
+
+import json
+import logging
+import threading
+import time
+from concurrent.futures import Future
+from typing import Any, Dict, List, Optional
+
+from ...api.record import Header, Record
+from ...api.topics import (TopicAdmin, TopicConnectionsRuntime, TopicConnectionsRuntimeRegistry, TopicConsumer,
+                           TopicOffsetPosition, TopicProducer, TopicReader, TopicReadResult, decode_offsets,
+                           encode_offsets)
+from .client import GroupConsumer, KafkaClient, PartitionReader, Producer
+
+log = logging.getLogger(__name__)
+
+
+def serialize(v: Any) -> Optional[bytes]:
+    if v is None:
+        return None
+    if isinstance(v, bytes):
+        return v
+    if isinstance(v, str):
+        return v.encode()
+    if isinstance(v, bool):
+        return b"true" if v else b"false"
+    if isinstance(v, (dict, list)):
+        return json.dumps(v).encode()
+    return str(v).encode()
+
+
+def deserialize(b: Optional[bytes]) -> Any:
+    if b is None:
+        return None
+    try:
+        return b.decode()
+    except UnicodeDecodeError:
+        return b
+
+
+class KafkaRecord(Record):
+    __slots__ = ("topic", "partition", "offset")
+
+    def __init__(self, topic: str, partition: int, offset: int, ts: int, key, value, headers):
+        super().__init__(deserialize(key), deserialize(value), topic, ts,
+                         [Header(k, deserialize(v)) for k, v in headers])
+        self.topic, self.partition, self.offset = topic, partition, offset
+
+
+def _bootstrap(streaming_cluster) -> str:
+    cfg = (streaming_cluster.configuration if streaming_cluster is not None else {}) or {}
+    admin = cfg.get("admin") or {}
+    bs = admin.get("bootstrap.servers") or cfg.get("bootstrap.servers") or cfg.get("bootstrapServers")
+    if not bs:
+        raise ValueError("kafka streaming cluster needs admin.bootstrap.servers")
+    return str(bs)
+
+
+class KafkaConsumer(TopicConsumer):
+    def __init__(self, bootstrap: str, topic: str, group: str, reset: str, max_records: int, poll_ms: int):
+        self.client = KafkaClient(bootstrap, client_id=f"consumer-{group}")
+        self.c = GroupConsumer(self.client, topic, group, reset, max_poll_records=max_records)
+        self.topic, self.group, self.poll_ms = topic, group, poll_ms
+        self._out = 0
+
+    def start(self) -> None:
+        self.c.start()
+
+    def close(self) -> None:
+        self.c.close()
+        self.client.close()
+
+    def read(self) -> List[Record]:
+        recs = self.c.poll(self.poll_ms)
+        out = [KafkaRecord(self.topic, p, off, ts, k, v, hs) for p, off, ts, k, v, hs in recs]
+        self._out += len(out)
+        return out
+
+    def commit(self, records: List[Record]) -> None:
+        self.c.commit([(r.partition, r.offset) for r in records if isinstance(r, KafkaRecord)])
+
+    def get_info(self) -> Dict[str, Any]:
+        return {"topic": self.topic, "group": self.group, "member": self.c.member_id,
+                "assignment": self.c.assigned, "committed": self.c.committed()}
+
+    def get_total_out(self) -> int:
+        return self._out
+
+
+class KafkaProducer(TopicProducer):
+    def __init__(self, bootstrap: str, topic: str):
+        self.client = KafkaClient(bootstrap, client_id=f"producer-{topic}")
+        self.p = Producer(self.client, topic)
+        self.topic = topic
+        self._in = 0
+        self._lock = threading.Lock()
+
+    def close(self) -> None:
+        self.client.close()
+
+    def write(self, record: Record) -> Future:
+        f: Future = Future()
+        try:
+            hs = [(h.key, serialize(h.value)) for h in record.headers()]
+            with self._lock:
+                self.p.send(serialize(record.key()), serialize(record.value()), hs,
+                            int(record.timestamp() or time.time() * 1000))
+            self._in += 1
+            f.set_result(None)
+        except Exception as e:  # noqa: BLE001
+            f.set_exception(e)
+        return f
+
+    def get_total_in(self) -> int:
+        return self._in
+
+    def get_info(self) -> Dict[str, Any]:
+        return {"topic": self.topic}
+
+
+class KafkaReader(TopicReader):
+    def __init__(self, bootstrap: str, topic: str, position: TopicOffsetPosition, poll_ms: int = 500):
+        self.client = KafkaClient(bootstrap, client_id=f"reader-{topic}")
+        self.topic, self.position, self.poll_ms = topic, position, poll_ms
+        self.r: Optional[PartitionReader] = None
+
+    def start(self) -> None:
+        if self.position.position == "absolute":
+            self.r = PartitionReader(self.client, self.topic, offsets=decode_offsets(self.position.offset))
+        else:
+            self.r = PartitionReader(self.client, self.topic, start=self.position.position)
+
+    def close(self) -> None:
+        self.client.close()
+
+    def read(self) -> TopicReadResult:
+        recs = self.r.read(self.poll_ms)
+        out = [KafkaRecord(self.topic, p, off, ts, k, v, hs) for p, off, ts, k, v, hs in recs]
+        return TopicReadResult(out, encode_offsets(dict(self.r.positions)))
+
+
+class KafkaTopicConnectionsRuntime(TopicConnectionsRuntime):
+    def init(self, streaming_cluster) -> None:
+        self.sc = streaming_cluster
+        self.bootstrap = _bootstrap(streaming_cluster)
+
+    def deploy(self, plan) -> None:
+        client = KafkaClient(self.bootstrap, client_id="langstream-admin")
+        try:
+            for t in plan.topics.values():
+                if t.creation_mode == "create-if-not-exists":
+                    rf = int((t.options or {}).get("replication-factor", 1))
+                    client.create_topic(t.name, max(1, t.partitions), rf, t.config or {})
+        finally:
+            client.close()
+
+    def delete(self, plan) -> None:
+        client = KafkaClient(self.bootstrap, client_id="langstream-admin")
+        try:
+            for t in plan.topics.values():
+                if t.deletion_mode == "delete":
+                    client.delete_topic(t.name)
+        finally:
+            client.close()
+
+    def create_consumer(self, agent_id, streaming_cluster, configuration) -> TopicConsumer:
+        group = configuration.get("group.id") or f"langstream-agent-{agent_id}"
+        return KafkaConsumer(self.bootstrap, configuration["topic"], group,
+                             str(configuration.get("auto.offset.reset", "earliest")),
+                             int(configuration.get("max.poll.records", 500)),
+                             int(configuration.get("poll.timeout.ms", 500)))
+
+    def create_producer(self, agent_id, streaming_cluster, configuration) -> TopicProducer:
+        return KafkaProducer(self.bootstrap, configuration["topic"])
+
+    def create_reader(self, streaming_cluster, configuration, initial_position) -> TopicReader:
+        return KafkaReader(self.bootstrap, configuration["topic"], initial_position,
+                           int(configuration.get("poll.timeout.ms", 500)))
+
+    def create_topic_admin(self, agent_id, streaming_cluster, configuration) -> TopicAdmin:
+        return TopicAdmin()
+
+
+TopicConnectionsRuntimeRegistry.register("kafka", KafkaTopicConnectionsRuntime)

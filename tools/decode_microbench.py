@@ -36,7 +36,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--ctx", type=int, default=512)
+    ap.add_argument("--blas", default="", help="'rocblas' or 'hipblaslt' (torch preferred BLAS library)")
     a = ap.parse_args()
+    if a.blas:
+        torch.backends.cuda.preferred_blas_library(a.blas)
     B, ctx = a.batch, a.ctx
     H, Fi, Hq, Hkv, D, L = 4096, 14336, 32, 8, 128, 32
     dev = "cuda"
