@@ -1,20 +1,25 @@
-"""Headline benchmark: RAG query pipeline, Llama-3-8B, records/sec (whole node) + p50 e2e latency.
+"""Headline benchmark: full RAG pipeline, Llama-3-8B, records/sec (whole node) + p50 e2e latency.
 
-BASELINE.json config 4 ("full RAG pipeline ... Llama-3-8B, 8 agent replicas DP on
-8xMI355X"), query side, run through the framework itself (YAML app -> planner ->
-fused composite agent -> AgentRunner on memory topics):
+BASELINE.json config 4 ("full RAG pipeline (crawl->split->embed->vector-write;
+query->vector-query->chat) Llama-3-8B, 8 agent replicas DP on 8xMI355X"), run through
+the framework itself (YAML app -> planner -> fused composite agents -> AgentRunner on
+memory topics), both pipelines concurrently in every timed step:
 
-  questions -> document-to-json -> compute-ai-embeddings (bge-small-en, GPU)
-            -> query-vector-db (HBM vector store, GPU kNN top-20)
-            -> re-rank (MMR, top-5) -> ai-chat-completions (Llama-3-8B, GPU,
-               streamed to answers-topic) -> drop-fields -> log-topic
+  ingest: documents -> text-splitter (cl100k length) -> document-to-json
+          -> compute-ai-embeddings (bge-small-en, GPU) -> vector-db-sink (HBM store)
+  query:  questions -> document-to-json -> compute-ai-embeddings (GPU)
+          -> query-vector-db (GPU kNN top-20) -> re-rank (MMR, top-5)
+          -> ai-chat-completions (Llama-3-8B, GPU, streamed to answers-topic)
+          -> drop-fields -> log-topic
 
 One process per GPU (torchrun), each an independent agent replica (data parallel,
-weak scaling: a fixed batch of questions per GPU per step).  Before timing, each rank
-ingests a synthetic corpus through the GPU encoder into its vector store (untimed).
-A step = produce B questions, wait for all B final records; time K steps after W
-warmup steps; value = total records/s over all ranks (max time over ranks).
-Weights are random-init (no checkpoints offline); data is synthetic.
+weak scaling: a fixed batch per GPU per step).  Before timing, each rank loads a
+synthetic corpus through the GPU encoder into its vector store (untimed).  A step =
+produce B questions + D documents (the crawled pages), wait for all B answers and for
+every chunk of the D documents to be indexed; time K steps after W warmup steps.
+value = answered questions per second over all ranks (max time over ranks); the
+ingest rate is reported alongside.  Weights are random-init (no checkpoints offline);
+data is synthetic.
 """
 from __future__ import annotations
 
@@ -107,6 +112,46 @@ pipeline:
         - "related_documents"
 """
 
+INGEST = """
+topics:
+  - name: "documents-topic"
+    creation-mode: create-if-not-exists
+    partitions: 2
+pipeline:
+  - name: "split"
+    type: "text-splitter"
+    input: "documents-topic"
+    configuration:
+      chunk_size: 256
+      chunk_overlap: 32
+      length_function: "cl100k_base"
+  - name: "to-json"
+    type: "document-to-json"
+    configuration:
+      text-field: "text"
+  - name: "embed-chunks"
+    type: "compute-ai-embeddings"
+    configuration:
+      model: "{embed_model}"
+      embeddings-field: "value.embeddings"
+      text: "{{{{ value.text }}}}"
+      batch-size: 64
+      concurrency: 4
+      flush-interval: 5
+  - name: "write"
+    type: "vector-db-sink"
+    configuration:
+      datasource: "LocalVectors"
+      collection-name: "documents"
+      fields:
+        - name: "id"
+          expression: "fn:concat(key, '-', properties.chunk_id)"
+        - name: "vector"
+          expression: "value.embeddings"
+        - name: "text"
+          expression: "value.text"
+"""
+
 CONFIGURATION = """
 configuration:
   resources:
@@ -141,6 +186,7 @@ def main():
     ap.add_argument("--batch", type=int, default=256, help="questions per GPU per step")
     ap.add_argument("--max-tokens", type=int, default=128)
     ap.add_argument("--corpus", type=int, default=50000, help="documents in each rank's vector store")
+    ap.add_argument("--docs", type=int, default=32, help="documents ingested per GPU per step (0: query only)")
     ap.add_argument("--chat-model", default="llama-3-8b")
     ap.add_argument("--embed-model", default="bge-small-en")
     ap.add_argument("--device", default=None)
@@ -173,7 +219,8 @@ def main():
         chat_model, embed_model = "llama-tiny", "bert-tiny"  # CPU plumbing mode only
     fmt = dict(chat_model=chat_model, embed_model=embed_model, max_tokens=args.max_tokens,
                max_batch=max(args.batch, 1), max_len=4096, prefill=16384)
-    files = {"pipeline.yaml": APP.format(**fmt), "configuration.yaml": CONFIGURATION.format(**fmt)}
+    files = {"pipeline.yaml": APP.format(**fmt), "ingest.yaml": INGEST.format(**fmt),
+             "configuration.yaml": CONFIGURATION.format(**fmt)}
     services = ServiceRegistry({"device": device})
     ServiceRegistry.set_default(services)
 
@@ -192,16 +239,31 @@ def main():
     runner = LocalApplicationRunner.from_yaml(files, application_id="rag-bench", services=services)
     runner.start()
     prod = runner.producer("questions-topic")
+    doc_prod = runner.producer("documents-topic")
     reader = runner.reader("log-topic")
     setup_s = time.time() - t_setup
 
+    from langstream_amd.agents.text import RecursiveCharacterTextSplitter
     from langstream_amd.api.record import SimpleRecord
+    from langstream_amd.tokenizers import cl100k_counter
+    splitter = RecursiveCharacterTextSplitter(["\n\n", "\n", " ", ""], False, 256, 32, cl100k_counter())
     qwords = corpus
     seq = [0]
+    ingested = {"docs": 0, "chunks": 0}
 
-    def run_step(n):
+    def make_doc(i: int) -> str:  # a crawled page: ~12 paragraphs of corpus sentences
+        return "\n\n".join(" ".join(corpus[(i * 31 + p * 7 + j) % len(corpus)] for j in range(5))
+                           for p in range(12))
+
+    def run_step(n, n_docs):
         sent = {}
         t0 = time.time()
+        base = len(store)
+        expect = 0
+        for d in range(n_docs):
+            text = make_doc(seq[0] * 7 + d)
+            expect += len(splitter.split_text(text))
+            doc_prod.write(SimpleRecord.of(f"doc-{rank}-{seq[0]}-{d}", text))
         for i in range(n):
             k = f"{rank}-{seq[0]}"
             seq[0] += 1
@@ -211,27 +273,29 @@ def main():
         lats = []
         got = 0
         deadline = time.time() + args.timeout
-        while got < n:
+        while got < n or len(store) < base + expect:
             if runner.errors:
                 raise runner.errors[0]
             if time.time() > deadline:
-                raise TimeoutError(f"only {got}/{n} records completed")
+                raise TimeoutError(f"only {got}/{n} records and {len(store) - base}/{expect} chunks completed")
             for r in reader.read().records:
                 t = sent.pop(r.key(), None)
                 if t is not None:
                     got += 1
                     lats.append(time.time() - t)
+        ingested["docs"] += n_docs
+        ingested["chunks"] += expect
         return time.time() - t0, lats
 
     for _ in range(args.warmup):
-        run_step(args.batch)
+        run_step(args.batch, args.docs)
     barrier()
     from langstream_amd.utils import threads as _threads
     cpu0 = _threads.snapshot()
     t0 = time.time()
     all_lats = []
     for _ in range(args.steps):
-        _, lats = run_step(args.batch)
+        _, lats = run_step(args.batch, args.docs)
         all_lats.extend(lats)
     barrier()
     elapsed = time.time() - t0
@@ -253,7 +317,11 @@ def main():
             "dtype": "bf16" if use_gpu else "fp32", "data": "synthetic questions + synthetic corpus, random-init weights",
             "config": {"model": chat_model, "embedding_model": embed_model, "global_batch": args.batch * world,
                        "seq_len": 4096, "max_new_tokens": args.max_tokens, "corpus_docs_per_gpu": args.corpus,
-                       "top_k": 20, "rerank": 5, "parallelism": f"dp{world}"},
+                       "top_k": 20, "rerank": 5, "ingest_docs_per_gpu_per_step": args.docs,
+                       "parallelism": f"dp{world}"},
+            "ingest": {"docs_per_s": round(args.docs * args.steps * world / elapsed, 2),
+                       "chunks_per_s_rank0": round(ingested["chunks"] * args.steps / max(1, args.steps + args.warmup)
+                                                   / elapsed, 2)},
             "setup_s": round(setup_s, 1),
             "engine": dict(llm.stats, exec_ms=dict(zip(("upload", "enqueue", "download", "wait"),
                                                        (round(x, 1) for x in llm.exec.timings())))),

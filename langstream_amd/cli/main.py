@@ -330,6 +330,18 @@ def cmd_python(args) -> int:
     return 2
 
 
+def cmd_broker(args) -> int:
+    from ..topics.kafka.broker import KafkaBroker
+    b = KafkaBroker(args.host, args.port, default_partitions=args.partitions).start()
+    print(f"kafka-protocol broker listening on {b.bootstrap}", flush=True)
+    try:
+        while True:
+            time.sleep(3600)
+    except KeyboardInterrupt:
+        b.stop()
+    return 0
+
+
 def cmd_code_download(args) -> int:
     import io
     import zipfile
@@ -451,6 +463,12 @@ def build_parser() -> argparse.ArgumentParser:
     for c in ("load-pip-requirements", "run-tests"):
         pys.add_parser(c).add_argument("-app", "--app", required=True)
     py.set_defaults(fn=cmd_python)
+
+    bk = sub.add_parser("broker", help="run the in-tree single-node Kafka-protocol broker")
+    bk.add_argument("--host", default="127.0.0.1")
+    bk.add_argument("--port", type=int, default=9092)
+    bk.add_argument("--partitions", type=int, default=1, help="default partitions of auto-created topics")
+    bk.set_defaults(fn=cmd_broker)
 
     cd = sub.add_parser("code-download")
     cd.add_argument("--tenant", default="default")
