@@ -284,7 +284,11 @@ class LlamaModel:
 
     def logits(self, hidden: torch.Tensor) -> torch.Tensor:
         """[N, H] -> f32 [N, V] (vocab-parallel matmul + all-gather under TP)."""
-        lg = F.linear(hidden, self.lm_head).float()
+        if hidden.is_cuda and hidden.dtype != torch.float32:
+            # f32 output from the GEMM itself (same as the native runner's LM head)
+            lg = torch.mm(hidden, self.lm_head.t(), out_dtype=torch.float32)
+        else:
+            lg = F.linear(hidden, self.lm_head).float()
         if self.tp.world > 1:
             lg = self.tp.all_gather_last(lg)
         return lg[:, : self.cfg.vocab_size]

@@ -135,12 +135,13 @@ def rope_and_cache(qkv, pos, cos_sin, slots, k_cache, v_cache, Hq: int, Hkv: int
 
 
 # ---------------------------------------------------------------- attention
-def decode_splits(max_blocks: int, blocks_per_split: int = 8) -> tuple[int, int]:
-    """Split-KV plan for decode: each workgroup covers at most `blocks_per_split` KV
-    blocks (512 keys); the grid is sized for `max_blocks`, and workgroups past a
-    sequence's own context exit at once (the merge reads only the splits that exist),
-    so one captured graph serves every context length."""
-    bps = max(1, blocks_per_split)
+def decode_splits(max_blocks: int, min_blocks_per_split: int = 4) -> tuple[int, int]:
+    """Split-KV plan for decode: (nsplit_max, min_blocks_per_split).  The kernel picks
+    the split count per launch from the batch (no split once B*Hkv workgroups fill the
+    chip; see attention_decode.hip), and each sequence spreads its own context evenly
+    over the splits (at least `min_blocks_per_split` blocks each, one per wave), so one
+    captured graph serves every context length.  The workspace is sized for nsplit_max."""
+    bps = max(1, min_blocks_per_split)
     nsplit = max(1, (max_blocks + bps - 1) // bps)
     return nsplit, bps
 

@@ -16,20 +16,38 @@
 //
 // Grid: (B*Hkv, S splits).  4 waves per workgroup stride over the split's KV blocks
 // and are merged through LDS; with S > 1 a second kernel merges the splits.
+//
+// Split policy (decided per launch, so it is fixed inside a captured HIP graph):
+// S = min(nsplit_max, ceil(TARGET_WG / (B*Hkv))).  At large batch the (seq, kv-head)
+// pairs alone fill the chip, S = 1, and there are no partials and no merge launch; at
+// small batch a long context is cut into S pieces.  Each sequence divides its OWN
+// context evenly over the S splits (bps = max(min_bps, ceil(nblk / S)), computed on
+// the device), so the grid carries no idle workgroups for short sequences.
+//
+// Per wave, all 32 KiB of a block's K and V fragments are issued before its first
+// MFMA (177 VGPRs, 2 waves/SIMD).  Measured on MI355X (tools/attn_bench.py, B=256,
+// ctx=448, scattered blocks): 89.8 us = 5.2 TB/s, vs 114.7 us for the previous
+// fixed-split kernel, 103 us with next-block K prefetch (256 VGPRs, 1 wave/SIMD) and
+// 106 us when squeezed to 125 VGPRs / 4 waves (V loaded after the softmax).
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
 #include "common.h"
 
 namespace {
 
-constexpr int BS = 64;  // tokens per KV block (engine-wide constant)
+constexpr int BS = 64;            // tokens per KV block (engine-wide constant)
+constexpr int TARGET_WG = 1024;   // ~4 workgroups per CU before contexts are split
 constexpr float LOG2E = 1.4426950408889634f;
+
+__device__ __forceinline__ int split_blocks(int nblk, int nsplit, int min_bps) {
+  return max(min_bps, (nblk + nsplit - 1) / nsplit);
+}
 
 template <int D>
 __global__ void __launch_bounds__(256) decode_attn_kernel(
     bf16* __restrict__ out, const bf16* __restrict__ q, int64_t q_stride, const bf16* __restrict__ kc,
     const bf16* __restrict__ vc, const int32_t* __restrict__ block_tables, int max_blocks,
-    const int32_t* __restrict__ ctx_lens, int Hkv, int G, int NB, float scale_log2, int blocks_per_split,
+    const int32_t* __restrict__ ctx_lens, int Hkv, int G, int NB, float scale_log2, int min_bps,
     float* __restrict__ part_o, float* __restrict__ part_ml) {
   constexpr int KS = D / 32;  // k-steps over the head dim
   constexpr int DT = D / 16;  // 16-wide output tiles over the head dim
@@ -43,13 +61,12 @@ __global__ void __launch_bounds__(256) decode_attn_kernel(
   const int i16 = lane & 15, h = lane >> 4;
 
   const int ctx = ctx_lens[b];
-  int nblk = (ctx + BS - 1) / BS;
-  nblk = min(nblk, max_blocks);
-  const int bstart = split * blocks_per_split;
-  const int bend = min(nblk, bstart + blocks_per_split);
+  const int nblk = min((ctx + BS - 1) / BS, max_blocks);
+  const int bps = split_blocks(nblk, nsplit, min_bps);
+  const int bstart = split * bps;
+  const int bend = min(nblk, bstart + bps);
   // splits past this sequence's context exit at once; the merge kernel only reads
-  // the ceil(nblk / blocks_per_split) splits that exist (graph-friendly: the grid is
-  // sized for the longest context the graph may see).
+  // the ceil(nblk / bps) splits that exist.
   if (split > 0 && bstart >= nblk) return;
 
   // Q^T fragments (B operand): lane holds Q[head kvh*G + i16][32ks + 8h .. +7]
@@ -68,23 +85,35 @@ __global__ void __launch_bounds__(256) decode_attn_kernel(
   float m = -1e30f, l = 0.f;
 
   const int32_t* bt = block_tables + (int64_t)b * max_blocks;
+  auto block_of = [&](int bi) { return min(max(bt[bi], 0), NB - 1); };
+  auto load_k = [&](int blk, uint4(&dst)[4][KS]) {
+    const bf16* kb = kc + ((int64_t)blk * Hkv + kvh) * BS * D + 8 * h;
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) {
+      const int key = 32 * (kt >> 1) + 8 * (i16 >> 2) + 4 * (kt & 1) + (i16 & 3);
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) dst[kt][ks] = ld16(kb + key * D + 32 * ks);
+    }
+  };
+
   for (int bi = bstart + wid; bi < bend; bi += 4) {
-    const int blk = min(max(bt[bi], 0), NB - 1);
-    const bf16* kb = kc + ((int64_t)blk * Hkv + kvh) * BS * D;
+    const int blk = block_of(bi);
+    uint4 kf[4][KS];
+    load_k(blk, kf);
     const bf16* vb = vc + ((int64_t)blk * Hkv + kvh) * D * BS;
+    uint4 vf[2][DT];
+#pragma unroll
+    for (int kg = 0; kg < 2; ++kg)
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) vf[kg][dt] = ld16(vb + (16 * dt + i16) * BS + 32 * kg + 8 * h);
     // ---- S^T = K Q^T for the 64 keys of this block (4 tiles of 16 keys)
     f32x4 s[4];
 #pragma unroll
     for (int kt = 0; kt < 4; ++kt) {
-      const int kg = kt >> 1, e = kt & 1;
-      const int key = 32 * kg + 8 * (i16 >> 2) + 4 * e + (i16 & 3);
-      const bf16* kr = kb + key * D + 8 * h;
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {
-        const bf16x8 a = __builtin_bit_cast(bf16x8, ld16(kr + 32 * ks));
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, qf[ks], acc, 0, 0, 0);
-      }
+      for (int ks = 0; ks < KS; ++ks)
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, kf[kt][ks]), qf[ks], acc, 0, 0, 0);
       s[kt] = acc;
     }
     // ---- online softmax (row = qrow = lane&15; this lane holds 16 of the 64 keys)
@@ -131,10 +160,8 @@ __global__ void __launch_bounds__(256) decode_attn_kernel(
         pf[4 + j] = (bf16)s[2 * kg + 1][j];
       }
 #pragma unroll
-      for (int dt = 0; dt < DT; ++dt) {
-        const bf16x8 a = __builtin_bit_cast(bf16x8, ld16(vb + (16 * dt + i16) * BS + 32 * kg + 8 * h));
-        o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, pf, o[dt], 0, 0, 0);
-      }
+      for (int dt = 0; dt < DT; ++dt)
+        o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, vf[kg][dt]), pf, o[dt], 0, 0, 0);
     }
   }
 
@@ -172,7 +199,9 @@ __global__ void __launch_bounds__(256) decode_attn_kernel(
       const float inv = lt > 0.f ? 1.f / lt : 0.f;
       bf16* op = out + ((int64_t)b * Hkv * G + head) * D + dc * CH;
 #pragma unroll
-      for (int c = 0; c < CH; ++c) op[c] = (bf16)(acc[c] * inv);
+      for (int c = 0; c < CH; ++c) acc[c] *= inv;
+#pragma unroll
+      for (int c = 0; c < CH; c += 8) st16(op + c, pack8(acc + c));
     } else {
       const int64_t pi = (((int64_t)b * Hkv * G + head) * nsplit + split);
       float* po = part_o + pi * D + dc * CH;
@@ -189,14 +218,15 @@ __global__ void __launch_bounds__(256) decode_attn_kernel(
 template <int D>
 __global__ void __launch_bounds__(256) decode_merge_kernel(bf16* __restrict__ out, const float* __restrict__ part_o,
                                                            const float* __restrict__ part_ml, int nsplit_grid, int nrows,
-                                                           const int32_t* __restrict__ ctx_lens, int Hq,
-                                                           int blocks_per_split, int max_blocks) {
+                                                           const int32_t* __restrict__ ctx_lens, int Hq, int min_bps,
+                                                           int max_blocks) {
   // one wave per (b, head) row; lanes over d
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= nrows) return;
   const int nblk = min((ctx_lens[row / Hq] + BS - 1) / BS, max_blocks);
-  const int nsplit = max(1, min(nsplit_grid, (nblk + blocks_per_split - 1) / blocks_per_split));
+  const int bps = split_blocks(nblk, nsplit_grid, min_bps);
+  const int nsplit = max(1, min(nsplit_grid, (nblk + bps - 1) / bps));
   const float* ml = part_ml + (int64_t)row * nsplit_grid * 2;
   float mstar = -1e30f;
   for (int s = 0; s < nsplit; ++s) mstar = fmaxf(mstar, ml[2 * s]);
@@ -212,11 +242,19 @@ __global__ void __launch_bounds__(256) decode_merge_kernel(bf16* __restrict__ ou
 
 }  // namespace
 
+// Number of KV splits a decode launch over B sequences uses (<= nsplit_max).
+int64_t decode_nsplit(int64_t B, int64_t Hkv, int64_t nsplit_max) {
+  const int64_t pairs = std::max<int64_t>(1, B * Hkv);
+  return std::max<int64_t>(1, std::min<int64_t>(nsplit_max, (TARGET_WG + pairs - 1) / pairs));
+}
+
 // q: [B, Hq*D] view (row stride q_stride elements), out: [B, Hq, D] contiguous.
-// workspace: f32 tensor with >= B*Hq*nsplit*(D+2) elements when nsplit > 1.
+// nsplit: the MAXIMUM split count (the workspace is sized for it); a launch uses
+// decode_nsplit(B, Hkv, nsplit).  min_bps: the fewest KV blocks one split covers.
+// workspace: f32 tensor with >= B*Hq*S*(D+2) elements when the launch splits (S > 1).
 void paged_decode_attention(at::Tensor out, at::Tensor q, at::Tensor k_cache, at::Tensor v_cache,
                             at::Tensor block_tables, at::Tensor ctx_lens, double scale, int64_t nsplit,
-                            int64_t blocks_per_split, at::Tensor workspace) {
+                            int64_t min_bps, at::Tensor workspace) {
   TORCH_CHECK(q.is_cuda() && q.scalar_type() == at::kBFloat16 && out.scalar_type() == at::kBFloat16);
   TORCH_CHECK(out.is_contiguous() && q.stride(-1) == 1);
   TORCH_CHECK(k_cache.dim() == 4 && v_cache.dim() == 4);
@@ -230,30 +268,32 @@ void paged_decode_attention(at::Tensor out, at::Tensor q, at::Tensor k_cache, at
   TORCH_CHECK(G <= 16, "GQA group too large for the 16-row MFMA tile");
   TORCH_CHECK(block_tables.scalar_type() == at::kInt && block_tables.is_contiguous() && block_tables.size(0) == B);
   TORCH_CHECK(ctx_lens.scalar_type() == at::kInt && ctx_lens.is_contiguous());
-  TORCH_CHECK(nsplit >= 1 && blocks_per_split >= 1);
+  TORCH_CHECK(nsplit >= 1 && min_bps >= 1);
   const int64_t q_stride = q.dim() >= 2 ? q.stride(0) : (int64_t)Hq * D;
   TORCH_CHECK(q_stride % 8 == 0);
   if (B == 0) return;
+  const int64_t ns = decode_nsplit(B, Hkv, nsplit);
   float* po = nullptr;
   float* pml = nullptr;
-  if (nsplit > 1) {
-    TORCH_CHECK(workspace.scalar_type() == at::kFloat && workspace.numel() >= (int64_t)B * Hq * nsplit * (D + 2));
+  if (ns > 1) {
+    TORCH_CHECK(workspace.scalar_type() == at::kFloat && workspace.numel() >= (int64_t)B * Hq * ns * (D + 2),
+                "decode workspace too small");
     po = workspace.data_ptr<float>();
-    pml = po + (int64_t)B * Hq * nsplit * D;
+    pml = po + (int64_t)B * Hq * ns * D;
   }
   auto stream = at::hip::getCurrentHIPStream();
-  dim3 grid(B * Hkv, nsplit);
+  dim3 grid(B * Hkv, ns);
   const float sl2 = (float)scale * LOG2E;
-#define LAUNCH(DD)                                                                                               \
+#define LAUNCH(DD)                                                                                                  \
   decode_attn_kernel<DD><<<grid, 256, 0, stream>>>((bf16*)out.data_ptr(), (const bf16*)q.data_ptr(), q_stride, \
                                                    (const bf16*)k_cache.data_ptr(), (const bf16*)v_cache.data_ptr(), \
                                                    block_tables.data_ptr<int32_t>(), (int)block_tables.size(1),  \
                                                    ctx_lens.data_ptr<int32_t>(), Hkv, G, (int)k_cache.size(0),    \
-                                                   sl2, (int)blocks_per_split, po, pml);                          \
-  if (nsplit > 1)                                                                                                \
-    decode_merge_kernel<DD><<<(B * Hq + 3) / 4, 256, 0, stream>>>((bf16*)out.data_ptr(), po, pml, (int)nsplit,   \
+                                                   sl2, (int)min_bps, po, pml);                                   \
+  if (ns > 1)                                                                                                    \
+    decode_merge_kernel<DD><<<(B * Hq + 3) / 4, 256, 0, stream>>>((bf16*)out.data_ptr(), po, pml, (int)ns,       \
                                                                   B * Hq, ctx_lens.data_ptr<int32_t>(), Hq,       \
-                                                                  (int)blocks_per_split, (int)block_tables.size(1))
+                                                                  (int)min_bps, (int)block_tables.size(1))
   if (D == 128) { LAUNCH(128); }
   else if (D == 64) { LAUNCH(64); }
   else TORCH_CHECK(false, "unsupported head dim ", D);

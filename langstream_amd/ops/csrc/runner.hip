@@ -89,6 +89,20 @@ class LlamaRunner {
     if (!process_group.is_none()) pg_ = py::cast<c10::intrusive_ptr<::c10d::ProcessGroup>>(process_group);
   }
 
+  // LM head with f32 OUTPUT straight from the GEMM (hipBLASLt bf16 x bf16 -> f32): a bf16
+  // logit tensor quantises logits to 2^-7 relative steps (0.125 at |logit| ~ 20), which
+  // ties near-equal tokens and coarsens the log-probs FLARE and `logprobs` consume.
+  at::Tensor lm_head(const at::Tensor& x) {
+    if (f32_head_) {
+      try {
+        return at::mm(x, lm_head_.t(), at::kFloat);
+      } catch (const c10::Error&) {
+        f32_head_ = false;  // this torch build has no bf16->f32 mm: round through bf16
+      }
+    }
+    return at::linear(x, lm_head_).to(at::kFloat);
+  }
+
   // f32 logits [rows or T, vocab]; decode rows are [0, num_decode), prefill rows after.
   at::Tensor forward_impl(const at::Tensor& ids, const at::Tensor& pos, const at::Tensor& slots, int64_t num_decode,
                           const at::Tensor& d_bt, const at::Tensor& d_ctx, int64_t nsplit, int64_t bps,
@@ -123,7 +137,7 @@ class LlamaRunner {
       x = dn;
     }
     at::Tensor sel = rows.has_value() ? x.index_select(0, *rows) : x;
-    at::Tensor lg = at::linear(sel, lm_head_).to(at::kFloat);
+    at::Tensor lg = lm_head(sel);
     if (pg_) {
       const int64_t world = pg_->getSize();
       std::vector<at::Tensor> parts;
@@ -177,6 +191,7 @@ class LlamaRunner {
     pg_->allreduce(v)->wait();
   }
 
+  bool f32_head_ = true;
   at::Tensor embed_;
   std::vector<at::Tensor> qkv_w_, o_w_, gate_up_w_, down_w_, in_norm_, post_norm_;
   at::Tensor final_norm_, lm_head_;

@@ -110,13 +110,31 @@ def test_llama_graph_decode_matches_eager():
 
 
 def test_llama_chunked_prefill_consistent():
+    """Whole vs 100-token-chunked prefill: the prefill's and the first decode step's
+    top-20 distributions agree to bf16 noise.  (Greedy token equality is not asserted:
+    random-init logits have top-2 gaps of 1e-3 nats, so argmax flips on rounding.)"""
     cfg = PRESETS["llama-small"]
     model = LlamaModel(cfg, device="cuda")
     prompt = list(range(10, 10 + 300))
-    sp = SamplingParams(max_tokens=6, temperature=0.0, ignore_eos=True)
-    a = LLMEngine(model, None, num_blocks=64, max_model_len=1024, max_prefill_tokens=4096).generate([prompt], sp)[0]
-    b = LLMEngine(model, None, num_blocks=64, max_model_len=1024, max_prefill_tokens=100).generate([prompt], sp)[0]
-    assert a.output_ids[:3] == b.output_ids[:3]
+
+    def run(chunk):
+        events = []
+        e = LLMEngine(model, None, num_blocks=64, max_model_len=1024, max_prefill_tokens=chunk)
+        r = e.submit(prompt, SamplingParams(max_tokens=2, temperature=0.0, ignore_eos=True, logprobs=20),
+                     callback=events.append)
+        while not r.finished:
+            e.step()
+        e._flush()
+        return events
+
+    ea, eb = run(4096), run(100)
+    for step in range(2):
+        ta, tb = dict(ea[step].top), dict(eb[step].top)
+        common = set(ta) & set(tb)
+        assert len(common) >= 15, (step, ta, tb)
+        assert max(abs(ta[t] - tb[t]) for t in common) < 0.05, (step, ta, tb)
+        if ea[0].token_id != eb[0].token_id:
+            break  # the decode step conditions on different tokens
 
 
 def test_bert_encoder_matches_cpu():

@@ -125,8 +125,8 @@ def _random_paged(B, ctx, Hkv, D, dev, seed=0):
 
 
 @pytest.mark.parametrize("G", [4, 8])
-@pytest.mark.parametrize("nsplit", [1, 3])
-def test_paged_decode_attention(G, nsplit):
+@pytest.mark.parametrize("nsplit,min_bps", [(1, 4), (3, 4), (3, 1), (16, 1)])
+def test_paged_decode_attention(G, nsplit, min_bps):
     Hkv, D = 2, 128
     Hq = Hkv * G
     ctx = [1, 63, 64, 65, 300, 777]
@@ -136,10 +136,8 @@ def test_paged_decode_attention(G, nsplit):
     q = qkv[:, : Hq * D]
     cl = torch.tensor(ctx, dtype=torch.int32, device=DEV)
     scale = 1 / math.sqrt(D)
-    maxb = bt.shape[1]
-    bps = (maxb + nsplit - 1) // nsplit
     ws = torch.empty(B * Hq * nsplit * (D + 2), device=DEV, dtype=torch.float32)
-    got = ops.paged_decode_attention(q, kc, vc, bt, cl, scale, nsplit=nsplit, blocks_per_split=bps, workspace=ws)
+    got = ops.paged_decode_attention(q, kc, vc, bt, cl, scale, nsplit=nsplit, blocks_per_split=min_bps, workspace=ws)
     exp = ref.paged_decode_attention(q.cpu().reshape(B, Hq, D), kc.cpu(), vc.cpu(), bt.cpu(), cl.cpu(), scale)
     _close(got, exp.reshape(B, Hq * D), 0.03, 0.03)
 

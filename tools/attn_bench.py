@@ -1,0 +1,69 @@
+"""Decode-attention timing over (batch, context) shapes + a correctness spot check.
+
+usage (GPU box): python tools/attn_bench.py [--shapes 256x448,64x2048,8x4000]
+
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from langstream_amd import ops  # noqa: E402
+from langstream_amd.ops import reference as ref  # noqa: E402
+
+
+def timeit(fn, iters=50):
+    for _ in range(5):
+        fn()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) * 1000.0 / iters
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--shapes", default="256x448,256x1024,64x2048,16x4096,4x4096,1x4096")
+    a = ap.parse_args()
+    Hq, Hkv, D = 32, 8, 128
+    dev, bf = "cuda", torch.bfloat16
+    nsplit, mbps = ops.decode_splits(64)
+    for shp in a.shapes.split(","):
+        B, ctx = (int(x) for x in shp.split("x"))
+        nb = (ctx + 63) // 64
+        # blocks scattered over a pool 2x the live size (like a busy engine)
+        pool = 2 * B * nb
+        g = torch.Generator(device="cpu").manual_seed(0)
+        perm = torch.randperm(pool, generator=g)[: B * nb].to(torch.int32)
+        bt = perm.view(B, nb).to(dev)
+        kc = torch.randn(pool, Hkv, 64, D, device=dev, dtype=bf)
+        vc = torch.randn(pool, Hkv, D, 64, device=dev, dtype=bf)
+        cl = torch.full((B,), ctx, device=dev, dtype=torch.int32)
+        q = torch.randn(B, Hq * D, device=dev, dtype=bf)
+        ws = torch.empty(B * Hq * nsplit * (D + 2), device=dev, dtype=torch.float32)
+        o = torch.empty(B, Hq * D, device=dev, dtype=bf)
+        scale = 1 / math.sqrt(D)
+        us = timeit(lambda: ops.hip().paged_decode_attention(o, q, kc, vc, bt, cl, scale, nsplit, mbps, ws))
+        byts = B * ctx * Hkv * D * 2 * 2
+        rec = {"B": B, "ctx": ctx, "us": round(us, 2), "TBps": round(byts / us / 1e6, 2),
+               "kernel": "decode_attn_kernel"}
+        if B <= 16:
+            exp = ref.paged_decode_attention(q.float().cpu().reshape(B, Hq, D), kc.float().cpu(), vc.float().cpu(),
+                                             bt.cpu(), cl.cpu(), scale).reshape(B, Hq * D)
+            rec["max_err"] = round(float((o.float().cpu() - exp).abs().max()), 4)
+        print(json.dumps(rec), flush=True)
+
+
+if __name__ == "__main__":
+    main()
