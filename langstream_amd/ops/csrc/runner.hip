@@ -61,6 +61,10 @@ void sample_tokens(at::Tensor logits, at::Tensor temperature, at::Tensor top_k, 
                    at::Tensor steps, at::Tensor out_tok, at::Tensor out_lp, at::Tensor top_ids, at::Tensor top_lps,
                    int64_t n_top);
 
+void skinny_gemm(at::Tensor out, at::Tensor x, at::Tensor w);
+void skinny_gemm_add_rmsnorm(at::Tensor out, at::Tensor x, at::Tensor w, at::Tensor residual, at::Tensor norm_w,
+                             double eps);
+
 #define HIP_OK(x)                                                                  \
   do {                                                                             \
     hipError_t e_ = (x);                                                           \
@@ -115,8 +119,20 @@ class LlamaRunner {
     at::Tensor x = at::empty_like(h);
     rmsnorm(x, h, in_norm_[0], eps_);
     const int64_t L = qkv_w_.size();
+    // Decode-sized steps use the hand-written skinny MFMA GEMM (ops/csrc/gemm_skinny.hip)
+    // where it measured faster than hipBLASLt on MI355X (profiles/skinny_gemm_v2.log):
+    // qkv at T <= 32, o_proj at T <= 192 and down_proj at 48 <= T <= 256, the last two
+    // with the residual add + RMSNorm fused into the split-K reduction (TP=1 only: under
+    // TP the all-reduce sits between the GEMM and the residual add).
+    const bool sk = skinny_enabled() && !pg_;
     for (int64_t l = 0; l < L; ++l) {
-      at::Tensor qkv = at::linear(x, qkv_w_[l]);
+      at::Tensor qkv;
+      if (sk && T <= 32 && skinny_shape(qkv_w_[l])) {
+        qkv = at::empty({T, qkv_w_[l].size(0)}, x.options());
+        skinny_gemm(qkv, x, qkv_w_[l]);
+      } else {
+        qkv = at::linear(x, qkv_w_[l]);
+      }
       rope_and_cache(qkv, pos, cos_sin_, slots, kc_[l], vc_[l], hq_, hkv_, true);
       at::Tensor q = qkv.narrow(1, 0, hq_ * d_);
       at::Tensor attn = at::empty({T, hq_ * d_}, qkv.options());
@@ -125,15 +141,28 @@ class LlamaRunner {
                                d_ctx, scale_, nsplit, bps, ws);
       if (num_prefill > 0)
         paged_prefill_attention(attn, q, kc_[l], vc_[l], p_bt, q_start, q_len, ctx_len, tiles, hq_, scale_);
-      at::Tensor o = at::linear(attn, o_w_[l]);
-      all_reduce(o);
-      fused_add_rmsnorm(o, residual, post_norm_[l], eps_);
+      at::Tensor o;
+      if (sk && T <= 192 && skinny_shape(o_w_[l])) {
+        o = at::empty_like(residual);
+        skinny_gemm_add_rmsnorm(o, attn, o_w_[l], residual, post_norm_[l], eps_);
+      } else {
+        o = at::linear(attn, o_w_[l]);
+        all_reduce(o);
+        fused_add_rmsnorm(o, residual, post_norm_[l], eps_);
+      }
       at::Tensor gu = at::linear(o, gate_up_w_[l]);
       at::Tensor a = at::empty({T, gu.size(1) / 2}, gu.options());
       silu_and_mul(a, gu);
-      at::Tensor dn = at::linear(a, down_w_[l]);
-      all_reduce(dn);
-      fused_add_rmsnorm(dn, residual, l + 1 < L ? in_norm_[l + 1] : final_norm_, eps_);
+      const at::Tensor& nxt = l + 1 < L ? in_norm_[l + 1] : final_norm_;
+      at::Tensor dn;
+      if (sk && T >= 48 && T <= 256 && skinny_shape(down_w_[l])) {
+        dn = at::empty_like(residual);
+        skinny_gemm_add_rmsnorm(dn, a, down_w_[l], residual, nxt, eps_);
+      } else {
+        dn = at::linear(a, down_w_[l]);
+        all_reduce(dn);
+        fused_add_rmsnorm(dn, residual, nxt, eps_);
+      }
       x = dn;
     }
     at::Tensor sel = rows.has_value() ? x.index_select(0, *rows) : x;
@@ -184,6 +213,15 @@ class LlamaRunner {
     all_reduce(h);
     return h;
   }
+
+  static bool skinny_enabled() {
+    static const bool on = [] {
+      const char* e = getenv("LS_SKINNY_GEMM");
+      return e == nullptr || e[0] != '0';
+    }();
+    return on;
+  }
+  static bool skinny_shape(const at::Tensor& w) { return w.size(0) % 128 == 0 && w.size(1) % 64 == 0; }
 
   void all_reduce(at::Tensor& t) {
     if (!pg_) return;

@@ -279,3 +279,44 @@ def test_knn_topk(N, Qn, k):
                 assert abs(sc - s[q, j].item()) < 2e-3
             else:
                 assert not valid[q, j]
+
+
+@pytest.mark.parametrize("M", [1, 37, 64, 256])
+@pytest.mark.parametrize("N,K", [(384, 512), (1024, 4096)])
+def test_skinny_gemm(M, N, K):
+    torch.manual_seed(M + N)
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=DEV) * 0.05).to(torch.bfloat16)
+    out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    ops.hip().skinny_gemm(out, x, w)
+    exp = x.float().cpu() @ w.float().cpu().t()
+    _close(out, exp, 0.03, 0.03)
+
+
+@pytest.mark.parametrize("M", [3, 64, 200])
+def test_skinny_gemm_silu(M):
+    K, F = 512, 320
+    torch.manual_seed(M)
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(2 * F, K, device=DEV) * 0.05).to(torch.bfloat16)
+    out = torch.empty(M, F, device=DEV, dtype=torch.bfloat16)
+    ops.hip().skinny_gemm_silu(out, x, w)
+    gu = x.float().cpu() @ w.float().cpu().t()
+    exp = torch.nn.functional.silu(gu[:, :F]) * gu[:, F:]
+    _close(out, exp, 0.03, 0.03)
+
+
+@pytest.mark.parametrize("M", [5, 128])
+def test_skinny_gemm_add_rmsnorm(M):
+    K, N = 1024, 512
+    torch.manual_seed(M)
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=DEV) * 0.05).to(torch.bfloat16)
+    res = torch.randn(M, N, device=DEV).to(torch.bfloat16)
+    g = (1 + 0.1 * torch.randn(N, device=DEV)).to(torch.bfloat16)
+    res_exp = res.float().cpu() + x.float().cpu() @ w.float().cpu().t()
+    out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    ops.hip().skinny_gemm_add_rmsnorm(out, x, w, res, g, 1e-5)
+    _close(res, res_exp, 0.03, 0.03)
+    exp = res_exp * torch.rsqrt(res_exp.pow(2).mean(-1, keepdim=True) + 1e-5) * g.float().cpu()
+    _close(out, exp, 0.05, 0.05)
