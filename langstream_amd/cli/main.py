@@ -342,6 +342,11 @@ def cmd_broker(args) -> int:
     return 0
 
 
+def cmd_pulsar_standalone(args) -> int:
+    from ..topics.pulsar.standalone import main as pulsar_main
+    return pulsar_main(["--host", args.host, "--port", str(args.port)])
+
+
 def cmd_code_download(args) -> int:
     import io
     import zipfile
@@ -469,6 +474,12 @@ def build_parser() -> argparse.ArgumentParser:
     bk.add_argument("--port", type=int, default=9092)
     bk.add_argument("--partitions", type=int, default=1, help="default partitions of auto-created topics")
     bk.set_defaults(fn=cmd_broker)
+
+    ps = sub.add_parser("pulsar-standalone",
+                        help="run the in-tree Pulsar-compatible broker (WebSocket API + admin REST)")
+    ps.add_argument("--host", default="127.0.0.1")
+    ps.add_argument("--port", type=int, default=8080)
+    ps.set_defaults(fn=cmd_pulsar_standalone)
 
     cd = sub.add_parser("code-download")
     cd.add_argument("--tenant", default="default")

@@ -1,11 +1,11 @@
 """Streaming adapters.  Importing this package registers the built-in
-TopicConnectionsRuntime implementations (memory, noop, kafka, broker)."""
+TopicConnectionsRuntime implementations (memory, noop, kafka, pulsar)."""
 from . import memory  # noqa: F401
 try:  # optional adapters register themselves when importable
     from . import kafka  # noqa: F401
 except ImportError:  # pragma: no cover
     pass
 try:
-    from . import broker  # noqa: F401
+    from . import pulsar  # noqa: F401
 except ImportError:  # pragma: no cover
     pass
