@@ -127,6 +127,11 @@ class _JdbcWriter:
                 VectorStoreRegistry.get(name).delete(rowids)
 
 
+def _remote_writers():
+    from .remote import WRITERS
+    return WRITERS
+
+
 @register_agent("vector-db-sink")
 class VectorDBSinkAgent(AgentSink):
     def init(self, configuration: Dict[str, Any]) -> None:
@@ -137,6 +142,8 @@ class VectorDBSinkAgent(AgentSink):
             self.writer = _LocalWriter(self.cfg)
         elif svc in ("jdbc", "sqlite"):
             self.writer = _JdbcWriter(self.cfg)
+        elif svc in _remote_writers():
+            self.writer = _remote_writers()[svc](self.cfg)
         else:
             from .datasources import UnavailableDataSource
             self.writer = None
@@ -150,7 +157,12 @@ class VectorDBSinkAgent(AgentSink):
             except Exception as e:  # noqa: BLE001
                 return failed(e)
         try:
-            self.writer.upsert(MutableRecord.from_record(record))
-            return completed(None)
+            res = self.writer.upsert(MutableRecord.from_record(record))
+            return res if isinstance(res, Future) else completed(None)
         except Exception as e:  # noqa: BLE001
             return failed(e)
+
+    def close(self) -> None:
+        close = getattr(self.writer, "close", None)
+        if close is not None:
+            close()

@@ -278,4 +278,7 @@ def datasource_for(cfg: Optional[Dict[str, Any]]) -> DataSource:
         return LocalVectorDataSource(cfg)
     if svc in ("jdbc", "sqlite"):
         return SqliteDataSource.shared(cfg)
+    from .remote import DATASOURCES
+    if svc in DATASOURCES:
+        return DATASOURCES[svc](cfg)
     return UnavailableDataSource(svc)
