@@ -126,8 +126,10 @@ class MutableRecord:
         elif field == "messageKey":
             self.message_key = str(content)
         elif field.startswith("properties."):
+            # header values are strings; booleans render like Java's Boolean.toString
             self.properties[field[len("properties."):]] = content if isinstance(content, str) else (
-                json.dumps(content) if isinstance(content, (dict, list)) else str(content))
+                json.dumps(content) if isinstance(content, (dict, list)) else
+                ("true" if content else "false") if isinstance(content, bool) else str(content))
         elif field.startswith("value."):
             name = field[len("value."):]
             if not isinstance(self.value, dict):
