@@ -223,6 +223,162 @@ __global__ void __launch_bounds__(256) splitk_add_rmsnorm_kernel(const float* __
   }
 }
 
+// ---------------------------------------------------------------------------------
+// LDS-DMA pipelined variant.  The register-staged kernel above keeps ONE K-step of W in
+// flight per CU (16 KB): by Little's law at ~1.5 us loaded HBM latency that streams
+// ~10 GB/s per CU, well under the ~24 GB/s a CU can pull (MI355X_MICROARCH 'global_load
+// dwordx4 ~10 B/cyc/CU'), so every M = 256 shape was latency-bound.  Here both tiles go
+// global -> LDS by global_load_lds_dwordx4 (no VGPRs) into an S-deep ring of 32-deep
+// K-stages with S-1 stages in flight (5 x 8 KB of W per CU at BM = 256).
+//   * LDS image: rows of 64 B (32 bf16); one wave-instruction fills 16 rows (1 KiB,
+//     lane-linear), so the bank swizzle goes on the SOURCE address: LDS chunk p of row r
+//     holds global k-chunk p ^ g((r >> 2) & 3) with g = {0, 2, 3, 1}; a fragment read
+//     (lane = 16h + fr reads row fr, chunk h) then puts the 16 lanes of each ds_read_b128
+//     bank group ({0-3,12-15,20-27}, ... MI355X_MICROARCH LDS table) on 16 distinct
+//     16-B bank slots: conflict-free;
+//   * one raw s_barrier per K-step after a counted `s_waitcnt vmcnt((S-2) x pieces)`;
+//     never __syncthreads() in the loop, which would drain every DMA in flight;
+//   * the refill of the buffer read in step kt-1 is issued right after that barrier;
+//     past the last stage it re-loads the last stage into a buffer nobody reads again,
+//     so the wait count stays a compile-time constant.
+constexpr int GBK = 32;
+
+__device__ __forceinline__ int swz_g(int q) { return (0x78 >> (2 * q)) & 3; }
+
+// LDS-DMA through inline asm (cdna_hip_programming.md §5.7): with the builtin, hipcc sees
+// an LDS write and puts `s_waitcnt vmcnt(0)` in front of the next ds_read, which drains
+// the whole ring every K-step; the asm form is invisible to its wait insertion, and the
+// kernel counts these loads itself (wait_vmcnt).
+__device__ __forceinline__ void glds16(const bf16* src, char* lds_wave_base) {
+  const unsigned dst = __builtin_amdgcn_readfirstlane(
+      (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)lds_wave_base);
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(src), "s"(dst)
+      : "memory");
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int BM, int S, int EPI>
+__global__ void __launch_bounds__(BM * 2) skinny_glds_kernel(const bf16* __restrict__ x, int64_t ldx,
+                                                             const bf16* __restrict__ w, int M, int N, int K,
+                                                             int k_per_split, bf16* __restrict__ out, int64_t ldo,
+                                                             float* __restrict__ part, int MT, int silu_F) {
+  constexpr int NW = BM / 32;                 // waves
+  constexpr int XB = BM * GBK * 2, WB = BN * GBK * 2, SB = XB + WB;
+  constexpr int WPW = 8 / NW;                 // 16-row W pieces per wave (X: 2 per wave)
+  constexpr int PER = 2 + WPW;                // LDS-DMA instructions per wave per stage
+  __shared__ __attribute__((aligned(1024))) char lds[S * SB];
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int logical = xcd_remap(blockIdx.x, gridDim.x);
+  const int mt = logical % MT, nt = logical / MT;
+  const int m0 = mt * BM;
+  const int kbeg = blockIdx.y * k_per_split;
+  const int nk = k_per_split / GBK;
+
+  // this lane's source row / swizzled k-chunk inside each 16-row piece
+  const int prow = lane >> 2;
+  const int sck = ((lane & 3) ^ swz_g(lane >> 4)) * 8;
+  const bf16* xs[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int row = 16 * (2 * wid + j) + prow;
+    xs[j] = x + (int64_t)min(m0 + row, M - 1) * ldx + kbeg + sck;   // rows >= M: any valid row, never stored
+  }
+  const bf16* wsrc[WPW];
+#pragma unroll
+  for (int j = 0; j < WPW; ++j) {
+    const int row = 16 * (wid * WPW + j) + prow;
+    int wrow;
+    if (EPI == EPI_SILU) wrow = row < 64 ? nt * 64 + row : silu_F + nt * 64 + (row - 64);
+    else wrow = nt * BN + row;
+    wsrc[j] = w + (int64_t)wrow * K + kbeg + sck;
+  }
+  auto issue = [&](int kt, int buf) {
+    const int ko = kt * GBK;
+    char* base = lds + buf * SB;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) glds16(xs[j] + ko, base + (2 * wid + j) * 1024);
+#pragma unroll
+    for (int j = 0; j < WPW; ++j) glds16(wsrc[j] + ko, base + XB + (wid * WPW + j) * 1024);
+  };
+
+  const int wm = wid >> 1, wn = wid & 1;
+  const int fr = lane & 15, h = lane >> 4;
+  const int swz = 16 * (h ^ swz_g(fr >> 2));   // byte offset of this lane's chunk in a 64-B row
+  auto bcol = [&](int j) {
+    if (EPI == EPI_SILU) return (j < 2 ? 32 * wn + 16 * j : 64 + 32 * wn + 16 * (j - 2)) + fr;
+    return 64 * wn + 16 * j + fr;
+  };
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int s = 0; s < S - 1; ++s) issue(min(s, nk - 1), s);
+  int buf = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    wait_vmcnt<(S - 2) * PER>();          // this wave's DMA of stage kt has landed
+    __builtin_amdgcn_s_barrier();         // ... and every other wave's; step kt-1's reads are done
+    int nb = buf + S - 1;
+    if (nb >= S) nb -= S;
+    issue(min(kt + S - 1, nk - 1), nb);
+    const char* lx = lds + buf * SB;
+    const char* lw = lx + XB;
+    bf16x8 a[4], b[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a[i] = __builtin_bit_cast(bf16x8, ld16(lx + (64 * wm + 16 * i + fr) * 64 + swz));
+#pragma unroll
+    for (int j = 0; j < 4; ++j) b[j] = __builtin_bit_cast(bf16x8, ld16(lw + bcol(j) * 64 + swz));
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    buf = buf + 1 == S ? 0 : buf + 1;
+  }
+  wait_vmcnt<0>();  // no LDS-DMA may outlive the workgroup
+
+  const int rbase = 64 * wm + 4 * (lane >> 4);
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = m0 + rbase + 16 * i + r;
+      if (m >= M) continue;
+      if (EPI == EPI_SILU) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const float g = acc[i][j][r], u = acc[i][j + 2][r];
+          out[(int64_t)m * ldo + nt * 64 + 32 * wn + 16 * j + fr] = (bf16)(g / (1.f + __expf(-g)) * u);
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int n = nt * BN + bcol(j);
+          if (EPI == EPI_STORE) out[(int64_t)m * ldo + n] = (bf16)acc[i][j][r];
+          else part[((int64_t)blockIdx.y * M + m) * N + n] = acc[i][j][r];
+        }
+      }
+    }
+}
+
+bool use_glds() {
+  static const bool on = [] {
+    const char* e = getenv("LS_SKINNY_GLDS");
+    return e == nullptr || e[0] != '0';
+  }();
+  return on;
+}
+
 int pick_bm(int64_t M) { return M <= 64 ? 64 : (M <= 128 ? 128 : 256); }
 
 // split-K so that (M-tiles x N-tiles x S) workgroups cover the CUs: 256-row tiles are
@@ -237,13 +393,19 @@ int pick_splitk(int bm, int tiles, int K) {
 template <int EPI>
 void launch(int bm, dim3 grid, hipStream_t st, const at::Tensor& x, const at::Tensor& w, int M, int N, int K, int kps,
             bf16* out, int64_t ldo, float* part, int MT, int F) {
-#define L(BMV)                                                                                              \
-  skinny_gemm_kernel<BMV, EPI><<<grid, BMV * 2, 0, st>>>((const bf16*)x.data_ptr(), x.stride(0),           \
-                                                         (const bf16*)w.data_ptr(), M, N, K, kps, out, ldo, \
-                                                         part, MT, F)
-  if (bm == 64) L(64);
-  else if (bm == 128) L(128);
-  else L(256);
+#define L(KERNEL, BMV, ...)                                                                                    \
+  KERNEL<BMV, __VA_ARGS__><<<grid, BMV * 2, 0, st>>>((const bf16*)x.data_ptr(), x.stride(0),                  \
+                                                     (const bf16*)w.data_ptr(), M, N, K, kps, out, ldo, part, MT, F)
+  if (use_glds()) {
+    // ring depth by LDS budget: BM=256 -> 6 x 24 KB (1 WG/CU); 128 -> 4 x 16 KB and 64 -> 4 x 12 KB (2-3 WG/CU)
+    if (bm == 64) L(skinny_glds_kernel, 64, 4, EPI);
+    else if (bm == 128) L(skinny_glds_kernel, 128, 4, EPI);
+    else L(skinny_glds_kernel, 256, 6, EPI);
+  } else {
+    if (bm == 64) L(skinny_gemm_kernel, 64, EPI);
+    else if (bm == 128) L(skinny_gemm_kernel, 128, EPI);
+    else L(skinny_gemm_kernel, 256, EPI);
+  }
 #undef L
 }
 
