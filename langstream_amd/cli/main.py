@@ -347,6 +347,16 @@ def cmd_pulsar_standalone(args) -> int:
     return pulsar_main(["--host", args.host, "--port", str(args.port)])
 
 
+def cmd_operator(args) -> int:
+    from ..operator import main as operator_main
+    argv = ["--resync", str(args.resync)]
+    for k in ("api_server", "token", "namespace", "image"):
+        v = getattr(args, k)
+        if v:
+            argv += ["--" + k.replace("_", "-"), v]
+    return operator_main(argv)
+
+
 def cmd_code_download(args) -> int:
     import io
     import zipfile
@@ -480,6 +490,14 @@ def build_parser() -> argparse.ArgumentParser:
     ps.add_argument("--host", default="127.0.0.1")
     ps.add_argument("--port", type=int, default=8080)
     ps.set_defaults(fn=cmd_pulsar_standalone)
+
+    opr = sub.add_parser("operator", help="run the Kubernetes operator (Application / Agent CRs)")
+    opr.add_argument("--api-server", default=None)
+    opr.add_argument("--token", default=None)
+    opr.add_argument("--namespace", default=None)
+    opr.add_argument("--image", default=None)
+    opr.add_argument("--resync", type=float, default=5.0)
+    opr.set_defaults(fn=cmd_operator)
 
     cd = sub.add_parser("code-download")
     cd.add_argument("--tenant", default="default")

@@ -20,6 +20,7 @@ YAML); ``apply_manifests`` shells out to kubectl when it exists.
 from __future__ import annotations
 
 import base64
+import hashlib
 import json
 import shutil
 import subprocess
@@ -66,8 +67,11 @@ def agent_pod_configuration(plan: ExecutionPlan, node: AgentNode, tenant: str) -
     }
 
 
-def render_manifests(plan: ExecutionPlan, tenant: str, code_archive_id: Optional[str] = None,
-                     image: str = DEFAULT_IMAGE, namespace_prefix: str = "langstream-") -> List[Dict[str, Any]]:
+def render_agent_resources(plan: ExecutionPlan, tenant: str, code_archive_id: Optional[str] = None,
+                           image: str = DEFAULT_IMAGE, namespace_prefix: str = "langstream-") -> List[Dict[str, Any]]:
+    """What the deployer job of the reference produces (``KubernetesClusterRuntime.java:93-140``):
+    per plan agent a Secret holding the RuntimePodConfiguration and an ``Agent`` custom
+    resource carrying everything the agent controller needs to build the workload."""
     ns = f"{namespace_prefix}{tenant}"
     out: List[Dict[str, Any]] = []
     app = _name(plan.application_id)
@@ -78,65 +82,101 @@ def render_manifests(plan: ExecutionPlan, tenant: str, code_archive_id: Optional
         tp = int(getattr(node.resources, "tp", 1) or 1)
         secret_name = f"{agent}-config"
         pod_cfg = agent_pod_configuration(plan, node, tenant)
+        cfg_b64 = base64.b64encode(json.dumps(pod_cfg).encode()).decode()
         out.append({"apiVersion": "v1", "kind": "Secret", "metadata": {"name": secret_name, "namespace": ns},
-                    "data": {"app-config": base64.b64encode(json.dumps(pod_cfg).encode()).decode()}})
+                    "data": {"app-config": cfg_b64}})
         out.append({"apiVersion": "langstream.ai/v1alpha1", "kind": "Agent",
                     "metadata": {"name": agent, "namespace": ns, "labels": {"app.kubernetes.io/name": app}},
                     "spec": {"agentId": node.id, "applicationId": plan.application_id, "tenant": tenant,
-                             "agentConfigSecretRef": secret_name, "codeArchiveId": code_archive_id,
-                             "resources": {"parallelism": replicas, "size": size},
+                             "agentConfigSecretRef": secret_name,
+                             "agentConfigSecretRefChecksum": hashlib.sha256(cfg_b64.encode()).hexdigest()[:16],
+                             "codeArchiveId": code_archive_id, "image": image,
+                             "resources": {"parallelism": replicas, "size": size, "tp": tp,
+                                           "gpus": tp if _uses_gpu(node) else 0},
                              "options": {"disks": [{"agentId": k, "size": v.size, "type": v.type}
                                                    for k, v in node.disks.items()]}}})
-        gpus = tp if _uses_gpu(node) else 0
-        limits = {"cpu": f"{size * 0.5:g}", "memory": f"{size * 512}M"}
-        if gpus:
-            limits["amd.com/gpu"] = str(gpus)
-        cmd = ["python", "-m", "langstream_amd.runtime.pod", "/app-config/config"]
-        if tp > 1:
-            cmd = ["torchrun", "--nnodes=1", f"--nproc-per-node={tp}", "--master-addr=127.0.0.1", "-m",
-                   "langstream_amd.runtime.pod", "/app-config/config"]
-        container = {
-            "name": "agent-runtime", "image": image, "command": cmd,
-            "ports": [{"name": "http", "containerPort": 8080}, {"name": "service", "containerPort": 8000}],
-            "env": [{"name": "LANGSTREAM_AGENT_RUNNER_POD_CONFIGURATION", "value": "/app-config/config"},
-                    {"name": "LANGSTREAM_AGENT_RUNNER_CODE_PATH", "value": "/app-code-download"},
-                    {"name": "HSA_ENABLE_IPC_MODE_LEGACY", "value": "0"}],
-            "resources": {"requests": dict(limits), "limits": limits},
-            "livenessProbe": {"httpGet": {"path": "/metrics", "port": 8080}, "initialDelaySeconds": 10,
-                              "periodSeconds": 30, "timeoutSeconds": 5},
-            "readinessProbe": {"httpGet": {"path": "/metrics", "port": 8080}, "initialDelaySeconds": 10,
-                               "periodSeconds": 30, "timeoutSeconds": 5},
-            "volumeMounts": [{"name": "app-config", "mountPath": "/app-config"},
-                             {"name": "code-download", "mountPath": "/app-code-download"}]
-                            + [{"name": _name(f"{k}-disk"), "mountPath": f"/persistent-state/{k}"} for k in node.disks],
-        }
-        init = [{"name": "code-download", "image": image,
-                 "command": ["python", "-m", "langstream_amd.cli", "code-download", "--tenant", tenant,
-                             "--application", plan.application_id, "--code-archive-id", str(code_archive_id),
-                             "--target", "/app-code-download"],
-                 "volumeMounts": [{"name": "code-download", "mountPath": "/app-code-download"}]}]
-        out.append({
-            "apiVersion": "apps/v1", "kind": "StatefulSet",
-            "metadata": {"name": agent, "namespace": ns,
-                         "labels": {"app": agent, "langstream-application": app, "langstream-agent": node.id}},
-            "spec": {"replicas": replicas, "podManagementPolicy": "Parallel", "serviceName": agent,
-                     "selector": {"matchLabels": {"app": agent}},
-                     "template": {"metadata": {"labels": {"app": agent}},
-                                  "spec": {"initContainers": init, "containers": [container],
-                                           "terminationGracePeriodSeconds": 60,
-                                           "volumes": [{"name": "app-config", "secret": {
-                                               "secretName": secret_name,
-                                               "items": [{"key": "app-config", "path": "config"}]}},
-                                               {"name": "code-download", "emptyDir": {}}]}},
-                     "volumeClaimTemplates": [
-                         {"metadata": {"name": _name(f"{k}-disk")},
-                          "spec": {"accessModes": ["ReadWriteOnce"],
-                                   "resources": {"requests": {"storage": v.size or "256M"}},
-                                   **({"storageClassName": v.type} if v.type and v.type != "default" else {})}}
-                         for k, v in node.disks.items()]}})
-        out.append({"apiVersion": "v1", "kind": "Service", "metadata": {"name": agent, "namespace": ns},
-                    "spec": {"clusterIP": "None", "selector": {"app": agent},
-                             "ports": [{"name": "http", "port": 8080}, {"name": "service", "port": 8000}]}})
+    return out
+
+
+def render_agent_workload(agent_cr: Dict[str, Any]) -> List[Dict[str, Any]]:
+    """Agent CR -> StatefulSet + headless Service (``DEPL/agents/AgentResourcesFactory.java:98-586``):
+    replicas = parallelism, parallel pod management, the code-download init container,
+    ``agent-runtime`` on 8080/8000, probes on /metrics, CPU = size x 0.5, memory =
+    size x 512M, one PVC template per agent disk; GPUs as ``amd.com/gpu``."""
+    md, spec = agent_cr["metadata"], agent_cr["spec"]
+    ns, agent = md["namespace"], md["name"]
+    app = _name(spec["applicationId"])
+    res = spec.get("resources") or {}
+    size = int(res.get("size") or 1)
+    replicas = max(1, min(MAX_REPLICAS, int(res.get("parallelism") or 1)))
+    tp, gpus = int(res.get("tp") or 1), int(res.get("gpus") or 0)
+    image = spec.get("image") or DEFAULT_IMAGE
+    secret_name = spec["agentConfigSecretRef"]
+    disks = (spec.get("options") or {}).get("disks") or []
+    limits = {"cpu": f"{size * 0.5:g}", "memory": f"{size * 512}M"}
+    if gpus:
+        limits["amd.com/gpu"] = str(gpus)
+    cmd = ["python", "-m", "langstream_amd.runtime.pod", "/app-config/config"]
+    if tp > 1:
+        cmd = ["torchrun", "--nnodes=1", f"--nproc-per-node={tp}", "--master-addr=127.0.0.1", "-m",
+               "langstream_amd.runtime.pod", "/app-config/config"]
+    container = {
+        "name": "agent-runtime", "image": image, "command": cmd,
+        "ports": [{"name": "http", "containerPort": 8080}, {"name": "service", "containerPort": 8000}],
+        "env": [{"name": "LANGSTREAM_AGENT_RUNNER_POD_CONFIGURATION", "value": "/app-config/config"},
+                {"name": "LANGSTREAM_AGENT_RUNNER_CODE_PATH", "value": "/app-code-download"},
+                {"name": "HSA_ENABLE_IPC_MODE_LEGACY", "value": "0"}],
+        "resources": {"requests": dict(limits), "limits": limits},
+        "livenessProbe": {"httpGet": {"path": "/metrics", "port": 8080}, "initialDelaySeconds": 10,
+                          "periodSeconds": 30, "timeoutSeconds": 5},
+        "readinessProbe": {"httpGet": {"path": "/metrics", "port": 8080}, "initialDelaySeconds": 10,
+                           "periodSeconds": 30, "timeoutSeconds": 5},
+        "volumeMounts": [{"name": "app-config", "mountPath": "/app-config"},
+                         {"name": "code-download", "mountPath": "/app-code-download"}]
+                        + [{"name": _name(f"{d['agentId']}-disk"), "mountPath": f"/persistent-state/{d['agentId']}"}
+                           for d in disks],
+    }
+    init = [{"name": "code-download", "image": image,
+             "command": ["python", "-m", "langstream_amd.cli", "code-download", "--tenant", spec["tenant"],
+                         "--application", spec["applicationId"], "--code-archive-id",
+                         str(spec.get("codeArchiveId")), "--target", "/app-code-download"],
+             "volumeMounts": [{"name": "code-download", "mountPath": "/app-code-download"}]}]
+    sts = {
+        "apiVersion": "apps/v1", "kind": "StatefulSet",
+        "metadata": {"name": agent, "namespace": ns,
+                     "labels": {"app": agent, "langstream-application": app, "langstream-agent": spec["agentId"]}},
+        "spec": {"replicas": replicas, "podManagementPolicy": "Parallel", "serviceName": agent,
+                 "selector": {"matchLabels": {"app": agent}},
+                 "template": {"metadata": {"labels": {"app": agent},
+                                           "annotations": {"langstream.ai/config-checksum":
+                                                           str(spec.get("agentConfigSecretRefChecksum", ""))}},
+                              "spec": {"initContainers": init, "containers": [container],
+                                       "terminationGracePeriodSeconds": 60,
+                                       "volumes": [{"name": "app-config", "secret": {
+                                           "secretName": secret_name,
+                                           "items": [{"key": "app-config", "path": "config"}]}},
+                                           {"name": "code-download", "emptyDir": {}}]}},
+                 "volumeClaimTemplates": [
+                     {"metadata": {"name": _name(f"{d['agentId']}-disk")},
+                      "spec": {"accessModes": ["ReadWriteOnce"],
+                               "resources": {"requests": {"storage": d.get("size") or "256M"}},
+                               **({"storageClassName": d["type"]} if d.get("type") and d["type"] != "default"
+                                  else {})}}
+                     for d in disks]}}
+    svc = {"apiVersion": "v1", "kind": "Service", "metadata": {"name": agent, "namespace": ns},
+           "spec": {"clusterIP": "None", "selector": {"app": agent},
+                    "ports": [{"name": "http", "port": 8080}, {"name": "service", "port": 8000}]}}
+    return [sts, svc]
+
+
+def render_manifests(plan: ExecutionPlan, tenant: str, code_archive_id: Optional[str] = None,
+                     image: str = DEFAULT_IMAGE, namespace_prefix: str = "langstream-") -> List[Dict[str, Any]]:
+    """Everything at once (no operator): Secret + Agent CR + StatefulSet + Service per agent."""
+    out: List[Dict[str, Any]] = []
+    res = render_agent_resources(plan, tenant, code_archive_id, image, namespace_prefix)
+    for i in range(0, len(res), 2):
+        out += res[i: i + 2]
+        out += render_agent_workload(res[i + 1])
     return out
 
 
