@@ -66,6 +66,51 @@ class VectorCollectionManager(AssetManager):
         VectorStoreRegistry.drop(self.cfg["collection-name"])
 
 
+class CassandraTableManager(AssetManager):
+    """``cassandra-table`` / ``cassandra-keyspace`` / ``astra-keyspace`` (reference
+    ``VEC/cassandra/CassandraAssetsManagerProvider.java``): existence from
+    ``system_schema``, ``create-statements`` / ``delete-statements`` run as CQL."""
+
+    def _session(self):
+        from .vector.cql import session_from_datasource
+        ds = dict(self.cfg["datasource"])
+        ds.pop("keyspace", None)
+        return session_from_datasource(ds)
+
+    def asset_exists(self) -> bool:
+        s = self._session()
+        try:
+            if self.asset.asset_type == "cassandra-table":
+                rows = s.execute("SELECT table_name FROM system_schema.tables WHERE keyspace_name = ? AND "
+                                 "table_name = ?", [self.cfg["keyspace"], self.cfg["table-name"]])
+            else:
+                rows = s.execute("SELECT keyspace_name FROM system_schema.keyspaces WHERE keyspace_name = ?",
+                                 [self.cfg["keyspace"]])
+            return bool(rows)
+        finally:
+            s.close()
+
+    def deploy_asset(self) -> None:
+        s = self._session()
+        try:
+            for stmt in self.cfg.get("create-statements") or []:
+                s.execute(stmt)
+        finally:
+            s.close()
+
+    def delete_asset_if_exists(self) -> None:
+        stmts = self.cfg.get("delete-statements")
+        if not stmts:
+            stmts = [f"DROP TABLE IF EXISTS {self.cfg['keyspace']}.{self.cfg['table-name']}"] \
+                if self.asset.asset_type == "cassandra-table" else [f"DROP KEYSPACE IF EXISTS {self.cfg['keyspace']}"]
+        s = self._session()
+        try:
+            for stmt in stmts:
+                s.execute(stmt)
+        finally:
+            s.close()
+
+
 class UnavailableAssetManager(AssetManager):
     def asset_exists(self) -> bool:
         raise RuntimeError(f"asset type {self.asset.asset_type} needs its database client and network access, which "
@@ -76,7 +121,9 @@ class UnavailableAssetManager(AssetManager):
 
 
 class AssetManagerRegistry:
-    _types = {"jdbc-table": JdbcTableManager, "vector-collection": VectorCollectionManager}
+    _types = {"jdbc-table": JdbcTableManager, "vector-collection": VectorCollectionManager,
+              "cassandra-table": CassandraTableManager, "cassandra-keyspace": CassandraTableManager,
+              "astra-keyspace": CassandraTableManager}
 
     @classmethod
     def register(cls, asset_type: str, factory) -> None:
@@ -84,4 +131,8 @@ class AssetManagerRegistry:
 
     @classmethod
     def create(cls, asset) -> AssetManager:
-        return cls._types.get(asset.asset_type, UnavailableAssetManager)(asset)
+        factory = cls._types.get(asset.asset_type)
+        if factory is None:
+            from .vector.remote_assets import MANAGERS
+            factory = MANAGERS.get(asset.asset_type, UnavailableAssetManager)
+        return factory(asset)

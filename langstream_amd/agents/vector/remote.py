@@ -497,3 +497,101 @@ DATASOURCES = {"opensearch": OpenSearchDataSource, "solr": SolrDataSource, "pine
 WRITERS = {"opensearch": OpenSearchWriter, "solr": SolrWriter, "pinecone": PineconeWriter, "milvus": MilvusWriter,
            "astra-vector-db": AstraVectorDBWriter}
 _lock = threading.Lock()
+
+
+# ============================================================== Cassandra / Astra (CQL native protocol)
+class CassandraDataSource(DataSource):
+    """``service: cassandra | astra`` (``AIA/.../datasource/CassandraDataSource.java``): the
+    query is a CQL statement with ``?`` markers bound positionally through PREPARE/EXECUTE;
+    rows come back as maps, vector columns as lists of floats."""
+
+    def __init__(self, cfg: Dict[str, Any]):
+        self.cfg = cfg
+        self._session = None
+        self._lock = threading.Lock()
+
+    @property
+    def session(self):
+        with self._lock:
+            if self._session is None:
+                from .cql import session_from_datasource
+                self._session = session_from_datasource(self.cfg)
+            return self._session
+
+    def fetch_data(self, query: str, params: List[Any]) -> List[Dict[str, Any]]:
+        return self.session.execute(query, params)
+
+    def execute_statement(self, query: str, generated_keys: Sequence[str], params: List[Any]) -> Dict[str, Any]:
+        self.session.execute(query, params)
+        return {}
+
+    def close(self) -> None:
+        if self._session is not None:
+            self._session.close()
+
+
+def parse_cassandra_mapping(mapping: str) -> List[tuple]:
+    """``"col=value.field, col2=key"`` (the DataStax sink mapping) -> [(col, EL expression)]."""
+    out = []
+    for part in (mapping or "").split(","):
+        if not part.strip():
+            continue
+        col, _, expr = part.partition("=")
+        out.append((col.strip(), expr.strip()))
+    return out
+
+
+class CassandraWriter:
+    """``vector-db-sink`` on Cassandra / Astra (``VEC/cassandra/CassandraWriter.java``):
+    ``table``/``table-name`` + ``keyspace`` + ``mapping``; each record is one INSERT of the
+    mapped columns (an upsert in Cassandra); a null record value deletes the row by its
+    primary key (read from ``system_schema.columns``)."""
+
+    def __init__(self, cfg: Dict[str, Any]):
+        self.ds = CassandraDataSource(cfg["datasource"])
+        table = cfg.get("table") or cfg.get("table-name")
+        if not table:
+            raise ValueError("vector-db-sink (cassandra): table-name is required")
+        self.keyspace = cfg.get("keyspace") or cfg["datasource"].get("keyspace")
+        self.table = table
+        self.qualified = f"{self.keyspace}.{table}" if self.keyspace else table
+        self.mapping = parse_cassandra_mapping(cfg.get("mapping", ""))
+        if not self.mapping:
+            raise ValueError("vector-db-sink (cassandra): mapping is required")
+        self._pk: Optional[List[str]] = None
+
+    def _primary_key(self) -> List[str]:
+        if self._pk is None:
+            rows = self.ds.session.execute(
+                "SELECT column_name, kind, position FROM system_schema.columns WHERE keyspace_name = ? "
+                "AND table_name = ?", [self.keyspace, self.table])
+            pk = [r for r in rows if r.get("kind") in ("partition_key", "clustering")]
+            pk.sort(key=lambda r: (r["kind"] != "partition_key", r.get("position") or 0))
+            self._pk = [r["column_name"] for r in pk]
+        return self._pk
+
+    def upsert(self, mr: MutableRecord) -> Future:
+        f: Future = Future()
+        try:
+            ctx = mr.el_context()
+            vals = {col: eval_expression(expr, ctx) for col, expr in self.mapping}
+            if mr.value is None:
+                pk = self._primary_key()
+                where = " AND ".join(f"{c} = ?" for c in pk)
+                self.ds.session.execute(f"DELETE FROM {self.qualified} WHERE {where}", [vals.get(c) for c in pk])
+            else:
+                cols = list(vals)
+                self.ds.session.execute(
+                    f"INSERT INTO {self.qualified} ({', '.join(cols)}) VALUES ({', '.join('?' * len(cols))})",
+                    [vals[c] for c in cols])
+            f.set_result(None)
+        except Exception as e:  # noqa: BLE001
+            f.set_exception(e)
+        return f
+
+    def close(self) -> None:
+        self.ds.close()
+
+
+DATASOURCES.update({"cassandra": CassandraDataSource, "astra": CassandraDataSource})
+WRITERS.update({"cassandra": CassandraWriter, "astra": CassandraWriter})

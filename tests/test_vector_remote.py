@@ -44,6 +44,13 @@ class Fake:
 
             do_GET = do_POST = do_PUT = do_DELETE = _do
 
+            def do_HEAD(self):
+                fake.requests.append({"method": "HEAD", "path": urlsplit(self.path).path, "query": {}, "body": "",
+                                      "headers": dict(self.headers)})
+                self.send_response(200)
+                self.send_header("Content-Length", "0")
+                self.end_headers()
+
         self.srv = ThreadingHTTPServer(("127.0.0.1", 0), H)
         self.port = self.srv.server_address[1]
         threading.Thread(target=self.srv.serve_forever, daemon=True).start()
@@ -176,3 +183,58 @@ def test_sink_agent_uses_remote_writer(fake):
     a.init({"datasource": cfg, "fields": [{"name": "id", "expression": "key"}]})
     a.write(SimpleRecord.of("z", json.dumps({"a": 1}))).result(5)
     assert json.loads(fake.last("/solr/c/update")["body"]) == [{"id": "z"}]
+
+
+def _asset(atype, cfg):
+    from langstream_amd.agents.assets import AssetManagerRegistry
+    from langstream_amd.api.model import AssetDefinition
+    return AssetManagerRegistry.create(AssetDefinition(id="a", name="a", asset_type=atype, config=cfg))
+
+
+def test_remote_asset_managers(fake):
+    os_ds = {"service": "opensearch", "host": "127.0.0.1", "port": fake.port, "https": False}
+    m = _asset("opensearch-index", {"index-name": "idx", "datasource": {"configuration": os_ds},
+                                    "settings": '{"index": {"knn": true}}',
+                                    "mappings": '{"properties": {"emb": {"type": "knn_vector", "dimension": 3}}}'})
+    assert m.asset_exists()
+    m.deploy_asset()
+    put = [r for r in fake.requests if r["method"] == "PUT" and r["path"] == "/idx"][-1]
+    assert json.loads(put["body"])["mappings"]["properties"]["emb"]["dimension"] == 3
+    m.delete_asset_if_exists()
+    assert fake.requests[-1]["method"] == "DELETE"
+
+    solr = {"service": "solr", "host": "127.0.0.1", "port": fake.port, "collection-name": "documents"}
+    m = _asset("solr-collection", {"collection-name": "documents", "datasource": solr, "create-statements": [
+        {"api": "/api/collections", "method": "POST", "body": '{"name": "documents", "numShards": 1}'},
+        {"api": "/schema", "body": '"add-field": {"name": "emb", "type": "knn_vector"}'}]})
+    m.deploy_asset()
+    assert json.loads(fake.last("/api/collections")["body"])["name"] == "documents"
+    assert json.loads(fake.last("/solr/documents/schema")["body"]) == {"add-field": {"name": "emb", "type": "knn_vector"}}
+
+    milvus = {"service": "milvus", "url": f"http://127.0.0.1:{fake.port}"}
+    fake.responses["/v2/vectordb/collections/has"] = {"code": 0, "data": {"has": False}}
+    m = _asset("milvus-collection", {"collection-name": "docs", "database-name": "default", "datasource": milvus,
+                                     "create-statements": [
+                                         json.dumps({"command": "create-collection", "collection-name": "docs",
+                                                     "field-types": [{"name": "id", "primary-key": True,
+                                                                      "data-type": "Varchar", "max-length": 64},
+                                                                     {"name": "vector", "data-type": "FloatVector",
+                                                                      "dimension": 4}]}),
+                                         json.dumps({"command": "create-index", "field-name": "vector",
+                                                     "index-type": "AUTOINDEX", "metric-type": "L2"}),
+                                         json.dumps({"command": "load-collection"})]})
+    assert not m.asset_exists()
+    m.deploy_asset()
+    create = json.loads(fake.last("/v2/vectordb/collections/create")["body"])
+    assert create["dbName"] == "default" and create["schema"]["fields"][1] == {
+        "fieldName": "vector", "dataType": "FloatVector", "elementTypeParams": {"dim": 4}}
+    assert json.loads(fake.last("/v2/vectordb/indexes/create")["body"])["indexParams"][0]["metricType"] == "L2"
+    assert json.loads(fake.last("/v2/vectordb/collections/load")["body"])["collectionName"] == "docs"
+
+    astra = {"service": "astra-vector-db", "endpoint": f"http://127.0.0.1:{fake.port}", "token": "t"}
+    fake.responses["/api/json/v1/default_keyspace"] = {"status": {"collections": ["docs"]}}
+    m = _asset("astra-collection", {"collection-name": "docs", "vector-dimension": 8, "datasource": astra})
+    assert m.asset_exists()
+    m.deploy_asset()
+    body = [json.loads(r["body"]) for r in fake.requests if r["path"] == "/api/json/v1/default_keyspace"]
+    assert body[-1]["createCollection"]["options"]["vector"]["dimension"] == 8
