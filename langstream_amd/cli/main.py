@@ -499,6 +499,11 @@ def build_parser() -> argparse.ArgumentParser:
     opr.add_argument("--resync", type=float, default=5.0)
     opr.set_defaults(fn=cmd_operator)
 
+    dc = sub.add_parser("docs", help="generate the agents / resources / assets configuration reference")
+    dc.add_argument("--format", choices=("json", "markdown"), default="json")
+    dc.add_argument("--output", "-o", default=None, help="file to write (default: stdout)")
+    dc.set_defaults(fn=cmd_docs)
+
     cd = sub.add_parser("code-download")
     cd.add_argument("--tenant", default="default")
     cd.add_argument("--application", required=True)
@@ -507,6 +512,19 @@ def build_parser() -> argparse.ArgumentParser:
     cd.add_argument("--web-service-url")
     cd.set_defaults(fn=cmd_code_download)
     return ap
+
+
+def cmd_docs(args) -> int:
+    """``DocumentationGeneratorStarter`` equivalent: the configuration models as JSON or Markdown."""
+    from ..core.config_model import docs_markdown, generate_docs
+    docs = generate_docs()
+    text = json.dumps(docs, indent=2) if args.format == "json" else docs_markdown(docs)
+    if args.output:
+        with open(args.output, "w") as f:
+            f.write(text + "\n")
+    else:
+        print(text)
+    return 0
 
 
 def main(argv: Optional[List[str]] = None) -> int:

@@ -29,7 +29,8 @@ ASSET_REQUIRED = {
 def validate_asset(asset: AssetDefinition, app: Application) -> Dict[str, Any]:
     if asset.asset_type not in ASSET_REQUIRED:
         raise ValueError(f"Asset type {asset.asset_type} is not supported; known: {sorted(ASSET_REQUIRED)}")
-    cfg = dict(asset.config or {})
+    from .config_model import validate_asset as validate_model
+    cfg = validate_model(asset.name or asset.id, asset.asset_type, dict(asset.config or {}))
     for k in ASSET_REQUIRED[asset.asset_type]:
         if cfg.get(k) is None:
             raise ValueError(f"Asset {asset.id} ({asset.asset_type}): missing required property '{k}'")

@@ -37,7 +37,13 @@ class AgentSpec:
         return self.runtime or ac.type
 
     def compute_configuration(self, ac: AgentConfiguration, module, pipeline, plan) -> Dict[str, Any]:
+        from .config_model import validate_agent
         cfg = dict(ac.configuration or {})
+        service = None
+        if ac.type == "vector-db-sink" and isinstance(cfg.get("datasource"), str):
+            r = plan.application.resources.get(cfg["datasource"])
+            service = (r.configuration or {}).get("service") if r is not None else None
+        cfg = validate_agent(ac.name or ac.id, ac.type, cfg, service)
         for k in self.required:
             if cfg.get(k) is None or (isinstance(cfg.get(k), str) and not cfg[k].strip()):
                 raise ValueError(f"Found error on agent configuration (agent: '{ac.name or ac.id}', type: "

@@ -29,6 +29,8 @@ def validate_resource(r: Resource) -> None:
     if r.type not in RESOURCE_TYPES:
         raise ValueError(f"Resource type {r.type} is not supported; known: {sorted(RESOURCE_TYPES)}")
     cfg = r.configuration or {}
+    from .config_model import validate_resource as validate_model
+    validate_model(r.name or r.id, r.type, cfg)
     if r.type in AI_RESOURCE_TYPES:
         for k in AI_RESOURCE_TYPES[r.type]:
             if r.type == "open-ai-configuration" and cfg.get("provider", "openai") == "local":

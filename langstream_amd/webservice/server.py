@@ -312,7 +312,13 @@ class WebServiceServer:
         r.add_get("/api/archetypes/{tenant}/{id}", self.archetype)
         r.add_post("/api/archetypes/{tenant}/{id}/applications/{app}", self.archetype_deploy)
         r.add_get("/management/health", lambda req: web.json_response({"status": "UP"}))
+        r.add_get("/api/docs", self.docs)
         return app
+
+    async def docs(self, request):
+        from aiohttp import web
+        from ..core.config_model import generate_docs
+        return web.json_response(generate_docs())
 
     async def _off(self, fn, *a, **kw):
         return await asyncio.get_running_loop().run_in_executor(None, lambda: fn(*a, **kw))

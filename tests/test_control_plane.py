@@ -103,6 +103,9 @@ def test_tenants_and_app_lifecycle(server, app_dir):
     assert cp.store.get("t1", "app").code_archive_id == old_archive
     cl.delete("app")
     assert cl.list() == []
+    import requests
+    docs = requests.get(f"{srv.url}/api/docs", timeout=10).json()
+    assert "ai-chat-completions" in docs["agents"] and "open-ai-configuration" in docs["resources"]
 
 
 def test_tenant_resource_limit(server, app_dir, tmp_path):

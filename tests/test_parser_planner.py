@@ -166,3 +166,78 @@ pipeline:
 """
     with pytest.raises(ValueError, match="Service agents"):
         _plan({"pipeline.yaml": pipe})
+
+
+# ---------------------------------------------------------------- configuration models
+def _one(agent_type, cfg, extra=""):
+    import yaml
+    body = yaml.safe_dump({"pipeline": [{"name": "a1", "type": agent_type, "input": "in", "configuration": cfg}],
+                           "topics": [{"name": "in", "creation-mode": "create-if-not-exists"}]})
+    return _plan({"pipeline.yaml": body, **({"configuration.yaml": extra} if extra else {})})
+
+
+def test_config_validator_unknown_required_types_and_el():
+    with pytest.raises(ValueError, match=r"Found error on agent configuration \(agent: 'a1', type: 'drop-fields'\). "
+                                         r"Property 'bogus' is unknown"):
+        _one("drop-fields", {"fields": ["a"], "bogus": 1})
+    with pytest.raises(ValueError, match="Property 'fields' is required"):
+        _one("drop-fields", {})
+    with pytest.raises(ValueError, match=r"Property 'fields\[0\]' has a wrong data type"):
+        _one("drop-fields", {"fields": [{"x": 1}]})
+    with pytest.raises(ValueError, match="Property 'fields.expression' is required"):
+        _one("compute", {"fields": [{"name": "value.x"}]})
+    with pytest.raises(ValueError, match="Property 'fields.expression' has an invalid EL expression"):
+        _one("compute", {"fields": [{"name": "value.x", "expression": "value.a +* 2"}]})
+    with pytest.raises(ValueError, match="Property 'max' has a wrong data type. Expected type: int"):
+        _one("re-rank", {"field": "f", "output-field": "o", "max": "many"})
+    # coercion as in the reference (numbers / booleans given as strings)
+    plan = _one("re-rank", {"field": "f", "output-field": "o", "max": "7", "lambda": "0.3"})
+    node = next(iter(plan.agents.values()))
+    assert node.configuration["max"] == 7 and node.configuration["lambda"] == 0.3
+    # python agents accept any extra keys
+    _one("python-processor", {"className": "x.Y", "anything": {"goes": True}})
+    with pytest.raises(ValueError, match="Property 'className' is required"):
+        _one("python-processor", {})
+
+
+def test_vector_sink_model_follows_datasource_service():
+    res = """
+configuration:
+  resources:
+    - type: datasource
+      name: ks
+      configuration:
+        service: cassandra
+        contact-points: 127.0.0.1
+        loadBalancing-localDc: dc1
+"""
+    _one("vector-db-sink", {"datasource": "ks", "table-name": "t", "mapping": "a=value.a"}, res)
+    with pytest.raises(ValueError, match="Property 'fields' is unknown"):
+        _one("vector-db-sink", {"datasource": "ks", "table-name": "t", "mapping": "a=value.a", "fields": []}, res)
+    with pytest.raises(ValueError, match=r"resource configuration \(resource: 'ks', type: 'datasource'\). "
+                                         r"Property 'loadBalancing-localDc' is required"):
+        _one("vector-db-sink", {"datasource": "ks", "table-name": "t", "mapping": "a=value.a"},
+             res.replace("        loadBalancing-localDc: dc1\n", ""))
+
+
+def test_asset_model_and_docs():
+    from langstream_amd.api.model import AssetDefinition
+    from langstream_amd.core.config_model import docs_markdown, generate_docs, validate_asset
+    with pytest.raises(ValueError, match=r"asset configuration \(asset: 'c', type: 'astra-collection'\). "
+                                         r"Property 'vector-dimension' is required"):
+        validate_asset("c", "astra-collection", {"datasource": "d", "collection-name": "c"})
+    assert validate_asset("c", "astra-collection", {"datasource": "d", "collection-name": "c",
+                                                     "vector-dimension": "8"})["vector-dimension"] == 8
+    docs = generate_docs("1.0")
+    assert docs["version"] == "1.0" and set(docs) == {"version", "agents", "resources", "assets"}
+    ce = docs["agents"]["compute-ai-embeddings"]
+    assert ce["properties"]["batch-size"] == {"description": "Records per embedding batch.", "required": False,
+                                              "type": "integer", "defaultValue": 10}
+    assert docs["agents"]["compute"]["properties"]["fields"]["items"]["properties"]["expression"][
+        "extendedValidationType"] == "EL_EXPRESSION"
+    assert "vector-db-sink_cassandra" in docs["agents"] and "datasource_milvus" in docs["resources"]
+    assert "milvus-collection" in docs["assets"]
+    md = docs_markdown(docs)
+    assert "### `text-splitter`" in md and "| `chunk_size` | integer |" in md
+    from langstream_amd.cli.main import main
+    assert main(["docs", "--format", "markdown", "-o", "/dev/null"]) == 0
