@@ -357,12 +357,30 @@ def cmd_operator(args) -> int:
     return operator_main(argv)
 
 
+def _json_arg(v: Optional[str]) -> Optional[dict]:
+    """A JSON object given inline or as ``@file``."""
+    if not v:
+        return None
+    if v.startswith("@"):
+        with open(v[1:]) as f:
+            v = f.read()
+    return json.loads(v)
+
+
 def cmd_code_download(args) -> int:
+    """Agent init step: fetch the application archive (from the code storage directly when
+    ``--code-storage`` is given, else through the control plane) and unpack it."""
     import io
     import zipfile
-    from .client import AdminClient
-    url = args.web_service_url or os.environ.get("LANGSTREAM_WEBSERVICE_URL", "http://langstream-control-plane:8090")
-    data = AdminClient(url, args.tenant).download(args.application)
+    cs = _json_arg(args.code_storage or os.environ.get("LANGSTREAM_CODE_STORAGE"))
+    if cs is not None and args.code_archive_id:
+        from ..core.codestorage import code_storage_for
+        data = code_storage_for(cs).download_application_code(args.tenant, args.code_archive_id)
+    else:
+        from .client import AdminClient
+        url = args.web_service_url or os.environ.get("LANGSTREAM_WEBSERVICE_URL",
+                                                     "http://langstream-control-plane:8090")
+        data = AdminClient(url, args.tenant).download(args.application)
     with zipfile.ZipFile(io.BytesIO(data)) as z:
         z.extractall(args.target)
     return 0
@@ -510,8 +528,48 @@ def build_parser() -> argparse.ArgumentParser:
     cd.add_argument("--code-archive-id")
     cd.add_argument("--target", required=True)
     cd.add_argument("--web-service-url")
+    cd.add_argument("--code-storage", help="code storage config JSON (or @file), e.g. "
+                                           "'{\"type\": \"s3\", \"configuration\": {...}}'")
     cd.set_defaults(fn=cmd_code_download)
+
+    cp = sub.add_parser("control-plane", help="run the control-plane web service (applications, tenants, code)")
+    cp.add_argument("--host", default="0.0.0.0")
+    cp.add_argument("--port", type=int, default=8090)
+    cp.add_argument("--store", choices=("memory", "kubernetes"), default="memory")
+    cp.add_argument("--api-server", default=None, help="Kubernetes API server (store=kubernetes)")
+    cp.add_argument("--code-storage", default=None, help="code storage config JSON (or @file)")
+    cp.add_argument("--code-dir", default=None, help="local cache of unpacked archives")
+    cp.add_argument("--auth-secret", default=None, help="HS256 secret for bearer tokens on /api/*")
+    cp.add_argument("--max-units-per-tenant", type=int, default=0)
+    cp.set_defaults(fn=cmd_control_plane)
     return ap
+
+
+def cmd_control_plane(args) -> int:
+    import logging
+    import signal
+    logging.basicConfig(level=logging.INFO)
+    from ..core.codestorage import code_storage_for
+    from ..webservice.server import ControlPlane, WebServiceServer
+    store = None
+    if args.store == "kubernetes":
+        from ..operator.kube import KubeClient
+        from ..operator.store import KubernetesApplicationStore
+        store = KubernetesApplicationStore(KubeClient(args.api_server))
+    cs = _json_arg(args.code_storage or os.environ.get("LANGSTREAM_CODE_STORAGE"))
+    cp = ControlPlane(store, code_dir=args.code_dir, max_units_per_tenant=args.max_units_per_tenant,
+                      code_storage=code_storage_for(cs) if cs else None)
+    srv = WebServiceServer(cp, host=args.host, port=args.port, auth_secret=args.auth_secret).start()
+    print(f"control plane listening on {srv.url}", flush=True)
+    stop = threading.Event()
+    signal.signal(signal.SIGTERM, lambda *_: stop.set())
+    try:
+        while not stop.wait(1.0):
+            pass
+    except KeyboardInterrupt:
+        pass
+    srv.stop()
+    return 0
 
 
 def cmd_docs(args) -> int:

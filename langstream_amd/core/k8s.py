@@ -140,6 +140,11 @@ def render_agent_workload(agent_cr: Dict[str, Any]) -> List[Dict[str, Any]]:
              "command": ["python", "-m", "langstream_amd.cli", "code-download", "--tenant", spec["tenant"],
                          "--application", spec["applicationId"], "--code-archive-id",
                          str(spec.get("codeArchiveId")), "--target", "/app-code-download"],
+             # the code storage config (same as the control plane's) comes from an optional
+             # secret; without it the archive is fetched through the control plane
+             "env": [{"name": "LANGSTREAM_CODE_STORAGE",
+                      "valueFrom": {"secretKeyRef": {"name": "langstream-code-storage", "key": "config",
+                                                     "optional": True}}}],
              "volumeMounts": [{"name": "code-download", "mountPath": "/app-code-download"}]}]
     sts = {
         "apiVersion": "apps/v1", "kind": "StatefulSet",

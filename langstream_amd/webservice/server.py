@@ -74,10 +74,13 @@ class ControlPlane:
     """Application lifecycle independent of HTTP (also used by the CLI's local mode)."""
 
     def __init__(self, store: Optional[ApplicationStore] = None, code_dir: Optional[str] = None,
-                 services=None, max_units_per_tenant: int = 0):
+                 services=None, max_units_per_tenant: int = 0, code_storage=None):
+        from ..core.codestorage import LocalDiskCodeStorage
         self.store = store or InMemoryApplicationStore()
         self.code_dir = code_dir or tempfile.mkdtemp(prefix="langstream-code-")
         os.makedirs(self.code_dir, exist_ok=True)
+        # archives live in the code storage; code_dir only caches unpacked copies for local runners
+        self.code_storage = code_storage or LocalDiskCodeStorage({"path": os.path.join(self.code_dir, "archives")})
         self.services = services
         self.max_units = max_units_per_tenant
         self._logs: Dict[tuple, _AppLogBuffer] = {}
@@ -133,7 +136,6 @@ class ControlPlane:
             files = self.unzip(app_zip, tmp)
             code_root = files.pop("__root__")
             digest = directory_digest(os.path.join(code_root, "python"))
-            archive = hashlib.sha256(app_zip).hexdigest()[:32]
         elif files is None:
             if existing is None:
                 raise ValueError("missing application archive")
@@ -147,17 +149,22 @@ class ControlPlane:
             raise PermissionError(f"Not enough resources to deploy application {app_id}: tenant limit "
                                   f"{self.max_units} units")
         if dry_run:
+            if code_root is not None:
+                shutil.rmtree(tmp, ignore_errors=True)
             return {"application": plan.to_dict(), "dry-run": True}
         if update and existing is not None and existing.code_archive_id and digest is not None:
-            old = os.path.join(self.code_dir, existing.code_archive_id)
-            if directory_digest(os.path.join(old, "python")) == digest:
+            md = self.code_storage.describe_application_code(tenant, existing.code_archive_id)
+            if md is not None and md.py_binaries_digest == digest:
                 archive = existing.code_archive_id  # python code unchanged: keep the archive
         if code_root is not None:
+            if archive is None:
+                version = hashlib.sha256(app_zip).hexdigest()[:12]
+                archive = self.code_storage.store_application_code(tenant, app_id, version, app_zip,
+                                                                   digest).code_store_id
             dst = os.path.join(self.code_dir, archive)
             if not os.path.exists(dst):
                 shutil.move(code_root, dst)
-            with open(os.path.join(self.code_dir, archive + ".zip"), "wb") as f:
-                f.write(app_zip)
+            shutil.rmtree(tmp, ignore_errors=True)
         if existing is not None and existing.runner is not None:
             existing.runner.stop(10)
         sa = StoredApplication(app_id, tenant, info.application, dict(files), instance, secrets,
@@ -178,7 +185,7 @@ class ControlPlane:
             self.store.put(sa)
             return
         from ..runtime.local import LocalApplicationRunner
-        code = os.path.join(self.code_dir, sa.code_archive_id) if sa.code_archive_id else ""
+        code = self.local_code(sa) if sa.code_archive_id else ""
         runner = LocalApplicationRunner(sa.application, application_id=sa.application_id, tenant=sa.tenant,
                                         code_directory=code, services=self.services)
         buf = _AppLogBuffer()
@@ -196,6 +203,17 @@ class ControlPlane:
             sa.error = str(e)
         self.store.put(sa)
 
+    def local_code(self, sa: StoredApplication) -> str:
+        """Unpacked code directory of ``sa``'s archive (fetched from the code storage on a miss,
+        e.g. after a control-plane restart)."""
+        dst = os.path.join(self.code_dir, sa.code_archive_id)
+        if not os.path.exists(dst):
+            tmp = tempfile.mkdtemp(prefix="app-", dir=self.code_dir)
+            root = self.unzip(self.code_storage.download_application_code(sa.tenant, sa.code_archive_id), tmp)
+            shutil.move(root["__root__"], dst)
+            shutil.rmtree(tmp, ignore_errors=True)
+        return dst
+
     def delete(self, tenant: str, app_id: str, force: bool = False) -> None:
         sa = self.store.get(tenant, app_id)
         if sa is None:
@@ -212,6 +230,10 @@ class ControlPlane:
         if buf is not None:
             logging.getLogger().removeHandler(buf)
         self.store.delete(tenant, app_id)
+        try:
+            self.code_storage.delete_application(tenant, app_id)
+        except Exception:  # noqa: BLE001
+            log.warning("deleting the code archives of %s failed", app_id)
 
     def describe(self, tenant: str, app_id: str, stats: bool = False) -> Dict[str, Any]:
         sa = self.store.get(tenant, app_id)
@@ -407,17 +429,18 @@ class WebServiceServer:
         sa = self.cp.store.get(request.match_info["tenant"], request.match_info["id"])
         if sa is None or not sa.code_archive_id:
             raise KeyError("code not found")
-        return web.FileResponse(os.path.join(self.cp.code_dir, sa.code_archive_id + ".zip"))
+        data = await self._off(self.cp.code_storage.download_application_code, sa.tenant, sa.code_archive_id)
+        return web.Response(body=data, content_type="application/zip")
 
     async def app_code_info(self, request):
         from aiohttp import web
         sa = self.cp.store.get(request.match_info["tenant"], request.match_info["id"])
         if sa is None:
             raise KeyError("application not found")
-        d = os.path.join(self.cp.code_dir, sa.code_archive_id or "")
+        md = self.cp.code_storage.describe_application_code(sa.tenant, sa.code_archive_id) \
+            if sa.code_archive_id else None
         return web.json_response({"code-archive-id": sa.code_archive_id,
-                                  "python-digest": directory_digest(os.path.join(d, "python")) if sa.code_archive_id
-                                  else None})
+                                  "python-digest": md.py_binaries_digest if md else None})
 
     async def archetypes(self, request):
         from aiohttp import web
