@@ -167,6 +167,8 @@ class LLMEngine:
         self.max_prefill_tokens = max_prefill_tokens
         self.is_gpu = self.device.type == "cuda"
         self.use_graphs = use_graphs and self.is_gpu
+        if self.is_gpu:
+            ops.enable_decode_gemm_tuning()   # cold-picked GEMM solutions, before any graph capture
         self.lookahead = lookahead
         D = self.cfg.head_dim
         hkv = model.hkv

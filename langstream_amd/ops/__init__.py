@@ -51,6 +51,31 @@ def _load():
     return _ext
 
 
+_TUNED = None
+
+
+def enable_decode_gemm_tuning(path: Optional[str] = None) -> bool:
+    """Load the cold-timed hipBLASLt/rocBLAS solution picks for the decode-step projection
+    GEMMs (``tools/gemm_cold_select.py``) into PyTorch TunableOp with tuning disabled: the
+    listed (M, N, K) use the picked solution, every other GEMM keeps the default heuristic.
+    Opt out with ``LS_GEMM_TUNING=0``."""
+    global _TUNED
+    if _TUNED is not None:
+        return _TUNED
+    path = path or os.path.join(os.path.dirname(os.path.abspath(__file__)), "tunableop_decode_gfx950.csv")
+    _TUNED = False
+    if os.environ.get("LS_GEMM_TUNING", "1") == "0" or not os.path.exists(path) or not torch.cuda.is_available():
+        return False
+    import tempfile
+    import torch.cuda.tunable as tun
+    tun.enable(True)
+    tun.tuning_enable(False)
+    tun.set_filename(os.path.join(tempfile.gettempdir(), f"ls_tunableop_{os.getpid()}.csv"),
+                     insert_device_ordinal=False)
+    _TUNED = bool(tun.read_file(path))
+    return _TUNED
+
+
 def hip_available() -> bool:
     return _load() is not None
 
