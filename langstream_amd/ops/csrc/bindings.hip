@@ -28,6 +28,8 @@ void l2_normalize_rows(at::Tensor out, at::Tensor x);
 void knn_topk(at::Tensor X, at::Tensor Q, int64_t K, at::Tensor out_s, at::Tensor out_i, at::Tensor ws_s,
               at::Tensor ws_i);
 void skinny_gemm(at::Tensor out, at::Tensor x, at::Tensor w);
+void gemv(at::Tensor out, at::Tensor x, at::Tensor w);
+void gemv_silu(at::Tensor out, at::Tensor x, at::Tensor w);
 void skinny_gemm_silu(at::Tensor out, at::Tensor x, at::Tensor w);
 void skinny_gemm_add_rmsnorm(at::Tensor out, at::Tensor x, at::Tensor w, at::Tensor residual, at::Tensor norm_w,
                              double eps);
@@ -51,6 +53,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("l2_normalize_rows", &l2_normalize_rows);
   m.def("knn_topk", &knn_topk);
   m.def("skinny_gemm", &skinny_gemm);
+  m.def("gemv", &gemv);
+  m.def("gemv_silu", &gemv_silu);
   m.def("skinny_gemm_silu", &skinny_gemm_silu);
   m.def("skinny_gemm_add_rmsnorm", &skinny_gemm_add_rmsnorm);
   bind_runners(m);

@@ -62,6 +62,9 @@ void sample_tokens(at::Tensor logits, at::Tensor temperature, at::Tensor top_k, 
                    int64_t n_top);
 
 void skinny_gemm(at::Tensor out, at::Tensor x, at::Tensor w);
+void gemv(at::Tensor out, at::Tensor x, at::Tensor w);
+void gemv_silu(at::Tensor out, at::Tensor x, at::Tensor w);
+bool gemv_supported(const at::Tensor& w, bool silu);
 void skinny_gemm_add_rmsnorm(at::Tensor out, at::Tensor x, at::Tensor w, at::Tensor residual, at::Tensor norm_w,
                              double eps);
 
@@ -125,9 +128,16 @@ class LlamaRunner {
     // with the residual add + RMSNorm fused into the split-K reduction (TP=1 only: under
     // TP the all-reduce sits between the GEMM and the residual add).
     const bool sk = skinny_enabled() && !pg_;
+    // T <= 4 (single-stream / low-concurrency chat): the register-streaming GEMV
+    // (ops/csrc/gemm_gemv.hip) for all four projections, gate_up with silu*up fused; it
+    // fuses no residual, so it also serves tensor-parallel ranks.
+    const bool gv = gemv_enabled() && T <= 4;
     for (int64_t l = 0; l < L; ++l) {
       at::Tensor qkv;
-      if (sk && T <= 32 && skinny_shape(qkv_w_[l])) {
+      if (gv && gemv_supported(qkv_w_[l], false)) {
+        qkv = at::empty({T, qkv_w_[l].size(0)}, x.options());
+        gemv(qkv, x, qkv_w_[l]);
+      } else if (sk && T <= 32 && skinny_shape(qkv_w_[l])) {
         qkv = at::empty({T, qkv_w_[l].size(0)}, x.options());
         skinny_gemm(qkv, x, qkv_w_[l]);
       } else {
@@ -142,7 +152,12 @@ class LlamaRunner {
       if (num_prefill > 0)
         paged_prefill_attention(attn, q, kc_[l], vc_[l], p_bt, q_start, q_len, ctx_len, tiles, hq_, scale_);
       at::Tensor o;
-      if (sk && T <= 192 && skinny_shape(o_w_[l])) {
+      if (gv && gemv_supported(o_w_[l], false)) {
+        o = at::empty_like(residual);
+        gemv(o, attn, o_w_[l]);
+        all_reduce(o);
+        fused_add_rmsnorm(o, residual, post_norm_[l], eps_);
+      } else if (sk && T <= 192 && skinny_shape(o_w_[l])) {
         o = at::empty_like(residual);
         skinny_gemm_add_rmsnorm(o, attn, o_w_[l], residual, post_norm_[l], eps_);
       } else {
@@ -150,12 +165,23 @@ class LlamaRunner {
         all_reduce(o);
         fused_add_rmsnorm(o, residual, post_norm_[l], eps_);
       }
-      at::Tensor gu = at::linear(o, gate_up_w_[l]);
-      at::Tensor a = at::empty({T, gu.size(1) / 2}, gu.options());
-      silu_and_mul(a, gu);
+      at::Tensor a;
+      if (gv && gemv_supported(gate_up_w_[l], true)) {
+        a = at::empty({T, gate_up_w_[l].size(0) / 2}, o.options());
+        gemv_silu(a, o, gate_up_w_[l]);
+      } else {
+        at::Tensor gu = at::linear(o, gate_up_w_[l]);
+        a = at::empty({T, gu.size(1) / 2}, gu.options());
+        silu_and_mul(a, gu);
+      }
       const at::Tensor& nxt = l + 1 < L ? in_norm_[l + 1] : final_norm_;
       at::Tensor dn;
-      if (sk && T >= 48 && T <= 256 && skinny_shape(down_w_[l])) {
+      if (gv && gemv_supported(down_w_[l], false)) {
+        dn = at::empty_like(residual);
+        gemv(dn, a, down_w_[l]);
+        all_reduce(dn);
+        fused_add_rmsnorm(dn, residual, nxt, eps_);
+      } else if (sk && T >= 48 && T <= 256 && skinny_shape(down_w_[l])) {
         dn = at::empty_like(residual);
         skinny_gemm_add_rmsnorm(dn, a, down_w_[l], residual, nxt, eps_);
       } else {
@@ -212,6 +238,14 @@ class LlamaRunner {
     h.masked_fill_(mask.unsqueeze(1), 0);
     all_reduce(h);
     return h;
+  }
+
+  static bool gemv_enabled() {
+    static const bool on = [] {
+      const char* v = std::getenv("LS_GEMV");
+      return !(v && std::string(v) == "0");
+    }();
+    return on;
   }
 
   static bool skinny_enabled() {

@@ -1,13 +1,17 @@
 // Token sampling + log-probs for the decode loop (one workgroup of 1024 threads per
-// sequence row; rows of 128K logits are streamed 16 B per lane, 2-3 passes, L2-hot).
+// sequence row; rows of 128K logits are swept 16 B per lane with 4 loads in flight per
+// lane -- `sweep` below -- in 2-3 passes, L2/Infinity-Cache hot).  The first version
+// loaded 4 B per lane per dependent iteration and was latency-bound: 342 us per row at
+// batch 1 (profiles/prof_b1_kernel_stats.csv).
 //
 // Per row r (all params are device tensors so the launch is graph-capturable):
 //   temperature[r] <= 0  -> greedy argmax
 //   otherwise            -> Gumbel-max sampling from softmax(logits / T), optionally
 //                           restricted by top_k[r] (>0) and top_p[r] (<1).  The cut is
-//                           found with a 2048-bin LDS histogram of (logit - max)/T over
-//                           [-32, 0] nats; the cutoff bin is kept whole (documented
-//                           approximation: ties within 1/64 nat).
+//                           found with a 1024-bin LDS histogram of (logit - max)/T over
+//                           [-32, 0] nats (8 lane-interleaved copies, merged by a
+//                           block-wide suffix scan); the cutoff bin is kept whole
+//                           (documented approximation: ties within 1/32 nat).
 // Outputs: token[r] (int32), logprob[r] = log softmax(logits)[token] at T = 1 (what
 // OpenAI-style `logprobs` and FLARE consume), and optionally the top-n alternatives.
 //
@@ -19,7 +23,8 @@
 
 namespace {
 
-constexpr int NBINS = 2048;
+constexpr int NBINS = 1024;   // == blockDim.x: one bin per thread in the cut scan
+constexpr int NCOPY = 8;      // histogram copies, picked by lane & 7 (LDS atomic contention / 8)
 constexpr float RANGE = 32.f;
 
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {
@@ -28,14 +33,65 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
   return z ^ (z >> 31);
 }
 
-__device__ __forceinline__ float uniform01(uint64_t seed, uint64_t idx) {
-  const uint64_t z = mix64(seed ^ mix64(idx + 0x9e3779b97f4a7c15ULL));
+// Per-row 32-bit key from the 64-bit (seed, step) mix; per-element draws hash (key, index)
+// with a 32-bit finaliser (two multiplies instead of two 64-bit mixes per element: the
+// Gumbel pass is ALU-bound on a 128K-entry row).
+__device__ __forceinline__ uint32_t hash32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352dU;
+  x ^= x >> 15;
+  x *= 0x846ca68bU;
+  x ^= x >> 16;
+  return x;
+}
+
+__device__ __forceinline__ uint32_t row_key(uint64_t seed) {
+  const uint64_t z = mix64(seed);
+  return (uint32_t)z ^ (uint32_t)(z >> 32);
+}
+
+__device__ __forceinline__ float uniform01(uint32_t key, uint32_t idx) {
+  const uint32_t z = hash32(idx * 0x9e3779b9U + key);
   // 24 random bits -> (0, 1)
-  return ((float)(z >> 40) + 0.5f) * (1.0f / 16777216.0f);
+  return ((float)(z >> 8) + 0.5f) * (1.0f / 16777216.0f);
 }
 
 template <typename T>
 __device__ __forceinline__ float ldf(const T* p) { return (float)(*p); }
+
+// Calls fn(value, index) for every element of a row: 16-B vector loads (4 f32 / 8 bf16),
+// four of them issued per lane before use; a scalar tail (and a scalar path for rows that
+// are not 16-B aligned).  Each thread sees its elements in increasing index order.
+template <typename T, typename Fn>
+__device__ __forceinline__ void sweep(const T* __restrict__ lr, int V, bool aligned, Fn&& fn) {
+  constexpr int N = 16 / sizeof(T);
+  const int tid = threadIdx.x, nt = blockDim.x;
+  int tail = 0;
+  if (aligned) {
+    const int nvec = V / N;
+    const uint4* vp = reinterpret_cast<const uint4*>(lr);
+    int v = tid;
+    for (; v + 3 * nt < nvec; v += 4 * nt) {
+      uint4 q[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) q[u] = vp[v + u * nt];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const T* e = reinterpret_cast<const T*>(&q[u]);
+#pragma unroll
+        for (int j = 0; j < N; ++j) fn((float)e[j], (v + u * nt) * N + j);
+      }
+    }
+    for (; v < nvec; v += nt) {
+      const uint4 q = vp[v];
+      const T* e = reinterpret_cast<const T*>(&q);
+#pragma unroll
+      for (int j = 0; j < N; ++j) fn((float)e[j], v * N + j);
+    }
+    tail = nvec * N;
+  }
+  for (int i = tail + tid; i < V; i += nt) fn(ldf(lr + i), i);
+}
 
 struct ArgMax {
   float v;
@@ -62,11 +118,11 @@ __global__ void __launch_bounds__(1024) sample_kernel(const T* __restrict__ logi
                                                       const int64_t* __restrict__ steps,
                                                       int32_t* __restrict__ out_tok, float* __restrict__ out_lp,
                                                       int n_top, int32_t* __restrict__ top_ids,
-                                                      float* __restrict__ top_lps) {
+                                                      float* __restrict__ top_lps, bool aligned) {
   __shared__ float red_f[16];
   __shared__ int red_i[16];
-  __shared__ float hist_mass[NBINS];
-  __shared__ int hist_cnt[NBINS];
+  __shared__ unsigned long long hist_mass[NCOPY][NBINS];  // fixed point, 2^-24 units
+  __shared__ int hist_cnt[NCOPY][NBINS];
   __shared__ int cut_bin;
   const int row = blockIdx.x;
   const T* lr = logits + (int64_t)row * row_stride;
@@ -78,8 +134,7 @@ __global__ void __launch_bounds__(1024) sample_kernel(const T* __restrict__ logi
   // ---- pass 1: max, argmax, sum exp (T = 1)
   ArgMax best{-INFINITY, 0x7fffffff};
   float mloc = -INFINITY, sloc = 0.f;
-  for (int i = tid; i < V; i += blockDim.x) {
-    const float x = ldf(lr + i);
+  sweep(lr, V, aligned, [&](float x, int i) {
     if (x > best.v) best = ArgMax{x, i};
     if (x > mloc) {
       sloc = sloc * __expf(mloc - x) + 1.f;
@@ -87,7 +142,7 @@ __global__ void __launch_bounds__(1024) sample_kernel(const T* __restrict__ logi
     } else {
       sloc += __expf(x - mloc);
     }
-  }
+  });
   best = wave_argmax(best);
   // combine (m, s) across the wave
 #pragma unroll
@@ -124,49 +179,77 @@ __global__ void __launch_bounds__(1024) sample_kernel(const T* __restrict__ logi
     float thresh = -INFINITY;  // in (x - max)/T units
     if (restrict_) {
       // ---- pass 2: histogram of scaled logits
-      for (int b = tid; b < NBINS; b += blockDim.x) {
-        hist_mass[b] = 0.f;
-        hist_cnt[b] = 0;
+      for (int b = tid; b < NCOPY * NBINS; b += blockDim.x) {
+        (&hist_mass[0][0])[b] = 0ull;
+        (&hist_cnt[0][0])[b] = 0;
       }
+      if (tid == 0) cut_bin = 0;
       __syncthreads();
-      for (int i = tid; i < V; i += blockDim.x) {
-        const float z = (ldf(lr + i) - gm) * invT;
+      const int cp = lane & (NCOPY - 1);
+      const bool need_cnt = k > 0 && k < V, need_mass = p > 0.f && p < 1.f;
+      sweep(lr, V, aligned, [&](float x, int) {
+        const float z = (x - gm) * invT;
         if (z >= -RANGE) {
           const int b = min(NBINS - 1, (int)((z + RANGE) * (NBINS / RANGE)));
-          atomicAdd(&hist_mass[b], __expf(z));
-          atomicAdd(&hist_cnt[b], 1);
+          // integer ds_add_u64: LDS float atomics measured ~6x slower here (sample_bench.log)
+          if (need_mass) atomicAdd(&hist_mass[cp][b], (unsigned long long)(__expf(z) * 16777216.f));
+          if (need_cnt) atomicAdd(&hist_cnt[cp][b], 1);
         }
+      });
+      __syncthreads();
+      // suffix scan from the top bin: thread t owns bin NBINS-1-t (blockDim.x == NBINS)
+      const int b = NBINS - 1 - tid;
+      float m = 0.f;
+      int c = 0;
+#pragma unroll
+      for (int q = 0; q < NCOPY; ++q) {
+        m += (float)hist_mass[q][b] * (1.0f / 16777216.f);
+        c += hist_cnt[q][b];
+      }
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {  // inclusive wave scan over increasing tid
+        const float mo = __shfl_up(m, o, 64);
+        const int co = __shfl_up(c, o, 64);
+        if (lane >= o) {
+          m += mo;
+          c += co;
+        }
+      }
+      __shared__ float wm[16];
+      __shared__ int wc[16];
+      if (lane == 63) {
+        wm[wid] = m;
+        wc[wid] = c;
       }
       __syncthreads();
-      if (tid == 0) {
-        float tot = 0.f;
-        for (int b = 0; b < NBINS; ++b) tot += hist_mass[b];
-        float acc = 0.f;
-        int cnt = 0, cb = 0;
-        for (int b = NBINS - 1; b >= 0; --b) {
-          acc += hist_mass[b];
-          cnt += hist_cnt[b];
-          cb = b;
-          if ((k > 0 && cnt >= k) || (p > 0.f && p < 1.f && acc >= p * tot)) break;
+      float tot = 0.f;
+      for (int w = 0; w < nw; ++w) {
+        if (w < wid) {
+          m += wm[w];
+          c += wc[w];
         }
-        cut_bin = cb;
+        tot += wm[w];
       }
+      const bool hit = (need_cnt && c >= k) || (need_mass && m >= p * tot);
+      // the cut is the highest bin whose suffix satisfies the rule = the lowest such tid
+      if (hit) atomicMax(&cut_bin, b);
       __syncthreads();
       thresh = cut_bin * (RANGE / NBINS) - RANGE;
     }
     // ---- pass 3: Gumbel-max among the kept tokens
-    const uint64_t seed = (uint64_t)seeds[row] * 0x2545F4914F6CDD1DULL + (uint64_t)steps[row];
+    const uint32_t key = row_key((uint64_t)seeds[row] * 0x2545F4914F6CDD1DULL + (uint64_t)steps[row]);
     ArgMax g{-INFINITY, 0x7fffffff};
-    for (int i = tid; i < V; i += blockDim.x) {
-      const float z = (ldf(lr + i) - gm) * invT;
+    const int cb = restrict_ ? cut_bin : -1;
+    sweep(lr, V, aligned, [&](float x, int i) {
+      const float z = (x - gm) * invT;
       if (restrict_) {
         const int b = z >= -RANGE ? min(NBINS - 1, (int)((z + RANGE) * (NBINS / RANGE))) : -1;
-        if (b < cut_bin) continue;
+        if (b < cb) return;
       }
-      const float u = uniform01(seed, (uint64_t)i);
+      const float u = uniform01(key, (uint32_t)i);
       const float gz = z - __logf(-__logf(u));
       if (gz > g.v) g = ArgMax{gz, i};
-    }
+    });
     (void)thresh;
     g = wave_argmax(g);
     __syncthreads();
@@ -188,13 +271,11 @@ __global__ void __launch_bounds__(1024) sample_kernel(const T* __restrict__ logi
     __shared__ int picked[32];
     for (int n = 0; n < n_top; ++n) {
       ArgMax bb{-INFINITY, 0x7fffffff};
-      for (int i = tid; i < V; i += blockDim.x) {
+      sweep(lr, V, aligned, [&](float x, int i) {
         bool skip = false;
         for (int j = 0; j < n; ++j) skip |= (picked[j] == i);
-        if (skip) continue;
-        const float x = ldf(lr + i);
-        if (x > bb.v) bb = ArgMax{x, i};
-      }
+        if (!skip && x > bb.v) bb = ArgMax{x, i};
+      });
       bb = wave_argmax(bb);
       __syncthreads();
       if (lane == 0) {
@@ -242,12 +323,14 @@ void sample_tokens(at::Tensor logits, at::Tensor temperature, at::Tensor top_k, 
   if (n_top > 0) TORCH_CHECK(top_ids.numel() >= B * n_top && top_lps.numel() >= B * n_top);
   if (B == 0) return;
   auto stream = at::hip::getCurrentHIPStream();
+  const bool aligned = (reinterpret_cast<uintptr_t>(logits.data_ptr()) % 16 == 0) &&
+                       (logits.stride(0) * (int64_t)logits.element_size()) % 16 == 0;
 #define LAUNCH(TT)                                                                                              \
-  sample_kernel<TT><<<B, 1024, 0, stream>>>(                                                                    \
+  sample_kernel<TT><<<B, NBINS, 0, stream>>>(                                                                    \
       (const TT*)logits.data_ptr(), logits.stride(0), V, temperature.data_ptr<float>(), top_k.data_ptr<int32_t>(), \
       top_p.data_ptr<float>(), seeds.data_ptr<int64_t>(), steps.data_ptr<int64_t>(), out_tok.data_ptr<int32_t>(), \
       out_lp.data_ptr<float>(), (int)n_top, n_top > 0 ? top_ids.data_ptr<int32_t>() : nullptr,                  \
-      n_top > 0 ? top_lps.data_ptr<float>() : nullptr)
+      n_top > 0 ? top_lps.data_ptr<float>() : nullptr, aligned)
   if (logits.scalar_type() == at::kFloat) LAUNCH(float);
   else if (logits.scalar_type() == at::kBFloat16) LAUNCH(bf16);
   else TORCH_CHECK(false, "logits must be f32 or bf16");

@@ -320,3 +320,27 @@ def test_skinny_gemm_add_rmsnorm(M):
     _close(res, res_exp, 0.03, 0.03)
     exp = res_exp * torch.rsqrt(res_exp.pow(2).mean(-1, keepdim=True) + 1e-5) * g.float().cpu()
     _close(out, exp, 0.05, 0.05)
+
+
+@pytest.mark.parametrize("T,N,K", [(1, 6144, 4096), (2, 4096, 4096), (3, 512, 1536), (4, 4096, 14336),
+                                   (1, 4096, 14336), (2, 1024, 3584)])
+def test_gemv(T, N, K):
+    torch.manual_seed(T * 7 + K)
+    x = torch.randn(T, K, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=DEV) * 0.05).to(torch.bfloat16)
+    out = torch.empty(T, N, device=DEV, dtype=torch.bfloat16)
+    ops.hip().gemv(out, x, w)
+    exp = x.float().cpu() @ w.float().cpu().t()
+    _close(out, exp, 0.03, 0.03)
+
+
+@pytest.mark.parametrize("T,F,K", [(1, 14336, 4096), (3, 1024, 2048), (4, 512, 14336)])
+def test_gemv_silu(T, F, K):
+    torch.manual_seed(T + F)
+    x = torch.randn(T, K, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(2 * F, K, device=DEV) * 0.05).to(torch.bfloat16)
+    out = torch.empty(T, F, device=DEV, dtype=torch.bfloat16)
+    ops.hip().gemv_silu(out, x, w)
+    gu = (x.float().cpu() @ w.float().cpu().t()).to(torch.bfloat16).float()
+    exp = torch.nn.functional.silu(gu[:, :F]) * gu[:, F:]
+    _close(out, exp, 0.03, 0.03)
