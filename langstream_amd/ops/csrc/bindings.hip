@@ -30,6 +30,12 @@ void knn_topk(at::Tensor X, at::Tensor Q, int64_t K, at::Tensor out_s, at::Tenso
 void skinny_gemm(at::Tensor out, at::Tensor x, at::Tensor w);
 void gemv(at::Tensor out, at::Tensor x, at::Tensor w);
 void gemv_silu(at::Tensor out, at::Tensor x, at::Tensor w);
+void gemv_add_rmsnorm(at::Tensor out, at::Tensor x, at::Tensor w, at::Tensor residual, at::Tensor norm_w,
+                      double eps, at::Tensor counter);
+void gemv_norm(at::Tensor out, at::Tensor o, at::Tensor res, at::Tensor res_out, at::Tensor norm_w, double eps,
+               at::Tensor w);
+void gemv_silu_norm(at::Tensor out, at::Tensor o, at::Tensor res, at::Tensor res_out, at::Tensor norm_w, double eps,
+                    at::Tensor w);
 void skinny_gemm_silu(at::Tensor out, at::Tensor x, at::Tensor w);
 void skinny_gemm_add_rmsnorm(at::Tensor out, at::Tensor x, at::Tensor w, at::Tensor residual, at::Tensor norm_w,
                              double eps);
@@ -55,6 +61,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("skinny_gemm", &skinny_gemm);
   m.def("gemv", &gemv);
   m.def("gemv_silu", &gemv_silu);
+  m.def("gemv_add_rmsnorm", &gemv_add_rmsnorm);
+  m.def("gemv_norm", &gemv_norm);
+  m.def("gemv_silu_norm", &gemv_silu_norm);
   m.def("skinny_gemm_silu", &skinny_gemm_silu);
   m.def("skinny_gemm_add_rmsnorm", &skinny_gemm_add_rmsnorm);
   bind_runners(m);

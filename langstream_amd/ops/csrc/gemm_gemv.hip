@@ -28,7 +28,29 @@ namespace {
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int EPI_NONE = 0, EPI_SILU = 1;
+constexpr int EPI_NONE = 0, EPI_SILU = 1, EPI_ADDNORM = 2;
+
+// EPI_ADDNORM operands: after the projection, residual = bf16(out + residual) and
+// out = bf16(rmsnorm(residual) * norm_w) -- the fused_add_rmsnorm of norm.hip -- done by
+// the block that finishes last (agent-scope release/acquire ticket on `counter`, which the
+// last block resets to 0 for the next launch; the buffer is zero-initialised once).
+struct AddNorm {
+  bf16* residual;
+  const bf16* norm_w;
+  unsigned int* counter;
+  float eps;
+};
+
+// PRO (prologue) operands: the GEMV input is x = rmsnorm(o + res) * norm_w, computed in
+// the kernel; block 0 writes res_out = bf16(o + res) (a different buffer than res: the
+// other blocks are still reading res).
+struct ProNorm {
+  const bf16* o;
+  const bf16* res;
+  bf16* res_out;
+  const bf16* norm_w;
+  float eps;
+};
 
 // 8-element bf16 dot on v_dot2c_f32_bf16.  The pairs are taken with shufflevector on the
 // whole 16-B value: bit-casting extracted u32 elements (a.y, a[1], ...) is miscompiled by
@@ -48,37 +70,106 @@ __device__ __forceinline__ float dot8(u32x4 a, u32x4 b, float acc) {
 
 // TR: rows of x handled (x rows >= T are clamped to T-1 and not stored); KCH: 512-element
 // chunks per wave (ceil(K / 2048)); RB: W rows per block.
-template <int TR, int KCH, int RB, int EPI>
+template <int TR, int KCH, int RB, int EPI, bool PRO>
 __global__ void __launch_bounds__(256) gemv_kernel(const bf16* __restrict__ x, int T, const bf16* __restrict__ W,
-                                                   int N, int K, bf16* __restrict__ out, int ldo) {
+                                                   int N, int K, bf16* __restrict__ out, int ldo, AddNorm an,
+                                                   ProNorm pro) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int nchunk = K >> 9;  // K % 512 == 0 (host-checked)
-  // ---- x fragments: chunk c of this wave = global chunk c*4 + wv
-  u32x4 xr[TR][KCH];
-#pragma unroll
-  for (int m = 0; m < TR; ++m) {
-    const bf16* xm = x + (int64_t)min(m, T - 1) * K;
-#pragma unroll
-    for (int c = 0; c < KCH; ++c) {
-      // branch-free tail: a chunk past K reloads the last one and is zeroed by a select, so
-      // no load sits behind control flow (which made the compiler drain vmcnt per row)
-      const int g = c * 4 + wv;
-      const u32x4 v = *reinterpret_cast<const u32x4*>(xm + (min(g, nchunk - 1) << 9) + lane * 8);
-      xr[m][c] = g < nchunk ? v : u32x4{0, 0, 0, 0};
-    }
-  }
-  // ---- W rows of this block
   constexpr int HALF = RB / 2;
   const int F = N >> 1;
   const int base = blockIdx.x * (EPI == EPI_SILU ? HALF : RB);
   u32x4 wr[RB][KCH];
+  u32x4 xr[TR][KCH];
+  if constexpr (PRO) {
+    // ---- prologue: x = rmsnorm(o + residual) * norm_w, recomputed by every block from
+    // the L2-resident [T, K] operands (16 KB per token at K = 4096 against >= 64 KB of W
+    // per block); block 0 also writes the new residual stream.  W loads go out first so
+    // they are in flight during the norm; a raw s_barrier keeps them outstanding.
 #pragma unroll
-  for (int r = 0; r < RB; ++r) {
-    const int row = EPI == EPI_SILU ? (r < HALF ? base + r : F + base + r - HALF) : base + r;
-    const bf16* wrow = W + (int64_t)row * K + lane * 8;
+    for (int r = 0; r < RB; ++r) {
+      const int row = EPI == EPI_SILU ? (r < HALF ? base + r : F + base + r - HALF) : base + r;
+      const bf16* wrow = W + (int64_t)row * K + lane * 8;
 #pragma unroll
-    for (int c = 0; c < KCH; ++c)
-      wr[r][c] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(wrow + (min(c * 4 + wv, nchunk - 1) << 9)));
+      for (int c = 0; c < KCH; ++c)
+        wr[r][c] =
+            __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(wrow + (min(c * 4 + wv, nchunk - 1) << 9)));
+    }
+    __shared__ float pro_red[4][TR];
+    float ss[TR];
+#pragma unroll
+    for (int m = 0; m < TR; ++m) {
+      const int mm = min(m, T - 1);
+      const bf16* om = pro.o + (int64_t)mm * K;
+      const bf16* rm = pro.res + (int64_t)mm * K;
+      ss[m] = 0.f;
+#pragma unroll
+      for (int c = 0; c < KCH; ++c) {
+        const int g = c * 4 + wv;
+        const int off = (min(g, nchunk - 1) << 9) + lane * 8;
+        float a[8], b[8];
+        unpack8(ld16(om + off), a);
+        unpack8(ld16(rm + off), b);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) a[j] += b[j];
+        const uint4 packed = pack8(a);  // the residual stream stays bf16: round once
+        unpack8(packed, a);
+        float s = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s += a[j] * a[j];
+        ss[m] += g < nchunk ? s : 0.f;
+        xr[m][c] = __builtin_bit_cast(u32x4, packed);
+        if (blockIdx.x == 0 && g < nchunk && m < T) st16(pro.res_out + (int64_t)m * K + off, packed);
+      }
+      ss[m] = wave_sum(ss[m]);
+    }
+    if (lane == 0) {
+#pragma unroll
+      for (int m = 0; m < TR; ++m) pro_red[wv][m] = ss[m];
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+#pragma unroll
+    for (int m = 0; m < TR; ++m)
+      ss[m] = rsqrtf((pro_red[0][m] + pro_red[1][m] + pro_red[2][m] + pro_red[3][m]) / K + pro.eps);
+#pragma unroll
+    for (int c = 0; c < KCH; ++c) {
+      const int g = c * 4 + wv;
+      float wf[8];
+      unpack8(ld16(pro.norm_w + (min(g, nchunk - 1) << 9) + lane * 8), wf);
+#pragma unroll
+      for (int m = 0; m < TR; ++m) {
+        float a[8];
+        unpack8(__builtin_bit_cast(uint4, xr[m][c]), a);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) a[j] = a[j] * ss[m] * wf[j];
+        xr[m][c] = g < nchunk ? __builtin_bit_cast(u32x4, pack8(a)) : u32x4{0, 0, 0, 0};
+      }
+    }
+  } else {
+    // ---- x fragments: chunk c of this wave = global chunk c*4 + wv
+#pragma unroll
+    for (int m = 0; m < TR; ++m) {
+      const bf16* xm = x + (int64_t)min(m, T - 1) * K;
+#pragma unroll
+      for (int c = 0; c < KCH; ++c) {
+        // branch-free tail: a chunk past K reloads the last one and is zeroed by a select, so
+        // no load sits behind control flow (which made the compiler drain vmcnt per row)
+        const int g = c * 4 + wv;
+        const u32x4 v = *reinterpret_cast<const u32x4*>(xm + (min(g, nchunk - 1) << 9) + lane * 8);
+        xr[m][c] = g < nchunk ? v : u32x4{0, 0, 0, 0};
+      }
+    }
+    // ---- W rows of this block
+#pragma unroll
+    for (int r = 0; r < RB; ++r) {
+      const int row = EPI == EPI_SILU ? (r < HALF ? base + r : F + base + r - HALF) : base + r;
+      const bf16* wrow = W + (int64_t)row * K + lane * 8;
+#pragma unroll
+      for (int c = 0; c < KCH; ++c)
+        wr[r][c] =
+            __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(wrow + (min(c * 4 + wv, nchunk - 1) << 9)));
+    }
   }
   float acc[RB][TR];
 #pragma unroll
@@ -118,6 +209,25 @@ __global__ void __launch_bounds__(256) gemv_kernel(const bf16* __restrict__ x, i
         out[(int64_t)m * ldo + base + r] = (bf16)(gb / (1.f + __expf(-gb)) * ub);
       }
     }
+  } else if (EPI == EPI_ADDNORM) {
+    // hand-off payload stored write-through (sc1: 8-byte agent-scope atomic stores of 4 packed
+    // bf16), so no block needs a release fence (an agent release = an L2 writeback in each of
+    // the 512-1024 blocks measured 4.3 vs 3.5 ms per batch-1 step); guide §6 Guideline 16 R1
+    const int t = threadIdx.x;
+    constexpr int G = RB / 4;  // 8-byte groups per output row
+    if (t < TR * G) {
+      const int m = t / G, gq = t % G;
+      if (m < T) {
+        bf16x4 v;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int i = (gq * 4 + j) * TR + m;
+          v[j] = (bf16)(red[0][i] + red[1][i] + red[2][i] + red[3][i]);
+        }
+        __hip_atomic_store(reinterpret_cast<unsigned long long*>(out + (int64_t)m * ldo + base + gq * 4),
+                           __builtin_bit_cast(unsigned long long, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
   } else {
     const int t = threadIdx.x;
     if (t < RB * TR) {
@@ -125,10 +235,59 @@ __global__ void __launch_bounds__(256) gemv_kernel(const bf16* __restrict__ x, i
       if (m < T) out[(int64_t)m * ldo + base + r] = (bf16)(red[0][t] + red[1][t] + red[2][t] + red[3][t]);
     }
   }
+  if constexpr (EPI == EPI_ADDNORM) {
+    // ---- ticket: every storing wave drains, then one relaxed agent-scope add; the last
+    // block acquires and runs the add + RMSNorm
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const unsigned int prev = __hip_atomic_fetch_add(an.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      red[0][0] = (prev == gridDim.x - 1) ? 1.f : 0.f;  // "I am last", through the one LDS array
+      if (prev == gridDim.x - 1) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+    }
+    __syncthreads();
+    if (red[0][0] == 0.f) return;
+    __syncthreads();  // every thread has read the flag before red is reused below
+    for (int m = 0; m < T; ++m) {
+      bf16* orow = out + (int64_t)m * ldo;
+      bf16* rrow = an.residual + (int64_t)m * N;
+      float ss = 0.f;
+      for (int c = threadIdx.x; c < (N >> 3); c += blockDim.x) {
+        float a[8], b[8];
+        unpack8(ld16(orow + c * 8), a);
+        unpack8(ld16(rrow + c * 8), b);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) a[j] += b[j];
+        const uint4 packed = pack8(a);
+        st16(rrow + c * 8, packed);
+        unpack8(packed, a);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ss += a[j] * a[j];
+      }
+      ss = wave_sum(ss);
+      __syncthreads();
+      if (lane == 0) red[1][wv] = ss;
+      __syncthreads();
+      const float inv = rsqrtf((red[1][0] + red[1][1] + red[1][2] + red[1][3]) / N + an.eps);
+      for (int c = threadIdx.x; c < (N >> 3); c += blockDim.x) {
+        float a[8], wf[8];
+        unpack8(ld16(rrow + c * 8), a);  // this thread's own rounded residual
+        unpack8(ld16(an.norm_w + c * 8), wf);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) a[j] = a[j] * inv * wf[j];
+        st16(orow + c * 8, pack8(a));
+      }
+    }
+    if (threadIdx.x == 0) __hip_atomic_store(an.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
-template <int TR, int KCH, int EPI>
-void launch_rb(const at::Tensor& x, const at::Tensor& w, at::Tensor& out, int T, int N, int K, hipStream_t st) {
+template <int TR, int KCH, int EPI, bool PRO>
+void launch_rb(const at::Tensor& x, const at::Tensor& w, at::Tensor& out, int T, int N, int K, hipStream_t st,
+               AddNorm an, ProNorm pro) {
   // the compiler streams W through a rolling window of ~8 loads per wave, so RB sets the
   // rows sharing one x fetch + reduction, not the VGPR count (RB = 2 at K = 14336, T = 4
   // measured 0.7x hipBLASLt; profiles/gemv_bench.log)
@@ -136,26 +295,29 @@ void launch_rb(const at::Tensor& x, const at::Tensor& w, at::Tensor& out, int T,
   const int rows_per_block = EPI == EPI_SILU ? RB / 2 : RB;
   const int nrows = EPI == EPI_SILU ? N / 2 : N;
   TORCH_CHECK(nrows % rows_per_block == 0, "gemv: output rows must be a multiple of ", rows_per_block);
-  gemv_kernel<TR, KCH, RB, EPI><<<nrows / rows_per_block, 256, 0, st>>>(
-      (const bf16*)x.data_ptr(), T, (const bf16*)w.data_ptr(), N, K, (bf16*)out.data_ptr(), (int)out.stride(0));
+  gemv_kernel<TR, KCH, RB, EPI, PRO><<<nrows / rows_per_block, 256, 0, st>>>(
+      (const bf16*)x.data_ptr(), T, (const bf16*)w.data_ptr(), N, K, (bf16*)out.data_ptr(), (int)out.stride(0), an,
+      pro);
 }
 
-template <int TR, int EPI>
-void launch_k(const at::Tensor& x, const at::Tensor& w, at::Tensor& out, int T, int N, int K, hipStream_t st) {
+template <int TR, int EPI, bool PRO>
+void launch_k(const at::Tensor& x, const at::Tensor& w, at::Tensor& out, int T, int N, int K, hipStream_t st,
+              AddNorm an, ProNorm pro) {
   switch ((K + 2047) / 2048) {
-    case 1: return launch_rb<TR, 1, EPI>(x, w, out, T, N, K, st);
-    case 2: return launch_rb<TR, 2, EPI>(x, w, out, T, N, K, st);
-    case 3: return launch_rb<TR, 3, EPI>(x, w, out, T, N, K, st);
-    case 4: return launch_rb<TR, 4, EPI>(x, w, out, T, N, K, st);
-    case 5: return launch_rb<TR, 5, EPI>(x, w, out, T, N, K, st);
-    case 6: return launch_rb<TR, 6, EPI>(x, w, out, T, N, K, st);
-    case 7: return launch_rb<TR, 7, EPI>(x, w, out, T, N, K, st);
+    case 1: return launch_rb<TR, 1, EPI, PRO>(x, w, out, T, N, K, st, an, pro);
+    case 2: return launch_rb<TR, 2, EPI, PRO>(x, w, out, T, N, K, st, an, pro);
+    case 3: return launch_rb<TR, 3, EPI, PRO>(x, w, out, T, N, K, st, an, pro);
+    case 4: return launch_rb<TR, 4, EPI, PRO>(x, w, out, T, N, K, st, an, pro);
+    case 5: return launch_rb<TR, 5, EPI, PRO>(x, w, out, T, N, K, st, an, pro);
+    case 6: return launch_rb<TR, 6, EPI, PRO>(x, w, out, T, N, K, st, an, pro);
+    case 7: return launch_rb<TR, 7, EPI, PRO>(x, w, out, T, N, K, st, an, pro);
     default: TORCH_CHECK(false, "gemv: K = ", K, " > 14336 is not supported");
   }
 }
 
-template <int EPI>
-void gemv_dispatch(at::Tensor out, const at::Tensor& x, const at::Tensor& w) {
+template <int EPI, bool PRO = false>
+void gemv_dispatch(at::Tensor out, const at::Tensor& x, const at::Tensor& w, AddNorm an = AddNorm{},
+                   ProNorm pro = ProNorm{}) {
   TORCH_CHECK(x.is_cuda() && w.is_cuda() && out.is_cuda(), "gemv: CUDA tensors expected");
   TORCH_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16 &&
                   out.scalar_type() == at::kBFloat16, "gemv: bf16 tensors expected");
@@ -165,14 +327,29 @@ void gemv_dispatch(at::Tensor out, const at::Tensor& x, const at::Tensor& w) {
   TORCH_CHECK(w.size(1) == K, "gemv: K mismatch");
   TORCH_CHECK(T >= 1 && T <= 4, "gemv: 1 <= T <= 4");
   TORCH_CHECK(K % 512 == 0, "gemv: K must be a multiple of 512");
-  TORCH_CHECK(out.dim() == 2 && out.size(0) == T && out.stride(1) == 1 && out.size(1) == (EPI ? N / 2 : N),
-              "gemv: bad output shape");
+  TORCH_CHECK(out.dim() == 2 && out.size(0) == T && out.stride(1) == 1 &&
+                  out.size(1) == (EPI == EPI_SILU ? N / 2 : N), "gemv: bad output shape");
   auto st = at::hip::getCurrentHIPStream();
   switch (T) {
-    case 1: return launch_k<1, EPI>(x, w, out, T, N, K, st);
-    case 2: return launch_k<2, EPI>(x, w, out, T, N, K, st);
-    default: return launch_k<4, EPI>(x, w, out, T, N, K, st);
+    case 1: return launch_k<1, EPI, PRO>(x, w, out, T, N, K, st, an, pro);
+    case 2: return launch_k<2, EPI, PRO>(x, w, out, T, N, K, st, an, pro);
+    default: return launch_k<4, EPI, PRO>(x, w, out, T, N, K, st, an, pro);
   }
+}
+
+template <int EPI>
+void gemv_norm_dispatch(at::Tensor out, const at::Tensor& o, const at::Tensor& res, at::Tensor res_out,
+                        const at::Tensor& norm_w, double eps, const at::Tensor& w) {
+  TORCH_CHECK(res.scalar_type() == at::kBFloat16 && res_out.scalar_type() == at::kBFloat16 &&
+                  norm_w.scalar_type() == at::kBFloat16, "gemv_norm: bf16 operands");
+  TORCH_CHECK(res.is_contiguous() && res_out.is_contiguous() && norm_w.is_contiguous() && o.is_contiguous(),
+              "gemv_norm: contiguous operands");
+  TORCH_CHECK(res.sizes() == o.sizes() && res_out.sizes() == o.sizes() && norm_w.numel() == o.size(1),
+              "gemv_norm: o / residual / norm shapes");
+  TORCH_CHECK(res_out.data_ptr() != res.data_ptr(), "gemv_norm: res_out must not alias res");
+  gemv_dispatch<EPI, true>(out, o, w, AddNorm{},
+                           ProNorm{(const bf16*)o.data_ptr(), (const bf16*)res.data_ptr(), (bf16*)res_out.data_ptr(),
+                                   (const bf16*)norm_w.data_ptr(), (float)eps});
 }
 
 }  // namespace
@@ -182,6 +359,31 @@ void gemv(at::Tensor out, at::Tensor x, at::Tensor w) { gemv_dispatch<EPI_NONE>(
 
 // out[T, F] = silu(x @ w[:F]^T) * (x @ w[F:]^T) for the fused gate_up weight w [2F, K].
 void gemv_silu(at::Tensor out, at::Tensor x, at::Tensor w) { gemv_dispatch<EPI_SILU>(out, x, w); }
+
+// Prologue-fused forms: the input is x = rmsnorm(o + res) * norm_w (the fused_add_rmsnorm
+// that follows the previous projection), res_out = bf16(o + res).
+void gemv_norm(at::Tensor out, at::Tensor o, at::Tensor res, at::Tensor res_out, at::Tensor norm_w, double eps,
+               at::Tensor w) {
+  gemv_norm_dispatch<EPI_NONE>(out, o, res, res_out, norm_w, eps, w);
+}
+void gemv_silu_norm(at::Tensor out, at::Tensor o, at::Tensor res, at::Tensor res_out, at::Tensor norm_w, double eps,
+                    at::Tensor w) {
+  gemv_norm_dispatch<EPI_SILU>(out, o, res, res_out, norm_w, eps, w);
+}
+
+// out = rmsnorm(residual += x @ w^T) * norm_w with the rounding of gemv + fused_add_rmsnorm;
+// `counter` is a zero-initialised int32 word owned by the caller (one launch at a time).
+void gemv_add_rmsnorm(at::Tensor out, at::Tensor x, at::Tensor w, at::Tensor residual, at::Tensor norm_w,
+                      double eps, at::Tensor counter) {
+  TORCH_CHECK(residual.scalar_type() == at::kBFloat16 && norm_w.scalar_type() == at::kBFloat16 &&
+                  residual.is_contiguous() && norm_w.is_contiguous() && out.is_contiguous(),
+              "gemv_add_rmsnorm: bf16 contiguous operands");
+  TORCH_CHECK(residual.numel() == out.numel() && norm_w.numel() == w.size(0), "gemv_add_rmsnorm: shapes");
+  TORCH_CHECK(counter.is_cuda() && counter.scalar_type() == at::kInt && counter.numel() >= 1, "counter: int32");
+  gemv_dispatch<EPI_ADDNORM>(out, x, w,
+                             AddNorm{(bf16*)residual.data_ptr(), (const bf16*)norm_w.data_ptr(),
+                                     (unsigned int*)counter.data_ptr(), (float)eps});
+}
 
 // Whether the GEMV path supports this weight (host-side shape rule used by the runner).
 bool gemv_supported(const at::Tensor& w, bool silu) {

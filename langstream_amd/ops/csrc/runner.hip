@@ -65,6 +65,10 @@ void skinny_gemm(at::Tensor out, at::Tensor x, at::Tensor w);
 void gemv(at::Tensor out, at::Tensor x, at::Tensor w);
 void gemv_silu(at::Tensor out, at::Tensor x, at::Tensor w);
 bool gemv_supported(const at::Tensor& w, bool silu);
+void gemv_norm(at::Tensor out, at::Tensor o, at::Tensor res, at::Tensor res_out, at::Tensor norm_w, double eps,
+               at::Tensor w);
+void gemv_silu_norm(at::Tensor out, at::Tensor o, at::Tensor res, at::Tensor res_out, at::Tensor norm_w, double eps,
+                    at::Tensor w);
 void skinny_gemm_add_rmsnorm(at::Tensor out, at::Tensor x, at::Tensor w, at::Tensor residual, at::Tensor norm_w,
                              double eps);
 
@@ -132,7 +136,51 @@ class LlamaRunner {
     // (ops/csrc/gemm_gemv.hip) for all four projections, gate_up with silu*up fused; it
     // fuses no residual, so it also serves tensor-parallel ranks.
     const bool gv = gemv_enabled() && T <= 4;
-    for (int64_t l = 0; l < L; ++l) {
+    auto attend = [&](int64_t l, const at::Tensor& qkv) {
+      rope_and_cache(qkv, pos, cos_sin_, slots, kc_[l], vc_[l], hq_, hkv_, true);
+      at::Tensor q = qkv.narrow(1, 0, hq_ * d_);
+      at::Tensor attn = at::empty({T, hq_ * d_}, qkv.options());
+      if (num_decode > 0)
+        paged_decode_attention(attn.narrow(0, 0, num_decode), q.narrow(0, 0, num_decode), kc_[l], vc_[l], d_bt,
+                               d_ctx, scale_, nsplit, bps, ws);
+      if (num_prefill > 0)
+        paged_prefill_attention(attn, q, kc_[l], vc_[l], p_bt, q_start, q_len, ctx_len, tiles, hq_, scale_);
+      return attn;
+    };
+    // TP = 1: the residual add + RMSNorm after o_proj and down_proj run in the PROLOGUE of
+    // the next GEMV (gate_up / the next layer's qkv), which recomputes the norm per block
+    // from the L2-resident activations -- no separate norm kernels or hand-offs.  (A
+    // last-block add+norm epilogue with an agent-scope ticket measured slower: 3.72 vs
+    // 3.48 ms per batch-1 step, the serial tail outweighs the launch it saves.)
+    bool fused = gv && !pg_;
+    for (int64_t l = 0; l < L && fused; ++l)
+      fused = gemv_supported(qkv_w_[l], false) && gemv_supported(o_w_[l], false) &&
+              gemv_supported(gate_up_w_[l], true) && gemv_supported(down_w_[l], false);
+    if (fused) {
+      at::Tensor dn;
+      for (int64_t l = 0; l < L; ++l) {
+        at::Tensor qkv = at::empty({T, qkv_w_[l].size(0)}, x.options());
+        if (l == 0) {
+          gemv(qkv, x, qkv_w_[l]);
+        } else {
+          at::Tensor rn = at::empty_like(residual);
+          gemv_norm(qkv, dn, residual, rn, in_norm_[l], eps_, qkv_w_[l]);
+          residual = rn;
+        }
+        at::Tensor attn = attend(l, qkv);
+        at::Tensor o = at::empty_like(residual);
+        gemv(o, attn, o_w_[l]);
+        at::Tensor a = at::empty({T, gate_up_w_[l].size(0) / 2}, o.options());
+        at::Tensor rn = at::empty_like(residual);
+        gemv_silu_norm(a, o, residual, rn, post_norm_[l], eps_, gate_up_w_[l]);
+        residual = rn;
+        dn = at::empty_like(residual);
+        gemv(dn, a, down_w_[l]);
+      }
+      fused_add_rmsnorm(dn, residual, final_norm_, eps_);
+      x = dn;
+    }
+    for (int64_t l = 0; l < L && !fused; ++l) {
       at::Tensor qkv;
       if (gv && gemv_supported(qkv_w_[l], false)) {
         qkv = at::empty({T, qkv_w_[l].size(0)}, x.options());

@@ -344,3 +344,44 @@ def test_gemv_silu(T, F, K):
     gu = (x.float().cpu() @ w.float().cpu().t()).to(torch.bfloat16).float()
     exp = torch.nn.functional.silu(gu[:, :F]) * gu[:, F:]
     _close(out, exp, 0.03, 0.03)
+
+
+@pytest.mark.parametrize("T,N,K", [(1, 4096, 4096), (2, 4096, 14336), (4, 1024, 2048)])
+def test_gemv_add_rmsnorm(T, N, K):
+    torch.manual_seed(T + N + K)
+    x = torch.randn(T, K, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=DEV) * 0.05).to(torch.bfloat16)
+    res = torch.randn(T, N, device=DEV).to(torch.bfloat16)
+    nw = (1 + 0.1 * torch.randn(N, device=DEV)).to(torch.bfloat16)
+    ticket = torch.zeros(1, dtype=torch.int32, device=DEV)
+    for rep in range(3):   # the ticket word must come back to 0 after every launch
+        r = res.clone()
+        out = torch.empty(T, N, device=DEV, dtype=torch.bfloat16)
+        ops.hip().gemv_add_rmsnorm(out, x, w, r, nw, 1e-5, ticket)
+        o = (x.float().cpu() @ w.float().cpu().t()).to(torch.bfloat16).float()
+        er = (o + res.float().cpu()).to(torch.bfloat16).float()
+        eo = er * torch.rsqrt(er.pow(2).mean(-1, keepdim=True) + 1e-5) * nw.float().cpu()
+        _close(r, er, 0.03, 0.02)
+        _close(out, eo, 0.03, 0.03)
+        assert int(ticket.item()) == 0
+
+
+@pytest.mark.parametrize("silu", [False, True])
+@pytest.mark.parametrize("T,N,K", [(1, 6144, 4096), (3, 1024, 2048), (4, 512, 14336)])
+def test_gemv_prologue_norm(silu, T, N, K):
+    torch.manual_seed(T + N + K + silu)
+    o = torch.randn(T, K, device=DEV).to(torch.bfloat16)
+    res = torch.randn(T, K, device=DEV).to(torch.bfloat16)
+    nw = (1 + 0.1 * torch.randn(K, device=DEV)).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=DEV) * 0.05).to(torch.bfloat16)
+    res_out = torch.empty_like(res)
+    out = torch.empty(T, N // 2 if silu else N, device=DEV, dtype=torch.bfloat16)
+    (ops.hip().gemv_silu_norm if silu else ops.hip().gemv_norm)(out, o, res, res_out, nw, 1e-5, w)
+    er = (o.float().cpu() + res.float().cpu()).to(torch.bfloat16).float()
+    x = (er * torch.rsqrt(er.pow(2).mean(-1, keepdim=True) + 1e-5) * nw.float().cpu()).to(torch.bfloat16).float()
+    y = x @ w.float().cpu().t()
+    if silu:
+        y = y.to(torch.bfloat16).float()
+        y = torch.nn.functional.silu(y[:, : N // 2]) * y[:, N // 2:]
+    _close(res_out, er, 0.02, 0.01)
+    _close(out, y, 0.05, 0.03)
