@@ -36,6 +36,10 @@ void gemv_norm(at::Tensor out, at::Tensor o, at::Tensor res, at::Tensor res_out,
                at::Tensor w);
 void gemv_silu_norm(at::Tensor out, at::Tensor o, at::Tensor res, at::Tensor res_out, at::Tensor norm_w, double eps,
                     at::Tensor w);
+void gemv_qkv(at::Tensor out, at::Tensor x, at::Tensor w, at::Tensor pos, at::Tensor cos_sin, at::Tensor slots,
+              at::Tensor k_cache, at::Tensor v_cache, int64_t Hq, int64_t Hkv, bool apply_rope,
+              c10::optional<at::Tensor> o, c10::optional<at::Tensor> res, c10::optional<at::Tensor> res_out,
+              c10::optional<at::Tensor> norm_w, double eps);
 void skinny_gemm_silu(at::Tensor out, at::Tensor x, at::Tensor w);
 void skinny_gemm_add_rmsnorm(at::Tensor out, at::Tensor x, at::Tensor w, at::Tensor residual, at::Tensor norm_w,
                              double eps);
@@ -64,6 +68,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemv_add_rmsnorm", &gemv_add_rmsnorm);
   m.def("gemv_norm", &gemv_norm);
   m.def("gemv_silu_norm", &gemv_silu_norm);
+  m.def("gemv_qkv", &gemv_qkv);
   m.def("skinny_gemm_silu", &skinny_gemm_silu);
   m.def("skinny_gemm_add_rmsnorm", &skinny_gemm_add_rmsnorm);
   bind_runners(m);

@@ -28,7 +28,7 @@ namespace {
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int EPI_NONE = 0, EPI_SILU = 1, EPI_ADDNORM = 2;
+constexpr int EPI_NONE = 0, EPI_SILU = 1, EPI_ADDNORM = 2, EPI_QKV = 3;
 
 // EPI_ADDNORM operands: after the projection, residual = bf16(out + residual) and
 // out = bf16(rmsnorm(residual) * norm_w) -- the fused_add_rmsnorm of norm.hip -- done by
@@ -52,6 +52,20 @@ struct ProNorm {
   float eps;
 };
 
+// EPI_QKV operands: W is the fused qkv projection [(Hq + 2 Hkv) * D, K]; each block owns
+// RB/2 rotary pairs (d, d + D/2) of one head, so the epilogue applies RoPE to q and k heads
+// and writes k to the paged K cache [NB, Hkv, BS, D] and v transposed to the V cache
+// [NB, Hkv, D, BS] -- the rope_cache kernel of rope.hip, fused (same bf16 rounding).
+struct QkvEpi {
+  const int32_t* pos;
+  const float* cos_sin;  // [max_pos, D]: cols [0, D/2) cos, [D/2, D) sin
+  const int64_t* slots;  // [T] cache slot, -1 = not cached
+  bf16* kc;
+  bf16* vc;
+  int64_t nslots;
+  int Hq, Hkv, BS, D, max_pos, apply_rope;
+};
+
 // 8-element bf16 dot on v_dot2c_f32_bf16.  The pairs are taken with shufflevector on the
 // whole 16-B value: bit-casting extracted u32 elements (a.y, a[1], ...) is miscompiled by
 // this hipcc (every pair reads element 0; checked in the ISA).
@@ -73,12 +87,20 @@ __device__ __forceinline__ float dot8(u32x4 a, u32x4 b, float acc) {
 template <int TR, int KCH, int RB, int EPI, bool PRO>
 __global__ void __launch_bounds__(256) gemv_kernel(const bf16* __restrict__ x, int T, const bf16* __restrict__ W,
                                                    int N, int K, bf16* __restrict__ out, int ldo, AddNorm an,
-                                                   ProNorm pro) {
+                                                   ProNorm pro, QkvEpi qe) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int nchunk = K >> 9;  // K % 512 == 0 (host-checked)
   constexpr int HALF = RB / 2;
   const int F = N >> 1;
   const int base = blockIdx.x * (EPI == EPI_SILU ? HALF : RB);
+  // EPI_QKV: head and first rotary index of this block's HALF pairs
+  const int qk_bph = EPI == EPI_QKV ? (qe.D / 2) / HALF : 1;
+  const int qk_head = blockIdx.x / qk_bph, qk_j0 = (blockIdx.x % qk_bph) * HALF;
+  auto w_row = [&](int r) -> int {
+    if constexpr (EPI == EPI_SILU) return r < HALF ? base + r : F + base + r - HALF;
+    else if constexpr (EPI == EPI_QKV) return qk_head * qe.D + (r < HALF ? qk_j0 + r : qe.D / 2 + qk_j0 + r - HALF);
+    else return base + r;
+  };
   u32x4 wr[RB][KCH];
   u32x4 xr[TR][KCH];
   if constexpr (PRO) {
@@ -88,7 +110,7 @@ __global__ void __launch_bounds__(256) gemv_kernel(const bf16* __restrict__ x, i
     // they are in flight during the norm; a raw s_barrier keeps them outstanding.
 #pragma unroll
     for (int r = 0; r < RB; ++r) {
-      const int row = EPI == EPI_SILU ? (r < HALF ? base + r : F + base + r - HALF) : base + r;
+      const int row = w_row(r);
       const bf16* wrow = W + (int64_t)row * K + lane * 8;
 #pragma unroll
       for (int c = 0; c < KCH; ++c)
@@ -163,7 +185,7 @@ __global__ void __launch_bounds__(256) gemv_kernel(const bf16* __restrict__ x, i
     // ---- W rows of this block
 #pragma unroll
     for (int r = 0; r < RB; ++r) {
-      const int row = EPI == EPI_SILU ? (r < HALF ? base + r : F + base + r - HALF) : base + r;
+      const int row = w_row(r);
       const bf16* wrow = W + (int64_t)row * K + lane * 8;
 #pragma unroll
       for (int c = 0; c < KCH; ++c)
@@ -197,7 +219,45 @@ __global__ void __launch_bounds__(256) gemv_kernel(const bf16* __restrict__ x, i
       for (int m = 0; m < TR; ++m) red[wv][r * TR + m] = acc[r][m];
   }
   __syncthreads();
-  if (EPI == EPI_SILU) {
+  if constexpr (EPI == EPI_QKV) {
+    const int t = threadIdx.x;
+    if (t < HALF * TR) {
+      const int u = t / TR, m = t % TR;
+      if (m < T) {
+        const int hd = qe.D / 2;
+        const int i1 = u * TR + m, i2 = (u + HALF) * TR + m;
+        // the unfused path rounds the projection to bf16 before rotating
+        float a = (float)(bf16)(red[0][i1] + red[1][i1] + red[2][i1] + red[3][i1]);
+        float b = (float)(bf16)(red[0][i2] + red[1][i2] + red[2][i2] + red[3][i2]);
+        const int d1 = qk_j0 + u, d2 = hd + qk_j0 + u;
+        const bool rot = qe.apply_rope && qk_head < qe.Hq + qe.Hkv;
+        if (rot) {
+          const int p = min(max(qe.pos[m], 0), qe.max_pos - 1);
+          const float co = qe.cos_sin[(int64_t)p * qe.D + d1], si = qe.cos_sin[(int64_t)p * qe.D + hd + d1];
+          const float x1 = a, x2 = b;
+          a = x1 * co - x2 * si;
+          b = x2 * co + x1 * si;
+        }
+        const bf16 ab = (bf16)a, bb = (bf16)b;
+        bf16* orow = out + (int64_t)m * ldo + qk_head * qe.D;
+        orow[d1] = ab;
+        orow[d2] = bb;
+        const int64_t s = qe.slots[m];
+        if (qk_head >= qe.Hq && s >= 0 && s < qe.nslots) {
+          const int64_t blk = s / qe.BS, off = s - blk * qe.BS;
+          if (qk_head < qe.Hq + qe.Hkv) {
+            bf16* kd = qe.kc + ((blk * qe.Hkv + (qk_head - qe.Hq)) * qe.BS + off) * qe.D;
+            kd[d1] = ab;
+            kd[d2] = bb;
+          } else {
+            bf16* vd = qe.vc + (blk * qe.Hkv + (qk_head - qe.Hq - qe.Hkv)) * (int64_t)qe.D * qe.BS + off;
+            vd[(int64_t)d1 * qe.BS] = ab;
+            vd[(int64_t)d2 * qe.BS] = bb;
+          }
+        }
+      }
+    }
+  } else if (EPI == EPI_SILU) {
     const int t = threadIdx.x;
     if (t < HALF * TR) {
       const int r = t / TR, m = t % TR;
@@ -285,9 +345,15 @@ __global__ void __launch_bounds__(256) gemv_kernel(const bf16* __restrict__ x, i
   }
 }
 
+struct Extra {
+  AddNorm an{};
+  ProNorm pro{};
+  QkvEpi qe{};
+};
+
 template <int TR, int KCH, int EPI, bool PRO>
 void launch_rb(const at::Tensor& x, const at::Tensor& w, at::Tensor& out, int T, int N, int K, hipStream_t st,
-               AddNorm an, ProNorm pro) {
+               const Extra& ex) {
   // the compiler streams W through a rolling window of ~8 loads per wave, so RB sets the
   // rows sharing one x fetch + reduction, not the VGPR count (RB = 2 at K = 14336, T = 4
   // measured 0.7x hipBLASLt; profiles/gemv_bench.log)
@@ -295,29 +361,29 @@ void launch_rb(const at::Tensor& x, const at::Tensor& w, at::Tensor& out, int T,
   const int rows_per_block = EPI == EPI_SILU ? RB / 2 : RB;
   const int nrows = EPI == EPI_SILU ? N / 2 : N;
   TORCH_CHECK(nrows % rows_per_block == 0, "gemv: output rows must be a multiple of ", rows_per_block);
+  if (EPI == EPI_QKV) TORCH_CHECK((ex.qe.D / 2) % (RB / 2) == 0, "gemv_qkv: head_dim / 2 must divide by ", RB / 2);
   gemv_kernel<TR, KCH, RB, EPI, PRO><<<nrows / rows_per_block, 256, 0, st>>>(
-      (const bf16*)x.data_ptr(), T, (const bf16*)w.data_ptr(), N, K, (bf16*)out.data_ptr(), (int)out.stride(0), an,
-      pro);
+      (const bf16*)x.data_ptr(), T, (const bf16*)w.data_ptr(), N, K, (bf16*)out.data_ptr(), (int)out.stride(0), ex.an,
+      ex.pro, ex.qe);
 }
 
 template <int TR, int EPI, bool PRO>
 void launch_k(const at::Tensor& x, const at::Tensor& w, at::Tensor& out, int T, int N, int K, hipStream_t st,
-              AddNorm an, ProNorm pro) {
+              const Extra& ex) {
   switch ((K + 2047) / 2048) {
-    case 1: return launch_rb<TR, 1, EPI, PRO>(x, w, out, T, N, K, st, an, pro);
-    case 2: return launch_rb<TR, 2, EPI, PRO>(x, w, out, T, N, K, st, an, pro);
-    case 3: return launch_rb<TR, 3, EPI, PRO>(x, w, out, T, N, K, st, an, pro);
-    case 4: return launch_rb<TR, 4, EPI, PRO>(x, w, out, T, N, K, st, an, pro);
-    case 5: return launch_rb<TR, 5, EPI, PRO>(x, w, out, T, N, K, st, an, pro);
-    case 6: return launch_rb<TR, 6, EPI, PRO>(x, w, out, T, N, K, st, an, pro);
-    case 7: return launch_rb<TR, 7, EPI, PRO>(x, w, out, T, N, K, st, an, pro);
+    case 1: return launch_rb<TR, 1, EPI, PRO>(x, w, out, T, N, K, st, ex);
+    case 2: return launch_rb<TR, 2, EPI, PRO>(x, w, out, T, N, K, st, ex);
+    case 3: return launch_rb<TR, 3, EPI, PRO>(x, w, out, T, N, K, st, ex);
+    case 4: return launch_rb<TR, 4, EPI, PRO>(x, w, out, T, N, K, st, ex);
+    case 5: return launch_rb<TR, 5, EPI, PRO>(x, w, out, T, N, K, st, ex);
+    case 6: return launch_rb<TR, 6, EPI, PRO>(x, w, out, T, N, K, st, ex);
+    case 7: return launch_rb<TR, 7, EPI, PRO>(x, w, out, T, N, K, st, ex);
     default: TORCH_CHECK(false, "gemv: K = ", K, " > 14336 is not supported");
   }
 }
 
 template <int EPI, bool PRO = false>
-void gemv_dispatch(at::Tensor out, const at::Tensor& x, const at::Tensor& w, AddNorm an = AddNorm{},
-                   ProNorm pro = ProNorm{}) {
+void gemv_dispatch(at::Tensor out, const at::Tensor& x, const at::Tensor& w, const Extra& ex = Extra{}) {
   TORCH_CHECK(x.is_cuda() && w.is_cuda() && out.is_cuda(), "gemv: CUDA tensors expected");
   TORCH_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16 &&
                   out.scalar_type() == at::kBFloat16, "gemv: bf16 tensors expected");
@@ -331,15 +397,14 @@ void gemv_dispatch(at::Tensor out, const at::Tensor& x, const at::Tensor& w, Add
                   out.size(1) == (EPI == EPI_SILU ? N / 2 : N), "gemv: bad output shape");
   auto st = at::hip::getCurrentHIPStream();
   switch (T) {
-    case 1: return launch_k<1, EPI, PRO>(x, w, out, T, N, K, st, an, pro);
-    case 2: return launch_k<2, EPI, PRO>(x, w, out, T, N, K, st, an, pro);
-    default: return launch_k<4, EPI, PRO>(x, w, out, T, N, K, st, an, pro);
+    case 1: return launch_k<1, EPI, PRO>(x, w, out, T, N, K, st, ex);
+    case 2: return launch_k<2, EPI, PRO>(x, w, out, T, N, K, st, ex);
+    default: return launch_k<4, EPI, PRO>(x, w, out, T, N, K, st, ex);
   }
 }
 
-template <int EPI>
-void gemv_norm_dispatch(at::Tensor out, const at::Tensor& o, const at::Tensor& res, at::Tensor res_out,
-                        const at::Tensor& norm_w, double eps, const at::Tensor& w) {
+ProNorm make_pro(const at::Tensor& o, const at::Tensor& res, const at::Tensor& res_out, const at::Tensor& norm_w,
+                 double eps) {
   TORCH_CHECK(res.scalar_type() == at::kBFloat16 && res_out.scalar_type() == at::kBFloat16 &&
                   norm_w.scalar_type() == at::kBFloat16, "gemv_norm: bf16 operands");
   TORCH_CHECK(res.is_contiguous() && res_out.is_contiguous() && norm_w.is_contiguous() && o.is_contiguous(),
@@ -347,9 +412,32 @@ void gemv_norm_dispatch(at::Tensor out, const at::Tensor& o, const at::Tensor& r
   TORCH_CHECK(res.sizes() == o.sizes() && res_out.sizes() == o.sizes() && norm_w.numel() == o.size(1),
               "gemv_norm: o / residual / norm shapes");
   TORCH_CHECK(res_out.data_ptr() != res.data_ptr(), "gemv_norm: res_out must not alias res");
-  gemv_dispatch<EPI, true>(out, o, w, AddNorm{},
-                           ProNorm{(const bf16*)o.data_ptr(), (const bf16*)res.data_ptr(), (bf16*)res_out.data_ptr(),
-                                   (const bf16*)norm_w.data_ptr(), (float)eps});
+  return ProNorm{(const bf16*)o.data_ptr(), (const bf16*)res.data_ptr(), (bf16*)res_out.data_ptr(),
+                 (const bf16*)norm_w.data_ptr(), (float)eps};
+}
+
+QkvEpi make_qkv(const at::Tensor& out, const at::Tensor& pos, const at::Tensor& cos_sin, const at::Tensor& slots,
+                const at::Tensor& kc, const at::Tensor& vc, int64_t Hq, int64_t Hkv, bool apply_rope) {
+  TORCH_CHECK(pos.scalar_type() == at::kInt && slots.scalar_type() == at::kLong && cos_sin.scalar_type() == at::kFloat &&
+                  cos_sin.is_contiguous(), "gemv_qkv: pos int32, slots int64, cos_sin f32");
+  TORCH_CHECK(kc.dim() == 4 && vc.dim() == 4 && kc.scalar_type() == at::kBFloat16 && vc.scalar_type() == at::kBFloat16,
+              "gemv_qkv: paged caches [NB, Hkv, BS, D] / [NB, Hkv, D, BS] bf16");
+  const int D = kc.size(3), BS = kc.size(2);
+  TORCH_CHECK(kc.size(1) == Hkv && vc.size(1) == Hkv && vc.size(2) == D && vc.size(3) == BS && cos_sin.size(1) == D,
+              "gemv_qkv: cache / rope table shapes");
+  TORCH_CHECK(out.size(1) == (Hq + 2 * Hkv) * D && pos.numel() == out.size(0) && slots.numel() == out.size(0),
+              "gemv_qkv: qkv / pos / slots shapes");
+  return QkvEpi{pos.data_ptr<int32_t>(), cos_sin.data_ptr<float>(), slots.data_ptr<int64_t>(), (bf16*)kc.data_ptr(),
+                (bf16*)vc.data_ptr(), kc.size(0) * (int64_t)BS, (int)Hq, (int)Hkv, BS, D, (int)cos_sin.size(0),
+                apply_rope ? 1 : 0};
+}
+
+template <int EPI>
+void gemv_norm_dispatch(at::Tensor out, const at::Tensor& o, const at::Tensor& res, at::Tensor res_out,
+                        const at::Tensor& norm_w, double eps, const at::Tensor& w) {
+  Extra ex;
+  ex.pro = make_pro(o, res, res_out, norm_w, eps);
+  gemv_dispatch<EPI, true>(out, o, w, ex);
 }
 
 }  // namespace
@@ -380,9 +468,28 @@ void gemv_add_rmsnorm(at::Tensor out, at::Tensor x, at::Tensor w, at::Tensor res
               "gemv_add_rmsnorm: bf16 contiguous operands");
   TORCH_CHECK(residual.numel() == out.numel() && norm_w.numel() == w.size(0), "gemv_add_rmsnorm: shapes");
   TORCH_CHECK(counter.is_cuda() && counter.scalar_type() == at::kInt && counter.numel() >= 1, "counter: int32");
-  gemv_dispatch<EPI_ADDNORM>(out, x, w,
-                             AddNorm{(bf16*)residual.data_ptr(), (const bf16*)norm_w.data_ptr(),
-                                     (unsigned int*)counter.data_ptr(), (float)eps});
+  Extra ex;
+  ex.an = AddNorm{(bf16*)residual.data_ptr(), (const bf16*)norm_w.data_ptr(), (unsigned int*)counter.data_ptr(),
+                  (float)eps};
+  gemv_dispatch<EPI_ADDNORM>(out, x, w, ex);
+}
+
+// qkv projection with RoPE + paged K/V cache writes fused into the epilogue (rope_and_cache
+// of rope.hip).  With `o` given (defined tensor), the input is the prologue norm of
+// gemv_norm (x ignored); else x is the normalised input.
+void gemv_qkv(at::Tensor out, at::Tensor x, at::Tensor w, at::Tensor pos, at::Tensor cos_sin, at::Tensor slots,
+              at::Tensor k_cache, at::Tensor v_cache, int64_t Hq, int64_t Hkv, bool apply_rope,
+              c10::optional<at::Tensor> o, c10::optional<at::Tensor> res, c10::optional<at::Tensor> res_out,
+              c10::optional<at::Tensor> norm_w, double eps) {
+  Extra ex;
+  ex.qe = make_qkv(out, pos, cos_sin, slots, k_cache, v_cache, Hq, Hkv, apply_rope);
+  if (o.has_value()) {
+    TORCH_CHECK(res.has_value() && res_out.has_value() && norm_w.has_value(), "gemv_qkv: prologue operands");
+    ex.pro = make_pro(*o, *res, *res_out, *norm_w, eps);
+    gemv_dispatch<EPI_QKV, true>(out, *o, w, ex);
+  } else {
+    gemv_dispatch<EPI_QKV, false>(out, x, w, ex);
+  }
 }
 
 // Whether the GEMV path supports this weight (host-side shape rule used by the runner).

@@ -67,6 +67,10 @@ void gemv_silu(at::Tensor out, at::Tensor x, at::Tensor w);
 bool gemv_supported(const at::Tensor& w, bool silu);
 void gemv_norm(at::Tensor out, at::Tensor o, at::Tensor res, at::Tensor res_out, at::Tensor norm_w, double eps,
                at::Tensor w);
+void gemv_qkv(at::Tensor out, at::Tensor x, at::Tensor w, at::Tensor pos, at::Tensor cos_sin, at::Tensor slots,
+              at::Tensor k_cache, at::Tensor v_cache, int64_t Hq, int64_t Hkv, bool apply_rope,
+              c10::optional<at::Tensor> o, c10::optional<at::Tensor> res, c10::optional<at::Tensor> res_out,
+              c10::optional<at::Tensor> norm_w, double eps);
 void gemv_silu_norm(at::Tensor out, at::Tensor o, at::Tensor res, at::Tensor res_out, at::Tensor norm_w, double eps,
                     at::Tensor w);
 void skinny_gemm_add_rmsnorm(at::Tensor out, at::Tensor x, at::Tensor w, at::Tensor residual, at::Tensor norm_w,
@@ -136,8 +140,8 @@ class LlamaRunner {
     // (ops/csrc/gemm_gemv.hip) for all four projections, gate_up with silu*up fused; it
     // fuses no residual, so it also serves tensor-parallel ranks.
     const bool gv = gemv_enabled() && T <= 4;
-    auto attend = [&](int64_t l, const at::Tensor& qkv) {
-      rope_and_cache(qkv, pos, cos_sin_, slots, kc_[l], vc_[l], hq_, hkv_, true);
+    auto attend = [&](int64_t l, const at::Tensor& qkv, bool roped) {
+      if (!roped) rope_and_cache(qkv, pos, cos_sin_, slots, kc_[l], vc_[l], hq_, hkv_, true);
       at::Tensor q = qkv.narrow(1, 0, hq_ * d_);
       at::Tensor attn = at::empty({T, hq_ * d_}, qkv.options());
       if (num_decode > 0)
@@ -159,15 +163,19 @@ class LlamaRunner {
     if (fused) {
       at::Tensor dn;
       for (int64_t l = 0; l < L; ++l) {
+        // qkv GEMV with RoPE + K/V cache writes in its epilogue (and, past layer 0, the
+        // previous layer's residual add + RMSNorm in its prologue)
         at::Tensor qkv = at::empty({T, qkv_w_[l].size(0)}, x.options());
         if (l == 0) {
-          gemv(qkv, x, qkv_w_[l]);
+          gemv_qkv(qkv, x, qkv_w_[l], pos, cos_sin_, slots, kc_[l], vc_[l], hq_, hkv_, true, c10::nullopt,
+                   c10::nullopt, c10::nullopt, c10::nullopt, eps_);
         } else {
           at::Tensor rn = at::empty_like(residual);
-          gemv_norm(qkv, dn, residual, rn, in_norm_[l], eps_, qkv_w_[l]);
+          gemv_qkv(qkv, x, qkv_w_[l], pos, cos_sin_, slots, kc_[l], vc_[l], hq_, hkv_, true, dn, residual, rn,
+                   in_norm_[l], eps_);
           residual = rn;
         }
-        at::Tensor attn = attend(l, qkv);
+        at::Tensor attn = attend(l, qkv, true);
         at::Tensor o = at::empty_like(residual);
         gemv(o, attn, o_w_[l]);
         at::Tensor a = at::empty({T, gate_up_w_[l].size(0) / 2}, o.options());

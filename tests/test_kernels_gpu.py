@@ -385,3 +385,48 @@ def test_gemv_prologue_norm(silu, T, N, K):
         y = torch.nn.functional.silu(y[:, : N // 2]) * y[:, N // 2:]
     _close(res_out, er, 0.02, 0.01)
     _close(out, y, 0.05, 0.03)
+
+
+@pytest.mark.parametrize("T,K,prologue", [(1, 4096, False), (3, 2048, True), (2, 14336, False)])
+def test_gemv_qkv_rope_cache(T, K, prologue):
+    # qkv GEMV with RoPE + paged K / V^T cache writes in the epilogue vs a PyTorch fp32 chain
+    torch.manual_seed(T * 5 + K)
+    Hq, Hkv, D, BS, NB = 4, 2, 128, 64, 6
+    N = (Hq + 2 * Hkv) * D
+    w = (torch.randn(N, K, device=DEV) * 0.05).to(torch.bfloat16)
+    x = torch.randn(T, K, device=DEV).to(torch.bfloat16)
+    pos = torch.tensor([5, 77, 300, 9][:T], dtype=torch.int32, device=DEV)
+    slots = torch.tensor([3, 64 + 10, -1, 200][:T], dtype=torch.int64, device=DEV)
+    inv = 1.0 / (500000.0 ** (torch.arange(0, D, 2).float() / D))
+    ang = torch.arange(512).float()[:, None] * inv[None]
+    cos_sin = torch.cat([ang.cos(), ang.sin()], 1).to(DEV)
+    kc = torch.zeros(NB, Hkv, BS, D, device=DEV, dtype=torch.bfloat16)
+    vc = torch.zeros(NB, Hkv, D, BS, device=DEV, dtype=torch.bfloat16)
+    out = torch.empty(T, N, device=DEV, dtype=torch.bfloat16)
+    if prologue:
+        o, res = x, torch.randn(T, K, device=DEV).to(torch.bfloat16)
+        nw = (1 + 0.1 * torch.randn(K, device=DEV)).to(torch.bfloat16)
+        res_out = torch.empty_like(res)
+        ops.hip().gemv_qkv(out, x, w, pos, cos_sin, slots, kc, vc, Hq, Hkv, True, o, res, res_out, nw, 1e-5)
+        er = (o.float().cpu() + res.float().cpu()).to(torch.bfloat16).float()
+        xin = (er * torch.rsqrt(er.pow(2).mean(-1, keepdim=True) + 1e-5) * nw.float().cpu()).to(torch.bfloat16).float()
+        _close(res_out, er, 0.02, 0.01)
+    else:
+        ops.hip().gemv_qkv(out, x, w, pos, cos_sin, slots, kc, vc, Hq, Hkv, True, None, None, None, None, 1e-5)
+        xin = x.float().cpu()
+    y = (xin @ w.float().cpu().t()).to(torch.bfloat16).float().view(T, Hq + 2 * Hkv, D)
+    cs = cos_sin.cpu()[pos.long().cpu()]
+    c, s = cs[:, None, : D // 2], cs[:, None, D // 2:]
+    qk = y[:, : Hq + Hkv]
+    a, b = qk[..., : D // 2], qk[..., D // 2:]
+    rot = torch.cat([a * c - b * s, b * c + a * s], -1)
+    exp = torch.cat([rot, y[:, Hq + Hkv:]], 1)
+    _close(out.view(T, -1, D), exp, 0.05, 0.02)
+    kcc, vcc = kc.float().cpu(), vc.float().cpu()
+    for t in range(T):
+        sl = int(slots[t])
+        if sl < 0:
+            continue
+        blk, off = divmod(sl, BS)
+        _close(kcc[blk, :, off], exp[t, Hq: Hq + Hkv], 0.05, 0.02)
+        _close(vcc[blk, :, :, off], exp[t, Hq + Hkv:], 0.05, 0.02)
