@@ -33,6 +33,7 @@ from __future__ import annotations
 import itertools
 import logging
 import os
+import collections
 import queue
 import threading
 import time
@@ -213,6 +214,7 @@ class LLMEngine:
         self._wake = threading.Event()
         self._inflight: Optional[_InFlight] = None
         self._step_id = 0
+        self.ttft_s: collections.deque = collections.deque(maxlen=4096)   # engine-side arrival -> first token
         self.stats = {"prefill_steps": 0, "decode_steps": 0, "mixed_steps": 0, "prefill_tokens": 0,
                       "decode_tokens": 0, "preemptions": 0, "requests": 0, "finished": 0, "graph_steps": 0,
                       "host_ms": 0.0, "wait_ms": 0.0, "launch_ms": 0.0, "retire_ms": 0.0}
@@ -618,6 +620,7 @@ class LLMEngine:
             r.output_logprobs.append(lp_h[j])
             if r.first_token_time is None:
                 r.first_token_time = now
+                self.ttft_s.append(now - r.arrival)
             p = r.params
             reason = None
             if not p.ignore_eos and t in self._eos and len(r.output_ids) > p.min_tokens:

@@ -18,6 +18,7 @@
 #include <pybind11/stl.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <cstdint>
@@ -33,6 +34,15 @@
 namespace py = pybind11;
 
 namespace {
+
+// Interpreter-exit gate.  A daemon reader parked in wait_for() (GIL released) when
+// CPython finalizes is ended with pthread_exit as it re-takes the GIL; that forced unwind
+// through pybind11 frames holding py::objects aborts the process.  shutdown_waiters()
+// (called from an atexit hook) closes the gate: parked waiters wake within one slice and
+// later calls return at once without dropping the GIL.
+std::atomic<bool> g_closing{false};
+std::atomic<int> g_waiters{0};
+constexpr auto kWaitSlice = std::chrono::milliseconds(20);
 
 struct Partition {
   std::deque<py::object> msgs;  // msgs[i] has offset base + i
@@ -285,10 +295,23 @@ class MemLog {
   }
   // Sleep (GIL released) until an append/rebalance bumps the sequence or the deadline
   // passes.  Returns false on timeout.
+  // Sleep (GIL released) in short slices until an append/rebalance bumps the sequence,
+  // the deadline passes or the exit gate closes.  Returns false on timeout.
   bool wait_for(uint64_t s0, std::chrono::steady_clock::time_point deadline) {
-    py::gil_scoped_release nogil;
-    std::unique_lock<std::mutex> lk(cvmu_);
-    return cv_.wait_until(lk, deadline, [&] { return seq_ != s0; });
+    if (g_closing.load()) return false;
+    g_waiters++;
+    bool woke = false;
+    {
+      py::gil_scoped_release nogil;
+      std::unique_lock<std::mutex> lk(cvmu_);
+      while (!woke && !g_closing.load()) {
+        auto now = std::chrono::steady_clock::now();
+        if (now >= deadline) break;
+        woke = cv_.wait_until(lk, std::min(deadline, now + kWaitSlice), [&] { return seq_ != s0; });
+      }
+    }
+    g_waiters--;
+    return woke;
   }
 
   Topic* get(const std::string& name) {
@@ -347,4 +370,6 @@ void bind_memlog(py::module_& m) {
            py::arg("timeout_ms") = 1000.0)
       .def("total", &MemLog::total)
       .def("wakeup", &MemLog::wakeup);
+  m.def("memlog_close_gate", [] { g_closing.store(true); });
+  m.def("memlog_waiters", [] { return g_waiters.load(); });
 }

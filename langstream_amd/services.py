@@ -13,6 +13,7 @@ Configuration (``local-gpu-configuration`` resource):
 """
 from __future__ import annotations
 
+import atexit
 import logging
 import os
 import re
@@ -54,6 +55,10 @@ class ServiceRegistry:
         self._embedders: Dict[str, Any] = {}
         self._lock = threading.RLock()
         self.tp = None  # set by the TP launcher for the chat agent
+        # Engine threads sit inside GIL-released native calls; if the interpreter finalizes
+        # while one is still running, its forced unwind through C++ aborts the process.
+        # Join them first (atexit runs before daemon threads are torn down).
+        atexit.register(self.shutdown)
 
     @classmethod
     def default(cls) -> "ServiceRegistry":

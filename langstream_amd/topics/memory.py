@@ -16,6 +16,7 @@ from __future__ import annotations
 
 import itertools
 import json
+import atexit
 import logging
 import threading
 import time
@@ -36,10 +37,21 @@ _logs: Dict[str, Any] = {}
 _logs_lock = threading.Lock()
 
 
+def _close_gate() -> None:
+    """atexit: let readers blocked in the native log leave it before finalization."""
+    native = lib()
+    native.memlog_close_gate()
+    deadline = time.monotonic() + 2.0
+    while native.memlog_waiters() > 0 and time.monotonic() < deadline:
+        time.sleep(0.005)
+
+
 def memlog(name: str = "default"):
     with _logs_lock:
         m = _logs.get(name)
         if m is None:
+            if not _logs:
+                atexit.register(_close_gate)
             m = lib().MemLog()
             _logs[name] = m
         return m

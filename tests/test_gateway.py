@@ -184,6 +184,11 @@ def test_http_produce_auth_and_events(env):
             ttok = encode_jwt_hs256({"sub": "t"}, b"testkey")
             r = await s.post(url + f"?test-credentials={ttok}", data="test mode")
             assert r.status == 200
+            # connect/disconnect events come from WebSocket sessions on a gateway with an
+            # events-topic (independent of which other tests ran first)
+            ws = await s.ws_connect(gw.url.replace("http", "ws")
+                                    + "/v1/produce/default/app1/produce-q?param:sessionId=ev")
+            await ws.close()
     _run(go())
     recs = runner.consume("questions", 10, timeout=5)
     users = {r.value(): r.header_value("user") for r in recs}
