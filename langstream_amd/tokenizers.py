@@ -3,7 +3,8 @@
 * :class:`BPETokenizer` -- byte-level BPE.  Loads an HF ``tokenizer.json`` (BPE model)
   or a tiktoken rank file when one is available; otherwise builds a deterministic,
   self-contained vocabulary by training BPE on a built-in English corpus and padding to
-  the model's vocab size with reserved special tokens (this environment has no model
+  the model's vocab size with filler words below 256 top special tokens, the Llama-3
+  layout, so sampled ids decode to text (this environment has no model
   hub; token ids are exact-size and lossless, merges are not the official ones --
   "parity unpinned" for exact token counts).
 * :class:`WordPieceTokenizer` -- BERT WordPiece (``vocab.txt`` or synthetic).
@@ -148,14 +149,32 @@ def _synthetic_bpe(vocab_size: int, num_merges: int, bos: str, eos: tuple) -> BP
         t = a + b
         if t not in vocab:
             vocab[t] = len(vocab)
-    n_special = max(0, vocab_size - len(vocab))
+    if vocab_size < len(vocab):
+        raise ValueError(f"vocab_size {vocab_size} smaller than trained vocab {len(vocab)}")
+    # Llama-3 layout: the top 256 ids are special tokens, everything below decodes to text.
+    # Ids between the trained vocab and the specials get filler words (never produced by
+    # encode, no merges reach them) so randomly sampled ids stream non-empty text the way a
+    # real 128K vocabulary does.
+    n_special = min(256, max(0, vocab_size - len(vocab)))
+    fill_to = vocab_size - n_special
+    alpha = b"abcdefghijklmnopqrstuvwxyz"
+    i = 0
+    while len(vocab) < fill_to:
+        n, w = i, b""
+        while True:
+            w = alpha[n % 26:n % 26 + 1] + w
+            n //= 26
+            if n == 0:
+                break
+        i += 1
+        t = b" " + w
+        if t not in vocab:
+            vocab[t] = len(vocab)
     names = [bos, *eos, "<|start_header_id|>", "<|end_header_id|>"]
     specials = {}
     for i in range(n_special):
         name = names[i] if i < len(names) else f"<|reserved_special_token_{i}|>"
         specials[name] = len(vocab) + i
-    if vocab_size < len(vocab):
-        raise ValueError(f"vocab_size {vocab_size} smaller than trained vocab {len(vocab)}")
     return BPETokenizer(vocab, merges, specials, bos=bos, eos=eos)
 
 
