@@ -38,7 +38,7 @@ import time
 import uuid
 from collections import OrderedDict
 from dataclasses import dataclass, field
-from typing import Any, Callable, Dict, List, Optional
+from typing import Any, Callable, Dict, List, Optional, Tuple
 
 from ..api.model import Application, ComputeCluster, Gateway, Instance, KeyValueComparison, StreamingCluster
 from ..api.record import Header, Record, SimpleRecord
@@ -334,6 +334,79 @@ class _ReaderPump:
         self.stop.set()
 
 
+class _ReaderHub:
+    """One topic reader shared by every ``latest``-positioned consume/chat session of a
+    gateway whose filters are header equalities (the chat case: one answers topic, a
+    ``session``-like header per client).
+
+    The reference gives every WebSocket its own reader that scans the whole topic and
+    drops records for other sessions (``GW/gateways/ConsumeGateway.java:40-270``), so N
+    sessions cost O(N) filter evaluations per record -- with per-token chunk streaming
+    that is the gateway's bottleneck well before the GPU's.  Here a record is read
+    once and routed by a dict lookup on its filter-header values: O(1) per record."""
+
+    def __init__(self, reader, keys: Tuple[str, ...], on_empty: Callable[["_ReaderHub"], None]):
+        self.reader, self.keys, self.on_empty = reader, keys, on_empty
+        self.subs: Dict[tuple, List[tuple]] = {}
+        self.lock = threading.Lock()
+        self.stop = threading.Event()
+        self.t = threading.Thread(target=self._run, daemon=True, name="gateway-hub")
+        self.t.start()
+
+    def subscribe(self, want: tuple, loop, on_msg) -> "_HubSubscription":
+        entry = (loop, on_msg)
+        with self.lock:
+            self.subs.setdefault(want, []).append(entry)
+        return _HubSubscription(self, want, entry)
+
+    def unsubscribe(self, want: tuple, entry) -> None:
+        with self.lock:
+            lst = self.subs.get(want)
+            if lst and entry in lst:
+                lst.remove(entry)
+                if not lst:
+                    del self.subs[want]
+            empty = not self.subs
+        if empty:
+            self.on_empty(self)
+
+    def _run(self) -> None:
+        keys = self.keys
+        try:
+            while not self.stop.is_set():
+                res = self.reader.read()
+                for rec in res.records:
+                    vals = []
+                    for k in keys:
+                        h = rec.get_header(k)
+                        v = h.value_as_string() if h is not None else None
+                        if v is None:
+                            break
+                        vals.append(v)
+                    else:
+                        with self.lock:
+                            targets = list(self.subs.get(tuple(vals), ()))
+                        if targets:
+                            msg = GatewayService.push_message(rec, res.offset)
+                            for loop, on_msg in targets:
+                                loop.call_soon_threadsafe(on_msg, msg)
+        except Exception as e:  # noqa: BLE001
+            log.info("gateway hub reader stopped: %s", e)
+        finally:
+            try:
+                self.reader.close()
+            except Exception:  # noqa: BLE001
+                pass
+
+
+class _HubSubscription:
+    def __init__(self, hub: _ReaderHub, want: tuple, entry):
+        self.hub, self.want, self.entry = hub, want, entry
+
+    def close(self) -> None:
+        self.hub.unsubscribe(self.want, self.entry)
+
+
 class GatewayServer:
     def __init__(self, service: GatewayService, host: str = "127.0.0.1", port: int = 8091):
         self.service = service
@@ -342,6 +415,8 @@ class GatewayServer:
         self._thread: Optional[threading.Thread] = None
         self._runner = None
         self._started = threading.Event()
+        self._hubs: Dict[tuple, _ReaderHub] = {}
+        self._hubs_lock = threading.Lock()
 
     # ------------------------------------------------------------------ app
     def make_app(self):
@@ -398,8 +473,12 @@ class GatewayServer:
     async def _pump_to_ws(self, ws, ctx, topic, kvs):
         loop = asyncio.get_running_loop()
         q: asyncio.Queue = asyncio.Queue()
-        reader = await loop.run_in_executor(None, self.service.reader, ctx, topic)
-        pump = _ReaderPump(loop, reader, message_filters(kvs, ctx), q.put_nowait)
+        pump = None
+        if kvs and str(ctx.options.get("position", "latest")).lower() == "latest":
+            pump = await loop.run_in_executor(None, self._hub_subscribe, ctx, topic, kvs, loop, q.put_nowait)
+        if pump is None:
+            reader = await loop.run_in_executor(None, self.service.reader, ctx, topic)
+            pump = _ReaderPump(loop, reader, message_filters(kvs, ctx), q.put_nowait)
 
         async def sender():
             while True:
@@ -408,6 +487,29 @@ class GatewayServer:
                     return
                 await ws.send_str(m)
         return pump, asyncio.ensure_future(sender())
+
+    def _hub_subscribe(self, ctx: RequestContext, topic: str, kvs, loop, on_msg):
+        message_filters(kvs, ctx)   # same validation as the per-session path
+        want = tuple(_kv_value(kv, ctx) for kv in kvs)
+        if any(w is None for w in want):
+            return None             # a filter that can never match: per-session semantics
+        keys = tuple(kv.key for kv in kvs)
+        hk = (ctx.tenant, ctx.application_id, topic, keys)
+        with self._hubs_lock:
+            hub = self._hubs.get(hk)
+            if hub is None or hub.stop.is_set():
+                hub = _ReaderHub(self.service.reader(ctx, topic), keys, lambda h, hk=hk: self._hub_empty(hk, h))
+                self._hubs[hk] = hub
+            return hub.subscribe(tuple(str(w) for w in want), loop, on_msg)
+
+    def _hub_empty(self, hk: tuple, hub: _ReaderHub) -> None:
+        with self._hubs_lock:
+            with hub.lock:
+                if hub.subs:
+                    return          # re-subscribed meanwhile
+            hub.stop.set()
+            if self._hubs.get(hk) is hub:
+                del self._hubs[hk]
 
     async def _ws_consume(self, request):
         from aiohttp import WSMsgType

@@ -21,7 +21,7 @@ import sys
 import threading
 import time
 from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
-from typing import List, Optional
+from typing import Any, Dict, List, Optional, Tuple
 
 from .metrics import MetricsReporter
 from .runner import AgentRunner, RuntimePodConfiguration
@@ -106,7 +106,32 @@ def _replica_index() -> int:
     tail = host.rsplit("-", 1)[-1]
     if tail.isdigit():
         return int(tail)
+    if int(os.environ.get("WORLD_SIZE", "1") or 1) > 1:
+        return 0   # torchrun ranks of a TP pod are one replica
     return int(os.environ.get("RANK", "0"))
+
+
+def chat_engine_request(configuration: Dict[str, Any]) -> Tuple[Optional[str], Dict[str, Any]]:
+    """(model, local-engine config) of a planned ai-chat/text-completions agent: the
+    GenAI planner stores ``{steps: [{type, model, ...}], <service-key>: resource}``."""
+    steps = configuration.get("steps") or [configuration]
+    model = steps[0].get("model")
+    for key in ("local", "openai"):
+        res = configuration.get(key)
+        if isinstance(res, dict) and (key == "local" or res.get("provider") == "local"):
+            return model, res
+    raise ValueError("tensor-parallel pods need a local-gpu-configuration chat agent")
+
+
+def serve_tp_worker(configuration: Dict[str, Any], services=None) -> int:
+    """TP ranks > 0: build the same engine as rank 0 (weights shard, KV pool, lock-step
+    graph capture) and mirror its steps until rank 0 stops the engine."""
+    from ..services import ServiceRegistry
+    reg = services or ServiceRegistry.default()
+    model, res = chat_engine_request(configuration)
+    eng = reg.llm_engine(model, res)
+    eng.worker_loop()
+    return 0
 
 
 def main(argv: Optional[List[str]] = None) -> int:
@@ -119,6 +144,16 @@ def main(argv: Optional[List[str]] = None) -> int:
         return 2
     code = os.environ.get("LANGSTREAM_AGENT_RUNNER_CODE_PATH", "")
     state = os.environ.get("LANGSTREAM_AGENT_RUNNER_PERSISTENT_STATE_DIRECTORY")
+    tp_world = int(os.environ.get("WORLD_SIZE", "1") or 1)
+    if tp_world > 1:
+        # torchrun inside one pod = one tensor-parallel chat agent replica
+        from ..parallel import init_tensor_parallel
+        from ..services import ServiceRegistry
+        reg = ServiceRegistry.default()
+        reg.tp = init_tensor_parallel(tp_world)
+        if reg.tp.rank != 0:
+            pod = load_pod_configuration(cfg, code, state, _replica_index())
+            return serve_tp_worker(pod.configuration, reg)
     pod = load_pod_configuration(cfg, code, state, _replica_index())
     runner = AgentRunner(pod)
     api = AgentAPIServer([runner], port=int(os.environ.get("LANGSTREAM_AGENT_HTTP_PORT", "8080"))).start()

@@ -97,8 +97,11 @@ class ServiceRegistry:
             log.info("starting LLM engine %s on %s", name, device)
             model_ = LlamaModel(mcfg, device=device, dtype=dtype, tp=self.tp)
             if c.get("weights-path"):
-                from .models.loader import load_packed
-                model_.load_state_dict(load_packed(c["weights-path"], device))
+                from .models.loader import load_packed, shard_llama
+                sd = load_packed(c["weights-path"], device)
+                if self.tp is not None and self.tp.world > 1:
+                    sd = shard_llama(sd, mcfg, self.tp.rank, self.tp.world)
+                model_.load_state_dict(sd)
             tok = BPETokenizer.synthetic(mcfg.vocab_size) if not c.get("tokenizer-path") else (
                 BPETokenizer.from_hf_json(c["tokenizer-path"]))
             eng = LLMEngine(model_, tok, max_model_len=int(c.get("max-model-len", 4096)),
@@ -108,8 +111,9 @@ class ServiceRegistry:
                             use_graphs=str(c.get("use-graphs", "true")).lower() == "true",
                             num_blocks=c.get("num-blocks"))
             if eng.use_graphs and str(c.get("capture-graphs", "true")).lower() == "true":
-                eng.capture_graphs()
-            eng.start()
+                eng.capture_graphs()   # TP: every rank captures in lock-step
+            if self.tp is None or self.tp.rank == 0:
+                eng.start()            # TP ranks > 0 serve eng.worker_loop() instead
             self._llms[name] = eng
             return eng
 

@@ -117,3 +117,41 @@ def test_shard_llama_roundtrip_shapes():
     # concatenating the row-parallel shards restores the full matrix
     assert torch.equal(torch.cat([p["layers.0.o_w"] for p in parts], 1), sd["layers.0.o_w"])
     assert torch.equal(torch.cat([p["embed"] for p in parts], 0)[: cfg.vocab_size], sd["embed"])
+
+
+TP_AGENT_CFG = {"steps": [{"type": "ai-chat-completions", "model": "llama-tiny"}],
+                "local": {"chat-model": "llama-tiny", "device": "cpu", "num-blocks": 64,
+                          "max-model-len": 512, "max-batch": 8}}
+
+
+def _tp_pod_worker(rank, world, port, q):
+    """The TP pod wiring: parallel.init_tensor_parallel from torchrun env, rank 0 serves
+    the chat agent's completions service, rank 1 runs pod.serve_tp_worker."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    from langstream_amd.parallel import init_tensor_parallel
+    from langstream_amd.runtime.pod import serve_tp_worker
+    from langstream_amd.services import ServiceRegistry
+    reg = ServiceRegistry()
+    reg.tp = init_tensor_parallel()
+    try:
+        if rank == 0:
+            from langstream_amd.agents.genai.services import ChatMessage
+            svc = reg.completions_service(TP_AGENT_CFG, "llama-tiny")
+            chunks = []
+            res = svc.get_chat_completions(
+                [ChatMessage("user", "tell me about streaming")],
+                lambda aid, i, text, last: chunks.append((i, last)),
+                {"max-tokens": 7, "temperature": 0.0, "ignore-eos": True,
+                 "min-chunks-per-message": 2}).result(120)
+            reg.shutdown()   # stops the engine -> releases rank 1's worker loop
+            q.put((res.completion_tokens, len(res.content) > 0, chunks[-1][1]))
+        else:
+            serve_tp_worker(TP_AGENT_CFG, reg)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_tp_pod_serves_chat_agent():
+    ntok, has_text, last = _spawn(_tp_pod_worker)
+    assert ntok == 7 and has_text and last

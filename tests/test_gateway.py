@@ -149,6 +149,45 @@ def test_chat(env):
     _run(go())
 
 
+def test_chat_sessions_share_one_routed_reader(env):
+    """Concurrent chat sessions of one gateway share one answers-topic reader (the hub),
+    each still sees only its own answers, and the hub goes away with the last session."""
+    import aiohttp
+    _, gw = env
+    base = gw.url.replace("http", "ws")
+    sids = [f"hub{i}" for i in range(6)]
+
+    async def one(s, sid):
+        ws = await s.ws_connect(f"{base}/v1/chat/default/app1/chat?param:sessionId={sid}")
+        await asyncio.sleep(0.3)
+        got = []
+        for q in range(3):
+            await ws.send_str(json.dumps({"value": f"{sid}-q{q}"}))
+            while True:
+                m = json.loads((await ws.receive(timeout=10)).data)
+                if "record" in m:
+                    got.append(m["record"]["value"])
+                    break
+        return ws, got
+
+    async def go():
+        async with aiohttp.ClientSession() as s:
+            res = await asyncio.gather(*[one(s, sid) for sid in sids])
+            assert len(gw._hubs) == 1
+            hub = next(iter(gw._hubs.values()))
+            assert len(hub.subs) == len(sids)
+            for sid, (ws, got) in zip(sids, res):
+                assert got == [f"echo: {sid}-q{q}" for q in range(3)]
+            for ws, _ in res:
+                await ws.close()
+            for _ in range(50):
+                if not gw._hubs:
+                    break
+                await asyncio.sleep(0.05)
+            assert not gw._hubs
+    _run(go())
+
+
 def test_validation_errors(env):
     import aiohttp
     _, gw = env
