@@ -21,6 +21,26 @@ namespace {
 constexpr int CH = 1024;  // store rows per workgroup
 constexpr int QG = 16;    // queries per workgroup (one MFMA column group)
 
+// Bitonic sort of one (value, index) pair per lane across a 64-wide wave, descending by
+// value with ties broken towards the lower index (the order the argmax path produces):
+// afterwards lane L holds the L-th largest.  6*7/2 = 21 xor-shuffle compare-exchanges.
+__device__ __forceinline__ void wave_sort_desc(float& v, int& i, int lane) {
+#pragma unroll
+  for (int k = 2; k <= 64; k <<= 1) {
+#pragma unroll
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      const float ov = __shfl_xor(v, j, 64);
+      const int oi = __shfl_xor(i, j, 64);
+      const bool other_first = ov > v || (ov == v && oi < i);
+      // descending blocks where (lane & k) == 0; the lower lane of a pair keeps the "first"
+      const bool lower = (lane & j) == 0;
+      const bool desc = (lane & k) == 0;
+      const bool take = (lower == desc) ? other_first : !other_first;
+      if (take) { v = ov; i = oi; }
+    }
+  }
+}
+
 template <int DIM>
 __global__ void __launch_bounds__(256) knn_stage1_kernel(const bf16* __restrict__ X, int64_t N,
                                                          const bf16* __restrict__ Qm, int Qn, int K,
@@ -61,12 +81,62 @@ __global__ void __launch_bounds__(256) knn_stage1_kernel(const bf16* __restrict_
     }
   }
   __syncthreads();
-  // top-K per query: wave w handles queries w, w+4, w+8, w+12
+  // top-K per query: wave w handles queries w, w+4, w+8, w+12.
+  // Fast path (threshold + sort): every lane holds 16 of the 1024 scores in registers;
+  // the K-th largest of the 64 lane maxima, T, lower-bounds the K-th largest score (the
+  // K lanes owning those maxima each hold a score >= T), so only scores >= T can be in
+  // the top-K.  They are compacted by ballot into a 64-slot LDS list and bitonic-sorted
+  // across the wave (21 shuffle stages) -- instead of K rounds of a 1024-wide argmax.
+  // When more than 64 scores reach T (heavy ties, or a tail chunk where T = -inf) the
+  // wave falls back to the K-round argmax over LDS.
+  __shared__ float cv_lds[4][64];
+  __shared__ int ci_lds[4][64];
   for (int qq = wid; qq < QG; qq += 4) {
     const int qi = qg * QG + qq;
     if (qi >= Qn) continue;
     float* outs = cand_s + ((int64_t)qi * nchunks + chunk) * K;
     int32_t* outi = cand_i + ((int64_t)qi * nchunks + chunk) * K;
+    float v[CH / 64];
+    float m = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < CH / 64; ++j) {
+      v[j] = sc[qq][lane + 64 * j];
+      m = fmaxf(m, v[j]);
+    }
+    float tv = m;
+    int ti = lane;
+    wave_sort_desc(tv, ti, lane);
+    const float T = __shfl(tv, K - 1, 64);
+    int count = 0;
+    if (T > -INFINITY) {
+#pragma unroll
+      for (int j = 0; j < CH / 64; ++j) {
+        const bool p = v[j] >= T;
+        const uint64_t mask = __ballot(p);
+        const int pos = count + __popcll(mask & ((1ull << lane) - 1ull));
+        if (p && pos < 64) {
+          cv_lds[wid][pos] = v[j];
+          ci_lds[wid][pos] = lane + 64 * j;
+        }
+        count += __popcll(mask);
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (T > -INFINITY && count <= 64) {
+      float cvv = lane < count ? cv_lds[wid][lane] : -INFINITY;
+      int cii = lane < count ? ci_lds[wid][lane] : CH;
+      wave_sort_desc(cvv, cii, lane);
+      if (lane < K) {
+        outs[lane] = cvv;
+        outi[lane] = cii < CH ? (int32_t)((int64_t)chunk * CH + cii) : -1;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      continue;
+    }
     for (int k = 0; k < K; ++k) {
       float bv = -INFINITY;
       int bi = CH;

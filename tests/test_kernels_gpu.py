@@ -261,10 +261,16 @@ def test_pooling(mode):
     _close(got, exp, 2e-3, 1e-2)
 
 
-@pytest.mark.parametrize("N,Qn,k", [(5000, 3, 20), (1024, 20, 5), (10, 2, 20), (70000, 40, 64)])
-def test_knn_topk(N, Qn, k):
+@pytest.mark.parametrize("N,Qn,k,dup", [(5000, 3, 20, 0), (1024, 20, 5, 0), (10, 2, 20, 0), (70000, 40, 64, 0),
+                                         (100000, 17, 20, 0), (4096, 5, 20, 7), (3000, 4, 64, 50)])
+def test_knn_topk(N, Qn, k, dup):
+    """dup > 0 stores only `dup` distinct rows (massive score ties): exercises the
+    K-round fallback behind the threshold + wave-sort fast path."""
     torch.manual_seed(50)
-    X = torch.nn.functional.normalize(torch.randn(N, 384), dim=-1).to(DEV, torch.bfloat16)
+    X = torch.nn.functional.normalize(torch.randn(N, 384), dim=-1)
+    if dup:
+        X = X[torch.arange(N) % dup]
+    X = X.to(DEV, torch.bfloat16)
     Q = torch.nn.functional.normalize(torch.randn(Qn, 384), dim=-1).to(DEV, torch.bfloat16)
     s, i = ops.knn_topk(X, Q, k)
     es, ei = ref.knn_topk(X.cpu(), Q.cpu(), k)

@@ -68,7 +68,7 @@ configuration:
       name: "local"
       configuration:
         chat-model: "{model}"
-        max-batch: 64
+        max-batch: 256
         max-model-len: 4096
 """
 
@@ -122,7 +122,7 @@ def main():
              "configuration.yaml": CONFIG.format(**fmt)}
     services = ServiceRegistry({"device": "cuda:0" if torch.cuda.is_available() else "cpu"})
     ServiceRegistry.set_default(services)
-    engine = services.llm_engine(model, {"chat-model": model, "max-batch": 64, "max-model-len": 4096})   # load + graphs
+    engine = services.llm_engine(model, {"chat-model": model, "max-batch": 256, "max-model-len": 4096})   # load + graphs
     runner = LocalApplicationRunner.from_yaml(files, application_id="chatbench", services=services).start()
     store = InMemoryApplicationStore()
     store.put(StoredApplication("chatbench", "default", runner.application, files))
