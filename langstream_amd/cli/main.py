@@ -347,6 +347,11 @@ def cmd_pulsar_standalone(args) -> int:
     return pulsar_main(["--host", args.host, "--port", str(args.port)])
 
 
+def cmd_pravega_standalone(args) -> int:
+    from ..topics.pravega.standalone import main as pravega_main
+    return pravega_main(["--host", args.host, "--port", str(args.port)])
+
+
 def cmd_operator(args) -> int:
     from ..operator import main as operator_main
     argv = ["--resync", str(args.resync)]
@@ -508,6 +513,12 @@ def build_parser() -> argparse.ArgumentParser:
     ps.add_argument("--host", default="127.0.0.1")
     ps.add_argument("--port", type=int, default=8080)
     ps.set_defaults(fn=cmd_pulsar_standalone)
+
+    pv = sub.add_parser("pravega-standalone",
+                        help="run the in-tree single-node Pravega-style server (controller + segment store)")
+    pv.add_argument("--host", default="127.0.0.1")
+    pv.add_argument("--port", type=int, default=9090)
+    pv.set_defaults(fn=cmd_pravega_standalone)
 
     opr = sub.add_parser("operator", help="run the Kubernetes operator (Application / Agent CRs)")
     opr.add_argument("--api-server", default=None)

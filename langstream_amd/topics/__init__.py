@@ -1,5 +1,5 @@
 """Streaming adapters.  Importing this package registers the built-in
-TopicConnectionsRuntime implementations (memory, noop, kafka, pulsar)."""
+TopicConnectionsRuntime implementations (memory, noop, kafka, pulsar, pravega)."""
 from . import memory  # noqa: F401
 try:  # optional adapters register themselves when importable
     from . import kafka  # noqa: F401
@@ -7,5 +7,9 @@ except ImportError:  # pragma: no cover
     pass
 try:
     from . import pulsar  # noqa: F401
+except ImportError:  # pragma: no cover
+    pass
+try:
+    from . import pravega  # noqa: F401
 except ImportError:  # pragma: no cover
     pass
