@@ -21,10 +21,15 @@
 
 namespace {
 
-constexpr int TOK = 16;  // tokens per workgroup tile
+// Tokens per workgroup tile: 16 for prefill-sized T; 2 for decode-sized T, so a
+// B=256 decode step launches ~1.7k workgroups with one task per thread instead of
+// 208 workgroups looping over dependent pos -> cos/sin loads (12 us -> latency of one).
+constexpr int TOK_LARGE = 16;
+constexpr int TOK_SMALL = 2;
+constexpr int64_t SMALL_T = 2048;
 constexpr int HG = 8;    // heads per rotate workgroup
 
-template <int D>
+template <int D, int TOK>
 __global__ void __launch_bounds__(256) rope_cache_kernel(bf16* __restrict__ qkv, const int32_t* __restrict__ pos,
                                                          const float* __restrict__ cos_sin,
                                                          const int64_t* __restrict__ slots, bf16* __restrict__ kc,
@@ -86,7 +91,7 @@ __global__ void __launch_bounds__(256) rope_cache_kernel(bf16* __restrict__ qkv,
   // ---- V of one kv head, transposed into the cache.  thread -> (token lane, d-row)
   const int hv = y - nq - nk;
   const int tl = threadIdx.x % TOK;
-  const int dr = threadIdx.x / TOK;  // 0..15
+  const int dr = threadIdx.x / TOK;  // 0..256/TOK-1
   if (tl >= ntok) return;
   const int64_t t = t0 + tl;
   const int64_t s = slots[t];
@@ -116,15 +121,17 @@ void rope_and_cache(at::Tensor qkv, at::Tensor pos, at::Tensor cos_sin, at::Tens
   if (T == 0) return;
   auto stream = at::hip::getCurrentHIPStream();
   const int nq = (int)((Hq + HG - 1) / HG), nk = (int)((Hkv + HG - 1) / HG);
-  dim3 grid((unsigned)((T + TOK - 1) / TOK), nq + nk + (int)Hkv);
-#define LAUNCH(DD)                                                                                          \
-  rope_cache_kernel<DD><<<grid, 256, 0, stream>>>((bf16*)qkv.data_ptr(), pos.data_ptr<int32_t>(),          \
-                                                  cos_sin.data_ptr<float>(), slots.data_ptr<int64_t>(),     \
-                                                  (bf16*)k_cache.data_ptr(), (bf16*)v_cache.data_ptr(), T,  \
-                                                  (int)Hq, (int)Hkv, BS, (int)cos_sin.size(0), apply_rope ? 1 : 0, \
-                                                  (int64_t)k_cache.size(0) * BS)
-  if (D == 128) LAUNCH(128);
-  else if (D == 64) LAUNCH(64);
+  const bool small = T <= SMALL_T;
+  const int tok = small ? TOK_SMALL : TOK_LARGE;
+  dim3 grid((unsigned)((T + tok - 1) / tok), nq + nk + (int)Hkv);
+#define LAUNCH(DD, TT)                                                                                      \
+  rope_cache_kernel<DD, TT><<<grid, 256, 0, stream>>>((bf16*)qkv.data_ptr(), pos.data_ptr<int32_t>(),      \
+                                                      cos_sin.data_ptr<float>(), slots.data_ptr<int64_t>(), \
+                                                      (bf16*)k_cache.data_ptr(), (bf16*)v_cache.data_ptr(), T, \
+                                                      (int)Hq, (int)Hkv, BS, (int)cos_sin.size(0),          \
+                                                      apply_rope ? 1 : 0, (int64_t)k_cache.size(0) * BS)
+  if (D == 128) { if (small) LAUNCH(128, TOK_SMALL); else LAUNCH(128, TOK_LARGE); }
+  else if (D == 64) { if (small) LAUNCH(64, TOK_SMALL); else LAUNCH(64, TOK_LARGE); }
   else TORCH_CHECK(false, "unsupported head dim ", D);
 #undef LAUNCH
 }

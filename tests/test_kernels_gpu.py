@@ -88,17 +88,20 @@ def _alloc_cache(nb, Hkv, D, dev):
             torch.zeros(nb, Hkv, D, ops.KV_BLOCK, device=dev, dtype=torch.bfloat16))
 
 
-def test_rope_and_cache():
+@pytest.mark.parametrize("T,D", [(150, 128), (2600, 128), (37, 64)])
+def test_rope_and_cache(T, D):
+    # T <= 2048 takes the decode-sized 2-token tiles, larger T the 16-token tiles
     torch.manual_seed(5)
-    Hq, Hkv, D, T = 8, 2, 128, 150
+    Hq, Hkv = 8, 2
     qkv = torch.randn(T, (Hq + 2 * Hkv) * D, device=DEV, dtype=torch.bfloat16)
     pos = torch.arange(T, device=DEV, dtype=torch.int32) + 7
     cs = ref.rope_cos_sin(4096, D, 500000.0, device=DEV)
-    perm = torch.randperm(8 * ops.KV_BLOCK)[:T]
+    nb = (T + ops.KV_BLOCK - 1) // ops.KV_BLOCK + 4
+    perm = torch.randperm(nb * ops.KV_BLOCK)[:T]
     slots = perm.to(DEV, torch.int64)
     slots[3] = -1
-    kc, vc = _alloc_cache(8, Hkv, D, DEV)
-    kr, vr = _alloc_cache(8, Hkv, D, "cpu")
+    kc, vc = _alloc_cache(nb, Hkv, D, DEV)
+    kr, vr = _alloc_cache(nb, Hkv, D, "cpu")
     qkv_c = qkv.cpu().clone()
     ops.rope_and_cache(qkv, pos, cs, slots, kc, vc, Hq, Hkv)
     ref.rope_and_cache(qkv_c, pos.cpu(), cs.cpu(), slots.cpu(), kr, vr, Hq, Hkv)
