@@ -164,10 +164,18 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restr
   const int64_t total = (int64_t)M * N;
   if (idx >= total) return;
   const int m = idx / N, n = idx - (int64_t)m * N;
-  float4 a = *reinterpret_cast<const float4*>(part + idx);
-  for (int s = 1; s < S; ++s) {
-    const float4 b = *reinterpret_cast<const float4*>(part + (int64_t)s * total + idx);
-    a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+  constexpr int SMAX = 8;  // loads of the first 8 partials issued together (see below)
+  float4 b[SMAX];
+#pragma unroll
+  for (int s = 0; s < SMAX; ++s)
+    if (s < S) b[s] = *reinterpret_cast<const float4*>(part + (int64_t)s * total + idx);
+  float4 a = b[0];
+#pragma unroll
+  for (int s = 1; s < SMAX; ++s)
+    if (s < S) { a.x += b[s].x; a.y += b[s].y; a.z += b[s].z; a.w += b[s].w; }
+  for (int s = SMAX; s < S; ++s) {
+    const float4 c = *reinterpret_cast<const float4*>(part + (int64_t)s * total + idx);
+    a.x += c.x; a.y += c.y; a.z += c.z; a.w += c.w;
   }
   bf16x4 o = {(bf16)a.x, (bf16)a.y, (bf16)a.z, (bf16)a.w};
   *reinterpret_cast<bf16x4*>(out + (int64_t)m * ldo + n) = o;
@@ -175,7 +183,7 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restr
 
 // One row per workgroup:  v = sum_s part[s, m, :] + residual[m, :];  residual = bf16(v);
 // out[m, :] = rmsnorm(bf16(v)) * w.  (Same rounding as fused_add_rmsnorm in norm.hip.)
-template <int NV>
+template <int NV, int SMAX = 8>
 __global__ void __launch_bounds__(256) splitk_add_rmsnorm_kernel(const float* __restrict__ part, int S, int M, int H,
                                                                  bf16* __restrict__ residual,
                                                                  const bf16* __restrict__ w, float eps,
@@ -190,12 +198,29 @@ __global__ void __launch_bounds__(256) splitk_add_rmsnorm_kernel(const float* __
     const int c = (threadIdx.x + 256 * i) * 8;
     if (c < H) {
       const float* p = part + (int64_t)m * H + c;
-      float4 a0 = *reinterpret_cast<const float4*>(p), a1 = *reinterpret_cast<const float4*>(p + 4);
-      for (int s = 1; s < S; ++s) {
-        const float4 b0 = *reinterpret_cast<const float4*>(p + s * total);
-        const float4 b1 = *reinterpret_cast<const float4*>(p + s * total + 4);
-        a0.x += b0.x; a0.y += b0.y; a0.z += b0.z; a0.w += b0.w;
-        a1.x += b1.x; a1.y += b1.y; a1.z += b1.z; a1.w += b1.w;
+      // Issue the first SMAX partials' loads together (independent, predicated), then
+      // reduce: one memory latency instead of S back-to-back ones (S = 8 at decode M).
+      float4 b0[SMAX], b1[SMAX];
+#pragma unroll
+      for (int s = 0; s < SMAX; ++s) {
+        if (s < S) {
+          b0[s] = *reinterpret_cast<const float4*>(p + s * total);
+          b1[s] = *reinterpret_cast<const float4*>(p + s * total + 4);
+        }
+      }
+      float4 a0 = b0[0], a1 = b1[0];
+#pragma unroll
+      for (int s = 1; s < SMAX; ++s) {
+        if (s < S) {
+          a0.x += b0[s].x; a0.y += b0[s].y; a0.z += b0[s].z; a0.w += b0[s].w;
+          a1.x += b1[s].x; a1.y += b1[s].y; a1.z += b1[s].z; a1.w += b1[s].w;
+        }
+      }
+      for (int s = SMAX; s < S; ++s) {
+        const float4 c0 = *reinterpret_cast<const float4*>(p + s * total);
+        const float4 c1 = *reinterpret_cast<const float4*>(p + s * total + 4);
+        a0.x += c0.x; a0.y += c0.y; a0.z += c0.z; a0.w += c0.w;
+        a1.x += c1.x; a1.y += c1.y; a1.z += c1.z; a1.w += c1.w;
       }
       float r[8];
       unpack8(ld16(residual + (int64_t)m * H + c), r);

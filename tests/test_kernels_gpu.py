@@ -291,7 +291,7 @@ def test_knn_topk(N, Qn, k, dup):
 
 
 @pytest.mark.parametrize("M", [1, 37, 64, 256])
-@pytest.mark.parametrize("N,K", [(384, 512), (1024, 4096)])
+@pytest.mark.parametrize("N,K", [(384, 512), (1024, 4096), (256, 8192)])  # (256, 8192): split-K 16
 def test_skinny_gemm(M, N, K):
     torch.manual_seed(M + N)
     x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
@@ -315,9 +315,9 @@ def test_skinny_gemm_silu(M):
     _close(out, exp, 0.03, 0.03)
 
 
-@pytest.mark.parametrize("M", [5, 128])
-def test_skinny_gemm_add_rmsnorm(M):
-    K, N = 1024, 512
+@pytest.mark.parametrize("M,K,N", [(5, 1024, 512), (128, 1024, 512), (256, 4096, 4096), (256, 8192, 256)])
+def test_skinny_gemm_add_rmsnorm(M, K, N):
+    # split-K 2 / 2 / 8 (decode o_proj shape) / 16 (past the reduction's unrolled 8)
     torch.manual_seed(M)
     x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
     w = (torch.randn(N, K, device=DEV) * 0.05).to(torch.bfloat16)
