@@ -28,7 +28,9 @@
 // MFMA (177 VGPRs, 2 waves/SIMD).  Measured on MI355X (tools/attn_bench.py, B=256,
 // ctx=448, scattered blocks): 89.8 us = 5.2 TB/s, vs 114.7 us for the previous
 // fixed-split kernel, 103 us with next-block K prefetch (256 VGPRs, 1 wave/SIMD) and
-// 106 us when squeezed to 125 VGPRs / 4 waves (V loaded after the softmax).
+// 106 us when squeezed to 125 VGPRs / 4 waves (V loaded after the softmax); forcing
+// amdgpu_waves_per_eu(3) (164 VGPRs, no spills, 3 waves/SIMD) measured 106.9 vs 90.1 us
+// (profiles/decode_attn_waves_per_eu_ab.log): the in-flight K+V bytes per wave matter more.
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
 #include "common.h"
