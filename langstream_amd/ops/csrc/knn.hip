@@ -1,8 +1,8 @@
 // Brute-force k-nearest-neighbour search for the local vector store
 // (query-vector-db / `ORDER BY cosine_similarity(...) DESC LIMIT k`).
 //
-// Stage 1 (fused GEMM + chunk top-k): grid = (N/1024 row chunks, ceil(Q/16) query
-// groups).  Each wave streams 256 store rows through mfma_f32_16x16x32_bf16 as the
+// Stage 1 (fused GEMM + chunk top-k): grid = N/1024 row chunks x ceil(Q/16) query
+// groups, flattened and XCD-remapped (groups of a chunk share an XCD's L2).  Each wave streams 256 store rows through mfma_f32_16x16x32_bf16 as the
 // A operand (one 16-B load per lane per MFMA, straight from HBM: the rows are read
 // once per query group) against the 16 queries' Q^T fragments held in LDS.  Scores
 // for the 1024 x 16 block go to LDS; each wave then extracts the top-k of 4 queries
@@ -49,7 +49,12 @@ __global__ void __launch_bounds__(256) knn_stage1_kernel(const bf16* __restrict_
   constexpr int KS = DIM / 32;
   __shared__ __attribute__((aligned(16))) bf16 q_lds[QG * DIM];
   __shared__ float sc[QG][CH + 1];
-  const int chunk = blockIdx.x, qg = blockIdx.y;
+  // 1-D grid, XCD-aware: the query groups of one row chunk are consecutive logical ids
+  // on one XCD, so the chunk's rows come from HBM once and from that XCD's L2 after
+  // (with grid (chunks, groups) every group re-streamed the whole store from HBM).
+  const int nqg = gridDim.x / nchunks;
+  const int logical = xcd_remap(blockIdx.x, gridDim.x);
+  const int chunk = logical / nqg, qg = logical - chunk * nqg;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int i16 = lane & 15, h = lane >> 4;
   // stage the 16 queries (zero rows past Qn)
@@ -218,7 +223,8 @@ void knn_topk(at::Tensor X, at::Tensor Q, int64_t K, at::Tensor out_s, at::Tenso
   TORCH_CHECK(out_s.numel() >= (int64_t)Qn * K && out_i.numel() >= (int64_t)Qn * K);
   if (Qn == 0 || N == 0) return;
   auto stream = at::hip::getCurrentHIPStream();
-  dim3 grid(nchunks, (Qn + QG - 1) / QG);
+  TORCH_CHECK((int64_t)nchunks * ((Qn + QG - 1) / QG) < (1LL << 31), "kNN grid too large");
+  dim3 grid(nchunks * ((Qn + QG - 1) / QG));
 #define LAUNCH(DD)                                                                                          \
   knn_stage1_kernel<DD><<<grid, 256, 0, stream>>>((const bf16*)X.data_ptr(), N, (const bf16*)Q.data_ptr(), \
                                                   Qn, (int)K, ws_s.data_ptr<float>(), ws_i.data_ptr<int32_t>(), \
