@@ -7,8 +7,9 @@
   configured ``headers``; success iff the status is in ``accepted-statuses``
   (200, 201).  No principal values.
 * ``jwt``    (``JwtAuthenticationProvider.java``): HS256/384/512 with ``secret-key`` or
-  RS256/384/512 with ``public-key`` (PEM) or a JWKS fetched from the token's ``jku``
-  / ``jwks-uri`` (host must be in ``jwks-hosts-allowlist``); ``exp``/``nbf`` checked;
+  RS256/384/512 with ``public-key`` (PEM) or a JWKS fetched from ``jwks-uri`` or from
+  the token's ``jku`` (followed only when its host matches a non-empty
+  ``jwks-hosts-allowlist``); any other ``alg`` is rejected; ``exp``/``nbf`` checked;
   optional ``audience`` checked against ``audience-claim`` (aud); principal values are
   the string claims, ``subject`` = ``auth-claim`` (sub).  RSA verification is done with
   plain modular exponentiation (no crypto library is available offline).
@@ -26,8 +27,10 @@ import base64
 import hashlib
 import hmac
 import json
+import threading
 import time
 import urllib.parse
+from collections import OrderedDict
 from dataclasses import dataclass, field
 from typing import Any, Callable, Dict, List, Optional
 
@@ -119,6 +122,9 @@ class JwtError(Exception):
     pass
 
 
+_ALLOWED_ALGS = ("HS256", "HS384", "HS512", "RS256", "RS384", "RS512")
+
+
 def decode_jwt(token: str, *, secret: Optional[bytes] = None, rsa_key=None,
                jwks_fetch: Optional[Callable[[dict], Optional[tuple]]] = None, leeway: int = 0) -> dict:
     try:
@@ -129,6 +135,8 @@ def decode_jwt(token: str, *, secret: Optional[bytes] = None, rsa_key=None,
     except Exception as e:  # noqa: BLE001
         raise JwtError(f"malformed token: {e}") from e
     alg = header.get("alg", "")
+    if alg not in _ALLOWED_ALGS:
+        raise JwtError(f"unsupported alg {alg!r}")
     signing_input = f"{h64}.{p64}".encode()
     if alg.startswith("HS"):
         if secret is None:
@@ -136,7 +144,7 @@ def decode_jwt(token: str, *, secret: Optional[bytes] = None, rsa_key=None,
         mac = hmac.new(secret, signing_input, getattr(hashlib, "sha" + alg[2:])).digest()
         if not hmac.compare_digest(mac, sig):
             raise JwtError("bad signature")
-    elif alg.startswith("RS"):
+    else:
         key = rsa_key
         if key is None and jwks_fetch is not None:
             key = jwks_fetch(header)
@@ -144,8 +152,6 @@ def decode_jwt(token: str, *, secret: Optional[bytes] = None, rsa_key=None,
             raise JwtError("RSA token but no public key available")
         if not rsa_pkcs1_verify(key[0], key[1], signing_input, sig, "SHA" + alg[2:]):
             raise JwtError("bad signature")
-    else:
-        raise JwtError(f"unsupported alg {alg}")
     now = time.time()
     if "exp" in payload and now > float(payload["exp"]) + leeway:
         raise JwtError("token expired")
@@ -161,6 +167,41 @@ def encode_jwt_hs256(payload: dict, secret: bytes) -> str:
     p = enc(json.dumps(payload).encode())
     sig = hmac.new(secret, f"{h}.{p}".encode(), hashlib.sha256).digest()
     return f"{h}.{p}.{enc(sig)}"
+
+
+# ---------------------------------------------------------------- JWKS cache
+class _JwksCache:
+    """Process-wide JWKS documents keyed by the (trusted) URI, with a TTL.
+
+    Only configured URIs or allowlisted ``jku`` URIs reach it, so it cannot be grown by
+    arbitrary tokens; a lock makes concurrent first fetches of one URI fetch once."""
+
+    def __init__(self, ttl_s: float = 300.0, size: int = 64):
+        self.ttl_s = ttl_s
+        self.size = size
+        self._lock = threading.Lock()
+        self._docs: "OrderedDict[str, tuple]" = OrderedDict()
+
+    def get(self, uri: str) -> dict:
+        now = time.monotonic()
+        with self._lock:
+            hit = self._docs.get(uri)
+            if hit is not None and now - hit[0] < self.ttl_s:
+                return hit[1]
+            import requests
+            doc = requests.get(uri, timeout=10).json()
+            self._docs[uri] = (now, doc)
+            self._docs.move_to_end(uri)
+            while len(self._docs) > self.size:
+                self._docs.popitem(last=False)
+            return doc
+
+    def clear(self) -> None:
+        with self._lock:
+            self._docs.clear()
+
+
+_JWKS_CACHE = _JwksCache()
 
 
 # ---------------------------------------------------------------- providers
@@ -205,20 +246,29 @@ class JwtAuthProvider(AuthProvider):
         self.auth_claim = _cfg(self.cfg, "auth-claim", "authClaim", default="sub")
         self.audience = _cfg(self.cfg, "audience")
         self.audience_claim = _cfg(self.cfg, "audience-claim", "audienceClaim", default="aud")
-        self._jwks_cache: Dict[str, dict] = {}
+
+    def _trusted_uri(self, header: dict) -> Optional[str]:
+        """The JWKS URI to use for this token.
+
+        A token-supplied ``jku`` is followed only when a non-empty allowlist matches its
+        host (``JwksUriSigningKeyResolver.java:131-134`` throws 'Untrusted hostname' when
+        the allowlist is missing); otherwise the configured ``jwks-uri`` is used."""
+        jku = header.get("jku")
+        if jku and jku != self.jwks_uri:
+            host = urllib.parse.urlparse(str(jku)).hostname or ""
+            if not self.jwks_hosts or not any(host == h or str(jku).startswith(h) for h in self.jwks_hosts):
+                raise JwtError(f"Untrusted hostname {host!r} for jku")
+            return str(jku)
+        return self.jwks_uri
 
     def _jwks(self, header: dict) -> Optional[tuple]:
-        uri = header.get("jku") or self.jwks_uri
+        uri = self._trusted_uri(header)
         if not uri:
             return None
-        host = urllib.parse.urlparse(uri).hostname or ""
-        if self.jwks_hosts and not any(host == h or uri.startswith(h) for h in self.jwks_hosts):
-            raise JwtError(f"jwks host {host} not allowed")
-        keys = self._jwks_cache.get(uri)
-        if keys is None:
-            import requests
-            keys = requests.get(uri, timeout=30).json()
-            self._jwks_cache[uri] = keys
+        try:
+            keys = _JWKS_CACHE.get(uri)
+        except Exception as e:  # noqa: BLE001
+            raise JwtError(f"cannot fetch JWKS from {uri}: {e}") from e
         for k in keys.get("keys", []):
             if header.get("kid") in (None, k.get("kid")) and k.get("kty") == "RSA":
                 return rsa_from_jwk(k)
@@ -261,6 +311,7 @@ class GoogleAuthProvider(JwtAuthProvider):
     def __init__(self, configuration):
         super().__init__(configuration)
         self.jwks_uri = self.jwks_uri or self.GOOGLE_JWKS
+        self.jwks_hosts = []  # Google's provider never trusts token-supplied key URIs
         self.audience = _cfg(self.cfg, "clientId", "client-id")
 
     def authenticate(self, ctx) -> AuthResult:
@@ -281,3 +332,30 @@ def load_provider(name: str, configuration: Dict[str, Any]) -> AuthProvider:
     if f is None:
         raise ValueError(f"unknown gateway authentication provider {name}; known: {sorted(PROVIDERS)}")
     return f(configuration)
+
+
+class _ProviderCache:
+    """One provider instance per (provider, configuration): the gateway authenticates
+    every request, and building a provider per request would drop its state."""
+
+    def __init__(self, size: int = 256):
+        self._lock = threading.Lock()
+        self._items: "OrderedDict[str, AuthProvider]" = OrderedDict()
+        self._size = size
+
+    def get(self, name: str, configuration: Dict[str, Any]) -> AuthProvider:
+        key = name + "\x00" + json.dumps(configuration or {}, sort_keys=True, default=str)
+        with self._lock:
+            p = self._items.get(key)
+            if p is not None:
+                self._items.move_to_end(key)
+                return p
+        p = load_provider(name, configuration)
+        with self._lock:
+            self._items[key] = p
+            while len(self._items) > self._size:
+                self._items.popitem(last=False)
+        return p
+
+
+PROVIDER_CACHE = _ProviderCache()

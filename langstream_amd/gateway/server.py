@@ -45,7 +45,7 @@ from ..api.record import Header, Record, SimpleRecord
 from ..api.topics import TopicConnectionsRuntimeRegistry, TopicOffsetPosition
 from ..core.placeholders import resolve_placeholders
 from ..core.store import ApplicationStore
-from .auth import AuthResult, load_provider, test_principal_values
+from .auth import PROVIDER_CACHE, AuthResult, load_provider, test_principal_values
 
 log = logging.getLogger(__name__)
 SERVICE_REQUEST_ID_HEADER = "langstream-service-request-id"
@@ -219,7 +219,7 @@ class GatewayService:
                 raise GatewayError(res.reason if res else "Authentication provider returned null", 401)
             ctx.principal_values = test_principal_values(ctx.test_credentials)
             return
-        res: AuthResult = load_provider(auth.provider, auth.configuration).authenticate(ctx)
+        res: AuthResult = PROVIDER_CACHE.get(auth.provider, auth.configuration).authenticate(ctx)
         if res is None:
             raise GatewayError("Authentication provider returned null", 401)
         if not res.authenticated:
