@@ -63,7 +63,7 @@ class VectorCollectionManager(AssetManager):
 
     def delete_asset_if_exists(self) -> None:
         from ..engine.vector_store import VectorStoreRegistry
-        VectorStoreRegistry.drop(self.cfg["collection-name"])
+        VectorStoreRegistry.drop(self.cfg["collection-name"], purge=True)
 
 
 class CassandraTableManager(AssetManager):

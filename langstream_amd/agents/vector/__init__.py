@@ -48,6 +48,70 @@ class QueryVectorDBAgent(AgentProcessor):
             fut.add_done_callback(done)
 
 
+class _UpsertBatcher:
+    """Coalesces the sink's per-record writes into batched store mutations: one
+    normalise + one ``index_copy_`` (+ one WAL append) per batch instead of per record.
+    A single flusher thread applies operations in submission order, so per-id order
+    is kept; each record's future completes once its batch is applied (and logged)."""
+
+    def __init__(self, collection: str, max_batch: int = 512, linger_s: float = 0.002):
+        self.collection = collection
+        self.max_batch = max_batch
+        self.linger_s = linger_s
+        self._q: List[tuple] = []
+        self._cv = threading.Condition()
+        self._stop = False
+        self._t = threading.Thread(target=self._loop, name=f"vector-upsert-{collection}", daemon=True)
+        self._t.start()
+
+    def submit(self, op: str, rid, vec, vals) -> Future:
+        f: Future = Future()
+        with self._cv:
+            self._q.append((op, rid, vec, vals, f))
+            self._cv.notify()
+        return f
+
+    def close(self) -> None:
+        with self._cv:
+            self._stop = True
+            self._cv.notify()
+        self._t.join(5)
+
+    def _loop(self) -> None:
+        while True:
+            with self._cv:
+                while not self._q and not self._stop:
+                    self._cv.wait()
+                if not self._q and self._stop:
+                    return
+                if len(self._q) < self.max_batch and not self._stop:
+                    self._cv.wait(self.linger_s)
+                batch, self._q = self._q[: self.max_batch], self._q[self.max_batch:]
+            i = 0
+            while i < len(batch):   # runs of the same operation
+                j = i
+                while j < len(batch) and batch[j][0] == batch[i][0]:
+                    j += 1
+                self._apply(batch[i][0], batch[i:j])
+                i = j
+
+    def _apply(self, op: str, items) -> None:
+        try:
+            if op == "d":
+                if VectorStoreRegistry.exists(self.collection):
+                    VectorStoreRegistry.get(self.collection).delete([it[1] for it in items])
+            else:
+                dim = len(items[0][2])
+                VectorStoreRegistry.get(self.collection, dim).upsert(
+                    [it[1] for it in items], [it[2] for it in items], [it[3] for it in items])
+            for it in items:
+                it[4].set_result(None)
+        except Exception as e:  # noqa: BLE001
+            for it in items:
+                if not it[4].done():
+                    it[4].set_exception(e)
+
+
 class _LocalWriter:
     """fields: id / vector / anything else -> metadata; collection-name."""
 
@@ -58,8 +122,9 @@ class _LocalWriter:
         names = {f.get("name") for f in self.fields}
         if "vector" not in names:
             raise ValueError("vector-db-sink (local): a field named 'vector' is required")
+        self.batcher = _UpsertBatcher(self.collection, int(cfg.get("batch-size", 512)))
 
-    def upsert(self, mr: MutableRecord) -> None:
+    def upsert(self, mr: MutableRecord) -> Future:
         ctx = mr.el_context()
         vals = {f["name"]: eval_expression(f["expression"], ctx) for f in self.fields}
         rid = vals.pop("id", None)
@@ -69,12 +134,13 @@ class _LocalWriter:
             rid = json.dumps(rid, sort_keys=True)
         vec = vals.pop("vector")
         if mr.value is None or vec is None:
-            if VectorStoreRegistry.exists(self.collection):
-                VectorStoreRegistry.get(self.collection).delete([rid])
-            return
+            return self.batcher.submit("d", rid, None, None)
         if isinstance(vec, str):
             vec = json.loads(vec)
-        VectorStoreRegistry.get(self.collection, len(vec)).upsert([rid], [vec], [vals])
+        return self.batcher.submit("u", rid, vec, vals)
+
+    def close(self) -> None:
+        self.batcher.close()
 
 
 class _JdbcWriter:
@@ -119,12 +185,12 @@ class _JdbcWriter:
             if table == self.table.lower():
                 for k, v in vals.items():
                     if k.lower() == col and isinstance(v, list):
-                        VectorStoreRegistry.get(name, len(v)).upsert([rowid], [v])
+                        VectorStoreRegistry.get(name, len(v), persist=False).upsert([rowid], [v])
 
     def _mirror_delete(self, rowids) -> None:
         for (table, col), name in list(self.ds.vector_cols.items()):
             if table == self.table.lower() and VectorStoreRegistry.exists(name):
-                VectorStoreRegistry.get(name).delete(rowids)
+                VectorStoreRegistry.get(name, persist=False).delete(rowids)
 
 
 def _remote_writers():
@@ -139,6 +205,8 @@ class VectorDBSinkAgent(AgentSink):
         ds = self.cfg.get("datasource") or {}
         svc = ds.get("service", "local")
         if svc in ("local", "local-gpu"):
+            if ds.get("persist-directory"):
+                VectorStoreRegistry.configure(persist_dir=ds["persist-directory"], fsync=ds.get("fsync"))
             self.writer = _LocalWriter(self.cfg)
         elif svc in ("jdbc", "sqlite"):
             self.writer = _JdbcWriter(self.cfg)

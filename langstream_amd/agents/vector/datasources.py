@@ -73,6 +73,8 @@ class LocalVectorDataSource(DataSource):
 
     def __init__(self, cfg: Dict[str, Any]):
         self.cfg = cfg
+        if cfg.get("persist-directory"):
+            VectorStoreRegistry.configure(persist_dir=cfg["persist-directory"], fsync=cfg.get("fsync"))
         self.default_collection = cfg.get("collection-name") or cfg.get("collection") or "default"
 
     def _store(self, name: Optional[str], dim: Optional[int] = None):
@@ -100,7 +102,7 @@ class LocalVectorDataSource(DataSource):
                     out[i] = []
                 continue
             flt = json.loads(flt_s)
-            over = k if not flt else min(64, max(k * 4, k))
+            over = k if not flt else k * 4
             res = self._store(coll).search([parsed[i]["vector"] for i in idxs], over, with_vectors=inc)
             for i, rows in zip(idxs, res):
                 if flt:
@@ -190,8 +192,8 @@ class SqliteDataSource(DataSource):
             if isinstance(vec, str):
                 vec = json.loads(vec)
             self._ensure_mirror(table, col, len(vec))
-            store = VectorStoreRegistry.get(name)
-            hits = store.search([vec], min(k, 64))[0] if len(store) else []
+            store = VectorStoreRegistry.get(name, persist=False)
+            hits = store.search([vec], k)[0] if len(store) else []
             if not hits:
                 return []
             ids = [h["id"] for h in hits]
@@ -221,7 +223,7 @@ class SqliteDataSource(DataSource):
         if key in self.vector_cols:
             return
         name = self._store_name(table, col)
-        store = VectorStoreRegistry.get(name, dim)
+        store = VectorStoreRegistry.get(name, dim, persist=False)  # a mirror: rebuilt from SQL
         with self.lock:
             rows = self.conn.execute(f"SELECT rowid, {col} FROM {table}").fetchall()
         ids, vecs = [], []

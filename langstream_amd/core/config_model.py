@@ -272,7 +272,8 @@ for _t in ("sink", "source"):
 _SINK_FIELDS = L("Fields to write.", True, _NAMED_EXPR)
 VECTOR_SINK_MODELS: Dict[str, Model] = {
     "local": Model("Local GPU vector store", "Writes into the HBM-resident vector collection.", {
-        "collection-name": S("Collection."), "fields": L("Fields to write.", items=_NAMED_EXPR)}),
+        "collection-name": S("Collection."), "fields": L("Fields to write.", items=_NAMED_EXPR),
+        "batch-size": I("Max records per batched store mutation.", default=512)}),
     "jdbc": Model("JDBC", "Upserts rows into a table.", {
         "table-name": S("Table.", True), "fields": L("Columns.", True, O(properties={
             "name": S("Column.", True), "expression": S("EL expression.", True, el=True),
@@ -354,7 +355,8 @@ DATASOURCE_MODELS: Dict[str, Model] = {
     "astra-vector-db": Model("Astra Vector DB", "Astra Data API.", {
         "endpoint": S("API endpoint."), "token": S("Token."), "keyspace": S("Keyspace.")}),
     "local": Model("Local GPU vector store", "HBM-resident vector collections + SQLite tables.", {
-        "path": S("Persistence directory."), "collection": S("Default collection."),
+        "path": S("SQLite path."), "persist-directory": S("Vector-store persistence directory (WAL + snapshots)."),
+        "fsync": B("fsync every WAL append (default: flush to the OS only)."), "collection": S("Default collection."),
         "collection-name": S("Default collection."), "url": S("SQLite URL.")}, allow_unknown=True),
 }
 for _a, _b in (("local-gpu", "local"), ("sqlite", "jdbc")):

@@ -12,6 +12,7 @@
 namespace py = pybind11;
 
 void bind_memlog(py::module_& m);
+void bind_shmlog(py::module_& m);
 void bind_tokenizer(py::module_& m);
 
 namespace {
@@ -58,7 +59,7 @@ class BlockAllocator {
 }  // namespace
 
 PYBIND11_MODULE(_lsnative, m) {
-  m.doc() = "langstream_amd native host runtime (memlog, tokenizers, KV block allocator)";
+  m.doc() = "langstream_amd native host runtime (memlog, shared-memory log, tokenizers, KV block allocator)";
   py::class_<BlockAllocator>(m, "BlockAllocator")
       .def(py::init<int>())
       .def("num_free", &BlockAllocator::num_free)
@@ -69,5 +70,6 @@ PYBIND11_MODULE(_lsnative, m) {
       .def("free", &BlockAllocator::free)
       .def("refcount", &BlockAllocator::refcount);
   bind_memlog(m);
+  bind_shmlog(m);
   bind_tokenizer(m);
 }

@@ -1,0 +1,198 @@
+"""Local vector store: explicit limits (k > 64, dims without a kernel), batched deletes,
+WAL + snapshot persistence, and a kill -9 / restart of an ingest pipeline on shared-
+memory topics that must lose no chunk (write-ahead of upserts relative to the offset
+commit; parity: VEC/jdbc/JdbcWriter.java:33-208 persists before the commit)."""
+import os
+import signal
+import subprocess
+import sys
+import textwrap
+import time
+import uuid
+
+import pytest
+import torch
+
+from langstream_amd.engine.vector_store import VectorStore, VectorStoreRegistry
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _brute(vecs, q, k):
+    X = torch.nn.functional.normalize(torch.tensor(vecs, dtype=torch.float32), dim=-1)
+    qq = torch.nn.functional.normalize(torch.tensor(q, dtype=torch.float32), dim=-1)
+    return torch.topk(qq @ X.t(), k, dim=-1).indices.tolist()
+
+
+def test_k_above_64_is_exact_not_clamped():
+    g = torch.Generator().manual_seed(0)
+    vecs = torch.randn(500, 64, generator=g).tolist()
+    s = VectorStore(64, device="cpu", dtype=torch.float32)
+    s.upsert(list(range(500)), vecs)
+    q = torch.randn(3, 64, generator=g).tolist()
+    res = s.search(q, 100)
+    assert all(len(r) == 100 for r in res)
+    assert [[d["id"] for d in r] for r in res] == _brute(vecs, q, 100)
+
+
+def test_dim_without_kernel_instantiation_works():
+    s = VectorStore(100, device="cpu", dtype=torch.float32)
+    assert not s.kernel_dim
+    g = torch.Generator().manual_seed(1)
+    vecs = torch.randn(50, 100, generator=g).tolist()
+    s.upsert([f"r{i}" for i in range(50)], vecs)
+    res = s.search([vecs[7]], 3)[0]
+    assert res[0]["id"] == "r7" and abs(res[0]["similarity"] - 1.0) < 1e-5
+    with pytest.raises(ValueError):
+        s.upsert(["bad"], [[0.0] * 99])
+
+
+def test_batched_delete_keeps_dense_rows_consistent():
+    g = torch.Generator().manual_seed(2)
+    vecs = torch.randn(40, 32, generator=g)
+    s = VectorStore(32, device="cpu", dtype=torch.float32)
+    s.upsert(list(range(40)), vecs.tolist(), [{"i": i} for i in range(40)])
+    dead = [0, 3, 39, 38, 20, 21, 22, 7, 999]
+    assert s.delete(dead) == 8
+    alive = [i for i in range(40) if i not in dead]
+    assert len(s) == len(alive)
+    for i in alive:  # every survivor is still found as its own nearest neighbour
+        r = s.search([vecs[i].tolist()], 1)[0][0]
+        assert r["id"] == i and r["i"] == i
+    # duplicate ids in one upsert: last wins
+    s.upsert([1, 1], [vecs[5].tolist(), vecs[6].tolist()], [{"v": 5}, {"v": 6}])
+    assert s.get(1) == {"v": 6}
+
+
+def test_wal_and_snapshot_restore(tmp_path):
+    d = str(tmp_path / "coll")
+    g = torch.Generator().manual_seed(3)
+    vecs = torch.randn(30, 16, generator=g)
+    s = VectorStore(16, device="cpu", dtype=torch.float32, persist_dir=d, name="c")
+    s.upsert(list(range(20)), vecs[:20].tolist(), [{"t": str(i)} for i in range(20)])
+    s.delete([2, 4])
+    s.snapshot()                                   # compaction point
+    s.upsert(list(range(20, 30)), vecs[20:].tolist(), [{"t": str(i)} for i in range(20, 30)])
+    s.delete([25])
+    s.upsert(["x"], [vecs[0].tolist()], [{"t": "x"}])
+    s.close()
+    r = VectorStore(16, device="cpu", dtype=torch.float32, persist_dir=d, name="c")
+    assert len(r) == 28
+    assert r.get(3) == {"t": "3"} and r.get(2) is None and r.get(25) is None and r.get("x") == {"t": "x"}
+    assert r.search([vecs[27].tolist()], 1)[0][0]["id"] == 27
+
+
+def test_registry_restores_collection_after_restart(tmp_path):
+    VectorStoreRegistry.reset()
+    VectorStoreRegistry.configure(persist_dir=str(tmp_path))
+    try:
+        VectorStoreRegistry.get("docs", 8, device="cpu").upsert(["a"], [[1.0] * 8], [{"text": "hello"}])
+        VectorStoreRegistry.reset()                   # "process restart"
+        assert VectorStoreRegistry.exists("docs")
+        assert VectorStoreRegistry.get("docs", device="cpu").get("a") == {"text": "hello"}
+        VectorStoreRegistry.drop("docs", purge=True)
+        assert not VectorStoreRegistry.exists("docs")
+    finally:
+        VectorStoreRegistry.reset()
+        VectorStoreRegistry.persist_dir = None
+
+
+WORKER = textwrap.dedent('''
+    import sys, time
+    sys.path.insert(0, {root!r})
+    from langstream_amd.runtime.local import LocalApplicationRunner
+    APP = """
+    topics:
+      - name: "chunks"
+        creation-mode: create-if-not-exists
+        partitions: 2
+    pipeline:
+      - name: "write"
+        id: "write"
+        type: "vector-db-sink"
+        input: "chunks"
+        configuration:
+          datasource: "LocalVectors"
+          collection-name: "docs"
+          fields:
+            - name: "id"
+              expression: "key"
+            - name: "vector"
+              expression: "value.vec"
+            - name: "text"
+              expression: "value.text"
+    """
+    CONF = """
+    configuration:
+      resources:
+        - type: "vector-database"
+          name: "LocalVectors"
+          configuration:
+            service: "local"
+            persist-directory: "{store}"
+    """
+    INSTANCE = """
+    instance:
+      streamingCluster:
+        type: "shm"
+        configuration:
+          name: "{log}"
+          size-mb: 64
+          block-kb: 64
+      computeCluster:
+        type: "none"
+    """
+    r = LocalApplicationRunner.from_yaml({{"pipeline.yaml": APP, "configuration.yaml": CONF}}, instance=INSTANCE,
+                                         application_id="durable")
+    r.start()
+    print("started", flush=True)
+    while not r.errors:
+        time.sleep(0.05)
+    raise r.errors[0]
+''')
+
+
+def test_kill_restart_replays_committed_offsets_without_loss(tmp_path):
+    from langstream_amd.api.model import StreamingCluster
+    from langstream_amd.api.record import SimpleRecord
+    from langstream_amd.topics.shm import ShmTopicConnectionsRuntime, unlink_shmlog
+    logname = f"dur-{uuid.uuid4().hex[:8]}"
+    store = str(tmp_path / "store")
+    script = tmp_path / "worker.py"
+    script.write_text(WORKER.format(root=ROOT, store=store, log=logname))
+    rt = ShmTopicConnectionsRuntime()
+    rt.init(StreamingCluster("shm", {"name": logname, "size-mb": 64, "block-kb": 64}))
+    rt.log.create_topic("chunks", 2, 0)
+    group = "langstream-agent-write"
+    prod = rt.create_producer("t", None, {"topic": "chunks"})
+    n = 400
+    try:
+        a = subprocess.Popen([sys.executable, str(script)], stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+        assert a.stdout.readline().strip() == b"started"
+        for i in range(n):
+            prod.write(SimpleRecord.of(f"c{i}", {"vec": [float(i % 7 + 1), 1.0, float(i % 3)], "text": f"t{i}"})) \
+                .result(5)
+        deadline = time.time() + 60
+        while sum(rt.log.committed("chunks", group)) < 40 and time.time() < deadline:
+            time.sleep(0.001)
+        a.send_signal(signal.SIGKILL)                     # crash mid-stream
+        a.wait(30)
+        done_at_kill = sum(rt.log.committed("chunks", group))
+        assert 0 < done_at_kill
+        b = subprocess.Popen([sys.executable, str(script)], stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+        assert b.stdout.readline().strip() == b"started"
+        deadline = time.time() + 90
+        while sum(rt.log.committed("chunks", group)) < n and time.time() < deadline:
+            time.sleep(0.05)
+        assert sum(rt.log.committed("chunks", group)) == n
+        b.send_signal(signal.SIGKILL)
+        b.wait(30)
+        VectorStoreRegistry.reset()
+        VectorStoreRegistry.configure(persist_dir=store)
+        s = VectorStoreRegistry.get("docs", device="cpu")
+        assert len(s) == n                                # every chunk indexed exactly once
+        assert s.get("c123") == {"text": "t123"}
+    finally:
+        VectorStoreRegistry.reset()
+        VectorStoreRegistry.persist_dir = None
+        unlink_shmlog(logname, size_mb=64)
