@@ -2,24 +2,36 @@
 
 BASELINE.json config 4 ("full RAG pipeline (crawl->split->embed->vector-write;
 query->vector-query->chat) Llama-3-8B, 8 agent replicas DP on 8xMI355X"), run through
-the framework itself (YAML app -> planner -> fused composite agents -> AgentRunner on
-memory topics), both pipelines concurrently in every timed step:
+the framework itself (YAML app -> planner -> fused composite agents -> AgentRunner),
+all three pipelines concurrently in every timed step:
 
-  ingest: documents -> text-splitter (cl100k length) -> document-to-json
-          -> compute-ai-embeddings (bge-small-en, GPU) -> vector-db-sink (HBM store)
+  crawl:  webcrawler-source (rank 0 only, like the reference's single crawler replica)
+          fetching the step's new pages from a local HTTP site -> documents-topic
+  ingest: documents -> text-extractor -> text-splitter (cl100k length) -> document-to-json
+          -> compute-ai-embeddings (bge-small-en, GPU) -> vector-db-sink (HBM shard)
   query:  questions -> document-to-json -> compute-ai-embeddings (GPU)
-          -> query-vector-db (GPU kNN top-20) -> re-rank (MMR, top-5)
+          -> query-vector-db (GPU kNN top-20 over EVERY rank's shard) -> re-rank (MMR, top-5)
           -> ai-chat-completions (Llama-3-8B, GPU, streamed to answers-topic)
           -> drop-fields -> log-topic
 
-One process per GPU (torchrun), each an independent agent replica (data parallel,
-weak scaling: a fixed batch per GPU per step).  Before timing, each rank loads a
-synthetic corpus through the GPU encoder into its vector store (untimed).  A step =
-produce B questions + D documents (the crawled pages), wait for all B answers and for
-every chunk of the D documents to be indexed; time K steps after W warmup steps.
-value = answered questions per second over all ranks (max time over ranks); the
-ingest rate is reported alongside.  Weights are random-init (no checkpoints offline);
-data is synthetic.
+Data parallelism is the reference's: one process per GPU, every process
+running a replica of each agent, the replicas of an agent forming ONE consumer group
+over the partitions of its input topic.  Topics live in the cross-process shared-memory
+log (``shm`` streaming type), so any replica may answer any rank's question; the vector
+store is sharded (each rank indexes the chunks it consumed) and query-vector-db returns
+the global top-k through the sharded kNN service (RCCL all-gather / all-to-all).
+
+``python bench.py --gpus N`` (no torchrun environment) launches N rank processes with
+torch.distributed.run itself before anything touches the GPU; under torchrun
+(WORLD_SIZE set) ``--gpus`` must equal WORLD_SIZE.
+
+Weak scaling: per GPU per step, B questions and D crawled pages; before timing each rank
+loads a synthetic corpus into its shard (untimed).  A step ends when every question of
+the rank has its answer and every page crawled so far is fully indexed (committed by the
+ingest consumer group).  K steps are timed after W warmup steps, bracketed by a barrier
+and a device synchronize on both sides; value = answered questions per second over all
+ranks (max elapsed over ranks).  Weights are random-init (no checkpoints offline); data
+is synthetic.
 """
 from __future__ import annotations
 
@@ -27,8 +39,12 @@ import argparse
 import json
 import os
 import statistics
+import subprocess
 import sys
+import threading
 import time
+import uuid
+import zlib
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
@@ -37,7 +53,7 @@ APP = """
 topics:
   - name: "questions-topic"
     creation-mode: create-if-not-exists
-    partitions: 4
+    partitions: {q_parts}
   - name: "answers-topic"
     creation-mode: create-if-not-exists
   - name: "log-topic"
@@ -46,6 +62,7 @@ errors:
   on-failure: "fail"
 pipeline:
   - name: "convert-to-structure"
+    id: "query"
     type: "document-to-json"
     input: "questions-topic"
     configuration:
@@ -116,11 +133,14 @@ INGEST = """
 topics:
   - name: "documents-topic"
     creation-mode: create-if-not-exists
-    partitions: 2
+    partitions: {d_parts}
 pipeline:
+  - name: "extract"
+    id: "ingest"
+    type: "text-extractor"
+    input: "documents-topic"
   - name: "split"
     type: "text-splitter"
-    input: "documents-topic"
     configuration:
       chunk_size: 256
       chunk_overlap: 32
@@ -152,6 +172,28 @@ pipeline:
           expression: "value.text"
 """
 
+CRAWL = """
+topics:
+  - name: "documents-topic"
+    creation-mode: create-if-not-exists
+    partitions: {d_parts}
+pipeline:
+  - name: "crawl"
+    id: "crawler"
+    type: "webcrawler-source"
+    output: "documents-topic"
+    configuration:
+      seed-urls: ["{site}/step/0/index.html"]
+      allowed-domains: ["{site}"]
+      max-urls: 10000000
+      max-depth: 10000000
+      handle-robots-file: false
+      min-time-between-requests: 0
+      http-timeout: 1800000
+      state-storage: disk
+      max-unflushed-pages: 1000
+"""
+
 CONFIGURATION = """
 configuration:
   resources:
@@ -170,12 +212,115 @@ configuration:
         collection-name: "documents"
 """
 
+INSTANCE = """
+instance:
+  streamingCluster:
+    type: "shm"
+    configuration:
+      name: "{shm}"
+      size-mb: {shm_mb}
+  computeCluster:
+    type: "none"
+"""
+
+METRIC = "records/sec (whole node) + p50 end-to-end latency, RAG pipeline Llama-3-8B"
+
 
 def _env_int(k, d):
     try:
         return int(os.environ.get(k, d))
     except ValueError:
         return d
+
+
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _launch(argv, n: int) -> int:
+    """Start N ranks with torch.distributed.run (this process never touches the GPU)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__), *argv]
+    return subprocess.call(cmd)
+
+
+def balanced_key(prefix: str, target: int, parts: int) -> str:
+    """A record key whose crc32 partition (the producers' key hash) is ``target``: keys
+    are spread evenly over the partitions, so every consumer-group member gets the same
+    share of each step."""
+    salt = 0
+    while True:
+        k = f"{prefix}.{salt}"
+        if zlib.crc32(k.encode()) % parts == target:
+            return k
+        salt += 1
+
+
+def make_page(i: int, corpus) -> str:
+    """A crawled page: ~12 paragraphs of corpus sentences."""
+    return "\n\n".join(" ".join(corpus[(i * 31 + p * 7 + j) % len(corpus)] for j in range(5)) for p in range(12))
+
+
+class Site:
+    """Local HTTP site the crawler walks: /step/<n>/index.html lists that step's pages
+    and links the next step's index, which long-polls until the step is published."""
+
+    def __init__(self, corpus, per_step: int):
+        import http.server
+        self.corpus, self.per_step = corpus, per_step
+        self.published = -1
+        self.cv = threading.Condition()
+        site = self
+
+        class H(http.server.BaseHTTPRequestHandler):
+            protocol_version = "HTTP/1.1"
+
+            def log_message(self, *a):
+                pass
+
+            def do_GET(self):
+                parts = self.path.strip("/").split("/")
+                if len(parts) != 3 or parts[0] != "step":
+                    return self._send(404, b"")
+                step = int(parts[1])
+                with site.cv:
+                    site.cv.wait_for(lambda: site.published >= step, timeout=1800)
+                if site.published < step:
+                    return self._send(503, b"")
+                if parts[2] == "index.html":
+                    links = "".join(f'<a href="/step/{step}/{d}.html">p{d}</a>' for d in range(site.per_step))
+                    body = f'<html><body>{links}<a href="/step/{step + 1}/index.html">next</a></body></html>'
+                else:
+                    d = int(parts[2].split(".")[0])
+                    text = make_page(step * site.per_step + d, site.corpus)
+                    body = "<html><body>" + "".join(f"<p>{p}</p>" for p in text.split("\n\n")) + "</body></html>"
+                self._send(200, body.encode())
+
+            def _send(self, code, body):
+                self.send_response(code)
+                self.send_header("Content-Type", "text/html; charset=utf-8")
+                self.send_header("Content-Length", str(len(body)))
+                self.end_headers()
+                self.wfile.write(body)
+
+        self.httpd = http.server.ThreadingHTTPServer(("127.0.0.1", 0), H)
+        self.httpd.daemon_threads = True
+        self.url = f"http://127.0.0.1:{self.httpd.server_address[1]}"
+        threading.Thread(target=self.httpd.serve_forever, daemon=True).start()
+
+    def publish(self, step: int) -> None:
+        with self.cv:
+            self.published = step
+            self.cv.notify_all()
+
+    def close(self) -> None:
+        self.publish(1 << 30)
+        self.httpd.shutdown()
 
 
 def main():
@@ -185,151 +330,216 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--batch", type=int, default=256, help="questions per GPU per step")
     ap.add_argument("--max-tokens", type=int, default=128)
-    ap.add_argument("--corpus", type=int, default=50000, help="documents in each rank's vector store")
-    ap.add_argument("--docs", type=int, default=32, help="documents ingested per GPU per step (0: query only)")
+    ap.add_argument("--corpus", type=int, default=50000, help="documents in each rank's vector-store shard")
+    ap.add_argument("--docs", type=int, default=32, help="pages crawled per GPU per step (0: query only)")
+    ap.add_argument("--no-crawl", action="store_true", help="produce pages into documents-topic directly")
     ap.add_argument("--chat-model", default="llama-3-8b")
     ap.add_argument("--embed-model", default="bge-small-en")
     ap.add_argument("--device", default=None)
     ap.add_argument("--timeout", type=float, default=900.0)
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(_launch(sys.argv[1:], args.gpus))
     rank, world, local = _env_int("RANK", 0), _env_int("WORLD_SIZE", 1), _env_int("LOCAL_RANK", 0)
+    if world != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+
     import torch
     import torch.distributed as dist
     use_gpu = torch.cuda.is_available()
     if use_gpu:
         torch.cuda.set_device(local)
+    ctrl = None
     if world > 1:
         dist.init_process_group("nccl" if use_gpu else "gloo")
+        ctrl = dist.new_group(backend="gloo")   # barriers / small host exchanges
 
     def barrier():
         if world > 1:
-            dist.barrier()
+            dist.barrier(group=ctrl)
         if use_gpu:
             torch.cuda.synchronize()
 
+    def bcast(obj):
+        if world == 1:
+            return obj
+        box = [obj]
+        dist.broadcast_object_list(box, src=0, group=ctrl)
+        return box[0]
+
+    from langstream_amd.engine import dist_knn
     from langstream_amd.engine.vector_store import VectorStoreRegistry
     from langstream_amd.runtime.local import LocalApplicationRunner
     from langstream_amd.services import ServiceRegistry
     from langstream_amd.tokenizers import builtin_corpus
+    from langstream_amd.topics.shm import unlink_shmlog
 
     device = args.device or (f"cuda:{local}" if use_gpu else "cpu")
     chat_model, embed_model = args.chat_model, args.embed_model
     if not use_gpu and args.chat_model == "llama-3-8b":
         chat_model, embed_model = "llama-tiny", "bert-tiny"  # CPU plumbing mode only
+    q_parts, d_parts = max(4, 2 * world), max(2, 2 * world)
+    shm = bcast(f"bench-{uuid.uuid4().hex[:12]}")
+    shm_mb = 2048 + 512 * world
     fmt = dict(chat_model=chat_model, embed_model=embed_model, max_tokens=args.max_tokens,
-               max_batch=max(args.batch, 1), max_len=4096, prefill=16384)
+               max_batch=max(args.batch, 1), max_len=4096, prefill=16384, q_parts=q_parts, d_parts=d_parts,
+               shm=shm, shm_mb=shm_mb)
+    corpus = builtin_corpus(max(4000, args.corpus // 4 + 1))
+    crawl = args.docs > 0 and not args.no_crawl
+    site = Site(corpus, args.docs * world) if crawl and rank == 0 else None
     files = {"pipeline.yaml": APP.format(**fmt), "ingest.yaml": INGEST.format(**fmt),
              "configuration.yaml": CONFIGURATION.format(**fmt)}
+    if crawl:
+        files["crawl.yaml"] = CRAWL.format(site=bcast(site.url if site else None), d_parts=d_parts)
     services = ServiceRegistry({"device": device})
     ServiceRegistry.set_default(services)
 
-    # ---- untimed setup: engines, corpus ingest into the HBM vector store
+    # ---- untimed setup: engines, corpus ingest into this rank's HBM shard
     t_setup = time.time()
     emb = services.embedding_engine(embed_model, {"embeddings-model": embed_model})
-    corpus = builtin_corpus(max(4000, args.corpus // 4 + 1))
     docs = [" ".join(corpus[(i * 7 + j) % len(corpus)] for j in range(4)) for i in range(args.corpus)]
     store = VectorStoreRegistry.get("documents", emb.dim, device=device)
     for i in range(0, len(docs), 8192):
         chunk = docs[i: i + 8192]
         vec = emb.embed_tensor(chunk)
-        store.upsert(list(range(i, i + len(chunk))), vec, [{"text": t} for t in chunk])
+        store.upsert([f"c{rank}-{j}" for j in range(i, i + len(chunk))], vec, [{"text": t} for t in chunk])
     llm = services.llm_engine(chat_model, {"chat-model": chat_model, "max-batch": fmt["max_batch"],
                                            "max-model-len": 4096, "max-prefill-tokens": 16384})
-    runner = LocalApplicationRunner.from_yaml(files, application_id="rag-bench", services=services)
+    if world > 1:
+        dist_knn.start(device=device)
+    only = None if rank == 0 else ["query", "ingest"]   # the crawler runs once (rank 0)
+    runner = LocalApplicationRunner.from_yaml(files, instance=INSTANCE.format(**fmt), application_id="rag-bench",
+                                              services=services, agents=only)
     runner.start()
+    log = runner.topic_runtime.log
+    barrier()
     prod = runner.producer("questions-topic")
     doc_prod = runner.producer("documents-topic")
     reader = runner.reader("log-topic")
+    ingest_group = "langstream-agent-ingest"
     setup_s = time.time() - t_setup
 
-    from langstream_amd.agents.text import RecursiveCharacterTextSplitter
-    from langstream_amd.api.record import SimpleRecord
-    from langstream_amd.tokenizers import cl100k_counter
-    splitter = RecursiveCharacterTextSplitter(["\n\n", "\n", " ", ""], False, 256, 32, cl100k_counter())
-    qwords = corpus
     seq = [0]
-    ingested = {"docs": 0, "chunks": 0}
+    steps_done = [0]
 
-    def make_doc(i: int) -> str:  # a crawled page: ~12 paragraphs of corpus sentences
-        return "\n\n".join(" ".join(corpus[(i * 31 + p * 7 + j) % len(corpus)] for j in range(5))
-                           for p in range(12))
+    def ingest_done(expected_docs: int) -> bool:
+        end = log.end_offsets("documents-topic")
+        return sum(end) >= expected_docs and log.committed("documents-topic", ingest_group) == end
 
-    def run_step(n, n_docs):
+    def run_step():
+        step = steps_done[0]
         sent = {}
         t0 = time.time()
-        base = len(store)
-        expect = 0
-        for d in range(n_docs):
-            text = make_doc(seq[0] * 7 + d)
-            expect += len(splitter.split_text(text))
-            doc_prod.write(SimpleRecord.of(f"doc-{rank}-{seq[0]}-{d}", text))
-        for i in range(n):
-            k = f"{rank}-{seq[0]}"
+        if args.docs > 0:
+            if crawl:
+                if site is not None:
+                    site.publish(step)
+            else:
+                for d in range(args.docs):
+                    i = (step * world + rank) * args.docs + d
+                    doc_prod.write(_rec(balanced_key(f"doc-{i}", i % d_parts, d_parts), make_page(i, corpus)))
+        for i in range(args.batch):
+            g = (step * world + rank) * args.batch + i
+            k = balanced_key(f"{rank}-{seq[0]}", g % q_parts, q_parts)
             seq[0] += 1
-            q = qwords[(seq[0] * 13) % len(qwords)]
             sent[k] = time.time()
-            prod.write(SimpleRecord.of(k, q))
+            prod.write(_rec(k, corpus[(g * 13) % len(corpus)]))
+        expect_docs = (step + 1) * args.docs * world
         lats = []
-        got = 0
         deadline = time.time() + args.timeout
-        while got < n or len(store) < base + expect:
+        while sent or (args.docs > 0 and not ingest_done(expect_docs)):
             if runner.errors:
                 raise runner.errors[0]
             if time.time() > deadline:
-                raise TimeoutError(f"only {got}/{n} records and {len(store) - base}/{expect} chunks completed")
+                raise TimeoutError(f"rank {rank}: {len(sent)} answers missing; documents end "
+                                   f"{log.end_offsets('documents-topic')} committed "
+                                   f"{log.committed('documents-topic', ingest_group)} (expected {expect_docs})")
             for r in reader.read().records:
                 t = sent.pop(r.key(), None)
                 if t is not None:
-                    got += 1
                     lats.append(time.time() - t)
-        ingested["docs"] += n_docs
-        ingested["chunks"] += expect
+        steps_done[0] += 1
         return time.time() - t0, lats
 
     for _ in range(args.warmup):
-        run_step(args.batch, args.docs)
+        run_step()
+    chunks0 = len(store)
     barrier()
     from langstream_amd.utils import threads as _threads
     cpu0 = _threads.snapshot()
+    stats0 = dict(llm.stats)
     t0 = time.time()
-    all_lats = []
+    my_lats = []
     for _ in range(args.steps):
-        _, lats = run_step(args.batch, args.docs)
-        all_lats.extend(lats)
+        _, lats = run_step()
+        my_lats.extend(lats)
     barrier()
     elapsed = time.time() - t0
+    chunks = len(store) - chunks0
     if os.environ.get("LANGSTREAM_THREAD_CPU"):
         print(json.dumps({"thread_cpu_s": _threads.diff(cpu0, _threads.snapshot())}), file=sys.stderr, flush=True)
-    p50 = statistics.median(all_lats) if all_lats else 0.0
+    stats = {k: v - stats0.get(k, 0) if isinstance(v, (int, float)) else v for k, v in llm.stats.items()}
+    assign = {}
+    for r in runner.runners:   # partitions this rank's replicas own (disjoint across ranks)
+        c = getattr(getattr(r, "source", None), "consumer", None)
+        if c is not None and hasattr(c, "get_info"):
+            info = c.get_info()
+            assign[info["topic"]] = info.get("assignment")
+    mine = {"elapsed": elapsed, "lats": my_lats, "chunks": chunks, "assign": assign,
+            "prefill_tokens": stats.get("prefill_tokens", 0), "requests": stats.get("requests", 0),
+            "knn_rounds": dist_knn.active().rounds if dist_knn.active() else 0}
     if world > 1:
-        t = torch.tensor([elapsed, p50], dtype=torch.float64, device=device if use_gpu else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, p50 = float(t[0]), float(t[1])
+        gathered = [None] * world
+        dist.all_gather_object(gathered, mine, group=ctrl)
+    else:
+        gathered = [mine]
+    elapsed = max(g["elapsed"] for g in gathered)
+    all_lats = [x for g in gathered for x in g["lats"]]
+    p50 = statistics.median(all_lats) if all_lats else 0.0
+    reqs = sum(g["requests"] for g in gathered)
+    mean_prompt = sum(g["prefill_tokens"] for g in gathered) / reqs if reqs else 0.0
     total = args.batch * args.steps * world
     value = total / elapsed
     if rank == 0:
         print(json.dumps({
-            "metric": "records/sec (whole node) + p50 end-to-end latency, RAG pipeline Llama-3-8B",
+            "metric": METRIC,
             "value": round(value, 3), "unit": "records/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(1000 * elapsed / args.steps, 2),
             "p50_latency_s": round(p50, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": "bf16" if use_gpu else "fp32", "data": "synthetic questions + synthetic corpus, random-init weights",
+            "dtype": "bf16" if use_gpu else "fp32",
+            "data": "synthetic questions + synthetic crawled pages + synthetic corpus, random-init weights",
             "config": {"model": chat_model, "embedding_model": embed_model, "global_batch": args.batch * world,
-                       "seq_len": 4096, "max_new_tokens": args.max_tokens, "corpus_docs_per_gpu": args.corpus,
-                       "top_k": 20, "rerank": 5, "ingest_docs_per_gpu_per_step": args.docs,
+                       "seq_len": round(mean_prompt, 1), "max_model_len": 4096, "max_new_tokens": args.max_tokens,
+                       "corpus_docs_per_gpu": args.corpus, "top_k": 20, "rerank": 5,
+                       "crawled_pages_per_gpu_per_step": args.docs, "crawl": crawl,
+                       "topics": "shm (cross-process consumer groups)",
                        "parallelism": f"dp{world}"},
-            "ingest": {"docs_per_s": round(args.docs * args.steps * world / elapsed, 2),
-                       "chunks_per_s_rank0": round(ingested["chunks"] * args.steps / max(1, args.steps + args.warmup)
-                                                   / elapsed, 2)},
+            "ingest": {"pages_per_s": round(args.docs * args.steps * world / elapsed, 2),
+                       "chunks_per_s": round(sum(g["chunks"] for g in gathered) / elapsed, 2)},
+            "latency_samples": len(all_lats), "knn_rounds_per_rank": [g["knn_rounds"] for g in gathered],
+            "partitions_per_rank": [g["assign"] for g in gathered],
             "setup_s": round(setup_s, 1),
-            "engine": dict(llm.stats, exec_ms=dict(zip(("upload", "enqueue", "download", "wait"),
-                                                       (round(x, 1) for x in llm.exec.timings())))),
+            "engine_rank0": dict(stats, exec_ms=dict(zip(("upload", "enqueue", "download", "wait"),
+                                                         (round(x, 1) for x in llm.exec.timings())))),
         }), flush=True)
+    barrier()
     runner.stop(timeout=10)
+    if world > 1:
+        dist_knn.stop()
     services.shutdown()
+    if site is not None:
+        site.close()
+    barrier()
+    if rank == 0:
+        unlink_shmlog(shm, size_mb=shm_mb)
     if world > 1:
         dist.destroy_process_group()
+
+
+def _rec(key, value):
+    from langstream_amd.api.record import SimpleRecord
+    return SimpleRecord.of(key, value)
 
 
 if __name__ == "__main__":

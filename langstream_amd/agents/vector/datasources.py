@@ -96,14 +96,20 @@ class LocalVectorDataSource(DataSource):
             flt = q.get("filter") or {}
             key = (coll, k, json.dumps(flt, sort_keys=True), bool(q.get("include-vector", False)))
             groups.setdefault(key, []).append(i)
+        from ...engine import dist_knn
+        sharded = dist_knn.active()   # DP replicas: global top-k over every rank's shard
         for (coll, k, flt_s, inc), idxs in groups.items():
-            if not VectorStoreRegistry.exists(coll):
+            if sharded is None and not VectorStoreRegistry.exists(coll):
                 for i in idxs:
                     out[i] = []
                 continue
             flt = json.loads(flt_s)
             over = k if not flt else k * 4
-            res = self._store(coll).search([parsed[i]["vector"] for i in idxs], over, with_vectors=inc)
+            vecs = [parsed[i]["vector"] for i in idxs]
+            if sharded is not None:
+                res = sharded.search(coll, vecs, over, with_vectors=inc).result()
+            else:
+                res = self._store(coll).search(vecs, over, with_vectors=inc)
             for i, rows in zip(idxs, res):
                 if flt:
                     rows = [r for r in rows if all(r.get(f) == v for f, v in flt.items())]

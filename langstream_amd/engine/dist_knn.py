@@ -1,0 +1,288 @@
+"""Global top-k over the vector-store shards of all data-parallel replicas (SURVEY
+§2.10 C-DP).
+
+With one process per GPU every replica of the ingest pipeline writes the chunks it
+consumed into ITS OWN HBM store, so each store holds a shard of the corpus.  A
+``query-vector-db`` lookup must still see the whole corpus, as it does against the
+reference's shared database (VEC/QueryVectorDBAgent.java:27-93 over one datasource).
+
+``ShardedKnn`` runs a background thread on every rank that executes lock-step search
+rounds (every rank takes part in every round, so collectives always match):
+
+1. all-gather of a small JSON header (gloo, CPU): each rank's pending requests
+   ``(collection, n_queries, k, include_vector, dim)`` and its stop flag; an empty round
+   sleeps ``tick`` and repeats;
+2. per collection: all-gather of the query vectors ``[W*Qmax, d]`` over the data group
+   (RCCL over xGMI on the GPU), the fused MFMA kNN kernel of the LOCAL shard on every
+   rank for all ``W*Qmax`` queries, then one all-to-all of ``(score, row)`` candidates
+   ``[W, Qmax, k]`` back to the ranks that asked;
+3. merge on the device: top-k of the ``W*k`` candidates per query -> ``(owner, row)``;
+4. two-phase payload fetch over gloo: each rank asks every owner only for the rows in
+   its merged top-k (``k/W`` per query on average) and the owners answer with the
+   metadata (and vectors when ``include-vector``) -- bandwidth-optimal for the text
+   payloads that stay on the host.
+
+Store locks are held on each rank from its local search to its payload answer, so row
+indices cannot be moved by a concurrent delete in between.
+"""
+from __future__ import annotations
+
+import json
+import logging
+import threading
+import time
+from concurrent.futures import Future
+from typing import Any, Dict, List, Optional
+
+import msgpack
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from ..utils.gpu import on_aux, to_host
+from .vector_store import VectorStoreRegistry
+
+log = logging.getLogger(__name__)
+
+_service: Optional["ShardedKnn"] = None
+
+
+def active() -> Optional["ShardedKnn"]:
+    return _service
+
+
+def start(device=None, tick_s: float = 0.001) -> "ShardedKnn":
+    """Start the process-wide service (collective: every rank of the default group)."""
+    global _service
+    if _service is None:
+        _service = ShardedKnn(device=device, tick_s=tick_s)
+    return _service
+
+
+def stop() -> None:
+    global _service
+    s, _service = _service, None
+    if s is not None:
+        s.close()
+
+
+class _Req:
+    __slots__ = ("coll", "q", "k", "inc", "fut")
+
+    def __init__(self, coll, q, k, inc):
+        self.coll, self.q, self.k, self.inc = coll, q, k, inc
+        self.fut: Future = Future()
+
+
+class ShardedKnn:
+    def __init__(self, device=None, tick_s: float = 0.001, max_queries_per_round: int = 4096):
+        if not dist.is_initialized():
+            raise RuntimeError("ShardedKnn needs an initialised default process group")
+        self.rank, self.world = dist.get_rank(), dist.get_world_size()
+        backend = dist.get_backend()
+        self.device = torch.device(device or ("cuda" if backend == "nccl" else "cpu"))
+        # separate groups so the service never interleaves with the caller's collectives
+        self.meta = dist.new_group(backend="gloo")
+        self.data = dist.new_group(backend=backend) if backend == "nccl" else dist.new_group(backend="gloo")
+        self.data_dev = self.device if backend == "nccl" else torch.device("cpu")
+        self.tick_s = tick_s
+        self.max_q = max_queries_per_round
+        self._pending: List[_Req] = []
+        self._cv = threading.Condition()
+        self._stop = False
+        self.rounds = 0
+        self._thread = threading.Thread(target=self._loop, name="sharded-knn", daemon=True)
+        self._thread.start()
+
+    # ------------------------------------------------------------------ client API
+    def search(self, collection: str, queries, k: int, with_vectors: bool = False) -> Future:
+        """Global top-k for the rows of ``queries`` ([Q, d]) -> Future[List[List[dict]]]
+        in the local store's result format (id, similarity, metadata[, vector])."""
+        q = torch.as_tensor(queries, dtype=torch.float32)
+        if q.dim() == 1:
+            q = q[None]
+        q = torch.nn.functional.normalize(q, dim=-1, eps=1e-12)
+        r = _Req(collection, q, int(k), bool(with_vectors))
+        if r.k < 1:
+            r.fut.set_exception(ValueError("top-k must be >= 1"))
+            return r.fut
+        with self._cv:
+            if self._stop:
+                r.fut.set_exception(RuntimeError("sharded kNN service stopped"))
+                return r.fut
+            self._pending.append(r)
+            self._cv.notify()
+        return r.fut
+
+    def close(self, timeout: float = 30.0) -> None:
+        with self._cv:
+            self._stop = True
+            self._cv.notify()
+        self._thread.join(timeout)
+
+    # ------------------------------------------------------------------ collectives
+    def _allgather_bytes(self, b: bytes) -> List[bytes]:
+        n = torch.tensor([len(b)], dtype=torch.int64)
+        ns = torch.empty(self.world, dtype=torch.int64)
+        dist.all_gather_into_tensor(ns, n, group=self.meta)
+        m = int(ns.max())
+        buf = torch.zeros(m, dtype=torch.uint8)
+        if b:
+            buf[: len(b)] = torch.frombuffer(bytearray(b), dtype=torch.uint8)
+        out = torch.empty(self.world * m, dtype=torch.uint8)
+        dist.all_gather_into_tensor(out, buf, group=self.meta)
+        o = out.numpy()
+        return [o[i * m: i * m + int(ns[i])].tobytes() for i in range(self.world)]
+
+    def _alltoall_bytes(self, per_dest: List[bytes]) -> List[bytes]:
+        send_n = torch.tensor([len(b) for b in per_dest], dtype=torch.int64)
+        recv_n = torch.empty(self.world, dtype=torch.int64)
+        dist.all_to_all_single(recv_n, send_n, group=self.meta)
+        flat = b"".join(per_dest)
+        send = torch.frombuffer(bytearray(flat), dtype=torch.uint8) if flat else torch.zeros(0, dtype=torch.uint8)
+        recv = torch.empty(int(recv_n.sum()), dtype=torch.uint8)
+        dist.all_to_all_single(recv, send, recv_n.tolist(), send_n.tolist(), group=self.meta)
+        o, out, p = recv.numpy(), [], 0
+        for n in recv_n.tolist():
+            out.append(o[p: p + n].tobytes())
+            p += n
+        return out
+
+    # ------------------------------------------------------------------ service loop
+    def _loop(self) -> None:
+        if self.device.type == "cuda":
+            torch.cuda.set_device(self.device)
+        try:
+            while True:
+                with self._cv:
+                    take, n = [], 0
+                    while self._pending and (not take or n + self._pending[0].q.shape[0] <= self.max_q):
+                        r = self._pending.pop(0)
+                        take.append(r)
+                        n += r.q.shape[0]
+                    stopping = self._stop and not take and not self._pending
+                hdr = {"s": stopping, "r": [[r.coll, int(r.q.shape[0]), r.k, r.inc, int(r.q.shape[1])] for r in take]}
+                hdrs = [json.loads(b) for b in self._allgather_bytes(json.dumps(hdr).encode())]
+                if all(h["s"] for h in hdrs):
+                    return
+                if not any(h["r"] for h in hdrs):
+                    with self._cv:
+                        if not self._pending:
+                            self._cv.wait(self.tick_s)
+                    continue
+                self.rounds += 1
+                try:
+                    self._round(take, hdrs)
+                except Exception as e:  # noqa: BLE001  (a local failure after the collectives)
+                    log.exception("sharded kNN round failed")
+                    for r in take:
+                        if not r.fut.done():
+                            r.fut.set_exception(e)
+        except Exception as e:  # noqa: BLE001  (a collective failed: the service is dead)
+            log.exception("sharded kNN service stopped")
+            with self._cv:
+                self._stop = True
+                pend, self._pending = self._pending, []
+            for r in pend:
+                r.fut.set_exception(e)
+
+    def _round(self, take: List[_Req], hdrs: List[Dict[str, Any]]) -> None:
+        W, me = self.world, self.rank
+        colls = sorted({r[0] for h in hdrs for r in h["r"]})
+        stores = {c: VectorStoreRegistry.get(c) for c in colls if VectorStoreRegistry.exists(c)}
+        locks = [stores[c].lock for c in sorted(stores)]
+        for lk in locks:
+            lk.acquire()
+        try:
+            hits: Dict[int, List[List[tuple]]] = {}   # id(req) -> per query [(score, owner, row)]
+            need: List[Dict[str, set]] = [dict() for _ in range(W)]
+            vec_colls = set()
+            for coll in colls:
+                reqs_all = [(h_i, r) for h_i, h in enumerate(hdrs) for r in h["r"] if r[0] == coll]
+                dims = {r[4] for _, r in reqs_all}
+                mine = [r for r in take if r.coll == coll]
+                if len(dims) != 1:   # every rank sees the same headers -> all skip consistently
+                    for r in mine:
+                        r.fut.set_exception(ValueError(f"collection {coll}: queries of different dims {dims}"))
+                    continue
+                dim = dims.pop()
+                counts = [sum(r[1] for hi, r in reqs_all if hi == i) for i in range(W)]
+                kmax = max(r[2] for _, r in reqs_all)
+                if any(r[3] for _, r in reqs_all):
+                    vec_colls.add(coll)
+                qmax = max(counts)
+                qloc = torch.zeros(qmax, dim, dtype=torch.float32)
+                if mine:
+                    qloc[: counts[me]] = torch.cat([r.q for r in mine])
+                qloc = qloc.to(self.data_dev)
+                qall = torch.empty(W * qmax, dim, dtype=torch.float32, device=self.data_dev)
+                dist.all_gather_into_tensor(qall, qloc, group=self.data)
+                store = stores.get(coll)
+                if store is not None and store.dim == dim and len(store):
+                    with on_aux(store.device):
+                        s, idx = store.topk_rows(qall.to(store.device, store.dtype), kmax)
+                        s, idx = s.to(self.data_dev), idx.to(self.data_dev)
+                else:
+                    s = torch.full((W * qmax, kmax), float("-inf"), device=self.data_dev)
+                    idx = torch.full((W * qmax, kmax), -1, dtype=torch.int32, device=self.data_dev)
+                send = torch.stack([s.float(), idx.int().view(torch.float32)], -1).contiguous()  # [W*qmax,k,2]
+                recv = torch.empty_like(send)
+                dist.all_to_all_single(recv, send, group=self.data)
+                n_me = counts[me]
+                if n_me == 0:
+                    continue
+                recv = recv.view(W, qmax, kmax, 2)[:, :n_me]                 # [W, n_me, k, 2]
+                cs = recv[..., 0].permute(1, 0, 2).reshape(n_me, W * kmax)
+                ci = recv[..., 1].contiguous().view(torch.int32).permute(1, 0, 2).reshape(n_me, W * kmax)
+                top_s, sel = torch.topk(cs, kmax, dim=-1)
+                rows = torch.gather(ci, 1, sel)
+                owners = sel // kmax
+                top_s, rows, owners = (t.tolist() for t in to_host(top_s, rows, owners.int()))
+                qi = 0
+                for r in mine:
+                    per_q = []
+                    for j in range(qi, qi + r.q.shape[0]):
+                        lst = [(sc, o, rw) for sc, o, rw in zip(top_s[j][: r.k], owners[j][: r.k], rows[j][: r.k])
+                               if rw >= 0 and sc != float("-inf")]
+                        for _, o, rw in lst:
+                            need[o].setdefault(coll, set()).add(rw)
+                        per_q.append(lst)
+                    hits[id(r)] = per_q
+                    qi += r.q.shape[0]
+            # phase 2: payloads of the merged top-k rows, asked from their owners
+            asks = [msgpack.packb({c: sorted(v) for c, v in need[d].items()}) for d in range(W)]
+            got_asks = [msgpack.unpackb(b, strict_map_key=False) if b else {} for b in self._alltoall_bytes(asks)]
+            answers = []
+            for src in range(W):
+                ans = {}
+                for coll, rws in got_asks[src].items():
+                    st = stores.get(coll)
+                    if st is None:
+                        continue
+                    vecs = st.row_vectors(rws) if coll in vec_colls else {}
+                    ans[coll] = {rw: (st.row_payload(rw),
+                                      np.asarray(vecs[rw], np.float32).tobytes() if rw in vecs else None)
+                                 for rw in rws if 0 <= rw < len(st)}
+                answers.append(msgpack.packb(ans, use_bin_type=True))
+        finally:
+            for lk in reversed(locks):
+                lk.release()
+        payload = [msgpack.unpackb(b, raw=False, strict_map_key=False) if b else {}
+                   for b in self._alltoall_bytes(answers)]
+        for r in take:
+            if r.fut.done():
+                continue
+            out = []
+            for lst in hits.get(id(r), [[] for _ in range(r.q.shape[0])]):
+                res = []
+                for sc, o, rw in lst:
+                    p = payload[o].get(r.coll, {}).get(rw)
+                    if p is None:
+                        continue
+                    d = dict(p[0])
+                    d["similarity"] = sc
+                    if r.inc and p[1] is not None:
+                        d["vector"] = np.frombuffer(p[1], np.float32).tolist()
+                    res.append(d)
+                out.append(res)
+            r.fut.set_result(out)

@@ -236,6 +236,8 @@ void knn_topk(at::Tensor X, at::Tensor Q, int64_t K, at::Tensor out_s, at::Tenso
     case 512: LAUNCH(512); break;
     case 768: LAUNCH(768); break;
     case 1024: LAUNCH(1024); break;
+    case 1536: LAUNCH(1536); break;
+    case 2048: LAUNCH(2048); break;
     default: TORCH_CHECK(false, "unsupported embedding dim ", dim);
   }
 #undef LAUNCH

@@ -1,0 +1,28 @@
+"""bench.py contract on CPU (gloo): ``--gpus 2`` self-launches two rank processes whose
+agent replicas share the topics through the shared-memory log as ONE consumer group
+(disjoint partitions), with the crawl stage and the sharded kNN in the loop."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_bench_two_ranks_consumer_group_dp(tmp_path):
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1", "--warmup", "1",
+                        "--batch", "4", "--max-tokens", "4", "--corpus", "1000", "--docs", "2"],
+                       cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("{") and '"metric"' in ln]
+    assert len(line) == 1, r.stdout[-2000:]
+    d = json.loads(line[0])
+    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp2" and d["value"] > 0
+    assert d["latency_samples"] == 2 * 4
+    a, b = d["partitions_per_rank"]
+    for topic in ("questions-topic", "documents-topic"):
+        assert a[topic] and b[topic] and not set(a[topic]) & set(b[topic])
+    assert all(n > 0 for n in d["knn_rounds_per_rank"])   # queries went through the sharded kNN
+    assert d["config"]["crawl"] and d["ingest"]["chunks_per_s"] > 0

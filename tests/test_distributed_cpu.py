@@ -155,3 +155,62 @@ def _tp_pod_worker(rank, world, port, q):
 def test_tp_pod_serves_chat_agent():
     ntok, has_text, last = _spawn(_tp_pod_worker)
     assert ntok == 7 and has_text and last
+
+
+def _knn_corpus():
+    g = torch.Generator().manual_seed(11)
+    vecs = torch.randn(600, 48, generator=g)
+    queries = torch.randn(10, 48, generator=g)
+    return vecs, queries
+
+
+def _sharded_knn_worker(rank, world, port, q):
+    """Each rank holds a disjoint shard (rows i % world == rank) of one collection and
+    asks a different subset of the queries; the service returns global top-k."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from langstream_amd.engine import dist_knn
+        from langstream_amd.engine.vector_store import VectorStoreRegistry
+        vecs, queries = _knn_corpus()
+        rows = [i for i in range(vecs.shape[0]) if i % world == rank]
+        VectorStoreRegistry.get("docs", 48, device="cpu").upsert(
+            [f"d{i}" for i in rows], vecs[rows].tolist(), [{"text": f"t{i}", "owner": rank} for i in rows])
+        svc = dist_knn.start(device="cpu")
+        mine = list(range(rank, queries.shape[0], world))
+        # several concurrent requests of different k -> one round may carry them all
+        futs = [svc.search("docs", queries[i:i + 1].tolist(), 7 + (i % 3), with_vectors=(i % 2 == 0)) for i in mine]
+        res = {i: f.result(60)[0] for i, f in zip(mine, futs)}
+        # a query for a collection nobody has
+        assert svc.search("nope", queries[:1].tolist(), 3).result(60) == [[]]
+        gathered = [None] * world
+        dist.all_gather_object(gathered, res)
+        dist_knn.stop()
+        if rank == 0:
+            allres = {}
+            for g in gathered:
+                allres.update(g)
+            q.put(allres)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_knn_equals_single_store():
+    from langstream_amd.engine.vector_store import VectorStore
+    out = _spawn(_sharded_knn_worker)
+    vecs, queries = _knn_corpus()
+    single = VectorStore(48, device="cpu")          # same bf16 rows as the shards
+    single.upsert([f"d{i}" for i in range(vecs.shape[0])], vecs.tolist())
+    for i in range(queries.shape[0]):
+        k = 7 + (i % 3)
+        want = single.search(queries[i:i + 1].tolist(), k, with_vectors=True)[0]
+        got = out[i]
+        assert len(got) == len(want) == k
+        assert all(abs(a["similarity"] - b["similarity"]) < 1e-4 for a, b in zip(got, want))
+        # identical ranking except within exact score ties
+        for a, b in zip(got, want):
+            assert a["id"] == b["id"] or abs(a["similarity"] - b["similarity"]) < 1e-6
+        assert all(d["text"] == "t" + d["id"][1:] for d in got)
+        assert {d["owner"] for d in got} == {0, 1} or len(got) < 2
+        if i % 2 == 0:
+            assert all(len(d["vector"]) == 48 for d in got)
