@@ -80,7 +80,12 @@ class AdminClient:
             files["app"] = ("app.zip", data, "application/zip")
         for name, p in (("instance", instance), ("secrets", secrets)):
             if p:
-                files[name] = (name + ".yaml", open(p).read() if os.path.exists(p) else p, "text/yaml")
+                if os.path.exists(p):   # ${ENV:-default} / <file:...> (LocalFileReferenceResolver.java)
+                    from ..core.file_refs import read_yaml_with_references
+                    content = read_yaml_with_references(p)
+                else:
+                    content = p
+                files[name] = (name + ".yaml", content, "text/yaml")
         return files
 
     def deploy(self, app_id: str, app: Optional[str], instance: Optional[str] = None, secrets: Optional[str] = None,

@@ -257,8 +257,9 @@ def cmd_run(args) -> int:
     store = InMemoryApplicationStore()
     cp = ControlPlane(store)
     store.put_tenant(args.tenant)
-    instance = open(args.instance).read() if args.instance else None
-    secrets = open(args.secrets).read() if args.secrets else None
+    from ..core.file_refs import read_yaml_with_references
+    instance = read_yaml_with_references(args.instance) if args.instance else None
+    secrets = read_yaml_with_references(args.secrets) if args.secrets else None
     res = cp.deploy(args.tenant, args.name, zip_directory(args.app), instance, secrets, dry_run=args.dry_run)
     if args.dry_run:
         _print(res, "yaml")

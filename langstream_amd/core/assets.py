@@ -19,9 +19,9 @@ ASSET_REQUIRED = {
     "astra-keyspace": ("keyspace", "datasource"),
     "jdbc-table": ("table-name", "datasource", "create-statements"),
     "milvus-collection": ("collection-name", "datasource", "create-statements"),
-    "opensearch-index": ("index-name", "datasource"),
-    "solr-collection": ("collection-name", "datasource"),
-    "astra-collection": ("collection-name", "datasource"),
+    "opensearch-index": ("datasource",),            # index-name comes from the datasource
+    "solr-collection": ("datasource", "create-statements"),
+    "astra-collection": ("collection-name", "datasource", "vector-dimension"),
     "vector-collection": ("collection-name", "datasource"),
 }
 

@@ -275,8 +275,11 @@ def read_app_directory(path: str) -> Dict[str, str]:
 
 def build_from_directory(app_dir: str, instance_file: Optional[str] = None,
                          secrets_file: Optional[str] = None) -> ApplicationWithPackageInfo:
-    inst = open(instance_file, encoding="utf-8").read() if instance_file else None
-    sec = open(secrets_file, encoding="utf-8").read() if secrets_file else None
+    # instance / secrets files get ${ENV:-default} and <file:...> resolution, as the
+    # reference CLI does for them (LocalFileReferenceResolver.java:37-160)
+    from .file_refs import read_yaml_with_references
+    inst = read_yaml_with_references(instance_file) if instance_file else None
+    sec = read_yaml_with_references(secrets_file) if secrets_file else None
     info = build_application_instance(read_app_directory(app_dir), inst, sec)
     info.py_binaries_digest = directory_digest(os.path.join(app_dir, "python"))
     info.java_binaries_digest = directory_digest(os.path.join(app_dir, "java", "lib"))

@@ -35,7 +35,7 @@ def validate_resource(r: Resource) -> None:
         for k in AI_RESOURCE_TYPES[r.type]:
             if r.type == "open-ai-configuration" and cfg.get("provider", "openai") == "local":
                 continue
-            if cfg.get(k) in (None, ""):
+            if cfg.get(k) is None:   # required = present (ClassConfigValidator.java:300-304)
                 raise ValueError(f"Resource {r.id} ({r.type}): missing required property '{k}'")
     else:
         svc = cfg.get("service")

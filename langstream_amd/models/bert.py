@@ -6,13 +6,22 @@ time -- comment at :192-193) and for the remote embedding services (SURVEY §2.1
 
 Padding-free: a batch is packed into one [T, H] token matrix with per-sequence
 start/len; attention is the varlen MFMA encoder kernel, so no FLOPs are spent on pad
-tokens.  Per layer: QKV GEMM (+bias, hipBLASLt) -> varlen attention (HIP) -> O GEMM ->
-fused bias+residual+LayerNorm (HIP) -> FFN1 GEMM -> fused bias+GELU (HIP) -> FFN2 GEMM
--> fused bias+residual+LayerNorm (HIP); then CLS/mean pooling + L2 normalise (HIP).
+tokens.
+
+Fused path (default; ops/csrc/gemm_fused.hip): per layer FOUR hand-written MFMA GEMMs +
+the attention kernel and nothing else -- every bias, the erf-GELU, both residual adds
+and both LayerNorms live in GEMM epilogues.  A GEMM that feeds a LayerNorm stores the
+un-normalised row and per-row partial statistics; the next GEMM applies the LayerNorm
+algebraically (input side: LN(x).W^T = r (x.W'^T) - r mu c1 + c2 with W' = W*gamma,
+c1 = rowsum(W'), c2 = W.beta precomputed here; residual side: elementwise).  Only the
+last layer's LayerNorm runs as a kernel, before CLS/mean pooling + L2 normalise.
+Unfused path (LS_BERT_FUSED=0 or unsupported widths): library GEMMs + the bias/GELU and
+bias+residual+LayerNorm kernels.
 """
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 from typing import List, Optional
 
@@ -101,6 +110,63 @@ class BertEncoder:
             for n in BertLayer.NAMES:
                 getattr(l, n).copy_(sd[f"layers.{i}.{n}"])
 
+    # ------------------------------------------------------------------ fused layout
+    def fused_supported(self) -> bool:
+        c = self.cfg
+        return (os.environ.get("LS_BERT_FUSED", "1") != "0" and c.hidden_size % 128 == 0
+                and c.intermediate_size % 128 == 0)
+
+    def fused_params(self):
+        """Per layer: (qkv W' or W, c1, c2), (ff1 W', c1, c2) -- the LayerNorm of the
+        previous sub-block folded into the weights (cached)."""
+        if getattr(self, "_fused", None) is None:
+            out = []
+            prev_g = prev_b = None
+            for l in self.layers:
+                if prev_g is None:
+                    qkv = (l.qkv_w, None, None)
+                else:
+                    qkv = self._fold(l.qkv_w, prev_g, prev_b)
+                out.append((qkv, self._fold(l.ff1_w, l.ln1_g, l.ln1_b)))
+                prev_g, prev_b = l.ln2_g, l.ln2_b
+            self._fused = out
+        return self._fused
+
+    @staticmethod
+    def _fold(w, g, b):
+        wp = (w.float() * g.float()[None]).to(w.dtype)
+        return wp, wp.float().sum(1).contiguous(), (w.float() @ b.float()).contiguous()
+
+    def forward_fused(self, ids, pos, starts, lens, tiles, out_dtype=torch.float32):
+        """The fused layer sequence through ops.gemm_fused (GPU kernels or fp32 reference)."""
+        cfg = self.cfg
+        H, nh, eps = cfg.hidden_size, cfg.num_heads, cfg.ln_eps
+        T = ids.shape[0]
+        x = ops.embed_layernorm(ids, pos, None, self.wte, self.wpe, self.wtt, self.emb_g, self.emb_b, eps)
+        xp2 = st2 = None
+        prev_g = prev_b = None
+        for l, ((wq, qc1, qc2), (w1, fc1, fc2)) in zip(self.layers, self.fused_params()):
+            if xp2 is None:
+                qkv = ops.gemm_fused(x, wq, bias=l.qkv_b)
+            else:
+                qkv = ops.gemm_fused(xp2, wq, bias=l.qkv_b, ln_stats_in=st2, ln_width=H, c1=qc1, c2=qc2, eps=eps)
+            a = ops.varlen_encoder_attention(qkv, starts, lens, tiles, nh, nh, self.scale)
+            st1 = torch.empty(T, H // 64, 2, dtype=torch.float32, device=x.device)
+            if xp2 is None:
+                xp1 = ops.gemm_fused(a, l.o_w, bias=l.o_b, residual=x, stats_out=st1)
+            else:
+                xp1 = ops.gemm_fused(a, l.o_w, bias=l.o_b, residual=xp2, ln_stats_in=st2, ln_width=H,
+                                     res_g=prev_g, res_b=prev_b, eps=eps, stats_out=st1)
+            h = ops.gemm_fused(xp1, w1, bias=l.ff1_b, gelu=True, ln_stats_in=st1, ln_width=H, c1=fc1, c2=fc2,
+                               eps=eps)
+            st2 = torch.empty(T, H // 64, 2, dtype=torch.float32, device=x.device)
+            xp2 = ops.gemm_fused(h, l.ff2_w, bias=l.ff2_b, residual=xp1, ln_stats_in=st1, ln_width=H,
+                                 res_g=l.ln1_g, res_b=l.ln1_b, eps=eps, stats_out=st2)
+            prev_g, prev_b = l.ln2_g, l.ln2_b
+        x = ops.layernorm(xp2, prev_g, prev_b, eps)
+        mode = 0 if cfg.pooling == "cls" else 1
+        return ops.pool_embeddings(x, starts, lens, mode, cfg.normalize, out_dtype=out_dtype)
+
     @torch.inference_mode()
     def forward_packed(self, ids: torch.Tensor, pos: torch.Tensor, starts: torch.Tensor, lens: torch.Tensor,
                        tiles: torch.Tensor, out_dtype=torch.float32) -> torch.Tensor:
@@ -111,11 +177,18 @@ class BertEncoder:
         if self.device.type == "cuda" and ops.hip_available() and out_dtype in (torch.float32, self.dtype):
             # native executor (ops/csrc/runner.hip): whole encoder with the GIL released
             if getattr(self, "_runner", None) is None:
+                fused = []
+                if self.fused_supported():   # 6 extra tensors per layer select the fused path
+                    for (wq, qc1, qc2), (w1, fc1, fc2) in self.fused_params():
+                        z = torch.zeros(0, device=self.device)
+                        fused.append([wq, qc1 if qc1 is not None else z, qc2 if qc2 is not None else z, w1, fc1, fc2])
                 self._runner = ops.hip().BertRunner(
                     self.wte, self.wpe, self.wtt, self.emb_g, self.emb_b,
                     [[getattr(l, n) for n in BertLayer.NAMES] for l in self.layers], nh, cfg.ln_eps, self.scale,
-                    mode, cfg.normalize)
+                    mode, cfg.normalize, fused)
             return self._runner.forward(ids, pos, starts, lens, tiles, out_dtype == torch.float32)
+        if self.fused_supported():
+            return self.forward_fused(ids, pos, starts, lens, tiles, out_dtype)
         x = ops.embed_layernorm(ids, pos, None, self.wte, self.wpe, self.wtt, self.emb_g, self.emb_b, cfg.ln_eps)
         for l in self.layers:
             qkv = F.linear(x, l.qkv_w, l.qkv_b)

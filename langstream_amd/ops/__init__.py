@@ -133,6 +133,39 @@ def embed_layernorm(ids, pos_ids, type_ids, wte, wpe, wtt, g, b, eps):
     return ref.embed_layernorm(ids, pos_ids, type_ids, wte, wpe, wtt, g, b, eps)
 
 
+# ---------------------------------------------------------------- GEMM with fused epilogues
+def gemm_fused(x, w, bias=None, gelu=False, residual=None, ln_stats_in=None, ln_width=0, c1=None, c2=None,
+               res_g=None, res_b=None, eps=1e-12, stats_out=None, out=None):
+    """out = epilogue(x . w^T) on MFMA (ops/csrc/gemm_fused.hip): bias, erf-GELU, residual,
+    and LayerNorm folded in from the neighbours (``ln_stats_in`` partial row statistics of
+    the LayerNorm input + ``c1``/``c2`` for an un-normalised input, or + ``res_g``/``res_b``
+    to normalise the residual); ``stats_out`` [M, N/64, 2] receives the output rows'
+    partial (sum, sumsq)."""
+    if _gpu(x):
+        out = torch.empty(x.shape[0], w.shape[0], dtype=x.dtype, device=x.device) if out is None else out
+        hip().gemm_fused(out, x, w, bias, gelu, residual, ln_stats_in, ln_width, c1, c2, res_g, res_b, eps,
+                         stats_out)
+        return out
+    r = ref.gemm_fused(x, w, bias, gelu, residual, ln_stats_in, ln_width, c1, c2, res_g, res_b, eps, stats_out)
+    if out is not None:
+        out.copy_(r)
+        return out
+    return r
+
+
+def gemm(x, w, bias=None, act=None, residual=None):
+    """Hand-written MFMA linear: act in (None, "gelu", "swiglu"); swiglu takes the fused
+    gate_up weight [2F, K] and returns silu(x.g^T) * (x.u^T)."""
+    if act == "swiglu":
+        F = w.shape[0] // 2
+        if _gpu(x):
+            out = torch.empty(x.shape[0], F, dtype=x.dtype, device=x.device)
+            hip().skinny_gemm_silu(out, x, w)
+            return out
+        return ref.silu_and_mul(x.float() @ w.float().t()).to(x.dtype)
+    return gemm_fused(x, w, bias=bias, gelu=act == "gelu", residual=residual)
+
+
 # ---------------------------------------------------------------- activations
 def silu_and_mul(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     if _gpu(x):

@@ -41,6 +41,10 @@ void gemv_qkv(at::Tensor out, at::Tensor x, at::Tensor w, at::Tensor pos, at::Te
               c10::optional<at::Tensor> o, c10::optional<at::Tensor> res, c10::optional<at::Tensor> res_out,
               c10::optional<at::Tensor> norm_w, double eps);
 void skinny_gemm_silu(at::Tensor out, at::Tensor x, at::Tensor w);
+void gemm_fused(at::Tensor out, at::Tensor x, at::Tensor w, c10::optional<at::Tensor> bias, bool gelu,
+                c10::optional<at::Tensor> residual, c10::optional<at::Tensor> ln_stats_in, int64_t ln_width,
+                c10::optional<at::Tensor> c1, c10::optional<at::Tensor> c2, c10::optional<at::Tensor> res_g,
+                c10::optional<at::Tensor> res_b, double eps, c10::optional<at::Tensor> stats_out);
 void skinny_gemm_add_rmsnorm(at::Tensor out, at::Tensor x, at::Tensor w, at::Tensor residual, at::Tensor norm_w,
                              double eps);
 void bind_runners(pybind11::module_& m);
@@ -70,6 +74,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemv_silu_norm", &gemv_silu_norm);
   m.def("gemv_qkv", &gemv_qkv);
   m.def("skinny_gemm_silu", &skinny_gemm_silu);
+  m.def("gemm_fused", &gemm_fused, py::arg("out"), py::arg("x"), py::arg("w"), py::arg("bias") = py::none(),
+        py::arg("gelu") = false, py::arg("residual") = py::none(), py::arg("ln_stats_in") = py::none(),
+        py::arg("ln_width") = 0, py::arg("c1") = py::none(), py::arg("c2") = py::none(),
+        py::arg("res_g") = py::none(), py::arg("res_b") = py::none(), py::arg("eps") = 1e-12,
+        py::arg("stats_out") = py::none());
   m.def("skinny_gemm_add_rmsnorm", &skinny_gemm_add_rmsnorm);
   bind_runners(m);
 }

@@ -79,3 +79,30 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
   const int q = nwg / 8, r = nwg % 8, xcd = orig % 8;
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
 }
+
+// ---------------------------------------------------------------------------------
+// LDS-DMA helpers shared by the glds-ring GEMMs (gemm_skinny.hip, gemm_fused.hip).
+// 64-B LDS rows of 32 bf16; chunk p of row r holds global k-chunk p ^ swz_g((r >> 2) & 3)
+// so the 16 lanes of each ds_read_b128 bank group hit 16 distinct 16-B slots.
+static __device__ __forceinline__ int swz_g(int q) { return (0x78 >> (2 * q)) & 3; }
+
+// LDS-DMA through inline asm (cdna_hip_programming.md §5.7): with the builtin, hipcc sees
+// an LDS write and puts `s_waitcnt vmcnt(0)` in front of the next ds_read, which drains
+// the whole ring every K-step; the asm form is invisible to its wait insertion, and the
+// kernel counts these loads itself (wait_vmcnt).
+static __device__ __forceinline__ void glds16(const bf16* src, char* lds_wave_base) {
+  const unsigned dst = __builtin_amdgcn_readfirstlane(
+      (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)lds_wave_base);
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(src), "s"(dst)
+      : "memory");
+}
+
+template <int N>
+static __device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+

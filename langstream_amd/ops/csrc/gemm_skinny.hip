@@ -268,28 +268,6 @@ __global__ void __launch_bounds__(256) splitk_add_rmsnorm_kernel(const float* __
 //     so the wait count stays a compile-time constant.
 constexpr int GBK = 32;
 
-__device__ __forceinline__ int swz_g(int q) { return (0x78 >> (2 * q)) & 3; }
-
-// LDS-DMA through inline asm (cdna_hip_programming.md §5.7): with the builtin, hipcc sees
-// an LDS write and puts `s_waitcnt vmcnt(0)` in front of the next ds_read, which drains
-// the whole ring every K-step; the asm form is invisible to its wait insertion, and the
-// kernel counts these loads itself (wait_vmcnt).
-__device__ __forceinline__ void glds16(const bf16* src, char* lds_wave_base) {
-  const unsigned dst = __builtin_amdgcn_readfirstlane(
-      (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)lds_wave_base);
-  unsigned keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(src), "s"(dst)
-      : "memory");
-}
-
-template <int N>
-__device__ __forceinline__ void wait_vmcnt() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
 template <int BM, int S, int EPI>
 __global__ void __launch_bounds__(BM * 2) skinny_glds_kernel(const bf16* __restrict__ x, int64_t ldx,
                                                              const bf16* __restrict__ w, int M, int N, int K,
@@ -439,7 +417,7 @@ void check_operands(const at::Tensor& x, const at::Tensor& w, int64_t K) {
   TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && x.stride(0) % 8 == 0, "x must be [M, K] with unit column stride");
   TORCH_CHECK(w.dim() == 2 && w.is_contiguous() && w.size(1) == K, "w must be contiguous [N, K]");
   TORCH_CHECK(K % BK == 0, "K must be a multiple of 64");
-  TORCH_CHECK(x.size(0) <= 4096, "skinny GEMM is for decode-sized M");
+  TORCH_CHECK(x.size(0) <= 65536, "skinny GEMM: M too large");
 }
 
 }  // namespace

@@ -62,6 +62,10 @@ void sample_tokens(at::Tensor logits, at::Tensor temperature, at::Tensor top_k, 
                    int64_t n_top);
 
 void skinny_gemm(at::Tensor out, at::Tensor x, at::Tensor w);
+void gemm_fused(at::Tensor out, at::Tensor x, at::Tensor w, c10::optional<at::Tensor> bias, bool gelu,
+                c10::optional<at::Tensor> residual, c10::optional<at::Tensor> ln_stats_in, int64_t ln_width,
+                c10::optional<at::Tensor> c1, c10::optional<at::Tensor> c2, c10::optional<at::Tensor> res_g,
+                c10::optional<at::Tensor> res_b, double eps, c10::optional<at::Tensor> stats_out);
 void gemv(at::Tensor out, at::Tensor x, at::Tensor w);
 void gemv_silu(at::Tensor out, at::Tensor x, at::Tensor w);
 bool gemv_supported(const at::Tensor& w, bool silu);
@@ -334,12 +338,16 @@ class LlamaRunner {
 // ---------------------------------------------------------------------------- BERT
 class BertRunner {
  public:
+  // fused: empty, or per layer {qkv W' (W for layer 0), qkv c1, qkv c2, ff1 W', ff1 c1, ff1 c2}
+  // -> the fused layer sequence of models/bert.py forward_fused (gemm_fused.hip epilogues).
   BertRunner(at::Tensor wte, at::Tensor wpe, at::Tensor wtt, at::Tensor emb_g, at::Tensor emb_b,
              std::vector<std::vector<at::Tensor>> layers, int64_t heads, double eps, double scale, int64_t pooling,
-             bool normalize)
+             bool normalize, std::vector<std::vector<at::Tensor>> fused)
       : wte_(wte), wpe_(wpe), wtt_(wtt), emb_g_(emb_g), emb_b_(emb_b), layers_(layers), heads_(heads), eps_(eps),
-        scale_(scale), pooling_(pooling), normalize_(normalize) {
+        scale_(scale), pooling_(pooling), normalize_(normalize), fused_(fused) {
     for (auto& l : layers_) TORCH_CHECK(l.size() == 12, "bert layer needs 12 tensors");
+    TORCH_CHECK(fused_.empty() || fused_.size() == layers_.size(), "fused params: one entry per layer");
+    for (auto& f : fused_) TORCH_CHECK(f.size() == 6, "fused layer needs 6 tensors");
   }
 
   at::Tensor forward(at::Tensor ids, at::Tensor pos, at::Tensor starts, at::Tensor lens, at::Tensor tiles,
@@ -347,20 +355,24 @@ class BertRunner {
     const int64_t T = ids.size(0), H = wte_.size(1);
     at::Tensor x = at::empty({T, H}, wte_.options());
     embed_layernorm(x, ids, pos, c10::nullopt, wte_, wpe_, wtt_, emb_g_, emb_b_, eps_);
-    for (auto& l : layers_) {
-      // qkv_w, qkv_b, o_w, o_b, ln1_g, ln1_b, ff1_w, ff1_b, ff2_w, ff2_b, ln2_g, ln2_b
-      at::Tensor qkv = at::linear(x, l[0], l[1]);
-      at::Tensor a = at::empty({T, H}, x.options());
-      varlen_encoder_attention(a, qkv, starts, lens, tiles, heads_, heads_, scale_);
-      at::Tensor o = at::linear(a, l[2]);
-      at::Tensor x1 = at::empty_like(x);
-      layernorm(x1, o, l[3], x, l[4], l[5], eps_);
-      at::Tensor hdn = at::linear(x1, l[6]);
-      bias_gelu(hdn, l[7]);
-      at::Tensor o2 = at::linear(hdn, l[8]);
-      at::Tensor x2 = at::empty_like(x);
-      layernorm(x2, o2, l[9], x1, l[10], l[11], eps_);
-      x = x2;
+    if (!fused_.empty()) {
+      x = forward_fused(x, starts, lens, tiles);
+    } else {
+      for (auto& l : layers_) {
+        // qkv_w, qkv_b, o_w, o_b, ln1_g, ln1_b, ff1_w, ff1_b, ff2_w, ff2_b, ln2_g, ln2_b
+        at::Tensor qkv = at::linear(x, l[0], l[1]);
+        at::Tensor a = at::empty({T, H}, x.options());
+        varlen_encoder_attention(a, qkv, starts, lens, tiles, heads_, heads_, scale_);
+        at::Tensor o = at::linear(a, l[2]);
+        at::Tensor x1 = at::empty_like(x);
+        layernorm(x1, o, l[3], x, l[4], l[5], eps_);
+        at::Tensor hdn = at::linear(x1, l[6]);
+        bias_gelu(hdn, l[7]);
+        at::Tensor o2 = at::linear(hdn, l[8]);
+        at::Tensor x2 = at::empty_like(x);
+        layernorm(x2, o2, l[9], x1, l[10], l[11], eps_);
+        x = x2;
+      }
     }
     at::Tensor out = at::empty({starts.size(0), H}, x.options().dtype(out_f32 ? at::kFloat : x.scalar_type()));
     pool_embeddings(out, x, starts, lens, pooling_, normalize_);
@@ -368,12 +380,54 @@ class BertRunner {
   }
 
  private:
+  at::Tensor forward_fused(at::Tensor x, const at::Tensor& starts, const at::Tensor& lens, const at::Tensor& tiles) {
+    const int64_t T = x.size(0), H = x.size(1);
+    auto st_opts = x.options().dtype(at::kFloat);
+    at::Tensor xp2, st2;
+    const at::Tensor* pg = nullptr;
+    const at::Tensor* pb = nullptr;
+    for (size_t i = 0; i < layers_.size(); ++i) {
+      auto& l = layers_[i];
+      auto& f = fused_[i];
+      at::Tensor qkv = at::empty({T, f[0].size(0)}, x.options());
+      if (i == 0)
+        gemm_fused(qkv, x, f[0], l[1], false, c10::nullopt, c10::nullopt, 0, c10::nullopt, c10::nullopt,
+                   c10::nullopt, c10::nullopt, eps_, c10::nullopt);
+      else
+        gemm_fused(qkv, xp2, f[0], l[1], false, c10::nullopt, st2, H, f[1], f[2], c10::nullopt, c10::nullopt, eps_,
+                   c10::nullopt);
+      at::Tensor a = at::empty({T, H}, x.options());
+      varlen_encoder_attention(a, qkv, starts, lens, tiles, heads_, heads_, scale_);
+      at::Tensor xp1 = at::empty({T, H}, x.options());
+      at::Tensor st1 = at::empty({T, H / 64, 2}, st_opts);
+      if (i == 0)
+        gemm_fused(xp1, a, l[2], l[3], false, x, c10::nullopt, 0, c10::nullopt, c10::nullopt, c10::nullopt,
+                   c10::nullopt, eps_, st1);
+      else
+        gemm_fused(xp1, a, l[2], l[3], false, xp2, st2, H, c10::nullopt, c10::nullopt, *pg, *pb, eps_, st1);
+      at::Tensor hdn = at::empty({T, f[3].size(0)}, x.options());
+      gemm_fused(hdn, xp1, f[3], l[7], true, c10::nullopt, st1, H, f[4], f[5], c10::nullopt, c10::nullopt, eps_,
+                 c10::nullopt);
+      at::Tensor nx = at::empty({T, H}, x.options());
+      at::Tensor nst = at::empty({T, H / 64, 2}, st_opts);
+      gemm_fused(nx, hdn, l[8], l[9], false, xp1, st1, H, c10::nullopt, c10::nullopt, l[4], l[5], eps_, nst);
+      xp2 = nx;
+      st2 = nst;
+      pg = &l[10];
+      pb = &l[11];
+    }
+    at::Tensor out = at::empty_like(xp2);
+    layernorm(out, xp2, c10::nullopt, c10::nullopt, *pg, *pb, eps_);
+    return out;
+  }
+
   at::Tensor wte_, wpe_, wtt_, emb_g_, emb_b_;
   std::vector<std::vector<at::Tensor>> layers_;
   int64_t heads_;
   double eps_, scale_;
   int64_t pooling_;
   bool normalize_;
+  std::vector<std::vector<at::Tensor>> fused_;
 };
 
 // ---------------------------------------------------------------------------- step executor
@@ -714,7 +768,7 @@ void bind_runners(py::module_& m) {
       .def("forward", &LlamaRunner::forward, py::call_guard<py::gil_scoped_release>());
   py::class_<BertRunner>(m, "BertRunner")
       .def(py::init<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor, std::vector<std::vector<at::Tensor>>,
-                    int64_t, double, double, int64_t, bool>())
+                    int64_t, double, double, int64_t, bool, std::vector<std::vector<at::Tensor>>>())
       .def("forward", &BertRunner::forward, py::call_guard<py::gil_scoped_release>());
   py::class_<StepExecutor>(m, "StepExecutor")
       .def(py::init<std::shared_ptr<LlamaRunner>, std::map<std::string, int64_t>, int64_t, int64_t, int64_t,

@@ -50,6 +50,41 @@ def bias_gelu(x, bias):
     return torch.nn.functional.gelu(v).to(x.dtype)
 
 
+def ln_row_stats(st, width, eps):
+    """(mean, rstd) per row from partial (sum, sumsq) statistics [M, T, 2]."""
+    s = st[..., 0].sum(-1)
+    ss = st[..., 1].sum(-1)
+    mu = s / width
+    var = (ss / width - mu * mu).clamp_min(0.0)
+    return mu, torch.rsqrt(var + eps)
+
+
+def gemm_fused(x, w, bias=None, gelu=False, residual=None, ln_stats_in=None, ln_width=0, c1=None, c2=None,
+               res_g=None, res_b=None, eps=1e-12, stats_out=None):
+    """fp32 reference of ops/csrc/gemm_fused.hip (epilogue order documented there)."""
+    v = x.float() @ w.float().t()
+    mu = rs = None
+    if ln_stats_in is not None:
+        mu, rs = ln_row_stats(ln_stats_in.float(), ln_width, eps)
+        mu, rs = mu[:, None], rs[:, None]
+        if res_g is None:
+            v = rs * (v - mu * c1.float()[None]) + c2.float()[None]
+    if bias is not None:
+        v = v + bias.float()
+    if gelu:
+        v = torch.nn.functional.gelu(v)
+    if residual is not None:
+        r = residual.float()
+        if ln_stats_in is not None and res_g is not None:
+            r = (r - mu) * rs * res_g.float() + res_b.float()
+        v = v + r
+    out = v.to(x.dtype)
+    if stats_out is not None:
+        o = out.float().view(out.shape[0], -1, 64)
+        stats_out.copy_(torch.stack([o.sum(-1), (o * o).sum(-1)], -1))
+    return out
+
+
 def rope_cos_sin(max_pos: int, head_dim: int, theta: float, scaling: dict | None = None,
                  device=None) -> torch.Tensor:
     """[max_pos, D] f32: cols [0, D/2) = cos, [D/2, D) = sin.  Supports the Llama-3.1
