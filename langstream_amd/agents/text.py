@@ -9,8 +9,9 @@ document-to-json, text-splitter.
   text_num_chunks.
 * text-extractor: Tika AutoDetect in the reference; here: plain text, HTML, XML, JSON,
   DOCX/PPTX/XLSX/ODT (zip + XML), RTF, and PDF text streams (uncompressed / Flate).
-* language-detector: stop-word profile scoring (Tika LanguageIdentifier in the
-  reference) -> header ``language`` (configurable), ``allowedLanguages`` filter.
+* language-detector: character 1-3-gram profiles scored naive-Bayes (the n-gram
+  approach of Tika's LanguageIdentifier in the reference) -> header ``language``
+  (configurable), ``allowedLanguages`` filter.
 """
 from __future__ import annotations
 
@@ -289,28 +290,95 @@ class TextExtractorAgent(SingleRecordAgentProcessor):
 
 
 # ---------------------------------------------------------------- language detection
-_STOPWORDS = {
-    "en": "the and of to in is that it for was on are with as be this by have not at from or but".split(),
-    "it": "il di che e la per un in non una sono del della si con le da al lo ma".split(),
-    "fr": "le de la et les des un une du en est que pas pour dans qui sur au avec".split(),
-    "de": "der die und das ist nicht ein eine zu den von mit sich des auf für im dem".split(),
-    "es": "el la de que y en los se del las un por con no una para es al lo como".split(),
-    "pt": "o a de que e do da em um para com não uma os no se na por mais as dos".split(),
-    "nl": "de het een en van in is dat op te zijn niet met voor die aan er".split(),
+# Character n-gram profiles (the technique of Tika's LanguageIdentifier, which the
+# reference uses: TXT/LanguageDetectorAgent.java:30-76): each language's profile is the
+# 1-3-gram distribution of a built-in sample text (word-boundary padded); a text is
+# scored by the naive-Bayes log-likelihood of its n-grams under each profile (add-k
+# smoothed) and labelled with the best language, or "unknown" when it has no letters.
+_SAMPLES = {
+    "en": "the weather is nice today and we are going to the park with our friends. this is a simple "
+          "english sentence that shows how the language works. people in the city like to read books, "
+          "watch movies and talk about their work. what would you like to do this weekend? i think that "
+          "we should visit the museum because there is a new exhibition about history and science. "
+          "they have been waiting for the train since the morning, but it was late again. which one is "
+          "yours? she said that it was the best thing she had ever seen.",
+    "it": "questo è un esempio di testo in lingua italiana. oggi il tempo è bello e andiamo al parco con "
+          "gli amici. la gente della città ama leggere libri, guardare film e parlare del proprio lavoro. "
+          "che cosa vorresti fare questo fine settimana? penso che dovremmo visitare il museo perché c'è "
+          "una nuova mostra sulla storia e sulla scienza. aspettano il treno dalla mattina, ma era ancora "
+          "in ritardo. quale è il tuo? lei ha detto che era la cosa più bella che avesse mai visto. "
+          "questo libro è molto interessante e parla di italiano, cultura e tradizioni.",
+    "fr": "ceci est un exemple de texte en langue française. aujourd'hui il fait beau et nous allons au "
+          "parc avec nos amis. les gens de la ville aiment lire des livres, regarder des films et parler "
+          "de leur travail. qu'est-ce que vous voulez faire ce week-end? je pense que nous devrions "
+          "visiter le musée parce qu'il y a une nouvelle exposition sur l'histoire et la science. ils "
+          "attendent le train depuis le matin, mais il était encore en retard. parlez-vous français? "
+          "elle a dit que c'était la plus belle chose qu'elle ait jamais vue. voilà, ça va très bien.",
+    "de": "dies ist ein beispiel für einen text in deutscher sprache. heute ist das wetter schön und wir "
+          "gehen mit unseren freunden in den park. die menschen in der stadt lesen gerne bücher, sehen "
+          "filme und sprechen über ihre arbeit. was möchtest du an diesem wochenende machen? ich denke, "
+          "dass wir das museum besuchen sollten, weil es eine neue ausstellung über geschichte und "
+          "wissenschaft gibt. sie warten seit dem morgen auf den zug, aber er hatte wieder verspätung. "
+          "sie sagte, dass es das schönste war, was sie je gesehen hatte. sprechen sie deutsch?",
+    "es": "este es un ejemplo de texto en lengua española. hoy hace buen tiempo y vamos al parque con los "
+          "amigos. la gente de la ciudad disfruta leyendo libros, viendo películas y hablando de su "
+          "trabajo. ¿qué te gustaría hacer este fin de semana? creo que deberíamos visitar el museo "
+          "porque hay una nueva exposición sobre la historia y la ciencia. esperan el tren desde la "
+          "mañana, pero llegó tarde otra vez. ¿cuál es el tuyo? ella dijo que era lo más bonito que "
+          "había visto nunca. ¿hablas español? sí, un poco.",
+    "pt": "este é um exemplo de texto em língua portuguesa. hoje o tempo está bom e vamos ao parque com os "
+          "amigos. as pessoas da cidade gostam de ler livros, ver filmes e falar sobre o seu trabalho. o "
+          "que você gostaria de fazer neste fim de semana? acho que deveríamos visitar o museu porque há "
+          "uma nova exposição sobre a história e a ciência. eles esperam o comboio desde a manhã, mas "
+          "estava atrasado outra vez. ela disse que foi a coisa mais bonita que já tinha visto. você "
+          "fala português? não, ainda não. obrigado pela atenção.",
+    "nl": "dit is een voorbeeld van een tekst in de nederlandse taal. vandaag is het mooi weer en gaan we "
+          "met onze vrienden naar het park. de mensen in de stad lezen graag boeken, kijken films en "
+          "praten over hun werk. wat wil je dit weekend doen? ik denk dat we het museum moeten bezoeken "
+          "omdat er een nieuwe tentoonstelling is over geschiedenis en wetenschap. ze wachten sinds de "
+          "ochtend op de trein, maar hij was weer te laat. zij zei dat het het mooiste was dat ze ooit "
+          "had gezien. spreekt u nederlands? ja, een beetje.",
 }
+_WORD = re.compile(r"[^\W\d_]+", re.UNICODE)
+
+
+def _ngrams(text: str):
+    for w in _WORD.findall(text.lower()):
+        p = f" {w} "
+        for n in (1, 2, 3):
+            for i in range(len(p) - n + 1):
+                g = p[i:i + n]
+                if g.strip():
+                    yield g
+
+
+def _build_profiles():
+    import math
+    from collections import Counter
+    profs = {}
+    for lang, txt in _SAMPLES.items():
+        c = Counter(_ngrams(txt))
+        tot = {n: sum(v for g, v in c.items() if len(g) == n) for n in (1, 2, 3)}
+        vocab = {n: sum(1 for g in c if len(g) == n) for n in (1, 2, 3)}
+        # add-0.5 smoothing per n-gram order; unseen grams get the floor log-prob
+        profs[lang] = ({g: math.log((v + 0.5) / (tot[len(g)] + 0.5 * (vocab[len(g)] + 1))) for g, v in c.items()},
+                       {n: math.log(0.5 / (tot[n] + 0.5 * (vocab[n] + 1))) for n in (1, 2, 3)})
+    return profs
+
+
+_PROFILES = _build_profiles()
 
 
 def detect_language(text: str) -> str:
-    words = re.findall(r"[a-zàâäéèêëïîôöùûüçñßáíóúãõ]+", text.lower())
-    if not words:
+    grams = list(_ngrams(text))
+    if not grams:
         return "unknown"
-    best, score = "unknown", 0.0
-    for lang, sw in _STOPWORDS.items():
-        s = set(sw)
-        sc = sum(1 for w in words if w in s) / len(words)
+    best, score = "unknown", float("-inf")
+    for lang, (lp, floor) in _PROFILES.items():
+        sc = sum(lp.get(g, floor[len(g)]) * len(g) for g in grams)   # longer grams weigh more
         if sc > score:
             best, score = lang, sc
-    return best if score > 0.02 else "unknown"
+    return best
 
 
 @register_agent("language-detector")

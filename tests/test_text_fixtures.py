@@ -1,0 +1,104 @@
+"""Reference fixtures of the text-processing agents, ported:
+TXT tests TextChunkerAgentTest.java:87-127, LanguageDetectorTest.java:37-39 and
+TextExtractorTest.java (the PDF / DOCX fixtures are read from the reference checkout
+when it is present; they are not copied into this repository).
+
+cl100k parity: no cl100k_base rank file exists offline, so the native BPE counter is a
+synthetic-vocabulary byte-level BPE and its counts differ from tiktoken's ("parity
+unpinned").  The cl100k fixture is therefore checked twice: the splitter's merge /
+overlap algorithm with a counter that returns cl100k's real counts for the fixture's
+words (must equal the reference output exactly), and the agent with the native counter
+(chunk sizes within the configured budget)."""
+import os
+
+import pytest
+
+from langstream_amd.agents.text import LanguageDetectorAgent, RecursiveCharacterTextSplitter, TextExtractorAgent, \
+    TextSplitterAgent
+from langstream_amd.api.record import SimpleRecord
+
+RES = "/root/reference/langstream-agents/langstream-agents-text-processing/src/test/resources"
+
+
+def _chunks(cfg, text):
+    a = TextSplitterAgent()
+    a.init(cfg)
+    return [r.value() for r in a.process_record(SimpleRecord.of("filename.txt", text.encode()))]
+
+
+@pytest.mark.parametrize("size,overlap,text,expected", [
+    (20, 5, "Hello world", ["Hello world"]),
+    (15, 5, "Hello world. This is a great day", ["Hello world.", "This is a great", "great day"]),
+    (20, 5, "", []),
+    (20, 5, " ", []),
+])
+def test_chunker_length_fixtures(size, overlap, text, expected):
+    cfg = {"splitter_type": "RecursiveCharacterTextSplitter", "separators": ["\n\n", "\n", " ", ""],
+           "keep_separator": "false", "chunk_size": size, "chunk_overlap": overlap, "length_function": "length"}
+    assert _chunks(cfg, text) == expected
+
+
+def test_chunker_keep_separator_fixture():
+    cfg = {"splitter_type": "RecursiveCharacterTextSplitter", "separators": ["\n\n", "\n", " ", ""],
+           "keep_separator": True, "chunk_size": 15, "chunk_overlap": 5, "length_function": "length"}
+    assert _chunks(cfg, "Hello world. This is a great day") == ["Hello world.", "This is a", "is a great day"]
+
+
+# cl100k_base token counts of the fixture's pieces (one token each, "world," = world + ",")
+_CL100K = {"Hello": 1, "world,": 2, "I": 1, "would": 1, "like": 1, "to": 1, "see": 1, "some": 1, "overlap": 1,
+           "here": 1, " ": 1}
+
+
+def _cl100k_like(s: str) -> int:
+    if s in _CL100K:
+        return _CL100K[s]
+    return sum(_CL100K.get(w, 1) for w in s.split(" ")) + s.count(" ")
+
+
+def test_chunker_cl100k_fixture_merge_algorithm():
+    sp = RecursiveCharacterTextSplitter(["\n\n", "\n", " ", ""], False, 10, 2, _cl100k_like)
+    assert sp.split_text("Hello world, I would like to see some overlap here") == \
+        ["Hello world, I would like", "like to see some overlap", "overlap here"]
+    sp = RecursiveCharacterTextSplitter(["\n\n", "\n", " ", ""], False, 20, 5, _cl100k_like)
+    assert sp.split_text("Hello world") == ["Hello world"]
+
+
+def test_chunker_cl100k_native_counter_budget():
+    from langstream_amd.tokenizers import cl100k_counter
+    count = cl100k_counter()
+    cfg = {"chunk_size": 10, "chunk_overlap": 2, "length_function": "cl100k_base"}
+    out = _chunks(cfg, "Hello world, I would like to see some overlap here")
+    assert out and all(count(c) <= 10 for c in out)
+    assert " ".join(out).replace("  ", " ").startswith("Hello world")
+
+
+@pytest.mark.parametrize("text,lang", [("This is a English", "en"), ("Questo é italiano", "it"),
+                                       ("Parlez-vous français?", "fr")])
+def test_language_detector_fixtures(text, lang):
+    a = LanguageDetectorAgent()
+    a.init({"property": "detected-language"})
+    out = a.process_record(SimpleRecord.of("filename.txt", text.encode()))
+    assert out[0].header_value("detected-language") == lang
+
+
+def test_language_detector_allowed_languages_filter():
+    a = LanguageDetectorAgent()
+    a.init({"property": "language", "allowedLanguages": ["en"]})
+    assert a.process_record(SimpleRecord.of("k", "Questo é italiano")) == []
+    assert len(a.process_record(SimpleRecord.of("k", "This is a English"))) == 1
+
+
+def test_text_extractor_plain_text_fixture():
+    a = TextExtractorAgent()
+    out = a.process_record(SimpleRecord.of("filename.txt", b"This is a test"))
+    assert out[0].value().strip() == "This is a test"
+
+
+@pytest.mark.skipif(not os.path.isdir(RES), reason="reference checkout not present")
+@pytest.mark.parametrize("fn,expected", [("simple.pdf", "This is a very simple PDF"),
+                                         ("simple.docx", "This is a very simple Word Document")])
+def test_text_extractor_binary_fixtures(fn, expected):
+    with open(os.path.join(RES, fn), "rb") as f:
+        data = f.read()
+    out = TextExtractorAgent().process_record(SimpleRecord.of("filename", data))
+    assert out[0].value().strip() == expected
