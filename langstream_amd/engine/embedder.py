@@ -54,24 +54,27 @@ class EmbeddingEngine:
             return self.encoder.encode_tokens(toks)
 
     def _embed_batch(self, texts: List[str]):
-        res = []
+        """Tokenise once (native, multi-threaded), encode in packed batches of at most
+        ``max_batch_tokens`` on the auxiliary stream, one device->host copy at the end."""
+        all_toks = self.tok.encode_batch(texts, max_len=self.max_len)
+        outs = []
         i = 0
-        while i < len(texts):
-            toks, ntok = [], 0
-            batch_toks = self.tok.encode_batch(texts[i:], max_len=self.max_len)
-            for t in batch_toks:
-                if toks and ntok + len(t) > self.max_batch_tokens:
-                    break
-                toks.append(t)
-                ntok += len(t)
-            with on_aux(self.encoder.device):  # do not queue behind the LLM engine's steps
-                emb = self.encoder.encode_tokens(toks)
-                res.append(to_host(emb)[0])
-            self.stats["batches"] += 1
-            self.stats["texts"] += len(toks)
-            self.stats["tokens"] += ntok
-            i += len(toks)
-        return torch.cat(res) if res else torch.zeros(0, self.dim)
+        with on_aux(self.encoder.device):  # do not queue behind the LLM engine's steps
+            while i < len(all_toks):
+                toks, ntok = [], 0
+                for t in all_toks[i:]:
+                    if toks and ntok + len(t) > self.max_batch_tokens:
+                        break
+                    toks.append(t)
+                    ntok += len(t)
+                outs.append(self.encoder.encode_tokens(toks))
+                self.stats["batches"] += 1
+                self.stats["texts"] += len(toks)
+                self.stats["tokens"] += ntok
+                i += len(toks)
+            if not outs:
+                return torch.zeros(0, self.dim)
+            return to_host(outs[0] if len(outs) == 1 else torch.cat(outs))[0]
 
     # ------------------------------------------------------------------ async api
     def embed_async(self, texts: Sequence[str]) -> Future:

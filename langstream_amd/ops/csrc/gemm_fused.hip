@@ -196,6 +196,19 @@ __global__ void __launch_bounds__(BM * 2) gemm_fused_kernel(const bf16* __restri
     }
 }
 
+// ring depth: the LDS ring bounds workgroups per CU (BM=256: 24 KB per stage), so a short
+// K (encoder: 12-48 stages) runs a 3-deep ring at 2 workgroups per CU, overlapping one
+// workgroup's prologue / epilogue with another's main loop; LS_GEMM_RING overrides.
+int ring_depth(int bm, int nk) {
+  static const int env = [] {
+    const char* v = getenv("LS_GEMM_RING");
+    return v ? atoi(v) : 0;
+  }();
+  if (env == 3 || env == 4 || env == 6) return env;
+  if (bm == 256) return nk <= 48 ? 3 : 6;
+  return nk <= 48 ? 3 : 4;
+}
+
 template <int FL>
 void launch_fl(int bm, dim3 grid, hipStream_t st, const at::Tensor& x, const at::Tensor& w, int M, int N, int K,
                at::Tensor& out, int MT, const Epi& e) {
@@ -203,9 +216,16 @@ void launch_fl(int bm, dim3 grid, hipStream_t st, const at::Tensor& x, const at:
   gemm_fused_kernel<BMV, SV, FL><<<grid, BMV * 2, 0, st>>>((const bf16*)x.data_ptr(), x.stride(0),            \
                                                           (const bf16*)w.data_ptr(), M, N, K,                 \
                                                           (bf16*)out.data_ptr(), out.stride(0), MT, e)
-  if (bm == 64) L(64, 4);
-  else if (bm == 128) L(128, 4);
-  else L(256, 6);
+#define LS(BMV)                      \
+  switch (ring_depth(BMV, K / GBK)) { \
+    case 3: L(BMV, 3); break;        \
+    case 4: L(BMV, 4); break;        \
+    default: L(BMV, 6); break;       \
+  }
+  if (bm == 64) { LS(64) }
+  else if (bm == 128) { LS(128) }
+  else { LS(256) }
+#undef LS
 #undef L
 }
 
