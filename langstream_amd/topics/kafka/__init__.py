@@ -18,6 +18,10 @@ Parity:
   (``{partition: offset}`` JSON, base64 in the gateway API).
 * admin (``KafkaTopicConnectionsRuntime.java:166-291``): create-if-not-exists topics
   on deploy, delete topics with deletion-mode ``delete``.
+* security (``security.py``): TLS and SASL/PLAIN from the Java property names of the
+  ``admin`` map (consumer / producer maps may override) -- the reference's
+  ``examples/instances/astra.yaml`` shape; compressed record batches (gzip / snappy /
+  lz4) decode on fetch, and ``producer.compression.type`` compresses produced batches.
 """
 from __future__ import annotations
 
@@ -32,7 +36,9 @@ from ...api.record import Header, Record
 from ...api.topics import (TopicAdmin, TopicConnectionsRuntime, TopicConnectionsRuntimeRegistry, TopicConsumer,
                            TopicOffsetPosition, TopicProducer, TopicReader, TopicReadResult, decode_offsets,
                            encode_offsets)
+from . import codecs
 from .client import GroupConsumer, KafkaClient, PartitionReader, Producer
+from .security import SecurityConfig
 
 log = logging.getLogger(__name__)
 
@@ -79,8 +85,9 @@ def _bootstrap(streaming_cluster) -> str:
 
 
 class KafkaConsumer(TopicConsumer):
-    def __init__(self, bootstrap: str, topic: str, group: str, reset: str, max_records: int, poll_ms: int):
-        self.client = KafkaClient(bootstrap, client_id=f"consumer-{group}")
+    def __init__(self, bootstrap: str, topic: str, group: str, reset: str, max_records: int, poll_ms: int,
+                 security: Optional[SecurityConfig] = None):
+        self.client = KafkaClient(bootstrap, client_id=f"consumer-{group}", security=security)
         self.c = GroupConsumer(self.client, topic, group, reset, max_poll_records=max_records)
         self.topic, self.group, self.poll_ms = topic, group, poll_ms
         self._out = 0
@@ -110,9 +117,9 @@ class KafkaConsumer(TopicConsumer):
 
 
 class KafkaProducer(TopicProducer):
-    def __init__(self, bootstrap: str, topic: str):
-        self.client = KafkaClient(bootstrap, client_id=f"producer-{topic}")
-        self.p = Producer(self.client, topic)
+    def __init__(self, bootstrap: str, topic: str, security: Optional[SecurityConfig] = None, codec: int = 0):
+        self.client = KafkaClient(bootstrap, client_id=f"producer-{topic}", security=security)
+        self.p = Producer(self.client, topic, codec=codec)
         self.topic = topic
         self._in = 0
         self._lock = threading.Lock()
@@ -141,8 +148,9 @@ class KafkaProducer(TopicProducer):
 
 
 class KafkaReader(TopicReader):
-    def __init__(self, bootstrap: str, topic: str, position: TopicOffsetPosition, poll_ms: int = 500):
-        self.client = KafkaClient(bootstrap, client_id=f"reader-{topic}")
+    def __init__(self, bootstrap: str, topic: str, position: TopicOffsetPosition, poll_ms: int = 500,
+                 security: Optional[SecurityConfig] = None):
+        self.client = KafkaClient(bootstrap, client_id=f"reader-{topic}", security=security)
         self.topic, self.position, self.poll_ms = topic, position, poll_ms
         self.r: Optional[PartitionReader] = None
 
@@ -165,9 +173,16 @@ class KafkaTopicConnectionsRuntime(TopicConnectionsRuntime):
     def init(self, streaming_cluster) -> None:
         self.sc = streaming_cluster
         self.bootstrap = _bootstrap(streaming_cluster)
+        cfg = (streaming_cluster.configuration if streaming_cluster is not None else {}) or {}
+        self.admin_cfg = cfg.get("admin") or {}
+        self.consumer_cfg = cfg.get("consumer") or {}
+        self.producer_cfg = cfg.get("producer") or {}
+        self.security = SecurityConfig.from_config(self.admin_cfg)
+        self.consumer_security = SecurityConfig.from_config(self.admin_cfg, self.consumer_cfg)
+        self.producer_security = SecurityConfig.from_config(self.admin_cfg, self.producer_cfg)
 
     def deploy(self, plan) -> None:
-        client = KafkaClient(self.bootstrap, client_id="langstream-admin")
+        client = KafkaClient(self.bootstrap, client_id="langstream-admin", security=self.security)
         try:
             for t in plan.topics.values():
                 if t.creation_mode == "create-if-not-exists":
@@ -177,7 +192,7 @@ class KafkaTopicConnectionsRuntime(TopicConnectionsRuntime):
             client.close()
 
     def delete(self, plan) -> None:
-        client = KafkaClient(self.bootstrap, client_id="langstream-admin")
+        client = KafkaClient(self.bootstrap, client_id="langstream-admin", security=self.security)
         try:
             for t in plan.topics.values():
                 if t.deletion_mode == "delete":
@@ -190,14 +205,15 @@ class KafkaTopicConnectionsRuntime(TopicConnectionsRuntime):
         return KafkaConsumer(self.bootstrap, configuration["topic"], group,
                              str(configuration.get("auto.offset.reset", "earliest")),
                              int(configuration.get("max.poll.records", 500)),
-                             int(configuration.get("poll.timeout.ms", 500)))
+                             int(configuration.get("poll.timeout.ms", 500)), self.consumer_security)
 
     def create_producer(self, agent_id, streaming_cluster, configuration) -> TopicProducer:
-        return KafkaProducer(self.bootstrap, configuration["topic"])
+        ctype = configuration.get("compression.type", self.producer_cfg.get("compression.type"))
+        return KafkaProducer(self.bootstrap, configuration["topic"], self.producer_security, codecs.codec_of(ctype))
 
     def create_reader(self, streaming_cluster, configuration, initial_position) -> TopicReader:
         return KafkaReader(self.bootstrap, configuration["topic"], initial_position,
-                           int(configuration.get("poll.timeout.ms", 500)))
+                           int(configuration.get("poll.timeout.ms", 500)), self.consumer_security)
 
     def create_topic_admin(self, agent_id, streaming_cluster, configuration) -> TopicAdmin:
         return TopicAdmin()

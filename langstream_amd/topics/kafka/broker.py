@@ -46,8 +46,14 @@ class _Group:
 
 class KafkaBroker:
     def __init__(self, host: str = "127.0.0.1", port: int = 0, auto_create_topics: bool = True,
-                 default_partitions: int = 1, node_id: int = 0):
+                 default_partitions: int = 1, node_id: int = 0, ssl_context=None,
+                 sasl_users: Optional[Dict[str, str]] = None):
+        """``ssl_context``: a server-side SSLContext -> TLS listener (SSL / SASL_SSL);
+        ``sasl_users``: {username: password} -> SASL/PLAIN required before any other API
+        (an unauthenticated request closes the connection, as a Kafka broker does)."""
         self.host, self.port = host, port
+        self.ssl_context = ssl_context
+        self.sasl_users = sasl_users
         self.node_id = node_id
         self.auto_create = auto_create_topics
         self.default_partitions = default_partitions
@@ -66,7 +72,8 @@ class KafkaBroker:
             self._loop = asyncio.new_event_loop()
             asyncio.set_event_loop(self._loop)
             self._data_cv = asyncio.Condition()
-            self._server = self._loop.run_until_complete(asyncio.start_server(self._handle, self.host, self.port))
+            self._server = self._loop.run_until_complete(
+                asyncio.start_server(self._handle, self.host, self.port, ssl=self.ssl_context))
             self.port = self._server.sockets[0].getsockname()[1]
             self._loop.create_task(self._expire_sessions())
             self._started.set()
@@ -101,6 +108,7 @@ class KafkaBroker:
 
     # ------------------------------------------------------------------ connection
     async def _handle(self, reader: asyncio.StreamReader, writer: asyncio.StreamWriter) -> None:
+        authed = not self.sasl_users
         try:
             while True:
                 hdr = await reader.readexactly(4)
@@ -114,7 +122,22 @@ class KafkaBroker:
                         log.warning("unsupported api %s v%s", api, ver)
                         writer.close()
                         return
-                resp = await self._dispatch(api, body, client_id or "client")
+                if api == P.SASL_HANDSHAKE:
+                    ok = bool(self.sasl_users) and body["mechanism"] == "PLAIN"
+                    resp = {"error": P.NONE if ok else P.UNSUPPORTED_SASL_MECHANISM,
+                            "mechanisms": ["PLAIN"] if self.sasl_users else []}
+                elif api == P.SASL_AUTHENTICATE:
+                    parts = bytes(body["auth_bytes"]).split(b"\0")
+                    user, pw = (parts[1].decode(), parts[2].decode()) if len(parts) == 3 else (None, None)
+                    authed = user is not None and self.sasl_users.get(user) == pw
+                    resp = {"error": P.NONE if authed else P.SASL_AUTHENTICATION_FAILED,
+                            "error_message": None if authed else "Authentication failed: invalid credentials",
+                            "auth_bytes": b""}
+                elif not authed and api != P.API_VERSIONS:
+                    log.warning("unauthenticated request %s from %s: closing", api, client_id)
+                    return
+                else:
+                    resp = await self._dispatch(api, body, client_id or "client")
                 writer.write(P.response_frame(corr, api, resp))
                 await writer.drain()
         except (asyncio.IncompleteReadError, ConnectionError):

@@ -38,12 +38,29 @@ class KafkaError(Exception):
 
 
 class KafkaConnection:
-    def __init__(self, host: str, port: int, client_id: str, timeout: float = 30.0):
-        self.sock = socket.create_connection((host, port), timeout=timeout)
-        self.sock.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+    def __init__(self, host: str, port: int, client_id: str, timeout: float = 30.0, security=None):
+        sock = socket.create_connection((host, port), timeout=timeout)
+        sock.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+        if security is not None and security.tls:
+            sock = security.ssl_context().wrap_socket(sock, server_hostname=host)
+        self.sock = sock
         self.client_id = client_id
         self._corr = itertools.count(1)
         self._lock = threading.Lock()
+        if security is not None and security.sasl:
+            self._sasl_plain(security)
+
+    def _sasl_plain(self, security) -> None:
+        """SaslHandshake v1 + SaslAuthenticate v0 (KIP-152) with the PLAIN mechanism."""
+        r = self.request(P.SASL_HANDSHAKE, {"mechanism": security.mechanism})
+        if r["error"] != P.NONE:
+            self.close()
+            raise KafkaError(r["error"], f"SASL mechanism {security.mechanism} not enabled; broker offers "
+                                         f"{r['mechanisms']}")
+        r = self.request(P.SASL_AUTHENTICATE, {"auth_bytes": security.plain_token()})
+        if r["error"] != P.NONE:
+            self.close()
+            raise KafkaError(r["error"], f"SASL authentication failed: {r.get('error_message')}")
 
     def _recv_exact(self, n: int) -> bytes:
         buf = bytearray()
@@ -74,10 +91,11 @@ class KafkaConnection:
 
 
 class KafkaClient:
-    def __init__(self, bootstrap_servers: str, client_id: str = "langstream-amd"):
+    def __init__(self, bootstrap_servers: str, client_id: str = "langstream-amd", security=None):
         self.bootstrap = [(h.rsplit(":", 1)[0], int(h.rsplit(":", 1)[1]))
                           for h in str(bootstrap_servers).split(",") if h.strip()]
         self.client_id = client_id
+        self.security = security
         self._conns: Dict[Tuple[str, int], KafkaConnection] = {}
         self.brokers: Dict[int, Tuple[str, int]] = {}
         self.partitions: Dict[str, Dict[int, int]] = {}  # topic -> partition -> leader
@@ -87,7 +105,7 @@ class KafkaClient:
         with self._lock:
             c = self._conns.get(addr)
             if c is None:
-                c = KafkaConnection(addr[0], addr[1], self.client_id)
+                c = KafkaConnection(addr[0], addr[1], self.client_id, security=self.security)
                 self._conns[addr] = c
             return c
 
@@ -180,9 +198,10 @@ class KafkaClient:
 
 
 class Producer:
-    def __init__(self, client: KafkaClient, topic: str):
+    def __init__(self, client: KafkaClient, topic: str, codec: int = 0):
         self.client = client
         self.topic = topic
+        self.codec = codec
         self._rr = itertools.count(random.randrange(1 << 16))
 
     def partition(self, key: Optional[bytes]) -> int:
@@ -200,7 +219,7 @@ class Producer:
             r = self.client.leader_conn(self.topic, p).request(P.PRODUCE, {
                 "transactional_id": None, "acks": -1, "timeout": 30000,
                 "topics": [{"name": self.topic, "partitions": [{"partition": p,
-                                                                "records": P.encode_batch(0, recs)}]}]})
+                                                                "records": P.encode_batch(0, recs, self.codec)}]}]})
             pr = r["topics"][0]["partitions"][0]
             if pr["error"] != P.NONE:
                 raise KafkaError(pr["error"], f"produce {self.topic}/{p}")

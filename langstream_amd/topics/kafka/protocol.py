@@ -22,16 +22,18 @@ PRODUCE, FETCH, LIST_OFFSETS, METADATA = 0, 1, 2, 3
 OFFSET_COMMIT, OFFSET_FETCH, FIND_COORDINATOR = 8, 9, 10
 JOIN_GROUP, HEARTBEAT, LEAVE_GROUP, SYNC_GROUP = 11, 12, 13, 14
 API_VERSIONS, CREATE_TOPICS, DELETE_TOPICS = 18, 19, 20
+SASL_HANDSHAKE, SASL_AUTHENTICATE = 17, 36
 
 VERSIONS = {PRODUCE: 3, FETCH: 4, LIST_OFFSETS: 1, METADATA: 1, OFFSET_COMMIT: 2, OFFSET_FETCH: 1,
             FIND_COORDINATOR: 0, JOIN_GROUP: 1, HEARTBEAT: 0, LEAVE_GROUP: 0, SYNC_GROUP: 0, API_VERSIONS: 0,
-            CREATE_TOPICS: 0, DELETE_TOPICS: 0}
+            CREATE_TOPICS: 0, DELETE_TOPICS: 0, SASL_HANDSHAKE: 1, SASL_AUTHENTICATE: 0}
 
 # error codes
 NONE, OFFSET_OUT_OF_RANGE, UNKNOWN_TOPIC_OR_PARTITION = 0, 1, 3
 COORDINATOR_NOT_AVAILABLE, NOT_COORDINATOR = 15, 16
 ILLEGAL_GENERATION, UNKNOWN_MEMBER_ID, REBALANCE_IN_PROGRESS = 22, 25, 27
 TOPIC_ALREADY_EXISTS, UNSUPPORTED_VERSION = 36, 35
+UNSUPPORTED_SASL_MECHANISM, ILLEGAL_SASL_STATE, SASL_AUTHENTICATION_FAILED = 33, 34, 58
 
 # ---------------------------------------------------------------- schemas
 # a schema is a list of (name, type); type is a primitive name, ("array", schema|primitive)
@@ -44,6 +46,8 @@ def A(t):
 
 REQ = {
     API_VERSIONS: [],
+    SASL_HANDSHAKE: [("mechanism", STR)],
+    SASL_AUTHENTICATE: [("auth_bytes", BYTES)],
     METADATA: [("topics", A(STR))],  # null array = all topics
     PRODUCE: [("transactional_id", NSTR), ("acks", I16), ("timeout", I32),
               ("topics", A([("name", STR), ("partitions", A([("partition", I32), ("records", NBYTES)]))]))],
@@ -71,6 +75,8 @@ REQ = {
 
 RESP = {
     API_VERSIONS: [("error", I16), ("apis", A([("key", I16), ("min", I16), ("max", I16)]))],
+    SASL_HANDSHAKE: [("error", I16), ("mechanisms", A(STR))],
+    SASL_AUTHENTICATE: [("error", I16), ("error_message", NSTR), ("auth_bytes", BYTES)],
     METADATA: [("brokers", A([("node_id", I32), ("host", STR), ("port", I32), ("rack", NSTR)])),
                ("controller_id", I32),
                ("topics", A([("error", I16), ("name", STR), ("internal", BOOL),
@@ -302,8 +308,9 @@ def partition_for_key(key: bytes, num_partitions: int) -> int:
 
 # ---------------------------------------------------------------- record batches (v2)
 def encode_batch(base_offset: int, records: List[Tuple[Optional[bytes], Optional[bytes], List[Tuple[str, bytes]],
-                                                         int]]) -> bytes:
-    """records: (key, value, headers, timestamp_ms)."""
+                                                         int]], codec: int = 0) -> bytes:
+    """records: (key, value, headers, timestamp_ms); codec: attributes compression bits
+    (topics/kafka/codecs.py) applied to the records section."""
     first_ts = records[0][3] if records else 0
     max_ts = max((r[3] for r in records), default=0)
     body = bytearray()
@@ -325,7 +332,11 @@ def encode_batch(base_offset: int, records: List[Tuple[Optional[bytes], Optional
             else:
                 rec += zigzag_varint(len(hv)) + hv
         body += zigzag_varint(len(rec)) + rec
-    tail = struct.pack(">hiqqqhii", 0, len(records) - 1, first_ts, max_ts, -1, -1, -1, len(records)) + bytes(body)
+    if codec:
+        from . import codecs
+        body = codecs.compress(codec, bytes(body))
+    tail = struct.pack(">hiqqqhii", codec & 0x07, len(records) - 1, first_ts, max_ts, -1, -1, -1,
+                       len(records)) + bytes(body)
     crc = crc32c(tail)
     head = struct.pack(">ib", -1, 2) + struct.pack(">I", crc)  # partitionLeaderEpoch, magic, crc
     batch_len = len(head) + len(tail)
@@ -350,29 +361,38 @@ def decode_batches(data: Optional[bytes], verify_crc: bool = False):
         if verify_crc and crc32c(data[pos + 21: end]) != crc:
             raise ValueError("record batch CRC mismatch")
         attrs, _lod, first_ts, _max_ts, _pid, _pe, _bs, count = struct.unpack_from(">hiqqqhii", data, pos + 21)
-        if attrs & 0x07:
-            raise ValueError("compressed record batches are not supported")
         p = pos + 21 + 2 + 4 + 8 + 8 + 8 + 2 + 4 + 4
-        for _ in range(count):
-            _ln, p = read_varint(data, p)
-            p += 1  # attributes
-            tsd, p = read_varint(data, p)
-            od, p = read_varint(data, p)
-            kl, p = read_varint(data, p)
-            key = None if kl < 0 else bytes(data[p: p + kl])
-            p += max(kl, 0)
-            vl, p = read_varint(data, p)
-            val = None if vl < 0 else bytes(data[p: p + vl])
-            p += max(vl, 0)
-            nh, p = read_varint(data, p)
-            hs = []
-            for _h in range(nh):
-                hkl, p = read_varint(data, p)
-                hk = bytes(data[p: p + hkl]).decode()
-                p += hkl
-                hvl, p = read_varint(data, p)
-                hv = None if hvl < 0 else bytes(data[p: p + hvl])
-                p += max(hvl, 0)
-                hs.append((hk, hv))
-            yield base + od, first_ts + tsd, key, val, hs
+        if attrs & 0x07:   # compressed records section: decode it, then parse the records from it
+            from . import codecs
+            rdata = codecs.decompress(attrs & 0x07, bytes(data[p:end]))
+            yield from _records(rdata, 0, count, base, first_ts)
+            pos = end
+            continue
+        yield from _records(data, p, count, base, first_ts)
         pos = end
+
+
+def _records(data, p: int, count: int, base: int, first_ts: int):
+    """Records of one (decompressed) batch starting at byte ``p``."""
+    for _ in range(count):
+        _ln, p = read_varint(data, p)
+        p += 1  # attributes
+        tsd, p = read_varint(data, p)
+        od, p = read_varint(data, p)
+        kl, p = read_varint(data, p)
+        key = None if kl < 0 else bytes(data[p: p + kl])
+        p += max(kl, 0)
+        vl, p = read_varint(data, p)
+        val = None if vl < 0 else bytes(data[p: p + vl])
+        p += max(vl, 0)
+        nh, p = read_varint(data, p)
+        hs = []
+        for _h in range(nh):
+            hkl, p = read_varint(data, p)
+            hk = bytes(data[p: p + hkl]).decode()
+            p += hkl
+            hvl, p = read_varint(data, p)
+            hv = None if hvl < 0 else bytes(data[p: p + hvl])
+            p += max(hvl, 0)
+            hs.append((hk, hv))
+        yield base + od, first_ts + tsd, key, val, hs
