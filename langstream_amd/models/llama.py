@@ -126,13 +126,24 @@ class AttnMeta:
     tiles: Optional[torch.Tensor] = None           # [ntiles, 2] int32
 
 
+def tp_kv_heads(num_kv_heads: int, world: int) -> int:
+    """KV heads per TP rank.  With more ranks than KV heads every KV head is REPLICATED on
+    world / num_kv_heads consecutive ranks (each rank keeps the one KV head its query
+    heads attend to), so e.g. an 8-KV-head model still shards over TP=16."""
+    if num_kv_heads % world == 0:
+        return num_kv_heads // world
+    if world % num_kv_heads == 0:
+        return 1
+    raise ValueError(f"TP degree {world} must divide or be a multiple of the {num_kv_heads} KV heads")
+
+
 class LlamaLayer:
     def __init__(self, cfg: LlamaConfig, tp: TPInfo, device, dtype):
         H, D = cfg.hidden_size, cfg.head_dim
-        assert cfg.num_heads % tp.world == 0 and cfg.num_kv_heads % tp.world == 0, "TP must divide heads"
+        assert cfg.num_heads % tp.world == 0, "TP must divide the query heads"
         assert cfg.intermediate_size % tp.world == 0
         self.hq = cfg.num_heads // tp.world
-        self.hkv = cfg.num_kv_heads // tp.world
+        self.hkv = tp_kv_heads(cfg.num_kv_heads, tp.world)
         self.f = cfg.intermediate_size // tp.world
         std = 0.02
         mk = lambda *s: (torch.randn(*s, device=device, dtype=torch.float32) * std).to(dtype)  # noqa: E731
@@ -169,7 +180,7 @@ class LlamaModel:
             self.lm_head = self.embed if cfg.tie_embeddings else (
                 torch.randn(self.vocab_per_rank, H, device=self.device) * 0.02).to(dtype)
         self.hq = cfg.num_heads // self.tp.world
-        self.hkv = cfg.num_kv_heads // self.tp.world
+        self.hkv = tp_kv_heads(cfg.num_kv_heads, self.tp.world)
         self.cos_sin = ref.rope_cos_sin(cfg.max_position, cfg.head_dim, cfg.rope_theta, cfg.rope_scaling,
                                         device=self.device)
         self.scale = 1.0 / math.sqrt(cfg.head_dim)

@@ -103,16 +103,19 @@ def shard_llama(sd: Dict[str, torch.Tensor], cfg: LlamaConfig, rank: int, world:
     (padded to a multiple of ``world``), replicated norms."""
     if world == 1:
         return dict(sd)
+    from .llama import tp_kv_heads
     D = cfg.head_dim
-    hq, hkv, f = cfg.num_heads // world, cfg.num_kv_heads // world, cfg.intermediate_size // world
+    hq, hkv, f = cfg.num_heads // world, tp_kv_heads(cfg.num_kv_heads, world), cfg.intermediate_size // world
+    # first KV head of this rank (replicated heads when world > num_kv_heads)
+    kv0 = rank * hkv if cfg.num_kv_heads >= world else rank // (world // cfg.num_kv_heads)
     Hq, Hkv, F = cfg.num_heads * D, cfg.num_kv_heads * D, cfg.intermediate_size
     vpr = (cfg.vocab_size + world - 1) // world
     out = {}
     for k, v in sd.items():
         if k.endswith(".qkv_w"):
             q, kk, vv = v[:Hq], v[Hq: Hq + Hkv], v[Hq + Hkv:]
-            out[k] = torch.cat([q[rank * hq * D:(rank + 1) * hq * D], kk[rank * hkv * D:(rank + 1) * hkv * D],
-                                vv[rank * hkv * D:(rank + 1) * hkv * D]], 0)
+            out[k] = torch.cat([q[rank * hq * D:(rank + 1) * hq * D], kk[kv0 * D:(kv0 + hkv) * D],
+                                vv[kv0 * D:(kv0 + hkv) * D]], 0)
         elif k.endswith(".o_w"):
             out[k] = v[:, rank * hq * D:(rank + 1) * hq * D]
         elif k.endswith(".gate_up_w"):

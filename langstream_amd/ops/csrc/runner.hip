@@ -137,9 +137,10 @@ class LlamaRunner {
     // Decode-sized steps use the hand-written skinny MFMA GEMM (ops/csrc/gemm_skinny.hip)
     // where it measured faster than hipBLASLt on MI355X (profiles/skinny_gemm_v2.log):
     // qkv at T <= 32, o_proj at T <= 192 and down_proj at 48 <= T <= 256, the last two
-    // with the residual add + RMSNorm fused into the split-K reduction (TP=1 only: under
-    // TP the all-reduce sits between the GEMM and the residual add).
-    const bool sk = skinny_enabled() && !pg_;
+    // with the residual add + RMSNorm fused into the split-K reduction at TP=1; under TP
+    // the row-parallel partial sums are all-reduced first, so o/down store the plain
+    // GEMM and the residual add + RMSNorm runs after the all-reduce.
+    const bool sk = skinny_enabled();
     // T <= 4 (single-stream / low-concurrency chat): the register-streaming GEMV
     // (ops/csrc/gemm_gemv.hip) for all four projections, gate_up with silu*up fused; it
     // fuses no residual, so it also serves tensor-parallel ranks.
@@ -219,7 +220,13 @@ class LlamaRunner {
         fused_add_rmsnorm(o, residual, post_norm_[l], eps_);
       } else if (sk && T <= 192 && skinny_shape(o_w_[l])) {
         o = at::empty_like(residual);
-        skinny_gemm_add_rmsnorm(o, attn, o_w_[l], residual, post_norm_[l], eps_);
+        if (!pg_) {
+          skinny_gemm_add_rmsnorm(o, attn, o_w_[l], residual, post_norm_[l], eps_);
+        } else {
+          skinny_gemm(o, attn, o_w_[l]);
+          all_reduce(o);
+          fused_add_rmsnorm(o, residual, post_norm_[l], eps_);
+        }
       } else {
         o = at::linear(attn, o_w_[l]);
         all_reduce(o);
@@ -243,7 +250,13 @@ class LlamaRunner {
         fused_add_rmsnorm(dn, residual, nxt, eps_);
       } else if (sk && T >= 48 && T <= 256 && skinny_shape(down_w_[l])) {
         dn = at::empty_like(residual);
-        skinny_gemm_add_rmsnorm(dn, a, down_w_[l], residual, nxt, eps_);
+        if (!pg_) {
+          skinny_gemm_add_rmsnorm(dn, a, down_w_[l], residual, nxt, eps_);
+        } else {
+          skinny_gemm(dn, a, down_w_[l]);
+          all_reduce(dn);
+          fused_add_rmsnorm(dn, residual, nxt, eps_);
+        }
       } else {
         dn = at::linear(a, down_w_[l]);
         all_reduce(dn);

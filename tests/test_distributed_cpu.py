@@ -104,6 +104,55 @@ def test_tensor_parallel_matches_single():
     assert _spawn(_tp_worker) == _single_run()
 
 
+SMALL_PROMPTS = [list(range(3, 3 + n)) for n in (7, 70)]
+
+
+def _small_full():
+    from langstream_amd.models.llama import LlamaModel, PRESETS
+    return LlamaModel(PRESETS["llama-small"], device="cpu", dtype=torch.float32, seed=9)
+
+
+def _small_run(model):
+    from langstream_amd.engine.llm_engine import LLMEngine, SamplingParams
+    eng = LLMEngine(model, None, num_blocks=32, max_model_len=512)
+    sp = SamplingParams(max_tokens=4, temperature=0.0, ignore_eos=True, logprobs=2)
+    res = [(r.output_ids, r.output_logprobs) for r in eng.generate(SMALL_PROMPTS, sp)]
+    return eng, res
+
+
+def _tp_small_worker(rank, world, port, q):
+    """llama-small sharded TP=world (KV heads replicated when world > 2); rank 0 reports
+    tokens + logprobs."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from langstream_amd.models.llama import LlamaModel, PRESETS, TPInfo
+        from langstream_amd.models.loader import shard_llama
+        cfg = PRESETS["llama-small"]
+        m = LlamaModel(cfg, device="cpu", dtype=torch.float32, tp=TPInfo(rank, world, None))
+        m.load_state_dict(shard_llama(_small_full().state_dict(), cfg, rank, world))
+        if rank == 0:
+            eng, res = _small_run(m)
+            eng.stop()
+            q.put(res)
+        else:
+            from langstream_amd.engine.llm_engine import LLMEngine
+            LLMEngine(m, None, num_blocks=32, max_model_len=512).worker_loop()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_tp_llama_small_logprobs_match_tp1(world):
+    """TP=2 and TP=4 (2 KV heads -> replicated at TP=4) greedy tokens and their logprobs
+    equal the TP=1 engine on the same full weights."""
+    _, ref_res = _small_run(_small_full())
+    got = _spawn(_tp_small_worker, world)
+    for (ids_a, lp_a), (ids_b, lp_b) in zip(got, ref_res):
+        assert ids_a == ids_b
+        assert max(abs(a - b) for a, b in zip(lp_a, lp_b)) < 1e-3
+
+
 def test_data_parallel_replicas_match_single():
     assert _spawn(_dp_worker) == _single_run()
 

@@ -517,3 +517,41 @@ def test_bert_fused_layers_match_plain_fp32():
         os.environ.pop("LS_BERT_FUSED", None)
     cos = torch.nn.functional.cosine_similarity(eg.cpu(), ec, dim=-1)
     assert cos.min() > 0.995, cos
+
+
+# Llama-3-70B at TP=8: the per-rank shard shapes the TP decode path runs:
+# qkv 8192 -> 1280, o 1024 -> 8192, gate_up 8192 -> 2x3584, down 3584 -> 8192.
+TP8_SHAPES = [("qkv", 1280, 8192), ("o", 8192, 1024), ("down", 8192, 3584)]
+
+
+@pytest.mark.parametrize("M", [1, 4, 64, 256])
+@pytest.mark.parametrize("name,N,K", TP8_SHAPES)
+def test_tp8_shard_shapes_skinny_and_gemv(M, name, N, K):
+    torch.manual_seed(M + N + K)
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=DEV) / K ** 0.5).to(torch.bfloat16)
+    exp = x.float().cpu() @ w.float().cpu().t()
+    out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    ops.hip().skinny_gemm(out, x, w)
+    _close(out, exp, 0.03, 0.03, f"skinny {name}")
+    if M <= 4 and ops.hip().gemv_supported(w, False):
+        out2 = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+        ops.hip().gemv(out2, x, w)
+        _close(out2, exp, 0.03, 0.03, f"gemv {name}")
+
+
+@pytest.mark.parametrize("M", [1, 3, 64, 256])
+def test_tp8_gate_up_shard_silu(M):
+    F, K = 3584, 8192
+    torch.manual_seed(M)
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(2 * F, K, device=DEV) / K ** 0.5).to(torch.bfloat16)
+    gu = (x.float().cpu() @ w.float().cpu().t()).to(torch.bfloat16).float()
+    exp = torch.nn.functional.silu(gu[:, :F]) * gu[:, F:]
+    out = torch.empty(M, F, device=DEV, dtype=torch.bfloat16)
+    ops.hip().skinny_gemm_silu(out, x, w)
+    _close(out, exp, 0.03, 0.03, "skinny silu")
+    if M <= 4 and ops.hip().gemv_supported(w, True):
+        out2 = torch.empty(M, F, device=DEV, dtype=torch.bfloat16)
+        ops.hip().gemv_silu(out2, x, w)
+        _close(out2, exp, 0.03, 0.03, "gemv silu")
