@@ -14,6 +14,7 @@ from __future__ import annotations
 import json
 import logging
 import threading
+import urllib.parse
 import uuid
 from concurrent.futures import Future
 from dataclasses import dataclass, field
@@ -322,6 +323,150 @@ class HuggingFaceAPIService(EmbeddingsService, CompletionsService):
     def compute_embeddings(self, texts):
         headers = {"Authorization": f"Bearer {self.cfg.get('access-key', '')}"}
         return _run_async(lambda: _http_json(f"{self.url}/{self.model}", {"inputs": texts}, headers))
+
+
+class VertexAIService(CompletionsService, EmbeddingsService):
+    """Vertex AI ``:predict`` REST (VertexAIProvider.java:59-500): chat = instances
+    [{context, examples, messages[{author, content}]}] -> predictions[0].candidates[0];
+    text = instances[{prompt}] (one prompt) -> predictions[0].content; embeddings =
+    instances[{content}] -> predictions[i].embeddings.values.  Parameters temperature,
+    max-tokens -> maxOutputTokens, topP, topK.  Auth: static ``token`` or an OAuth2 token
+    minted from ``serviceAccountJson``."""
+
+    def __init__(self, cfg: Dict[str, Any], model: Optional[str] = None):
+        self.cfg = cfg
+        self.model = model
+        self.project = cfg.get("project")
+        self.region = cfg.get("region") or "us-central1"
+        self.url = (cfg.get("url") or f"https://{self.region}-aiplatform.googleapis.com").rstrip("/")
+        tok = (cfg.get("token") or "").strip()
+        sa = (cfg.get("serviceAccountJson") or "").strip()
+        self._static = tok or None
+        self._sa = None
+        if not tok and sa:
+            from ...utils.cloudauth import GoogleServiceAccount
+            self._sa = GoogleServiceAccount(sa)
+        if not tok and not sa:
+            raise ValueError("vertex: either token or serviceAccountJson is required")
+
+    def _headers(self):
+        return {"Authorization": f"Bearer {self._static or self._sa.token()}"}
+
+    def _predict(self, model: str, body: dict) -> dict:
+        url = f"{self.url}/v1/projects/{self.project}/locations/{self.region}/publishers/google/models/{model}:predict"
+        return _http_json(url, body, self._headers())
+
+    @staticmethod
+    def _params(options: Dict[str, Any]) -> Dict[str, Any]:
+        out = {}
+        for src, dst, cast in (("temperature", "temperature", float), ("max-tokens", "maxOutputTokens", int),
+                               ("topP", "topP", float), ("topK", "topK", int)):
+            if options.get(src) is not None:
+                out[dst] = cast(options[src])
+        return out
+
+    def compute_embeddings(self, texts):
+        model = self.model or "textembedding-gecko"
+        return _run_async(lambda: [p["embeddings"]["values"] for p in self._predict(
+            model, {"instances": [{"content": t} for t in texts]})["predictions"]])
+
+    def get_chat_completions(self, messages, consumer, options):
+        model = options.get("model") or self.model
+
+        def run():
+            body = {"instances": [{"context": "", "examples": [],
+                                   "messages": [{"author": m.role, "content": m.content} for m in messages]}],
+                    "parameters": self._params(options)}
+            preds = self._predict(model, body)["predictions"]
+            cands = preds[0].get("candidates") or [] if preds else []
+            text = cands[0].get("content", "") if cands else ""
+            aid = f"vertex-{uuid.uuid4().hex[:16]}"
+            if consumer is not None:
+                consumer(aid, 0, text, True)
+            return CompletionResult(text, aid)
+
+        return _run_async(run)
+
+    def get_text_completions(self, prompts, consumer, options):
+        if len(prompts) != 1:
+            raise ValueError("Vertex AI only supports a single prompt for text completions.")
+        model = options.get("model") or self.model
+
+        def run():
+            body = {"instances": [{"prompt": prompts[0]}], "parameters": self._params(options)}
+            text = self._predict(model, body)["predictions"][0].get("content", "")
+            aid = f"vertex-{uuid.uuid4().hex[:16]}"
+            if consumer is not None:
+                consumer(aid, 0, text, True)
+            return CompletionResult(text, aid)
+
+        return _run_async(run)
+
+
+class BedrockService(CompletionsService, EmbeddingsService):
+    """AWS Bedrock runtime ``/model/{modelId}/invoke`` with SigV4 (BedrockServiceProvider.java,
+    bedrock/BedrockClient.java): embeddings = one Titan call per text ({"inputText"} ->
+    {"embedding"}); completions = one prompt, body {request-prompt-property: prompt,
+    **request-parameters} from ``options``, the answer = the EL expression
+    ``response-completions-expression`` evaluated over the JSON response (a leading
+    newline stripped); chat joins the message contents as the prompt list."""
+
+    def __init__(self, cfg: Dict[str, Any], model: Optional[str] = None):
+        self.cfg = cfg
+        self.model = model
+        self.region = cfg.get("region") or "us-east-1"
+        self.ak, self.sk = cfg.get("access-key"), cfg.get("secret-key")
+        if not self.ak or not self.sk:
+            raise ValueError("bedrock: access-key and secret-key are required")
+        self.url = (cfg.get("endpoint-override") or cfg.get("url")
+                    or f"https://bedrock-runtime.{self.region}.amazonaws.com").rstrip("/")
+
+    def _invoke(self, model: str, body: dict) -> dict:
+        import requests
+        url = f"{self.url}/model/{urllib.parse.quote(model, safe='')}/invoke"
+        data = json.dumps(body).encode()
+        from ...utils.cloudauth import sigv4_headers
+        headers = sigv4_headers("POST", url, self.region, "bedrock", self.ak, self.sk, data,
+                                {"content-type": "application/json", "accept": "application/json"},
+                                session_token=self.cfg.get("session-token"))
+        r = requests.post(url, data=data, headers=headers, timeout=120)
+        if r.status_code != 200:
+            raise RuntimeError(f"bedrock invoke {model}: HTTP {r.status_code} {r.text[:300]}")
+        return r.json()
+
+    def compute_embeddings(self, texts):
+        model = self.model or "amazon.titan-embed-text-v1"
+        return _run_async(lambda: [self._invoke(model, {"inputText": t})["embedding"] for t in texts])
+
+    def get_text_completions(self, prompts, consumer, options):
+        if len(prompts) != 1:
+            raise ValueError("Bedrock models only support a single prompt for completions.")
+        model = options.get("model") or self.model
+        bo = options.get("options") or {}
+        expr = bo.get("response-completions-expression")
+        if not expr:
+            raise ValueError("bedrock: options.response-completions-expression is required")
+
+        def run():
+            from .el import eval_expression
+            body = {bo.get("request-prompt-property", "prompt"): prompts[0]}
+            body.update(bo.get("request-parameters") or {})
+            resp = self._invoke(model, body)
+            val = eval_expression(expr, dict(resp))
+            if val is None:
+                raise RuntimeError(f"No result found in response (tried with expression {expr}, response was: {resp})")
+            text = str(val)
+            if text.startswith("\n"):
+                text = text[1:]
+            aid = f"bedrock-{uuid.uuid4().hex[:16]}"
+            if consumer is not None:
+                consumer(aid, 0, text, True)
+            return CompletionResult(text, aid)
+
+        return _run_async(run)
+
+    def get_chat_completions(self, messages, consumer, options):
+        return self.get_text_completions(["\n".join(m.content for m in messages)], consumer, options)
 
 
 class UnavailableService(CompletionsService, EmbeddingsService):

@@ -1,0 +1,186 @@
+"""Vertex AI and AWS Bedrock providers against recording fake servers.
+
+* SigV4: checked against the AWS documentation example (IAM ListUsers, 20150830T123600Z)
+  and re-verified server-side for every Bedrock call.
+* Vertex: static token and service-account JSON (an RSA key made with the openssl CLI;
+  the fake token endpoint verifies the RS256 assertion with the public key) -> Bearer.
+"""
+import datetime as dt
+import hashlib
+import http.server
+import json
+import shutil
+import subprocess
+import threading
+import urllib.parse
+
+import pytest
+
+from langstream_amd.agents.genai.services import BedrockService, ChatMessage, VertexAIService
+from langstream_amd.utils.cloudauth import rsa_private_key_from_pem, rsa_sign_sha256, sigv4_headers
+
+
+def test_sigv4_matches_aws_documented_example():
+    h = sigv4_headers("GET", "https://iam.amazonaws.com/?Action=ListUsers&Version=2010-05-08", "us-east-1", "iam",
+                      "AKIDEXAMPLE", "wJalrXUtnFEMI/K7MDENG+bPxRfiCYEXAMPLEKEY", b"",
+                      {"Content-Type": "application/x-www-form-urlencoded; charset=utf-8"},
+                      now=dt.datetime(2015, 8, 30, 12, 36, 0, tzinfo=dt.timezone.utc))
+    assert h["Authorization"].endswith("Signature=5d672d79c15b13162d9279b0855cfba6789a8edb4c82c400e06b5924a6f2b5d7")
+
+
+class _Fake:
+    def __init__(self, handler):
+        fake = self
+        self.calls = []
+
+        class H(http.server.BaseHTTPRequestHandler):
+            def log_message(self, *a):
+                pass
+
+            def do_POST(self):
+                n = int(self.headers.get("Content-Length", 0))
+                body = self.rfile.read(n)
+                fake.calls.append((self.path, dict(self.headers), body))
+                code, out = handler(self.path, self.headers, body)
+                data = json.dumps(out).encode()
+                self.send_response(code)
+                self.send_header("Content-Type", "application/json")
+                self.send_header("Content-Length", str(len(data)))
+                self.end_headers()
+                self.wfile.write(data)
+
+        self.srv = http.server.ThreadingHTTPServer(("127.0.0.1", 0), H)
+        self.url = f"http://127.0.0.1:{self.srv.server_address[1]}"
+        threading.Thread(target=self.srv.serve_forever, daemon=True).start()
+
+    def close(self):
+        self.srv.shutdown()
+
+
+def _vertex_handler(path, headers, body):
+    req = json.loads(body)
+    if path.endswith("/models/textembedding-gecko:predict"):
+        return 200, {"predictions": [{"embeddings": {"values": [float(len(i["content"])), 1.0]}}
+                                     for i in req["instances"]]}
+    if path.endswith("/models/chat-bison:predict"):
+        msgs = req["instances"][0]["messages"]
+        return 200, {"predictions": [{"candidates": [{"author": "bot", "content":
+                                                      f"echo:{msgs[-1]['content']}:{req['parameters']}"}]}]}
+    if path.endswith("/models/text-bison:predict"):
+        return 200, {"predictions": [{"content": "text:" + req["instances"][0]["prompt"]}]}
+    return 404, {}
+
+
+def test_vertex_static_token_chat_text_embeddings():
+    fake = _Fake(_vertex_handler)
+    try:
+        cfg = {"url": fake.url, "token": "tok-123", "project": "proj", "region": "us-central1"}
+        emb = VertexAIService(cfg, "textembedding-gecko").compute_embeddings(["ab", "abcd"]).result(10)
+        assert emb == [[2.0, 1.0], [4.0, 1.0]]
+        chunks = []
+        res = VertexAIService(cfg, "chat-bison").get_chat_completions(
+            [ChatMessage("user", "hi")], lambda *a: chunks.append(a),
+            {"temperature": 0.5, "max-tokens": 10}).result(10)
+        assert res.content.startswith("echo:hi:") and "'maxOutputTokens': 10" in res.content and chunks[-1][3]
+        txt = VertexAIService(cfg, "text-bison").get_text_completions(["p1"], None, {}).result(10)
+        assert txt.content == "text:p1"
+        path, headers, _ = fake.calls[0]
+        assert path.startswith("/v1/projects/proj/locations/us-central1/publishers/google/models/")
+        assert headers["Authorization"] == "Bearer tok-123"
+    finally:
+        fake.close()
+
+
+@pytest.mark.skipif(shutil.which("openssl") is None, reason="openssl CLI not available")
+def test_vertex_service_account_oauth(tmp_path):
+    key = tmp_path / "k.pem"
+    subprocess.run(["openssl", "genpkey", "-algorithm", "RSA", "-pkeyopt", "rsa_keygen_bits:2048", "-out", str(key)],
+                   check=True, capture_output=True)
+    pem = key.read_text()
+    pub = subprocess.run(["openssl", "rsa", "-in", str(key), "-noout", "-modulus"], check=True, capture_output=True,
+                         text=True).stdout.strip().split("=", 1)[1]
+    n_pub = int(pub, 16)
+    n, d = rsa_private_key_from_pem(pem)
+    assert n == n_pub
+    assert pow(int.from_bytes(rsa_sign_sha256(n, d, b"m"), "big"), 65537, n).to_bytes(256, "big").endswith(
+        hashlib.sha256(b"m").digest())
+    seen = {}
+
+    def handler(path, headers, body):
+        if path == "/token":
+            form = dict(urllib.parse.parse_qsl(body.decode()))
+            h, c, s = form["assertion"].split(".")
+            import base64
+            pad = lambda x: x + "=" * (-len(x) % 4)  # noqa: E731
+            sig = int.from_bytes(base64.urlsafe_b64decode(pad(s)), "big")
+            em = pow(sig, 65537, n_pub).to_bytes(256, "big")
+            ok = em.endswith(hashlib.sha256(f"{h}.{c}".encode()).digest())
+            seen["claims"] = json.loads(base64.urlsafe_b64decode(pad(c)))
+            return (200, {"access_token": "minted", "expires_in": 3600}) if ok else (401, {})
+        seen["auth"] = headers["Authorization"]
+        return _vertex_handler(path, headers, body)
+
+    fake = _Fake(handler)
+    try:
+        sa = json.dumps({"client_email": "svc@proj.iam.gserviceaccount.com", "private_key": pem,
+                         "private_key_id": "kid1", "token_uri": fake.url + "/token"})
+        cfg = {"url": fake.url, "serviceAccountJson": sa, "project": "proj", "region": "us-central1"}
+        VertexAIService(cfg, "textembedding-gecko").compute_embeddings(["x"]).result(10)
+        assert seen["auth"] == "Bearer minted"
+        assert seen["claims"]["scope"] == "https://www.googleapis.com/auth/cloud-platform"
+    finally:
+        fake.close()
+
+
+def test_bedrock_sigv4_titan_embeddings_and_completions():
+    ak, sk = "AKIDTEST", "secretkeytest"
+
+    def handler(path, headers, body):
+        # re-derive the signature server-side from the received request
+        url = "http://" + headers["Host"] + path
+        exp = sigv4_headers("POST", url, "us-east-1", "bedrock", ak, sk, body,
+                            {"content-type": headers["Content-Type"], "accept": headers["Accept"]},
+                            now=dt.datetime.strptime(headers["X-Amz-Date"], "%Y%m%dT%H%M%SZ").replace(
+                                tzinfo=dt.timezone.utc))
+        if exp["Authorization"] != headers["Authorization"]:
+            return 403, {"message": "signature mismatch"}
+        req = json.loads(body)
+        if path == "/model/amazon.titan-embed-text-v1/invoke":
+            return 200, {"embedding": [len(req["inputText"]), 0.5]}
+        if path.startswith("/model/anthropic.claude-v2/invoke"):
+            return 200, {"completion": "\nanswer to " + req["prompt"], "params": req.get("max_tokens_to_sample")}
+        return 404, {}
+
+    fake = _Fake(handler)
+    try:
+        cfg = {"access-key": ak, "secret-key": sk, "region": "us-east-1", "endpoint-override": fake.url}
+        emb = BedrockService(cfg, "amazon.titan-embed-text-v1").compute_embeddings(["abc", "de"]).result(10)
+        assert emb == [[3, 0.5], [2, 0.5]]
+        opts = {"model": "anthropic.claude-v2", "options": {
+            "request-parameters": {"max_tokens_to_sample": 300},
+            "response-completions-expression": "completion"}}
+        res = BedrockService(cfg).get_text_completions(["Human: hi"], None, opts).result(10)
+        assert res.content == "answer to Human: hi"
+        chat = BedrockService(cfg).get_chat_completions([ChatMessage("user", "yo")], None, opts).result(10)
+        assert chat.content == "answer to yo"
+    finally:
+        fake.close()
+
+
+def test_local_ai_routes_hosted_model_names_to_local_engines(monkeypatch):
+    from langstream_amd.agents.genai import services as s
+    from langstream_amd.services import ServiceRegistry, _norm_model
+    assert _norm_model("gpt-3.5-turbo") == "llama-3-8b"
+    assert _norm_model("text-embedding-ada-002") == "bge-small-en"
+    reg = ServiceRegistry({"local-ai": True, "device": "cpu", "chat-model": "llama-tiny",
+                           "embeddings-model": "bert-tiny", "force-chat-model": "llama-tiny",
+                           "force-embeddings-model": "bert-tiny", "use-graphs": "false", "num-blocks": 16,
+                           "max-model-len": 256})
+    try:
+        svc = reg.embeddings_service({"openai": {"access-key": "", "provider": "openai"}}, "text-embedding-ada-002")
+        assert isinstance(svc, s.LocalEmbeddingsService)
+        assert len(svc.compute_embeddings(["hello"]).result(60)[0]) == 128
+        chat = reg.completions_service({"openai": {"access-key": ""}}, "gpt-3.5-turbo")
+        assert isinstance(chat, s.LocalCompletionsService)
+    finally:
+        reg.shutdown()
