@@ -115,11 +115,34 @@ class TopicConnectionsRuntimeRegistry:
     def register(cls, type_: str, factory: Callable[[], TopicConnectionsRuntime]) -> None:
         cls._factories[type_] = factory
 
+    _plugins_loaded = False
+
+    @classmethod
+    def _load_plugins(cls) -> None:
+        """Streaming runtimes of installed bundles: entry-point group ``langstream_amd.topics``
+        (the reference's META-INF/ai.langstream.streamingClusters.index)."""
+        if cls._plugins_loaded:
+            return
+        cls._plugins_loaded = True
+        try:
+            from importlib.metadata import entry_points
+            for ep in entry_points().select(group="langstream_amd.topics"):
+                try:
+                    ep.load()
+                except Exception:  # noqa: BLE001
+                    import logging
+                    logging.getLogger(__name__).exception("failed to load streaming plugin %s", ep.name)
+        except Exception:  # noqa: BLE001
+            pass
+
     @classmethod
     def get(cls, streaming_cluster) -> TopicConnectionsRuntime:
         from .. import topics as _topics  # noqa: F401  (registers built-in runtimes)
         t = streaming_cluster.type if streaming_cluster is not None else "noop"
         f = cls._factories.get(t)
+        if f is None:
+            cls._load_plugins()
+            f = cls._factories.get(t)
         if f is None:
             raise ValueError(f"No TopicConnectionsRuntime found for type {t}; known: {sorted(cls._factories)}")
         rt = f()

@@ -355,7 +355,7 @@ def cmd_pravega_standalone(args) -> int:
 
 def cmd_operator(args) -> int:
     from ..operator import main as operator_main
-    argv = ["--resync", str(args.resync)]
+    argv = ["--resync", str(args.resync)] + (["--in-process"] if args.in_process else [])
     for k in ("api_server", "token", "namespace", "image"):
         v = getattr(args, k)
         if v:
@@ -527,7 +527,16 @@ def build_parser() -> argparse.ArgumentParser:
     opr.add_argument("--namespace", default=None)
     opr.add_argument("--image", default=None)
     opr.add_argument("--resync", type=float, default=5.0)
+    opr.add_argument("--in-process", action="store_true",
+                     help="run application setup / deployer in the operator instead of as Kubernetes Jobs")
     opr.set_defaults(fn=cmd_operator)
+
+    gws = sub.add_parser("gateway-server", help="run the API gateway (WebSocket + HTTP) over an application store")
+    gws.add_argument("--host", default="0.0.0.0")
+    gws.add_argument("--port", type=int, default=8091)
+    gws.add_argument("--store", choices=("kubernetes",), default="kubernetes")
+    gws.add_argument("--api-server", default=None, help="Kubernetes API server (default: in-cluster)")
+    gws.set_defaults(fn=cmd_gateway_server)
 
     dc = sub.add_parser("docs", help="generate the agents / resources / assets configuration reference")
     dc.add_argument("--format", choices=("json", "markdown"), default="json")
@@ -581,6 +590,29 @@ def cmd_control_plane(args) -> int:
     except KeyboardInterrupt:
         pass
     srv.stop()
+    return 0
+
+
+def cmd_gateway_server(args) -> int:
+    """The reference's langstream-api-gateway deployment: gateways of the applications in
+    the Kubernetes application store, topics reached through each app's instance."""
+    import logging
+    import signal
+    logging.basicConfig(level=logging.INFO)
+    from ..gateway.server import GatewayServer, GatewayService
+    from ..operator.kube import KubeClient
+    from ..operator.store import KubernetesApplicationStore
+    gw = GatewayServer(GatewayService(KubernetesApplicationStore(KubeClient(args.api_server))),
+                       host=args.host, port=args.port).start()
+    print(f"api gateway listening on {args.host}:{args.port}", flush=True)
+    stop = threading.Event()
+    signal.signal(signal.SIGTERM, lambda *_: stop.set())
+    try:
+        while not stop.wait(1.0):
+            pass
+    except KeyboardInterrupt:
+        pass
+    gw.stop()
     return 0
 
 

@@ -30,6 +30,7 @@ _BUILTIN_MODULES = (
     "langstream_amd.agents.webcrawler",
     "langstream_amd.agents.storage",
     "langstream_amd.agents.python_agents",
+    "langstream_amd.agents.kafka_connect",
 )
 
 

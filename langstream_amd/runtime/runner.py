@@ -291,7 +291,10 @@ class AgentRunner:
         self._check_fatal()
 
     def _drain(self, timeout: float) -> None:
-        """Wait (bounded) for in-flight records to reach the sink (E4)."""
+        """Wait (bounded) for in-flight records to reach the sink (E4).  A sink that
+        handles its own commits (Kafka Connect) drains on close() instead."""
+        if self.sink is not None and self.sink.handles_commit():
+            return
         deadline = time.time() + timeout
         while self.tracker is not None and self.tracker.pending() > 0 and time.time() < deadline:
             if self._fatal is not None:

@@ -252,3 +252,55 @@ def test_tenant_limits_block_deploy(kube):
     st = client.get(CR_API, "Application", "langstream-t1", "big")["status"]["status"]
     assert "Not enough resources" in st["reason"]
     assert kube.kinds("agents") == []
+
+
+def _run_job(client, kube, job_name, monkeypatch, tmp_path):
+    """Play the Kubernetes Job controller: run the Job's container command in-process
+    against the fake API server, then mark the Job succeeded."""
+    import base64
+    from langstream_amd.runtime import jobs
+    job = client.get("batch/v1", "Job", "langstream-t1", job_name)
+    assert job is not None, job_name
+    c = job["spec"]["template"]["spec"]["containers"][0]
+    assert c["command"][:3] == ["python", "-m", "langstream_amd.runtime.jobs"]
+    secret = job["spec"]["template"]["spec"]["volumes"][0]["secret"]["secretName"]
+    cfg = base64.b64decode(client.get("v1", "Secret", "langstream-t1", secret)["data"]["config"]).decode()
+    path = tmp_path / f"{job_name}.json"
+    path.write_text(cfg)
+    monkeypatch.setenv("LANGSTREAM_JOB_PHASE", c["env"][0]["value"])
+    monkeypatch.setenv("LANGSTREAM_KUBE_API", kube.url)
+    assert jobs.main([c["command"][3], str(path)]) == 0
+    client.merge_patch("batch/v1", "Job", "langstream-t1", job_name, {"status": {"succeeded": 1}}, "status")
+
+
+def test_operator_runs_setup_and_deployer_as_jobs(kube, monkeypatch, tmp_path):
+    client = KubeClient(kube.url)
+    store = KubernetesApplicationStore(client)
+    store.put_tenant("t1")
+    store.put(_stored("app2", {"pipeline.yaml": PIPE}))
+    op = Operator(client, use_jobs=True)
+    assert op.reconcile_all()["app/langstream-t1/app2"] == "DEPLOYING"
+    assert kube.kinds("jobs") == ["langstream-runtime-setup-app2-1"] and kube.kinds("agents") == []
+    assert op.reconcile_all()["app/langstream-t1/app2"] == "DEPLOYING"       # job still running
+    _run_job(client, kube, "langstream-runtime-setup-app2-1", monkeypatch, tmp_path)
+    assert op.reconcile_all()["app/langstream-t1/app2"] == "DEPLOYING"
+    assert "langstream-runtime-deployer-app2-1" in kube.kinds("jobs")
+    _run_job(client, kube, "langstream-runtime-deployer-app2-1", monkeypatch, tmp_path)
+    assert kube.kinds("agents") == ["app2-step1", "app2-step2"]                # created by the deployer job
+    assert op.reconcile_all()["app/langstream-t1/app2"] == "DEPLOYED"
+    assert store.get("t1", "app2").status == "DEPLOYED"
+    # a failed setup job of a new revision -> ERROR_SETUP
+    store.put(_stored("app2", {"pipeline.yaml": PIPE.replace("parallelism: 2", "parallelism: 1")}))
+    assert op.reconcile_all()["app/langstream-t1/app2"] == "DEPLOYING"
+    client.merge_patch("batch/v1", "Job", "langstream-t1", "langstream-runtime-setup-app2-2",
+                       {"status": {"failed": 2}}, "status")
+    assert op.reconcile_all()["app/langstream-t1/app2"] == "ERROR_SETUP"
+    # deletion: deployer-cleanup job, then setup-cleanup job, then the CR goes
+    assert store.delete("t1", "app2")
+    assert op.reconcile_all()["app/langstream-t1/app2"] == "DELETING"
+    _run_job(client, kube, "langstream-runtime-deployer-cleanup-app2-2", monkeypatch, tmp_path)
+    assert kube.kinds("agents") == []
+    assert op.reconcile_all()["app/langstream-t1/app2"] == "DELETING"
+    _run_job(client, kube, "langstream-runtime-setup-cleanup-app2-2", monkeypatch, tmp_path)
+    op.reconcile_all()
+    assert kube.kinds("applications") == []
