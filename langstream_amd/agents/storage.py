@@ -28,6 +28,7 @@ import datetime as _dt
 import hashlib
 import hmac
 import logging
+import json
 import os
 import queue
 import threading
@@ -315,9 +316,9 @@ class CamelSource(AgentSource):
         path, _, qs = rest.partition("?")
         self.path = path.lstrip("/") if scheme == "timer" else path
         self.params = dict(urllib.parse.parse_qsl(qs))
-        if scheme not in ("file", "timer"):
+        if scheme not in CAMEL_COMPONENTS:
             raise ValueError(f"camel-source: component '{scheme}' is not supported natively "
-                             f"(supported: file:, timer:)")
+                             f"(supported: {', '.join(sorted(CAMEL_COMPONENTS))})")
         self._stop = threading.Event()
         self._inflight: Set[str] = set()
 
@@ -341,7 +342,14 @@ class CamelSource(AgentSource):
                 continue
 
     def _run(self) -> None:
-        if self.scheme == "timer":
+        if self.scheme in ("github", "kafka"):
+            try:
+                CAMEL_COMPONENTS[self.scheme](self)
+            except Exception as e:  # noqa: BLE001
+                log.exception("camel %s consumer failed", self.scheme)
+                self._error = e
+            return
+        if self.scheme in ("timer", "scheduler"):
             period = float(self.params.get("period", 1000)) / 1000.0
             repeat = int(self.params.get("repeatCount", 0))
             n = 0
@@ -370,6 +378,9 @@ class CamelSource(AgentSource):
             self._stop.wait(delay)
 
     def read(self) -> List[Record]:
+        err = getattr(self, "_error", None)
+        if err is not None:
+            raise err
         try:
             r = self.q.get(timeout=1.0)
         except queue.Empty:
@@ -400,3 +411,72 @@ class CamelSource(AgentSource):
 
     def build_additional_info(self):
         return {"component-uri": self.uri}
+
+
+def _camel_github(src: "CamelSource") -> None:
+    """camel-github consumer: ``github:<type>[/<branch>]?repoOwner=&repoName=&oauthToken=``
+    with type PULLREQUESTCOMMENT | PULLREQUEST | COMMIT | TAG | EVENT; polls the GitHub REST
+    API every ``delay`` ms (default 5000) and emits each NEW item once (the first poll only
+    records what exists, as the Camel consumer does).  ``apiUrl`` overrides the API base."""
+    import requests
+    typ, _, branch = src.path.partition("/")
+    typ = typ.upper()
+    p = src.params
+    owner, repo = p.get("repoOwner"), p.get("repoName")
+    if not owner or not repo:
+        raise ValueError("camel github: repoOwner and repoName are required")
+    base = p.get("apiUrl", "https://api.github.com").rstrip("/")
+    paths = {"PULLREQUESTCOMMENT": f"/repos/{owner}/{repo}/pulls/comments",
+             "PULLREQUEST": f"/repos/{owner}/{repo}/pulls", "COMMIT": f"/repos/{owner}/{repo}/commits",
+             "TAG": f"/repos/{owner}/{repo}/tags", "EVENT": f"/repos/{owner}/{repo}/events"}
+    if typ not in paths:
+        raise ValueError(f"camel github: unsupported type {typ}; known: {sorted(paths)}")
+    params = {"sha": branch or p.get("branch")} if typ == "COMMIT" and (branch or p.get("branch")) else {}
+    headers = {"Accept": "application/vnd.github+json"}
+    if p.get("oauthToken"):
+        headers["Authorization"] = f"Bearer {p['oauthToken']}"
+    delay = float(p.get("delay", 5000)) / 1000.0
+    seen: Set[str] = set()
+    first = True
+    while not src._stop.is_set():
+        r = requests.get(base + paths[typ], params=params, headers=headers, timeout=30)
+        r.raise_for_status()
+        for item in reversed(r.json()):     # oldest first
+            ident = str(item.get("id") or item.get("sha") or item.get("name") or json.dumps(item, sort_keys=True))
+            if ident in seen:
+                continue
+            seen.add(ident)
+            if not first:
+                src._emit(ident, json.dumps(item), {"GitHubType": typ, "GitHubId": ident})
+        first = False
+        src._stop.wait(delay)
+
+
+def _camel_kafka(src: "CamelSource") -> None:
+    """camel-kafka consumer: ``kafka:<topic>?brokers=host:port[&groupId=..]`` through the
+    in-tree Kafka client (consumer group, earliest reset, commit after emission)."""
+    from ..topics.kafka.client import GroupConsumer, KafkaClient
+    brokers = src.params.get("brokers")
+    if not brokers:
+        raise ValueError("camel kafka: brokers is required")
+    client = KafkaClient(brokers, client_id="camel-kafka")
+    c = GroupConsumer(client, src.path, src.params.get("groupId", "camel-" + src.path),
+                      src.params.get("autoOffsetReset", "earliest"))
+    c.start()
+    try:
+        while not src._stop.is_set():
+            recs = c.poll(500)
+            for part, off, ts, k, v, hs in recs:
+                key = k.decode("utf-8", "replace") if isinstance(k, bytes) else k
+                src._emit(key, v, {"kafka.TOPIC": src.path, "kafka.PARTITION": part, "kafka.OFFSET": off,
+                                   **{hk: (hv.decode("utf-8", "replace") if isinstance(hv, bytes) else hv)
+                                      for hk, hv in hs}})
+            if recs:
+                c.commit([(p_, o_) for p_, o_, *_ in recs])
+    finally:
+        c.close()
+        client.close()
+
+
+# Camel component URI schemes this runtime implements natively; register more here.
+CAMEL_COMPONENTS = {"file": None, "timer": None, "scheduler": None, "github": _camel_github, "kafka": _camel_kafka}

@@ -232,4 +232,47 @@ def test_camel_file_and_timer(tmp_path):
     assert [r.header_value("CamelTimerCounter") for r in got] == [1, 2, 3]
     t.close()
     with pytest.raises(ValueError):
-        create_agent("camel-source").init({"component-uri": "kafka:topic"})
+        create_agent("camel-source").init({"component-uri": "ftp:host/dir"})
+
+
+def test_camel_github_pull_request_comments():
+    """camel-github consumer (the reference's examples/applications/camel-source shape):
+    items present at the first poll are skipped, later ones are emitted once."""
+    import http.server
+    import json as _json
+    state = {"items": [{"id": 1, "body": "old"}]}
+
+    class H(http.server.BaseHTTPRequestHandler):
+        def log_message(self, *a):
+            pass
+
+        def do_GET(self):
+            assert self.path.startswith("/repos/acme/widgets/pulls/comments")
+            assert self.headers["Authorization"] == "Bearer t0k"
+            body = _json.dumps(list(reversed(state["items"]))).encode()   # newest first, as GitHub
+            self.send_response(200)
+            self.send_header("Content-Type", "application/json")
+            self.send_header("Content-Length", str(len(body)))
+            self.end_headers()
+            self.wfile.write(body)
+
+    srv = http.server.ThreadingHTTPServer(("127.0.0.1", 0), H)
+    threading.Thread(target=srv.serve_forever, daemon=True).start()
+    try:
+        a = create_agent("camel-source")
+        a.set_metadata("gh", "camel-source", 0)
+        a.init({"component-uri": "github:PULLREQUESTCOMMENT/main",
+                "component-options": {"repoOwner": "acme", "repoName": "widgets", "oauthToken": "t0k",
+                                      "delay": 50, "apiUrl": f"http://127.0.0.1:{srv.server_address[1]}"}})
+        a.start()
+        time.sleep(0.3)
+        state["items"] = state["items"] + [{"id": 2, "body": "new one"}, {"id": 3, "body": "newer"}]
+        got = []
+        deadline = time.time() + 5
+        while len(got) < 2 and time.time() < deadline:
+            got += a.read()
+        assert [_json.loads(r.value())["body"] for r in got] == ["new one", "newer"]
+        assert got[0].header_value("GitHubType") == "PULLREQUESTCOMMENT"
+        a.close()
+    finally:
+        srv.shutdown()
