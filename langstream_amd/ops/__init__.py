@@ -341,8 +341,10 @@ def l2_normalize_rows(x):
     return torch.nn.functional.normalize(x.float(), dim=-1, eps=1e-12).to(x.dtype)
 
 
-def knn_topk(X, Q, k: int):
-    """Top-k rows of X by dot product with each query row.  Returns (scores f32 [Q,k], idx int32 [Q,k])."""
+def knn_topk(X, Q, k: int, sample_chunks: int = 32):
+    """Top-k rows of X by dot product with each query row.  Returns (scores f32 [Q,k], idx int32 [Q,k]).
+    GPU: the first ``sample_chunks`` x 1024 rows are searched exactly and set a per-query
+    threshold for the rest (0 = search every chunk exactly); ties go to the lower row."""
     if _gpu(X):
         Qn, N = Q.shape[0], X.shape[0]
         nchunks = (N + 1023) // 1024
@@ -350,7 +352,10 @@ def knn_topk(X, Q, k: int):
         out_s = torch.empty(Qn, k, dtype=torch.float32, device=dev)
         out_i = torch.empty(Qn, k, dtype=torch.int32, device=dev)
         ws_s = torch.empty(max(1, Qn * nchunks * k), dtype=torch.float32, device=dev)
-        ws_i = torch.empty(max(1, Qn * nchunks * k), dtype=torch.int32, device=dev)
-        hip().knn_topk(X, Q, k, out_s, out_i, ws_s, ws_i)
+        ws_i = torch.empty(Qn * nchunks * k + 3 * Qn, dtype=torch.int32, device=dev)
+        hip().knn_topk(X, Q, k, out_s, out_i, ws_s, ws_i, sample_chunks)
+        if sample_chunks > 0 and nchunks > sample_chunks and bool(ws_i[-Qn:].any()):
+            # a candidate list overflowed (many rows above the sample's K-th best): exact rerun
+            hip().knn_topk(X, Q, k, out_s, out_i, ws_s, ws_i, 0)
         return out_s, out_i
     return ref.knn_topk(X, Q, k)

@@ -14,8 +14,10 @@
 //                          exactly acc(kt=2kg+(j>>2))[j&3] of the same lane.
 // The K-row permutation above is what makes the P^T fragment lane-local.
 //
-// Grid: (B*Hkv, S splits).  4 waves per workgroup stride over the split's KV blocks
-// and are merged through LDS; with S > 1 a second kernel merges the splits.
+// Grid: (B*Hkv, S splits).  WPP waves per workgroup stride over the split's KV blocks:
+// WPP = 1 (one wave owns a (seq, kv-head) pair, writes straight from its accumulators)
+// once the pairs alone fill every wave slot of the chip (B*Hkv >= 2048, no split);
+// otherwise WPP = 4, merged through LDS, and with S > 1 a second kernel merges splits.
 //
 // Split policy (decided per launch, so it is fixed inside a captured HIP graph):
 // S = min(nsplit_max, ceil(TARGET_WG / (B*Hkv))).  At large batch the (seq, kv-head)
@@ -24,13 +26,22 @@
 // context evenly over the S splits (bps = max(min_bps, ceil(nblk / S)), computed on
 // the device), so the grid carries no idle workgroups for short sequences.
 //
-// Per wave, all 32 KiB of a block's K and V fragments are issued before its first
-// MFMA (177 VGPRs, 2 waves/SIMD).  Measured on MI355X (tools/attn_bench.py, B=256,
-// ctx=448, scattered blocks): 89.8 us = 5.2 TB/s, vs 114.7 us for the previous
-// fixed-split kernel, 103 us with next-block K prefetch (256 VGPRs, 1 wave/SIMD) and
-// 106 us when squeezed to 125 VGPRs / 4 waves (V loaded after the softmax); forcing
-// amdgpu_waves_per_eu(3) (164 VGPRs, no spills, 3 waves/SIMD) measured 106.9 vs 90.1 us
-// (profiles/decode_attn_waves_per_eu_ab.log): the in-flight K+V bytes per wave matter more.
+// Memory path: K and V fragments are raw buffer loads through per-block descriptors
+// (wave-uniform, readfirstlane'd).  The K descriptor covers only the block's valid
+// keys and masked V groups get an out-of-range offset, so the tail of a sequence's
+// last block is never fetched (the hardware range check returns zeros).  Per wave, all
+// 32 KiB of a block's K and V are in flight before its first MFMA; with PIPE the next
+// block's K is issued right after the scores and its V right after O += V P (same
+// registers), so a wave keeps streaming through its softmax.  250 VGPRs, 2 waves/SIMD.
+//
+// Measured on MI355X (tools/attn_bench.py, 32 q / 8 kv heads x 128, scattered blocks;
+// profiles/decode_attn_*_r2i.log), B=256:
+//   ctx 448: 89.8 us (flat loads, r1) -> 84.3 (buffer loads) -> 80.0 us = 5.9 TB/s
+//            (WPP=1 + PIPE); ctx 1024: 176 us = 6.1 TB/s; ctx 410 (ragged tail) 77 us.
+// Rejected: nt loads (+7%, back-to-back replays lose the L2/MALL reuse), a select on
+// the loaded data for the tail mask (139 us: each load waited before the next issued),
+// next-block prefetch into extra registers (1 wave/SIMD, 103 us), 125 VGPRs / 4 waves
+// (106 us), amdgpu_waves_per_eu(3) (106.9 us).
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
 #include "common.h"
@@ -39,22 +50,21 @@ namespace {
 
 constexpr int BS = 64;            // tokens per KV block (engine-wide constant)
 constexpr int TARGET_WG = 1024;   // ~4 workgroups per CU before contexts are split
+constexpr int WAVE_SLOTS = 2048;  // 256 CUs x 4 SIMDs x 2 waves/SIMD
 constexpr float LOG2E = 1.4426950408889634f;
 
 __device__ __forceinline__ int split_blocks(int nblk, int nsplit, int min_bps) {
   return max(min_bps, (nblk + nsplit - 1) / nsplit);
 }
 
-template <int D>
-__global__ void __launch_bounds__(256) decode_attn_kernel(
+template <int D, int WPP, bool PIPE>
+__global__ void __launch_bounds__(64 * WPP) __attribute__((amdgpu_waves_per_eu(2, 2))) decode_attn_kernel(
     bf16* __restrict__ out, const bf16* __restrict__ q, int64_t q_stride, const bf16* __restrict__ kc,
     const bf16* __restrict__ vc, const int32_t* __restrict__ block_tables, int max_blocks,
     const int32_t* __restrict__ ctx_lens, int Hkv, int G, int NB, float scale_log2, int min_bps,
     float* __restrict__ part_o, float* __restrict__ part_ml) {
   constexpr int KS = D / 32;  // k-steps over the head dim
   constexpr int DT = D / 16;  // 16-wide output tiles over the head dim
-  __shared__ float sh_o[4][16][D + 4];
-  __shared__ float sh_m[4][16], sh_l[4][16];
 
   const int pair = blockIdx.x;
   const int b = pair / Hkv, kvh = pair - b * Hkv;
@@ -88,26 +98,65 @@ __global__ void __launch_bounds__(256) decode_attn_kernel(
 
   const int32_t* bt = block_tables + (int64_t)b * max_blocks;
   auto block_of = [&](int bi) { return min(max(bt[bi], 0), NB - 1); };
-  auto load_k = [&](int blk, uint4(&dst)[4][KS]) {
-    const bf16* kb = kc + ((int64_t)blk * Hkv + kvh) * BS * D + 8 * h;
+  // Keys at or past the context are never fetched (the last block of a sequence is
+  // partly filled).  K and V go through per-block buffer descriptors: a K descriptor
+  // covers exactly the valid rows, so the hardware range check returns zeros for the
+  // rest without touching memory; a V^T group whose 8 keys all lie past the context
+  // gets an out-of-range offset.  (A select on the loaded data instead made every
+  // load wait before the next one issued: 139 vs 90 us at B=256.)
+  constexpr int OOB = 1 << 30;
+  constexpr int AUX = 0;            // default cache policy (nt measured slower, see above)
+  const int kbyte = 8 * h * 2;
+
+  auto issue_k = [&](int bi, uint4(&kf)[4][KS]) {
+    const int blk = __builtin_amdgcn_readfirstlane(block_of(bi));
+    const int lim = __builtin_amdgcn_readfirstlane(min(ctx - bi * BS, BS));   // valid keys here (>= 1)
+    const int64_t boff = ((int64_t)blk * Hkv + kvh) * BS * D;
+    auto krs = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(kc + boff), 0, lim * D * 2, 0x00020000);
 #pragma unroll
     for (int kt = 0; kt < 4; ++kt) {
       const int key = 32 * (kt >> 1) + 8 * (i16 >> 2) + 4 * (kt & 1) + (i16 & 3);
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) dst[kt][ks] = ld16(kb + key * D + 32 * ks);
+      for (int ks = 0; ks < KS; ++ks)
+        kf[kt][ks] = __builtin_bit_cast(
+            uint4, __builtin_amdgcn_raw_buffer_load_b128(krs, key * D * 2 + 64 * ks + kbyte, 0, AUX));
+    }
+  };
+  auto issue_v = [&](int bi, uint4(&vf)[2][DT]) {
+    const int blk = __builtin_amdgcn_readfirstlane(block_of(bi));
+    const int lim = __builtin_amdgcn_readfirstlane(min(ctx - bi * BS, BS));
+    const int64_t boff = ((int64_t)blk * Hkv + kvh) * BS * D;
+    auto vrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(vc + boff), 0, BS * D * 2, 0x00020000);
+#pragma unroll
+    for (int kg = 0; kg < 2; ++kg) {
+      const bool vok = 32 * kg + 8 * h < lim;
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) {
+        const int off = ((16 * dt + i16) * BS + 32 * kg + 8 * h) * 2;
+        vf[kg][dt] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(vrs, vok ? off : OOB, 0, AUX));
+      }
     }
   };
 
-  for (int bi = bstart + wid; bi < bend; bi += 4) {
-    const int blk = block_of(bi);
-    uint4 kf[4][KS];
-    load_k(blk, kf);
-    const bf16* vb = vc + ((int64_t)blk * Hkv + kvh) * D * BS;
-    uint4 vf[2][DT];
-#pragma unroll
-    for (int kg = 0; kg < 2; ++kg)
-#pragma unroll
-      for (int dt = 0; dt < DT; ++dt) vf[kg][dt] = ld16(vb + (16 * dt + i16) * BS + 32 * kg + 8 * h);
+  // K and V of block i are in flight together; with PIPE, block i+1's K loads are
+  // issued as soon as the scores of block i are computed (its K registers are free) and
+  // its V loads right after O += V P (same registers, no extra VGPRs), so a wave keeps
+  // streaming while it does the softmax and the PV products.
+  uint4 kf[4][KS];
+  uint4 vf[2][DT];
+  if (PIPE && bstart + wid < bend) {
+    issue_k(bstart + wid, kf);
+    issue_v(bstart + wid, vf);
+  }
+  for (int bi = bstart + wid; bi < bend; bi += WPP) {
+    const bool more = bi + WPP < bend;
+    if (!PIPE) {
+      issue_k(bi, kf);
+      issue_v(bi, vf);
+    }
+    // all 32 KiB of the block in flight before the first MFMA (the scheduler would
+    // otherwise sink the V loads past the softmax to raise occupancy)
+    __builtin_amdgcn_sched_barrier(0);
     // ---- S^T = K Q^T for the 64 keys of this block (4 tiles of 16 keys)
     f32x4 s[4];
 #pragma unroll
@@ -152,6 +201,8 @@ __global__ void __launch_bounds__(256) decode_attn_kernel(
     m = mnew;
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt) o[dt] *= alpha;
+    if (PIPE && more) issue_k(bi + WPP, kf);
+    __builtin_amdgcn_sched_barrier(0);
     // ---- O^T += V^T P^T
 #pragma unroll
     for (int kg = 0; kg < 2; ++kg) {
@@ -165,9 +216,41 @@ __global__ void __launch_bounds__(256) decode_attn_kernel(
       for (int dt = 0; dt < DT; ++dt)
         o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, vf[kg][dt]), pf, o[dt], 0, 0, 0);
     }
+    __builtin_amdgcn_sched_barrier(0);
+    if (PIPE && more) issue_v(bi + WPP, vf);
   }
 
-  // ---- merge the 4 waves through LDS.  o[dt][r] = O[qrow i16][d = 16dt + 4h + r]
+  // o[dt][r] = O[qrow i16][d = 16dt + 4h + r]
+  if constexpr (WPP == 1) {
+    // one wave owns the (pair, split): write straight from the accumulators
+    if (i16 < G) {
+      const int64_t row = (int64_t)b * Hkv * G + kvh * G + i16;
+      if (nsplit == 1) {
+        const float inv = l > 0.f ? 1.f / l : 0.f;
+        bf16* op = out + row * D + 4 * h;
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) {
+          bf16x4 v;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = (bf16)(o[dt][r] * inv);
+          *reinterpret_cast<bf16x4*>(op + 16 * dt) = v;
+        }
+      } else {
+        const int64_t pi = row * nsplit + split;
+        float* po = part_o + pi * D + 4 * h;
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) *reinterpret_cast<f32x4*>(po + 16 * dt) = o[dt];
+        if (h == 0) {
+          part_ml[pi * 2] = m;
+          part_ml[pi * 2 + 1] = l;
+        }
+      }
+    }
+  } else {
+  static_assert(WPP == 4, "the LDS merge maps 256 threads onto (16 rows x 16 chunks)");
+  // ---- merge the WPP waves through LDS
+  __shared__ float sh_o[WPP][16][D + 4];
+  __shared__ float sh_m[WPP][16], sh_l[WPP][16];
 #pragma unroll
   for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
@@ -182,18 +265,18 @@ __global__ void __launch_bounds__(256) decode_attn_kernel(
   const int dc = threadIdx.x & 15;    // chunk of D/16 elements
   constexpr int CH = D / 16;
   if (row < G) {
-    float mw[4], mstar = -1e30f;
+    float mw[WPP], mstar = -1e30f;
 #pragma unroll
-    for (int w = 0; w < 4; ++w) { mw[w] = sh_m[w][row]; mstar = fmaxf(mstar, mw[w]); }
-    float lt = 0.f, f[4];
+    for (int w = 0; w < WPP; ++w) { mw[w] = sh_m[w][row]; mstar = fmaxf(mstar, mw[w]); }
+    float lt = 0.f, f[WPP];
 #pragma unroll
-    for (int w = 0; w < 4; ++w) { f[w] = exp2f(mw[w] - mstar); lt += sh_l[w][row] * f[w]; }
+    for (int w = 0; w < WPP; ++w) { f[w] = exp2f(mw[w] - mstar); lt += sh_l[w][row] * f[w]; }
     float acc[CH];
 #pragma unroll
     for (int c = 0; c < CH; ++c) {
       float a = 0.f;
 #pragma unroll
-      for (int w = 0; w < 4; ++w) a += sh_o[w][row][dc * CH + c] * f[w];
+      for (int w = 0; w < WPP; ++w) a += sh_o[w][row][dc * CH + c] * f[w];
       acc[c] = a;
     }
     const int head = kvh * G + row;
@@ -214,6 +297,7 @@ __global__ void __launch_bounds__(256) decode_attn_kernel(
         part_ml[pi * 2 + 1] = lt;
       }
     }
+  }
   }
 }
 
@@ -284,20 +368,32 @@ void paged_decode_attention(at::Tensor out, at::Tensor q, at::Tensor k_cache, at
     pml = po + (int64_t)B * Hq * ns * D;
   }
   auto stream = at::hip::getCurrentHIPStream();
+  // Wave-per-pair (WPP=1) once the (seq, kv-head) pairs alone fill every wave slot of
+  // the chip (256 CUs x 8 resident waves): each wave then streams its whole context
+  // with no LDS merge and no idle waves in a workgroup whose block count is not a
+  // multiple of 4.  Smaller batches keep 4 waves per pair (and split long contexts).
+  static const int env_wpp = getenv("LS_ATTN_WPP") ? atoi(getenv("LS_ATTN_WPP")) : 0;
+  static const bool pipe = getenv("LS_ATTN_PIPE") ? atoi(getenv("LS_ATTN_PIPE")) != 0 : true;
+  const int wpp = env_wpp == 1 || env_wpp == 4 ? env_wpp : ((int64_t)B * Hkv >= WAVE_SLOTS && ns == 1 ? 1 : 4);
   dim3 grid(B * Hkv, ns);
   const float sl2 = (float)scale * LOG2E;
-#define LAUNCH(DD)                                                                                                  \
-  decode_attn_kernel<DD><<<grid, 256, 0, stream>>>((bf16*)out.data_ptr(), (const bf16*)q.data_ptr(), q_stride, \
-                                                   (const bf16*)k_cache.data_ptr(), (const bf16*)v_cache.data_ptr(), \
-                                                   block_tables.data_ptr<int32_t>(), (int)block_tables.size(1),  \
-                                                   ctx_lens.data_ptr<int32_t>(), Hkv, G, (int)k_cache.size(0),    \
-                                                   sl2, (int)min_bps, po, pml);                                   \
-  if (ns > 1)                                                                                                    \
-    decode_merge_kernel<DD><<<(B * Hq + 3) / 4, 256, 0, stream>>>((bf16*)out.data_ptr(), po, pml, (int)ns,       \
-                                                                  B * Hq, ctx_lens.data_ptr<int32_t>(), Hq,       \
+#define LAUNCH_P(DD, W, P)                                                                                    \
+  decode_attn_kernel<DD, W, P><<<grid, 64 * W, 0, stream>>>(                                                  \
+      (bf16*)out.data_ptr(), (const bf16*)q.data_ptr(), q_stride, (const bf16*)k_cache.data_ptr(),            \
+      (const bf16*)v_cache.data_ptr(), block_tables.data_ptr<int32_t>(), (int)block_tables.size(1),          \
+      ctx_lens.data_ptr<int32_t>(), Hkv, G, (int)k_cache.size(0), sl2, (int)min_bps, po, pml)
+#define LAUNCH_K(DD, W) \
+  if (pipe) LAUNCH_P(DD, W, true); else LAUNCH_P(DD, W, false)
+#define LAUNCH(DD)                                                                                            \
+  if (wpp == 1) { LAUNCH_K(DD, 1); } else { LAUNCH_K(DD, 4); }                                                \
+  if (ns > 1)                                                                                                 \
+    decode_merge_kernel<DD><<<(B * Hq + 3) / 4, 256, 0, stream>>>((bf16*)out.data_ptr(), po, pml, (int)ns,    \
+                                                                  B * Hq, ctx_lens.data_ptr<int32_t>(), Hq,    \
                                                                   (int)min_bps, (int)block_tables.size(1))
   if (D == 128) { LAUNCH(128); }
   else if (D == 64) { LAUNCH(64); }
   else TORCH_CHECK(false, "unsupported head dim ", D);
+#undef LAUNCH_K
+#undef LAUNCH_P
 #undef LAUNCH
 }

@@ -26,9 +26,11 @@ void apply_logit_deltas(at::Tensor logits, at::Tensor rows, at::Tensor toks, at:
 void pool_embeddings(at::Tensor out, at::Tensor x, at::Tensor start, at::Tensor len, int64_t mode, bool normalize);
 void l2_normalize_rows(at::Tensor out, at::Tensor x);
 void knn_topk(at::Tensor X, at::Tensor Q, int64_t K, at::Tensor out_s, at::Tensor out_i, at::Tensor ws_s,
-              at::Tensor ws_i);
+              at::Tensor ws_i, int64_t sample);
+int64_t knn_default_sample();
 void skinny_gemm(at::Tensor out, at::Tensor x, at::Tensor w);
 void gemv(at::Tensor out, at::Tensor x, at::Tensor w);
+bool gemv_supported(const at::Tensor& w, bool silu);
 void gemv_silu(at::Tensor out, at::Tensor x, at::Tensor w);
 void gemv_add_rmsnorm(at::Tensor out, at::Tensor x, at::Tensor w, at::Tensor residual, at::Tensor norm_w,
                       double eps, at::Tensor counter);
@@ -66,8 +68,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("pool_embeddings", &pool_embeddings);
   m.def("l2_normalize_rows", &l2_normalize_rows);
   m.def("knn_topk", &knn_topk);
+  m.def("knn_default_sample", &knn_default_sample);
   m.def("skinny_gemm", &skinny_gemm);
   m.def("gemv", &gemv);
+  m.def("gemv_supported", &gemv_supported);
   m.def("gemv_silu", &gemv_silu);
   m.def("gemv_add_rmsnorm", &gemv_add_rmsnorm);
   m.def("gemv_norm", &gemv_norm);

@@ -58,6 +58,11 @@ __device__ __forceinline__ float block_max(float v, float* red) {
 
 __device__ __forceinline__ uint4 ld16(const void* p) { return *reinterpret_cast<const uint4*>(p); }
 __device__ __forceinline__ void st16(void* p, uint4 v) { *reinterpret_cast<uint4*>(p) = v; }
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+// streamed-once data (KV cache, database rows): non-temporal load, keeps L2 for reused lines
+__device__ __forceinline__ uint4 ld16_nt(const void* p) {
+  return __builtin_bit_cast(uint4, __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p)));
+}
 
 __device__ __forceinline__ void unpack8(uint4 v, float* f) {
   const bf16x8 b = __builtin_bit_cast(bf16x8, v);

@@ -5,10 +5,17 @@
 // groups, flattened and XCD-remapped (groups of a chunk share an XCD's L2).  Each wave streams 256 store rows through mfma_f32_16x16x32_bf16 as the
 // A operand (one 16-B load per lane per MFMA, straight from HBM: the rows are read
 // once per query group) against the 16 queries' Q^T fragments held in LDS.  Scores
-// for the 1024 x 16 block go to LDS; each wave then extracts the top-k of 4 queries
-// by k rounds of wave-argmax (k <= 64), writing (score, row) candidates.
-// Stage 2: one workgroup per query selects the global top-k from all chunk
-// candidates (k rounds of block-argmax over an L2-resident candidate list).
+// for the 1024 x 16 block go to LDS; each wave then extracts the top-k of 4 queries,
+// filtered by a per-query score threshold (the K-th best of an exact search over a
+// sample of the store; see the top-k comment in the kernel), appending (score, row)
+// candidates to a per-query list.
+// Select: one workgroup per query selects the global top-k from its candidates
+// (k rounds of block-argmax over a short, L2-resident list).
+//
+// Measured (tools/engine_bench.py --what knn, 1M x 384, k=20; profiles/knn_*):
+// per-chunk exact top-k (before) Q=256 1.96 ms; with a running atomic-max threshold
+// 1.81 ms (stage 1 1.49 ms + select 0.33 ms: contention on the per-query atomics and
+// long candidate lists).
 //
 // Scores are raw dot products; the store keeps rows L2-normalised so this is
 // cosine similarity.  Rows >= N (tail chunk) score -inf.
@@ -20,6 +27,16 @@ namespace {
 
 constexpr int CH = 1024;  // store rows per workgroup
 constexpr int QG = 16;    // queries per workgroup (one MFMA column group)
+// queries per workgroup of the thresholded main pass (their rows staged in LDS)
+constexpr int qf_of(int dim) { return dim <= 512 ? 64 : dim <= 1024 ? 32 : 16; }
+constexpr int SAMPLE_CHUNKS = 32;  // chunks searched exactly first, to set the per-query thresholds
+
+// order-preserving float <-> int key (for atomic max on a float threshold)
+__device__ __forceinline__ int f2key(float f) {
+  const int b = __float_as_int(f);
+  return b >= 0 ? b : b ^ 0x7FFFFFFF;
+}
+__device__ __forceinline__ float key2f(int k) { return __int_as_float(k >= 0 ? k : k ^ 0x7FFFFFFF); }
 
 // Bitonic sort of one (value, index) pair per lane across a 64-wide wave, descending by
 // value with ties broken towards the lower index (the order the argmax path produces):
@@ -42,106 +59,154 @@ __device__ __forceinline__ void wave_sort_desc(float& v, int& i, int lane) {
 }
 
 template <int DIM>
-__global__ void __launch_bounds__(256) knn_stage1_kernel(const bf16* __restrict__ X, int64_t N,
+__global__ void __launch_bounds__(256) knn_exact_kernel(const bf16* __restrict__ X, int64_t N,
                                                          const bf16* __restrict__ Qm, int Qn, int K,
                                                          float* __restrict__ cand_s, int32_t* __restrict__ cand_i,
+                                                         int* __restrict__ ctrl, int nchunks_total, int chunk0,
                                                          int nchunks) {
   constexpr int KS = DIM / 32;
-  __shared__ __attribute__((aligned(16))) bf16 q_lds[QG * DIM];
+  constexpr int QROW = DIM + 8;   // +16 B per query row: the 16 lanes i16 of a B-fragment read hit distinct banks
+  constexpr int KB = KS < 32 ? KS : 32;   // k-steps per load batch (DIM 2048: two batches)
+  // subtiles whose A fragments are in flight together (<= 48 16-B loads per lane)
+  constexpr int U = (48 / KB) >= 8 ? 8 : (48 / KB) >= 4 ? 4 : (48 / KB) >= 2 ? 2 : 1;
+  __shared__ __attribute__((aligned(16))) bf16 q_lds[QG * QROW];
   __shared__ float sc[QG][CH + 1];
+  __shared__ float sh_thr[QG];
   // 1-D grid, XCD-aware: the query groups of one row chunk are consecutive logical ids
   // on one XCD, so the chunk's rows come from HBM once and from that XCD's L2 after
   // (with grid (chunks, groups) every group re-streamed the whole store from HBM).
   const int nqg = gridDim.x / nchunks;
   const int logical = xcd_remap(blockIdx.x, gridDim.x);
-  const int chunk = logical / nqg, qg = logical - chunk * nqg;
+  const int lchunk = logical / nqg, qg = logical - lchunk * nqg;
+  const int chunk = chunk0 + lchunk;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int i16 = lane & 15, h = lane >> 4;
-  // stage the 16 queries (zero rows past Qn)
+  // stage the 16 queries (zero rows past Qn) and their score thresholds
   for (int c = threadIdx.x; c < QG * DIM / 8; c += 256) {
     const int qq = c / (DIM / 8), cc = c - qq * (DIM / 8);
     const int qi = qg * QG + qq;
-    *reinterpret_cast<uint4*>(&q_lds[qq * DIM + cc * 8]) =
+    *reinterpret_cast<uint4*>(&q_lds[qq * QROW + cc * 8]) =
         qi < Qn ? ld16(Qm + (int64_t)qi * DIM + cc * 8) : make_uint4(0, 0, 0, 0);
+  }
+  if (threadIdx.x < QG) {
+    const int qi = qg * QG + threadIdx.x;
+    sh_thr[threadIdx.x] = qi < Qn ? key2f(ctrl[Qn + qi]) : INFINITY;
   }
   __syncthreads();
   const int64_t row0 = (int64_t)chunk * CH + wid * 256;
-  for (int st = 0; st < 16; ++st) {
-    const int64_t r = row0 + st * 16 + i16;
-    const bool valid = r < N;
-    const bf16* xr = X + (valid ? r : 0) * DIM + 8 * h;
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int st0 = 0; st0 < 16; st0 += U) {
+    f32x4 acc[U];
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      const bf16x8 a = __builtin_bit_cast(bf16x8, ld16(xr + 32 * ks));
-      const bf16x8 b = *reinterpret_cast<const bf16x8*>(&q_lds[i16 * DIM + 32 * ks + 8 * h]);
-      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc, 0, 0, 0);
-    }
-    // acc[rr] = score(row 4h+rr of the subtile, query i16)
+    for (int u = 0; u < U; ++u) acc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int rr = 0; rr < 4; ++rr) {
-      const int lr = wid * 256 + st * 16 + 4 * h + rr;
-      const bool ok = row0 + st * 16 + 4 * h + rr < N;
-      sc[i16][lr] = ok ? acc[rr] : -INFINITY;
+    for (int kb = 0; kb < KS; kb += KB) {
+      uint4 af[U][KB];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t r = row0 + (st0 + u) * 16 + i16;
+        const bf16* xr = X + (r < N ? r : 0) * DIM + 8 * h + 32 * kb;
+#pragma unroll
+        for (int ks = 0; ks < KB; ++ks) af[u][ks] = ld16(xr + 32 * ks);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int ks = 0; ks < KB; ++ks) {
+          const bf16x8 bq = *reinterpret_cast<const bf16x8*>(&q_lds[i16 * QROW + 32 * (kb + ks) + 8 * h]);
+          acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, af[u][ks]), bq, acc[u], 0, 0, 0);
+        }
     }
+    // acc[u][rr] = score(row 4h+rr of subtile st0+u, query i16)
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int lr = wid * 256 + (st0 + u) * 16 + 4 * h + rr;
+        sc[i16][lr] = row0 + (st0 + u) * 16 + 4 * h + rr < N ? acc[u][rr] : -INFINITY;
+      }
   }
   __syncthreads();
-  // top-K per query: wave w handles queries w, w+4, w+8, w+12.
-  // Fast path (threshold + sort): every lane holds 16 of the 1024 scores in registers;
-  // the K-th largest of the 64 lane maxima, T, lower-bounds the K-th largest score (the
-  // K lanes owning those maxima each hold a score >= T), so only scores >= T can be in
-  // the top-K.  They are compacted by ballot into a 64-slot LDS list and bitonic-sorted
-  // across the wave (21 shuffle stages) -- instead of K rounds of a 1024-wide argmax.
-  // When more than 64 scores reach T (heavy ties, or a tail chunk where T = -inf) the
-  // wave falls back to the K-round argmax over LDS.
+  // top-K per query: wave w handles queries w, w+4, w+8, w+12.  Every lane holds 16 of
+  // the chunk's 1024 scores in registers.
+  //
+  // Threshold: thr[q] is the K-th best score over a SAMPLE of the store (the first
+  // chunks, searched exactly by an earlier launch), so it lower-bounds the final K-th
+  // best and scores below it can never be in the answer.  Almost every (chunk, query)
+  // of the main pass then finds no score >= thr and costs one ballot per register; the
+  // few chunks that can contribute append at most K candidates to the query's list
+  // (one atomic slot reservation per chunk; capacity nchunks*K can never overflow).
+  // The sample launch itself runs with thr = -inf.
+  //
+  // Selection inside a contributing chunk: if more than 64 scores pass, the K-th
+  // largest of the 64 lane maxima, Tl, is a second lower bound (the K lanes owning
+  // those maxima each hold a score >= Tl); scores >= max(thr, Tl) are compacted by
+  // ballot into a 64-slot LDS list and bitonic-sorted across the wave.  When more than
+  // 64 still pass (heavy ties, or a tail chunk of -inf rows) the wave falls back to K
+  // rounds of argmax over LDS.
   __shared__ float cv_lds[4][64];
   __shared__ int ci_lds[4][64];
+  const int64_t cap = (int64_t)nchunks_total * K;
   for (int qq = wid; qq < QG; qq += 4) {
     const int qi = qg * QG + qq;
     if (qi >= Qn) continue;
-    float* outs = cand_s + ((int64_t)qi * nchunks + chunk) * K;
-    int32_t* outi = cand_i + ((int64_t)qi * nchunks + chunk) * K;
+    int* cnt = ctrl + qi;
+    float* outs = cand_s + (int64_t)qi * cap;
+    int32_t* outi = cand_i + (int64_t)qi * cap;
     float v[CH / 64];
-    float m = -INFINITY;
 #pragma unroll
-    for (int j = 0; j < CH / 64; ++j) {
-      v[j] = sc[qq][lane + 64 * j];
-      m = fmaxf(m, v[j]);
-    }
-    float tv = m;
-    int ti = lane;
-    wave_sort_desc(tv, ti, lane);
-    const float T = __shfl(tv, K - 1, 64);
+    for (int j = 0; j < CH / 64; ++j) v[j] = sc[qq][lane + 64 * j];
+    const float T0 = sh_thr[qq];
     int count = 0;
+#pragma unroll
+    for (int j = 0; j < CH / 64; ++j) count += __popcll(__ballot(v[j] >= T0));
+    if (count == 0) continue;
+    float T = T0;
+    if (count > 64) {
+      float m = -INFINITY;
+#pragma unroll
+      for (int j = 0; j < CH / 64; ++j) m = fmaxf(m, v[j]);
+      int ti = lane;
+      wave_sort_desc(m, ti, lane);
+      T = fmaxf(T0, __shfl(m, K - 1, 64));
+    }
+    int count2 = 0;
     if (T > -INFINITY) {
 #pragma unroll
       for (int j = 0; j < CH / 64; ++j) {
         const bool p = v[j] >= T;
         const uint64_t mask = __ballot(p);
-        const int pos = count + __popcll(mask & ((1ull << lane) - 1ull));
+        const int pos = count2 + __popcll(mask & ((1ull << lane) - 1ull));
         if (p && pos < 64) {
           cv_lds[wid][pos] = v[j];
           ci_lds[wid][pos] = lane + 64 * j;
         }
-        count += __popcll(mask);
+        count2 += __popcll(mask);
       }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (T > -INFINITY && count <= 64) {
-      float cvv = lane < count ? cv_lds[wid][lane] : -INFINITY;
-      int cii = lane < count ? ci_lds[wid][lane] : CH;
-      wave_sort_desc(cvv, cii, lane);
-      if (lane < K) {
-        outs[lane] = cvv;
-        outi[lane] = cii < CH ? (int32_t)((int64_t)chunk * CH + cii) : -1;
+    if (T > -INFINITY && count2 <= 64) {
+      float cvv = lane < count2 ? cv_lds[wid][lane] : -INFINITY;
+      int cii = lane < count2 ? ci_lds[wid][lane] : CH;
+      const int n = min(count2, K);
+      if (count2 > K) wave_sort_desc(cvv, cii, lane);
+      int base = 0;
+      if (lane == 0) base = __hip_atomic_fetch_add(cnt, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      base = __shfl(base, 0, 64);
+      if (lane < n) {
+        outs[base + lane] = cvv;
+        outi[base + lane] = (int32_t)((int64_t)chunk * CH + cii);
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       continue;
     }
+    int base = 0;
+    if (lane == 0) base = __hip_atomic_fetch_add(cnt, K, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    base = __shfl(base, 0, 64);
     for (int k = 0; k < K; ++k) {
       float bv = -INFINITY;
       int bi = CH;
@@ -156,8 +221,8 @@ __global__ void __launch_bounds__(256) knn_stage1_kernel(const bf16* __restrict_
         if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
       }
       if (lane == 0) {
-        outs[k] = bv;
-        outi[k] = bi < CH ? (int32_t)((int64_t)chunk * CH + bi) : -1;
+        outs[base + k] = bv;
+        outi[base + k] = bi < CH ? (int32_t)((int64_t)chunk * CH + bi) : -1;
         if (bi < CH) sc[qq][bi] = -INFINITY;
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -167,40 +232,167 @@ __global__ void __launch_bounds__(256) knn_stage1_kernel(const bf16* __restrict_
   }
 }
 
-__global__ void __launch_bounds__(256) knn_stage2_kernel(float* __restrict__ cand_s, const int32_t* __restrict__ cand_i,
-                                                         int ncand, int K, float* __restrict__ out_s,
-                                                         int32_t* __restrict__ out_i) {
-  __shared__ float rv[4];
-  __shared__ int ri[4];
-  const int qi = blockIdx.x;
-  float* cs = cand_s + (int64_t)qi * ncand;
-  const int32_t* ci = cand_i + (int64_t)qi * ncand;
+
+// Main pass: the rows of the chunks after the sample, 64 queries per workgroup at
+// dim <= 512 (four MFMA column groups share every A fragment, so the store streams
+// through L2 a quarter as often as with 16), scores stay in the MFMA accumulators and only those strictly
+// above the query's sample threshold are appended to its list.  Strict: a row outside
+// the sample that TIES the sample's K-th best loses to it on row index, since the
+// sample is the lowest rows.  A list that fills up (adversarial data: many rows above
+// the sample's K-th best) sets the query's overflow flag; the host then reruns the
+// search exactly.
+template <int DIM>
+__global__ void __launch_bounds__(256) knn_filter_kernel(const bf16* __restrict__ X, int64_t N,
+                                                         const bf16* __restrict__ Qm, int Qn,
+                                                         float* __restrict__ cand_s, int32_t* __restrict__ cand_i,
+                                                         int* __restrict__ ctrl, int64_t cap, int chunk0,
+                                                         int nchunks) {
+  constexpr int KS = DIM / 32;
+  constexpr int QROW = DIM + 8;
+  constexpr int KB = KS < 32 ? KS : 32;
+  constexpr int U = KB <= 6 ? 4 : KB <= 12 ? 2 : 1;
+  constexpr int QF = qf_of(DIM);
+  __shared__ __attribute__((aligned(16))) bf16 q_lds[QF * QROW];
+  const int nqf = gridDim.x / nchunks;
+  const int logical = xcd_remap(blockIdx.x, gridDim.x);
+  const int lchunk = logical / nqf, qf = logical - lchunk * nqf;
+  const int chunk = chunk0 + lchunk;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  for (int k = 0; k < K; ++k) {
-    float bv = -INFINITY;
-    int bi = ncand;
-    for (int j = threadIdx.x; j < ncand; j += 256) {
-      const float v = cs[j];
-      if (v > bv) { bv = v; bi = j; }
-    }
+  const int i16 = lane & 15, h = lane >> 4;
+  for (int c = threadIdx.x; c < QF * DIM / 8; c += 256) {
+    const int qq = c / (DIM / 8), cc = c - qq * (DIM / 8);
+    const int qi = qf * QF + qq;
+    *reinterpret_cast<uint4*>(&q_lds[qq * QROW + cc * 8]) =
+        qi < Qn ? ld16(Qm + (int64_t)qi * DIM + cc * 8) : make_uint4(0, 0, 0, 0);
+  }
+  // this lane's 4 queries: column i16 of each group g
+  float thr[QF / 16];
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const float ov = __shfl_xor(bv, o, 64);
-      const int oi = __shfl_xor(bi, o, 64);
-      if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
+  for (int g = 0; g < QF / 16; ++g) {
+    const int qi = qf * QF + 16 * g + i16;
+    thr[g] = qi < Qn ? key2f(ctrl[Qn + qi]) : INFINITY;
+  }
+  __syncthreads();
+  const int64_t row0 = (int64_t)chunk * CH + wid * 256;
+  for (int st0 = 0; st0 < 16; st0 += U) {
+    f32x4 acc[U][QF / 16];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int g = 0; g < QF / 16; ++g) acc[u][g] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kb = 0; kb < KS; kb += KB) {
+      uint4 af[U][KB];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t r = row0 + (st0 + u) * 16 + i16;
+        const bf16* xr = X + (r < N ? r : 0) * DIM + 8 * h + 32 * kb;
+#pragma unroll
+        for (int ks = 0; ks < KB; ++ks) af[u][ks] = ld16(xr + 32 * ks);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int ks = 0; ks < KB; ++ks)
+#pragma unroll
+        for (int g = 0; g < QF / 16; ++g) {
+          const bf16x8 bq = *reinterpret_cast<const bf16x8*>(&q_lds[(16 * g + i16) * QROW + 32 * (kb + ks) + 8 * h]);
+#pragma unroll
+          for (int u = 0; u < U; ++u)
+            acc[u][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, af[u][ks]), bq, acc[u][g],
+                                                                0, 0, 0);
+        }
     }
-    if (lane == 0) { rv[wid] = bv; ri[wid] = bi; }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      float b = rv[0];
-      int bb = ri[0];
-      for (int w = 1; w < 4; ++w)
-        if (rv[w] > b || (rv[w] == b && ri[w] < bb)) { b = rv[w]; bb = ri[w]; }
-      out_s[(int64_t)qi * K + k] = b;
-      out_i[(int64_t)qi * K + k] = bb < ncand ? ci[bb] : -1;
-      if (bb < ncand) cs[bb] = -INFINITY;
+    // acc[u][g][rr] = score(row 4h+rr of subtile st0+u, query 16g+i16)
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int g = 0; g < QF / 16; ++g)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+          const int64_t row = row0 + (st0 + u) * 16 + 4 * h + rr;
+          if (acc[u][g][rr] > thr[g] && row < N) {
+            const int qi = qf * QF + 16 * g + i16;
+            const int slot = __hip_atomic_fetch_add(ctrl + qi, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (slot < cap) {
+              cand_s[(int64_t)qi * cap + slot] = acc[u][g][rr];
+              cand_i[(int64_t)qi * cap + slot] = (int32_t)row;
+            } else {
+              ctrl[2 * Qn + qi] = 1;
+            }
+          }
+        }
+  }
+}
+
+__global__ void knn_init_kernel(int* __restrict__ ctrl, int Qn) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < Qn) {
+    ctrl[i] = 0;
+    ctrl[Qn + i] = f2key(-INFINITY);
+    ctrl[2 * Qn + i] = 0;
+  }
+}
+
+// Bitonic merge of a bitonic 64-sequence into descending order (ties: lower index first).
+__device__ __forceinline__ void wave_merge_desc(float& v, int& i, int lane) {
+#pragma unroll
+  for (int j = 32; j > 0; j >>= 1) {
+    const float ov = __shfl_xor(v, j, 64);
+    const int oi = __shfl_xor(i, j, 64);
+    const bool other_first = ov > v || (ov == v && oi < i);
+    const bool lower = (lane & j) == 0;
+    if (lower ? other_first : !other_first) { v = ov; i = oi; }
+  }
+}
+
+// One wave per query: the top-K of the query's candidate list, ordered by score then
+// row index (so the answer does not depend on the order candidates were appended).
+// The wave keeps its best 64 sorted across lanes; each batch of 64 candidates is
+// skipped when none beats the current K-th best, else sorted and merged (max of best[i]
+// and batch[63-i] is bitonic and holds the top 64 of both).
+// write_thr: store the K-th best score as the query's threshold instead of the answer.
+__global__ void __launch_bounds__(256) knn_select_kernel(const float* __restrict__ cand_s,
+                                                         const int32_t* __restrict__ cand_i, int* __restrict__ ctrl,
+                                                         int Qn, int64_t cap, int K, float* __restrict__ out_s,
+                                                         int32_t* __restrict__ out_i, int write_thr) {
+  const int lane = threadIdx.x & 63;
+  const int qi = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (qi >= Qn) return;
+  const int n = (int)min((int64_t)ctrl[qi], cap);
+  const float* cs = cand_s + (int64_t)qi * cap;
+  const int32_t* ci = cand_i + (int64_t)qi * cap;
+  float bv = -INFINITY;
+  int br = INT_MAX;
+  float nv = -INFINITY;
+  int nr = INT_MAX;
+  if (lane < n) {
+    nv = cs[lane];
+    nr = ci[lane];
+  }
+  for (int base = 0; base < n; base += 64) {
+    float v = nv;
+    int r = nr < 0 || v == -INFINITY ? INT_MAX : nr;
+    nv = -INFINITY;
+    nr = INT_MAX;
+    if (base + 64 + lane < n) {   // prefetch the next batch
+      nv = cs[base + 64 + lane];
+      nr = ci[base + 64 + lane];
     }
-    __syncthreads();
+    const float kv = __shfl(bv, K - 1, 64);
+    const int kr = __shfl(br, K - 1, 64);
+    if (__ballot(v > kv || (v == kv && r < kr)) == 0) continue;
+    wave_sort_desc(v, r, lane);
+    const float ov = __shfl(v, 63 - lane, 64);
+    const int orr = __shfl(r, 63 - lane, 64);
+    if (ov > bv || (ov == bv && orr < br)) { bv = ov; br = orr; }
+    wave_merge_desc(bv, br, lane);
+  }
+  if (write_thr) {
+    const float kv = __shfl(bv, K - 1, 64);
+    if (lane == 0) ctrl[Qn + qi] = f2key(kv);   // -inf when the sample holds fewer than K rows
+  } else if (lane < K) {
+    out_s[(int64_t)qi * K + lane] = bv;
+    out_i[(int64_t)qi * K + lane] = bv > -INFINITY && br != INT_MAX ? br : -1;
   }
 }
 
@@ -208,9 +400,15 @@ __global__ void __launch_bounds__(256) knn_stage2_kernel(float* __restrict__ can
 
 // X: [N, dim] bf16 (rows L2-normalised), Q: [Qn, dim] bf16.  Returns via out tensors
 // the top-K scores (f32 [Qn, K]) and row indices (int32 [Qn, K], -1 if N < K).
-// workspace: f32 [Qn * nchunks * K] and int32 same count.
+// workspace: f32 [Qn * nchunks * K] and int32 [Qn * nchunks * K + 3 * Qn] (candidate
+// lists, then per-query candidate counts, thresholds and overflow flags).
+//
+// Launch sequence: init; exact per-chunk top-K over the first `sample` chunks; select
+// (K-th best of the sample -> threshold); thresholded main pass over the rest; select
+// (answer).  sample <= 0 or >= nchunks: every chunk is searched exactly.  The caller
+// checks the overflow flags (ws_i tail) and reruns exactly if any is set.
 void knn_topk(at::Tensor X, at::Tensor Q, int64_t K, at::Tensor out_s, at::Tensor out_i, at::Tensor ws_s,
-              at::Tensor ws_i) {
+              at::Tensor ws_i, int64_t sample) {
   TORCH_CHECK(X.scalar_type() == at::kBFloat16 && Q.scalar_type() == at::kBFloat16);
   TORCH_CHECK(X.is_contiguous() && Q.is_contiguous() && X.dim() == 2 && Q.dim() == 2);
   const int dim = X.size(1);
@@ -219,28 +417,59 @@ void knn_topk(at::Tensor X, at::Tensor Q, int64_t K, at::Tensor out_s, at::Tenso
   const int64_t N = X.size(0);
   const int Qn = Q.size(0);
   const int nchunks = (int)((N + CH - 1) / CH);
-  TORCH_CHECK(ws_s.numel() >= (int64_t)Qn * nchunks * K && ws_i.numel() >= (int64_t)Qn * nchunks * K);
+  TORCH_CHECK(ws_s.numel() >= (int64_t)Qn * nchunks * K && ws_i.numel() >= (int64_t)Qn * nchunks * K + 3 * Qn,
+              "kNN workspace too small");
   TORCH_CHECK(out_s.numel() >= (int64_t)Qn * K && out_i.numel() >= (int64_t)Qn * K);
   if (Qn == 0 || N == 0) return;
   auto stream = at::hip::getCurrentHIPStream();
-  TORCH_CHECK((int64_t)nchunks * ((Qn + QG - 1) / QG) < (1LL << 31), "kNN grid too large");
-  dim3 grid(nchunks * ((Qn + QG - 1) / QG));
-#define LAUNCH(DD)                                                                                          \
-  knn_stage1_kernel<DD><<<grid, 256, 0, stream>>>((const bf16*)X.data_ptr(), N, (const bf16*)Q.data_ptr(), \
-                                                  Qn, (int)K, ws_s.data_ptr<float>(), ws_i.data_ptr<int32_t>(), \
-                                                  nchunks)
-  switch (dim) {
-    case 128: LAUNCH(128); break;
-    case 256: LAUNCH(256); break;
-    case 384: LAUNCH(384); break;
-    case 512: LAUNCH(512); break;
-    case 768: LAUNCH(768); break;
-    case 1024: LAUNCH(1024); break;
-    case 1536: LAUNCH(1536); break;
-    case 2048: LAUNCH(2048); break;
-    default: TORCH_CHECK(false, "unsupported embedding dim ", dim);
+  const int nqg = (Qn + QG - 1) / QG, nqf = (Qn + qf_of(dim) - 1) / qf_of(dim);
+  TORCH_CHECK((int64_t)nchunks * nqg < (1LL << 31), "kNN grid too large");
+  int* ctrl = ws_i.data_ptr<int32_t>() + (int64_t)Qn * nchunks * K;
+  const int64_t cap = (int64_t)nchunks * K;
+  knn_init_kernel<<<(Qn + 255) / 256, 256, 0, stream>>>(ctrl, Qn);
+#define DISPATCH_DIM(LAUNCH)                                       \
+  switch (dim) {                                                   \
+    case 128: LAUNCH(128); break;                                  \
+    case 256: LAUNCH(256); break;                                  \
+    case 384: LAUNCH(384); break;                                  \
+    case 512: LAUNCH(512); break;                                  \
+    case 768: LAUNCH(768); break;                                  \
+    case 1024: LAUNCH(1024); break;                                \
+    case 1536: LAUNCH(1536); break;                                \
+    case 2048: LAUNCH(2048); break;                                \
+    default: TORCH_CHECK(false, "unsupported embedding dim ", dim); \
   }
-#undef LAUNCH
-  knn_stage2_kernel<<<Qn, 256, 0, stream>>>(ws_s.data_ptr<float>(), ws_i.data_ptr<int32_t>(), nchunks * (int)K,
-                                            (int)K, out_s.data_ptr<float>(), out_i.data_ptr<int32_t>());
+  auto exact = [&](int nc) {
+    dim3 grid(nc * nqg);
+#define LAUNCH_E(DD)                                                                                          \
+  knn_exact_kernel<DD><<<grid, 256, 0, stream>>>((const bf16*)X.data_ptr(), N, (const bf16*)Q.data_ptr(),    \
+                                                 Qn, (int)K, ws_s.data_ptr<float>(), ws_i.data_ptr<int32_t>(), \
+                                                 ctrl, nchunks, 0, nc)
+    DISPATCH_DIM(LAUNCH_E)
+#undef LAUNCH_E
+  };
+  auto filter = [&](int c0, int nc) {
+    dim3 grid(nc * nqf);
+#define LAUNCH_F(DD)                                                                                            \
+  knn_filter_kernel<DD><<<grid, 256, 0, stream>>>((const bf16*)X.data_ptr(), N, (const bf16*)Q.data_ptr(), Qn, \
+                                                  ws_s.data_ptr<float>(), ws_i.data_ptr<int32_t>(), ctrl, cap, c0, \
+                                                  nc)
+    DISPATCH_DIM(LAUNCH_F)
+#undef LAUNCH_F
+  };
+#undef DISPATCH_DIM
+  auto select = [&](int write_thr) {
+    knn_select_kernel<<<(Qn + 3) / 4, 256, 0, stream>>>(ws_s.data_ptr<float>(), ws_i.data_ptr<int32_t>(), ctrl, Qn,
+                                                        cap, (int)K, out_s.data_ptr<float>(),
+                                                        out_i.data_ptr<int32_t>(), write_thr);
+  };
+  const int ns = sample <= 0 ? nchunks : (int)std::min<int64_t>(nchunks, sample);
+  exact(ns);
+  if (ns < nchunks) {
+    select(1);
+    filter(ns, nchunks - ns);
+  }
+  select(0);
 }
+
+int64_t knn_default_sample() { return SAMPLE_CHUNKS; }

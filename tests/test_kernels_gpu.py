@@ -145,6 +145,23 @@ def test_paged_decode_attention(G, nsplit, min_bps):
     _close(got, exp.reshape(B, Hq * D), 0.03, 0.03)
 
 
+def test_paged_decode_attention_wave_per_pair():
+    """B*Hkv >= 2048 takes the one-wave-per-(seq, kv-head) kernel; ragged contexts
+    exercise the masked tail-block loads."""
+    Hkv, G, D = 8, 4, 128
+    Hq = Hkv * G
+    gen = torch.Generator().manual_seed(7)
+    ctx = torch.randint(1, 300, (256,), generator=gen).tolist()
+    B = len(ctx)
+    kc, vc, bt = _random_paged(B, ctx, Hkv, D, DEV, seed=3)
+    q = torch.randn(B, Hq * D, device=DEV, dtype=torch.bfloat16)
+    cl = torch.tensor(ctx, dtype=torch.int32, device=DEV)
+    scale = 1 / math.sqrt(D)
+    got = ops.paged_decode_attention(q, kc, vc, bt, cl, scale, nsplit=1)
+    exp = ref.paged_decode_attention(q.cpu().reshape(B, Hq, D), kc.cpu(), vc.cpu(), bt.cpu(), cl.cpu(), scale)
+    _close(got, exp.reshape(B, Hq * D), 0.03, 0.03)
+
+
 @pytest.mark.parametrize("G", [1, 4, 8])
 def test_paged_prefill_attention(G):
     Hkv, D = 2, 128
@@ -265,7 +282,8 @@ def test_pooling(mode):
 
 
 @pytest.mark.parametrize("N,Qn,k,dup", [(5000, 3, 20, 0), (1024, 20, 5, 0), (10, 2, 20, 0), (70000, 40, 64, 0),
-                                         (100000, 17, 20, 0), (4096, 5, 20, 7), (3000, 4, 64, 50)])
+                                         (100000, 17, 20, 0), (4096, 5, 20, 7), (3000, 4, 64, 50),
+                                         (200000, 256, 20, 0), (50000, 64, 64, 3)])
 def test_knn_topk(N, Qn, k, dup):
     """dup > 0 stores only `dup` distinct rows (massive score ties): exercises the
     K-round fallback behind the threshold + wave-sort fast path."""
@@ -288,6 +306,26 @@ def test_knn_topk(N, Qn, k, dup):
                 assert abs(sc - s[q, j].item()) < 2e-3
             else:
                 assert not valid[q, j]
+
+
+def test_knn_topk_threshold_overflow_and_exact():
+    """Rows get MORE similar to the queries further into the store, so the sample's
+    K-th best is a weak threshold: candidate lists overflow and the search reruns
+    exactly.  Also: the sampled and the all-exact searches return identical answers."""
+    torch.manual_seed(51)
+    N, D, k = 120_000, 384, 20
+    q = torch.nn.functional.normalize(torch.randn(3, D), dim=-1)
+    alpha = torch.linspace(0, 1, N).unsqueeze(1)
+    X = torch.nn.functional.normalize(alpha * q[torch.arange(N) % 3] + 0.5 * torch.randn(N, D), dim=-1)
+    X = X.to(DEV, torch.bfloat16)
+    Q = q.to(DEV, torch.bfloat16)
+    s, i = ops.knn_topk(X, Q, k)
+    es, ei = ref.knn_topk(X.cpu(), Q.cpu(), k)
+    _close(s.cpu(), es, 2e-3)
+    Q2 = torch.nn.functional.normalize(torch.randn(100, D), dim=-1).to(DEV, torch.bfloat16)
+    s1, i1 = ops.knn_topk(X, Q2, k)
+    s0, i0 = ops.knn_topk(X, Q2, k, sample_chunks=0)
+    assert torch.equal(s1, s0) and torch.equal(i1, i0)
 
 
 @pytest.mark.parametrize("M", [1, 37, 64, 256])

@@ -34,7 +34,8 @@ def timeit(fn, iters=50):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--shapes", default="256x448,256x1024,64x2048,16x4096,4x4096,1x4096")
+    ap.add_argument("--shapes", default="256x448,256x410,256x1024,128x448,64x2048,16x4096,4x4096,1x4096")
+    ap.add_argument("--check-all", action="store_true")
     a = ap.parse_args()
     Hq, Hkv, D = 32, 8, 128
     dev, bf = "cuda", torch.bfloat16
@@ -57,8 +58,9 @@ def main():
         us = timeit(lambda: ops.hip().paged_decode_attention(o, q, kc, vc, bt, cl, scale, nsplit, mbps, ws))
         byts = B * ctx * Hkv * D * 2 * 2
         rec = {"B": B, "ctx": ctx, "us": round(us, 2), "TBps": round(byts / us / 1e6, 2),
-               "kernel": "decode_attn_kernel"}
-        if B <= 16:
+               "kernel": "decode_attn_kernel", "wpp": os.environ.get("LS_ATTN_WPP", "auto"),
+               "pipe": os.environ.get("LS_ATTN_PIPE", "1")}
+        if B <= 16 or (a.check_all and B * ctx <= 256 * 1024):
             exp = ref.paged_decode_attention(q.float().cpu().reshape(B, Hq, D), kc.float().cpu(), vc.float().cpu(),
                                              bt.cpu(), cl.cpu(), scale).reshape(B, Hq * D)
             rec["max_err"] = round(float((o.float().cpu() - exp).abs().max()), 4)

@@ -103,17 +103,18 @@ def bench_embed(args):
 def bench_knn(args):
     from langstream_amd import ops
     X = torch.nn.functional.normalize(torch.randn(args.rows, 384, device="cuda"), dim=-1).bfloat16()
-    Q = torch.nn.functional.normalize(torch.randn(args.queries, 384, device="cuda"), dim=-1).bfloat16()
-    for _ in range(3):
-        ops.knn_topk(X, Q, 20)
-    sync()
-    t0 = time.time()
-    for _ in range(20):
-        ops.knn_topk(X, Q, 20)
-    sync()
-    dt = (time.time() - t0) / 20
-    print(json.dumps({"test": "knn", "rows": args.rows, "queries": args.queries, "ms": round(dt * 1000, 3),
-                      "GB_per_s": round(args.rows * 384 * 2 / dt / 1e9, 1)}), flush=True)
+    for nq in str(args.queries).split(","):
+        Q = torch.nn.functional.normalize(torch.randn(int(nq), 384, device="cuda"), dim=-1).bfloat16()
+        for _ in range(3):
+            ops.knn_topk(X, Q, 20)
+        sync()
+        t0 = time.time()
+        for _ in range(20):
+            ops.knn_topk(X, Q, 20)
+        sync()
+        dt = (time.time() - t0) / 20
+        print(json.dumps({"test": "knn", "rows": args.rows, "queries": int(nq), "ms": round(dt * 1000, 3),
+                          "GB_per_s": round(args.rows * 384 * 2 / dt / 1e9, 1)}), flush=True)
 
 
 if __name__ == "__main__":
@@ -128,7 +129,7 @@ if __name__ == "__main__":
     ap.add_argument("--texts", type=int, default=2048)
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--rows", type=int, default=1_000_000)
-    ap.add_argument("--queries", type=int, default=64)
+    ap.add_argument("--queries", default="64", help="comma-separated query counts (knn)")
     a = ap.parse_args()
     for w in a.what.split(","):
         {"llm": bench_llm, "embed": bench_embed, "knn": bench_knn}[w](a)
