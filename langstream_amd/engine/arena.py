@@ -200,14 +200,23 @@ class PyStepExecutor:
                         ctx_len=tt(a["ctx_len"][:nps]) if nps else None,
                         tiles=tt(a["tiles"][:ntiles]) if nps else None)
         rows = None if (h[H_ROWS_ALL] or bucket) else tt(a["rows"][:nrows])
-        logits = self.model.forward_logits(tt(ids), meta, self.kv, rows)
+        tp = self.model.tp
+        vp = tp.world > 1   # vocab-parallel sampling: no logit all-gather
+        logits = self.model.forward_logits(tt(ids), meta, self.kv, rows, local=vp)
         if nrows == 0:
             return
         logits = logits[:nrows].float().clone()
+        voff = self.model.vocab_start if vp else 0
         for r, t, v in a["deltas"][:ndl]:
-            logits[int(r), int(t)] += float(np.array(v, np.int32).view(np.float32))
-        tok, lp, ti, tl = ops.sample(logits, tt(a["temp"][:nrows]), tt(a["top_k"][:nrows]), tt(a["top_p"][:nrows]),
-                                     tt(a["seeds"][:nrows]), tt(a["steps"][:nrows]), n_top=ntop)
+            if 0 <= int(t) - voff < logits.shape[1]:
+                logits[int(r), int(t) - voff] += float(np.array(v, np.int32).view(np.float32))
+        args = (tt(a["temp"][:nrows]), tt(a["top_k"][:nrows]), tt(a["top_p"][:nrows]), tt(a["seeds"][:nrows]),
+                tt(a["steps"][:nrows]))
+        if vp:
+            tok, lp, ti, tl = ops.sample_vocab_parallel(logits, voff, self.model.cfg.vocab_size, *args, n_top=ntop,
+                                                        group=tp.group, world=tp.world)
+        else:
+            tok, lp, ti, tl = ops.sample(logits, *args, n_top=ntop)
         self._tok[:nrows] = tok.cpu().numpy()
         if out is not None:
             out["tok"][:nrows] = self._tok[:nrows]

@@ -86,6 +86,7 @@ class TPInfo:
     rank: int = 0
     world: int = 1
     group: Optional[object] = None
+    force_pg: bool = False   # run the native TP path (collectives, vocab-parallel sampling) even at world 1
 
     def all_reduce(self, t: torch.Tensor) -> torch.Tensor:
         if self.world > 1:
@@ -262,7 +263,7 @@ class LlamaModel:
             return r[1]
         L = self.layers
         pg = None
-        if self.tp.world > 1:
+        if self.tp.world > 1 or self.tp.force_pg:
             pg = self.tp.group if self.tp.group is not None else dist.group.WORLD
         runner = ops.hip().LlamaRunner(
             self.embed, [l.qkv_w for l in L], [l.o_w for l in L], [l.gate_up_w for l in L],
@@ -273,9 +274,10 @@ class LlamaModel:
         return runner
 
     def forward_logits(self, ids: torch.Tensor, meta: AttnMeta, kv_caches: list,
-                       rows: Optional[torch.Tensor] = None) -> torch.Tensor:
+                       rows: Optional[torch.Tensor] = None, local: bool = False) -> torch.Tensor:
         """Forward + LM head for ``rows`` (all rows if None) -> f32 [N, V].  On the GPU
-        the native executor runs it; elsewhere the Python path (same math)."""
+        the native executor runs it; elsewhere the Python path (same math).  local: see
+        ``logits`` (the Python path only; the native executor samples vocab-parallel itself)."""
         if self.device.type == "cuda" and ops.hip_available():
             ws = meta.workspace
             bps = meta.blocks_per_split
@@ -291,15 +293,22 @@ class LlamaModel:
         hidden = self.forward(ids, meta, kv_caches)
         if rows is not None:
             hidden = hidden.index_select(0, rows)
-        return self.logits(hidden)
+        return self.logits(hidden, local=local)
 
-    def logits(self, hidden: torch.Tensor) -> torch.Tensor:
-        """[N, H] -> f32 [N, V] (vocab-parallel matmul + all-gather under TP)."""
+    def local_vocab(self) -> int:
+        """Valid vocabulary entries of this rank's LM-head slice."""
+        return max(0, min(self.vocab_per_rank, self.cfg.vocab_size - self.vocab_start))
+
+    def logits(self, hidden: torch.Tensor, local: bool = False) -> torch.Tensor:
+        """[N, H] -> f32 [N, V] (vocab-parallel matmul + all-gather under TP).  local=True
+        under TP: this rank's [N, local_vocab()] slice (ops.sample_vocab_parallel)."""
         if hidden.is_cuda and hidden.dtype != torch.float32:
             # f32 output from the GEMM itself (same as the native runner's LM head)
             lg = torch.mm(hidden, self.lm_head.t(), out_dtype=torch.float32)
         else:
             lg = F.linear(hidden, self.lm_head).float()
         if self.tp.world > 1:
+            if local:
+                return lg[:, : self.local_vocab()]
             lg = self.tp.all_gather_last(lg)
         return lg[:, : self.cfg.vocab_size]

@@ -315,6 +315,78 @@ def sample(logits, temperature, top_k, top_p, seeds, steps, n_top: int = 0):
     return tok, lp, None, None
 
 
+def sample_vocab_parallel(local, vstart: int, vocab: int, temperature, top_k, top_p, seeds, steps, n_top: int = 0,
+                          group=None, world: int = 1):
+    """``sample`` over vocab-sharded logits (tensor parallelism): ``local`` is this rank's
+    f32 [R, Vl] slice starting at global token ``vstart``.  Exchanges per-row statistics,
+    top-k/top-p histograms and candidates instead of the logit rows (sampling.hip), and
+    returns the same (tokens, logprobs, top_ids, top_lps) on every rank."""
+    import torch.distributed as dist
+    R = local.shape[0]
+    if _gpu(local):
+        dev = local.device
+        h = hip()
+        local = local.float().contiguous()
+        stats = torch.empty(R * 4, dtype=torch.float32, device=dev)
+        h.tp_sample_stats(local, vstart, stats)
+        stats_all = torch.empty(world * R * 4, dtype=torch.float32, device=dev)
+        dist.all_gather_into_tensor(stats_all, stats, group=group)
+        hist = torch.empty(R * 2 * 1024, dtype=torch.int64, device=dev)
+        h.tp_sample_hist(local, vocab, temperature, top_k, top_p, stats_all, world, hist)
+        dist.all_reduce(hist, group=group)
+        cw = 3 + 2 * n_top
+        cand = torch.empty(R * cw, dtype=torch.float32, device=dev)
+        h.tp_sample_pick(local, vstart, vocab, temperature, top_k, top_p, seeds, steps, stats_all, world, hist,
+                         n_top, cand)
+        cand_all = torch.empty(world * R * cw, dtype=torch.float32, device=dev)
+        dist.all_gather_into_tensor(cand_all, cand, group=group)
+        tok = torch.empty(R, dtype=torch.int32, device=dev)
+        lp = torch.empty(R, dtype=torch.float32, device=dev)
+        ti = torch.empty(R * max(n_top, 1), dtype=torch.int32, device=dev)
+        tl = torch.empty(R * max(n_top, 1), dtype=torch.float32, device=dev)
+        h.tp_sample_final(stats_all, cand_all, world, R, temperature, n_top, tok, lp, ti, tl)
+        if n_top:
+            return tok, lp, ti.view(R, n_top), tl.view(R, n_top)
+        return tok, lp, None, None
+    # CPU (gloo): exact greedy tokens, log-probs and top-n from exchanged row statistics;
+    # rows that sample gather their full logit rows and use the reference sampler.
+    lf = local.float()
+    mx, am = lf.max(dim=-1)
+    lse = torch.logsumexp(lf, dim=-1)
+    st = torch.stack([mx, (am + vstart).double().float(), lse], -1).contiguous()
+    parts = [torch.empty_like(st) for _ in range(world)]
+    dist.all_gather(parts, st, group=group)
+    allst = torch.stack(parts)                                  # [W, R, 3]
+    logZ = torch.logsumexp(allst[..., 2], dim=0)
+    w_best = allst[..., 0].argmax(dim=0)                        # first rank wins ties = lower index
+    rr = torch.arange(R)
+    tok = allst[w_best, rr, 1].round().long()
+    lp = allst[w_best, rr, 0] - logZ
+    sampled = (temperature.float() > 0).cpu()
+    if bool(sampled.any()):
+        idx = sampled.nonzero()[:, 0]
+        rows = lf.index_select(0, idx).contiguous()
+        rparts = [torch.empty_like(rows) for _ in range(world)]
+        dist.all_gather(rparts, rows, group=group)
+        full = torch.cat(rparts, -1)[:, :vocab]
+        t2, l2, _, _ = sample(full, temperature[idx], top_k[idx], top_p[idx], seeds[idx], steps[idx])
+        tok[idx] = t2.long()
+        lp[idx] = l2.float()
+    ti = tl = None
+    if n_top:
+        v, i = torch.topk(lf, min(n_top, lf.shape[1]), dim=-1)
+        c = torch.cat([v, (i + vstart).float()], -1).contiguous()
+        cparts = [torch.empty_like(c) for _ in range(world)]
+        dist.all_gather(cparts, c, group=group)
+        k = v.shape[1]
+        vs = torch.cat([p[:, :k] for p in cparts], -1)
+        ids = torch.cat([p[:, k:] for p in cparts], -1)
+        tv, pos = torch.topk(vs, n_top, dim=-1)
+        ti = ids.gather(1, pos).round().int()
+        tl = tv - logZ[:, None]
+    return tok.int(), lp, ti, tl
+
+
 def apply_logit_deltas(logits, rows, toks, delta):
     if _gpu(logits):
         hip().apply_logit_deltas(logits, rows, toks, delta)

@@ -25,6 +25,14 @@ void sample_tokens(at::Tensor logits, at::Tensor temperature, at::Tensor top_k, 
 void apply_logit_deltas(at::Tensor logits, at::Tensor rows, at::Tensor toks, at::Tensor delta);
 void pool_embeddings(at::Tensor out, at::Tensor x, at::Tensor start, at::Tensor len, int64_t mode, bool normalize);
 void l2_normalize_rows(at::Tensor out, at::Tensor x);
+void tp_sample_stats(at::Tensor logits, int64_t vstart, at::Tensor stats);
+void tp_sample_hist(at::Tensor logits, int64_t vtot, at::Tensor temperature, at::Tensor top_k, at::Tensor top_p,
+                    at::Tensor stats_all, int64_t world, at::Tensor hist);
+void tp_sample_pick(at::Tensor logits, int64_t vstart, int64_t vtot, at::Tensor temperature, at::Tensor top_k,
+                    at::Tensor top_p, at::Tensor seeds, at::Tensor steps, at::Tensor stats_all, int64_t world,
+                    at::Tensor hist_all, int64_t n_top, at::Tensor cand);
+void tp_sample_final(at::Tensor stats_all, at::Tensor cand_all, int64_t world, int64_t rows, at::Tensor temperature,
+                     int64_t n_top, at::Tensor out_tok, at::Tensor out_lp, at::Tensor top_ids, at::Tensor top_lps);
 void knn_topk(at::Tensor X, at::Tensor Q, int64_t K, at::Tensor out_s, at::Tensor out_i, at::Tensor ws_s,
               at::Tensor ws_i, int64_t sample);
 int64_t knn_default_sample();
@@ -68,6 +76,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("pool_embeddings", &pool_embeddings);
   m.def("l2_normalize_rows", &l2_normalize_rows);
   m.def("knn_topk", &knn_topk);
+  m.def("tp_sample_stats", &tp_sample_stats);
+  m.def("tp_sample_hist", &tp_sample_hist);
+  m.def("tp_sample_pick", &tp_sample_pick);
+  m.def("tp_sample_final", &tp_sample_final);
   m.def("knn_default_sample", &knn_default_sample);
   m.def("skinny_gemm", &skinny_gemm);
   m.def("gemv", &gemv);

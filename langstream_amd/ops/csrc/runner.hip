@@ -60,6 +60,14 @@ void pool_embeddings(at::Tensor out, at::Tensor x, at::Tensor start, at::Tensor 
 void sample_tokens(at::Tensor logits, at::Tensor temperature, at::Tensor top_k, at::Tensor top_p, at::Tensor seeds,
                    at::Tensor steps, at::Tensor out_tok, at::Tensor out_lp, at::Tensor top_ids, at::Tensor top_lps,
                    int64_t n_top);
+void tp_sample_stats(at::Tensor logits, int64_t vstart, at::Tensor stats);
+void tp_sample_hist(at::Tensor logits, int64_t vtot, at::Tensor temperature, at::Tensor top_k, at::Tensor top_p,
+                    at::Tensor stats_all, int64_t world, at::Tensor hist);
+void tp_sample_pick(at::Tensor logits, int64_t vstart, int64_t vtot, at::Tensor temperature, at::Tensor top_k,
+                    at::Tensor top_p, at::Tensor seeds, at::Tensor steps, at::Tensor stats_all, int64_t world,
+                    at::Tensor hist_all, int64_t n_top, at::Tensor cand);
+void tp_sample_final(at::Tensor stats_all, at::Tensor cand_all, int64_t world, int64_t rows, at::Tensor temperature,
+                     int64_t n_top, at::Tensor out_tok, at::Tensor out_lp, at::Tensor top_ids, at::Tensor top_lps);
 
 void skinny_gemm(at::Tensor out, at::Tensor x, at::Tensor w);
 void gemm_fused(at::Tensor out, at::Tensor x, at::Tensor w, c10::optional<at::Tensor> bias, bool gelu,
@@ -127,7 +135,7 @@ class LlamaRunner {
                           const at::Tensor& d_bt, const at::Tensor& d_ctx, int64_t nsplit, int64_t bps,
                           const at::Tensor& ws, int64_t num_prefill, const at::Tensor& p_bt, const at::Tensor& q_start,
                           const at::Tensor& q_len, const at::Tensor& ctx_len, const at::Tensor& tiles,
-                          const c10::optional<at::Tensor>& rows) {
+                          const c10::optional<at::Tensor>& rows, bool gather_logits = true) {
     const int64_t T = ids.size(0);
     at::Tensor h = embed(ids);
     at::Tensor residual = h;
@@ -266,6 +274,11 @@ class LlamaRunner {
     }
     at::Tensor sel = rows.has_value() ? x.index_select(0, *rows) : x;
     at::Tensor lg = lm_head(sel);
+    if (pg_ && !gather_logits) {
+      // vocab-parallel sampling downstream: this rank's valid slice only
+      const int64_t valid = std::max<int64_t>(0, std::min<int64_t>(lg.size(1), vocab_ - vocab_start_));
+      return valid == lg.size(1) ? lg : lg.narrow(1, 0, valid);
+    }
     if (pg_) {
       const int64_t world = pg_->getSize();
       std::vector<at::Tensor> parts;
@@ -298,6 +311,7 @@ class LlamaRunner {
   int64_t hq() const { return hq_; }
   int64_t head_dim() const { return d_; }
   int64_t vocab() const { return vocab_; }
+  int64_t vocab_start() const { return vocab_start_; }
   c10::intrusive_ptr<::c10d::ProcessGroup> pg() const { return pg_; }
 
  private:
@@ -469,11 +483,13 @@ __global__ void gather_feedback_kernel(int32_t* __restrict__ ids, const int64_t*
 }
 
 // logits[row, tok] += val for each (row, tok, val) triple, count read on the device.
+// Under TP the logits are this rank's vocabulary slice starting at voff.
 __global__ void logit_delta_kernel(float* __restrict__ logits, int64_t ld, int V, int nrows,
-                                   const int32_t* __restrict__ trip, const int32_t* __restrict__ hdr, int cap) {
+                                   const int32_t* __restrict__ trip, const int32_t* __restrict__ hdr, int cap,
+                                   int voff) {
   const int n = min(hdr[H_NDELTA], cap);
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    const int r = trip[3 * i], t = trip[3 * i + 1];
+    const int r = trip[3 * i], t = trip[3 * i + 1] - voff;
     const float v = __int_as_float(trip[3 * i + 2]);
     if (r >= 0 && r < nrows && t >= 0 && t < V) atomicAdd(&logits[(int64_t)r * ld + t], v);
   }
@@ -514,6 +530,14 @@ class StepExecutor {
     tl_ = at::zeros({maxS_ * kMaxTop}, dev.dtype(at::kFloat));
     ws_ = at::empty({std::max<int64_t>(1, maxS_ * r_->hq() * nsplit_ * (r_->head_dim() + 2))},
                     dev.dtype(at::kFloat));
+    if (r_->pg()) {   // vocab-parallel sampling exchange buffers (tp_sample_* in sampling.hip)
+      const int64_t W = r_->pg()->getSize(), cw = 3 + 2 * kMaxTop;
+      tp_stats_ = at::zeros({maxS_ * 4}, dev.dtype(at::kFloat));
+      tp_stats_all_ = at::zeros({W * maxS_ * 4}, dev.dtype(at::kFloat));
+      tp_hist_ = at::zeros({maxS_ * 2 * 1024}, dev.dtype(at::kLong));
+      tp_cand_ = at::zeros({maxS_ * cw}, dev.dtype(at::kFloat));
+      tp_cand_all_ = at::zeros({W * maxS_ * cw}, dev.dtype(at::kFloat));
+    }
     pool_ = at::cuda::graph_pool_handle();
   }
 
@@ -670,19 +694,56 @@ class StepExecutor {
     at::Tensor tiles = view<int32_t>("tiles", std::max<int64_t>(ntiles, 1) * 2, at::kInt).view({-1, 2});
     c10::optional<at::Tensor> rows;
     if (!rows_all) rows = view<int64_t>("rows", nrows, at::kLong);
+    const bool tp = (bool)r_->pg();
     at::Tensor logits = r_->forward_impl(ids, pos, slots, nd, dbt, dctx, nsplit_, std::min(bps_, maxB_), ws_,
-                                         T - nd, pbt, qs, ql, cl, tiles, rows);
+                                         T - nd, pbt, qs, ql, cl, tiles, rows, /*gather_logits=*/!tp);
     last_logits_ = logits;
     if (nrows == 0) return;
     const int V = (int)logits.size(1);
     logit_delta_kernel<<<(int)std::max<int64_t>(1, std::min<int64_t>((maxD_ + 255) / 256, 1024)), 256, 0,
                          stream()>>>(logits.data_ptr<float>(), logits.stride(0), V, (int)logits.size(0),
                                      reinterpret_cast<const int32_t*>((char*)arena_.data_ptr() + off_.at("deltas")),
-                                     dh, (int)maxD_);
+                                     dh, (int)maxD_, tp ? (int)r_->vocab_start() : 0);
     at::Tensor lg = logits.narrow(0, 0, nrows);
-    sample_tokens(lg, view<float>("temp", nrows, at::kFloat), view<int32_t>("top_k", nrows, at::kInt),
-                  view<float>("top_p", nrows, at::kFloat), view<int64_t>("seeds", nrows, at::kLong),
-                  view<int64_t>("steps", nrows, at::kLong), tok_, lp_, ti_, tl_, ntop);
+    at::Tensor temp = view<float>("temp", nrows, at::kFloat), topk = view<int32_t>("top_k", nrows, at::kInt);
+    at::Tensor topp = view<float>("top_p", nrows, at::kFloat), seeds = view<int64_t>("seeds", nrows, at::kLong);
+    at::Tensor steps = view<int64_t>("steps", nrows, at::kLong);
+    if (!tp) {
+      sample_tokens(lg, temp, topk, topp, seeds, steps, tok_, lp_, ti_, tl_, ntop);
+      return;
+    }
+    sample_vocab_parallel(lg, temp, topk, topp, seeds, steps, nrows, ntop);
+  }
+
+  // Vocab-parallel sampling: four tp_sample_* phases with an all-gather of [R, 4] row
+  // statistics, an all-reduce of the [R, 2, 1024] top-k/top-p histograms and an
+  // all-gather of [R, 3 + 2 n] candidates, instead of all-gathering f32 logit rows
+  // ([R, vocab] x 4 B: 128 MiB per step at R = 256 on Llama-3).  Same tokens as the
+  // single-GPU sampler on the same logits (sampling.hip).
+  void sample_vocab_parallel(const at::Tensor& lg, const at::Tensor& temp, const at::Tensor& topk,
+                             const at::Tensor& topp, const at::Tensor& seeds, const at::Tensor& steps, int64_t R,
+                             int64_t ntop) {
+    auto pg = r_->pg();
+    const int64_t W = pg->getSize(), cw = 3 + 2 * ntop;
+    auto gather = [&](const at::Tensor& src, const at::Tensor& dst, int64_t per) {
+      std::vector<at::Tensor> parts;
+      for (int64_t w = 0; w < W; ++w) parts.push_back(dst.narrow(0, w * per, per));
+      std::vector<std::vector<at::Tensor>> outs{parts};
+      std::vector<at::Tensor> ins{src.narrow(0, 0, per)};
+      pg->allgather(outs, ins)->wait();
+    };
+    at::Tensor stats = tp_stats_.narrow(0, 0, R * 4), stats_all = tp_stats_all_.narrow(0, 0, W * R * 4);
+    tp_sample_stats(lg, r_->vocab_start(), stats);
+    gather(tp_stats_, stats_all, R * 4);
+    at::Tensor hist = tp_hist_.narrow(0, 0, R * 2 * 1024);
+    tp_sample_hist(lg, r_->vocab(), temp, topk, topp, stats_all, W, hist);
+    std::vector<at::Tensor> hv{hist};
+    pg->allreduce(hv)->wait();
+    at::Tensor cand_all = tp_cand_all_.narrow(0, 0, W * R * cw);
+    tp_sample_pick(lg, r_->vocab_start(), r_->vocab(), temp, topk, topp, seeds, steps, stats_all, W, hist, ntop,
+                   tp_cand_);
+    gather(tp_cand_, cand_all, R * cw);
+    tp_sample_final(stats_all, cand_all, W, R, temp, ntop, tok_, lp_, ti_, tl_);
   }
 
   void run(const int32_t* h) {
@@ -764,6 +825,7 @@ class StepExecutor {
   std::vector<hipEvent_t> in_ev_, out_ev_;
   std::vector<bool> in_used_;
   at::Tensor arena_, hdr_small_, tok_, lp_, ti_, tl_, ws_, last_logits_;
+  at::Tensor tp_stats_, tp_stats_all_, tp_hist_, tp_cand_, tp_cand_all_;
   std::map<int64_t, std::unique_ptr<at::cuda::CUDAGraph>> graphs_;
   std::map<int64_t, at::Tensor> graph_logits_;
   at::cuda::MempoolId_t pool_;

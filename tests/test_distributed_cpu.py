@@ -82,11 +82,11 @@ def _dp_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def _spawn(fn, world=2):
+def _spawn(fn, world=2, *extra):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    procs = [ctx.Process(target=fn, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=fn, args=(r, world, port, q, *extra)) for r in range(world)]
     for p in procs:
         p.start()
     try:
@@ -112,15 +112,24 @@ def _small_full():
     return LlamaModel(PRESETS["llama-small"], device="cpu", dtype=torch.float32, seed=9)
 
 
-def _small_run(model):
+def _small_run(model, sampled=False):
     from langstream_amd.engine.llm_engine import LLMEngine, SamplingParams
     eng = LLMEngine(model, None, num_blocks=32, max_model_len=512)
-    sp = SamplingParams(max_tokens=4, temperature=0.0, ignore_eos=True, logprobs=2)
-    res = [(r.output_ids, r.output_logprobs) for r in eng.generate(SMALL_PROMPTS, sp)]
+    if sampled:
+        sp = SamplingParams(max_tokens=6, temperature=0.9, top_k=40, top_p=0.9, seed=123, ignore_eos=True,
+                            logprobs=3)
+    else:
+        sp = SamplingParams(max_tokens=4, temperature=0.0, ignore_eos=True, logprobs=2)
+    tops = {}
+    reqs = [eng.submit(p, sp, callback=lambda ev: tops.setdefault(ev.request_id, []).append(ev.top))
+            for p in SMALL_PROMPTS]
+    while not all(r.finished for r in reqs):
+        eng.step()
+    res = [(r.output_ids, r.output_logprobs, tops.get(r.request_id)) for r in reqs]
     return eng, res
 
 
-def _tp_small_worker(rank, world, port, q):
+def _tp_small_worker(rank, world, port, q, sampled=False):
     """llama-small sharded TP=world (KV heads replicated when world > 2); rank 0 reports
     tokens + logprobs."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -132,7 +141,7 @@ def _tp_small_worker(rank, world, port, q):
         m = LlamaModel(cfg, device="cpu", dtype=torch.float32, tp=TPInfo(rank, world, None))
         m.load_state_dict(shard_llama(_small_full().state_dict(), cfg, rank, world))
         if rank == 0:
-            eng, res = _small_run(m)
+            eng, res = _small_run(m, sampled)
             eng.stop()
             q.put(res)
         else:
@@ -142,15 +151,32 @@ def _tp_small_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 4])
-def test_tp_llama_small_logprobs_match_tp1(world):
-    """TP=2 and TP=4 (2 KV heads -> replicated at TP=4) greedy tokens and their logprobs
-    equal the TP=1 engine on the same full weights."""
-    _, ref_res = _small_run(_small_full())
-    got = _spawn(_tp_small_worker, world)
-    for (ids_a, lp_a), (ids_b, lp_b) in zip(got, ref_res):
+@pytest.mark.parametrize("world,sampled", [(2, False), (4, False), (2, True)])
+def test_tp_llama_small_logprobs_match_tp1(world, sampled):
+    """TP=2 and TP=4 (2 KV heads -> replicated at TP=4) tokens, their logprobs and the
+    top-n alternatives equal the TP=1 engine on the same full weights -- greedy, and
+    seeded top-k/top-p sampling.  The TP engine never all-gathers full logit rows for
+    greedy rows: ops.sample_vocab_parallel exchanges row statistics and candidates."""
+    _, ref_res = _small_run(_small_full(), sampled)
+    got = _spawn(_tp_small_worker, world, sampled)
+    for (ids_a, lp_a, top_a), (ids_b, lp_b, top_b) in zip(got, ref_res):
         assert ids_a == ids_b
         assert max(abs(a - b) for a, b in zip(lp_a, lp_b)) < 1e-3
+        if top_b is not None:
+            assert _top_close(top_a, top_b)
+
+
+def _top_close(a, b) -> bool:
+    """Per-step top-n alternatives [(token_id, logprob)]: same ids, log-probs within 1e-3."""
+    if a is None or b is None or len(a) != len(b):
+        return False
+    for sa, sb in zip(a, b):
+        if len(sa) != len(sb):
+            return False
+        for (ka, va), (kb, vb) in zip(sa, sb):
+            if ka != kb or abs(float(va) - float(vb)) > 1e-3:
+                return False
+    return True
 
 
 def test_data_parallel_replicas_match_single():

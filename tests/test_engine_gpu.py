@@ -162,3 +162,44 @@ def test_vector_store_search():
     assert res[1][0]["id"] == 100
     assert abs(res[0][0]["similarity"] - 1.0) < 1e-2
     assert vs.search(v[[5]], k=1)[0][0]["id"] != 5
+
+
+def test_native_executor_tp_path_world1_rccl():
+    """The TP code path of the native executor at world size 1 over a real RCCL process
+    group: all-reduces inside the graph-captured forward, and the vocab-parallel sampler
+    (statistics / histogram / candidate exchanges) instead of the single-GPU sampler.
+    Same greedy tokens and log-probs as the non-TP executor on the same weights."""
+    import socket
+    import torch.distributed as dist
+    from langstream_amd.models.llama import TPInfo
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    try:
+        cfg = PRESETS["llama-small"]
+        m0 = LlamaModel(cfg, device="cuda")
+        m1 = LlamaModel(cfg, device="cuda", tp=TPInfo(0, 1, None, force_pg=True))
+        m1.load_state_dict(m0.state_dict())
+        prompts = [list(range(3, 3 + n)) for n in (5, 33, 64, 200)]
+        e0 = LLMEngine(m0, None, num_blocks=128, max_model_len=1024, max_batch=8)
+        e1 = LLMEngine(m1, None, num_blocks=128, max_model_len=1024, max_batch=8)
+        e1.capture_graphs()
+        a, b = _first_token_tops(e0, prompts, 5), _first_token_tops(e1, prompts, 5)
+        for x, y in zip(a, b):
+            assert x.token_id == y.token_id
+            assert abs(x.logprob - y.logprob) < 0.05
+            assert [t for t, _ in x.top[:2]] == [t for t, _ in y.top[:2]]
+        sp = SamplingParams(max_tokens=8, temperature=0.0, ignore_eos=True)
+        out0 = [r.output_ids for r in e0.generate(prompts, sp)]
+        out1 = [r.output_ids for r in e1.generate(prompts, sp)]
+        assert e1.stats["graph_steps"] > 0
+        for x, y in zip(out0, out1):
+            assert x[:4] == y[:4]
+        spr = SamplingParams(max_tokens=8, temperature=0.8, top_k=20, top_p=0.9, seed=5, ignore_eos=True)
+        for r in e1.generate(prompts, spr):
+            assert len(r.output_ids) == 8 and all(0 <= t < cfg.vocab_size for t in r.output_ids)
+        e0.stop()
+        e1.stop()
+    finally:
+        dist.destroy_process_group()

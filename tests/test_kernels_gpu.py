@@ -593,3 +593,49 @@ def test_tp8_gate_up_shard_silu(M):
         out2 = torch.empty(M, F, device=DEV, dtype=torch.bfloat16)
         ops.hip().gemv_silu(out2, x, w)
         _close(out2, exp, 0.03, 0.03, "gemv silu")
+
+
+@pytest.mark.parametrize("W", [2, 3, 8])
+def test_vocab_parallel_sampling_matches_single_gpu_sampler(W):
+    """The four tp_sample_* phases (sampling.hip), run per vocabulary slice with the
+    exchanges done in torch (all-gather = concatenation, all-reduce = sum), reproduce the
+    single-GPU sampler on the full rows: greedy and seeded top-k / top-p tokens, token
+    log-probs and the top-n alternatives."""
+    torch.manual_seed(60 + W)
+    R, V, n_top = 37, 32005, 5
+    h = ops.hip()
+    logits = (torch.randn(R, V) * 3).to(DEV)
+    temp = torch.tensor([0.0, 0.7, 1.0, 1.3] * 10, dtype=torch.float32)[:R].to(DEV)
+    top_k = torch.tensor([0, 40, 0, 1, 7] * 8, dtype=torch.int32)[:R].to(DEV)
+    top_p = torch.tensor([1.0, 0.9, 0.5] * 13, dtype=torch.float32)[:R].to(DEV)
+    seeds = torch.randint(0, 1 << 30, (R,), dtype=torch.int64).to(DEV)
+    steps = torch.randint(0, 100, (R,), dtype=torch.int64).to(DEV)
+    tok, lp, ti, tl = ops.sample(logits, temp, top_k, top_p, seeds, steps, n_top=n_top)
+    per = (V + W - 1) // W
+    sl = [(w * per, min(V, (w + 1) * per)) for w in range(W)]
+    parts = [logits[:, a:b].contiguous() for a, b in sl]
+    stats = []
+    for (a, _), p in zip(sl, parts):
+        st = torch.empty(R * 4, device=DEV)
+        h.tp_sample_stats(p, a, st)
+        stats.append(st)
+    stats_all = torch.cat(stats)
+    hist = torch.zeros(R * 2 * 1024, dtype=torch.int64, device=DEV)
+    for p in parts:
+        hh = torch.empty_like(hist)
+        h.tp_sample_hist(p, V, temp, top_k, top_p, stats_all, W, hh)
+        hist += hh
+    cands = []
+    for (a, _), p in zip(sl, parts):
+        c = torch.empty(R * (3 + 2 * n_top), device=DEV)
+        h.tp_sample_pick(p, a, V, temp, top_k, top_p, seeds, steps, stats_all, W, hist, n_top, c)
+        cands.append(c)
+    tok2 = torch.empty(R, dtype=torch.int32, device=DEV)
+    lp2 = torch.empty(R, device=DEV)
+    ti2 = torch.empty(R * n_top, dtype=torch.int32, device=DEV)
+    tl2 = torch.empty(R * n_top, device=DEV)
+    h.tp_sample_final(stats_all, torch.cat(cands), W, R, temp, n_top, tok2, lp2, ti2, tl2)
+    assert torch.equal(tok.cpu(), tok2.cpu())
+    assert (lp.cpu() - lp2.cpu()).abs().max() < 1e-4
+    assert torch.equal(ti.cpu(), ti2.view(R, n_top).cpu())
+    assert (tl.cpu() - tl2.view(R, n_top).cpu()).abs().max() < 1e-4
