@@ -38,6 +38,10 @@
 // profiles/decode_attn_*_r2i.log), B=256:
 //   ctx 448: 89.8 us (flat loads, r1) -> 84.3 (buffer loads) -> 80.0 us = 5.9 TB/s
 //            (WPP=1 + PIPE); ctx 1024: 176 us = 6.1 TB/s; ctx 410 (ragged tail) 77 us.
+// Ragged contexts (uniform +-30 %) cost ~12 % at WPP=1 (the launch ends with the
+// longest sequence: 2048 waves fill the 2048 slots, nothing rebalances) and ~11 % at
+// WPP=4; forcing 2-3 KV splits to rebalance was slower still (107 vs 94 us,
+// profiles/decode_attn_ragged_split_ab_r2i.log).
 // Rejected: nt loads (+7%, back-to-back replays lose the L2/MALL reuse), a select on
 // the loaded data for the tail mask (139 us: each load waited before the next issued),
 // next-block prefetch into extra registers (1 wave/SIMD, 103 us), 125 VGPRs / 4 waves

@@ -76,6 +76,33 @@ def test_native_runner_matches_python_forward():
         assert _cos(a[i], b[i]) > 0.999
 
 
+def _run_tops(e: LLMEngine, prompts, sp: SamplingParams):
+    """Run to completion; per request the output ids and each step's top-2 alternatives."""
+    tops = {}
+    reqs = [e.submit(p, sp, callback=lambda ev, i=i: tops.setdefault(i, []).append(ev.top))
+            for i, p in enumerate(prompts)]
+    while not all(r.finished for r in reqs):
+        e.step()
+    e._flush()
+    return [(r.output_ids, tops[i]) for i, r in enumerate(reqs)]
+
+
+def _same_or_near_tie(a, b, gap: float = 0.1) -> None:
+    """Greedy sequences from two bf16 paths agree over their WHOLE length, except that
+    they may part at a genuine near-tie: at the first differing position both tokens are
+    in b's top-2 and within `gap` nats of each other (random-init weights have top-2 gaps
+    of ~1e-3 nats, so rounding may flip argmax there).  After such a split the sequences
+    condition on different tokens and are not compared."""
+    (ids_a, _), (ids_b, tops_b) = a, b
+    assert len(ids_a) == len(ids_b)
+    for t, (x, y) in enumerate(zip(ids_a, ids_b)):
+        if x == y:
+            continue
+        alt = dict(tops_b[t])
+        assert x in alt and y in alt and abs(alt[x] - alt[y]) < gap, (t, x, y, tops_b[t])
+        return
+
+
 def test_native_executor_matches_python_executor():
     """Whole-step native executor (arena upload, feedback gather, graphs, sampling)
     against the Python executor driving the same model on the same GPU."""
@@ -84,29 +111,31 @@ def test_native_executor_matches_python_executor():
     cfg = PRESETS["llama-small"]
     model = LlamaModel(cfg, device="cuda")
     prompts = [list(range(3, 3 + n)) for n in (5, 33, 64, 65, 200)]
-    sp = SamplingParams(max_tokens=10, temperature=0.0, ignore_eos=True)
+    sp = SamplingParams(max_tokens=16, temperature=0.0, ignore_eos=True, logprobs=2)
     e1 = LLMEngine(model, None, num_blocks=128, max_model_len=1024, max_batch=8)
-    out1 = [r.output_ids for r in e1.generate(prompts, sp)]
+    out1 = _run_tops(e1, prompts, sp)
     assert e1.stats["graph_steps"] > 0
     e2 = LLMEngine(model, None, num_blocks=128, max_model_len=1024, max_batch=8, use_graphs=False)
     e2.exec = PyStepExecutor(model, e2.kv_caches, e2.layout, NSLOTS, e2.nsplit, e2.bps, e2.device)
-    out2 = [r.output_ids for r in e2.generate(prompts, sp)]
+    out2 = _run_tops(e2, prompts, sp)
     for a, b in zip(out1, out2):
-        assert a[:4] == b[:4]
+        _same_or_near_tie(a, b)
 
 
 def test_llama_graph_decode_matches_eager():
     cfg = PRESETS["llama-small"]
     model = LlamaModel(cfg, device="cuda")
     prompts = [list(range(3, 3 + n)) for n in (5, 33, 64, 65, 200)]
-    sp = SamplingParams(max_tokens=12, temperature=0.0, ignore_eos=True)
+    sp = SamplingParams(max_tokens=24, temperature=0.0, ignore_eos=True, logprobs=2)
     e1 = LLMEngine(model, None, num_blocks=128, max_model_len=1024, use_graphs=True, max_batch=8)
-    out1 = [r.output_ids for r in e1.generate(prompts, sp)]
+    out1 = _run_tops(e1, prompts, sp)
+    assert e1.stats["graph_steps"] > 0
     e2 = LLMEngine(model, None, num_blocks=128, max_model_len=1024, use_graphs=False, max_batch=8)
-    out2 = [r.output_ids for r in e2.generate(prompts, sp)]
-    # greedy decode with bf16: allow a late divergence on near-ties, first tokens must agree
+    out2 = _run_tops(e2, prompts, sp)
+    # the same kernels replayed from a graph: identical over the whole length (a split
+    # is only tolerated at a genuine near-tie)
     for a, b in zip(out1, out2):
-        assert a[:4] == b[:4]
+        _same_or_near_tie(a, b, gap=0.02)
 
 
 def test_llama_chunked_prefill_consistent():
@@ -190,12 +219,12 @@ def test_native_executor_tp_path_world1_rccl():
             assert x.token_id == y.token_id
             assert abs(x.logprob - y.logprob) < 0.05
             assert [t for t, _ in x.top[:2]] == [t for t, _ in y.top[:2]]
-        sp = SamplingParams(max_tokens=8, temperature=0.0, ignore_eos=True)
-        out0 = [r.output_ids for r in e0.generate(prompts, sp)]
-        out1 = [r.output_ids for r in e1.generate(prompts, sp)]
+        sp = SamplingParams(max_tokens=12, temperature=0.0, ignore_eos=True, logprobs=2)
+        out1 = _run_tops(e1, prompts, sp)
+        out0 = _run_tops(e0, prompts, sp)
         assert e1.stats["graph_steps"] > 0
-        for x, y in zip(out0, out1):
-            assert x[:4] == y[:4]
+        for x, y in zip(out1, out0):
+            _same_or_near_tie(x, y)
         spr = SamplingParams(max_tokens=8, temperature=0.8, top_k=20, top_p=0.9, seed=5, ignore_eos=True)
         for r in e1.generate(prompts, spr):
             assert len(r.output_ids) == 8 and all(0 <= t < cfg.vocab_size for t in r.output_ids)

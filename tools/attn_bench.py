@@ -36,31 +36,49 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--shapes", default="256x448,256x410,256x1024,128x448,64x2048,16x4096,4x4096,1x4096")
     ap.add_argument("--check-all", action="store_true")
+    ap.add_argument("--ragged", type=float, default=0.0,
+                    help="per-sequence context drawn uniformly from ctx*(1 +- ragged) (mean ctx)")
+    ap.add_argument("--pool-gb", type=float, default=0.0,
+                    help="scatter the blocks over a KV pool of this size (TLB reach), like a real engine")
     a = ap.parse_args()
     Hq, Hkv, D = 32, 8, 128
     dev, bf = "cuda", torch.bfloat16
     nsplit, mbps = ops.decode_splits(64)
     for shp in a.shapes.split(","):
         B, ctx = (int(x) for x in shp.split("x"))
-        nb = (ctx + 63) // 64
-        # blocks scattered over a pool 2x the live size (like a busy engine)
-        pool = 2 * B * nb
         g = torch.Generator(device="cpu").manual_seed(0)
+        if a.ragged > 0:
+            lo, hi = int(ctx * (1 - a.ragged)), int(ctx * (1 + a.ragged))
+            ctxs = torch.randint(max(1, lo), hi + 1, (B,), generator=g)
+        else:
+            ctxs = torch.full((B,), ctx)
+        nb = int((ctxs.max() + 63) // 64)
+        # blocks scattered over a pool 2x the live size (like a busy engine), or --pool-gb
+        blk_bytes = Hkv * 64 * D * 2 * 2
+        pool = max(2 * B * nb, int(a.pool_gb * 1e9 // blk_bytes))
         perm = torch.randperm(pool, generator=g)[: B * nb].to(torch.int32)
         bt = perm.view(B, nb).to(dev)
-        kc = torch.randn(pool, Hkv, 64, D, device=dev, dtype=bf)
-        vc = torch.randn(pool, Hkv, D, 64, device=dev, dtype=bf)
-        cl = torch.full((B,), ctx, device=dev, dtype=torch.int32)
+        if pool > 2 * B * nb:
+            kc = torch.zeros(pool, Hkv, 64, D, device=dev, dtype=bf)
+            vc = torch.zeros(pool, Hkv, D, 64, device=dev, dtype=bf)
+            idx = perm.long().to(dev)
+            kc[idx] = torch.randn(len(idx), Hkv, 64, D, device=dev, dtype=bf)
+            vc[idx] = torch.randn(len(idx), Hkv, D, 64, device=dev, dtype=bf)
+        else:
+            kc = torch.randn(pool, Hkv, 64, D, device=dev, dtype=bf)
+            vc = torch.randn(pool, Hkv, D, 64, device=dev, dtype=bf)
+        cl = ctxs.to(torch.int32).to(dev)
         q = torch.randn(B, Hq * D, device=dev, dtype=bf)
         ws = torch.empty(B * Hq * nsplit * (D + 2), device=dev, dtype=torch.float32)
         o = torch.empty(B, Hq * D, device=dev, dtype=bf)
         scale = 1 / math.sqrt(D)
         us = timeit(lambda: ops.hip().paged_decode_attention(o, q, kc, vc, bt, cl, scale, nsplit, mbps, ws))
-        byts = B * ctx * Hkv * D * 2 * 2
+        byts = int(ctxs.sum()) * Hkv * D * 2 * 2
         rec = {"B": B, "ctx": ctx, "us": round(us, 2), "TBps": round(byts / us / 1e6, 2),
                "kernel": "decode_attn_kernel", "wpp": os.environ.get("LS_ATTN_WPP", "auto"),
-               "pipe": os.environ.get("LS_ATTN_PIPE", "1")}
-        if B <= 16 or (a.check_all and B * ctx <= 256 * 1024):
+               "pipe": os.environ.get("LS_ATTN_PIPE", "1"),
+               "ragged": a.ragged, "pool_gb": a.pool_gb}
+        if (B <= 16 or (a.check_all and B * ctx <= 256 * 1024)) and a.pool_gb == 0:
             exp = ref.paged_decode_attention(q.float().cpu().reshape(B, Hq, D), kc.float().cpu(), vc.float().cpu(),
                                              bt.cpu(), cl.cpu(), scale).reshape(B, Hq * D)
             rec["max_err"] = round(float((o.float().cpu() - exp).abs().max()), 4)
