@@ -25,10 +25,14 @@ the global top-k through the sharded kNN service (RCCL all-gather / all-to-all).
 torch.distributed.run itself before anything touches the GPU; under torchrun
 (WORLD_SIZE set) ``--gpus`` must equal WORLD_SIZE.
 
-Weak scaling: per GPU per step, B questions and D crawled pages; before timing each rank
-loads a synthetic corpus into its shard (untimed).  A step ends when every question of
-the rank has its answer and every page crawled so far is fully indexed (committed by the
-ingest consumer group).  K steps are timed after W warmup steps, bracketed by a barrier
+Weak scaling: per GPU per step, B answered questions and D crawled pages; before timing
+each rank loads a synthetic corpus into its shard (untimed).  Load (``--load``): by
+default a closed loop -- B questions in flight per GPU, a new one written as each answer
+arrives (a streaming pipeline's steady state: new prompts' prefill chunks ride in the
+same engine steps as the running sequences' decode tokens); ``--load burst`` writes B
+questions at the start of each step instead.  A step ends when the rank has B more
+answers and every page crawled so far is fully indexed (committed by the ingest
+consumer group).  K steps are timed after W warmup steps, bracketed by a barrier
 and a device synchronize on both sides; value = answered questions per second over all
 ranks (max elapsed over ranks).  Weights are random-init (no checkpoints offline); data
 is synthetic.
@@ -337,6 +341,10 @@ def main():
     ap.add_argument("--embed-model", default="bge-small-en")
     ap.add_argument("--device", default=None)
     ap.add_argument("--timeout", type=float, default=900.0)
+    ap.add_argument("--load", choices=("stream", "burst"), default="stream",
+                    help="stream: closed loop, --batch questions in flight per GPU, a new question as each "
+                         "answer arrives, a step = --batch answers; burst: --batch questions at the start of "
+                         "each step, the step ends when all are answered")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -427,9 +435,17 @@ def main():
         end = log.end_offsets("documents-topic")
         return sum(end) >= expected_docs and log.committed("documents-topic", ingest_group) == end
 
+    def send_question():
+        g = seq[0] * world + rank
+        k = balanced_key(f"{rank}-{seq[0]}", g % q_parts, q_parts)
+        seq[0] += 1
+        sent[k] = time.time()
+        prod.write(_rec(k, corpus[(g * 13) % len(corpus)]))
+
+    sent = {}
+
     def run_step():
         step = steps_done[0]
-        sent = {}
         t0 = time.time()
         if args.docs > 0:
             if crawl:
@@ -439,26 +455,25 @@ def main():
                 for d in range(args.docs):
                     i = (step * world + rank) * args.docs + d
                     doc_prod.write(_rec(balanced_key(f"doc-{i}", i % d_parts, d_parts), make_page(i, corpus)))
-        for i in range(args.batch):
-            g = (step * world + rank) * args.batch + i
-            k = balanced_key(f"{rank}-{seq[0]}", g % q_parts, q_parts)
-            seq[0] += 1
-            sent[k] = time.time()
-            prod.write(_rec(k, corpus[(g * 13) % len(corpus)]))
+        if args.load == "burst" or step == 0:
+            for _ in range(args.batch):
+                send_question()
         expect_docs = (step + 1) * args.docs * world
         lats = []
         deadline = time.time() + args.timeout
-        while sent or (args.docs > 0 and not ingest_done(expect_docs)):
+        while len(lats) < args.batch or (args.docs > 0 and not ingest_done(expect_docs)):
             if runner.errors:
                 raise runner.errors[0]
             if time.time() > deadline:
-                raise TimeoutError(f"rank {rank}: {len(sent)} answers missing; documents end "
+                raise TimeoutError(f"rank {rank}: {args.batch - len(lats)} answers missing; documents end "
                                    f"{log.end_offsets('documents-topic')} committed "
                                    f"{log.committed('documents-topic', ingest_group)} (expected {expect_docs})")
             for r in reader.read().records:
                 t = sent.pop(r.key(), None)
                 if t is not None:
                     lats.append(time.time() - t)
+                    if args.load == "stream":
+                        send_question()   # closed loop: keep --batch questions in flight
         steps_done[0] += 1
         return time.time() - t0, lats
 
@@ -514,6 +529,8 @@ def main():
                        "corpus_docs_per_gpu": args.corpus, "top_k": 20, "rerank": 5,
                        "crawled_pages_per_gpu_per_step": args.docs, "crawl": crawl,
                        "topics": "shm (cross-process consumer groups)",
+                       "load": (f"closed loop, {args.batch} questions in flight per GPU" if args.load == "stream"
+                                else f"bursts of {args.batch} questions per GPU per step"),
                        "parallelism": f"dp{world}"},
             "ingest": {"pages_per_s": round(args.docs * args.steps * world / elapsed, 2),
                        "chunks_per_s": round(sum(g["chunks"] for g in gathered) / elapsed, 2)},

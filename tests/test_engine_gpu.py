@@ -77,14 +77,15 @@ def test_native_runner_matches_python_forward():
 
 
 def _run_tops(e: LLMEngine, prompts, sp: SamplingParams):
-    """Run to completion; per request the output ids and each step's top-2 alternatives."""
+    """Run to completion; per request the output ids and each step's top-n alternatives
+    (None when sp.logprobs == 0 -- the only mode the decode graphs serve)."""
     tops = {}
     reqs = [e.submit(p, sp, callback=lambda ev, i=i: tops.setdefault(i, []).append(ev.top))
             for i, p in enumerate(prompts)]
     while not all(r.finished for r in reqs):
         e.step()
     e._flush()
-    return [(r.output_ids, tops[i]) for i, r in enumerate(reqs)]
+    return [(r.output_ids, tops.get(i)) for i, r in enumerate(reqs)]
 
 
 def _same_or_near_tie(a, b, gap: float = 0.1) -> None:
@@ -111,13 +112,14 @@ def test_native_executor_matches_python_executor():
     cfg = PRESETS["llama-small"]
     model = LlamaModel(cfg, device="cuda")
     prompts = [list(range(3, 3 + n)) for n in (5, 33, 64, 65, 200)]
-    sp = SamplingParams(max_tokens=16, temperature=0.0, ignore_eos=True, logprobs=2)
+    sp = SamplingParams(max_tokens=16, temperature=0.0, ignore_eos=True)
+    sp_ref = SamplingParams(max_tokens=16, temperature=0.0, ignore_eos=True, logprobs=2)
     e1 = LLMEngine(model, None, num_blocks=128, max_model_len=1024, max_batch=8)
     out1 = _run_tops(e1, prompts, sp)
     assert e1.stats["graph_steps"] > 0
     e2 = LLMEngine(model, None, num_blocks=128, max_model_len=1024, max_batch=8, use_graphs=False)
     e2.exec = PyStepExecutor(model, e2.kv_caches, e2.layout, NSLOTS, e2.nsplit, e2.bps, e2.device)
-    out2 = _run_tops(e2, prompts, sp)
+    out2 = _run_tops(e2, prompts, sp_ref)
     for a, b in zip(out1, out2):
         _same_or_near_tie(a, b)
 
@@ -126,12 +128,12 @@ def test_llama_graph_decode_matches_eager():
     cfg = PRESETS["llama-small"]
     model = LlamaModel(cfg, device="cuda")
     prompts = [list(range(3, 3 + n)) for n in (5, 33, 64, 65, 200)]
-    sp = SamplingParams(max_tokens=24, temperature=0.0, ignore_eos=True, logprobs=2)
+    sp = SamplingParams(max_tokens=24, temperature=0.0, ignore_eos=True)
     e1 = LLMEngine(model, None, num_blocks=128, max_model_len=1024, use_graphs=True, max_batch=8)
     out1 = _run_tops(e1, prompts, sp)
     assert e1.stats["graph_steps"] > 0
     e2 = LLMEngine(model, None, num_blocks=128, max_model_len=1024, use_graphs=False, max_batch=8)
-    out2 = _run_tops(e2, prompts, sp)
+    out2 = _run_tops(e2, prompts, SamplingParams(max_tokens=24, temperature=0.0, ignore_eos=True, logprobs=2))
     # the same kernels replayed from a graph: identical over the whole length (a split
     # is only tolerated at a genuine near-tie)
     for a, b in zip(out1, out2):
@@ -219,9 +221,8 @@ def test_native_executor_tp_path_world1_rccl():
             assert x.token_id == y.token_id
             assert abs(x.logprob - y.logprob) < 0.05
             assert [t for t, _ in x.top[:2]] == [t for t, _ in y.top[:2]]
-        sp = SamplingParams(max_tokens=12, temperature=0.0, ignore_eos=True, logprobs=2)
-        out1 = _run_tops(e1, prompts, sp)
-        out0 = _run_tops(e0, prompts, sp)
+        out1 = _run_tops(e1, prompts, SamplingParams(max_tokens=12, temperature=0.0, ignore_eos=True))
+        out0 = _run_tops(e0, prompts, SamplingParams(max_tokens=12, temperature=0.0, ignore_eos=True, logprobs=2))
         assert e1.stats["graph_steps"] > 0
         for x, y in zip(out1, out0):
             _same_or_near_tie(x, y)
