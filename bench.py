@@ -341,6 +341,8 @@ def main():
     ap.add_argument("--embed-model", default="bge-small-en")
     ap.add_argument("--device", default=None)
     ap.add_argument("--timeout", type=float, default=900.0)
+    ap.add_argument("--prefill-chunk", type=int, default=16384,
+                    help="engine max-prefill-tokens per step (chunked prefill)")
     ap.add_argument("--load", choices=("stream", "burst"), default="stream",
                     help="stream: closed loop, --batch questions in flight per GPU, a new question as each "
                          "answer arrives, a step = --batch answers; burst: --batch questions at the start of "
@@ -391,7 +393,7 @@ def main():
     shm = bcast(f"bench-{uuid.uuid4().hex[:12]}")
     shm_mb = 2048 + 512 * world
     fmt = dict(chat_model=chat_model, embed_model=embed_model, max_tokens=args.max_tokens,
-               max_batch=max(args.batch, 1), max_len=4096, prefill=16384, q_parts=q_parts, d_parts=d_parts,
+               max_batch=max(args.batch, 1), max_len=4096, prefill=args.prefill_chunk, q_parts=q_parts, d_parts=d_parts,
                shm=shm, shm_mb=shm_mb)
     corpus = builtin_corpus(max(4000, args.corpus // 4 + 1))
     crawl = args.docs > 0 and not args.no_crawl
@@ -413,7 +415,7 @@ def main():
         vec = emb.embed_tensor(chunk)
         store.upsert([f"c{rank}-{j}" for j in range(i, i + len(chunk))], vec, [{"text": t} for t in chunk])
     llm = services.llm_engine(chat_model, {"chat-model": chat_model, "max-batch": fmt["max_batch"],
-                                           "max-model-len": 4096, "max-prefill-tokens": 16384})
+                                           "max-model-len": 4096, "max-prefill-tokens": args.prefill_chunk})
     if world > 1:
         dist_knn.start(device=device)
     only = None if rank == 0 else ["query", "ingest"]   # the crawler runs once (rank 0)
@@ -525,7 +527,8 @@ def main():
             "dtype": "bf16" if use_gpu else "fp32",
             "data": "synthetic questions + synthetic crawled pages + synthetic corpus, random-init weights",
             "config": {"model": chat_model, "embedding_model": embed_model, "global_batch": args.batch * world,
-                       "seq_len": round(mean_prompt, 1), "max_model_len": 4096, "max_new_tokens": args.max_tokens,
+                       "seq_len": round(mean_prompt, 1), "max_model_len": 4096,
+                       "prefill_chunk": args.prefill_chunk, "max_new_tokens": args.max_tokens,
                        "corpus_docs_per_gpu": args.corpus, "top_k": 20, "rerank": 5,
                        "crawled_pages_per_gpu_per_step": args.docs, "crawl": crawl,
                        "topics": "shm (cross-process consumer groups)",
