@@ -38,6 +38,9 @@ def main():
     ap.add_argument("--check-all", action="store_true")
     ap.add_argument("--ragged", type=float, default=0.0,
                     help="per-sequence context drawn uniformly from ctx*(1 +- ragged) (mean ctx)")
+    ap.add_argument("--ring", type=int, default=1,
+                    help="rotate over this many KV pools per call (> 256 MB Infinity Cache in total: cold "
+                         "caches, as in an engine step that streams 32 layers between two calls)")
     ap.add_argument("--pool-gb", type=float, default=0.0,
                     help="scatter the blocks over a KV pool of this size (TLB reach), like a real engine")
     a = ap.parse_args()
@@ -67,17 +70,25 @@ def main():
         else:
             kc = torch.randn(pool, Hkv, 64, D, device=dev, dtype=bf)
             vc = torch.randn(pool, Hkv, D, 64, device=dev, dtype=bf)
+        kvs = [(kc, vc)] + [(torch.randn_like(kc), torch.randn_like(vc)) for _ in range(a.ring - 1)]
         cl = ctxs.to(torch.int32).to(dev)
         q = torch.randn(B, Hq * D, device=dev, dtype=bf)
         ws = torch.empty(B * Hq * nsplit * (D + 2), device=dev, dtype=torch.float32)
         o = torch.empty(B, Hq * D, device=dev, dtype=bf)
         scale = 1 / math.sqrt(D)
-        us = timeit(lambda: ops.hip().paged_decode_attention(o, q, kc, vc, bt, cl, scale, nsplit, mbps, ws))
+        it = [0]
+
+        def call():
+            k_, v_ = kvs[it[0] % len(kvs)]
+            it[0] += 1
+            ops.hip().paged_decode_attention(o, q, k_, v_, bt, cl, scale, nsplit, mbps, ws)
+        us = timeit(call)
+        ops.hip().paged_decode_attention(o, q, kc, vc, bt, cl, scale, nsplit, mbps, ws)
         byts = int(ctxs.sum()) * Hkv * D * 2 * 2
         rec = {"B": B, "ctx": ctx, "us": round(us, 2), "TBps": round(byts / us / 1e6, 2),
                "kernel": "decode_attn_kernel", "wpp": os.environ.get("LS_ATTN_WPP", "auto"),
                "pipe": os.environ.get("LS_ATTN_PIPE", "1"),
-               "ragged": a.ragged, "pool_gb": a.pool_gb}
+               "ragged": a.ragged, "pool_gb": a.pool_gb, "ring": a.ring}
         if (B <= 16 or (a.check_all and B * ctx <= 256 * 1024)) and a.pool_gb == 0:
             exp = ref.paged_decode_attention(q.float().cpu().reshape(B, Hq, D), kc.float().cpu(), vc.float().cpu(),
                                              bt.cpu(), cl.cpu(), scale).reshape(B, Hq * D)
