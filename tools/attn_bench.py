@@ -41,6 +41,9 @@ def main():
     ap.add_argument("--ring", type=int, default=1,
                     help="rotate over this many KV pools per call (> 256 MB Infinity Cache in total: cold "
                          "caches, as in an engine step that streams 32 layers between two calls)")
+    ap.add_argument("--interleave-gemm", action="store_true",
+                    help="run a decode-sized gate_up GEMM before every call (engine-like power / cache state); "
+                         "time the attention kernel with rocprofv3 in this mode")
     ap.add_argument("--pool-gb", type=float, default=0.0,
                     help="scatter the blocks over a KV pool of this size (TLB reach), like a real engine")
     a = ap.parse_args()
@@ -77,8 +80,13 @@ def main():
         o = torch.empty(B, Hq * D, device=dev, dtype=bf)
         scale = 1 / math.sqrt(D)
         it = [0]
+        if a.interleave_gemm:
+            gx = torch.randn(B, 4096, device=dev, dtype=bf)
+            gw = torch.randn(28672, 4096, device=dev, dtype=bf) * 0.02
 
         def call():
+            if a.interleave_gemm:
+                torch.nn.functional.linear(gx, gw)
             k_, v_ = kvs[it[0] % len(kvs)]
             it[0] += 1
             ops.hip().paged_decode_attention(o, q, k_, v_, bt, cl, scale, nsplit, mbps, ws)
