@@ -152,6 +152,16 @@ class ShardedKnn:
     def _loop(self) -> None:
         if self.device.type == "cuda":
             torch.cuda.set_device(self.device)
+            # Every device op of a round -- the H2D query copy, the RCCL all-gather and
+            # all-to-all (which order themselves after the CURRENT stream), the kNN kernel
+            # and the D2H copies -- runs on the one auxiliary stream, so they are ordered
+            # with each other and never queue behind the LLM engine's default stream.
+            with on_aux(self.device):
+                self._serve()
+        else:
+            self._serve()
+
+    def _serve(self) -> None:
         try:
             while True:
                 with self._cv:
@@ -219,9 +229,8 @@ class ShardedKnn:
                 dist.all_gather_into_tensor(qall, qloc, group=self.data)
                 store = stores.get(coll)
                 if store is not None and store.dim == dim and len(store):
-                    with on_aux(store.device):
-                        s, idx = store.topk_rows(qall.to(store.device, store.dtype), kmax)
-                        s, idx = s.to(self.data_dev), idx.to(self.data_dev)
+                    s, idx = store.topk_rows(qall.to(store.device, store.dtype), kmax)
+                    s, idx = s.to(self.data_dev), idx.to(self.data_dev)
                 else:
                     s = torch.full((W * qmax, kmax), float("-inf"), device=self.data_dev)
                     idx = torch.full((W * qmax, kmax), -1, dtype=torch.int32, device=self.data_dev)
