@@ -81,6 +81,8 @@ class ShardedKnn:
         self.rank, self.world = dist.get_rank(), dist.get_world_size()
         backend = dist.get_backend()
         self.device = torch.device(device or ("cuda" if backend == "nccl" else "cpu"))
+        if self.device.type == "cuda" and self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
         # separate groups so the service never interleaves with the caller's collectives
         self.meta = dist.new_group(backend="gloo")
         self.data = dist.new_group(backend=backend) if backend == "nccl" else dist.new_group(backend="gloo")
@@ -150,16 +152,26 @@ class ShardedKnn:
 
     # ------------------------------------------------------------------ service loop
     def _loop(self) -> None:
-        if self.device.type == "cuda":
-            torch.cuda.set_device(self.device)
-            # Every device op of a round -- the H2D query copy, the RCCL all-gather and
-            # all-to-all (which order themselves after the CURRENT stream), the kNN kernel
-            # and the D2H copies -- runs on the one auxiliary stream, so they are ordered
-            # with each other and never queue behind the LLM engine's default stream.
-            with on_aux(self.device):
+        try:
+            if self.device.type == "cuda":
+                torch.cuda.set_device(self.device)
+                # Every device op of a round -- the H2D query copy, the RCCL all-gather and
+                # all-to-all (which order themselves after the CURRENT stream), the kNN
+                # kernel and the D2H copies -- runs on the one auxiliary stream, so they are
+                # ordered with each other and never queue behind the LLM engine's default
+                # stream.
+                with on_aux(self.device):
+                    self._serve()
+            else:
                 self._serve()
-        else:
-            self._serve()
+        except BaseException as e:  # noqa: BLE001  (setup failed: fail what is pending)
+            log.exception("sharded kNN service failed")
+            with self._cv:
+                self._stop = True
+                pend, self._pending = self._pending, []
+            for r in pend:
+                if not r.fut.done():
+                    r.fut.set_exception(e if isinstance(e, Exception) else RuntimeError(str(e)))
 
     def _serve(self) -> None:
         try:

@@ -1,0 +1,54 @@
+"""The data-parallel GPU paths at world size 1 over a real RCCL process group (no
+multi-GPU box is available to the build): the sharded kNN service's RCCL all-gather /
+all-to-all data path and its stream ordering on the auxiliary stream, against the local
+store's own search on the same device."""
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture()
+def rccl_world1():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    try:
+        yield
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_knn_service_rccl_world1(rccl_world1):
+    from langstream_amd.engine import dist_knn
+    from langstream_amd.engine.vector_store import VectorStoreRegistry
+    g = torch.Generator().manual_seed(12)
+    vecs = torch.randn(50_000, 384, generator=g)
+    queries = torch.randn(40, 384, generator=g)
+    VectorStoreRegistry.reset()
+    store = VectorStoreRegistry.get("docs-gpu", 384, device="cuda")
+    store.upsert([f"d{i}" for i in range(vecs.shape[0])], vecs, [{"text": f"t{i}"} for i in range(vecs.shape[0])])
+    svc = dist_knn.start(device="cuda")
+    try:
+        # concurrent requests of different k, some with vectors, while the default
+        # stream is kept busy (the service must not depend on it for ordering)
+        busy = torch.randn(4096, 4096, device="cuda")
+        futs = []
+        for i in range(queries.shape[0]):
+            torch.mm(busy, busy)
+            futs.append(svc.search("docs-gpu", queries[i:i + 1].tolist(), 5 + (i % 4), with_vectors=(i % 3 == 0)))
+        got = [f.result(120)[0] for f in futs]
+        assert svc.rounds >= 1
+    finally:
+        dist_knn.stop()
+    for i, res in enumerate(got):
+        want = store.search(queries[i:i + 1].tolist(), 5 + (i % 4))[0]
+        assert [d["id"] for d in res] == [d["id"] for d in want] or all(
+            abs(a["similarity"] - b["similarity"]) < 1e-5 for a, b in zip(res, want))
+        assert all(d["text"] == "t" + d["id"][1:] for d in res)
+        if i % 3 == 0:
+            assert all(len(d["vector"]) == 384 for d in res)
