@@ -365,12 +365,15 @@ def main():
     if use_gpu:
         torch.cuda.set_device(local)
     ctrl = None
-    if world > 1:
+    # LS_BENCH_FORCE_DIST=1 (under torchrun): take the multi-rank code path even at world
+    # size 1 -- RCCL/gloo groups, barriers, the sharded kNN service -- to rehearse it on one GPU
+    multi = world > 1 or os.environ.get("LS_BENCH_FORCE_DIST") == "1" and "WORLD_SIZE" in os.environ
+    if multi:
         dist.init_process_group("nccl" if use_gpu else "gloo")
         ctrl = dist.new_group(backend="gloo")   # barriers / small host exchanges
 
     def barrier():
-        if world > 1:
+        if multi:
             dist.barrier(group=ctrl)
         if use_gpu:
             torch.cuda.synchronize()
@@ -420,7 +423,7 @@ def main():
         store.upsert([f"c{rank}-{j}" for j in range(i, i + len(chunk))], vec, [{"text": t} for t in chunk])
     llm = services.llm_engine(chat_model, {"chat-model": chat_model, "max-batch": fmt["max_batch"],
                                            "max-model-len": 4096, "max-prefill-tokens": args.prefill_chunk})
-    if world > 1:
+    if multi:
         dist_knn.start(device=device)
     only = None if rank == 0 else ["query", "ingest"]   # the crawler runs once (rank 0)
     runner = LocalApplicationRunner.from_yaml(files, instance=INSTANCE.format(**fmt), application_id="rag-bench",
@@ -560,7 +563,7 @@ def main():
     mine = {"elapsed": elapsed, "lats": my_lats, "chunks": chunks, "assign": assign,
             "prefill_tokens": stats.get("prefill_tokens", 0), "requests": stats.get("requests", 0),
             "knn_rounds": dist_knn.active().rounds if dist_knn.active() else 0}
-    if world > 1:
+    if multi:
         gathered = [None] * world
         dist.all_gather_object(gathered, mine, group=ctrl)
     else:
@@ -600,7 +603,7 @@ def main():
         }), flush=True)
     barrier()
     runner.stop(timeout=10)
-    if world > 1:
+    if multi:
         dist_knn.stop()
     services.shutdown()
     if site is not None:
@@ -608,7 +611,7 @@ def main():
     barrier()
     if rank == 0:
         unlink_shmlog(shm, size_mb=shm_mb)
-    if world > 1:
+    if multi:
         dist.destroy_process_group()
 
 
