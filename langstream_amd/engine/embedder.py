@@ -49,6 +49,10 @@ class EmbeddingEngine:
     def embed_tensor(self, texts: Sequence[str]) -> torch.Tensor:
         """Device tensor, produced on the device's auxiliary stream (consume it there,
         e.g. VectorStore.upsert, or synchronise)."""
+        if hasattr(self.tok, "encode_batch_packed"):
+            ids, lens = self.tok.encode_batch_packed(list(texts), max_len=self.max_len)
+            with on_aux(self.encoder.device):
+                return self.encoder.encode_arrays(ids, lens)
         toks = self.tok.encode_batch(list(texts), max_len=self.max_len)
         with on_aux(self.encoder.device):
             return self.encoder.encode_tokens(toks)
@@ -56,22 +60,27 @@ class EmbeddingEngine:
     def _embed_batch(self, texts: List[str]):
         """Tokenise once (native, multi-threaded), encode in packed batches of at most
         ``max_batch_tokens`` on the auxiliary stream, one device->host copy at the end."""
-        all_toks = self.tok.encode_batch(texts, max_len=self.max_len)
+        import numpy as np
+        if hasattr(self.tok, "encode_batch_packed"):
+            ids, lens = self.tok.encode_batch_packed(texts, max_len=self.max_len)
+        else:
+            tl = self.tok.encode_batch(texts, max_len=self.max_len)
+            lens = np.array([len(t) for t in tl], dtype=np.int32)
+            ids = np.array([x for t in tl for x in t], dtype=np.int32)
+        ends = np.cumsum(lens, dtype=np.int64)
         outs = []
-        i = 0
+        i, n = 0, len(lens)
         with on_aux(self.encoder.device):  # do not queue behind the LLM engine's steps
-            while i < len(all_toks):
-                toks, ntok = [], 0
-                for t in all_toks[i:]:
-                    if toks and ntok + len(t) > self.max_batch_tokens:
-                        break
-                    toks.append(t)
-                    ntok += len(t)
-                outs.append(self.encoder.encode_tokens(toks))
+            while i < n:
+                # as many texts as fit in max_batch_tokens (at least one)
+                t0 = ends[i - 1] if i else 0
+                j = max(i + 1, int(np.searchsorted(ends, t0 + self.max_batch_tokens, side="right")))
+                t1 = ends[j - 1]
+                outs.append(self.encoder.encode_arrays(ids[t0:t1], lens[i:j]))
                 self.stats["batches"] += 1
-                self.stats["texts"] += len(toks)
-                self.stats["tokens"] += ntok
-                i += len(toks)
+                self.stats["texts"] += j - i
+                self.stats["tokens"] += int(t1 - t0)
+                i = j
             if not outs:
                 return torch.zeros(0, self.dim)
             return to_host(outs[0] if len(outs) == 1 else torch.cat(outs))[0]

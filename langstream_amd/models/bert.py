@@ -215,6 +215,29 @@ class BertEncoder:
                 torch.tensor(starts, dtype=torch.int32), torch.tensor(lens, dtype=torch.int32),
                 ops.prefill_tiles(lens, 1))
 
+    def pack_arrays(self, ids, lens):
+        """``pack`` for already-packed numpy token ids / lengths (tokenizer
+        ``encode_batch_packed``): positions and starts built vectorised."""
+        import numpy as np
+        lens0 = np.asarray(lens, dtype=np.int64)
+        lens = np.minimum(lens0, self.cfg.max_position)
+        starts = np.cumsum(lens) - lens
+        if (lens != lens0).any():   # rows longer than max_position: keep each row's prefix
+            src = np.cumsum(lens0) - lens0
+            keep = np.repeat(src, lens) + (np.arange(int(lens.sum())) - np.repeat(starts, lens))
+            ids = np.asarray(ids)[keep]
+        pos = np.arange(int(lens.sum()), dtype=np.int64) - np.repeat(starts, lens)
+        return (torch.from_numpy(np.ascontiguousarray(ids, dtype=np.int32)),
+                torch.from_numpy(pos.astype(np.int32)), torch.from_numpy(starts.astype(np.int32)),
+                torch.from_numpy(lens.astype(np.int32)),
+                torch.from_numpy(ops.prefill_tiles_np(lens, 1, np.zeros(len(lens), np.int64))))
+
+    def encode_arrays(self, ids, lens, out_dtype=torch.float32) -> torch.Tensor:
+        if len(lens) == 0:
+            return torch.zeros(0, self.cfg.hidden_size, dtype=out_dtype, device=self.device)
+        d_ids, pos, st, ln, tiles = (t.to(self.device, non_blocking=True) for t in self.pack_arrays(ids, lens))
+        return self.forward_packed(d_ids, pos, st, ln, tiles, out_dtype)
+
     def encode_tokens(self, token_lists: List[List[int]], out_dtype=torch.float32) -> torch.Tensor:
         if not token_lists:
             return torch.zeros(0, self.cfg.hidden_size, dtype=out_dtype, device=self.device)

@@ -15,6 +15,7 @@
 //               used to build self-contained vocabularies when no tokenizer files exist
 //               (this environment has no network / model hub).
 #include <pybind11/pybind11.h>
+#include <pybind11/numpy.h>
 #include <pybind11/stl.h>
 
 #include <algorithm>
@@ -25,6 +26,7 @@
 #include <set>
 #include <shared_mutex>
 #include <string>
+#include <string_view>
 #include <thread>
 #include <unordered_map>
 #include <unordered_set>
@@ -398,6 +400,20 @@ class WordPiece {
     id2tok_ = vocab;
     auto it = vocab_.find(unk);
     unk_id_ = it == vocab_.end() ? 0 : it->second;
+    // allocation-free lookup tables: word-initial pieces and "##" continuations, keyed
+    // by string_views into id2tok_ (never resized after this point)
+    for (size_t i = 0; i < id2tok_.size(); ++i) {
+      const std::string& t = id2tok_[i];
+      if (t.size() > 2 && t[0] == '#' && t[1] == '#') {
+        std::string_view k(t.data() + 2, t.size() - 2);
+        cont_.emplace(k, (int)i);
+        max_cont_ = std::max(max_cont_, k.size());
+      } else if (!t.empty()) {
+        std::string_view k(t);
+        head_.emplace(k, (int)i);
+        max_head_ = std::max(max_head_, k.size());
+      }
+    }
   }
 
   std::vector<std::string> basic_tokens(const std::string& text) const {
@@ -422,36 +438,71 @@ class WordPiece {
     return words;
   }
 
+  // Greedy longest-match-first WordPiece of one normalised word, appended to out.
+  // Candidate pieces are string_views into the word (no allocation per attempt); the
+  // search starts at the longest vocabulary piece instead of the whole remaining word.
+  void wordpiece(const std::string& w, std::vector<uint32_t>& offs, std::vector<int>& out) const {
+    offs.clear();
+    for (size_t o = 0; o < w.size(); o += utf8_len((unsigned char)w[o])) offs.push_back((uint32_t)o);
+    const size_t ncp = offs.size();
+    offs.push_back((uint32_t)w.size());
+    if ((int)ncp > max_chars_) { out.push_back(unk_id_); return; }
+    const size_t mark = out.size();
+    size_t start = 0;
+    while (start < ncp) {
+      const auto& map = start == 0 ? head_ : cont_;
+      const size_t maxb = start == 0 ? max_head_ : max_cont_;
+      size_t end = ncp;
+      int found = -1;
+      for (; end > start; --end) {
+        const size_t nb = offs[end] - offs[start];
+        if (nb > maxb) continue;
+        auto it = map.find(std::string_view(w.data() + offs[start], nb));
+        if (it != map.end()) { found = it->second; break; }
+      }
+      if (found < 0) {   // the whole word is unknown
+        out.resize(mark);
+        out.push_back(unk_id_);
+        return;
+      }
+      out.push_back(found);
+      start = end;
+    }
+  }
+
   std::vector<int> encode(const std::string& text) const {
     std::vector<int> out;
-    for (auto& w : basic_tokens(text)) {
-      const std::vector<uint32_t> cps = utf8_decode(w);
-      if ((int)cps.size() > max_chars_) { out.push_back(unk_id_); continue; }
-      // byte offsets of code points
-      std::vector<size_t> offs;
-      size_t o = 0;
-      for (uint32_t cp : cps) { offs.push_back(o); std::string t; utf8_append(t, cp); o += t.size(); }
-      offs.push_back(o);
-      std::vector<int> pieces;
-      size_t start = 0;
-      bool bad = false;
-      while (start < cps.size()) {
-        size_t end = cps.size();
-        int found = -1;
-        while (start < end) {
-          std::string sub = w.substr(offs[start], offs[end] - offs[start]);
-          if (start > 0) sub = "##" + sub;
-          auto it = vocab_.find(sub);
-          if (it != vocab_.end()) { found = it->second; break; }
-          --end;
-        }
-        if (found < 0) { bad = true; break; }
-        pieces.push_back(found);
-        start = end;
+    out.reserve(text.size() / 3 + 4);
+    std::string cur;
+    std::vector<uint32_t> offs;
+    auto flush = [&]() {
+      if (!cur.empty()) { wordpiece(cur, offs, out); cur.clear(); }
+    };
+    const unsigned char* p = (const unsigned char*)text.data();
+    const size_t n = text.size();
+    for (size_t i = 0; i < n;) {
+      // one code point, decoded exactly as utf8_decode does
+      const unsigned char c = p[i];
+      const int l = utf8_len(c);
+      uint32_t cp = c;
+      if (l == 2 && i + 1 < n) cp = ((c & 0x1F) << 6) | (p[i + 1] & 0x3F);
+      else if (l == 3 && i + 2 < n) cp = ((c & 0x0F) << 12) | ((p[i + 1] & 0x3F) << 6) | (p[i + 2] & 0x3F);
+      else if (l == 4 && i + 3 < n)
+        cp = ((c & 0x07) << 18) | ((p[i + 1] & 0x3F) << 12) | ((p[i + 2] & 0x3F) << 6) | (p[i + 3] & 0x3F);
+      i += l;
+      if (cp == 0 || cp == 0xFFFD || (cp < 32 && cp != '\t' && cp != '\n' && cp != '\r')) continue;
+      if (cp == ' ' || cp == '\t' || cp == '\n' || cp == '\r' || cp == 0xA0 || cp == 0x3000) { flush(); continue; }
+      cp = fold_latin(cp, lower_, strip_);
+      if (strip_ && cp >= 0x300 && cp <= 0x36F) continue;  // combining marks
+      if (is_punct_cp(cp) || is_cjk(cp)) {
+        flush();
+        utf8_append(cur, cp);
+        flush();
+        continue;
       }
-      if (bad) out.push_back(unk_id_);
-      else out.insert(out.end(), pieces.begin(), pieces.end());
+      utf8_append(cur, cp);
     }
+    flush();
     return out;
   }
 
@@ -468,6 +519,33 @@ class WordPiece {
     work();
     for (auto& t : pool) t.join();
     return out;
+  }
+
+  // [CLS] + ids[:max_len-2] + [SEP] of every text, packed: (ids int32 [sum lens],
+  // lens int32 [n]) -- no per-token Python objects on the way to the encoder.
+  py::tuple encode_batch_packed(const std::vector<std::string>& texts, int max_len, int cls, int sep,
+                                int threads) const {
+    std::vector<std::vector<int>> toks = encode_batch(texts, threads);
+    const size_t n = toks.size();
+    const int keep = std::max(0, max_len - 2);
+    py::array_t<int32_t> lens((py::ssize_t)n);
+    auto L = lens.mutable_unchecked<1>();
+    size_t total = 0;
+    for (size_t i = 0; i < n; ++i) {
+      const int l = (int)std::min<size_t>(toks[i].size(), (size_t)keep) + 2;
+      L(i) = l;
+      total += l;
+    }
+    py::array_t<int32_t> ids((py::ssize_t)total);
+    int32_t* d = ids.mutable_data();
+    for (size_t i = 0; i < n; ++i) {
+      *d++ = cls;
+      const size_t m = (size_t)L(i) - 2;
+      std::copy(toks[i].begin(), toks[i].begin() + m, d);
+      d += m;
+      *d++ = sep;
+    }
+    return py::make_tuple(ids, lens);
   }
 
   std::string decode(const std::vector<int>& ids) const {
@@ -490,6 +568,8 @@ class WordPiece {
  private:
   std::unordered_map<std::string, int> vocab_;
   std::vector<std::string> id2tok_;
+  std::unordered_map<std::string_view, int> head_, cont_;
+  size_t max_head_ = 0, max_cont_ = 0;
   bool lower_, strip_;
   int max_chars_;
   int unk_id_;
@@ -596,7 +676,9 @@ void bind_tokenizer(py::module_& m) {
            py::arg("lower") = true, py::arg("strip_accents") = true, py::arg("unk") = "[UNK]",
            py::arg("max_chars") = 100)
       .def("encode", &WordPiece::encode, py::call_guard<py::gil_scoped_release>())
-      .def("encode_batch", &WordPiece::encode_batch, py::arg("texts"), py::arg("threads") = 4)
+      .def("encode_batch", &WordPiece::encode_batch, py::arg("texts"), py::arg("threads") = 8)
+      .def("encode_batch_packed", &WordPiece::encode_batch_packed, py::arg("texts"), py::arg("max_len"),
+           py::arg("cls"), py::arg("sep"), py::arg("threads") = 8)
       .def("basic_tokens", &WordPiece::basic_tokens)
       .def("decode", &WordPiece::decode)
       .def("token_to_id", &WordPiece::token_to_id)

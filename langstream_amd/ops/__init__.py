@@ -250,7 +250,9 @@ def prefill_tiles_np(q_lens, G: int, prefix_lens, out=None):
     rows = q_lens * G
     n_per = (rows + PREFILL_ROWS - 1) // PREFILL_ROWS
     seq = np.repeat(np.arange(len(q_lens)), n_per)
-    first = np.concatenate([np.arange(n) for n in n_per]) * PREFILL_ROWS if len(seq) else np.zeros(0, np.int64)
+    # index of each tile within its sequence, vectorised
+    base = np.repeat(np.cumsum(n_per) - n_per, n_per)
+    first = (np.arange(len(seq)) - base) * PREFILL_ROWS
     last = np.minimum(first + PREFILL_ROWS, rows[seq]) - 1
     work = prefix[seq] + last // G
     order = np.argsort(-work, kind="stable")

@@ -202,9 +202,13 @@ class WordPieceTokenizer:
             ids = [self.cls_id] + ids[: max_len - 2] + [self.sep_id]
         return ids[:max_len]
 
-    def encode_batch(self, texts: Sequence[str], max_len: int = 512, threads: int = 4) -> List[List[int]]:
+    def encode_batch(self, texts: Sequence[str], max_len: int = 512, threads: int = 8) -> List[List[int]]:
         out = self._tok.encode_batch(list(texts), threads)
         return [[self.cls_id] + ids[: max_len - 2] + [self.sep_id] for ids in out]
+
+    def encode_batch_packed(self, texts: Sequence[str], max_len: int = 512, threads: int = 8):
+        """Same tokens as ``encode_batch``, packed: (ids int32 [sum lens], lens int32 [n])."""
+        return self._tok.encode_batch_packed(list(texts), max_len, self.cls_id, self.sep_id, threads)
 
     def decode(self, ids: Iterable[int]) -> str:
         return self._tok.decode([i for i in ids if i not in (self.cls_id, self.sep_id, self.pad_id)])
