@@ -31,7 +31,12 @@
 #include <torch/csrc/distributed/c10d/ProcessGroup.hpp>
 
 #include <chrono>
+#include <condition_variable>
+#include <deque>
+#include <exception>
 #include <map>
+#include <mutex>
+#include <thread>
 #include <memory>
 #include <string>
 #include <vector>
@@ -539,9 +544,28 @@ class StepExecutor {
       tp_cand_all_ = at::zeros({W * maxS_ * cw}, dev.dtype(at::kFloat));
     }
     pool_ = at::cuda::graph_pool_handle();
+    slot_job_.assign(nslots, -1);
+    // Launcher thread (single-GPU executors): hipGraphLaunch of a ~300-node decode graph
+    // returns only ~1 ms before the graph finishes (measured with --hip-trace,
+    // tools/gap_analysis.py), so a launch issued from the engine thread came only after
+    // the engine's own bookkeeping for the previous step -- the GPU idled ~0.5 ms per step
+    // in the RAG pipeline.  A dedicated thread keeps the next step's launch queued.
+    static const bool async_env = getenv("LS_ASYNC_LAUNCH") ? atoi(getenv("LS_ASYNC_LAUNCH")) != 0 : true;
+    if (!r_->pg() && async_env) {
+      stream_ = at::hip::getCurrentHIPStreamMasqueradingAsCUDA();
+      launcher_ = std::thread([this] { launcher_loop(); });
+    }
   }
 
   ~StepExecutor() {
+    if (launcher_.joinable()) {
+      {
+        std::lock_guard<std::mutex> lk(mu_);
+        stop_ = true;
+      }
+      cv_.notify_all();
+      launcher_.join();
+    }
     for (auto e : in_ev_) (void)hipEventDestroy(e);
     for (auto e : out_ev_) (void)hipEventDestroy(e);
   }
@@ -553,17 +577,31 @@ class StepExecutor {
 
   // Block until the H2D copy that last read host slot i has finished (slot reusable).
   void wait_in(int64_t i) {
+    wait_submitted(i);
     if (in_used_.at(i)) HIP_OK(hipEventSynchronize(in_ev_[i]));
   }
   // Block until the results of the step that wrote out slot i are on the host.
-  void wait_out(int64_t i) { HIP_OK(hipEventSynchronize(out_ev_.at(i))); }
+  void wait_out(int64_t i) {
+    wait_submitted(i);
+    HIP_OK(hipEventSynchronize(out_ev_.at(i)));
+  }
 
   // One scheduler round trip in a single GIL-released call: launch the step in host
   // slot `slot` (results -> out slot `slot`), then block until the previous step's
   // results (out slot `prev`, -1: none) are on the host, then until host slot `next`
   // is free for the scheduler to fill.
   void step(int64_t slot, int64_t prev, int64_t next) {
-    launch(slot, slot);
+    if (launcher_.joinable()) {
+      {
+        std::lock_guard<std::mutex> lk(mu_);
+        rethrow_locked();
+        slot_job_.at(slot) = issued_++;
+        jobs_.push_back(slot);
+      }
+      cv_.notify_all();
+    } else {
+      launch(slot, slot);
+    }
     auto t0 = clk::now();
     if (prev >= 0) wait_out(prev);
     auto t1 = clk::now();
@@ -573,6 +611,12 @@ class StepExecutor {
 
   // {upload, run (enqueue forward/graph), download, wait} milliseconds, cumulative.
   std::vector<double> timings() const { return {t_up_, t_run_, t_down_, t_wait_}; }
+
+  // Python entry: launch synchronously, after anything the launcher thread still holds.
+  void launch_sync(int64_t slot, int64_t oslot) {
+    drain();
+    launch(slot, oslot);
+  }
 
   // Rank 0: run the step described by host slot `slot`; results land in out slot `oslot`.
   void launch(int64_t slot, int64_t oslot) {
@@ -592,6 +636,7 @@ class StepExecutor {
 
   // All ranks (rank 0 announces it to the workers): capture the decode graph for bucket B.
   void capture(int64_t B) {
+    drain();
     if (graphs_.count(B)) return;
     if (r_->pg()) {
       int32_t* hdr = reinterpret_cast<int32_t*>(hdr_small_.data_ptr());
@@ -604,6 +649,7 @@ class StepExecutor {
   }
 
   void shutdown() {
+    drain();
     if (!r_->pg()) return;
     int32_t* hdr = reinterpret_cast<int32_t*>(hdr_small_.data_ptr());
     for (int i = 0; i < 16; ++i) hdr[i] = 0;
@@ -635,6 +681,54 @@ class StepExecutor {
 
  private:
   hipStream_t stream() const { return at::hip::getCurrentHIPStream().stream(); }
+
+  void rethrow_locked() {
+    if (err_) {
+      auto e = err_;
+      err_ = nullptr;
+      std::rethrow_exception(e);
+    }
+  }
+
+  // The job that last used slot i has been handed to HIP (its events are recorded).
+  void wait_submitted(int64_t i) {
+    if (!launcher_.joinable()) return;
+    std::unique_lock<std::mutex> lk(mu_);
+    cv_.wait(lk, [&] { return err_ || done_ > slot_job_.at(i); });
+    rethrow_locked();
+  }
+
+  void drain() {
+    if (!launcher_.joinable()) return;
+    std::unique_lock<std::mutex> lk(mu_);
+    cv_.wait(lk, [&] { return err_ || done_ == issued_; });
+    rethrow_locked();
+  }
+
+  void launcher_loop() {
+    at::hip::HIPStreamGuardMasqueradingAsCUDA guard(*stream_);
+    while (true) {
+      int64_t slot;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return stop_ || !jobs_.empty(); });
+        if (jobs_.empty()) return;   // stop_ and nothing left to launch
+        slot = jobs_.front();
+        jobs_.pop_front();
+      }
+      try {
+        launch(slot, slot);
+      } catch (...) {
+        std::lock_guard<std::mutex> lk(mu_);
+        err_ = std::current_exception();
+      }
+      {
+        std::lock_guard<std::mutex> lk(mu_);
+        ++done_;
+      }
+      cv_.notify_all();
+    }
+  }
 
   template <typename T>
   at::Tensor view(const char* name, int64_t n, at::ScalarType st) {
@@ -827,6 +921,16 @@ class StepExecutor {
   at::Tensor arena_, hdr_small_, tok_, lp_, ti_, tl_, ws_, last_logits_;
   at::Tensor tp_stats_, tp_stats_all_, tp_hist_, tp_cand_, tp_cand_all_;
   std::map<int64_t, std::unique_ptr<at::cuda::CUDAGraph>> graphs_;
+  // launcher thread state (guarded by mu_): jobs in issue order, per-slot job index
+  std::thread launcher_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<int64_t> jobs_;
+  std::vector<int64_t> slot_job_;
+  int64_t issued_ = 0, done_ = 0;
+  bool stop_ = false;
+  std::exception_ptr err_;
+  c10::optional<at::hip::HIPStreamMasqueradingAsCUDA> stream_;
   std::map<int64_t, at::Tensor> graph_logits_;
   at::cuda::MempoolId_t pool_;
   double t_up_ = 0, t_run_ = 0, t_down_ = 0, t_wait_ = 0;
@@ -853,7 +957,7 @@ void bind_runners(py::module_& m) {
       .def("has_graph", &StepExecutor::has_graph)
       .def("wait_in", &StepExecutor::wait_in, py::call_guard<py::gil_scoped_release>())
       .def("wait_out", &StepExecutor::wait_out, py::call_guard<py::gil_scoped_release>())
-      .def("launch", &StepExecutor::launch, py::call_guard<py::gil_scoped_release>())
+      .def("launch", &StepExecutor::launch_sync, py::call_guard<py::gil_scoped_release>())
       .def("step", &StepExecutor::step, py::call_guard<py::gil_scoped_release>())
       .def("timings", &StepExecutor::timings)
       .def("capture", &StepExecutor::capture, py::call_guard<py::gil_scoped_release>())
