@@ -1,0 +1,254 @@
+// One-shot all-reduce for decode-sized tensor-parallel messages (bf16 sum), an
+// alternative to the RCCL ring for the two per-layer all-reduces of a TP decode step
+// (LlamaRunner::all_reduce; enabled with LS_ONESHOT_AR=1).
+//
+// Why: a decode step's all-reduce moves B x hidden bf16 (256 x 8192 x 2 B = 4 MiB at
+// B = 256 on Llama-3-70B), and a ring pays 2(W-1) latency-bound hops for it.  On xGMI
+// every GPU has a direct link to every other one (point-to-point, 8 GPUs fully
+// connected), so one step suffices: every rank publishes its input in a buffer the
+// others can read (IPC-mapped device memory), and every rank reads all W inputs and
+// sums them itself -- (W-1) x message bytes in over W-1 links in parallel.
+//
+// Protocol (per workgroup b, which owns a fixed slice of the message):
+//   e = ++epoch[b]                          (local counter, one per workgroup)
+//   copy my slice of the input into my buffer half (e & 1)
+//   system-scope release fence; store flag[peer][my rank][b] = e on every peer (vector
+//     atomic stores -- never scalar stores)
+//   wait until flag[me][src][b] >= e for every src (system-scope acquire loads; the spin
+//     is bounded: on timeout *err is set and the kernel finishes instead of hanging)
+//   out slice = sum over w = 0..W-1 of rank w's buffer half (e & 1), same order on every
+//     rank, so every rank produces bit-identical results
+// Two buffer halves make back-to-back calls safe: a rank reaches call k+2 (which
+// rewrites half k & 1) only after every peer has flagged call k+1, i.e. finished call k.
+#include <torch/extension.h>
+#include <ATen/hip/HIPContext.h>
+#include <torch/csrc/distributed/c10d/ProcessGroup.hpp>
+#include <hip/hip_runtime.h>
+#include <vector>
+#include "common.h"
+
+namespace py = pybind11;
+
+#define AR_OK(x)                                                                    \
+  do {                                                                              \
+    hipError_t e_ = (x);                                                            \
+    TORCH_CHECK(e_ == hipSuccess, #x " failed: ", hipGetErrorString(e_));           \
+  } while (0)
+
+namespace {
+
+constexpr int kMaxRanks = 8;
+constexpr int kBlocks = 64;          // workgroups (message slices) per call
+constexpr int kThreads = 256;
+constexpr long long kSpinLimit = 1LL << 21;   // ~seconds: a peer that never arrives sets *err
+
+// Per-launch I/O of up to kMaxRanks ranks: a real call fills entry 0 (one rank per
+// process); the single-GPU rehearsal launches every simulated rank in ONE grid
+// (blockIdx.y = entry) so all of them are co-resident -- separate streams could share a
+// hardware queue and serialise, leaving the first kernel waiting for the others.
+struct IOTable {
+  const bf16* in[kMaxRanks];
+  bf16* out[kMaxRanks];
+  int* epoch[kMaxRanks];
+  int* err[kMaxRanks];
+};
+
+struct PeerTable {
+  bf16* data[kMaxRanks];   // rank w's buffer base (two halves of `cap` elements)
+  int* flags[kMaxRanks];   // rank w's flag array [kMaxRanks][kBlocks]
+};
+
+// in and out may alias (in place): a workgroup reads only its own slice of `in`, before
+// its first barrier, and writes `out` after the exchange.
+__global__ void __launch_bounds__(kThreads) oneshot_ar_kernel(IOTable io, int64_t n, int64_t cap, int rank0, int W,
+                                                              PeerTable tbl) {
+  const int b = blockIdx.x, tid = threadIdx.x, y = blockIdx.y;
+  const int rank = rank0 + y;
+  const bf16* in = io.in[y];
+  bf16* out = io.out[y];
+  int* epoch = io.epoch[y];
+  const int e = epoch[b] + 1;
+  const int64_t half = (int64_t)(e & 1) * cap;
+  // slice of whole 8-element vectors owned by this workgroup
+  const int64_t nvec = n / 8;
+  const int64_t per = (nvec + kBlocks - 1) / kBlocks;
+  const int64_t v0 = b * per, v1 = min(nvec, v0 + per);
+  bf16* mine = tbl.data[rank] + half;
+  for (int64_t v = v0 + tid; v < v1; v += kThreads) st16(mine + v * 8, ld16(in + v * 8));
+  if (b == 0)   // ragged tail (n % 8 elements)
+    for (int64_t i = nvec * 8 + tid; i < n; i += kThreads) mine[i] = in[i];
+  __threadfence_system();
+  __syncthreads();
+  if (tid < W) __hip_atomic_store(tbl.flags[tid] + rank * kBlocks + b, e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (tid < W) {
+    const int* f = tbl.flags[rank] + tid * kBlocks + b;
+    long long spins = 0;
+    while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < e) {
+      if (++spins > kSpinLimit) {
+        __hip_atomic_store(io.err[y], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  __syncthreads();
+  __threadfence_system();
+  for (int64_t v = v0 + tid; v < v1; v += kThreads) {
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int w = 0; w < W; ++w) {
+      float x[8];
+      unpack8(ld16(tbl.data[w] + half + v * 8), x);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += x[j];
+    }
+    st16(out + v * 8, pack8(acc));
+  }
+  if (b == 0)
+    for (int64_t i = nvec * 8 + tid; i < n; i += kThreads) {
+      float a = 0.f;
+      for (int w = 0; w < W; ++w) a += (float)tbl.data[w][half + i];
+      out[i] = (bf16)a;
+    }
+  __syncthreads();
+  if (tid == 0) epoch[b] = e;
+}
+
+void launch_oneshot(const IOTable& io, int ranks_in_grid, int64_t n, int64_t cap, int rank0, int W,
+                    const PeerTable& tbl, hipStream_t stream) {
+  oneshot_ar_kernel<<<dim3(kBlocks, ranks_in_grid), kThreads, 0, stream>>>(io, n, cap, rank0, W, tbl);
+}
+
+int64_t region_bytes(int64_t cap) { return 2 * cap * (int64_t)sizeof(bf16) + kMaxRanks * kBlocks * sizeof(int); }
+
+}  // namespace
+
+// ---------------------------------------------------------------------------------
+// Multi-process form: one instance per TP rank, built collectively over the process
+// group (IPC handles exchanged with an all-gather).
+class OneShotAllReduce {
+ public:
+  OneShotAllReduce(c10::intrusive_ptr<::c10d::ProcessGroup> pg, int64_t max_elems)
+      : pg_(std::move(pg)), cap_(max_elems) {
+    W_ = pg_->getSize();
+    rank_ = pg_->getRank();
+    TORCH_CHECK(W_ >= 1 && W_ <= kMaxRanks, "one-shot all-reduce supports up to ", kMaxRanks, " ranks");
+    const int64_t bytes = region_bytes(cap_);
+    AR_OK(hipMalloc(&base_, bytes));
+    AR_OK(hipMemset(base_, 0, bytes));
+    AR_OK(hipMalloc(&epoch_, kBlocks * sizeof(int) + sizeof(int)));
+    AR_OK(hipMemset(epoch_, 0, kBlocks * sizeof(int) + sizeof(int)));
+    err_ = epoch_ + kBlocks;
+    hipIpcMemHandle_t h;
+    AR_OK(hipIpcGetMemHandle(&h, base_));
+    auto opts = at::TensorOptions().dtype(at::kByte).device(at::kCUDA, at::hip::current_device());
+    at::Tensor mine = at::from_blob(&h, {(int64_t)sizeof(h)}, at::kByte).to(opts);
+    std::vector<at::Tensor> parts;
+    for (int w = 0; w < W_; ++w) parts.push_back(at::empty({(int64_t)sizeof(h)}, opts));
+    std::vector<std::vector<at::Tensor>> outs{parts};
+    std::vector<at::Tensor> ins{mine};
+    pg_->allgather(outs, ins)->wait();
+    for (int w = 0; w < W_; ++w) {
+      char* p = nullptr;
+      if (w == rank_) {
+        p = (char*)base_;
+      } else {
+        hipIpcMemHandle_t hw;
+        at::Tensor hb = parts[w].cpu();
+        memcpy(&hw, hb.data_ptr(), sizeof(hw));
+        void* q = nullptr;
+        AR_OK(hipIpcOpenMemHandle(&q, hw, hipIpcMemLazyEnablePeerAccess));
+        opened_.push_back(q);
+        p = (char*)q;
+      }
+      tbl_.data[w] = (bf16*)p;
+      tbl_.flags[w] = (int*)(p + 2 * cap_ * sizeof(bf16));
+    }
+  }
+
+  ~OneShotAllReduce() {
+    for (void* q : opened_) (void)hipIpcCloseMemHandle(q);
+    (void)hipFree(base_);
+    (void)hipFree(epoch_);
+  }
+
+  int64_t capacity() const { return cap_; }
+
+  // In place: t = sum over ranks of t (bf16, contiguous, numel <= capacity()).
+  void run(at::Tensor& t) {
+    TORCH_CHECK(t.scalar_type() == at::kBFloat16 && t.is_contiguous() && t.numel() <= cap_,
+                "one-shot all-reduce: contiguous bf16 up to ", cap_, " elements");
+    IOTable io{};
+    io.in[0] = (const bf16*)t.data_ptr();
+    io.out[0] = (bf16*)t.data_ptr();
+    io.epoch[0] = epoch_;
+    io.err[0] = err_;
+    launch_oneshot(io, 1, t.numel(), cap_, rank_, W_, tbl_, at::hip::getCurrentHIPStream().stream());
+  }
+
+  // Non-zero when a wait timed out (a peer never arrived): the results are invalid.
+  int64_t error() {
+    int e = 0;
+    AR_OK(hipMemcpy(&e, err_, sizeof(int), hipMemcpyDeviceToHost));
+    return e;
+  }
+
+ private:
+  c10::intrusive_ptr<::c10d::ProcessGroup> pg_;
+  int64_t cap_;
+  int W_ = 1, rank_ = 0;
+  void* base_ = nullptr;
+  int* epoch_ = nullptr;
+  int* err_ = nullptr;
+  PeerTable tbl_{};
+  std::vector<void*> opened_;
+};
+
+std::shared_ptr<OneShotAllReduce> make_oneshot_allreduce(c10::intrusive_ptr<::c10d::ProcessGroup> pg,
+                                                         int64_t max_elems) {
+  return std::make_shared<OneShotAllReduce>(std::move(pg), max_elems);
+}
+
+void oneshot_allreduce_run(const std::shared_ptr<OneShotAllReduce>& ar, at::Tensor t) { ar->run(t); }
+
+// Single-GPU rehearsal of the protocol: W simulated ranks with their own buffers, flag
+// arrays and epoch counters on one device, all launched in ONE grid (co-resident),
+// `calls` back-to-back calls.  Returns the per-rank outputs of the last call and the
+// per-rank error flags.
+std::vector<at::Tensor> oneshot_allreduce_sim(std::vector<at::Tensor> inputs, int64_t calls) {
+  const int W = (int)inputs.size();
+  TORCH_CHECK(W >= 1 && W <= kMaxRanks && calls >= 1);
+  const int64_t n = inputs[0].numel();
+  for (auto& t : inputs)
+    TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kBFloat16 && t.is_contiguous() && t.numel() == n);
+  auto opts = inputs[0].options();
+  std::vector<at::Tensor> regions, outs;
+  at::Tensor epochs = at::zeros({W, kBlocks + 1}, opts.dtype(at::kInt));
+  PeerTable tbl{};
+  IOTable io{};
+  for (int w = 0; w < W; ++w) {
+    regions.push_back(at::zeros({region_bytes(n)}, opts.dtype(at::kByte)));
+    outs.push_back(at::empty_like(inputs[w]));
+    char* p = (char*)regions[w].data_ptr();
+    tbl.data[w] = (bf16*)p;
+    tbl.flags[w] = (int*)(p + 2 * n * sizeof(bf16));
+    io.in[w] = (const bf16*)inputs[w].data_ptr();
+    io.out[w] = (bf16*)outs[w].data_ptr();
+    io.epoch[w] = epochs.data_ptr<int>() + w * (kBlocks + 1);
+    io.err[w] = io.epoch[w] + kBlocks;
+  }
+  auto stream = at::hip::getCurrentHIPStream().stream();
+  for (int64_t c = 0; c < calls; ++c) launch_oneshot(io, W, n, n, 0, W, tbl, stream);
+  AR_OK(hipStreamSynchronize(stream));
+  outs.push_back(epochs.select(1, kBlocks).contiguous());
+  return outs;
+}
+
+// World-size-agnostic self test over a real process group: build the instance, run one
+// in-place all-reduce of t, return the error flag (0 = every peer arrived).
+int64_t oneshot_allreduce_selftest(py::object process_group, at::Tensor t) {
+  auto pg = py::cast<c10::intrusive_ptr<::c10d::ProcessGroup>>(process_group);
+  auto ar = make_oneshot_allreduce(pg, t.numel());
+  ar->run(t);
+  AR_OK(hipStreamSynchronize(at::hip::getCurrentHIPStream().stream()));
+  return ar->error();
+}

@@ -33,6 +33,8 @@ void tp_sample_pick(at::Tensor logits, int64_t vstart, int64_t vtot, at::Tensor 
                     at::Tensor hist_all, int64_t n_top, at::Tensor cand);
 void tp_sample_final(at::Tensor stats_all, at::Tensor cand_all, int64_t world, int64_t rows, at::Tensor temperature,
                      int64_t n_top, at::Tensor out_tok, at::Tensor out_lp, at::Tensor top_ids, at::Tensor top_lps);
+std::vector<at::Tensor> oneshot_allreduce_sim(std::vector<at::Tensor> inputs, int64_t calls);
+int64_t oneshot_allreduce_selftest(py::object process_group, at::Tensor t);
 void knn_topk(at::Tensor X, at::Tensor Q, int64_t K, at::Tensor out_s, at::Tensor out_i, at::Tensor ws_s,
               at::Tensor ws_i, int64_t sample);
 int64_t knn_default_sample();
@@ -76,6 +78,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("pool_embeddings", &pool_embeddings);
   m.def("l2_normalize_rows", &l2_normalize_rows);
   m.def("knn_topk", &knn_topk);
+  m.def("oneshot_allreduce_sim", &oneshot_allreduce_sim);
+  m.def("oneshot_allreduce_selftest", &oneshot_allreduce_selftest);
   m.def("tp_sample_stats", &tp_sample_stats);
   m.def("tp_sample_hist", &tp_sample_hist);
   m.def("tp_sample_pick", &tp_sample_pick);

@@ -74,6 +74,11 @@ void tp_sample_pick(at::Tensor logits, int64_t vstart, int64_t vtot, at::Tensor 
 void tp_sample_final(at::Tensor stats_all, at::Tensor cand_all, int64_t world, int64_t rows, at::Tensor temperature,
                      int64_t n_top, at::Tensor out_tok, at::Tensor out_lp, at::Tensor top_ids, at::Tensor top_lps);
 
+class OneShotAllReduce;
+std::shared_ptr<OneShotAllReduce> make_oneshot_allreduce(c10::intrusive_ptr<::c10d::ProcessGroup> pg,
+                                                         int64_t max_elems);
+void oneshot_allreduce_run(const std::shared_ptr<OneShotAllReduce>& ar, at::Tensor t);
+
 void skinny_gemm(at::Tensor out, at::Tensor x, at::Tensor w);
 void gemm_fused(at::Tensor out, at::Tensor x, at::Tensor w, c10::optional<at::Tensor> bias, bool gelu,
                 c10::optional<at::Tensor> residual, c10::optional<at::Tensor> ln_stats_in, int64_t ln_width,
@@ -119,6 +124,13 @@ class LlamaRunner {
                 in_norm_.size() == L && post_norm_.size() == L && kc_.size() == L && vc_.size() == L,
                 "inconsistent layer lists");
     if (!process_group.is_none()) pg_ = py::cast<c10::intrusive_ptr<::c10d::ProcessGroup>>(process_group);
+    // LS_ONESHOT_AR=1: decode-sized all-reduces (<= LS_ONESHOT_AR_MAX elements, default
+    // 256 x 8192) through the one-shot IPC kernel (allreduce.hip) instead of RCCL
+    if (pg_ && getenv("LS_ONESHOT_AR") && atoi(getenv("LS_ONESHOT_AR")) != 0) {
+      const int64_t mx = getenv("LS_ONESHOT_AR_MAX") ? atoll(getenv("LS_ONESHOT_AR_MAX")) : 256 * 8192;
+      oneshot_ = make_oneshot_allreduce(pg_, mx);
+      oneshot_max_ = mx;
+    }
   }
 
   // LM head with f32 OUTPUT straight from the GEMM (hipBLASLt bf16 x bf16 -> f32): a bf16
@@ -351,9 +363,16 @@ class LlamaRunner {
 
   void all_reduce(at::Tensor& t) {
     if (!pg_) return;
+    if (oneshot_ && t.scalar_type() == at::kBFloat16 && t.is_contiguous() && t.numel() <= oneshot_max_) {
+      oneshot_allreduce_run(oneshot_, t);
+      return;
+    }
     std::vector<at::Tensor> v{t};
     pg_->allreduce(v)->wait();
   }
+
+  std::shared_ptr<OneShotAllReduce> oneshot_;
+  int64_t oneshot_max_ = 0;
 
   bool f32_head_ = true;
   at::Tensor embed_;

@@ -52,3 +52,31 @@ def test_sharded_knn_service_rccl_world1(rccl_world1):
         assert all(d["text"] == "t" + d["id"][1:] for d in res)
         if i % 3 == 0:
             assert all(len(d["vector"]) == 384 for d in res)
+
+
+@pytest.mark.parametrize("W", [2, 3, 4, 8])
+def test_oneshot_allreduce_protocol_simulated_ranks(W):
+    """allreduce.hip's flag/epoch protocol with W simulated ranks (own buffers, flag
+    arrays and epoch counters) in one grid on one GPU, three back-to-back calls: every
+    rank gets the same bits, equal to the fp32 sum rounded once, and no wait timed out."""
+    from langstream_amd import ops
+    torch.manual_seed(W)
+    n = 256 * 1024 + 5                      # a ragged tail too
+    ins = [torch.randn(n, device="cuda").to(torch.bfloat16) for _ in range(W)]
+    res = ops.hip().oneshot_allreduce_sim(ins, 3)
+    outs, errs = res[:W], res[W]
+    assert int(errs.sum()) == 0
+    want = torch.stack([t.float() for t in ins]).sum(0)
+    for o in outs:
+        assert torch.equal(o, outs[0])
+    assert (outs[0].float() - want).abs().max() <= 0.02 * want.abs().max()
+
+
+def test_oneshot_allreduce_world1_rccl(rccl_world1):
+    """The multi-process form over a real RCCL group (IPC handle exchange by all-gather;
+    at world 1 the only buffer is the rank's own)."""
+    from langstream_amd import ops
+    t = torch.randn(8192 * 3 + 3, device="cuda").to(torch.bfloat16)
+    ref = t.clone()
+    assert ops.hip().oneshot_allreduce_selftest(dist.group.WORLD, t) == 0
+    assert torch.equal(t, ref)

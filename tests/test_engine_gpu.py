@@ -195,12 +195,16 @@ def test_vector_store_search():
     assert vs.search(v[[5]], k=1)[0][0]["id"] != 5
 
 
-def test_native_executor_tp_path_world1_rccl():
+@pytest.mark.parametrize("oneshot", [False, True])
+def test_native_executor_tp_path_world1_rccl(oneshot, monkeypatch):
     """The TP code path of the native executor at world size 1 over a real RCCL process
     group: all-reduces inside the graph-captured forward, and the vocab-parallel sampler
     (statistics / histogram / candidate exchanges) instead of the single-GPU sampler.
-    Same greedy tokens and log-probs as the non-TP executor on the same weights."""
+    Same greedy tokens and log-probs as the non-TP executor on the same weights.
+    oneshot: the per-layer all-reduces go through allreduce.hip (LS_ONESHOT_AR=1)."""
     import socket
+    if oneshot:
+        monkeypatch.setenv("LS_ONESHOT_AR", "1")
     import torch.distributed as dist
     from langstream_amd.models.llama import TPInfo
     with socket.socket() as s:
