@@ -88,6 +88,7 @@ class ShardedKnn:
         self.data = dist.new_group(backend=backend) if backend == "nccl" else dist.new_group(backend="gloo")
         self.data_dev = self.device if backend == "nccl" else torch.device("cpu")
         self.tick_s = tick_s
+        self.max_idle_s = max(tick_s, 0.004)
         self.max_q = max_queries_per_round
         self._pending: List[_Req] = []
         self._cv = threading.Condition()
@@ -123,18 +124,32 @@ class ShardedKnn:
         self._thread.join(timeout)
 
     # ------------------------------------------------------------------ collectives
+    _SLOT = 2048   # round headers fit in one fixed-size all-gather slot almost always
+
     def _allgather_bytes(self, b: bytes) -> List[bytes]:
-        n = torch.tensor([len(b)], dtype=torch.int64)
-        ns = torch.empty(self.world, dtype=torch.int64)
-        dist.all_gather_into_tensor(ns, n, group=self.meta)
-        m = int(ns.max())
+        """All-gather of variable-length byte strings over the gloo group: ONE collective
+        with a fixed 2 KiB slot per rank (4-byte length + payload); only when some rank's
+        payload is longer do all ranks (who all see every length) run a second round."""
+        slot = torch.zeros(self._SLOT, dtype=torch.uint8)
+        n = len(b)
+        slot[:4] = torch.tensor([n], dtype=torch.int32).view(torch.uint8)
+        if 0 < n <= self._SLOT - 4:
+            slot[4: 4 + n] = torch.frombuffer(bytearray(b), dtype=torch.uint8)
+        out = torch.empty(self.world * self._SLOT, dtype=torch.uint8)
+        dist.all_gather_into_tensor(out, slot, group=self.meta)
+        o = out.numpy()
+        lens = [int(np.frombuffer(o[i * self._SLOT: i * self._SLOT + 4].tobytes(), np.int32)[0])
+                for i in range(self.world)]
+        if max(lens) <= self._SLOT - 4:
+            return [o[i * self._SLOT + 4: i * self._SLOT + 4 + lens[i]].tobytes() for i in range(self.world)]
+        m = max(lens)
         buf = torch.zeros(m, dtype=torch.uint8)
         if b:
-            buf[: len(b)] = torch.frombuffer(bytearray(b), dtype=torch.uint8)
+            buf[:n] = torch.frombuffer(bytearray(b), dtype=torch.uint8)
         out = torch.empty(self.world * m, dtype=torch.uint8)
         dist.all_gather_into_tensor(out, buf, group=self.meta)
         o = out.numpy()
-        return [o[i * m: i * m + int(ns[i])].tobytes() for i in range(self.world)]
+        return [o[i * m: i * m + lens[i]].tobytes() for i in range(self.world)]
 
     def _alltoall_bytes(self, per_dest: List[bytes]) -> List[bytes]:
         send_n = torch.tensor([len(b) for b in per_dest], dtype=torch.int64)
@@ -174,6 +189,7 @@ class ShardedKnn:
                     r.fut.set_exception(e if isinstance(e, Exception) else RuntimeError(str(e)))
 
     def _serve(self) -> None:
+        idle = 0
         try:
             while True:
                 with self._cv:
@@ -188,10 +204,15 @@ class ShardedKnn:
                 if all(h["s"] for h in hdrs):
                     return
                 if not any(h["r"] for h in hdrs):
+                    # idle: back off (tick, 2 tick, ... up to max_idle_s) so an idle service
+                    # does not run a collective every millisecond next to the engines; a
+                    # local request wakes this rank at once, remote ones within the backoff
+                    idle = min(idle + 1, 16)
                     with self._cv:
                         if not self._pending:
-                            self._cv.wait(self.tick_s)
+                            self._cv.wait(min(self.max_idle_s, self.tick_s * (1 << min(idle, 10))))
                     continue
+                idle = 0
                 self.rounds += 1
                 try:
                     self._round(take, hdrs)

@@ -289,3 +289,23 @@ def test_sharded_knn_equals_single_store():
         assert {d["owner"] for d in got} == {0, 1} or len(got) < 2
         if i % 2 == 0:
             assert all(len(d["vector"]) == 48 for d in got)
+
+
+def _allgather_bytes_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from langstream_amd.engine.dist_knn import ShardedKnn
+        x = ShardedKnn.__new__(ShardedKnn)       # only the byte collectives
+        x.world, x.meta = world, dist.new_group(backend="gloo")
+        r1 = x._allgather_bytes(b"a" * (10 if rank == 0 else 5000))   # one rank overflows the slot
+        r2 = x._allgather_bytes(b"" if rank == 0 else b"xyz")          # fast path, an empty entry
+        if rank == 0:
+            q.put(([len(a) for a in r1], r2))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_knn_header_allgather_slot_and_overflow():
+    lens, r2 = _spawn(_allgather_bytes_worker)
+    assert lens == [10, 5000] and r2 == [b"", b"xyz"]
