@@ -562,7 +562,9 @@ def main():
             assign[info["topic"]] = info.get("assignment")
     mine = {"elapsed": elapsed, "lats": my_lats, "chunks": chunks, "assign": assign,
             "prefill_tokens": stats.get("prefill_tokens", 0), "requests": stats.get("requests", 0),
-            "knn_rounds": dist_knn.active().rounds if dist_knn.active() else 0}
+            "knn_rounds": dist_knn.active().rounds if dist_knn.active() else 0,
+            "knn_stats": ({k: (round(v, 3) if isinstance(v, float) else v) for k, v in dist_knn.active().stats.items()}
+                          if dist_knn.active() else None)}
     if multi:
         gathered = [None] * world
         dist.all_gather_object(gathered, mine, group=ctrl)
@@ -596,6 +598,7 @@ def main():
             "ingest": {"pages_per_s": round(args.docs * args.steps * world / elapsed, 2),
                        "chunks_per_s": round(sum(g["chunks"] for g in gathered) / elapsed, 2)},
             "latency_samples": len(all_lats), "knn_rounds_per_rank": [g["knn_rounds"] for g in gathered],
+            "knn_stats_rank0": gathered[0]["knn_stats"],
             "partitions_per_rank": [g["assign"] for g in gathered],
             "setup_s": round(setup_s, 1),
             "engine_rank0": dict(stats, exec_ms=dict(zip(("upload", "enqueue", "download", "wait"),

@@ -94,6 +94,8 @@ class ShardedKnn:
         self._cv = threading.Condition()
         self._stop = False
         self.rounds = 0
+        self.stats = {"rounds": 0, "queries": 0, "search_s": 0.0, "payload_s": 0.0, "round_s": 0.0,
+                      "header_s": 0.0}
         self._thread = threading.Thread(target=self._loop, name="sharded-knn", daemon=True)
         self._thread.start()
 
@@ -200,7 +202,9 @@ class ShardedKnn:
                         n += r.q.shape[0]
                     stopping = self._stop and not take and not self._pending
                 hdr = {"s": stopping, "r": [[r.coll, int(r.q.shape[0]), r.k, r.inc, int(r.q.shape[1])] for r in take]}
+                t_h = time.perf_counter()
                 hdrs = [json.loads(b) for b in self._allgather_bytes(json.dumps(hdr).encode())]
+                self.stats["header_s"] += time.perf_counter() - t_h
                 if all(h["s"] for h in hdrs):
                     return
                 if not any(h["r"] for h in hdrs):
@@ -214,8 +218,12 @@ class ShardedKnn:
                     continue
                 idle = 0
                 self.rounds += 1
+                self.stats["rounds"] += 1
+                self.stats["queries"] += sum(int(r.q.shape[0]) for r in take)
+                t_r = time.perf_counter()
                 try:
                     self._round(take, hdrs)
+                    self.stats["round_s"] += time.perf_counter() - t_r
                 except Exception as e:  # noqa: BLE001  (a local failure after the collectives)
                     log.exception("sharded kNN round failed")
                     for r in take:
@@ -254,6 +262,7 @@ class ShardedKnn:
                 if any(r[3] for _, r in reqs_all):
                     vec_colls.add(coll)
                 qmax = max(counts)
+                t_s = time.perf_counter()
                 qloc = torch.zeros(qmax, dim, dtype=torch.float32)
                 if mine:
                     qloc[: counts[me]] = torch.cat([r.q for r in mine])
@@ -280,6 +289,7 @@ class ShardedKnn:
                 rows = torch.gather(ci, 1, sel)
                 owners = sel // kmax
                 top_s, rows, owners = (t.tolist() for t in to_host(top_s, rows, owners.int()))
+                self.stats["search_s"] += time.perf_counter() - t_s
                 qi = 0
                 for r in mine:
                     per_q = []
@@ -291,26 +301,35 @@ class ShardedKnn:
                         per_q.append(lst)
                     hits[id(r)] = per_q
                     qi += r.q.shape[0]
-            # phase 2: payloads of the merged top-k rows, asked from their owners
-            asks = [msgpack.packb({c: sorted(v) for c, v in need[d].items()}) for d in range(W)]
-            got_asks = [msgpack.unpackb(b, strict_map_key=False) if b else {} for b in self._alltoall_bytes(asks)]
-            answers = []
-            for src in range(W):
+            # phase 2: payloads of the merged top-k rows, asked from their owners; the rows
+            # this rank owns are served directly (no serialisation, no exchange)
+            t_p = time.perf_counter()
+
+            def serve(asked):
                 ans = {}
-                for coll, rws in got_asks[src].items():
+                for coll, rws in asked.items():
                     st = stores.get(coll)
                     if st is None:
                         continue
+                    rws = sorted(rws)
                     vecs = st.row_vectors(rws) if coll in vec_colls else {}
                     ans[coll] = {rw: (st.row_payload(rw),
                                       np.asarray(vecs[rw], np.float32).tobytes() if rw in vecs else None)
                                  for rw in rws if 0 <= rw < len(st)}
-                answers.append(msgpack.packb(ans, use_bin_type=True))
+                return ans
+
+            local = serve(need[me])
+            asks = [b"" if d == me else msgpack.packb({c: sorted(v) for c, v in need[d].items()}) for d in range(W)]
+            got_asks = [msgpack.unpackb(b, strict_map_key=False) if b else {} for b in self._alltoall_bytes(asks)]
+            answers = [b"" if src == me else msgpack.packb(serve(got_asks[src]), use_bin_type=True)
+                       for src in range(W)]
         finally:
             for lk in reversed(locks):
                 lk.release()
         payload = [msgpack.unpackb(b, raw=False, strict_map_key=False) if b else {}
                    for b in self._alltoall_bytes(answers)]
+        payload[me] = local
+        self.stats["payload_s"] += time.perf_counter() - t_p
         for r in take:
             if r.fut.done():
                 continue
