@@ -29,6 +29,7 @@ from __future__ import annotations
 
 import json
 import logging
+import os
 import threading
 import time
 from concurrent.futures import Future
@@ -39,7 +40,7 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
-from ..utils.gpu import on_aux, to_host
+from ..utils.gpu import on_search, to_host
 from .vector_store import VectorStoreRegistry
 
 log = logging.getLogger(__name__)
@@ -85,7 +86,14 @@ class ShardedKnn:
             self.device = torch.device("cuda", torch.cuda.current_device())
         # separate groups so the service never interleaves with the caller's collectives
         self.meta = dist.new_group(backend="gloo")
-        self.data = dist.new_group(backend=backend) if backend == "nccl" else dist.new_group(backend="gloo")
+        if backend == "nccl":
+            # high-priority RCCL streams: a round's collectives must not queue behind the
+            # LLM engine's decode graphs on a shared hardware queue
+            opts = dist.ProcessGroupNCCL.Options()
+            opts.is_high_priority_stream = os.environ.get("LS_KNN_HIPRI", "1") != "0"
+            self.data = dist.new_group(backend="nccl", pg_options=opts)
+        else:
+            self.data = dist.new_group(backend="gloo")
         self.data_dev = self.device if backend == "nccl" else torch.device("cpu")
         self.tick_s = tick_s
         self.max_idle_s = max(tick_s, 0.004)
@@ -96,6 +104,10 @@ class ShardedKnn:
         self.rounds = 0
         self.stats = {"rounds": 0, "queries": 0, "search_s": 0.0, "payload_s": 0.0, "round_s": 0.0,
                       "header_s": 0.0}
+        # LS_KNN_PROFILE=1: synchronise after each phase of a round's search (diagnosis only)
+        self._prof = os.environ.get("LS_KNN_PROFILE") == "1" and self.device.type == "cuda"
+        if self._prof:
+            self.stats.update(gather_s=0.0, topk_s=0.0, a2a_s=0.0)
         self._thread = threading.Thread(target=self._loop, name="sharded-knn", daemon=True)
         self._thread.start()
 
@@ -174,10 +186,11 @@ class ShardedKnn:
                 torch.cuda.set_device(self.device)
                 # Every device op of a round -- the H2D query copy, the RCCL all-gather and
                 # all-to-all (which order themselves after the CURRENT stream), the kNN
-                # kernel and the D2H copies -- runs on the one auxiliary stream, so they are
-                # ordered with each other and never queue behind the LLM engine's default
-                # stream.
-                with on_aux(self.device):
+                # kernel and the D2H copies -- runs on the one search stream, so they are
+                # ordered with each other and queue neither behind the LLM engine's steps
+                # nor behind ingest embedding batches (the store orders each search after
+                # its last write).
+                with on_search(self.device):
                     self._serve()
             else:
                 self._serve()
@@ -237,6 +250,17 @@ class ShardedKnn:
             for r in pend:
                 r.fut.set_exception(e)
 
+    def _phase(self, key: str, t0: float) -> float:
+        """LS_KNN_PROFILE: charge the time since ``t0`` (after a device sync) to ``key``;
+        the remainder of the search keeps accruing to search_s."""
+        if not self._prof:
+            return t0
+        torch.cuda.current_stream().synchronize()   # the search stream, not the LLM's
+        t = time.perf_counter()
+        self.stats[key] += t - t0
+        self.stats["search_s"] += t - t0
+        return t
+
     def _round(self, take: List[_Req], hdrs: List[Dict[str, Any]]) -> None:
         W, me = self.world, self.rank
         colls = sorted({r[0] for h in hdrs for r in h["r"]})
@@ -263,12 +287,14 @@ class ShardedKnn:
                     vec_colls.add(coll)
                 qmax = max(counts)
                 t_s = time.perf_counter()
-                qloc = torch.zeros(qmax, dim, dtype=torch.float32)
+                pin = self.data_dev.type == "cuda"
+                qloc = torch.zeros(qmax, dim, dtype=torch.float32, pin_memory=pin)
                 if mine:
-                    qloc[: counts[me]] = torch.cat([r.q for r in mine])
-                qloc = qloc.to(self.data_dev)
+                    torch.cat([r.q for r in mine], out=qloc[: counts[me]])
+                qloc = qloc.to(self.data_dev, non_blocking=pin)   # pinned: async, no staging copy
                 qall = torch.empty(W * qmax, dim, dtype=torch.float32, device=self.data_dev)
                 dist.all_gather_into_tensor(qall, qloc, group=self.data)
+                t_s = self._phase("gather_s", t_s)
                 store = stores.get(coll)
                 if store is not None and store.dim == dim and len(store):
                     s, idx = store.topk_rows(qall.to(store.device, store.dtype), kmax)
@@ -277,8 +303,10 @@ class ShardedKnn:
                     s = torch.full((W * qmax, kmax), float("-inf"), device=self.data_dev)
                     idx = torch.full((W * qmax, kmax), -1, dtype=torch.int32, device=self.data_dev)
                 send = torch.stack([s.float(), idx.int().view(torch.float32)], -1).contiguous()  # [W*qmax,k,2]
+                t_s = self._phase("topk_s", t_s)
                 recv = torch.empty_like(send)
                 dist.all_to_all_single(recv, send, group=self.data)
+                t_s = self._phase("a2a_s", t_s)
                 n_me = counts[me]
                 if n_me == 0:
                     continue

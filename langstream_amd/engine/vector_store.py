@@ -38,7 +38,7 @@ import numpy as np
 import torch
 
 from .. import ops
-from ..utils.gpu import on_aux, to_host
+from ..utils.gpu import aux_stream, on_search, to_host
 
 log = logging.getLogger(__name__)
 
@@ -128,16 +128,19 @@ class VectorStore:
         if not self.kernel_dim:
             log.warning("vector collection %s: dim %d has no kNN kernel instantiation %s; searches use the exact "
                         "GEMM + torch.topk path", name, dim, KERNEL_DIMS)
-        with on_aux(self.device):  # every GPU op of the store runs on the auxiliary stream
+        with on_search(self.device):  # every GPU op of the store runs on the search stream
             self._vecs = torch.zeros(max(16, capacity), dim, device=self.device, dtype=dtype)
         self._n = 0
         self._ids: List[Any] = []
         self._meta: List[Dict[str, Any]] = []
         self._row: Dict[Any, int] = {}
         self.lock = threading.RLock()
+        self._write_ev = None   # recorded on the store stream after every device write
         self._persist = _Persistence(persist_dir, fsync) if persist_dir else None
         if self._persist is not None:
-            self._restore()
+            with on_search(self.device), self.lock:
+                self._restore()
+                self._mark_written()
 
     def __len__(self) -> int:
         return self._n
@@ -166,13 +169,17 @@ class VectorStore:
         metadata = list(metadata) if metadata is not None else [{} for _ in ids]
         if len(metadata) != len(ids):
             raise ValueError("ids and metadata lengths differ")
-        with on_aux(self.device), self.lock:
+        with on_search(self.device), self.lock:
+            if isinstance(vectors, torch.Tensor) and vectors.is_cuda:
+                # device vectors come from the embedding engine's auxiliary stream
+                torch.cuda.current_stream().wait_stream(aux_stream(self.device))
             vecs = self._normalize(vectors)
             if vecs.shape[0] != len(ids):
                 raise ValueError("ids and vectors lengths differ")
             if self._persist is not None:
                 self._persist.log_upsert(ids, to_host(vecs.float())[0].numpy(), metadata)
             self._apply_upsert(ids, vecs, metadata)
+            self._mark_written()
             self._maybe_compact()
 
     def _apply_upsert(self, ids, vecs: torch.Tensor, metadata) -> None:
@@ -200,13 +207,14 @@ class VectorStore:
                                if len(src) != len(rows) else vecs)
 
     def delete(self, ids: Sequence[Any]) -> int:
-        with on_aux(self.device), self.lock:
+        with on_search(self.device), self.lock:
             present = [k for k in dict.fromkeys(ids) if k in self._row]
             if not present:
                 return 0
             if self._persist is not None:
                 self._persist.log_delete(present)
             n = self._apply_delete(present)
+            self._mark_written()
             self._maybe_compact()
             return n
 
@@ -248,6 +256,22 @@ class VectorStore:
         if self._n:
             log.info("vector collection %s restored: %d rows (%d WAL entries)", self.name, self._n, len(entries))
 
+    def _mark_written(self) -> None:
+        """(caller holding the lock) order later reads on other streams after the device
+        writes just enqueued on the store's stream."""
+        if self.device.type == "cuda":
+            ev = torch.cuda.Event()
+            ev.record()
+            self._write_ev = ev
+
+    def _order_read(self) -> None:
+        """(caller holding the lock, on the stream that will read) wait for the last
+        write and keep the row buffer alive for this stream."""
+        if self.device.type == "cuda":
+            if self._write_ev is not None:
+                torch.cuda.current_stream().wait_event(self._write_ev)
+            self._vecs.record_stream(torch.cuda.current_stream())
+
     def _maybe_compact(self) -> None:
         p = self._persist
         if p is None or p.wal_bytes() < max(64 << 20, self._n * self.dim * 2):
@@ -258,7 +282,7 @@ class VectorStore:
         """Write a snapshot of the collection and truncate the WAL."""
         if self._persist is None:
             return
-        with on_aux(self.device), self.lock:
+        with on_search(self.device), self.lock:
             v = to_host(self._vecs[: self._n].contiguous())[0]
             self._persist.snapshot(self.dim, self._ids, self._meta, v)
 
@@ -277,19 +301,20 @@ class VectorStore:
             r = self._row.get(key)
             if r is None:
                 return None
-            with on_aux(self.device):
+            with on_search(self.device):
                 return to_host(self._vecs[r].float())[0].tolist()
 
     # ------------------------------------------------------------------ search
     def topk_rows(self, q: torch.Tensor, k: int) -> Tuple[torch.Tensor, torch.Tensor]:
-        """Device top-k over the live rows (caller holds ``lock`` and is on the aux
-        stream).  q: normalised [Q, dim] in the store dtype.  Returns (scores f32 [Q,k],
+        """Device top-k over the live rows (caller holds ``lock``; any stream -- the read
+        is ordered after the store's last write).  q: normalised [Q, dim] in the store dtype.  Returns (scores f32 [Q,k],
         rows int32 [Q,k]); missing entries are (-inf, -1)."""
         n = self._n
         Qn = q.shape[0]
         if n == 0 or Qn == 0:
             return (torch.full((Qn, k), float("-inf"), device=self.device),
                     torch.full((Qn, k), -1, device=self.device, dtype=torch.int32))
+        self._order_read()
         X = self._vecs[:n]
         if self.device.type == "cuda" and self.kernel_dim and k <= KERNEL_MAX_K:
             return ops.knn_topk(X, q.contiguous(), k)
@@ -300,7 +325,7 @@ class VectorStore:
         {"id", "similarity", **metadata} sorted by decreasing cosine similarity."""
         if k < 1:
             raise ValueError("top-k must be >= 1")
-        with on_aux(self.device), self.lock:
+        with on_search(self.device), self.lock:
             q = self._normalize(queries)
             s, idx = self.topk_rows(q, k)
             s, idx = (t.tolist() for t in to_host(s, idx))
@@ -332,7 +357,8 @@ class VectorStore:
         flat = sorted(rows)
         if not flat:
             return {}
-        with on_aux(self.device):
+        with on_search(self.device):
+            self._order_read()
             vv = to_host(self._vecs[torch.tensor(flat, device=self.device)].float())[0].tolist()
         return dict(zip(flat, vv))
 

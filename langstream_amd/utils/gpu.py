@@ -17,27 +17,50 @@ import torch
 
 _lock = threading.Lock()
 _aux: Dict[int, "torch.cuda.Stream"] = {}
+_search: Dict[int, "torch.cuda.Stream"] = {}
 
 
-def aux_stream(device) -> Optional["torch.cuda.Stream"]:
+def _hp_stream(table, device) -> Optional["torch.cuda.Stream"]:
     device = torch.device(device)
     if device.type != "cuda":
         return None
     idx = device.index if device.index is not None else torch.cuda.current_device()
     with _lock:
-        s = _aux.get(idx)
+        s = table.get(idx)
         if s is None:
             lo, hi = torch.cuda.Stream.priority_range()
             s = torch.cuda.Stream(device=idx, priority=min(lo, hi))
             # everything enqueued on the device so far (weights, setup) happens-before
             s.wait_stream(torch.cuda.current_stream(idx))
-            _aux[idx] = s
+            table[idx] = s
     return s
+
+
+def aux_stream(device) -> Optional["torch.cuda.Stream"]:
+    """Embeddings and vector-store writes."""
+    return _hp_stream(_aux, device)
+
+
+def search_stream(device) -> Optional["torch.cuda.Stream"]:
+    """Vector-store searches: their own high-priority stream, so a query's kNN never
+    queues behind a large ingest embedding batch on the auxiliary stream (searches wait
+    only for the store's last write, VectorStore._write_ev)."""
+    return _hp_stream(_search, device)
 
 
 @contextlib.contextmanager
 def on_aux(device):
     s = aux_stream(device)
+    if s is None:
+        yield None
+        return
+    with torch.cuda.stream(s):
+        yield s
+
+
+@contextlib.contextmanager
+def on_search(device):
+    s = search_stream(device)
     if s is None:
         yield None
         return
