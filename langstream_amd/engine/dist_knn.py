@@ -86,7 +86,11 @@ class ShardedKnn:
             self.device = torch.device("cuda", torch.cuda.current_device())
         # separate groups so the service never interleaves with the caller's collectives
         self.meta = dist.new_group(backend="gloo")
-        if backend == "nccl":
+        # LS_KNN_DATA=gloo|nccl: which group carries a round's queries and partial results.
+        # They are KB-sized and latency-bound: on host (gloo) they never queue behind the
+        # LLM's decode graphs on a shared hardware queue; measured in profiles/.
+        data_backend = os.environ.get("LS_KNN_DATA", "gloo") if backend == "nccl" else "gloo"
+        if data_backend == "nccl":
             # high-priority RCCL streams: a round's collectives must not queue behind the
             # LLM engine's decode graphs on a shared hardware queue
             opts = dist.ProcessGroupNCCL.Options()
@@ -94,7 +98,7 @@ class ShardedKnn:
             self.data = dist.new_group(backend="nccl", pg_options=opts)
         else:
             self.data = dist.new_group(backend="gloo")
-        self.data_dev = self.device if backend == "nccl" else torch.device("cpu")
+        self.data_dev = self.device if data_backend == "nccl" else torch.device("cpu")
         self.tick_s = tick_s
         self.max_idle_s = max(tick_s, 0.004)
         self.max_q = max_queries_per_round
@@ -107,7 +111,7 @@ class ShardedKnn:
         # LS_KNN_PROFILE=1: synchronise after each phase of a round's search (diagnosis only)
         self._prof = os.environ.get("LS_KNN_PROFILE") == "1" and self.device.type == "cuda"
         if self._prof:
-            self.stats.update(gather_s=0.0, topk_s=0.0, a2a_s=0.0)
+            self.stats.update(upload_s=0.0, gather_s=0.0, topk_s=0.0, a2a_s=0.0)
         self._thread = threading.Thread(target=self._loop, name="sharded-knn", daemon=True)
         self._thread.start()
 
@@ -184,12 +188,11 @@ class ShardedKnn:
         try:
             if self.device.type == "cuda":
                 torch.cuda.set_device(self.device)
-                # Every device op of a round -- the H2D query copy, the RCCL all-gather and
-                # all-to-all (which order themselves after the CURRENT stream), the kNN
-                # kernel and the D2H copies -- runs on the one search stream, so they are
-                # ordered with each other and queue neither behind the LLM engine's steps
-                # nor behind ingest embedding batches (the store orders each search after
-                # its last write).
+                # Every device op of a round -- the H2D query copy, the kNN kernel and the
+                # D2H copies (plus the RCCL collectives under LS_KNN_DATA=nccl, which order
+                # themselves after the CURRENT stream) -- runs on the one high-priority search
+                # stream: they queue neither behind the LLM engine's steps nor behind ingest
+                # embedding batches, and the store's writes share the stream.
                 with on_search(self.device):
                     self._serve()
             else:
@@ -292,13 +295,18 @@ class ShardedKnn:
                 if mine:
                     torch.cat([r.q for r in mine], out=qloc[: counts[me]])
                 qloc = qloc.to(self.data_dev, non_blocking=pin)   # pinned: async, no staging copy
+                t_s = self._phase("upload_s", t_s)
                 qall = torch.empty(W * qmax, dim, dtype=torch.float32, device=self.data_dev)
                 dist.all_gather_into_tensor(qall, qloc, group=self.data)
                 t_s = self._phase("gather_s", t_s)
                 store = stores.get(coll)
                 if store is not None and store.dim == dim and len(store):
-                    s, idx = store.topk_rows(qall.to(store.device, store.dtype), kmax)
-                    s, idx = s.to(self.data_dev), idx.to(self.data_dev)
+                    if store.device.type == "cuda" and self.data_dev.type == "cpu":
+                        s, idx = to_host(*store.topk_rows(qall.pin_memory().to(
+                            store.device, non_blocking=True).to(store.dtype), kmax))
+                    else:
+                        s, idx = store.topk_rows(qall.to(store.device, store.dtype), kmax)
+                        s, idx = s.to(self.data_dev), idx.to(self.data_dev)
                 else:
                     s = torch.full((W * qmax, kmax), float("-inf"), device=self.data_dev)
                     idx = torch.full((W * qmax, kmax), -1, dtype=torch.int32, device=self.data_dev)
