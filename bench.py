@@ -287,6 +287,9 @@ class Site:
 
         class H(http.server.BaseHTTPRequestHandler):
             protocol_version = "HTTP/1.1"
+            # headers and body leave in separate writes: with Nagle on, the body waits for
+            # the client's delayed ACK of the headers (~40 ms per page on loopback)
+            disable_nagle_algorithm = True
 
             def log_message(self, *a):
                 pass
