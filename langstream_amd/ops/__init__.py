@@ -226,6 +226,29 @@ def paged_decode_attention(q, k_cache, v_cache, block_tables, ctx_lens, scale, o
     return r
 
 
+def paged_decode_attention_rope(qkv, pos, cos_sin, slots, k_cache, v_cache, block_tables, ctx_lens, scale,
+                                Hq: int, out=None, nsplit: int = 1, blocks_per_split: int = 1 << 30,
+                                workspace=None):
+    """Decode-only step with RoPE + the KV-cache write fused into attention.  qkv:
+    [B, (Hq + 2 Hkv) D] un-rotated projection rows (left unmodified); the new token of
+    each row (ctx_lens count it) is written to the cache at ``slots`` and attended from
+    registers.  Returns [B, Hq*D]; numerically rope_and_cache + paged_decode_attention."""
+    B = ctx_lens.shape[0]
+    D = k_cache.shape[3]
+    Hkv = k_cache.shape[1]
+    if _gpu(qkv):
+        out = torch.empty(B, Hq * D, dtype=qkv.dtype, device=qkv.device) if out is None else out
+        if nsplit > 1:
+            assert workspace is not None and workspace.numel() >= B * Hq * nsplit * (D + 2)
+        ws = workspace if workspace is not None else out.new_empty(0, dtype=torch.float32)
+        hip().paged_decode_attention_rope(out, qkv, pos, cos_sin, slots, k_cache, v_cache, block_tables, ctx_lens,
+                                          scale, nsplit, min(blocks_per_split, block_tables.shape[1]), ws)
+        return out
+    work = qkv.clone()
+    ref.rope_and_cache(work, pos, cos_sin, slots, k_cache, v_cache, Hq, Hkv, True)
+    return paged_decode_attention(work[:, : Hq * D], k_cache, v_cache, block_tables, ctx_lens, scale, out=out)
+
+
 def prefill_tiles(q_lens: Sequence[int], G: int, prefix_lens: Sequence[int] | None = None) -> torch.Tensor:
     """Work list for the prefill kernel: (seq, first row), rows = token*G + g, heaviest first."""
     tiles = []

@@ -61,14 +61,34 @@ __device__ __forceinline__ int split_blocks(int nblk, int nsplit, int min_bps) {
   return max(min_bps, (nblk + nsplit - 1) / nsplit);
 }
 
-template <int D, int WPP, bool PIPE>
+// Fused RoPE + KV write (ROPE = true, decode-only steps): q holds the UN-rotated QKV
+// projection rows [B, (Hq + 2 Hkv) D].  Every wave rotates its Q^T fragments in
+// registers (a lane's dims 32ks + 8h + j, ks < KS/2, pair with the +D/2 dims of ks + KS/2
+// in the same lane).  The step's new token (position pos[b] = ctx - 1) is NOT read back
+// from the cache: waves attend over the ctx - 1 cached keys, and the owner wave (wave 0
+// of split 0) rotates the new key, writes K and V^T into the paged cache for later steps
+// and seeds its softmax state with the new token itself (m = s_new, l = 1, O = v_new).
+// This removes the separate rope_cache launch (~11 us per layer at B = 256 in the RAG
+// bench, profiles/rag_bench_kernel_stats_r2m.csv) from every decode step.
+struct RopeArgs {
+  const float* cos_sin;    // [max_pos, D]: cos in [0, D/2), sin in [D/2, D)
+  const int32_t* pos;      // [B]
+  int max_pos;
+  const int64_t* slots;    // [B] cache slot of the new token (-1: do not cache)
+  int64_t nslots;
+  bf16* kc;                // writable views of the caches
+  bf16* vc;
+};
+
+template <int D, int WPP, bool PIPE, bool ROPE>
 __global__ void __launch_bounds__(64 * WPP) __attribute__((amdgpu_waves_per_eu(2, 2))) decode_attn_kernel(
     bf16* __restrict__ out, const bf16* __restrict__ q, int64_t q_stride, const bf16* __restrict__ kc,
     const bf16* __restrict__ vc, const int32_t* __restrict__ block_tables, int max_blocks,
     const int32_t* __restrict__ ctx_lens, int Hkv, int G, int NB, float scale_log2, int min_bps,
-    float* __restrict__ part_o, float* __restrict__ part_ml) {
+    float* __restrict__ part_o, float* __restrict__ part_ml, RopeArgs ra) {
   constexpr int KS = D / 32;  // k-steps over the head dim
   constexpr int DT = D / 16;  // 16-wide output tiles over the head dim
+  constexpr int HALF = D / 2;
 
   const int pair = blockIdx.x;
   const int b = pair / Hkv, kvh = pair - b * Hkv;
@@ -76,7 +96,10 @@ __global__ void __launch_bounds__(64 * WPP) __attribute__((amdgpu_waves_per_eu(2
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int i16 = lane & 15, h = lane >> 4;
 
-  const int ctx = ctx_lens[b];
+  const int ctx_all = ctx_lens[b];
+  const int p_new = ROPE ? min(max(ra.pos[b], 0), ra.max_pos - 1) : 0;
+  // keys read from the cache: with ROPE the new token (the last one) comes from registers
+  const int ctx = ROPE ? max(ctx_all - 1, 0) : ctx_all;
   const int nblk = min((ctx + BS - 1) / BS, max_blocks);
   const int bps = split_blocks(nblk, nsplit, min_bps);
   const int bstart = split * bps;
@@ -152,6 +175,78 @@ __global__ void __launch_bounds__(64 * WPP) __attribute__((amdgpu_waves_per_eu(2
     issue_k(bstart + wid, kf);
     issue_v(bstart + wid, vf);
   }
+  // RoPE after the first block's K/V loads are issued: its loads and math hide
+  // behind that fetch, which the first MFMA waits for anyway
+  if constexpr (ROPE) {
+    // cos / sin of this lane's low-half dims c = 32ks + 8h + j (ks < KS/2)
+    const float* cs = ra.cos_sin + (int64_t)p_new * D;
+    float co[KS / 2][8], si[KS / 2][8];
+#pragma unroll
+    for (int ks = 0; ks < KS / 2; ++ks) {
+      const int c = 32 * ks + 8 * h;
+      *reinterpret_cast<float4*>(co[ks]) = *reinterpret_cast<const float4*>(cs + c);
+      *reinterpret_cast<float4*>(co[ks] + 4) = *reinterpret_cast<const float4*>(cs + c + 4);
+      *reinterpret_cast<float4*>(si[ks]) = *reinterpret_cast<const float4*>(cs + HALF + c);
+      *reinterpret_cast<float4*>(si[ks] + 4) = *reinterpret_cast<const float4*>(cs + HALF + c + 4);
+    }
+    auto rotate = [&](bf16x8 (&f)[KS]) {
+#pragma unroll
+      for (int ks = 0; ks < KS / 2; ++ks)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float x1 = (float)f[ks][j], x2 = (float)f[ks + KS / 2][j];
+          f[ks][j] = (bf16)(x1 * co[ks][j] - x2 * si[ks][j]);
+          f[ks + KS / 2][j] = (bf16)(x2 * co[ks][j] + x1 * si[ks][j]);
+        }
+    };
+    rotate(qf);
+    if (split == 0 && wid == 0 && ctx_all >= 1) {
+      // the new token: rotated key (every lane group h holds dims 32ks + 8h .. +7)
+      const bf16* kp = q + (int64_t)b * q_stride + (int64_t)(Hkv * G + kvh) * D + 8 * h;
+      const bf16* vp = q + (int64_t)b * q_stride + (int64_t)(Hkv * G + Hkv + kvh) * D;
+      bf16x8 kn[KS];
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) kn[ks] = __builtin_bit_cast(bf16x8, ld16(kp + 32 * ks));
+      rotate(kn);
+      // O^T layout: lane holds O[qrow][16dt + 4h + r]; the new token's V for those dims
+      bf16x4 vn[DT];
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) vn[dt] = *reinterpret_cast<const bf16x4*>(vp + 16 * dt + 4 * h);
+      float dot = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) dot += (float)qf[ks][j] * (float)kn[ks][j];
+      dot += __shfl_xor(dot, 16, 64);
+      dot += __shfl_xor(dot, 32, 64);
+      // first element of the online softmax: m = s_new, l = 1, O = v_new
+      m = dot * scale_log2;
+      l = 1.f;
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[dt][r] = (float)vn[dt][r];
+      const int64_t sl = ra.slots[b];
+      if (sl >= 0 && sl < ra.nslots) {
+        const int64_t blk = sl / BS, off = sl - blk * BS;
+        if (i16 == 0) {
+          bf16* kd = ra.kc + ((blk * Hkv + kvh) * BS + off) * D + 8 * h;
+#pragma unroll
+          for (int ks = 0; ks < KS; ++ks) st16(kd + 32 * ks, __builtin_bit_cast(uint4, kn[ks]));
+        }
+        if (i16 < DT) {
+          // V^T: lane (i16, h) stores dims 16 i16 + 4h + r (each a 2-B store at stride BS)
+          bf16* vd = ra.vc + ((blk * Hkv + kvh) * (int64_t)D) * BS + off;
+          bf16x4 vv = vn[0];
+#pragma unroll
+          for (int dt = 1; dt < DT; ++dt) if (i16 == dt) vv = vn[dt];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) vd[(int64_t)(16 * i16 + 4 * h + r) * BS] = vv[r];
+        }
+      }
+    }
+  }
+
   for (int bi = bstart + wid; bi < bend; bi += WPP) {
     const bool more = bi + WPP < bend;
     if (!PIPE) {
@@ -309,12 +404,13 @@ template <int D>
 __global__ void __launch_bounds__(256) decode_merge_kernel(bf16* __restrict__ out, const float* __restrict__ part_o,
                                                            const float* __restrict__ part_ml, int nsplit_grid, int nrows,
                                                            const int32_t* __restrict__ ctx_lens, int Hq, int min_bps,
-                                                           int max_blocks) {
+                                                           int max_blocks, int ctx_adj) {
   // one wave per (b, head) row; lanes over d
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= nrows) return;
-  const int nblk = min((ctx_lens[row / Hq] + BS - 1) / BS, max_blocks);
+  // ctx_adj = 1 under ROPE: the split kernel covered the ctx - 1 cached keys
+  const int nblk = min((max(ctx_lens[row / Hq] - ctx_adj, 0) + BS - 1) / BS, max_blocks);
   const int bps = split_blocks(nblk, nsplit_grid, min_bps);
   const int nsplit = max(1, min(nsplit_grid, (nblk + bps - 1) / bps));
   const float* ml = part_ml + (int64_t)row * nsplit_grid * 2;
@@ -342,9 +438,10 @@ int64_t decode_nsplit(int64_t B, int64_t Hkv, int64_t nsplit_max) {
 // nsplit: the MAXIMUM split count (the workspace is sized for it); a launch uses
 // decode_nsplit(B, Hkv, nsplit).  min_bps: the fewest KV blocks one split covers.
 // workspace: f32 tensor with >= B*Hq*S*(D+2) elements when the launch splits (S > 1).
-void paged_decode_attention(at::Tensor out, at::Tensor q, at::Tensor k_cache, at::Tensor v_cache,
-                            at::Tensor block_tables, at::Tensor ctx_lens, double scale, int64_t nsplit,
-                            int64_t min_bps, at::Tensor workspace) {
+static void decode_attention_launch(at::Tensor& out, const at::Tensor& q, const at::Tensor& k_cache,
+                                    const at::Tensor& v_cache, const at::Tensor& block_tables,
+                                    const at::Tensor& ctx_lens, double scale, int64_t nsplit, int64_t min_bps,
+                                    const at::Tensor& workspace, const RopeArgs* ra) {
   TORCH_CHECK(q.is_cuda() && q.scalar_type() == at::kBFloat16 && out.scalar_type() == at::kBFloat16);
   TORCH_CHECK(out.is_contiguous() && q.stride(-1) == 1);
   TORCH_CHECK(k_cache.dim() == 4 && v_cache.dim() == 4);
@@ -378,14 +475,18 @@ void paged_decode_attention(at::Tensor out, at::Tensor q, at::Tensor k_cache, at
   // multiple of 4.  Smaller batches keep 4 waves per pair (and split long contexts).
   static const int env_wpp = getenv("LS_ATTN_WPP") ? atoi(getenv("LS_ATTN_WPP")) : 0;
   static const bool pipe = getenv("LS_ATTN_PIPE") ? atoi(getenv("LS_ATTN_PIPE")) != 0 : true;
+  const bool rope = ra != nullptr;
+  const RopeArgs rargs = rope ? *ra : RopeArgs{};
   const int wpp = env_wpp == 1 || env_wpp == 4 ? env_wpp : ((int64_t)B * Hkv >= WAVE_SLOTS && ns == 1 ? 1 : 4);
   dim3 grid(B * Hkv, ns);
   const float sl2 = (float)scale * LOG2E;
-#define LAUNCH_P(DD, W, P)                                                                                    \
-  decode_attn_kernel<DD, W, P><<<grid, 64 * W, 0, stream>>>(                                                  \
+#define LAUNCH_R(DD, W, P, R)                                                                                 \
+  decode_attn_kernel<DD, W, P, R><<<grid, 64 * W, 0, stream>>>(                                               \
       (bf16*)out.data_ptr(), (const bf16*)q.data_ptr(), q_stride, (const bf16*)k_cache.data_ptr(),            \
       (const bf16*)v_cache.data_ptr(), block_tables.data_ptr<int32_t>(), (int)block_tables.size(1),          \
-      ctx_lens.data_ptr<int32_t>(), Hkv, G, (int)k_cache.size(0), sl2, (int)min_bps, po, pml)
+      ctx_lens.data_ptr<int32_t>(), Hkv, G, (int)k_cache.size(0), sl2, (int)min_bps, po, pml, rargs)
+#define LAUNCH_P(DD, W, P) \
+  if (rope) LAUNCH_R(DD, W, P, true); else LAUNCH_R(DD, W, P, false)
 #define LAUNCH_K(DD, W) \
   if (pipe) LAUNCH_P(DD, W, true); else LAUNCH_P(DD, W, false)
 #define LAUNCH(DD)                                                                                            \
@@ -393,11 +494,43 @@ void paged_decode_attention(at::Tensor out, at::Tensor q, at::Tensor k_cache, at
   if (ns > 1)                                                                                                 \
     decode_merge_kernel<DD><<<(B * Hq + 3) / 4, 256, 0, stream>>>((bf16*)out.data_ptr(), po, pml, (int)ns,    \
                                                                   B * Hq, ctx_lens.data_ptr<int32_t>(), Hq,    \
-                                                                  (int)min_bps, (int)block_tables.size(1))
+                                                                  (int)min_bps, (int)block_tables.size(1), rope ? 1 : 0)
   if (D == 128) { LAUNCH(128); }
   else if (D == 64) { LAUNCH(64); }
   else TORCH_CHECK(false, "unsupported head dim ", D);
+  (void)rope;
 #undef LAUNCH_K
 #undef LAUNCH_P
+#undef LAUNCH_R
 #undef LAUNCH
+}
+
+void paged_decode_attention(at::Tensor out, at::Tensor q, at::Tensor k_cache, at::Tensor v_cache,
+                            at::Tensor block_tables, at::Tensor ctx_lens, double scale, int64_t nsplit,
+                            int64_t min_bps, at::Tensor workspace) {
+  decode_attention_launch(out, q, k_cache, v_cache, block_tables, ctx_lens, scale, nsplit, min_bps, workspace,
+                          nullptr);
+}
+
+// Decode-only step with RoPE and the KV-cache write fused in (see RopeArgs above).
+// qkv: [B, (Hq + 2 Hkv) D] un-rotated projection rows (not modified); ctx_lens count the
+// new token; pos [B] int32 its position; slots [B] int64 its cache slot (-1: not cached).
+void paged_decode_attention_rope(at::Tensor out, at::Tensor qkv, at::Tensor pos, at::Tensor cos_sin,
+                                 at::Tensor slots, at::Tensor k_cache, at::Tensor v_cache, at::Tensor block_tables,
+                                 at::Tensor ctx_lens, double scale, int64_t nsplit, int64_t min_bps,
+                                 at::Tensor workspace) {
+  TORCH_CHECK(qkv.is_cuda() && qkv.dim() == 2 && qkv.stride(1) == 1, "qkv must be [B, (Hq + 2 Hkv) D]");
+  const int64_t Hkv = k_cache.size(1), D = k_cache.size(3), B = ctx_lens.numel();
+  TORCH_CHECK(qkv.size(0) == B && out.numel() % (B * D) == 0);
+  const int64_t Hq = out.numel() / (B * D);
+  TORCH_CHECK(qkv.size(1) == (Hq + 2 * Hkv) * D, "qkv width must be (Hq + 2 Hkv) * D");
+  TORCH_CHECK(pos.scalar_type() == at::kInt && pos.is_contiguous() && pos.numel() >= B);
+  TORCH_CHECK(slots.scalar_type() == at::kLong && slots.is_contiguous() && slots.numel() >= B);
+  TORCH_CHECK(cos_sin.scalar_type() == at::kFloat && cos_sin.is_contiguous() && cos_sin.dim() == 2 &&
+              cos_sin.size(1) == D && cos_sin.size(0) >= 1);
+  TORCH_CHECK(k_cache.is_contiguous() && v_cache.is_contiguous());
+  RopeArgs ra{cos_sin.data_ptr<float>(), pos.data_ptr<int32_t>(), (int)cos_sin.size(0), slots.data_ptr<int64_t>(),
+              k_cache.size(0) * BS, (bf16*)k_cache.data_ptr(), (bf16*)v_cache.data_ptr()};
+  decode_attention_launch(out, qkv, k_cache, v_cache, block_tables, ctx_lens, scale, nsplit, min_bps, workspace,
+                          &ra);
 }

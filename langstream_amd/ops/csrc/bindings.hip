@@ -14,6 +14,10 @@ void rope_and_cache(at::Tensor qkv, at::Tensor pos, at::Tensor cos_sin, at::Tens
 void paged_decode_attention(at::Tensor out, at::Tensor q, at::Tensor k_cache, at::Tensor v_cache,
                             at::Tensor block_tables, at::Tensor ctx_lens, double scale, int64_t nsplit,
                             int64_t blocks_per_split, at::Tensor workspace);
+void paged_decode_attention_rope(at::Tensor out, at::Tensor qkv, at::Tensor pos, at::Tensor cos_sin,
+                                 at::Tensor slots, at::Tensor k_cache, at::Tensor v_cache, at::Tensor block_tables,
+                                 at::Tensor ctx_lens, double scale, int64_t nsplit, int64_t min_bps,
+                                 at::Tensor workspace);
 void paged_prefill_attention(at::Tensor out, at::Tensor q, at::Tensor k_cache, at::Tensor v_cache,
                              at::Tensor block_tables, at::Tensor q_start, at::Tensor q_len, at::Tensor ctx_len,
                              at::Tensor tiles, int64_t Hq, double scale);
@@ -71,6 +75,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bias_gelu", &bias_gelu);
   m.def("rope_and_cache", &rope_and_cache);
   m.def("paged_decode_attention", &paged_decode_attention);
+  m.def("paged_decode_attention_rope", &paged_decode_attention_rope);
   m.def("paged_prefill_attention", &paged_prefill_attention);
   m.def("varlen_encoder_attention", &varlen_encoder_attention);
   m.def("sample_tokens", &sample_tokens);

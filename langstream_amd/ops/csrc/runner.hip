@@ -56,6 +56,10 @@ void rope_and_cache(at::Tensor qkv, at::Tensor pos, at::Tensor cos_sin, at::Tens
 void paged_decode_attention(at::Tensor out, at::Tensor q, at::Tensor k_cache, at::Tensor v_cache,
                             at::Tensor block_tables, at::Tensor ctx_lens, double scale, int64_t nsplit,
                             int64_t blocks_per_split, at::Tensor workspace);
+void paged_decode_attention_rope(at::Tensor out, at::Tensor qkv, at::Tensor pos, at::Tensor cos_sin,
+                                 at::Tensor slots, at::Tensor k_cache, at::Tensor v_cache, at::Tensor block_tables,
+                                 at::Tensor ctx_lens, double scale, int64_t nsplit, int64_t min_bps,
+                                 at::Tensor workspace);
 void paged_prefill_attention(at::Tensor out, at::Tensor q, at::Tensor k_cache, at::Tensor v_cache,
                              at::Tensor block_tables, at::Tensor q_start, at::Tensor q_len, at::Tensor ctx_len,
                              at::Tensor tiles, int64_t Hq, double scale);
@@ -229,12 +233,18 @@ class LlamaRunner {
       } else {
         qkv = at::linear(x, qkv_w_[l]);
       }
-      rope_and_cache(qkv, pos, cos_sin_, slots, kc_[l], vc_[l], hq_, hkv_, true);
-      at::Tensor q = qkv.narrow(1, 0, hq_ * d_);
       at::Tensor attn = at::empty({T, hq_ * d_}, qkv.options());
-      if (num_decode > 0)
-        paged_decode_attention(attn.narrow(0, 0, num_decode), q.narrow(0, 0, num_decode), kc_[l], vc_[l], d_bt,
-                               d_ctx, scale_, nsplit, bps, ws);
+      at::Tensor q = qkv.narrow(1, 0, hq_ * d_);
+      if (num_prefill == 0 && num_decode == T && rope_fused()) {
+        // decode-only step: RoPE + K/V cache write inside the attention kernel
+        paged_decode_attention_rope(attn, qkv, pos, cos_sin_, slots, kc_[l], vc_[l], d_bt, d_ctx, scale_, nsplit,
+                                    bps, ws);
+      } else {
+        rope_and_cache(qkv, pos, cos_sin_, slots, kc_[l], vc_[l], hq_, hkv_, true);
+        if (num_decode > 0)
+          paged_decode_attention(attn.narrow(0, 0, num_decode), q.narrow(0, 0, num_decode), kc_[l], vc_[l], d_bt,
+                                 d_ctx, scale_, nsplit, bps, ws);
+      }
       if (num_prefill > 0)
         paged_prefill_attention(attn, q, kc_[l], vc_[l], p_bt, q_start, q_len, ctx_len, tiles, hq_, scale_);
       at::Tensor o;
@@ -348,6 +358,15 @@ class LlamaRunner {
     static const bool on = [] {
       const char* v = std::getenv("LS_GEMV");
       return !(v && std::string(v) == "0");
+    }();
+    return on;
+  }
+
+  // LS_ATTN_ROPE=0: separate rope_cache launch before decode attention (A/B switch)
+  static bool rope_fused() {
+    static const bool on = [] {
+      const char* e = getenv("LS_ATTN_ROPE");
+      return e == nullptr || e[0] != '0';
     }();
     return on;
   }

@@ -162,6 +162,49 @@ def test_paged_decode_attention_wave_per_pair():
     _close(got, exp.reshape(B, Hq * D), 0.03, 0.03)
 
 
+def _rope_decode_case(ctx, Hkv, G, D, seed):
+    Hq = Hkv * G
+    B = len(ctx)
+    kc, vc, bt = _random_paged(B, ctx, Hkv, D, DEV, seed=seed)
+    qkv = torch.randn(B, (Hq + 2 * Hkv) * D, device=DEV, dtype=torch.bfloat16)
+    cl = torch.tensor(ctx, dtype=torch.int32, device=DEV)
+    pos = (cl - 1).clamp(min=0)
+    btc = bt.cpu()
+    slots = torch.tensor([int(btc[b, (c - 1) // ops.KV_BLOCK]) * ops.KV_BLOCK + (c - 1) % ops.KV_BLOCK if c > 0 else -1
+                          for b, c in enumerate(ctx)], dtype=torch.int64, device=DEV)
+    cs = ref.rope_cos_sin(4096, D, 500000.0, device=DEV)
+    return Hq, kc, vc, bt, qkv, cl, pos, slots, cs
+
+
+@pytest.mark.parametrize("ctx,Hkv,G,nsplit,min_bps", [
+    ([1, 2, 63, 64, 65, 66, 129, 300, 777], 2, 4, 1, 4),
+    ([1, 2, 63, 64, 65, 66, 129, 300, 777], 2, 4, 3, 1),
+    ([1, 65, 129, 777], 2, 8, 16, 1),
+    ("ragged256", 8, 4, 1, 4),
+])
+def test_paged_decode_attention_rope(ctx, Hkv, G, nsplit, min_bps):
+    """Fused RoPE + KV write + decode attention == rope_and_cache, then attention over
+    the cache (fp32 reference); the new token's K / V^T land in the cache."""
+    D = 128
+    if ctx == "ragged256":   # B*Hkv >= 2048: one wave per (seq, kv-head)
+        ctx = torch.randint(1, 300, (256,), generator=torch.Generator().manual_seed(11)).tolist()
+    Hq, kc, vc, bt, qkv, cl, pos, slots, cs = _rope_decode_case(ctx, Hkv, G, D, seed=G + nsplit)
+    B = len(ctx)
+    kr, vr = kc.cpu().clone(), vc.cpu().clone()
+    qkv_c = qkv.cpu().clone()
+    ref.rope_and_cache(qkv_c, pos.cpu(), cs.cpu(), slots.cpu(), kr, vr, Hq, Hkv)
+    exp = ref.paged_decode_attention(qkv_c[:, : Hq * D].reshape(B, Hq, D), kr, vr, bt.cpu(), cl.cpu(),
+                                     1 / math.sqrt(D))
+    qkv_before = qkv.clone()
+    ws = torch.empty(B * Hq * nsplit * (D + 2), device=DEV, dtype=torch.float32)
+    got = ops.paged_decode_attention_rope(qkv, pos, cs, slots, kc, vc, bt, cl, 1 / math.sqrt(D), Hq,
+                                          nsplit=nsplit, blocks_per_split=min_bps, workspace=ws)
+    _close(got, exp.reshape(B, Hq * D), 0.03, 0.03, "attention")
+    _close(kc, kr, 0.03, 0.01, "k cache")
+    _close(vc, vr, 0.0, 0.0, "v cache")
+    assert torch.equal(qkv, qkv_before), "the fused kernel must not modify the projection rows"
+
+
 @pytest.mark.parametrize("G", [1, 4, 8])
 def test_paged_prefill_attention(G):
     Hkv, D = 2, 128
