@@ -18,6 +18,7 @@ services (``ChatCompletionsStep.java:132-155`` ->
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field
 from typing import Optional
 
@@ -127,6 +128,21 @@ class AttnMeta:
     tiles: Optional[torch.Tensor] = None           # [ntiles, 2] int32
 
 
+_PGEMM = {"0": 0, "all": 2}.get(os.environ.get("LS_PGEMM", "1"), 1)
+_PGEMM_MIN_T = int(os.environ.get("LS_PGEMM_MIN_T", "1024"))
+
+
+def _pgemm(x: torch.Tensor, w: torch.Tensor, silu: bool) -> bool:
+    """Prefill-sized rows on the GPU go to the 256x256-tile MFMA GEMM (same rule as
+    runner.hip's pgemm())."""
+    return (_PGEMM > (0 if silu else 1) and x.is_cuda and x.shape[0] >= _PGEMM_MIN_T and x.dtype == torch.bfloat16
+            and x.stride(-1) == 1 and ops.hip().gemm_prefill_supported(w, silu))
+
+
+def _linear(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    return ops.gemm_prefill(x, w) if _pgemm(x, w, False) else F.linear(x, w)
+
+
 def tp_kv_heads(num_kv_heads: int, world: int) -> int:
     """KV heads per TP rank.  With more ranks than KV heads every KV head is REPLICATED on
     world / num_kv_heads consecutive ranks (each rank keeps the one KV head its query
@@ -225,7 +241,7 @@ class LlamaModel:
         D = cfg.head_dim
         for li, layer in enumerate(self.layers):
             kc, vc = kv_caches[li]
-            qkv = F.linear(x, layer.qkv_w)
+            qkv = _linear(x, layer.qkv_w)
             ops.rope_and_cache(qkv, meta.positions, self.cos_sin, meta.slots, kc, vc, self.hq, self.hkv)
             q = qkv[:, : self.hq * D]
             nd = meta.num_decode
@@ -241,12 +257,14 @@ class LlamaModel:
                                                blocks_per_split=meta.blocks_per_split, workspace=meta.workspace)
                 ops.paged_prefill_attention(q, kc, vc, meta.p_block_tables, meta.q_start, meta.q_len, meta.ctx_len,
                                             meta.tiles, self.hq, self.scale, out=attn)
-            o = F.linear(attn, layer.o_w)
+            o = _linear(attn, layer.o_w)
             self.tp.all_reduce(o)
             ops.fused_add_rmsnorm(o, residual, layer.post_norm, eps)
-            gu = F.linear(o, layer.gate_up_w)
-            a = ops.silu_and_mul(gu)
-            d = F.linear(a, layer.down_w)
+            if _pgemm(o, layer.gate_up_w, True):
+                a = ops.gemm_prefill(o, layer.gate_up_w, silu=True)
+            else:
+                a = ops.silu_and_mul(F.linear(o, layer.gate_up_w))
+            d = _linear(a, layer.down_w)
             self.tp.all_reduce(d)
             nxt = self.layers[li + 1].in_norm if li + 1 < len(self.layers) else self.final_norm
             ops.fused_add_rmsnorm(d, residual, nxt, eps)

@@ -153,6 +153,22 @@ def gemm_fused(x, w, bias=None, gelu=False, residual=None, ln_stats_in=None, ln_
     return r
 
 
+def gemm_prefill(x, w, silu=False, out=None):
+    """Prefill-sized MFMA GEMM (ops/csrc/gemm_prefill.hip, 256 x 256 tiles): x . w^T, or with
+    ``silu`` the Llama SwiGLU of the fused gate_up weight [2F, K]: silu(x.g^T) * (x.u^T)."""
+    if _gpu(x):
+        n = w.shape[0] // 2 if silu else w.shape[0]
+        out = torch.empty(x.shape[0], n, dtype=x.dtype, device=x.device) if out is None else out
+        hip().gemm_prefill(out, x, w, silu)
+        return out
+    y = x.float() @ w.float().t()
+    r = (ref.silu_and_mul(y) if silu else y).to(x.dtype)
+    if out is not None:
+        out.copy_(r)
+        return out
+    return r
+
+
 def gemm(x, w, bias=None, act=None, residual=None):
     """Hand-written MFMA linear: act in (None, "gelu", "swiglu"); swiglu takes the fused
     gate_up weight [2F, K] and returns silu(x.g^T) * (x.u^T)."""

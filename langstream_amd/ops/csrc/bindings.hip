@@ -63,6 +63,8 @@ void gemm_fused(at::Tensor out, at::Tensor x, at::Tensor w, c10::optional<at::Te
                 c10::optional<at::Tensor> res_b, double eps, c10::optional<at::Tensor> stats_out);
 void skinny_gemm_add_rmsnorm(at::Tensor out, at::Tensor x, at::Tensor w, at::Tensor residual, at::Tensor norm_w,
                              double eps);
+void gemm_prefill(at::Tensor out, at::Tensor x, at::Tensor w, bool silu);
+bool gemm_prefill_supported(const at::Tensor& w, bool silu);
 void bind_runners(pybind11::module_& m);
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -105,5 +107,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("res_g") = py::none(), py::arg("res_b") = py::none(), py::arg("eps") = 1e-12,
         py::arg("stats_out") = py::none());
   m.def("skinny_gemm_add_rmsnorm", &skinny_gemm_add_rmsnorm);
+  m.def("gemm_prefill", &gemm_prefill);
+  m.def("gemm_prefill_supported", &gemm_prefill_supported);
   bind_runners(m);
 }

@@ -1,0 +1,233 @@
+// Prefill-sized GEMM on MFMA for gfx950:  C[M, N] = X[M, K] . W[N, K]^T  (M in the
+// thousands: one chunked-prefill step of the LLM engine), optionally with the Llama
+// SwiGLU fused into the epilogue so the [T, 2F] gate_up product never reaches HBM.
+//
+// Why a second big-M kernel next to gemm_fused.hip: that one tiles 256 x 128 with one
+// 64 x 64 sub-tile per wave, which moves (64 + 64) x 32 x 2 B through LDS per 16 MFMAs.
+// Here the workgroup tile is 256 x 256 with one 128 x 64 sub-tile per wave (8 waves,
+// 2 per SIMD): 12 ds_read_b128 per 32 MFMA 16x16x32, i.e. per K step the CU reads
+// 96 KB of LDS (~384 cycles at 256 B/clk) under ~1030 cycles of MFMA per SIMD, so the
+// matrix cores, not the LDS array, set the pace (MI355X_MICROARCH LDS table).
+//   * both operands global -> LDS by global_load_lds_dwordx4 (no VGPR staging) into an
+//     S-deep ring of 32-deep K stages (32 KB each), S-1 stages in flight, one raw
+//     s_barrier per K step behind a counted vmcnt (same ring protocol as gemm_skinny.hip);
+//   * 64-B LDS rows with the source-side bank swizzle of common.h (conflict-free
+//     fragment reads);
+//   * grouped tile order on top of the XCD remap: the ~32 workgroups an XCD runs at once
+//     cover GROUP_M M-tiles x (32 / GROUP_M) N-tiles, so both the X and the W tiles they
+//     stream are shared through that XCD's L2 (a 1-D order would re-stream X from HBM
+//     once per N tile);
+//   * SILU epilogue: a tile's 256 W rows are 128 gate rows + the matching 128 up rows,
+//     laid out so every wave holds gate and up of the same output element in its own
+//     accumulators; out = silu(g) * u is stored as bf16 [M, F].
+#include <torch/extension.h>
+#include <ATen/hip/HIPContext.h>
+#include "common.h"
+
+namespace {
+
+constexpr int TM = 256, TN = 256, GBK = 32;
+constexpr int XB = TM * GBK * 2, WB = TN * GBK * 2, SB = XB + WB;  // 16 KB + 16 KB per stage
+
+enum { EPI_STORE = 0, EPI_SILU = 1 };
+
+// NWV = 8: 2 x 4 waves of 128 x 64 (2 waves per SIMD, 8 x 4 accumulators each);
+// NWV = 4: 2 x 2 waves of 128 x 128 (1 wave per SIMD, 8 x 8 accumulators in AGPRs), a
+// third less LDS read traffic per K step and no SIMD-sharing wave at the barrier.
+// (A register-staged ring -- global_load_dwordx4 + ds_write_b128 instead of LDS-DMA --
+// measured 10-15 % slower on every Llama shape: profiles/pgemm_bench_v3_rs.log.)
+template <int S, int EPI, int NWV>
+__global__ void __launch_bounds__(NWV * 64) gemm_prefill_kernel(const bf16* __restrict__ x, int64_t ldx,
+                                                                const bf16* __restrict__ w, int M, int K,
+                                                                bf16* __restrict__ out, int64_t ldo, int MT,
+                                                                int NTL, int F, int group_m) {
+  static_assert(S >= 3, "the ring keeps stage kt+1 readable while kt+2.. are in flight");
+  constexpr int PPW = 16 / NWV;           // 16-row X pieces (and W pieces) per wave per stage
+  constexpr int PER = 2 * PPW;            // LDS-DMA instructions per wave per stage
+  constexpr int WCOLS = 512 / NWV;        // columns per wave (64 / 128)
+  constexpr int JT = WCOLS / 16;          // 16-column MFMA tiles per wave
+  constexpr int NRD = 8 + JT;             // fragment reads per wave per K step
+  __shared__ __attribute__((aligned(1024))) char lds[S * SB];
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int logical = xcd_remap(blockIdx.x, gridDim.x);
+  const int per_group = group_m * NTL;
+  const int grp = logical / per_group, first = grp * group_m;
+  const int gsz = min(MT - first, group_m);
+  const int rem = logical - grp * per_group;
+  const int mt = first + rem % gsz, nt = rem / gsz;
+  const int m0 = mt * TM;
+  const int nk = K / GBK;
+
+  // LDS-DMA sources: wave w fills X pieces PPW*w.. and W pieces PPW*w.. (16 rows each)
+  const int prow = lane >> 2;
+  const int sck = ((lane & 3) ^ swz_g(lane >> 4)) * 8;
+  const bf16* xs[PPW];
+  const bf16* wsrc[PPW];
+#pragma unroll
+  for (int j = 0; j < PPW; ++j) {
+    const int row = 16 * (PPW * wid + j) + prow;
+    xs[j] = x + (int64_t)min(m0 + row, M - 1) * ldx + sck;   // rows >= M: any valid row, never stored
+    int wrow;
+    if (EPI == EPI_SILU) wrow = row < 128 ? nt * 128 + row : F + nt * 128 + (row - 128);
+    else wrow = nt * TN + row;
+    wsrc[j] = w + (int64_t)wrow * K + sck;
+  }
+  auto issue = [&](int kt, int slot) {
+    const int ko = kt * GBK;
+    char* base = lds + slot * SB;
+#pragma unroll
+    for (int j = 0; j < PPW; ++j) glds16(xs[j] + ko, base + (PPW * wid + j) * 1024);
+#pragma unroll
+    for (int j = 0; j < PPW; ++j) glds16(wsrc[j] + ko, base + XB + (PPW * wid + j) * 1024);
+  };
+
+  const int wm = wid / (NWV / 2), wn = wid % (NWV / 2);
+  const int fr = lane & 15, h = lane >> 4;
+  const int swz = 16 * (h ^ swz_g(fr >> 2));
+  // tile-local W row (= output column) of this lane's B fragment for column tile j.
+  // SILU: tiles [0, JT/2) are gate columns, [JT/2, JT) the matching up columns.
+  auto bcol = [&](int j) {
+    if (EPI == EPI_SILU)
+      return (j < JT / 2 ? (WCOLS / 2) * wn + 16 * j : 128 + (WCOLS / 2) * wn + 16 * (j - JT / 2)) + fr;
+    return WCOLS * wn + 16 * j + fr;
+  };
+  f32x4 acc[8][JT];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < JT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // Fragments are double-buffered in registers: step kt's MFMAs run on fragments read
+  // during step kt-1, while this step's ds_reads fetch stage kt+1 (left to itself hipcc
+  // reuses two fragment registers and exposes the LDS latency four times per K step).
+  auto load_frags = [&](int slot, bf16x8 (&a)[8], bf16x8 (&b)[JT]) {
+    const char* lx = lds + slot * SB;
+    const char* lw = lx + XB;
+#pragma unroll
+    for (int j = 0; j < JT; ++j) b[j] = __builtin_bit_cast(bf16x8, ld16(lw + bcol(j) * 64 + swz));
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a[i] = __builtin_bit_cast(bf16x8, ld16(lx + (128 * wm + 16 * i + fr) * 64 + swz));
+  };
+  auto mma = [&](const bf16x8 (&a)[8], const bf16x8 (&b)[JT]) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < JT; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+  };
+  int buf = 0;                            // ring slot of stage kt
+  // one K step: stage kt+1 visible to every wave -> refill the slot of stage kt-1 (its
+  // fragments were consumed by step kt-1's MFMAs, which waited for them) -> read stage
+  // kt+1's fragments into `nxt` -> MFMAs on `cur`.
+  auto step = [&](int kt, const bf16x8 (&ca)[8], const bf16x8 (&cb)[JT], bf16x8 (&na)[8], bf16x8 (&nb)[JT]) {
+    // stage kt's fragment reads (all but the NRD newest LDS ops) are complete before this
+    // wave joins the barrier after which another wave may refill their slot
+    asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(NRD < 15 ? NRD : 15) : "memory");  // counter max 15
+    wait_vmcnt<(S - 3) * PER>();          // this wave's DMA of stage kt+1 has landed
+    __builtin_amdgcn_s_barrier();         // ... and every other wave's
+    int rs = buf + S - 1;
+    if (rs >= S) rs -= S;
+    issue(min(kt + S - 1, nk - 1), rs);   // past the end: re-load the last stage into a dead slot
+    const int b1 = buf + 1 == S ? 0 : buf + 1;
+    load_frags(b1, na, nb);               // past the end: reads a dead slot, never used
+    mma(ca, cb);
+    constexpr int PERRD = 8 * JT / NRD;   // MFMAs between consecutive fragment reads
+#pragma unroll
+    for (int g = 0; g < NRD; ++g) {
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);       // 1 ds_read
+      __builtin_amdgcn_sched_group_barrier(0x008, PERRD, 0);   // PERRD MFMAs
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, 8 * JT - PERRD * NRD, 0);
+    buf = b1;
+  };
+
+#pragma unroll
+  for (int s = 0; s < S - 1; ++s) issue(min(s, nk - 1), s);
+  wait_vmcnt<(S - 2) * PER>();
+  __builtin_amdgcn_s_barrier();
+  bf16x8 a0[8], b0[JT], a1[8], b1[JT];
+  load_frags(0, a0, b0);
+  int kt = 0;
+  for (; kt + 1 < nk; kt += 2) {
+    step(kt, a0, b0, a1, b1);
+    step(kt + 1, a1, b1, a0, b0);
+  }
+  if (kt < nk) step(kt, a0, b0, a1, b1);
+  wait_vmcnt<0>();  // no LDS-DMA may outlive the workgroup
+
+  // acc[i][j][r] = C[128wm + 16i + 4h + r][bcol(j)] (tile-local)
+  const int rbase = m0 + 128 * wm + 4 * h;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = rbase + 16 * i + r;
+      if (m >= M) continue;
+      bf16* orow = out + (int64_t)m * ldo;
+      if (EPI == EPI_SILU) {
+#pragma unroll
+        for (int j = 0; j < JT / 2; ++j) {
+          const float g = acc[i][j][r], u = acc[i][j + JT / 2][r];
+          orow[nt * 128 + (WCOLS / 2) * wn + 16 * j + fr] = (bf16)(g / (1.f + __expf(-g)) * u);
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < JT; ++j) orow[nt * TN + WCOLS * wn + 16 * j + fr] = (bf16)acc[i][j][r];
+      }
+    }
+}
+
+int env_int(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return v ? atoi(v) : dflt;
+}
+
+template <int EPI>
+void launch(int ring, int nwv, dim3 grid, hipStream_t st, const at::Tensor& x, const at::Tensor& w, int M, int K,
+            at::Tensor& out, int MT, int NTL, int F, int gm) {
+#define L(SV, NW)                                                                                              \
+  gemm_prefill_kernel<SV, EPI, NW><<<grid, NW * 64, 0, st>>>((const bf16*)x.data_ptr(), x.stride(0),                  \
+                                                     (const bf16*)w.data_ptr(), M, K, (bf16*)out.data_ptr(),  \
+                                                     out.stride(0), MT, NTL, F, gm)
+  if (nwv == 4) {
+    if (ring == 3) L(3, 4);
+    else if (ring == 5) L(5, 4);
+    else L(4, 4);
+  } else {
+    if (ring == 3) L(3, 8);
+    else if (ring == 5) L(5, 8);
+    else L(4, 8);
+  }
+#undef L
+}
+
+}  // namespace
+
+// Shapes the kernel takes: K % 32 == 0 and N % 256 == 0 (silu: the fused [2F, K] gate_up
+// weight with F % 128 == 0).
+bool gemm_prefill_supported(const at::Tensor& w, bool silu) {
+  if (w.dim() != 2 || w.scalar_type() != at::kBFloat16 || !w.is_contiguous() || w.size(1) % GBK != 0) return false;
+  return silu ? (w.size(0) % 256 == 0) : (w.size(0) % TN == 0);
+}
+
+// silu == false: out[M, N] = x . w^T;  silu == true: out[M, F] = silu(x . w[:F]^T) * (x . w[F:]^T)
+void gemm_prefill(at::Tensor out, at::Tensor x, at::Tensor w, bool silu) {
+  const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16, "x must be bf16 on the GPU");
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && x.stride(0) % 8 == 0, "x must be [M, K] with unit column stride");
+  TORCH_CHECK(w.size(1) == K && gemm_prefill_supported(w, silu), "gemm_prefill: unsupported weight shape");
+  const int64_t NO = silu ? N / 2 : N;
+  TORCH_CHECK(out.scalar_type() == at::kBFloat16 && out.dim() == 2 && out.size(0) == M && out.size(1) == NO &&
+              out.stride(1) == 1, "out must be bf16 [M, ", NO, "]");
+  TORCH_CHECK(M < (1LL << 31) / TM);
+  if (M == 0) return;
+  const int MT = (int)((M + TM - 1) / TM), NTL = (int)(silu ? N / 2 / 128 : N / TN);
+  static const int ring = env_int("LS_PGEMM_RING", 4);
+  static const int gm_env = env_int("LS_PGEMM_GROUP", 8);
+  static const int nwv = env_int("LS_PGEMM_WAVES", 8) == 4 ? 4 : 8;
+  const int gm = std::max(1, std::min(gm_env, MT));
+  auto stream = at::hip::getCurrentHIPStream();
+  const dim3 grid((unsigned)(MT * NTL));
+  if (silu) launch<EPI_SILU>(ring, nwv, grid, stream, x, w, (int)M, (int)K, out, MT, NTL, (int)(N / 2), gm);
+  else launch<EPI_STORE>(ring, nwv, grid, stream, x, w, (int)M, (int)K, out, MT, NTL, 0, gm);
+}

@@ -101,6 +101,8 @@ void gemv_silu_norm(at::Tensor out, at::Tensor o, at::Tensor res, at::Tensor res
                     at::Tensor w);
 void skinny_gemm_add_rmsnorm(at::Tensor out, at::Tensor x, at::Tensor w, at::Tensor residual, at::Tensor norm_w,
                              double eps);
+void gemm_prefill(at::Tensor out, at::Tensor x, at::Tensor w, bool silu);
+bool gemm_prefill_supported(const at::Tensor& w, bool silu);
 
 #define HIP_OK(x)                                                                  \
   do {                                                                             \
@@ -230,6 +232,9 @@ class LlamaRunner {
       } else if (sk && T <= 32 && skinny_shape(qkv_w_[l])) {
         qkv = at::empty({T, qkv_w_[l].size(0)}, x.options());
         skinny_gemm(qkv, x, qkv_w_[l]);
+      } else if (pgemm(T, qkv_w_[l], false)) {
+        qkv = at::empty({T, qkv_w_[l].size(0)}, x.options());
+        gemm_prefill(qkv, x, qkv_w_[l], false);
       } else {
         qkv = at::linear(x, qkv_w_[l]);
       }
@@ -263,7 +268,12 @@ class LlamaRunner {
           fused_add_rmsnorm(o, residual, post_norm_[l], eps_);
         }
       } else {
-        o = at::linear(attn, o_w_[l]);
+        if (pgemm(T, o_w_[l], false)) {
+          o = at::empty_like(residual);
+          gemm_prefill(o, attn, o_w_[l], false);
+        } else {
+          o = at::linear(attn, o_w_[l]);
+        }
         all_reduce(o);
         fused_add_rmsnorm(o, residual, post_norm_[l], eps_);
       }
@@ -271,6 +281,10 @@ class LlamaRunner {
       if (gv && gemv_supported(gate_up_w_[l], true)) {
         a = at::empty({T, gate_up_w_[l].size(0) / 2}, o.options());
         gemv_silu(a, o, gate_up_w_[l]);
+      } else if (pgemm(T, gate_up_w_[l], true)) {
+        // prefill: SwiGLU in the GEMM epilogue, the [T, 2F] product never reaches HBM
+        a = at::empty({T, gate_up_w_[l].size(0) / 2}, o.options());
+        gemm_prefill(a, o, gate_up_w_[l], true);
       } else {
         at::Tensor gu = at::linear(o, gate_up_w_[l]);
         a = at::empty({T, gu.size(1) / 2}, gu.options());
@@ -293,7 +307,12 @@ class LlamaRunner {
           fused_add_rmsnorm(dn, residual, nxt, eps_);
         }
       } else {
-        dn = at::linear(a, down_w_[l]);
+        if (pgemm(T, down_w_[l], false)) {
+          dn = at::empty_like(residual);
+          gemm_prefill(dn, a, down_w_[l], false);
+        } else {
+          dn = at::linear(a, down_w_[l]);
+        }
         all_reduce(dn);
         fused_add_rmsnorm(dn, residual, nxt, eps_);
       }
@@ -377,6 +396,24 @@ class LlamaRunner {
       return e == nullptr || e[0] != '0';
     }();
     return on;
+  }
+  // Prefill-sized steps (T >= LS_PGEMM_MIN_T, default 1024) run the gate_up projection
+  // on the 256 x 256-tile hand-written GEMM (ops/csrc/gemm_prefill.hip) with SwiGLU in
+  // its epilogue (no [T, 2F] round trip, no silu_and_mul); qkv / o / down stay on
+  // hipBLASLt, which is faster on those plain shapes (profiles/pgemm_bench_*.log).
+  // LS_PGEMM=0: gate_up on hipBLASLt + silu_and_mul too; LS_PGEMM=all: all four here.
+  static bool pgemm(int64_t T, const at::Tensor& w, bool silu) {
+    static const int mode = [] {
+      const char* e = getenv("LS_PGEMM");
+      if (e == nullptr) return 1;
+      if (std::string(e) == "all") return 2;
+      return e[0] == '0' ? 0 : 1;
+    }();
+    static const int64_t min_t = [] {
+      const char* e = getenv("LS_PGEMM_MIN_T");
+      return e ? (int64_t)atoll(e) : (int64_t)1024;
+    }();
+    return mode > (silu ? 0 : 1) && T >= min_t && gemm_prefill_supported(w, silu);
   }
   static bool skinny_shape(const at::Tensor& w) { return w.size(0) % 128 == 0 && w.size(1) % 64 == 0; }
 

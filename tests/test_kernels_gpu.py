@@ -396,6 +396,31 @@ def test_skinny_gemm_silu(M):
     _close(out, exp, 0.03, 0.03)
 
 
+@pytest.mark.parametrize("M", [1, 300, 2048, 3000])
+@pytest.mark.parametrize("N,K", [(256, 64), (768, 1024), (512, 2080)])
+def test_gemm_prefill(M, N, K):
+    """256x256-tile prefill GEMM (gemm_prefill.hip) vs fp32: M tails, K not a multiple of
+    the ring depth, several N tiles per group."""
+    torch.manual_seed(M + N + K)
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=DEV) / K ** 0.5).to(torch.bfloat16)
+    assert ops.hip().gemm_prefill_supported(w, False)
+    out = ops.gemm_prefill(x, w)
+    _close(out, x.float().cpu() @ w.float().cpu().t(), 0.02, 0.02)
+
+
+@pytest.mark.parametrize("M,F,K", [(77, 128, 256), (1000, 384, 1024), (4096, 256, 512)])
+def test_gemm_prefill_silu(M, F, K):
+    """gate_up GEMM with the SwiGLU in the epilogue vs fp32 silu(x.g^T) * (x.u^T)."""
+    torch.manual_seed(M + F)
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(2 * F, K, device=DEV) / K ** 0.5).to(torch.bfloat16)
+    assert ops.hip().gemm_prefill_supported(w, True)
+    out = ops.gemm_prefill(x, w, silu=True)
+    gu = x.float().cpu() @ w.float().cpu().t()
+    _close(out, torch.nn.functional.silu(gu[:, :F]) * gu[:, F:], 0.02, 0.02)
+
+
 @pytest.mark.parametrize("M,K,N", [(5, 1024, 512), (128, 1024, 512), (256, 4096, 4096), (256, 8192, 256)])
 def test_skinny_gemm_add_rmsnorm(M, K, N):
     # split-K 2 / 2 / 8 (decode o_proj shape) / 16 (past the reduction's unrolled 8)

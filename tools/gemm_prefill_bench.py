@@ -2,7 +2,7 @@
 the engine runs after it) vs the hand-written MFMA GEMM (ops.gemm) with fused
 epilogues.  Random uniform operands (zero-filled operands read high on MFMA).
 
-usage (GPU): python tools/gemm_prefill_bench.py [--ms 4096,16384] [--only gate_up,...] [--ours]
+usage (GPU): python tools/gemm_prefill_bench.py [--ms 4096,16384] [--only gate_up,...] [--ours [--big]]
 """
 from __future__ import annotations
 
@@ -46,6 +46,8 @@ def main():
     ap.add_argument("--ms", default="2048,8192,16384")
     ap.add_argument("--only", default="")
     ap.add_argument("--ours", action="store_true", help="also time ops.gemm (hand-written)")
+    ap.add_argument("--big", action="store_true",
+                    help="llama shapes: time ops.gemm_prefill (256x256 tiles, SwiGLU epilogue) as 'ours'")
     a = ap.parse_args()
     from langstream_amd import ops
     dev = "cuda"
@@ -83,7 +85,9 @@ def main():
                     kw.update(bias=b)
                 elif epi == "bias_res":
                     kw.update(bias=b, residual=res)
-                out = ops.gemm(x, w, **kw)
+                big = a.big and name.startswith("llama")
+                fn = (lambda: ops.gemm_prefill(x, w, silu=epi == "swiglu")) if big else (lambda: ops.gemm(x, w, **kw))
+                out = fn()
                 ref = F.linear(x.float(), w.float(), None if b is None else b.float())
                 if epi == "swiglu":
                     g, u = ref.chunk(2, -1)
@@ -93,7 +97,7 @@ def main():
                 elif epi == "bias_res":
                     ref = ref + res.float()
                 err = ((out.float() - ref).abs().max() / ref.abs().max()).item()
-                t_ours = timeit(lambda: ops.gemm(x, w, **kw))
+                t_ours = timeit(fn)
                 row.update(ours_us=round(t_ours, 1), ours_tflops=round(flops / t_ours / 1e6, 1),
                            speedup=round(t_lib / t_ours, 3), rel_err=round(err, 5))
             print(json.dumps(row), flush=True)
