@@ -36,7 +36,10 @@ enum { EPI_STORE = 0, EPI_SILU = 1 };
 // third less LDS read traffic per K step and no SIMD-sharing wave at the barrier.
 // (A register-staged ring -- global_load_dwordx4 + ds_write_b128 instead of LDS-DMA --
 // measured 10-15 % slower on every Llama shape: profiles/pgemm_bench_v3_rs.log.)
-template <int S, int EPI, int NWV>
+// ABL (diagnostic ablation builds, wrong results, timing only; LS_PGEMM_ABL):
+// bit 0 drops the in-loop waits + barrier, bit 1 the in-loop LDS-DMA issue,
+// bit 2 the in-loop fragment reads.
+template <int S, int EPI, int NWV, int ABL = 0>
 __global__ void __launch_bounds__(NWV * 64) gemm_prefill_kernel(const bf16* __restrict__ x, int64_t ldx,
                                                                 const bf16* __restrict__ w, int M, int K,
                                                                 bf16* __restrict__ out, int64_t ldo, int MT,
@@ -122,14 +125,16 @@ __global__ void __launch_bounds__(NWV * 64) gemm_prefill_kernel(const bf16* __re
   auto step = [&](int kt, const bf16x8 (&ca)[8], const bf16x8 (&cb)[JT], bf16x8 (&na)[8], bf16x8 (&nb)[JT]) {
     // stage kt's fragment reads (all but the NRD newest LDS ops) are complete before this
     // wave joins the barrier after which another wave may refill their slot
-    asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(NRD < 15 ? NRD : 15) : "memory");  // counter max 15
-    wait_vmcnt<(S - 3) * PER>();          // this wave's DMA of stage kt+1 has landed
-    __builtin_amdgcn_s_barrier();         // ... and every other wave's
+    if constexpr ((ABL & 1) == 0) {
+      asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(NRD < 15 ? NRD : 15) : "memory");  // counter max 15
+      wait_vmcnt<(S - 3) * PER>();        // this wave's DMA of stage kt+1 has landed
+      __builtin_amdgcn_s_barrier();       // ... and every other wave's
+    }
     int rs = buf + S - 1;
     if (rs >= S) rs -= S;
-    issue(min(kt + S - 1, nk - 1), rs);   // past the end: re-load the last stage into a dead slot
+    if constexpr ((ABL & 2) == 0) issue(min(kt + S - 1, nk - 1), rs);  // past the end: re-load the last stage into a dead slot
     const int b1 = buf + 1 == S ? 0 : buf + 1;
-    load_frags(b1, na, nb);               // past the end: reads a dead slot, never used
+    if constexpr ((ABL & 4) == 0) load_frags(b1, na, nb);  // past the end: reads a dead slot, never used
     mma(ca, cb);
     constexpr int PERRD = 8 * JT / NRD;   // MFMAs between consecutive fragment reads
 #pragma unroll
@@ -189,6 +194,18 @@ void launch(int ring, int nwv, dim3 grid, hipStream_t st, const at::Tensor& x, c
   gemm_prefill_kernel<SV, EPI, NW><<<grid, NW * 64, 0, st>>>((const bf16*)x.data_ptr(), x.stride(0),                  \
                                                      (const bf16*)w.data_ptr(), M, K, (bf16*)out.data_ptr(),  \
                                                      out.stride(0), MT, NTL, F, gm)
+  static const int abl = env_int("LS_PGEMM_ABL", 0);
+  if (abl != 0 && EPI == EPI_STORE && nwv == 8 && ring == 4) {   // diagnostic ablations
+    auto* xp = (const bf16*)x.data_ptr();
+    auto* wp = (const bf16*)w.data_ptr();
+    auto* op = (bf16*)out.data_ptr();
+    if (abl == 1) gemm_prefill_kernel<4, EPI, 8, 1><<<grid, 512, 0, st>>>(xp, x.stride(0), wp, M, K, op, out.stride(0), MT, NTL, F, gm);
+    else if (abl == 2) gemm_prefill_kernel<4, EPI, 8, 2><<<grid, 512, 0, st>>>(xp, x.stride(0), wp, M, K, op, out.stride(0), MT, NTL, F, gm);
+    else if (abl == 3) gemm_prefill_kernel<4, EPI, 8, 3><<<grid, 512, 0, st>>>(xp, x.stride(0), wp, M, K, op, out.stride(0), MT, NTL, F, gm);
+    else if (abl == 4) gemm_prefill_kernel<4, EPI, 8, 4><<<grid, 512, 0, st>>>(xp, x.stride(0), wp, M, K, op, out.stride(0), MT, NTL, F, gm);
+    else gemm_prefill_kernel<4, EPI, 8, 7><<<grid, 512, 0, st>>>(xp, x.stride(0), wp, M, K, op, out.stride(0), MT, NTL, F, gm);
+    return;
+  }
   if (nwv == 4) {
     if (ring == 3) L(3, 4);
     else if (ring == 5) L(5, 4);
