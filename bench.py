@@ -456,6 +456,7 @@ def main():
         return k
 
     sent = {}
+    phases = []
 
     def publish_pages(step):
         if args.docs <= 0:
@@ -477,8 +478,11 @@ def main():
                 send_question()
         expect_docs = (step + 1) * args.docs * world
         lats = []
+        t_first = t_all = None
         deadline = time.time() + args.timeout
         while len(lats) < args.batch or (args.docs > 0 and not ingest_done(expect_docs)):
+            if t_all is None and len(lats) >= args.batch:
+                t_all = time.time()
             if runner.errors:
                 raise runner.errors[0]
             if time.time() > deadline:
@@ -489,10 +493,15 @@ def main():
                 t = sent.pop(r.key(), None)
                 if t is not None:
                     lats.append(time.time() - t)
+                    if t_first is None:
+                        t_first = time.time()
                     if args.load == "stream":
                         send_question()   # closed loop: keep --batch questions in flight
         steps_done[0] += 1
-        return time.time() - t0, lats
+        t_end = time.time()
+        # (first answer, last answer, step end incl. waiting for the crawled pages' indexing), s
+        phases.append([round((t_first or t_end) - t0, 3), round((t_all or t_end) - t0, 3), round(t_end - t0, 3)])
+        return t_end - t0, lats
 
     def run_window(k_steps):
         """Timed region of the streaming load.  Only questions SENT inside the window
@@ -543,6 +552,17 @@ def main():
     from langstream_amd.utils import threads as _threads
     cpu0 = _threads.snapshot()
     stats0 = dict(llm.stats)
+    phases.clear()
+    import gc
+    gc_t = {"start": 0.0, "ms": 0.0, "n": [0, 0, 0]}
+
+    def _gc_cb(phase, info):
+        if phase == "start":
+            gc_t["start"] = time.perf_counter()
+        else:
+            gc_t["ms"] += 1000 * (time.perf_counter() - gc_t["start"])
+            gc_t["n"][info["generation"]] += 1
+    gc.callbacks.append(_gc_cb)
     t0 = time.time()
     my_lats = []
     if args.load == "stream":
@@ -553,6 +573,7 @@ def main():
             my_lats.extend(lats)
     barrier()
     elapsed = time.time() - t0
+    gc.callbacks.remove(_gc_cb)
     chunks = len(store) - chunks0
     if os.environ.get("LANGSTREAM_THREAD_CPU"):
         print(json.dumps({"thread_cpu_s": _threads.diff(cpu0, _threads.snapshot())}), file=sys.stderr, flush=True)
@@ -565,6 +586,7 @@ def main():
             assign[info["topic"]] = info.get("assignment")
     mine = {"elapsed": elapsed, "lats": my_lats, "chunks": chunks, "assign": assign,
             "prefill_tokens": stats.get("prefill_tokens", 0), "requests": stats.get("requests", 0),
+            "phases": phases, "gc": {"pause_ms": round(gc_t["ms"], 1), "collections_by_gen": gc_t["n"]},
             "knn_rounds": dist_knn.active().rounds if dist_knn.active() else 0,
             "knn_stats": ({k: (round(v, 3) if isinstance(v, float) else v) for k, v in dist_knn.active().stats.items()}
                           if dist_knn.active() else None)}
@@ -600,7 +622,7 @@ def main():
                        "parallelism": f"dp{world}"},
             "ingest": {"pages_per_s": round(args.docs * args.steps * world / elapsed, 2),
                        "chunks_per_s": round(sum(g["chunks"] for g in gathered) / elapsed, 2)},
-            "latency_samples": len(all_lats), "knn_rounds_per_rank": [g["knn_rounds"] for g in gathered],
+            "latency_samples": len(all_lats), "step_phases_rank0_s": gathered[0]["phases"], "gc_rank0": gathered[0]["gc"], "knn_rounds_per_rank": [g["knn_rounds"] for g in gathered],
             "knn_stats_rank0": gathered[0]["knn_stats"],
             "partitions_per_rank": [g["assign"] for g in gathered],
             "setup_s": round(setup_s, 1),
