@@ -22,6 +22,7 @@ from ..api.record import Header, Record, SimpleRecord
 from ..api.topics import TopicConnectionsRuntimeRegistry, TopicOffsetPosition
 from ..core.deployer import ApplicationDeployer, pod_configuration
 from ..core.parser import build_application_instance, build_from_directory
+from ..utils import gctune
 from ..core.planner import ExecutionPlan
 from .runner import AgentRunner
 
@@ -97,6 +98,7 @@ class LocalApplicationRunner:
         deadline = time.time() + wait
         for r in self.runners:
             r.started.wait(max(0.0, deadline - time.time()))
+        gctune.tune()   # startup heap -> permanent generation, rare full collections
         return self
 
     def _run(self, runner: AgentRunner) -> None:

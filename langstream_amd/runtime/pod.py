@@ -163,6 +163,8 @@ def main(argv: Optional[List[str]] = None) -> int:
         signal.signal(signal.SIGTERM, lambda *_: (runner.stop(), stop.set()))
     except (ValueError, OSError):
         pass
+    from ..utils import gctune
+    threading.Thread(target=lambda: runner.started.wait() and gctune.tune(), name="gc-tune", daemon=True).start()
     try:
         runner.run()
         return 0

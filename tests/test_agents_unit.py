@@ -336,3 +336,20 @@ def test_source_record_tracker_commits_in_source_order():
     assert committed == []
     t.commit([outs[0][1]])                     # s0 done -> s0, s1 and the empty-fan-out s2 commit
     assert committed == ["s0", "s1", "s2"] and t.pending() == 0
+
+
+def test_gctune_freezes_startup_heap(monkeypatch):
+    import gc
+    from langstream_amd.utils import gctune
+    old = gc.get_threshold()
+    monkeypatch.setattr(gctune, "_done", False)
+    monkeypatch.setenv("LANGSTREAM_GC", "default")
+    assert gctune.tune() is False and gc.get_threshold() == old
+    monkeypatch.setenv("LANGSTREAM_GC", "tuned")
+    try:
+        assert gctune.tune() is True
+        assert gc.get_threshold() == (50_000, 20, 100) and gc.get_freeze_count() > 0
+        assert gctune.tune() is False   # once per process
+    finally:
+        gc.unfreeze()
+        gc.set_threshold(*old)
