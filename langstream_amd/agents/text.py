@@ -237,6 +237,144 @@ def _xml_text(data: bytes) -> str:
     return html.unescape(s)
 
 
+_PDF_ESC = {ord("n"): "\n", ord("r"): "\r", ord("t"): "\t", ord("b"): "\b", ord("f"): "\f"}
+_PDF_DELIM = b"()<>[]{}/%"
+
+
+def _pdf_bytes_to_str(raw: bytes) -> str:
+    if raw[:2] == b"\xfe\xff":                      # UTF-16BE with BOM (PDF text strings)
+        return raw[2:].decode("utf-16-be", errors="replace")
+    return raw.decode("latin-1")
+
+
+def _pdf_literal(buf: bytes, i: int):
+    """Literal string starting after '(' at i: balanced parentheses, backslash escapes
+    (\\n \\r \\t \\b \\f \\( \\) \\\\, octal \\ddd, line continuation).  Returns (bytes, next i)."""
+    out = bytearray()
+    depth = 1
+    n = len(buf)
+    while i < n:
+        c = buf[i]
+        if c == 0x5C:                                   # backslash
+            i += 1
+            if i >= n:
+                break
+            e = buf[i]
+            if e in _PDF_ESC:
+                out += _PDF_ESC[e].encode("latin-1")
+                i += 1
+            elif 0x30 <= e <= 0x37:
+                j = i
+                while j < n and j < i + 3 and 0x30 <= buf[j] <= 0x37:
+                    j += 1
+                out.append(int(buf[i:j], 8) & 0xFF)
+                i = j
+            elif e in (0x0D, 0x0A):                      # escaped end of line: continuation
+                i += 1
+                if e == 0x0D and i < n and buf[i] == 0x0A:
+                    i += 1
+            else:
+                out.append(e)
+                i += 1
+            continue
+        if c == 0x28:
+            depth += 1
+        elif c == 0x29:
+            depth -= 1
+            if depth == 0:
+                return bytes(out), i + 1
+        out.append(c)
+        i += 1
+    return bytes(out), i
+
+
+def _pdf_tokens(buf: bytes):
+    """Content-stream tokens: ('s', bytes) strings, ('n', float) numbers, ('[', None),
+    (']', None) and ('op', name) operators; dictionaries / names are skipped."""
+    i, n = 0, len(buf)
+    while i < n:
+        c = buf[i]
+        if c in b" \t\r\n\x0c\x00":
+            i += 1
+        elif c == 0x25:                                 # comment
+            while i < n and buf[i] not in b"\r\n":
+                i += 1
+        elif c == 0x28:
+            sv, i = _pdf_literal(buf, i + 1)
+            yield "s", sv
+        elif c == 0x3C and i + 1 < n and buf[i + 1] == 0x3C:   # << dict >>: skip markers
+            i += 2
+        elif c == 0x3E and i + 1 < n and buf[i + 1] == 0x3E:
+            i += 2
+        elif c == 0x3C:                                 # <hex string>
+            j = buf.find(b">", i)
+            j = n if j < 0 else j
+            hx = re.sub(rb"[^0-9A-Fa-f]", b"", buf[i + 1:j])
+            if len(hx) % 2:
+                hx += b"0"
+            yield "s", bytes.fromhex(hx.decode())
+            i = j + 1
+        elif c == 0x5B:
+            yield "[", None
+            i += 1
+        elif c == 0x5D:
+            yield "]", None
+            i += 1
+        elif c == 0x2F:                                 # /Name
+            i += 1
+            while i < n and buf[i] not in b" \t\r\n\x0c" and buf[i] not in _PDF_DELIM:
+                i += 1
+        else:
+            j = i
+            while j < n and buf[j] not in b" \t\r\n\x0c\x00" and buf[j] not in _PDF_DELIM:
+                j += 1
+            if j == i:
+                i += 1
+                continue
+            tok = buf[i:j]
+            i = j
+            try:
+                yield "n", float(tok)
+            except ValueError:
+                yield "op", tok.decode("latin-1")
+
+
+def _pdf_content_text(buf: bytes) -> str:
+    """Text of one content stream: Tj / TJ / ' / " show strings; TJ displacements below
+    -200 thousandths of an em become a space; Td / TD / T* / ' / " / ET start a new line
+    (Td with a zero vertical move continues the line)."""
+    out: List[str] = []
+    stack: list = []
+    arr = None
+    for kind, v in _pdf_tokens(buf):
+        if kind == "[":
+            arr = []
+        elif kind == "]":
+            stack.append(("a", arr or []))
+            arr = None
+        elif arr is not None:
+            arr.append((kind, v))
+        elif kind != "op":
+            stack.append((kind, v))
+        else:
+            if v == "Tj" and stack and stack[-1][0] == "s":
+                out.append(_pdf_bytes_to_str(stack[-1][1]))
+            elif v == "TJ" and stack and stack[-1][0] == "a":
+                for k2, v2 in stack[-1][1]:
+                    if k2 == "s":
+                        out.append(_pdf_bytes_to_str(v2))
+                    elif k2 == "n" and v2 < -200:
+                        out.append(" ")
+            elif v in ("'", '"') and stack and stack[-1][0] == "s":
+                out.append("\n" + _pdf_bytes_to_str(stack[-1][1]))
+            elif v in ("T*", "ET"):
+                out.append("\n")
+            elif v in ("Td", "TD") and len(stack) >= 2 and stack[-1][0] == "n":
+                out.append("\n" if stack[-1][1] != 0 else " ")
+            stack.clear()
+    return "".join(out)
+
+
 def _pdf_text(data: bytes) -> str:
     out = []
     for m in re.finditer(rb"stream\r?\n(.*?)\r?\nendstream", data, re.S):
@@ -245,13 +383,13 @@ def _pdf_text(data: bytes) -> str:
             raw = zlib.decompress(raw)
         except zlib.error:
             pass
-        for tm in re.finditer(rb"\[(.*?)\]\s*TJ|\((.*?)\)\s*Tj", raw, re.S):
-            if tm.group(1) is not None:
-                out.append(b"".join(re.findall(rb"\((.*?)\)", tm.group(1))).decode("latin-1"))
-            else:
-                out.append(tm.group(2).decode("latin-1"))
+        if b"BT" not in raw:                            # images, fonts, xref streams
+            continue
+        out.append(_pdf_content_text(raw))
         out.append("\n")
-    return re.sub(r"\n+", "\n", "".join(out)).strip()
+    text = "".join(out)
+    text = re.sub(r"[ \t]+\n", "\n", text)
+    return re.sub(r"\n{2,}", "\n", text).strip()
 
 
 def extract_text(data: Any) -> str:

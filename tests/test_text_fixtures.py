@@ -102,3 +102,15 @@ def test_text_extractor_binary_fixtures(fn, expected):
         data = f.read()
     out = TextExtractorAgent().process_record(SimpleRecord.of("filename", data))
     assert out[0].value().strip() == expected
+
+
+def test_pdf_content_stream_text():
+    """Flate-compressed content stream: literal-string escapes (\\( \\) octal), hex
+    strings, TJ kerning (< -200/1000 em -> space), Td/T*/' line breaks."""
+    import zlib
+    from langstream_amd.agents.text import extract_text
+    content = (b"BT /F1 12 Tf 72 712 Td (Hello \\(PDF\\) world) Tj 0 -14 Td [(Kern)-300(ed)20( text)] TJ "
+               b"T* <48657820737472696E67> Tj\n(oct\\101l) ' ET")
+    pdf = (b"%PDF-1.4\n1 0 obj << /Length 10 /Filter /FlateDecode >>\nstream\n" + zlib.compress(content)
+           + b"\nendstream\nendobj\n%%EOF")
+    assert extract_text(pdf) == "Hello (PDF) world\nKern ed text\nHex string\noctAl"
