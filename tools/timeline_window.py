@@ -29,6 +29,7 @@ def main():
     ap.add_argument("db")
     ap.add_argument("--window-s", type=float, required=True)
     ap.add_argument("--gaps", type=int, default=15)
+    ap.add_argument("--top", type=int, default=25, help="kernels (by name and grid) listed by time in the window")
     a = ap.parse_args()
     c = sqlite3.connect(a.db)
     k = c.execute("select start, end, name, grid_x from kernels order by start").fetchall()
@@ -61,6 +62,14 @@ def main():
     tot = sum(cat.values()) or 1
     for name, v in cat.most_common():
         print(f"  {name:20s} {v / 1e6:9.1f} ms  {v / tot * 100:5.1f} % of kernel time")
+    per = collections.defaultdict(lambda: [0, 0])
+    for s, e, n, g in k:
+        key = (n.split("(")[0][-70:], g)
+        per[key][0] += e - max(s, t0)
+        per[key][1] += 1
+    print("top kernels in the window (ms, calls, avg us, grid, name):")
+    for (n, g), (t, c) in sorted(per.items(), key=lambda kv: -kv[1][0])[: a.top]:
+        print(f"  {t / 1e6:8.1f} {c:6d} {t / c / 1e3:8.1f} {g:9d}  {n}")
     gaps.sort(reverse=True)
     print("longest idle gaps (ms @ offset s):",
           ", ".join(f"{d / 1e6:.1f}@{o / 1e9:.2f}" for d, o in gaps[: a.gaps]))
