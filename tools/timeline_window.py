@@ -64,7 +64,9 @@ def main():
         print(f"  {name:20s} {v / 1e6:9.1f} ms  {v / tot * 100:5.1f} % of kernel time")
     per = collections.defaultdict(lambda: [0, 0])
     for s, e, n, g in k:
-        key = (n.split("(")[0][-70:], g)
+        base = n[5:] if n.startswith("void ") else n
+        base = base.replace("(anonymous namespace)::", "")
+        key = (base.split("(")[0][-70:], g)
         per[key][0] += e - max(s, t0)
         per[key][1] += 1
     print("top kernels in the window (ms, calls, avg us, grid, name):")
