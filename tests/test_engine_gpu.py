@@ -237,3 +237,37 @@ def test_native_executor_tp_path_world1_rccl(oneshot, monkeypatch):
         e1.stop()
     finally:
         dist.destroy_process_group()
+
+
+def test_prefill_gate_up_gemm_in_model(monkeypatch):
+    """A prefill step of >= 1024 tokens runs gate_up on gemm_prefill.hip with the SwiGLU
+    epilogue (native runner and Python forward); its logits match the hipBLASLt +
+    silu_and_mul forward of the same weights."""
+    import langstream_amd.models.llama as llama_mod
+    cfg = PRESETS["llama-small"]
+    model = LlamaModel(cfg, device="cuda")
+    n = 1100
+    nblk = (n + 63) // 64
+    kv = [(torch.zeros(nblk, model.hkv, 64, cfg.head_dim, device="cuda", dtype=model.dtype),
+           torch.zeros(nblk, model.hkv, cfg.head_dim, 64, device="cuda", dtype=model.dtype))
+          for _ in range(cfg.num_layers)]
+    ids = torch.randint(5, 1000, (n,), dtype=torch.int32, device="cuda")
+    pos = torch.arange(n, dtype=torch.int32, device="cuda")
+    bt = torch.arange(nblk, dtype=torch.int32, device="cuda").unsqueeze(0)
+    slots = torch.arange(n, dtype=torch.long, device="cuda")
+    G = model.hq // model.hkv
+    meta = AttnMeta(positions=pos, slots=slots, num_decode=0, num_prefill_tokens=n, p_block_tables=bt,
+                    q_start=torch.tensor([0], dtype=torch.int32, device="cuda"),
+                    q_len=torch.tensor([n], dtype=torch.int32, device="cuda"),
+                    ctx_len=torch.tensor([n], dtype=torch.int32, device="cuda"),
+                    tiles=ops.prefill_tiles([n], G).cuda())
+    rows = torch.tensor([n // 2, n - 1], dtype=torch.long, device="cuda")
+    assert llama_mod._pgemm(torch.empty(n, cfg.hidden_size, device="cuda", dtype=torch.bfloat16),
+                            model.layers[0].gate_up_w, True)
+    native = model.forward_logits(ids, meta, kv, rows).float().cpu()
+    fused = model.logits(model.forward(ids, meta, kv).index_select(0, rows)).float().cpu()
+    monkeypatch.setattr(llama_mod, "_PGEMM", 0)
+    lib = model.logits(model.forward(ids, meta, kv).index_select(0, rows)).float().cpu()
+    for i in range(2):
+        assert _cos(fused[i], lib[i]) > 0.999
+        assert _cos(native[i], lib[i]) > 0.999
