@@ -129,7 +129,7 @@ class AttnMeta:
 
 
 _PGEMM = {"0": 0, "all": 2}.get(os.environ.get("LS_PGEMM", "1"), 1)
-_PGEMM_MIN_T = int(os.environ.get("LS_PGEMM_MIN_T", "1024"))
+_PGEMM_MIN_T = int(os.environ.get("LS_PGEMM_MIN_T", "8192"))   # below: hipBLASLt + silu_and_mul is faster
 
 
 def _pgemm(x: torch.Tensor, w: torch.Tensor, silu: bool) -> bool:

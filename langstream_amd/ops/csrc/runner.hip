@@ -397,7 +397,7 @@ class LlamaRunner {
     }();
     return on;
   }
-  // Prefill-sized steps (T >= LS_PGEMM_MIN_T, default 1024) run the gate_up projection
+  // Prefill-sized steps (T >= LS_PGEMM_MIN_T, default 8192) run the gate_up projection
   // on the 256 x 256-tile hand-written GEMM (ops/csrc/gemm_prefill.hip) with SwiGLU in
   // its epilogue (no [T, 2F] round trip, no silu_and_mul); qkv / o / down stay on
   // hipBLASLt, which is faster on those plain shapes (profiles/pgemm_bench_*.log).
@@ -411,7 +411,7 @@ class LlamaRunner {
     }();
     static const int64_t min_t = [] {
       const char* e = getenv("LS_PGEMM_MIN_T");
-      return e ? (int64_t)atoll(e) : (int64_t)1024;
+      return e ? (int64_t)atoll(e) : (int64_t)8192;
     }();
     return mode > (silu ? 0 : 1) && T >= min_t && gemm_prefill_supported(w, silu);
   }

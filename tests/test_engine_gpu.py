@@ -240,34 +240,39 @@ def test_native_executor_tp_path_world1_rccl(oneshot, monkeypatch):
 
 
 def test_prefill_gate_up_gemm_in_model(monkeypatch):
-    """A prefill step of >= 1024 tokens runs gate_up on gemm_prefill.hip with the SwiGLU
-    epilogue (native runner and Python forward); its logits match the hipBLASLt +
-    silu_and_mul forward of the same weights."""
+    """A prefill step of >= 8192 tokens (3 sequences of 2800, within llama-small's 4096
+    positions) runs gate_up on gemm_prefill.hip with the SwiGLU epilogue (native runner
+    and Python forward); its logits match the hipBLASLt + silu_and_mul forward."""
     import langstream_amd.models.llama as llama_mod
     cfg = PRESETS["llama-small"]
     model = LlamaModel(cfg, device="cuda")
-    n = 1100
-    nblk = (n + 63) // 64
+    lens = [2800, 2800, 2800]
+    n = sum(lens)
+    bps = (max(lens) + 63) // 64
+    nblk = bps * len(lens)
+    assert max(lens) <= cfg.max_position
     kv = [(torch.zeros(nblk, model.hkv, 64, cfg.head_dim, device="cuda", dtype=model.dtype),
            torch.zeros(nblk, model.hkv, cfg.head_dim, 64, device="cuda", dtype=model.dtype))
           for _ in range(cfg.num_layers)]
     ids = torch.randint(5, 1000, (n,), dtype=torch.int32, device="cuda")
-    pos = torch.arange(n, dtype=torch.int32, device="cuda")
-    bt = torch.arange(nblk, dtype=torch.int32, device="cuda").unsqueeze(0)
-    slots = torch.arange(n, dtype=torch.long, device="cuda")
+    pos = torch.cat([torch.arange(m, dtype=torch.int32) for m in lens]).cuda()
+    bt = torch.arange(nblk, dtype=torch.int32, device="cuda").view(len(lens), bps)
+    slots = torch.cat([bt[s].long()[torch.arange(m) // 64].cpu() * 64 + torch.arange(m) % 64
+                       for s, m in enumerate(lens)]).cuda()
     G = model.hq // model.hkv
+    starts = [sum(lens[:i]) for i in range(len(lens))]
     meta = AttnMeta(positions=pos, slots=slots, num_decode=0, num_prefill_tokens=n, p_block_tables=bt,
-                    q_start=torch.tensor([0], dtype=torch.int32, device="cuda"),
-                    q_len=torch.tensor([n], dtype=torch.int32, device="cuda"),
-                    ctx_len=torch.tensor([n], dtype=torch.int32, device="cuda"),
-                    tiles=ops.prefill_tiles([n], G).cuda())
-    rows = torch.tensor([n // 2, n - 1], dtype=torch.long, device="cuda")
+                    q_start=torch.tensor(starts, dtype=torch.int32, device="cuda"),
+                    q_len=torch.tensor(lens, dtype=torch.int32, device="cuda"),
+                    ctx_len=torch.tensor(lens, dtype=torch.int32, device="cuda"),
+                    tiles=ops.prefill_tiles(lens, G).cuda())
+    rows = torch.tensor([s + m - 1 for s, m in zip(starts, lens)], dtype=torch.long, device="cuda")
     assert llama_mod._pgemm(torch.empty(n, cfg.hidden_size, device="cuda", dtype=torch.bfloat16),
                             model.layers[0].gate_up_w, True)
     native = model.forward_logits(ids, meta, kv, rows).float().cpu()
     fused = model.logits(model.forward(ids, meta, kv).index_select(0, rows)).float().cpu()
     monkeypatch.setattr(llama_mod, "_PGEMM", 0)
     lib = model.logits(model.forward(ids, meta, kv).index_select(0, rows)).float().cpu()
-    for i in range(2):
+    for i in range(len(lens)):
         assert _cos(fused[i], lib[i]) > 0.999
         assert _cos(native[i], lib[i]) > 0.999
