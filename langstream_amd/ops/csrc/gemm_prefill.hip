@@ -413,6 +413,9 @@ void gemm_prefill(at::Tensor out, at::Tensor x, at::Tensor w, bool silu) {
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16, "x must be bf16 on the GPU");
   TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && x.stride(0) % 8 == 0, "x must be [M, K] with unit column stride");
   TORCH_CHECK(w.size(1) == K && gemm_prefill_supported(w, silu), "gemm_prefill: unsupported weight shape");
+  TORCH_CHECK(x.device() == w.device() && out.device() == x.device(), "gemm_prefill: tensors on different devices");
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(x.data_ptr()) & 15) == 0 && (reinterpret_cast<uintptr_t>(w.data_ptr()) & 15) == 0,
+              "gemm_prefill: x and w must be 16-byte aligned (16-B LDS-DMA rows)");
   const int64_t NO = silu ? N / 2 : N;
   TORCH_CHECK(out.scalar_type() == at::kBFloat16 && out.dim() == 2 && out.size(0) == M && out.size(1) == NO &&
               out.stride(1) == 1, "out must be bf16 [M, ", NO, "]");
