@@ -13,7 +13,8 @@ GC pause per 9.7 s, 3 full collections; `bench.py` reports `gc_rank0`).
     later collections never traverse the startup heap;
   * thresholds (50000, 20, 100): young collections every 50k net allocations, full
     collections rarely.
-Cycles are still collected.  LANGSTREAM_GC=default keeps CPython's policy.
+Cycles are still collected.  LANGSTREAM_GC=default keeps CPython's policy;
+LANGSTREAM_GC_GEN0 overrides the young-generation threshold.
 """
 from __future__ import annotations
 
@@ -29,6 +30,6 @@ def tune() -> bool:
         return False
     gc.collect()
     gc.freeze()
-    gc.set_threshold(50_000, 20, 100)
+    gc.set_threshold(int(os.environ.get("LANGSTREAM_GC_GEN0", "50000")), 20, 100)
     _done = True
     return True
