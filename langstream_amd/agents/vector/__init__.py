@@ -8,6 +8,7 @@ row matched; DELETE on null value).
 from __future__ import annotations
 
 import json
+import os
 import logging
 import threading
 from concurrent.futures import Future
@@ -204,10 +205,11 @@ class VectorDBSinkAgent(AgentSink):
         self.cfg = dict(configuration)
         ds = self.cfg.get("datasource") or {}
         svc = ds.get("service", "local")
-        if svc in ("local", "local-gpu"):
+        self._local = svc in ("local", "local-gpu")
+        if self._local:
             if ds.get("persist-directory"):
                 VectorStoreRegistry.configure(persist_dir=ds["persist-directory"], fsync=ds.get("fsync"))
-            self.writer = _LocalWriter(self.cfg)
+            self.writer = None   # built in set_context, once the durable default is known
         elif svc in ("jdbc", "sqlite"):
             self.writer = _JdbcWriter(self.cfg)
         elif svc in _remote_writers():
@@ -217,8 +219,27 @@ class VectorDBSinkAgent(AgentSink):
             self.writer = None
             self._unavailable = UnavailableDataSource(svc)
 
+    def set_context(self, context) -> None:
+        super().set_context(context)
+        if not self._local:
+            return
+        # Durable by default (parity: the reference sink writes to a database before the
+        # offset commit, VEC/jdbc/JdbcWriter.java:140+, and agents get a persistent state
+        # directory, API/runner/code/AgentContext.java:64): with no persist-directory /
+        # $LANGSTREAM_VECTOR_STORE_DIR configured, the local store's WAL + snapshots live
+        # in this agent's persistent state directory (the pod's PVC: the planner gives
+        # every vector-db-sink a disk), so a pod restart never loses indexed rows whose
+        # source offsets were committed.
+        if VectorStoreRegistry.persist_dir is None:
+            d = context.get_persistent_state_directory_for_agent(self.agent_id()) if context is not None else None
+            if d:
+                VectorStoreRegistry.configure(persist_dir=os.path.join(d, "vector-store"))
+        self.writer = _LocalWriter(self.cfg)
+
     def write(self, record) -> Future:
         self.processed(1, 0)
+        if self.writer is None and self._local:
+            self.writer = _LocalWriter(self.cfg)   # no context was ever set (unit use)
         if self.writer is None:
             try:
                 self._unavailable.execute_statement("", [], [])

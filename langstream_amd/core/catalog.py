@@ -77,6 +77,16 @@ def _webcrawler_disks(ac: AgentConfiguration) -> Dict[str, DiskSpec]:
     return {}
 
 
+def _vector_sink_disks(ac: AgentConfiguration) -> Dict[str, DiskSpec]:
+    """The local GPU vector store keeps its WAL + snapshots on the agent's disk (durable
+    by default); remote-database sinks need none."""
+    ds = (ac.configuration or {}).get("datasource")
+    if isinstance(ds, dict) and str(ds.get("service", "local")) not in ("local", "local-gpu"):
+        return {}
+    res = ac.resources
+    return {ac.id: res.disk if res is not None and res.disk is not None else DiskSpec(enabled=True)}
+
+
 P, S, K, V = ComponentType.PROCESSOR, ComponentType.SOURCE, ComponentType.SINK, ComponentType.SERVICE
 
 _SPECS = [
@@ -85,7 +95,8 @@ _SPECS = [
     AgentSpec(("re-rank",), P, description="MMR re-rank (BM25 relevance + cosine diversity)"),
     AgentSpec(("flare-controller",), P, required=("loop-topic",), description="FLARE active retrieval loop"),
     AgentSpec(("query-vector-db",), P, required=("datasource", "query"), configure=_datasource_configure),
-    AgentSpec(("vector-db-sink",), K, required=("datasource",), configure=_datasource_configure),
+    AgentSpec(("vector-db-sink",), K, required=("datasource",), configure=_datasource_configure,
+              disk_fn=_vector_sink_disks),
     AgentSpec(("text-extractor", "language-detector", "text-splitter", "text-normaliser", "document-to-json"), P),
     AgentSpec(("dispatch", "trigger-event", "log-event"), P),
     AgentSpec(("timer-source",), S),

@@ -125,6 +125,7 @@ def render_agent_workload(agent_cr: Dict[str, Any]) -> List[Dict[str, Any]]:
         "ports": [{"name": "http", "containerPort": 8080}, {"name": "service", "containerPort": 8000}],
         "env": [{"name": "LANGSTREAM_AGENT_RUNNER_POD_CONFIGURATION", "value": "/app-config/config"},
                 {"name": "LANGSTREAM_AGENT_RUNNER_CODE_PATH", "value": "/app-code-download"},
+                {"name": "LANGSTREAM_AGENT_RUNNER_PERSISTENT_STATE_DIRECTORY", "value": "/persistent-state"},
                 {"name": "HSA_ENABLE_IPC_MODE_LEGACY", "value": "0"}],
         "resources": {"requests": dict(limits), "limits": limits},
         "livenessProbe": {"httpGet": {"path": "/metrics", "port": 8080}, "initialDelaySeconds": 10,

@@ -271,6 +271,12 @@ class ShardedKnn:
         locks = [stores[c].lock for c in sorted(stores)]
         for lk in locks:
             lk.acquire()
+        # Every rank must run the SAME collective sequence in a round (the headers decide
+        # it, and every rank sees the same headers).  A local failure (OOM in the kNN, a
+        # store error, a bad payload) is therefore recorded here and substituted with an
+        # empty contribution; the round's collectives all still run, and the requests it
+        # touched fail afterwards with the recorded error.
+        errs: Dict[str, BaseException] = {}       # collection -> local failure
         try:
             hits: Dict[int, List[List[tuple]]] = {}   # id(req) -> per query [(score, owner, row)]
             need: List[Dict[str, set]] = [dict() for _ in range(W)]
@@ -300,14 +306,20 @@ class ShardedKnn:
                 dist.all_gather_into_tensor(qall, qloc, group=self.data)
                 t_s = self._phase("gather_s", t_s)
                 store = stores.get(coll)
+                s = idx = None
                 if store is not None and store.dim == dim and len(store):
-                    if store.device.type == "cuda" and self.data_dev.type == "cpu":
-                        s, idx = to_host(*store.topk_rows(qall.pin_memory().to(
-                            store.device, non_blocking=True).to(store.dtype), kmax))
-                    else:
-                        s, idx = store.topk_rows(qall.to(store.device, store.dtype), kmax)
-                        s, idx = s.to(self.data_dev), idx.to(self.data_dev)
-                else:
+                    try:
+                        if store.device.type == "cuda" and self.data_dev.type == "cpu":
+                            s, idx = to_host(*store.topk_rows(qall.pin_memory().to(
+                                store.device, non_blocking=True).to(store.dtype), kmax))
+                        else:
+                            s, idx = store.topk_rows(qall.to(store.device, store.dtype), kmax)
+                            s, idx = s.to(self.data_dev), idx.to(self.data_dev)
+                    except Exception as e:  # noqa: BLE001 - contribute nothing, keep the collectives
+                        log.exception("sharded kNN: local search of %s failed", coll)
+                        errs[coll] = e
+                        s = idx = None
+                if s is None:
                     s = torch.full((W * qmax, kmax), float("-inf"), device=self.data_dev)
                     idx = torch.full((W * qmax, kmax), -1, dtype=torch.int32, device=self.data_dev)
                 send = torch.stack([s.float(), idx.int().view(torch.float32)], -1).contiguous()  # [W*qmax,k,2]
@@ -318,13 +330,18 @@ class ShardedKnn:
                 n_me = counts[me]
                 if n_me == 0:
                     continue
-                recv = recv.view(W, qmax, kmax, 2)[:, :n_me]                 # [W, n_me, k, 2]
-                cs = recv[..., 0].permute(1, 0, 2).reshape(n_me, W * kmax)
-                ci = recv[..., 1].contiguous().view(torch.int32).permute(1, 0, 2).reshape(n_me, W * kmax)
-                top_s, sel = torch.topk(cs, kmax, dim=-1)
-                rows = torch.gather(ci, 1, sel)
-                owners = sel // kmax
-                top_s, rows, owners = (t.tolist() for t in to_host(top_s, rows, owners.int()))
+                try:
+                    recv = recv.view(W, qmax, kmax, 2)[:, :n_me]                 # [W, n_me, k, 2]
+                    cs = recv[..., 0].permute(1, 0, 2).reshape(n_me, W * kmax)
+                    ci = recv[..., 1].contiguous().view(torch.int32).permute(1, 0, 2).reshape(n_me, W * kmax)
+                    top_s, sel = torch.topk(cs, kmax, dim=-1)
+                    rows = torch.gather(ci, 1, sel)
+                    owners = sel // kmax
+                    top_s, rows, owners = (t.tolist() for t in to_host(top_s, rows, owners.int()))
+                except Exception as e:  # noqa: BLE001 - local merge only, no collective inside
+                    log.exception("sharded kNN: merge of %s failed", coll)
+                    errs.setdefault(coll, e)
+                    continue
                 self.stats["search_s"] += time.perf_counter() - t_s
                 qi = 0
                 for r in mine:
@@ -347,11 +364,15 @@ class ShardedKnn:
                     st = stores.get(coll)
                     if st is None:
                         continue
-                    rws = sorted(rws)
-                    vecs = st.row_vectors(rws) if coll in vec_colls else {}
-                    ans[coll] = {rw: (st.row_payload(rw),
-                                      np.asarray(vecs[rw], np.float32).tobytes() if rw in vecs else None)
-                                 for rw in rws if 0 <= rw < len(st)}
+                    try:
+                        rws = sorted(rws)
+                        vecs = st.row_vectors(rws) if coll in vec_colls else {}
+                        ans[coll] = {rw: (st.row_payload(rw),
+                                          np.asarray(vecs[rw], np.float32).tobytes() if rw in vecs else None)
+                                     for rw in rws if 0 <= rw < len(st)}
+                    except Exception as e:  # noqa: BLE001 - tell the asker instead of skipping the exchange
+                        log.exception("sharded kNN: payloads of %s failed", coll)
+                        ans.setdefault("__errors__", {})[coll] = f"{type(e).__name__}: {e}"
                 return ans
 
             local = serve(need[me])
@@ -365,9 +386,15 @@ class ShardedKnn:
         payload = [msgpack.unpackb(b, raw=False, strict_map_key=False) if b else {}
                    for b in self._alltoall_bytes(answers)]
         payload[me] = local
+        for src, ans in enumerate(payload):
+            for coll, msg in (ans.get("__errors__") or {}).items():
+                errs.setdefault(coll, RuntimeError(f"kNN shard {src} could not serve {coll}: {msg}"))
         self.stats["payload_s"] += time.perf_counter() - t_p
         for r in take:
             if r.fut.done():
+                continue
+            if r.coll in errs:
+                r.fut.set_exception(errs[r.coll])
                 continue
             out = []
             for lst in hits.get(id(r), [[] for _ in range(r.q.shape[0])]):

@@ -51,18 +51,39 @@ def _safe(name: str) -> str:
 
 
 class _Persistence:
-    """Snapshot + write-ahead log of one collection."""
+    """Snapshot + write-ahead log of one collection.
+
+    Crash safety:
+    * the snapshot is ONE file (``snapshot.lsv``: magic, JSON header with dim / dtype /
+      ids / metadata, then the raw vector rows) written to a temp file and swapped in with
+      a single ``os.replace`` -- a crash leaves either the old or the new snapshot, never
+      a vector file whose row count disagrees with its ids;
+    * the WAL is length-prefixed msgpack entries; ``load`` stops at a torn or corrupt
+      tail entry and TRUNCATES the log there before anything is appended, so entries
+      written after a restart are never parsed across the garbage;
+    * replaying WAL entries over a snapshot that already contains them is idempotent
+      (upserts by id, deletes of present ids), so a crash between the snapshot swap and
+      the WAL reset loses nothing."""
+
+    MAGIC = b"LSVS0001"
 
     def __init__(self, directory: str, fsync: bool = False):
         self.dir = directory
         self.fsync = fsync
         os.makedirs(directory, exist_ok=True)
         self.wal_path = os.path.join(directory, "wal.log")
-        self.snap_meta = os.path.join(directory, "snapshot.json")
-        self.snap_vec = os.path.join(directory, "snapshot.vec")
-        self._wal = open(self.wal_path, "ab")
+        self.snap_path = os.path.join(directory, "snapshot.lsv")
+        # pre-r3 layout (two files, swapped separately): read if present, never written
+        self.old_meta = os.path.join(directory, "snapshot.json")
+        self.old_vec = os.path.join(directory, "snapshot.vec")
+        self._wal = None
+
+    def _open_wal(self) -> None:
+        if self._wal is None:
+            self._wal = open(self.wal_path, "ab")
 
     def _append(self, entry) -> None:
+        self._open_wal()
         b = msgpack.packb(entry, use_bin_type=True)
         self._wal.write(len(b).to_bytes(4, "little") + b)
         self._wal.flush()
@@ -76,45 +97,99 @@ class _Persistence:
         self._append(("d", list(ids)))
 
     def wal_bytes(self) -> int:
+        self._open_wal()
         return self._wal.tell()
+
+    @classmethod
+    def read_snapshot_header(cls, path: str) -> Optional[Tuple[dict, int]]:
+        """(header, byte offset of the vector rows) of a snapshot file, or None."""
+        if not os.path.exists(path):
+            return None
+        with open(path, "rb") as f:
+            head = f.read(16)
+            if len(head) < 16 or head[:8] != cls.MAGIC:
+                raise ValueError(f"{path}: not a vector-store snapshot")
+            n = int.from_bytes(head[8:16], "little")
+            return json.loads(f.read(n).decode()), 16 + n
 
     def load(self):
         """-> (dim or None, ids, metas, vectors torch [n, dim] or None, wal entries)."""
         ids, metas, vec, dim = [], [], None, None
-        if os.path.exists(self.snap_meta) and os.path.exists(self.snap_vec):
-            with open(self.snap_meta) as f:
+        hdr = self.read_snapshot_header(self.snap_path)
+        if hdr is not None:
+            m, off = hdr
+            dim, ids, metas = m["dim"], m["ids"], m["meta"]
+            bf = m.get("dtype") == "bfloat16"
+            raw = np.fromfile(self.snap_path, dtype=np.int16 if bf else np.float32, offset=off)
+            vec = torch.from_numpy(raw[: len(ids) * dim].reshape(len(ids), dim).copy())
+            if bf:
+                vec = vec.view(torch.bfloat16)
+        elif os.path.exists(self.old_meta) and os.path.exists(self.old_vec):
+            with open(self.old_meta) as f:
                 m = json.load(f)
             dim, ids, metas = m["dim"], m["ids"], m["meta"]
-            raw = np.fromfile(self.snap_vec, dtype=np.int16 if m.get("dtype") == "bfloat16" else np.float32)
+            raw = np.fromfile(self.old_vec, dtype=np.int16 if m.get("dtype") == "bfloat16" else np.float32)
+            if raw.size != len(ids) * dim:
+                raise ValueError(f"{self.dir}: legacy snapshot.vec holds {raw.size} values for {len(ids)} ids")
             vec = torch.from_numpy(raw.reshape(len(ids), dim).copy())
             if m.get("dtype") == "bfloat16":
                 vec = vec.view(torch.bfloat16)
         entries = []
-        with open(self.wal_path, "rb") as f:
-            data = f.read()
+        data = b""
+        if os.path.exists(self.wal_path):
+            with open(self.wal_path, "rb") as f:
+                data = f.read()
         i = 0
         while i + 4 <= len(data):
             n = int.from_bytes(data[i:i + 4], "little")
             if i + 4 + n > len(data):
                 break  # torn tail write: everything before it was acknowledged
-            entries.append(msgpack.unpackb(data[i + 4:i + 4 + n], raw=False, strict_map_key=False))
+            try:
+                entries.append(msgpack.unpackb(data[i + 4:i + 4 + n], raw=False, strict_map_key=False))
+            except Exception:  # noqa: BLE001 - a corrupt entry ends the valid log like a torn one
+                break
             i += 4 + n
+        if i != len(data):
+            log.warning("vector store %s: dropping %d bytes of torn WAL tail", self.dir, len(data) - i)
+            if self._wal is not None:
+                self._wal.close()
+                self._wal = None
+            with open(self.wal_path, "r+b") as f:
+                f.truncate(i)
+                f.flush()
+                os.fsync(f.fileno())
         return dim, ids, metas, vec, entries
 
     def snapshot(self, dim: int, ids, metas, vec: torch.Tensor) -> None:
-        tmp_v, tmp_m = self.snap_vec + ".tmp", self.snap_meta + ".tmp"
+        tmp = self.snap_path + ".tmp"
         bf16 = vec.dtype == torch.bfloat16
-        (vec.view(torch.int16) if bf16 else vec.float()).numpy().tofile(tmp_v)
-        with open(tmp_m, "w") as f:
-            json.dump({"dim": dim, "dtype": "bfloat16" if bf16 else "float32", "ids": list(ids),
-                       "meta": list(metas)}, f)
-        os.replace(tmp_v, self.snap_vec)
-        os.replace(tmp_m, self.snap_meta)
-        self._wal.close()
+        hdr = json.dumps({"dim": dim, "dtype": "bfloat16" if bf16 else "float32", "ids": list(ids),
+                          "meta": list(metas)}).encode()
+        with open(tmp, "wb") as f:
+            f.write(self.MAGIC + len(hdr).to_bytes(8, "little") + hdr)
+            (vec.view(torch.int16) if bf16 else vec.float()).numpy().tofile(f)
+            f.flush()
+            os.fsync(f.fileno())
+        os.replace(tmp, self.snap_path)      # the single atomic swap
+        for old in (self.old_meta, self.old_vec):
+            if os.path.exists(old):
+                os.remove(old)
+        try:
+            dfd = os.open(self.dir, os.O_RDONLY)
+            try:
+                os.fsync(dfd)
+            finally:
+                os.close(dfd)
+        except OSError:
+            pass
+        if self._wal is not None:
+            self._wal.close()
         self._wal = open(self.wal_path, "wb")
 
     def close(self) -> None:
-        self._wal.close()
+        if self._wal is not None:
+            self._wal.close()
+            self._wal = None
 
 
 class VectorStore:
@@ -405,8 +480,12 @@ class VectorStoreRegistry:
     def _persisted_dim(cls, name: str) -> Optional[int]:
         if not cls.persist_dir:
             return None
-        meta = os.path.join(cls.persist_dir, _safe(name), "snapshot.json")
-        wal = os.path.join(cls.persist_dir, _safe(name), "wal.log")
+        d = os.path.join(cls.persist_dir, _safe(name))
+        meta = os.path.join(d, "snapshot.json")
+        wal = os.path.join(d, "wal.log")
+        hdr = _Persistence.read_snapshot_header(os.path.join(d, "snapshot.lsv"))
+        if hdr is not None:
+            return int(hdr[0]["dim"])
         if os.path.exists(meta):
             with open(meta) as f:
                 return int(json.load(f)["dim"])

@@ -24,6 +24,7 @@
 from __future__ import annotations
 
 import base64
+import re
 import hashlib
 import hmac
 import json
@@ -241,8 +242,19 @@ class JwtAuthProvider(AuthProvider):
         pk = _cfg(self.cfg, "public-key", "publicKey")
         self.rsa = rsa_from_pem(str(pk)) if pk else None
         self.jwks_uri = _cfg(self.cfg, "jwks-uri", "jwksUri")
-        allow = _cfg(self.cfg, "jwks-hosts-allowlist", "jwksHostsAllowlist", default="")
-        self.jwks_hosts = [h.strip() for h in str(allow).split(",") if h.strip()]
+        allow = str(_cfg(self.cfg, "jwks-hosts-allowlist", "jwksHostsAllowlist", default="") or "").strip()
+        # a regex full-matched against the jku's parsed HOST only, like the reference's
+        # Pattern.compile(hostsAllowlist).matcher(host).matches()
+        # (JwksUriSigningKeyResolver.java:72-75,132); a comma list of such patterns is
+        # accepted too.  Never a prefix test on the URL string: "https://issuer.example"
+        # must not admit https://issuer.example.evil.com/ or https://issuer.example@evil.com/.
+        self.jwks_hosts = []
+        if allow:
+            for pat in [allow] + [h.strip() for h in allow.split(",") if h.strip() and "," in allow]:
+                try:
+                    self.jwks_hosts.append(re.compile(pat))
+                except re.error as e:
+                    raise ValueError(f"invalid jwks-hosts-allowlist pattern {pat!r}: {e}") from e
         self.auth_claim = _cfg(self.cfg, "auth-claim", "authClaim", default="sub")
         self.audience = _cfg(self.cfg, "audience")
         self.audience_claim = _cfg(self.cfg, "audience-claim", "audienceClaim", default="aud")
@@ -255,8 +267,11 @@ class JwtAuthProvider(AuthProvider):
         the allowlist is missing); otherwise the configured ``jwks-uri`` is used."""
         jku = header.get("jku")
         if jku and jku != self.jwks_uri:
-            host = urllib.parse.urlparse(str(jku)).hostname or ""
-            if not self.jwks_hosts or not any(host == h or str(jku).startswith(h) for h in self.jwks_hosts):
+            try:
+                host = urllib.parse.urlparse(str(jku)).hostname or ""
+            except ValueError:
+                host = ""
+            if not host or not self.jwks_hosts or not any(p.fullmatch(host) for p in self.jwks_hosts):
                 raise JwtError(f"Untrusted hostname {host!r} for jku")
             return str(jku)
         return self.jwks_uri

@@ -521,6 +521,9 @@ class ShmLog : public std::enable_shared_from_this<ShmLog> {
     int64_t pos = -1;
   };
 
+  // First offset still stored in partition p (retention may have dropped older blocks).
+  int64_t part_base(int ti, int p) const { return h_->topics[ti].parts[p].base; }
+
   int read_part(int ti, int p, int64_t& pos, Cursor& cur, int max_records, uint64_t& budget, std::vector<Rec>& out) {
     PartMeta& pm = h_->topics[ti].parts[p];
     if (pos < pm.base) pos = pm.base;
@@ -787,6 +790,7 @@ class ShmConsumer {
           for (int k = 0; k < np && n < max_records && budget > 0; ++k) {
             const int p = (int)((rr_ + k) % np);
             if (!owned_[p]) continue;
+            clamp_to_base(*g, p);
             n += log_->read_part(ti_, p, pos_[p], cur_[p], max_records - n, budget, recs);
           }
           rr_++;
@@ -814,6 +818,7 @@ class ShmConsumer {
     for (auto& po : offsets) {
       const int p = po.first;
       if (p < 0 || p >= np || !owned_[p]) continue;  // stale ack after a rebalance
+      clamp_to_base(*g, p);
       if (po.second < committed_[p]) continue;
       done_[p].insert(po.second);
       while (!done_[p].empty() && *done_[p].begin() == committed_[p]) {
@@ -832,6 +837,29 @@ class ShmConsumer {
     GroupMeta& g = log_->h()->groups[gi_];
     if (!g.used || g.topic != ti_ || group_ != g.name) return nullptr;
     return &g;
+  }
+
+  // Retention dropped the head of partition p past offsets this group never committed
+  // (a lagging consumer): those offsets can no longer be delivered or acked, so the
+  // contiguous-prefix commit would freeze below them forever.  Move the committed offset
+  // (ours and the group's published one) and the read position up to the partition's
+  // first stored offset, and forget acks below it -- Kafka's "offset out of range ->
+  // earliest" for a consumer overtaken by retention.
+  void clamp_to_base(GroupMeta& g, int p) {
+    const int64_t base = log_->part_base(ti_, p);
+    if (committed_[p] < base) {
+      committed_[p] = base;
+      done_[p].erase(done_[p].begin(), done_[p].lower_bound(base));
+      while (!done_[p].empty() && *done_[p].begin() == committed_[p]) {
+        done_[p].erase(done_[p].begin());
+        committed_[p]++;
+      }
+    }
+    if (g.owner[p] == slot_ && g.committed[p] < committed_[p]) g.committed[p] = committed_[p];
+    if (pos_[p] < base) {
+      pos_[p] = base;
+      cur_[p] = ShmLog::Cursor();
+    }
   }
 
   void sync_assignment(GroupMeta& g, int np) {

@@ -15,7 +15,10 @@
 //   system-scope release fence; store flag[peer][my rank][b] = e on every peer (vector
 //     atomic stores -- never scalar stores)
 //   wait until flag[me][src][b] >= e for every src (system-scope acquire loads; the spin
-//     is bounded: on timeout *err is set and the kernel finishes instead of hanging)
+//     is bounded: on timeout *err is set (sticky), the workgroup writes NaN instead of a
+//     sum of possibly stale peer buffers, and the kernel finishes instead of hanging.  The
+//     step executor copies *err next to every step's results and fails the step when it
+//     is set -- a stalled peer can never turn into silently wrong logits)
 //   out slice = sum over w = 0..W-1 of rank w's buffer half (e & 1), same order on every
 //     rank, so every rank produces bit-identical results
 // Two buffer halves make back-to-back calls safe: a rank reaches call k+2 (which
@@ -61,7 +64,8 @@ struct PeerTable {
 // in and out may alias (in place): a workgroup reads only its own slice of `in`, before
 // its first barrier, and writes `out` after the exchange.
 __global__ void __launch_bounds__(kThreads) oneshot_ar_kernel(IOTable io, int64_t n, int64_t cap, int rank0, int W,
-                                                              PeerTable tbl) {
+                                                              PeerTable tbl, int stall_rank) {
+  __shared__ int timed_out;
   const int b = blockIdx.x, tid = threadIdx.x, y = blockIdx.y;
   const int rank = rank0 + y;
   const bf16* in = io.in[y];
@@ -77,15 +81,20 @@ __global__ void __launch_bounds__(kThreads) oneshot_ar_kernel(IOTable io, int64_
   for (int64_t v = v0 + tid; v < v1; v += kThreads) st16(mine + v * 8, ld16(in + v * 8));
   if (b == 0)   // ragged tail (n % 8 elements)
     for (int64_t i = nvec * 8 + tid; i < n; i += kThreads) mine[i] = in[i];
+  if (tid == 0) timed_out = 0;
   __threadfence_system();
   __syncthreads();
-  if (tid < W) __hip_atomic_store(tbl.flags[tid] + rank * kBlocks + b, e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  // stall_rank (rehearsal only): that simulated rank never publishes, like a peer that
+  // hangs before its all-reduce
+  if (tid < W && rank != stall_rank)
+    __hip_atomic_store(tbl.flags[tid] + rank * kBlocks + b, e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   if (tid < W) {
     const int* f = tbl.flags[rank] + tid * kBlocks + b;
     long long spins = 0;
     while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < e) {
       if (++spins > kSpinLimit) {
-        __hip_atomic_store(io.err[y], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(io.err[y], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        timed_out = 1;
         break;
       }
       __builtin_amdgcn_s_sleep(2);
@@ -93,6 +102,16 @@ __global__ void __launch_bounds__(kThreads) oneshot_ar_kernel(IOTable io, int64_
   }
   __syncthreads();
   __threadfence_system();
+  if (timed_out) {
+    // never hand out a sum over buffers a peer may not have written yet
+    const bf16 nan = (bf16)__builtin_nanf("");
+    for (int64_t i = v0 * 8 + tid; i < v1 * 8; i += kThreads) out[i] = nan;
+    if (b == 0)
+      for (int64_t i = nvec * 8 + tid; i < n; i += kThreads) out[i] = nan;
+    __syncthreads();
+    if (tid == 0) epoch[b] = e;
+    return;
+  }
   for (int64_t v = v0 + tid; v < v1; v += kThreads) {
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     for (int w = 0; w < W; ++w) {
@@ -114,8 +133,8 @@ __global__ void __launch_bounds__(kThreads) oneshot_ar_kernel(IOTable io, int64_
 }
 
 void launch_oneshot(const IOTable& io, int ranks_in_grid, int64_t n, int64_t cap, int rank0, int W,
-                    const PeerTable& tbl, hipStream_t stream) {
-  oneshot_ar_kernel<<<dim3(kBlocks, ranks_in_grid), kThreads, 0, stream>>>(io, n, cap, rank0, W, tbl);
+                    const PeerTable& tbl, hipStream_t stream, int stall_rank = -1) {
+  oneshot_ar_kernel<<<dim3(kBlocks, ranks_in_grid), kThreads, 0, stream>>>(io, n, cap, rank0, W, tbl, stall_rank);
 }
 
 int64_t region_bytes(int64_t cap) { return 2 * cap * (int64_t)sizeof(bf16) + kMaxRanks * kBlocks * sizeof(int); }
@@ -185,6 +204,9 @@ class OneShotAllReduce {
     launch_oneshot(io, 1, t.numel(), cap_, rank_, W_, tbl_, at::hip::getCurrentHIPStream().stream());
   }
 
+  // Device word that becomes non-zero (and stays so) when a wait timed out.
+  const int* err_ptr() const { return err_; }
+
   // Non-zero when a wait timed out (a peer never arrived): the results are invalid.
   int64_t error() {
     int e = 0;
@@ -209,12 +231,14 @@ std::shared_ptr<OneShotAllReduce> make_oneshot_allreduce(c10::intrusive_ptr<::c1
 }
 
 void oneshot_allreduce_run(const std::shared_ptr<OneShotAllReduce>& ar, at::Tensor t) { ar->run(t); }
+const int* oneshot_allreduce_err(const std::shared_ptr<OneShotAllReduce>& ar) { return ar->err_ptr(); }
 
 // Single-GPU rehearsal of the protocol: W simulated ranks with their own buffers, flag
 // arrays and epoch counters on one device, all launched in ONE grid (co-resident),
 // `calls` back-to-back calls.  Returns the per-rank outputs of the last call and the
-// per-rank error flags.
-std::vector<at::Tensor> oneshot_allreduce_sim(std::vector<at::Tensor> inputs, int64_t calls) {
+// per-rank error flags.  stall_rank >= 0: that rank never publishes its flags (a hung
+// peer): every other rank must time out, flag the error and write NaN, not a sum.
+std::vector<at::Tensor> oneshot_allreduce_sim(std::vector<at::Tensor> inputs, int64_t calls, int64_t stall_rank) {
   const int W = (int)inputs.size();
   TORCH_CHECK(W >= 1 && W <= kMaxRanks && calls >= 1);
   const int64_t n = inputs[0].numel();
@@ -237,7 +261,7 @@ std::vector<at::Tensor> oneshot_allreduce_sim(std::vector<at::Tensor> inputs, in
     io.err[w] = io.epoch[w] + kBlocks;
   }
   auto stream = at::hip::getCurrentHIPStream().stream();
-  for (int64_t c = 0; c < calls; ++c) launch_oneshot(io, W, n, n, 0, W, tbl, stream);
+  for (int64_t c = 0; c < calls; ++c) launch_oneshot(io, W, n, n, 0, W, tbl, stream, (int)stall_rank);
   AR_OK(hipStreamSynchronize(stream));
   outs.push_back(epochs.select(1, kBlocks).contiguous());
   return outs;

@@ -37,7 +37,7 @@ void tp_sample_pick(at::Tensor logits, int64_t vstart, int64_t vtot, at::Tensor 
                     at::Tensor hist_all, int64_t n_top, at::Tensor cand);
 void tp_sample_final(at::Tensor stats_all, at::Tensor cand_all, int64_t world, int64_t rows, at::Tensor temperature,
                      int64_t n_top, at::Tensor out_tok, at::Tensor out_lp, at::Tensor top_ids, at::Tensor top_lps);
-std::vector<at::Tensor> oneshot_allreduce_sim(std::vector<at::Tensor> inputs, int64_t calls);
+std::vector<at::Tensor> oneshot_allreduce_sim(std::vector<at::Tensor> inputs, int64_t calls, int64_t stall_rank);
 int64_t oneshot_allreduce_selftest(py::object process_group, at::Tensor t);
 void knn_topk(at::Tensor X, at::Tensor Q, int64_t K, at::Tensor out_s, at::Tensor out_i, at::Tensor ws_s,
               at::Tensor ws_i, int64_t sample);
@@ -65,6 +65,13 @@ void skinny_gemm_add_rmsnorm(at::Tensor out, at::Tensor x, at::Tensor w, at::Ten
                              double eps);
 void gemm_prefill(at::Tensor out, at::Tensor x, at::Tensor w, bool silu);
 bool gemm_prefill_supported(const at::Tensor& w, bool silu);
+bool decode_gemm_supported(const at::Tensor& w, bool silu);
+int64_t decode_gemm_workspace(int64_t M, int64_t N, int64_t K, bool silu);
+void decode_gemm(at::Tensor out, at::Tensor x, at::Tensor w, at::Tensor workspace, c10::optional<at::Tensor> residual,
+                 c10::optional<at::Tensor> norm_w, double eps, int64_t bn_force, int64_t splits_force);
+void decode_gemm_silu(at::Tensor out, at::Tensor x, at::Tensor w, at::Tensor workspace, at::Tensor tickets,
+                      at::Tensor err, int64_t splits);
+void decode_gemm_ablate(at::Tensor x, at::Tensor w, at::Tensor workspace, int64_t abl, int64_t splits);
 void bind_runners(pybind11::module_& m);
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -85,7 +92,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("pool_embeddings", &pool_embeddings);
   m.def("l2_normalize_rows", &l2_normalize_rows);
   m.def("knn_topk", &knn_topk);
-  m.def("oneshot_allreduce_sim", &oneshot_allreduce_sim);
+  m.def("oneshot_allreduce_sim", &oneshot_allreduce_sim, py::arg("inputs"), py::arg("calls"),
+        py::arg("stall_rank") = -1);
   m.def("oneshot_allreduce_selftest", &oneshot_allreduce_selftest);
   m.def("tp_sample_stats", &tp_sample_stats);
   m.def("tp_sample_hist", &tp_sample_hist);
@@ -109,5 +117,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("skinny_gemm_add_rmsnorm", &skinny_gemm_add_rmsnorm);
   m.def("gemm_prefill", &gemm_prefill);
   m.def("gemm_prefill_supported", &gemm_prefill_supported);
+  m.def("decode_gemm_supported", &decode_gemm_supported);
+  m.def("decode_gemm_workspace", &decode_gemm_workspace);
+  m.def("decode_gemm", &decode_gemm, py::arg("out"), py::arg("x"), py::arg("w"), py::arg("workspace"),
+        py::arg("residual") = py::none(), py::arg("norm_w") = py::none(), py::arg("eps") = 1e-5,
+        py::arg("bn") = 0, py::arg("splits") = 0);
+  m.def("decode_gemm_ablate", &decode_gemm_ablate);
+  m.def("decode_gemm_silu", &decode_gemm_silu, py::arg("out"), py::arg("x"), py::arg("w"), py::arg("workspace"),
+        py::arg("tickets"), py::arg("err"), py::arg("splits") = 0);
   bind_runners(m);
 }

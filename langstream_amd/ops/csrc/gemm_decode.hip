@@ -1,0 +1,439 @@
+// Decode-step GEMM on MFMA for gfx950:  C[M, N] = X[M, K] . W[N, K]^T  with the whole
+// decode batch (129 <= M <= 256 rows) in ONE 256-row workgroup tile.
+//
+// Replaces hipBLASLt on the Llama decode projections (qkv, o, gate_up + SwiGLU, down);
+// the reference's inference call site is ChatCompletionsStep.java:132-155 (remote
+// OpenAI / Ollama completions), which this engine serves locally.
+//
+// Why this shape of kernel.  At M = 256 a projection is neither HBM- nor MFMA-bound: it
+// is bound by what each CU can pull through its load path (~60-70 GB/s per CU,
+// MI355X_MICROARCH 'ring-gemm'), and every workgroup re-reads the activations X from L2.
+// The chip-wide bytes a CU must ingest are  (1 + M / BN) x W  plus, with K split S ways,
+// S x M x N x 4 of f32 partial sums.  So:
+//   * all 256 rows in one tile (X re-read N / BN times, never W);
+//   * BN = 128 or 256 output columns; split-K only as far as needed to put ~1 workgroup
+//     on every CU (qkv/o/down), and for gate_up a 2-way split whose halves are combined
+//     inside the launch (below) so SwiGLU stays in the epilogue;
+//   * 64-deep K stages with 128-B LDS rows filled by LDS-DMA (global_load_lds_dwordx4):
+//     one DMA instruction = 8 full 128-B lines (the 64-B rows of gemm_skinny.hip's ring
+//     issue two requests per line: twice the TA traffic for the same bytes);
+//   * separate rings: X (L2-resident, short latency) 2 slots, issued 1 stage ahead; W
+//     (HBM, long latency) 3 slots, issued 2 stages ahead.  One raw s_barrier per stage
+//     behind a counted vmcnt -- never __syncthreads() in the loop (it would drain the
+//     DMAs in flight);
+//   * bank swizzle on the SOURCE address (the DMA image is lane-linear): chunk p of LDS
+//     row r holds global k-chunk p ^ ((r >> 1) & 7), conflict-free ds_read_b128 fragments;
+//   * 8 waves as 4 (rows) x 2 (columns), 64 x BN/2 per wave, MFMA 16x16x32 bf16.
+//
+// gate_up (EPI_SILU2): tile = 128 gate + the matching 128 up rows of W, K split in two.
+// The two halves of a tile sit on one XCD.  The first to finish (ticket parity of a
+// monotonic per-tile counter, so no per-call reset) publishes its f32 accumulators
+// (plain stores -> agent release -> flag), the second waits for the flag (the first is
+// running: it already took its ticket, so no co-residency assumption), acquires, adds the
+// partner's half to its own registers (f32 a + b == b + a: the result does not depend on
+// which half came first) and writes silu(g) * u.  The wait is bounded; a timeout sets
+// err[0] and the host checks it (ops.decode_gemm_error).
+#include <torch/extension.h>
+#include <ATen/hip/HIPContext.h>
+#include "common.h"
+
+void splitk_reduce_launch(const float* part, int S, int M, int N, bf16* out, int64_t ldo, hipStream_t st);
+void splitk_add_rmsnorm_launch(const float* part, int S, int M, int N, bf16* residual, const bf16* norm_w, float eps,
+                               bf16* out, hipStream_t st);
+
+namespace {
+
+constexpr int BM = 256, BK = 64;
+constexpr int XSTAGE = BM * BK * 2;    // 32 KB
+constexpr int LDS_MAX = 160 * 1024;
+
+// s_waitcnt vmcnt(n) for a run-time n (the instruction takes an immediate)
+__device__ __forceinline__ void wait_vmcnt_dyn(int n) {
+  switch (n) {
+#define W_(k) case k: wait_vmcnt<k>(); break;
+    W_(0) W_(1) W_(2) W_(3) W_(4) W_(5) W_(6) W_(7) W_(8) W_(9) W_(10) W_(11) W_(12) W_(13) W_(14) W_(15)
+    W_(16) W_(17) W_(18) W_(19) W_(20) W_(21) W_(22) W_(23) W_(24) W_(25) W_(26) W_(27) W_(28) W_(29) W_(30)
+#undef W_
+    default: wait_vmcnt<0>(); break;
+  }
+}
+
+enum { EPI_STORE = 0, EPI_PARTIAL = 1, EPI_SILU = 2, EPI_SILU2 = 3 };
+
+// 8-row x 128-B piece p of an image: lane l fills row 8p + (l >> 3), LDS chunk l & 7
+// with global chunk (l & 7) ^ ((row >> 1) & 7).
+__device__ __forceinline__ int piece_chunk(int lane, int row) { return ((lane & 7) ^ ((row >> 1) & 7)) * 8; }
+
+// XS / WS: ring slots of X / W; stage t of X is issued XS-1 steps ahead, of W WS-1 ahead.
+// ABL (timing-only ablations, wrong results; tools/dgemm_bench.py --ablate): bit 0 drops
+// the MFMAs, bit 1 the fragment reads, bit 2 the LDS-DMA issue, bit 3 the W DMA only.
+template <int BN, int XS, int WS, int EPI, int ABL = 0>
+__global__ void __launch_bounds__(512) dgemm_kernel(const bf16* __restrict__ x, int64_t ldx,
+                                                   const bf16* __restrict__ w, int M, int N, int K, int S,
+                                                   bf16* __restrict__ out, int64_t ldo, float* __restrict__ part,
+                                                   int F, unsigned* __restrict__ tickets, float* __restrict__ xchg,
+                                                   int* __restrict__ err) {
+  constexpr int WSTAGE = BN * BK * 2;
+  constexpr int JT = BN / 32;              // 16-col tiles per wave (wave = 64 rows x BN/2 cols)
+  constexpr int IT = 4;                    // 16-row tiles per wave
+  constexpr int PX = 4;                    // X pieces per wave per stage (32 / 8 waves)
+  constexpr int PW = BN / 64;              // W pieces per wave per stage
+  constexpr int XA = XS - 1, WA = WS - 1;  // stages issued ahead
+  static_assert(XA >= 1 && WA >= XA, "W is issued at least as far ahead as X");
+  static_assert(XS * XSTAGE + WS * WSTAGE <= LDS_MAX, "LDS budget");
+  __shared__ __attribute__((aligned(1024))) char lds[XS * XSTAGE + WS * WSTAGE];
+  char* const lx0 = lds;
+  char* const lw0 = lds + XS * XSTAGE;
+
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // the S splits of one tile are consecutive logical ids: same XCD (speed only)
+  const int logical = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile = logical / S, split = logical - tile * S;
+  const int nk = K / BK;
+  const int kb = (int)(((int64_t)split * nk) / S), ke = (int)(((int64_t)(split + 1) * nk) / S);
+  const int nks = ke - kb;
+
+  // ---- LDS-DMA sources
+  const bf16* xsrc[PX];
+#pragma unroll
+  for (int j = 0; j < PX; ++j) {
+    const int row = 32 * wid + 8 * j + (lane >> 3);
+    xsrc[j] = x + (int64_t)min(row, M - 1) * ldx + (int64_t)kb * BK + piece_chunk(lane, row);  // rows >= M: never stored
+  }
+  const bf16* wsrc[PW];
+#pragma unroll
+  for (int j = 0; j < PW; ++j) {
+    const int lr = (8 * PW) * wid + 8 * j + (lane >> 3);   // tile-local W row
+    int wrow;
+    if constexpr (EPI == EPI_SILU || EPI == EPI_SILU2)
+      wrow = lr < BN / 2 ? tile * (BN / 2) + lr : F + tile * (BN / 2) + (lr - BN / 2);
+    else
+      wrow = tile * BN + lr;
+    wsrc[j] = w + (int64_t)wrow * K + (int64_t)kb * BK + piece_chunk(lane, lr);
+  }
+  auto issue_x = [&](int t) {
+    char* dst = lx0 + (t % XS) * XSTAGE + (PX * wid) * 1024;
+#pragma unroll
+    for (int j = 0; j < PX; ++j) glds16(xsrc[j] + t * BK, dst + j * 1024);
+  };
+  auto issue_w = [&](int t) {
+    char* dst = lw0 + (t % WS) * WSTAGE + (PW * wid) * 1024;
+#pragma unroll
+    for (int j = 0; j < PW; ++j) glds16(wsrc[j] + t * BK, dst + j * 1024);
+  };
+
+  // ---- fragments
+  const int wm = wid >> 1, wn = wid & 1;
+  const int fr = lane & 15, h = lane >> 4;
+  const int fsw = (fr >> 1) & 7;           // = (row >> 1) & 7 of every fragment row
+  auto bcol = [&](int j) {                 // tile-local W row of this lane's B fragment
+    if constexpr (EPI == EPI_SILU || EPI == EPI_SILU2)
+      return (j < JT / 2 ? (BN / 4) * wn + 16 * j : BN / 2 + (BN / 4) * wn + 16 * (j - JT / 2)) + fr;
+    return (BN / 2) * wn + 16 * j + fr;
+  };
+  int aoff[IT], boff[JT];
+#pragma unroll
+  for (int i = 0; i < IT; ++i) aoff[i] = (64 * wm + 16 * i + fr) * 128;
+#pragma unroll
+  for (int j = 0; j < JT; ++j) boff[j] = bcol(j) * 128;
+
+  f32x4 acc[IT][JT];
+#pragma unroll
+  for (int i = 0; i < IT; ++i)
+#pragma unroll
+    for (int j = 0; j < JT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // Issue order: pseudo-steps u = -WA .. -1 (prologue), then steps u = 0 .. nks-1, each
+  // issuing X(u + XA) then W(u + WA) (stages outside [0, nks) are skipped).  X(t) is
+  // issued at step t - XA and W(t) at step t - WA <= t - XA, before it, so once X(t) has
+  // landed so has W(t).  The DMAs issued AFTER X(t) are W(t - XA + WA) and, for the steps
+  // in between, X(t+1 .. t+XA-1) and W(t+WA-XA+1 .. t+WA-1): at the top of step t the
+  // wait is vmcnt(that count), computed exactly (the tail skips issues).
+  auto issue_step = [&](int u) {
+    if constexpr ((ABL & 4) == 0) {
+      if (u + XA >= 0 && u + XA < nks) issue_x(u + XA);
+      if constexpr ((ABL & 8) == 0)
+        if (u + WA >= 0 && u + WA < nks) issue_w(u + WA);
+    }
+  };
+  for (int u = -WA; u < 0; ++u) issue_step(u);
+  for (int t = 0; t < nks; ++t) {
+    const int nx = max(0, min(t + XA - 1, nks - 1) - t);                       // X(t+1 .. t+XA-1)
+    const int nw = max(0, min(t + WA - 1, nks - 1) - (t - XA + WA) + 1);       // W(t-XA+WA .. t+WA-1)
+    if constexpr ((ABL & 12) == 0) wait_vmcnt_dyn(PX * nx + PW * nw);
+    else if constexpr ((ABL & 4) == 0) wait_vmcnt_dyn(PX * nx);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // step t-1's fragment reads are done
+    __builtin_amdgcn_s_barrier();                         // every wave: stage t landed, t-1 read
+    issue_step(t);                                        // into the slots of stage t-1
+    const char* lx = lx0 + (t % XS) * XSTAGE;
+    const char* lw = lw0 + (t % WS) * WSTAGE;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int off = 16 * ((4 * ks + h) ^ fsw);
+      bf16x8 a[IT], b[JT];
+      if constexpr ((ABL & 2) == 0) {
+#pragma unroll
+        for (int j = 0; j < JT; ++j) b[j] = __builtin_bit_cast(bf16x8, ld16(lw + boff[j] + off));
+#pragma unroll
+        for (int i = 0; i < IT; ++i) a[i] = __builtin_bit_cast(bf16x8, ld16(lx + aoff[i] + off));
+      } else {
+#pragma unroll
+        for (int j = 0; j < JT; ++j) b[j] = bf16x8{} + (bf16)(float)(t + ks + j);
+#pragma unroll
+        for (int i = 0; i < IT; ++i) a[i] = bf16x8{} + (bf16)(float)(t + i);
+      }
+      if constexpr ((ABL & 1) == 0) {
+#pragma unroll
+        for (int i = 0; i < IT; ++i)
+#pragma unroll
+          for (int j = 0; j < JT; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+      } else {
+#pragma unroll
+        for (int i = 0; i < IT; ++i) asm volatile("" ::"v"(a[i]));
+#pragma unroll
+        for (int j = 0; j < JT; ++j) asm volatile("" ::"v"(b[j]));
+      }
+    }
+  }
+  wait_vmcnt<0>();  // no LDS-DMA may outlive the workgroup
+
+  // acc[i][j][r] = C[64wm + 16i + 4h + r][tile col of bcol(j)]
+  const int rbase = 64 * wm + 4 * h;
+  if constexpr (EPI == EPI_SILU2) {
+    // ---- in-launch combine of the two K halves (see the header)
+    __syncthreads();                                      // ring reads done: LDS reusable
+    unsigned* sh = reinterpret_cast<unsigned*>(lds);
+    if (threadIdx.x == 0) sh[0] = __hip_atomic_fetch_add(&tickets[2 * tile], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const unsigned tk = sh[0];
+    const unsigned gen = tk / 2 + 1;                      // this call's generation for the tile
+    float* xb = xchg + (int64_t)tile * (BM * BN);
+    if ((tk & 1u) == 0) {
+      // first half: publish the accumulators in a thread-linear, coalesced layout
+#pragma unroll
+      for (int i = 0; i < IT; ++i)
+#pragma unroll
+        for (int j = 0; j < JT; ++j)
+          *reinterpret_cast<f32x4*>(xb + ((int64_t)(i * JT + j) * 512 + threadIdx.x) * 4) = acc[i][j];
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(&tickets[2 * tile + 1], gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      return;
+    }
+    if (threadIdx.x == 0) {
+      int spins = 0;
+      while (__hip_atomic_load(&tickets[2 * tile + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != gen) {
+        __builtin_amdgcn_s_sleep(2);
+        if (++spins > (1 << 22)) {   // ~0.5 s: the partner never published -- flag it, never hang
+          __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          break;
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    // combine + SwiGLU + store one 16-row tile at a time (bounded live registers)
+#pragma unroll
+    for (int i = 0; i < IT; ++i) {
+      f32x4 g[JT];
+#pragma unroll
+      for (int j = 0; j < JT; ++j)
+        g[j] = acc[i][j] + *reinterpret_cast<const f32x4*>(xb + ((int64_t)(i * JT + j) * 512 + threadIdx.x) * 4);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = rbase + 16 * i + r;
+        if (m >= M) continue;
+        bf16* orow = out + (int64_t)m * ldo + tile * (BN / 2) + (BN / 4) * wn + fr;
+#pragma unroll
+        for (int j = 0; j < JT / 2; ++j) orow[16 * j] = (bf16)(g[j][r] / (1.f + __expf(-g[j][r])) * g[j + JT / 2][r]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < IT; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = rbase + 16 * i + r;
+      if (m >= M) continue;
+      if constexpr (EPI == EPI_SILU) {
+        bf16* orow = out + (int64_t)m * ldo + tile * (BN / 2) + (BN / 4) * wn + fr;
+#pragma unroll
+        for (int j = 0; j < JT / 2; ++j) {
+          const float g = acc[i][j][r], u = acc[i][j + JT / 2][r];
+          orow[16 * j] = (bf16)(g / (1.f + __expf(-g)) * u);
+        }
+      } else if constexpr (EPI == EPI_STORE) {
+        bf16* orow = out + (int64_t)m * ldo + tile * BN + (BN / 2) * wn + fr;
+#pragma unroll
+        for (int j = 0; j < JT; ++j) orow[16 * j] = (bf16)acc[i][j][r];
+      } else {
+        float* prow = part + ((int64_t)split * M + m) * N + tile * BN + (BN / 2) * wn + fr;
+#pragma unroll
+        for (int j = 0; j < JT; ++j) prow[16 * j] = acc[i][j][r];
+      }
+    }
+}
+
+int env_int(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return v ? atoi(v) : dflt;
+}
+
+// Splits so that tiles x S covers the chip about once (<= 256 + 8 workgroups, one per
+// CU) with at least `min_steps` 64-deep stages per split.
+int pick_split(int tiles, int K, int min_steps) {
+  const int nk = K / BK;
+  int best = 1;
+  for (int s = 1; s <= 64; ++s) {
+    if (tiles * s > 264 || nk / s < min_steps) break;
+    best = s;
+  }
+  return best;
+}
+
+// ring shapes: BN = 128: X 3 slots (2 ahead) + W 4 slots (3 ahead) = 160 KB;
+// BN = 256: X 2 + W 3 = 160 KB.
+template <int BN, int EPI>
+void dgemm_launch(int S, int tiles, hipStream_t st, const at::Tensor& x, const at::Tensor& w, int M, int N, int K,
+                  bf16* out, int64_t ldo, float* part, int F, unsigned* tickets, float* xchg, int* err) {
+  constexpr int XS = BN == 128 ? 3 : 2, WS = BN == 128 ? 4 : 3;
+  dgemm_kernel<BN, XS, WS, EPI><<<dim3(tiles * S), 512, 0, st>>>((const bf16*)x.data_ptr(), x.stride(0),
+                                                                 (const bf16*)w.data_ptr(), M, N, K, S, out, ldo,
+                                                                 part, F, tickets, xchg, err);
+}
+
+void check_xw(const at::Tensor& x, const at::Tensor& w) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16,
+              "decode_gemm: bf16 GPU tensors");
+  TORCH_CHECK(x.device() == w.device(), "decode_gemm: tensors on different devices");
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && x.stride(0) % 8 == 0, "x must be [M, K] with unit column stride");
+  TORCH_CHECK(w.dim() == 2 && w.is_contiguous() && w.size(1) == x.size(1), "w must be contiguous [N, K]");
+  TORCH_CHECK(x.size(1) % BK == 0, "K must be a multiple of 64");
+  TORCH_CHECK(x.size(0) >= 1 && x.size(0) <= BM, "decode_gemm: 1 <= M <= 256");
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(x.data_ptr()) & 15) == 0 && (reinterpret_cast<uintptr_t>(w.data_ptr()) & 15) == 0,
+              "decode_gemm: x and w must be 16-byte aligned (LDS-DMA rows)");
+}
+
+int pick_bn(int N) {
+  static const int env = env_int("LS_DGEMM_BN", 0);
+  if (env == 128 || env == 256) return N % env == 0 ? env : 128;
+  return 128;
+}
+
+}  // namespace
+
+// Shapes: K % 64 == 0, N % 128 == 0; silu: the fused [2F, K] gate_up weight, F % 128 == 0.
+bool decode_gemm_supported(const at::Tensor& w, bool silu) {
+  if (w.dim() != 2 || w.scalar_type() != at::kBFloat16 || !w.is_contiguous() || w.size(1) % BK != 0) return false;
+  return silu ? (w.size(0) % 256 == 0) : (w.size(0) % 128 == 0);
+}
+
+// Workspace bytes a decode_gemm call needs (f32 partials / exchange) -- callers that
+// capture graphs allocate it once.
+int64_t decode_gemm_workspace(int64_t M, int64_t N, int64_t K, bool silu) {
+  if (silu) return (N / 256) * (int64_t)BM * 256 * 4;
+  const int bn = pick_bn((int)N);
+  const int S = pick_split((int)(N / bn), (int)K, 4);
+  return S > 1 ? (int64_t)S * M * N * 4 : 0;
+}
+
+// out[M, N] = x . w^T  (mode 0), or with the split-K reduction fused with
+// residual += x . w^T; out = rmsnorm(residual) * norm_w  (mode 1).
+// bn / splits: 0 = automatic (tests and tools/dgemm_bench.py force them).
+void decode_gemm(at::Tensor out, at::Tensor x, at::Tensor w, at::Tensor workspace, c10::optional<at::Tensor> residual,
+                 c10::optional<at::Tensor> norm_w, double eps, int64_t bn_force, int64_t splits_force) {
+  check_xw(x, w);
+  const int M = (int)x.size(0), K = (int)x.size(1), N = (int)w.size(0);
+  TORCH_CHECK(N % 128 == 0, "decode_gemm: N % 128 == 0");
+  TORCH_CHECK(out.scalar_type() == at::kBFloat16 && out.size(0) == M && out.size(1) == N && out.stride(1) == 1);
+  const bool norm = residual.has_value();
+  TORCH_CHECK(!norm || (norm_w.has_value() && residual->is_contiguous() && residual->numel() == (int64_t)M * N &&
+                        out.is_contiguous() && norm_w->numel() == N), "decode_gemm: residual/norm shapes");
+  const int bn = (bn_force == 128 || bn_force == 256) && N % bn_force == 0 ? (int)bn_force : pick_bn(N);
+  const int tiles = N / bn;
+  const int S = splits_force > 0 ? (int)std::min<int64_t>(splits_force, K / BK) : pick_split(tiles, K, 4);
+  auto st = at::hip::getCurrentHIPStream();
+  if (S == 1 && !norm) {
+    if (bn == 256)
+      dgemm_launch<256, EPI_STORE>(1, tiles, st, x, w, M, N, K, (bf16*)out.data_ptr(), out.stride(0), nullptr, 0,
+                                   nullptr, nullptr, nullptr);
+    else
+      dgemm_launch<128, EPI_STORE>(1, tiles, st, x, w, M, N, K, (bf16*)out.data_ptr(), out.stride(0), nullptr, 0,
+                                   nullptr, nullptr, nullptr);
+    return;
+  }
+  TORCH_CHECK(workspace.scalar_type() == at::kFloat && workspace.is_cuda() &&
+              workspace.numel() >= (int64_t)S * M * N, "decode_gemm: workspace too small");
+  float* part = workspace.data_ptr<float>();
+  if (bn == 256)
+    dgemm_launch<256, EPI_PARTIAL>(S, tiles, st, x, w, M, N, K, nullptr, 0, part, 0, nullptr, nullptr, nullptr);
+  else
+    dgemm_launch<128, EPI_PARTIAL>(S, tiles, st, x, w, M, N, K, nullptr, 0, part, 0, nullptr, nullptr, nullptr);
+  if (norm)
+    splitk_add_rmsnorm_launch(part, S, M, N, (bf16*)residual->data_ptr(), (const bf16*)norm_w->data_ptr(), (float)eps,
+                              (bf16*)out.data_ptr(), st);
+  else
+    splitk_reduce_launch(part, S, M, N, (bf16*)out.data_ptr(), out.stride(0), st);
+}
+
+// out[M, F] = silu(x . w[:F]^T) * (x . w[F:]^T).  tickets: int32 [2 * (F / 128)] zeros
+// once at allocation (monotonic, never reset); err: int32 [1].
+// splits: 0 = automatic (2 with the in-launch combine), 1 = one launch over full K.
+void decode_gemm_silu(at::Tensor out, at::Tensor x, at::Tensor w, at::Tensor workspace, at::Tensor tickets,
+                      at::Tensor err, int64_t splits) {
+  check_xw(x, w);
+  const int M = (int)x.size(0), K = (int)x.size(1), F = (int)(w.size(0) / 2);
+  TORCH_CHECK(decode_gemm_supported(w, true), "decode_gemm_silu: gate_up rows must be 2F with F % 128 == 0");
+  TORCH_CHECK(out.scalar_type() == at::kBFloat16 && out.size(0) == M && out.size(1) == F && out.stride(1) == 1);
+  const int tiles = F / 128;
+  static const int split_env = env_int("LS_DGEMM_SILU_SPLIT", 2);
+  const int sp = splits > 0 ? (int)splits : split_env;
+  auto st = at::hip::getCurrentHIPStream();
+  if (sp != 2 || K / BK < 8) {
+    // one launch, no combine: 128-column tiles (64 gate + 64 up), full K
+    dgemm_launch<128, EPI_SILU>(1, F / 64, st, x, w, M, 2 * F, K, (bf16*)out.data_ptr(), out.stride(0), nullptr, F,
+                           nullptr, nullptr, nullptr);
+    return;
+  }
+  TORCH_CHECK(tickets.scalar_type() == at::kInt && tickets.is_cuda() && tickets.numel() >= 2 * tiles,
+              "decode_gemm_silu: tickets [2 * F / 128] int32");
+  TORCH_CHECK(err.scalar_type() == at::kInt && err.is_cuda() && err.numel() >= 1);
+  TORCH_CHECK(workspace.scalar_type() == at::kFloat && workspace.is_cuda() &&
+              workspace.numel() >= (int64_t)tiles * BM * 256, "decode_gemm_silu: workspace too small");
+  dgemm_launch<256, EPI_SILU2>(2, tiles, st, x, w, M, 2 * F, K, (bf16*)out.data_ptr(), out.stride(0), nullptr, F,
+                          reinterpret_cast<unsigned*>(tickets.data_ptr<int>()), workspace.data_ptr<float>(),
+                          err.data_ptr<int>());
+}
+
+// Timing-only ablation builds of the plain split-K GEMM (EPI_PARTIAL, BN = 128): abl bits
+// as documented at dgemm_kernel.  Results are garbage by design.
+void decode_gemm_ablate(at::Tensor x, at::Tensor w, at::Tensor workspace, int64_t abl, int64_t splits) {
+  check_xw(x, w);
+  const int M = (int)x.size(0), K = (int)x.size(1), N = (int)w.size(0);
+  const int tiles = N / 128;
+  const int S = splits > 0 ? (int)splits : pick_split(tiles, K, 4);
+  TORCH_CHECK(workspace.numel() >= (int64_t)S * M * N);
+  auto st = at::hip::getCurrentHIPStream();
+  const dim3 grid(tiles * S);
+  float* part = workspace.data_ptr<float>();
+#define A_(V)                                                                                          \
+  case V:                                                                                              \
+    dgemm_kernel<128, 3, 4, EPI_PARTIAL, V><<<grid, 512, 0, st>>>((const bf16*)x.data_ptr(), x.stride(0), \
+                                                                  (const bf16*)w.data_ptr(), M, N, K, S,  \
+                                                                  nullptr, 0, part, 0, nullptr, nullptr, \
+                                                                  nullptr);                              \
+    break;
+  switch (abl) {
+    A_(0) A_(1) A_(2) A_(3) A_(4) A_(5) A_(7) A_(8) A_(9) A_(11)
+    default: TORCH_CHECK(false, "unsupported ablation ", abl);
+  }
+#undef A_
+}

@@ -488,3 +488,21 @@ void skinny_gemm_add_rmsnorm(at::Tensor out, at::Tensor x, at::Tensor w, at::Ten
   else RED(8);
 #undef RED
 }
+
+// Launch helpers for the split-K reductions, shared with gemm_decode.hip.
+void splitk_reduce_launch(const float* part, int S, int M, int N, bf16* out, int64_t ldo, hipStream_t st) {
+  const int64_t total4 = (int64_t)M * N / 4;
+  splitk_reduce_kernel<<<(int)((total4 + 255) / 256), 256, 0, st>>>(part, S, M, N, out, ldo);
+}
+
+void splitk_add_rmsnorm_launch(const float* part, int S, int M, int N, bf16* residual, const bf16* norm_w, float eps,
+                               bf16* out, hipStream_t st) {
+  const int nv = (N / 8 + 255) / 256;
+  TORCH_CHECK(nv <= 8, "splitk_add_rmsnorm: N <= 16384");
+#define RED(NV) splitk_add_rmsnorm_kernel<NV><<<M, 256, 0, st>>>(part, S, M, N, residual, norm_w, eps, out)
+  if (nv <= 1) RED(1);
+  else if (nv <= 2) RED(2);
+  else if (nv <= 4) RED(4);
+  else RED(8);
+#undef RED
+}

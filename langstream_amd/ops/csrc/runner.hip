@@ -103,6 +103,13 @@ void skinny_gemm_add_rmsnorm(at::Tensor out, at::Tensor x, at::Tensor w, at::Ten
                              double eps);
 void gemm_prefill(at::Tensor out, at::Tensor x, at::Tensor w, bool silu);
 bool gemm_prefill_supported(const at::Tensor& w, bool silu);
+bool decode_gemm_supported(const at::Tensor& w, bool silu);
+int64_t decode_gemm_workspace(int64_t M, int64_t N, int64_t K, bool silu);
+void decode_gemm(at::Tensor out, at::Tensor x, at::Tensor w, at::Tensor workspace, c10::optional<at::Tensor> residual,
+                 c10::optional<at::Tensor> norm_w, double eps, int64_t bn_force, int64_t splits_force);
+void decode_gemm_silu(at::Tensor out, at::Tensor x, at::Tensor w, at::Tensor workspace, at::Tensor tickets,
+                      at::Tensor err, int64_t splits);
+const int* oneshot_allreduce_err(const std::shared_ptr<OneShotAllReduce>& ar);
 
 #define HIP_OK(x)                                                                  \
   do {                                                                             \
@@ -137,6 +144,35 @@ class LlamaRunner {
       oneshot_ = make_oneshot_allreduce(pg_, mx);
       oneshot_max_ = mx;
     }
+    // device status words that must stay 0 (see status_ptrs) and the decode-GEMM
+    // workspace: f32 split-K partials / the gate_up half exchange, sized once for the
+    // largest decode batch so graph captures never allocate
+    auto dev = embed_.options();
+    status_ = at::zeros({4}, dev.dtype(at::kInt));
+    if (dgemm_enabled()) {
+      int64_t wsz = 1, fmax = 0;
+      for (size_t l = 0; l < L; ++l) {
+        const at::Tensor* ws[3] = {&qkv_w_[l], &o_w_[l], &down_w_[l]};
+        for (auto* w : ws)
+          if (decode_gemm_supported(*w, false))
+            wsz = std::max(wsz, decode_gemm_workspace(kDgemmMaxM, w->size(0), w->size(1), false));
+        if (decode_gemm_supported(gate_up_w_[l], true)) {
+          wsz = std::max(wsz, decode_gemm_workspace(kDgemmMaxM, gate_up_w_[l].size(0), gate_up_w_[l].size(1), true));
+          fmax = std::max(fmax, gate_up_w_[l].size(0) / 2);
+        }
+      }
+      dg_ws_ = at::empty({(wsz + 3) / 4}, dev.dtype(at::kFloat));
+      dg_tickets_ = at::zeros({std::max<int64_t>(2, 2 * (fmax / 128))}, dev.dtype(at::kInt));
+    }
+  }
+
+  // Device int32 words that are 0 unless a step's results are invalid: [0] the gate_up
+  // half-exchange of gemm_decode.hip timed out; the one-shot all-reduce's sticky timeout
+  // word.  The step executor copies them next to every step's results and fails the step.
+  std::vector<const int*> status_ptrs() const {
+    std::vector<const int*> v{status_.data_ptr<int>()};
+    if (oneshot_) v.push_back(oneshot_allreduce_err(oneshot_));
+    return v;
   }
 
   // LM head with f32 OUTPUT straight from the GEMM (hipBLASLt bf16 x bf16 -> f32): a bf16
@@ -232,6 +268,9 @@ class LlamaRunner {
       } else if (sk && T <= 32 && skinny_shape(qkv_w_[l])) {
         qkv = at::empty({T, qkv_w_[l].size(0)}, x.options());
         skinny_gemm(qkv, x, qkv_w_[l]);
+      } else if (dgemm(T, qkv_w_[l], false)) {
+        qkv = at::empty({T, qkv_w_[l].size(0)}, x.options());
+        decode_gemm(qkv, x, qkv_w_[l], dg_ws_, c10::nullopt, c10::nullopt, eps_, 0, 0);
       } else if (pgemm(T, qkv_w_[l], false)) {
         qkv = at::empty({T, qkv_w_[l].size(0)}, x.options());
         gemm_prefill(qkv, x, qkv_w_[l], false);
@@ -258,6 +297,15 @@ class LlamaRunner {
         gemv(o, attn, o_w_[l]);
         all_reduce(o);
         fused_add_rmsnorm(o, residual, post_norm_[l], eps_);
+      } else if (dgemm(T, o_w_[l], false)) {
+        o = at::empty_like(residual);
+        if (!pg_) {
+          decode_gemm(o, attn, o_w_[l], dg_ws_, residual, post_norm_[l], eps_, 0, 0);
+        } else {
+          decode_gemm(o, attn, o_w_[l], dg_ws_, c10::nullopt, c10::nullopt, eps_, 0, 0);
+          all_reduce(o);
+          fused_add_rmsnorm(o, residual, post_norm_[l], eps_);
+        }
       } else if (sk && T <= 192 && skinny_shape(o_w_[l])) {
         o = at::empty_like(residual);
         if (!pg_) {
@@ -281,6 +329,10 @@ class LlamaRunner {
       if (gv && gemv_supported(gate_up_w_[l], true)) {
         a = at::empty({T, gate_up_w_[l].size(0) / 2}, o.options());
         gemv_silu(a, o, gate_up_w_[l]);
+      } else if (dgemm(T, gate_up_w_[l], true)) {
+        // decode batch: SwiGLU in the epilogue after the in-launch combine of the K halves
+        a = at::empty({T, gate_up_w_[l].size(0) / 2}, o.options());
+        decode_gemm_silu(a, o, gate_up_w_[l], dg_ws_, dg_tickets_, status_.narrow(0, 0, 1), 0);
       } else if (pgemm(T, gate_up_w_[l], true)) {
         // prefill: SwiGLU in the GEMM epilogue, the [T, 2F] product never reaches HBM
         a = at::empty({T, gate_up_w_[l].size(0) / 2}, o.options());
@@ -297,6 +349,15 @@ class LlamaRunner {
         gemv(dn, a, down_w_[l]);
         all_reduce(dn);
         fused_add_rmsnorm(dn, residual, nxt, eps_);
+      } else if (dgemm(T, down_w_[l], false)) {
+        dn = at::empty_like(residual);
+        if (!pg_) {
+          decode_gemm(dn, a, down_w_[l], dg_ws_, residual, nxt, eps_, 0, 0);
+        } else {
+          decode_gemm(dn, a, down_w_[l], dg_ws_, c10::nullopt, c10::nullopt, eps_, 0, 0);
+          all_reduce(dn);
+          fused_add_rmsnorm(dn, residual, nxt, eps_);
+        }
       } else if (sk && T >= 48 && T <= 256 && skinny_shape(down_w_[l])) {
         dn = at::empty_like(residual);
         if (!pg_) {
@@ -417,6 +478,25 @@ class LlamaRunner {
   }
   static bool skinny_shape(const at::Tensor& w) { return w.size(0) % 128 == 0 && w.size(1) % 64 == 0; }
 
+  // Decode batches of LS_DGEMM_MIN_T (default 129) .. 256 rows run all four projections
+  // on the 256-row decode GEMM (ops/csrc/gemm_decode.hip) instead of hipBLASLt / the
+  // skinny ring.  LS_DGEMM=0 turns it off (A/B switch).
+  static constexpr int64_t kDgemmMaxM = 256;
+  static bool dgemm_enabled() {
+    static const bool on = [] {
+      const char* e = getenv("LS_DGEMM");
+      return e == nullptr || e[0] != '0';
+    }();
+    return on;
+  }
+  bool dgemm(int64_t T, const at::Tensor& w, bool silu) const {
+    static const int64_t min_t = [] {
+      const char* e = getenv("LS_DGEMM_MIN_T");
+      return e ? (int64_t)atoll(e) : (int64_t)129;
+    }();
+    return dgemm_enabled() && dg_ws_.defined() && T >= min_t && T <= kDgemmMaxM && decode_gemm_supported(w, silu);
+  }
+
   void all_reduce(at::Tensor& t) {
     if (!pg_) return;
     if (oneshot_ && t.scalar_type() == at::kBFloat16 && t.is_contiguous() && t.numel() <= oneshot_max_) {
@@ -431,6 +511,7 @@ class LlamaRunner {
   int64_t oneshot_max_ = 0;
 
   bool f32_head_ = true;
+  at::Tensor status_, dg_ws_, dg_tickets_;
   at::Tensor embed_;
   std::vector<at::Tensor> qkv_w_, o_w_, gate_up_w_, down_w_, in_norm_, post_norm_;
   at::Tensor final_norm_, lm_head_;
@@ -603,7 +684,10 @@ class StepExecutor {
       in_used_.push_back(false);
     }
     arena_ = at::zeros({arena_bytes_}, dev.dtype(at::kByte));
-    hdr_small_ = at::zeros({16}, at::TensorOptions().dtype(at::kInt).pinned_memory(true));
+    status_ptrs_ = r_->status_ptrs();
+    st_host_ = at::zeros({nslots, kStatusWords}, at::TensorOptions().dtype(at::kInt).pinned_memory(true));
+    TORCH_CHECK((int64_t)status_ptrs_.size() <= kStatusWords);
+    hdr_small_ = at::zeros({16 + kStatusWords}, at::TensorOptions().dtype(at::kInt).pinned_memory(true));
     tok_ = at::zeros({maxS_}, dev.dtype(at::kInt));
     lp_ = at::zeros({maxS_}, dev.dtype(at::kFloat));
     ti_ = at::zeros({maxS_ * kMaxTop}, dev.dtype(at::kInt));
@@ -659,6 +743,7 @@ class StepExecutor {
   void wait_out(int64_t i) {
     wait_submitted(i);
     HIP_OK(hipEventSynchronize(out_ev_.at(i)));
+    check_status(st_host_[i].data_ptr<int>());
   }
 
   // One scheduler round trip in a single GIL-released call: launch the step in host
@@ -741,6 +826,7 @@ class StepExecutor {
       broadcast_arena();
       HIP_OK(hipMemcpyAsync(hdr, arena_.data_ptr(), 16 * sizeof(int32_t), hipMemcpyDeviceToHost, stream()));
       HIP_OK(hipStreamSynchronize(stream()));
+      check_status(hdr + 16);   // the previous step's
       const int kind = hdr[H_KIND];
       if (kind == 3) return;
       if (kind == 4) {
@@ -748,6 +834,9 @@ class StepExecutor {
       } else if (kind == 1) {
         validate(hdr);
         run(hdr);
+        // a worker has no result slot: its status words land behind the step and are
+        // checked after the next header's synchronisation (no extra sync per step)
+        copy_status(hdr + 16);
       } else {
         TORCH_CHECK(false, "bad step kind ", kind);
       }
@@ -940,7 +1029,21 @@ class StepExecutor {
                               hipMemcpyDeviceToHost, stream()));
       }
     }
+    copy_status(st_host_[oslot].data_ptr<int>());
     HIP_OK(hipEventRecord(out_ev_[oslot], stream()));
+  }
+
+  // status words (LlamaRunner::status_ptrs) -> pinned host ints, in stream order after the step
+  void copy_status(int* dst) {
+    for (size_t k = 0; k < status_ptrs_.size(); ++k)
+      HIP_OK(hipMemcpyAsync(dst + k, status_ptrs_[k], sizeof(int), hipMemcpyDeviceToHost, stream()));
+  }
+  static void check_status(const int* st) {
+    TORCH_CHECK(st[0] == 0, "decode GEMM: the gate_up K-half exchange timed out (partner workgroup never "
+                "published); this step's results are invalid");
+    for (int k = 1; k < kStatusWords; ++k)
+      TORCH_CHECK(st[k] == 0, "one-shot all-reduce timed out: a tensor-parallel peer never arrived; this step's "
+                  "results are invalid");
   }
 
   // Neutral inputs for graph warm-up: no KV writes (slot -1), empty contexts, no feedback.
@@ -992,6 +1095,9 @@ class StepExecutor {
   bool use_graphs_;
   std::vector<at::Tensor> host_, out_;
   std::vector<hipEvent_t> in_ev_, out_ev_;
+  static constexpr int kStatusWords = 4;
+  std::vector<const int*> status_ptrs_;
+  at::Tensor st_host_;
   std::vector<bool> in_used_;
   at::Tensor arena_, hdr_small_, tok_, lp_, ti_, tl_, ws_, last_logits_;
   at::Tensor tp_stats_, tp_stats_all_, tp_hist_, tp_cand_, tp_cand_all_;

@@ -84,3 +84,22 @@ def test_hs256_roundtrip_and_provider_cache():
     assert PROVIDER_CACHE.get("jwt", {"secret-key": "other"}) is not p1
     res = p1.authenticate(_Ctx(tok))
     assert res.authenticated and res.principal_values["subject"] == "u1"
+
+
+@pytest.mark.parametrize("jku", ["https://issuer.example.evil.com/jwks", "https://issuer.example@evil.com/jwks",
+                                 "https://evil.com/issuer.example/jwks", "https://evil.com/?h=issuer.example"])
+def test_jku_allowlist_is_a_host_fullmatch_not_a_prefix(fetched, jku):
+    """the allowlist used to admit any jku whose URL string started with an
+    entry; now it is a regex full-matched against the parsed host only."""
+    for allow in ("https://issuer.example", "issuer.example", r"issuer\.example"):
+        p = JwtAuthProvider({"jwks-uri": "https://issuer.example/jwks", "jwks-hosts-allowlist": allow})
+        res = p.authenticate(_Ctx(_token({"alg": "RS256", "jku": jku}, {"sub": "a"})))
+        assert not res.authenticated and "Untrusted" in res.reason, (allow, jku)
+    assert fetched == []  # the attacker's JWKS is never fetched
+
+
+def test_jku_allowlist_regex_matches_subdomains(fetched):
+    p = JwtAuthProvider({"jwks-uri": "https://issuer.example.com/jwks", "jwks-hosts-allowlist": r".*\.example\.com"})
+    assert p._trusted_uri({"jku": "https://keys.example.com/jwks"}) == "https://keys.example.com/jwks"
+    with pytest.raises(JwtError):
+        p._trusted_uri({"jku": "https://keys.example.com.evil.io/jwks"})

@@ -72,6 +72,26 @@ def test_oneshot_allreduce_protocol_simulated_ranks(W):
     assert (outs[0].float() - want).abs().max() <= 0.02 * want.abs().max()
 
 
+@pytest.mark.parametrize("W,stall", [(2, 1), (4, 0)])
+def test_oneshot_allreduce_stalled_rank_fails_loudly(W, stall):
+    """A rank that never publishes its flags (a hung peer): every bounded wait that
+    involves it times out, sets the sticky error word and writes NaN -- never a sum over
+    peer buffers that may not have been written.  (The stalled rank also waits on its own
+    missing flag, so every rank reports the error.)"""
+    from langstream_amd import ops
+    torch.manual_seed(W + 10)
+    n = 64 * 1024 + 3
+    ins = [torch.randn(n, device="cuda").to(torch.bfloat16) for _ in range(W)]
+    res = ops.hip().oneshot_allreduce_sim(ins, 1, stall)
+    outs, errs = res[:W], res[W].cpu()
+    for w in range(W):
+        assert int(errs[w]) == 1
+        assert torch.isnan(outs[w].float()).all()
+    # the same buffers with no stall afterwards: a fresh protocol run is clean again
+    res = ops.hip().oneshot_allreduce_sim(ins, 2)
+    assert int(res[W].sum()) == 0
+
+
 def test_oneshot_allreduce_world1_rccl(rccl_world1):
     """The multi-process form over a real RCCL group (IPC handle exchange by all-gather;
     at world 1 the only buffer is the rank's own)."""

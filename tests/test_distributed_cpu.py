@@ -309,3 +309,55 @@ def _allgather_bytes_worker(rank, world, port, q):
 def test_sharded_knn_header_allgather_slot_and_overflow():
     lens, r2 = _spawn(_allgather_bytes_worker)
     assert lens == [10, 5000] and r2 == [b"", b"xyz"]
+
+
+def _sharded_knn_fail_worker(rank, world, port, q):
+    """Rank 1's local search raises in the first round: its own requests fail with that
+    error, rank 0's requests still complete (with rank 0's rows), nobody hangs, and the
+    next round is healthy on both ranks (identical collective sequence)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from langstream_amd.engine import dist_knn
+        from langstream_amd.engine.vector_store import VectorStoreRegistry
+        vecs, queries = _knn_corpus()
+        rows = [i for i in range(vecs.shape[0]) if i % world == rank]
+        st = VectorStoreRegistry.get("docs", 48, device="cpu")
+        st.upsert([f"d{i}" for i in rows], vecs[rows].tolist(), [{"owner": rank} for i in rows])
+        orig = st.topk_rows
+        calls = {"n": 0}
+        if rank == 1:
+            def boom(*a, **k):
+                calls["n"] += 1
+                if calls["n"] == 1:
+                    raise MemoryError("simulated OOM in the kNN kernel")
+                return orig(*a, **k)
+            st.topk_rows = boom
+        svc = dist_knn.start(device="cpu")
+        dist.barrier()
+        f1 = svc.search("docs", queries[rank:rank + 1].tolist(), 5)
+        out = {}
+        try:
+            r = f1.result(60)[0]
+            out["first"] = ("ok", sorted({d["owner"] for d in r}), len(r))
+        except Exception as e:  # noqa: BLE001
+            out["first"] = ("err", type(e).__name__)
+        dist.barrier()
+        r2 = svc.search("docs", queries[rank:rank + 1].tolist(), 5).result(60)[0]
+        out["second"] = ("ok", sorted({d["owner"] for d in r2}), len(r2))
+        gathered = [None] * world
+        dist.all_gather_object(gathered, out)
+        dist_knn.stop()
+        VectorStoreRegistry.reset()
+        if rank == 0:
+            q.put(gathered)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_knn_local_failure_keeps_collectives_in_step():
+    g = _spawn(_sharded_knn_fail_worker)
+    assert g[1]["first"] == ("err", "MemoryError")
+    assert g[0]["first"][0] == "ok" and g[0]["first"][2] == 5
+    for r in range(2):
+        assert g[r]["second"] == ("ok", [0, 1], 5)

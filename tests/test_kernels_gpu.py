@@ -707,3 +707,67 @@ def test_vocab_parallel_sampling_matches_single_gpu_sampler(W):
     assert (lp.cpu() - lp2.cpu()).abs().max() < 1e-4
     assert torch.equal(ti.cpu(), ti2.view(R, n_top).cpu())
     assert (tl.cpu() - tl2.view(R, n_top).cpu()).abs().max() < 1e-4
+
+
+# ------------------------------------------------------------------ gemm_decode.hip
+# Exact Llama-3-8B decode shapes (M = batch rows) and the Llama-3-70B TP=8 shard shapes,
+# every tile width / split count the dispatcher can pick, against fp32.
+_DG_SHAPES = [("qkv8b", 6144, 4096), ("o8b", 4096, 4096), ("down8b", 4096, 14336),
+              ("qkv70b_tp8", 1280, 8192), ("o70b_tp8", 8192, 1024), ("down70b_tp8", 8192, 3584)]
+
+
+def _dg_ws(M, N):
+    return torch.empty(64 * M * N + 4 * 256 * 256, device=DEV, dtype=torch.float32)
+
+
+@pytest.mark.parametrize("M", [129, 200, 256])
+@pytest.mark.parametrize("name,N,K", _DG_SHAPES)
+@pytest.mark.parametrize("bn,splits", [(0, 0), (128, 1), (128, 5), (256, 3)])
+def test_decode_gemm(M, name, N, K, bn, splits):
+    if bn == 256 and N % 256:
+        pytest.skip("N not a multiple of 256")
+    torch.manual_seed(M + N + K)
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=DEV) / K ** 0.5).to(torch.bfloat16)
+    out = torch.full((M, N), float("nan"), device=DEV, dtype=torch.bfloat16)
+    assert ops.hip().decode_gemm_supported(w, False)
+    ops.hip().decode_gemm(out, x, w, _dg_ws(M, N), None, None, 1e-5, bn, splits)
+    _close(out, x.float().cpu() @ w.float().cpu().t(), 0.02, 0.02, name)
+
+
+@pytest.mark.parametrize("M", [129, 256])
+@pytest.mark.parametrize("name,N,K", [("o8b", 4096, 4096), ("down8b", 4096, 14336), ("o70b_tp8", 8192, 1024)])
+def test_decode_gemm_add_rmsnorm(M, name, N, K):
+    torch.manual_seed(M + K)
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=DEV) / K ** 0.5).to(torch.bfloat16)
+    res = torch.randn(M, N, device=DEV).to(torch.bfloat16)
+    g = (1 + 0.1 * torch.randn(N, device=DEV)).to(torch.bfloat16)
+    res_exp = res.float().cpu() + x.float().cpu() @ w.float().cpu().t()
+    out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    ops.hip().decode_gemm(out, x, w, _dg_ws(M, N), res, g, 1e-5)
+    _close(res, res_exp, 0.03, 0.03, "residual")
+    rb = res_exp.to(torch.bfloat16).float()
+    exp = rb * torch.rsqrt(rb.pow(2).mean(-1, keepdim=True) + 1e-5) * g.float().cpu()
+    _close(out, exp, 0.05, 0.05, "normed")
+
+
+@pytest.mark.parametrize("M", [129, 256])
+@pytest.mark.parametrize("F,K,splits", [(14336, 4096, 2), (14336, 4096, 1), (3584, 8192, 2), (384, 1024, 2)])
+def test_decode_gemm_silu(M, F, K, splits):
+    """gate_up + SwiGLU: the 2-way K split with the in-launch combine (ticket parity,
+    release/acquire hand-off) and the single-launch form; repeated calls exercise the
+    monotonic tickets (no per-call reset)."""
+    torch.manual_seed(M + F)
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(2 * F, K, device=DEV) / K ** 0.5).to(torch.bfloat16)
+    tickets = torch.zeros(2 * (F // 128), device=DEV, dtype=torch.int32)
+    err = torch.zeros(1, device=DEV, dtype=torch.int32)
+    ws = torch.empty((F // 128) * 256 * 256, device=DEV, dtype=torch.float32)
+    gu = x.float().cpu() @ w.float().cpu().t()
+    exp = torch.nn.functional.silu(gu[:, :F]) * gu[:, F:]
+    for _ in range(3):
+        out = torch.full((M, F), float("nan"), device=DEV, dtype=torch.bfloat16)
+        ops.hip().decode_gemm_silu(out, x, w, ws, tickets, err, splits)
+        _close(out, exp, 0.02, 0.02)
+    assert err.item() == 0

@@ -184,3 +184,40 @@ def test_dead_member_partitions_are_reassigned_and_redelivered(logname):
 def test_registry_type_shm(logname):
     rt = TopicConnectionsRuntimeRegistry.get(StreamingCluster("shm", {"name": logname, "size-mb": 64}))
     assert isinstance(rt, ShmTopicConnectionsRuntime)
+
+
+def test_retention_overtaking_an_unacked_consumer_does_not_freeze_commits(logname):
+    """with retention-messages, head blocks are dropped even when a group has
+    not committed them.  The lagging member must move its committed offset (and the
+    group's published one) up to the first stored offset, or the contiguous-prefix
+    commit freezes below offsets that can never be acked again."""
+    rt = _rt(logname)
+    rt.log.create_topic("r", 1, 200)                  # keep ~200 messages
+    c = rt.create_consumer("ag", None, {"topic": "r", "max.poll.records": 5})
+    c.start()
+    prod = rt.create_producer("a", None, {"topic": "r"})
+    blob = "y" * 2000
+    for i in range(10):
+        prod.write(SimpleRecord.of(None, f"{i}:" + blob)).result(5)
+    first = c.read()                                  # delivered, never acked
+    assert first
+    for i in range(10, 3000):                          # retention drops the head past them
+        prod.write(SimpleRecord.of(None, f"{i}:" + blob)).result(5)
+    base = rt.log.begin_offsets("r")[0]
+    assert base > 10
+    seen = 0
+    for _ in range(2000):
+        recs = c.read()
+        if not recs:
+            break
+        c.commit(recs)
+        seen += len(recs)
+    committed = rt.log.committed("r", "langstream-agent-ag")[0]
+    assert committed == rt.log.end_offsets("r")[0] == 3000
+    assert rt.log.lag("r", "langstream-agent-ag") in (0, [0], {0: 0}) or sum(
+        rt.log.lag("r", "langstream-agent-ag")) == 0
+    # a fresh member of the group starts at the committed end, not at stale offsets
+    c.close()
+    c2 = rt.create_consumer("ag", None, {"topic": "r"})
+    c2.start()
+    assert c2.read() == []

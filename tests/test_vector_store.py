@@ -10,6 +10,7 @@ import textwrap
 import time
 import uuid
 
+import numpy as np
 import pytest
 import torch
 
@@ -196,3 +197,101 @@ def test_kill_restart_replays_committed_offsets_without_loss(tmp_path):
         VectorStoreRegistry.reset()
         VectorStoreRegistry.persist_dir = None
         unlink_shmlog(logname, size_mb=64)
+
+
+def test_torn_wal_tail_is_truncated_before_new_writes(tmp_path):
+    """a crash mid-append leaves a torn entry; the next process must cut the
+    log there BEFORE appending, or the entries written after the restart are parsed
+    across the garbage on the restart after that."""
+    d = str(tmp_path / "coll")
+    s = VectorStore(4, device="cpu", dtype=torch.float32, persist_dir=d, name="c")
+    s.upsert(["a", "b"], [[1, 0, 0, 0], [0, 1, 0, 0]], [{"t": "a"}, {"t": "b"}])
+    s.close()
+    with open(os.path.join(d, "wal.log"), "ab") as f:     # torn write: length says 500 bytes
+        f.write((500).to_bytes(4, "little") + b"\x93\xa1u")
+    r = VectorStore(4, device="cpu", dtype=torch.float32, persist_dir=d, name="c")
+    assert len(r) == 2
+    r.upsert(["c"], [[0, 0, 1, 0]], [{"t": "c"}])          # acknowledged after the restart
+    r.delete(["a"])
+    r.close()
+    q = VectorStore(4, device="cpu", dtype=torch.float32, persist_dir=d, name="c")
+    assert len(q) == 2 and q.get("c") == {"t": "c"} and q.get("a") is None and q.get("b") == {"t": "b"}
+
+
+def test_snapshot_swap_is_atomic_and_replay_idempotent(tmp_path):
+    """The snapshot is one file swapped by one rename: a crash while writing it leaves the
+    previous snapshot (plus a stray temp file) intact; a crash after the swap but before
+    the WAL reset replays entries the snapshot already holds, harmlessly."""
+    d = str(tmp_path / "coll")
+    s = VectorStore(4, device="cpu", dtype=torch.float32, persist_dir=d, name="c")
+    s.upsert(list(range(6)), [[i, 1, 0, 0] for i in range(6)], [{"i": i} for i in range(6)])
+    s.snapshot()
+    s.upsert([6, 7], [[6, 1, 0, 0], [7, 1, 0, 0]], [{"i": 6}, {"i": 7}])
+    s.delete([0])
+    wal = open(os.path.join(d, "wal.log"), "rb").read()
+    s.snapshot()
+    s.close()
+    # crash after the swap, before the WAL reset: the old WAL comes back
+    open(os.path.join(d, "wal.log"), "wb").write(wal)
+    # and a half-written next snapshot lies around
+    open(os.path.join(d, "snapshot.lsv.tmp"), "wb").write(b"LSVS0001" + b"\xff" * 40)
+    r = VectorStore(4, device="cpu", dtype=torch.float32, persist_dir=d, name="c")
+    assert len(r) == 7 and r.get(0) is None and r.get(7) == {"i": 7}
+    assert sorted(r._ids) == list(range(1, 8))
+
+
+def test_legacy_two_file_snapshot_still_loads(tmp_path):
+    import json as _json
+    d = tmp_path / "coll"
+    d.mkdir()
+    _json.dump({"dim": 4, "dtype": "float32", "ids": ["x"], "meta": [{"t": "x"}]}, open(d / "snapshot.json", "w"))
+    np.asarray([[1, 0, 0, 0]], dtype=np.float32).tofile(d / "snapshot.vec")
+    r = VectorStore(4, device="cpu", dtype=torch.float32, persist_dir=str(d), name="c")
+    assert r.get("x") == {"t": "x"}
+    r.snapshot()
+    assert not (d / "snapshot.json").exists() and (d / "snapshot.lsv").exists()
+    r.close()
+    assert VectorStore(4, device="cpu", dtype=torch.float32, persist_dir=str(d), name="c").get("x") == {"t": "x"}
+
+
+def test_vector_sink_is_durable_by_default_in_its_state_dir(tmp_path):
+    """Zero config: a local vector-db-sink keeps its WAL in the agent's persistent state
+    directory, and the planner gives it a disk (the pod's PVC)."""
+    from langstream_amd.agents.vector import VectorDBSinkAgent
+    from langstream_amd.api.agent import AgentContext
+    from langstream_amd.api.record import SimpleRecord
+    VectorStoreRegistry.reset()
+    VectorStoreRegistry.persist_dir = None
+    try:
+        def agent():
+            a = VectorDBSinkAgent()
+            a.set_metadata("sink1", "vector-db-sink", 0) if hasattr(a, "set_metadata") else None
+            a.init({"datasource": {"service": "local"}, "collection-name": "durable",
+                    "fields": [{"name": "id", "expression": "key"}, {"name": "vector", "expression": "value.vec"},
+                               {"name": "text", "expression": "value.text"}]})
+            a.set_context(AgentContext(agent_id="sink1", global_agent_id="app-sink1",
+                                       persistent_state_directory=str(tmp_path)))
+            a.start()
+            return a
+        a = agent()
+        for i in range(5):
+            a.write(SimpleRecord.of(f"k{i}", {"vec": [1.0, float(i), 0.0], "text": f"t{i}"})).result(10)
+        a.close()
+        assert VectorStoreRegistry.persist_dir.startswith(str(tmp_path))
+        VectorStoreRegistry.reset()                  # pod restart: in-memory state gone
+        VectorStoreRegistry.persist_dir = None
+        agent()
+        s = VectorStoreRegistry.get("durable", device="cpu")
+        assert len(s) == 5 and s.get("k3") == {"text": "t3"}
+    finally:
+        VectorStoreRegistry.reset()
+        VectorStoreRegistry.persist_dir = None
+
+
+def test_planner_gives_local_vector_sinks_a_disk():
+    from langstream_amd.core.catalog import _vector_sink_disks
+    from langstream_amd.api.model import AgentConfiguration
+    assert _vector_sink_disks(AgentConfiguration(id="w", type="vector-db-sink",
+                                                 configuration={"datasource": "LocalVectors"}))
+    assert not _vector_sink_disks(AgentConfiguration(id="w", type="vector-db-sink",
+                                                     configuration={"datasource": {"service": "opensearch"}}))

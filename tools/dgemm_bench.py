@@ -1,0 +1,136 @@
+"""Decode-step GEMMs at M = 129..256: hipBLASLt (F.linear + separate epilogue kernels) vs
+the skinny ring (gemm_skinny.hip) vs the 256-row decode GEMM (gemm_decode.hip) with
+forced tile widths / split counts.
+
+Weights rotate through a ring of copies larger than the 256 MB Infinity Cache, as in a
+decode step that streams all 32 layers.  Every variant is checked against an fp32
+reference before it is timed, and all variants are timed interleaved in ONE process
+(rounds x variants, median reported).
+
+usage (GPU): python tools/dgemm_bench.py [--ms 256] [--only qkv,o,gate_up,down]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+import torch.nn.functional as F  # noqa: E402
+
+from langstream_amd import ops  # noqa: E402
+
+
+def time_once(fn, n, iters):
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for i in range(iters):
+        fn(i % n)
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) * 1000.0 / iters
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ms", default="256")
+    ap.add_argument("--only", default="")
+    ap.add_argument("--rounds", type=int, default=7)
+    ap.add_argument("--iters", type=int, default=30)
+    ap.add_argument("--hidden", type=int, default=4096)
+    ap.add_argument("--ffn", type=int, default=14336)
+    ap.add_argument("--qkv", type=int, default=6144)
+    ap.add_argument("--ablate", action="store_true",
+                    help="time the split-K kernel's ablation builds (no MFMA / no LDS reads / no DMA)")
+    a = ap.parse_args()
+    H, Fi = a.hidden, a.ffn
+    dev, bf = "cuda", torch.bfloat16
+    h = ops.hip()
+    shapes = {"qkv": (a.qkv, H), "o": (H, H), "gate_up": (2 * Fi, H), "down": (H, Fi)}
+    tickets = torch.zeros(2 * (Fi // 128) + 2, device=dev, dtype=torch.int32)
+    err = torch.zeros(1, device=dev, dtype=torch.int32)
+    for name, (N, K) in shapes.items():
+        if a.only and name not in a.only.split(","):
+            continue
+        ring = max(2, int(1.0e9 // (N * K * 2)))
+        ws = [(torch.randn(N, K, device=dev) * 0.02).to(bf) for _ in range(ring)]
+        for M in (int(v) for v in a.ms.split(",")):
+            x = torch.randn(M, K, device=dev).to(bf)
+            res0 = torch.randn(M, N, device=dev).to(bf)
+            res = res0.clone()
+            g = (torch.rand(N, device=dev) + 0.5).to(bf)
+            wsp = torch.empty(64 * M * N + (N // 256 + 1) * 256 * 256, device=dev, dtype=torch.float32)
+            variants = {}
+            if a.ablate:
+                out = torch.empty(M, N, device=dev, dtype=bf)
+                ref = None
+                for abl, nm in ((0, "full"), (1, "no_mfma"), (2, "no_lds_read"), (3, "dma_only"), (4, "no_dma"),
+                                (8, "no_w_dma"), (9, "no_w_dma_no_mfma"), (7, "barrier_only")):
+                    variants[f"abl{abl}_{nm}"] = lambda i, abl=abl: h.decode_gemm_ablate(x, ws[i], wsp, abl, 0)
+                check = None
+            elif name == "gate_up":
+                out = torch.empty(M, Fi, device=dev, dtype=bf)
+                ref = F.silu(x.float() @ ws[0][:Fi].float().t()) * (x.float() @ ws[0][Fi:].float().t())
+                variants["hipblaslt+silu"] = lambda i: h.silu_and_mul(out, F.linear(x, ws[i]))
+                variants["skinny"] = lambda i: h.skinny_gemm_silu(out, x, ws[i])
+                variants["dgemm_s1"] = lambda i: h.decode_gemm_silu(out, x, ws[i], wsp, tickets, err, 1)
+                variants["dgemm_s2"] = lambda i: h.decode_gemm_silu(out, x, ws[i], wsp, tickets, err, 2)
+                check = lambda: out.float()  # noqa: E731
+            elif name in ("o", "down"):
+                out = torch.empty(M, N, device=dev, dtype=bf)
+                v = res0.float() + x.float() @ ws[0].float().t()
+                vb = v.to(bf).float()
+                ref = vb * torch.rsqrt(vb.pow(2).mean(-1, keepdim=True) + 1e-5) * g.float()
+
+                def base(i):
+                    o = F.linear(x, ws[i])
+                    h.fused_add_rmsnorm(o, res, g, 1e-5)
+                    out.copy_(o)
+                variants["hipblaslt+norm"] = base
+                variants["skinny"] = lambda i: h.skinny_gemm_add_rmsnorm(out, x, ws[i], res, g, 1e-5)
+                for bn in (128, 256):
+                    for sp in (0, 4, 8, 16):
+                        variants[f"dgemm_bn{bn}_s{sp}"] = (
+                            lambda i, bn=bn, sp=sp: h.decode_gemm(out, x, ws[i], wsp, res, g, 1e-5, bn, sp))
+                check = lambda: out.float()  # noqa: E731
+            else:
+                out = torch.empty(M, N, device=dev, dtype=bf)
+                ref = x.float() @ ws[0].float().t()
+                variants["hipblaslt"] = lambda i: out.copy_(F.linear(x, ws[i]))
+                variants["skinny"] = lambda i: h.skinny_gemm(out, x, ws[i])
+                for bn in (128, 256):
+                    for sp in (0, 2, 4, 6, 8):
+                        variants[f"dgemm_bn{bn}_s{sp}"] = (
+                            lambda i, bn=bn, sp=sp: h.decode_gemm(out, x, ws[i], wsp, None, None, 1e-5, bn, sp))
+                check = lambda: out.float()  # noqa: E731
+            # correctness of every variant on weight copy 0 (residual reset each time)
+            errs = {}
+            for k, fn in (variants.items() if check is not None else ()):
+                res.copy_(res0)
+                out.zero_()
+                fn(0)
+                torch.cuda.synchronize()
+                d = (check() - ref).abs().max().item()
+                errs[k] = round(d / (ref.abs().max().item() + 1e-6), 4)
+            times = {k: [] for k in variants}
+            for k, fn in variants.items():   # warm
+                time_once(fn, ring, 3)
+            for _ in range(a.rounds):
+                for k, fn in variants.items():
+                    times[k].append(time_once(fn, ring, a.iters))
+            rec = {"gemm": name, "M": M, "N": N, "K": K,
+                   "us": {k: round(statistics.median(t), 1) for k, t in times.items()},
+                   "rel_err": errs, "err_flag": int(err.item())}
+            best = min(rec["us"], key=rec["us"].get)
+            rec["best"] = best
+            rec["weight_TBps_best"] = round(N * K * 2 / (rec["us"][best] * 1e-6) / 1e12, 2)
+            print(json.dumps(rec), flush=True)
+            del wsp
+
+
+if __name__ == "__main__":
+    main()
