@@ -313,16 +313,72 @@ class OllamaService(CompletionsService, EmbeddingsService):
 
 
 class HuggingFaceAPIService(EmbeddingsService, CompletionsService):
-    """HF inference REST (``provider: api``); ``provider: local`` maps to the GPU encoder."""
+    """HF inference REST (``provider: api``); ``provider: local`` maps to the GPU encoder.
 
-    def __init__(self, cfg: Dict[str, Any], model: Optional[str] = None):
+    Embeddings (HuggingFaceRestEmbeddingService.java:42-190): POST
+    ``{api-url}{model}`` (default ``https://api-inference.huggingface.co/pipeline/
+    feature-extraction/``) with ``{"inputs": texts, "options": options}`` (options default
+    ``{"wait_for_model": "true"}``, HuggingFaceProvider.java:135-139), Bearer
+    ``access-key``; a non-200 answer fails the batch.
+    Completions (HuggingFaceProvider.java:157-199): POST ``{inference-url}/models/{model}``
+    (default ``https://api-inference.huggingface.co``) with the JSON array of the message
+    contents / prompts; the answer is a list of ``{score, token_str, sequence}``.  Text
+    completions return ``[0].sequence``; chat completions return one choice per answer
+    bean, the first of which is the completion.  The API is not streamed: the chunk
+    consumer gets the whole answer as the last chunk."""
+
+    EMBED_URL = "https://api-inference.huggingface.co/pipeline/feature-extraction/"
+    INFER_URL = "https://api-inference.huggingface.co"
+
+    def __init__(self, cfg: Dict[str, Any], model: Optional[str] = None, options: Optional[Dict[str, Any]] = None):
         self.cfg = cfg
         self.model = model
-        self.url = cfg.get("inference-url", "https://api-inference.huggingface.co/pipeline/feature-extraction")
+        self.embed_url = cfg.get("api-url") or self.EMBED_URL
+        self.infer_url = (cfg.get("inference-url") or self.INFER_URL).rstrip("/")
+        self.options = options or {"wait_for_model": "true"}
+
+    def _headers(self) -> Dict[str, str]:
+        return {"Authorization": f"Bearer {self.cfg.get('access-key', '')}", "Content-Type": "application/json"}
 
     def compute_embeddings(self, texts):
-        headers = {"Authorization": f"Bearer {self.cfg.get('access-key', '')}"}
-        return _run_async(lambda: _http_json(f"{self.url}/{self.model}", {"inputs": texts}, headers))
+        if not self.model:
+            raise ValueError("huggingface api embeddings: model name is required")
+        url = self.embed_url + self.model
+        return _run_async(lambda: _http_json(url, {"inputs": list(texts), "options": self.options}, self._headers()))
+
+    def _infer(self, contents: List[str], options: Dict[str, Any]) -> List[dict]:
+        model = (options or {}).get("model") or self.model
+        if not model:
+            raise ValueError("huggingface completions: model is required")
+        import requests
+        r = requests.post(f"{self.infer_url}/models/{model}", data=json.dumps(list(contents)),
+                          headers=self._headers(), timeout=120)
+        r.raise_for_status()
+        beans = r.json()
+        if not isinstance(beans, list):
+            raise ValueError(f"huggingface completions: unexpected answer {str(beans)[:200]}")
+        return beans
+
+    def get_text_completions(self, prompts, consumer, options):
+        def run():
+            beans = self._infer(prompts, options)
+            text = (beans[0] or {}).get("sequence", "") if beans else ""
+            if consumer is not None:
+                ChunkCoalescer(consumer, 1, "").accept(text, True)
+            return CompletionResult(text)
+        return _run_async(run)
+
+    def get_chat_completions(self, messages, consumer, options):
+        def run():
+            beans = self._infer([m.content for m in messages], options)
+            choices = [(b or {}).get("sequence", "") for b in beans]
+            text = choices[0] if choices else ""
+            if consumer is not None:
+                ChunkCoalescer(consumer, 1, "").accept(text, True)
+            res = CompletionResult(text)
+            res.choices = choices
+            return res
+        return _run_async(run)
 
 
 class VertexAIService(CompletionsService, EmbeddingsService):

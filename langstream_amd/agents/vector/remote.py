@@ -40,6 +40,8 @@ Parity (configuration keys and result shapes) with the reference's
 from __future__ import annotations
 
 import json
+import urllib.parse
+import hashlib
 import logging
 import threading
 from concurrent.futures import Future
@@ -103,21 +105,69 @@ class _Http:
         self.s.close()
 
 
+class _SigV4Http(_Http):
+    """_Http whose every request is SigV4-signed (AWS OpenSearch Serverless, service
+    ``aoss``; the signed ``x-amz-content-sha256`` header AOSS requires is included)."""
+
+    def __init__(self, base: str, region: str, service: str, access_key: str, secret_key: str,
+                 session_token: Optional[str] = None, headers: Optional[Dict[str, str]] = None,
+                 timeout: float = 30.0):
+        super().__init__(base, headers, None, timeout)
+        self.region, self.service = region, service
+        self.ak, self.sk, self.token = access_key, secret_key, session_token
+
+    def call(self, method: str, path: str, **kw) -> Any:
+        from ...utils.cloudauth import sigv4_headers
+        data = kw.pop("data", None)
+        payload = (data.encode() if isinstance(data, str) else (data or b""))
+        params = kw.pop("params", None)
+        url = self.base + path
+        if params:
+            url += ("&" if "?" in url else "?") + urllib.parse.urlencode(params)
+        hdrs = {**self.s.headers, **(kw.pop("headers", None) or {})}
+        hdrs = {k: v for k, v in hdrs.items() if k.lower() in ("content-type",)}
+        hdrs["x-amz-content-sha256"] = hashlib.sha256(payload).hexdigest()
+        signed = sigv4_headers(method, url, self.region, self.service, self.ak, self.sk, payload, hdrs,
+                               session_token=self.token)
+        r = self.s.request(method, url, data=payload, headers=signed, timeout=self.timeout, **kw)
+        if r.status_code >= 400:
+            raise RuntimeError(f"{method} {url} -> {r.status_code}: {r.text[:500]}")
+        if not r.content:
+            return None
+        try:
+            return r.json()
+        except ValueError:
+            return r.text
+
+
 # ============================================================== OpenSearch
 class OpenSearchDataSource(DataSource):
+    """OpenSearch REST.  A host ending in ``amazonaws.com`` is AWS OpenSearch Serverless:
+    requests are SigV4-signed for service ``aoss`` in ``region`` with ``username`` /
+    ``password`` as the access / secret key, over HTTPS on 443
+    (OpenSearchDataSource.java:113-127, AwsSdk2Transport); any other host uses basic auth
+    (:128-140)."""
+
     def __init__(self, cfg: Dict[str, Any]):
         host = cfg.get("host")
         if not host:
             raise ValueError("opensearch datasource: missing host")
-        if str(host).endswith("amazonaws.com"):
-            raise RuntimeError("opensearch on AWS (SigV4-signed OpenSearch Serverless) is not supported by this "
-                               "build; use a host with basic auth")
+        host = str(host).replace("https://", "").replace("http://", "").rstrip("/")
+        self.index = cfg.get("index-name")
+        if host.endswith("amazonaws.com"):
+            region = cfg.get("region")
+            if not region:
+                raise ValueError("opensearch on AWS: region is required")
+            if not cfg.get("username") or not cfg.get("password"):
+                raise ValueError("opensearch on AWS: username (access key) and password (secret key) are required")
+            self.http = _SigV4Http(f"https://{host}", str(region), "aoss", str(cfg["username"]),
+                                   str(cfg["password"]), cfg.get("session-token"),
+                                   {"Content-Type": "application/json"})
+            return
         scheme = "https" if _bool(cfg.get("https"), True) else "http"
-        host = str(host).replace("https://", "").replace("http://", "")
         port = int(cfg.get("port") or 9200)
         auth = (cfg.get("username"), cfg.get("password") or "") if cfg.get("username") else None
         self.http = _Http(f"{scheme}://{host}:{port}", {"Content-Type": "application/json"}, auth)
-        self.index = cfg.get("index-name")
 
     def fetch_data(self, query: str, params: List[Any]) -> List[Dict[str, Any]]:
         body = build_object(query, params)

@@ -200,7 +200,7 @@ class ServiceRegistry:
         if "bedrock" in agent_cfg:
             return s.BedrockService(agent_cfg["bedrock"], model)
         if "huggingface" in agent_cfg:
-            return s.UnavailableService("huggingface", "HF inference API completions are not implemented")
+            return s.HuggingFaceAPIService(agent_cfg["huggingface"], model)
         raise ValueError("no AI service configured for completions")
 
     def embeddings_service(self, agent_cfg: Dict[str, Any], model: Optional[str]):

@@ -21,6 +21,7 @@ import uuid
 from typing import Any, Dict, List, Optional, Tuple
 
 from . import protocol as P
+from .security import SCRAM_MECHANISMS, ScramServer
 
 log = logging.getLogger(__name__)
 
@@ -49,7 +50,8 @@ class KafkaBroker:
                  default_partitions: int = 1, node_id: int = 0, ssl_context=None,
                  sasl_users: Optional[Dict[str, str]] = None):
         """``ssl_context``: a server-side SSLContext -> TLS listener (SSL / SASL_SSL);
-        ``sasl_users``: {username: password} -> SASL/PLAIN required before any other API
+        ``sasl_users``: {username: password} -> SASL (PLAIN or SCRAM-SHA-256/512) required
+        before any other API
         (an unauthenticated request closes the connection, as a Kafka broker does)."""
         self.host, self.port = host, port
         self.ssl_context = ssl_context
@@ -109,6 +111,7 @@ class KafkaBroker:
     # ------------------------------------------------------------------ connection
     async def _handle(self, reader: asyncio.StreamReader, writer: asyncio.StreamWriter) -> None:
         authed = not self.sasl_users
+        scram = None
         try:
             while True:
                 hdr = await reader.readexactly(4)
@@ -123,9 +126,18 @@ class KafkaBroker:
                         writer.close()
                         return
                 if api == P.SASL_HANDSHAKE:
-                    ok = bool(self.sasl_users) and body["mechanism"] == "PLAIN"
-                    resp = {"error": P.NONE if ok else P.UNSUPPORTED_SASL_MECHANISM,
-                            "mechanisms": ["PLAIN"] if self.sasl_users else []}
+                    offered = (["PLAIN"] + list(SCRAM_MECHANISMS)) if self.sasl_users else []
+                    mech = body["mechanism"]
+                    ok = mech in offered
+                    scram = ScramServer(mech, self.sasl_users) if ok and mech in SCRAM_MECHANISMS else None
+                    resp = {"error": P.NONE if ok else P.UNSUPPORTED_SASL_MECHANISM, "mechanisms": offered}
+                elif api == P.SASL_AUTHENTICATE and scram is not None:
+                    reply, done = scram.step(bytes(body["auth_bytes"]))
+                    authed = bool(done)
+                    failed = done is False
+                    resp = {"error": P.SASL_AUTHENTICATION_FAILED if failed else P.NONE,
+                            "error_message": "Authentication failed: SCRAM " + reply.decode() if failed else None,
+                            "auth_bytes": b"" if failed else reply}
                 elif api == P.SASL_AUTHENTICATE:
                     parts = bytes(body["auth_bytes"]).split(b"\0")
                     user, pw = (parts[1].decode(), parts[2].decode()) if len(parts) == 3 else (None, None)

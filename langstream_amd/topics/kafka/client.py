@@ -48,19 +48,34 @@ class KafkaConnection:
         self._corr = itertools.count(1)
         self._lock = threading.Lock()
         if security is not None and security.sasl:
-            self._sasl_plain(security)
+            self._sasl(security)
 
-    def _sasl_plain(self, security) -> None:
-        """SaslHandshake v1 + SaslAuthenticate v0 (KIP-152) with the PLAIN mechanism."""
+    def _sasl(self, security) -> None:
+        """SaslHandshake v1 + SaslAuthenticate v0 (KIP-152): PLAIN (one message) or
+        SCRAM-SHA-256/512 (client-first / client-final, server signature verified)."""
+        from .security import SCRAM_MECHANISMS, ScramClient, ScramError
         r = self.request(P.SASL_HANDSHAKE, {"mechanism": security.mechanism})
         if r["error"] != P.NONE:
             self.close()
             raise KafkaError(r["error"], f"SASL mechanism {security.mechanism} not enabled; broker offers "
                                          f"{r['mechanisms']}")
-        r = self.request(P.SASL_AUTHENTICATE, {"auth_bytes": security.plain_token()})
-        if r["error"] != P.NONE:
-            self.close()
-            raise KafkaError(r["error"], f"SASL authentication failed: {r.get('error_message')}")
+
+        def auth(msg: bytes) -> bytes:
+            r = self.request(P.SASL_AUTHENTICATE, {"auth_bytes": msg})
+            if r["error"] != P.NONE:
+                self.close()
+                raise KafkaError(r["error"], f"SASL authentication failed: {r.get('error_message')}")
+            return bytes(r.get("auth_bytes") or b"")
+
+        if security.mechanism in SCRAM_MECHANISMS:
+            sc = ScramClient(security.mechanism, security.username or "", security.password or "")
+            try:
+                sc.verify(auth(sc.final(auth(sc.first()))))
+            except ScramError as e:
+                self.close()
+                raise KafkaError(P.SASL_AUTHENTICATION_FAILED, f"SCRAM: {e}") from e
+            return
+        auth(security.plain_token())
 
     def _recv_exact(self, n: int) -> bytes:
         buf = bytearray()

@@ -184,3 +184,38 @@ def test_local_ai_routes_hosted_model_names_to_local_engines(monkeypatch):
         assert isinstance(chat, s.LocalCompletionsService)
     finally:
         reg.shutdown()
+
+
+def test_huggingface_api_completions_and_embeddings():
+    """HF inference API (HuggingFaceProvider.java:157-199): completions POST the JSON array
+    of message contents to {inference-url}/models/{model} and read [{score, token_str,
+    sequence}]; embeddings POST {inputs, options} to {api-url}{model}."""
+    from langstream_amd.agents.genai.services import HuggingFaceAPIService
+    from langstream_amd.services import ServiceRegistry
+
+    def handler(path, headers, body):
+        req = json.loads(body)
+        if path.startswith("/models/"):
+            assert isinstance(req, list)
+            return 200, [{"score": "0.9", "token_str": "x", "sequence": " | ".join(req) + " -> done"},
+                         {"score": "0.1", "token_str": "y", "sequence": "alt"}]
+        assert path == "/embed/bert-x" and req["options"] == {"wait_for_model": "true"}
+        return 200, [[0.5, 0.25] for _ in req["inputs"]]
+
+    f = _Fake(handler)
+    try:
+        cfg = {"access-key": "hf_secret", "inference-url": f.url, "api-url": f.url + "/embed/", "provider": "api"}
+        svc = ServiceRegistry().completions_service({"huggingface": cfg}, "gpt2")
+        assert isinstance(svc, HuggingFaceAPIService)
+        chunks = []
+        res = svc.get_chat_completions([ChatMessage("user", "hi"), ChatMessage("user", "there")],
+                                       lambda aid, i, t, last: chunks.append((t, last)), {"model": "gpt2"}).result(10)
+        assert res.content == "hi | there -> done" and res.choices == ["hi | there -> done", "alt"]
+        assert chunks == [("hi | there -> done", True)]
+        assert svc.get_text_completions(["a prompt"], None, {}).result(10).content == "a prompt -> done"
+        path, hdrs, body = f.calls[0]
+        assert path == "/models/gpt2" and hdrs["Authorization"] == "Bearer hf_secret"
+        emb = HuggingFaceAPIService(cfg, "bert-x").compute_embeddings(["a", "b"]).result(10)
+        assert emb == [[0.5, 0.25], [0.5, 0.25]]
+    finally:
+        f.close()

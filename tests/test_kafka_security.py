@@ -77,8 +77,11 @@ def test_plaintext_client_cannot_talk_to_tls_listener(tls_broker):
 
 def test_security_config_validation():
     with pytest.raises(ValueError):
-        SecurityConfig.from_config({"security.protocol": "SASL_SSL", "sasl.mechanism": "SCRAM-SHA-512",
+        SecurityConfig.from_config({"security.protocol": "SASL_SSL", "sasl.mechanism": "GSSAPI",
                                     "sasl.jaas.config": "x required username='a' password='b';"})
+    sc = SecurityConfig.from_config({"security.protocol": "SASL_SSL", "sasl.mechanism": "SCRAM-SHA-512",
+                                     "sasl.jaas.config": "x required username='a' password='b';"})
+    assert sc.mechanism == "SCRAM-SHA-512" and sc.username == "a"
     with pytest.raises(ValueError):
         SecurityConfig.from_config({"security.protocol": "SASL_PLAINTEXT"})      # no credentials
     sc = SecurityConfig.from_config({"security.protocol": "SSL", "ssl.endpoint.identification.algorithm": ""})
@@ -123,3 +126,36 @@ def test_codec_decoders_on_streams_with_back_references():
     # a batch compressed by a producer decodes through decode_batches
     recs = [(b"k", b"v" * 100, [], 5)]
     assert [x[3] for x in P.decode_batches(P.encode_batch(0, recs, codecs.GZIP), verify_crc=True)] == [b"v" * 100]
+
+
+def test_scram_sha256_rfc7677_test_vector():
+    """RFC 7677 section 3: user 'user', password 'pencil'."""
+    from langstream_amd.topics.kafka.security import ScramClient
+    c = ScramClient("SCRAM-SHA-256", "user", "pencil", nonce="rOprNGfwEbeRWgbNEkqO")
+    assert c.first() == b"n,,n=user,r=rOprNGfwEbeRWgbNEkqO"
+    sf = b"r=rOprNGfwEbeRWgbNEkqO%hvYDpWUa2RaTCAfuxFIlj)hNlF$k0,s=W22ZaJ0SNY7soEsUEjb6gQ==,i=4096"
+    assert c.final(sf) == (b"c=biws,r=rOprNGfwEbeRWgbNEkqO%hvYDpWUa2RaTCAfuxFIlj)hNlF$k0,"
+                           b"p=dHzbZapWIk4jUhN+Ute9ytag9zjfMHgsqmmiz7AndVQ=")
+    c.verify(b"v=6rriTRBi23WpRR/wtup+mMhUZUn/dB5nLTJRsjl95G4=")
+
+
+@pytest.mark.parametrize("mech", ["SCRAM-SHA-256", "SCRAM-SHA-512"])
+def test_sasl_scram_roundtrip_and_rejection(tls_broker, mech):
+    broker, ca = tls_broker
+    inst = _astra_instance(broker.bootstrap, ca)
+    inst.configuration["admin"]["sasl.mechanism"] = mech
+    inst.configuration["admin"]["sasl.jaas.config"] = (
+        "org.apache.kafka.common.security.scram.ScramLoginModule required username='tenant-user' password='s3cret';")
+    rt = KafkaTopicConnectionsRuntime()
+    rt.init(inst)
+    prod = rt.create_producer("a", None, {"topic": "scram-" + mech[-3:]})
+    prod.write(SimpleRecord.of("k", "via " + mech)).result(10)
+    prod.close()
+    bad = SecurityConfig.from_config({**inst.configuration["admin"], "sasl.jaas.config":
+                                      "x required username='tenant-user' password='wrong';"})
+    with pytest.raises(KafkaError):
+        KafkaClient(broker.bootstrap, security=bad).refresh_metadata()
+    nouser = SecurityConfig.from_config({**inst.configuration["admin"], "sasl.jaas.config":
+                                         "x required username='ghost' password='s3cret';"})
+    with pytest.raises(KafkaError):
+        KafkaClient(broker.bootstrap, security=nouser).refresh_metadata()

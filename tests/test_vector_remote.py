@@ -238,3 +238,32 @@ def test_remote_asset_managers(fake):
     m.deploy_asset()
     body = [json.loads(r["body"]) for r in fake.requests if r["path"] == "/api/json/v1/default_keyspace"]
     assert body[-1]["createCollection"]["options"]["vector"]["dimension"] == 8
+
+
+def test_opensearch_aws_serverless_is_sigv4_signed(fake):
+    """A host ending in amazonaws.com is AWS OpenSearch Serverless (OpenSearchDataSource.java
+    :113-127): every request is SigV4-signed for service 'aoss' in the configured region,
+    with username/password as the access/secret key.  The fake server re-computes the
+    signature from what it received."""
+    import datetime as dt
+    from langstream_amd.utils.cloudauth import sigv4_headers
+    fake.responses["/idx/_search"] = {"hits": {"hits": [{"_id": "a", "_source": {"t": 1}, "_score": 1.0}]}}
+    cfg = {"service": "opensearch", "host": "https://abc123.us-east-1.aoss.amazonaws.com", "region": "us-east-1",
+           "username": "AKIDEXAMPLE", "password": "SECRETKEY", "index-name": "idx"}
+    ds = OpenSearchDataSource(cfg)
+    assert ds.http.base == "https://abc123.us-east-1.aoss.amazonaws.com"
+    ds.http.base = f"http://127.0.0.1:{fake.port}"          # point the transport at the fake
+    rows = ds.fetch_data('{"query": {"match_all": {}}}', [])
+    assert rows[0]["id"] == "a"
+    req = fake.last("/idx/_search")
+    h = {k.lower(): v for k, v in req["headers"].items()}
+    assert h["authorization"].startswith("AWS4-HMAC-SHA256 Credential=AKIDEXAMPLE/")
+    assert "/us-east-1/aoss/aws4_request" in h["authorization"]
+    when = dt.datetime.strptime(h["x-amz-date"], "%Y%m%dT%H%M%SZ").replace(tzinfo=dt.timezone.utc)
+    again = sigv4_headers("POST", f"http://127.0.0.1:{fake.port}/idx/_search", "us-east-1", "aoss", "AKIDEXAMPLE",
+                          "SECRETKEY", req["body"].encode(),
+                          {"Content-Type": h["content-type"], "x-amz-content-sha256": h["x-amz-content-sha256"]},
+                          now=when)
+    assert again["Authorization"] == h["authorization"]
+    with pytest.raises(ValueError):
+        OpenSearchDataSource({"host": "x.aoss.amazonaws.com", "username": "a", "password": "b"})   # no region
