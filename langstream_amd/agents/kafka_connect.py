@@ -14,8 +14,10 @@ Python classes implementing the same contract as Kafka Connect's API:
 ``pkg.module:Class``, importable from the application's ``python/`` directory) or one of
 the Kafka-bundled class names mapped to built-in Python connectors:
 ``org.apache.kafka.connect.file.FileStreamSinkConnector`` (``file``: append one line per
-record) and ``org.apache.kafka.connect.file.FileStreamSourceConnector`` (``file``:
-emit new lines, ``batch.size``).
+record), ``org.apache.kafka.connect.file.FileStreamSourceConnector`` (``file``:
+emit new lines, ``batch.size``) and ``com.datastax.oss.kafka.sink.CassandraSinkConnector``
+(the reference's kafka-connect example: ``topic.<t>.<ks>.<table>.mapping`` upserts over
+the in-tree CQL client, see CassandraSinkTask).
 
 Sink agent semantics (as KafkaConnectSinkAgent): it HANDLES ITS OWN COMMITS -- records
 are buffered and handed to ``put`` in batches of ``adapterConfig.batchSize`` (16384) or
@@ -30,6 +32,7 @@ from __future__ import annotations
 import importlib
 import logging
 import os
+import re
 import threading
 import time
 from concurrent.futures import Future
@@ -148,9 +151,156 @@ class FileStreamSourceConnector(Connector):
         return FileStreamSourceTask
 
 
+# ---------------------------------------------------------------- DataStax Cassandra sink
+_TABLE_KEY = re.compile(r"^topic\.(.+)\.([A-Za-z0-9_]+)\.([A-Za-z0-9_]+)\.(mapping|deletesEnabled|ttl|"
+                        r"consistencyLevel|nullToUnset|ttlTimeUnit|timestampTimeUnit)$")
+
+
+def _secure_bundle(path: str) -> Dict[str, Any]:
+    """Astra secure-connect bundle (zip with config.json + CA): -> host, CQL port,
+    keyspace and the CA PEM.  (The bundle's SNI proxy routing by host id is not
+    implemented: the CQL endpoint in config.json is dialled directly over TLS.)"""
+    import base64 as _b64
+    import json as _json
+    import zipfile
+    data = path
+    if not os.path.exists(path) and not path.endswith(".zip"):
+        import io
+        data = io.BytesIO(_b64.b64decode(path))   # the bundle inlined as base64 (a secret)
+    with zipfile.ZipFile(data) as z:
+        cfg = _json.loads(z.read("config.json"))
+        ca = z.read("ca.crt").decode() if "ca.crt" in z.namelist() else None
+    return {"host": cfg.get("host"), "port": int(cfg.get("cql_port") or cfg.get("port") or 9042),
+            "keyspace": cfg.get("keyspace"), "ca": ca}
+
+
+class CassandraSinkTask(SinkTask):
+    """Python port of the behaviour of com.datastax.oss.kafka.sink.CassandraSinkConnector,
+    the connector of the reference's examples/applications/kafka-connect/pipeline.yaml,
+    on the in-tree CQL native-protocol client (agents/vector/cql.py):
+
+      contactPoints / port / loadBalancing.localDc / auth.username / auth.password, or
+      cloud.secureConnectBundle (Astra);
+      topic.<topic>.<keyspace>.<table>.mapping = "col=value.f, col2=key, col3=header.h, ..."
+        (one INSERT -- a Cassandra upsert -- per record per mapped table; string values
+        holding JSON are parsed, as the DataStax sink does for StringConverter records);
+      topic.<topic>.<keyspace>.<table>.deletesEnabled (true): a record whose value is null
+        deletes the row by its primary key (read from system_schema.columns);
+      topic.<topic>.<keyspace>.<table>.ttl (seconds, -1 = none), .consistencyLevel,
+      .nullToUnset (true: null mapped fields are left out of the INSERT instead of writing
+        tombstones).
+    Records are written in put(); flush/pre_commit then acknowledge them (the agent
+    commits source offsets only after that)."""
+
+    def start(self, props):
+        from .vector.cql import CqlSession
+        self.tables: Dict[str, List[Dict[str, Any]]] = {}
+        per: Dict[tuple, Dict[str, str]] = {}
+        for k, v in props.items():
+            m = _TABLE_KEY.match(k)
+            if m:
+                per.setdefault((m.group(1), m.group(2), m.group(3)), {})[m.group(4)] = v
+        for (topic, ks, table), opts in per.items():
+            if "mapping" not in opts:
+                raise ValueError(f"topic.{topic}.{ks}.{table}: a mapping is required")
+            mapping = []
+            for part in opts["mapping"].split(","):
+                if part.strip():
+                    col, _, expr = part.partition("=")
+                    mapping.append((col.strip(), expr.strip()))
+            self.tables.setdefault(topic, []).append({
+                "ks": ks, "table": table, "mapping": mapping,
+                "deletes": str(opts.get("deletesEnabled", "true")).lower() != "false",
+                "ttl": int(opts.get("ttl", -1)),
+                "null_to_unset": str(opts.get("nullToUnset", "true")).lower() != "false",
+                "pk": None})
+        if not self.tables:
+            raise ValueError("CassandraSinkConnector: no topic.<topic>.<keyspace>.<table>.mapping configured")
+        user, pwd = props.get("auth.username"), props.get("auth.password")
+        bundle = props.get("cloud.secureConnectBundle")
+        if bundle:
+            b = _secure_bundle(bundle)
+            ctx = None
+            if b["ca"]:
+                import ssl
+                ctx = ssl.create_default_context(cadata=b["ca"])
+                ctx.check_hostname = False   # Astra's proxy certificate names the host id, not the DNS name
+            self.session = CqlSession([f"{b['host']}:{b['port']}"], b["port"], user, pwd, None, False,
+                                      ssl_context=ctx)
+        else:
+            cps = [c.strip() for c in props.get("contactPoints", "localhost").split(",") if c.strip()]
+            self.session = CqlSession(cps, int(props.get("port", 9042)), user, pwd, None,
+                                      str(props.get("ssl.provider", "None")).lower() not in ("none", ""))
+        self.written = 0
+
+    @staticmethod
+    def _parse(v):
+        if isinstance(v, (bytes, bytearray)):
+            v = v.decode("utf-8", "replace")
+        if isinstance(v, str):
+            t = v.strip()
+            if t[:1] in ("{", "["):
+                try:
+                    import json as _json
+                    return _json.loads(t)
+                except ValueError:
+                    return v
+        return v
+
+    def _field(self, expr: str, rec: ConnectRecord):
+        root, _, path = expr.partition(".")
+        if root == "key":
+            base = self._parse(rec.key)
+        elif root == "value":
+            base = self._parse(rec.value)
+        elif root == "header":
+            return (rec.headers or {}).get(path)
+        else:
+            raise ValueError(f"unsupported mapping expression {expr!r} (key[.f], value[.f], header.h)")
+        for p in [x for x in path.split(".") if x]:
+            base = base.get(p) if isinstance(base, dict) else None
+        return base
+
+    def _pk(self, t) -> List[str]:
+        if t["pk"] is None:
+            rows = self.session.execute(
+                "SELECT column_name, kind, position FROM system_schema.columns WHERE keyspace_name = ? "
+                "AND table_name = ?", [t["ks"], t["table"]])
+            pk = [r for r in rows if r.get("kind") in ("partition_key", "clustering")]
+            pk.sort(key=lambda r: (r["kind"] != "partition_key", r.get("position") or 0))
+            t["pk"] = [r["column_name"] for r in pk]
+        return t["pk"]
+
+    def put(self, records):
+        for rec in records:
+            for t in self.tables.get(rec.topic, []):
+                q = f"{t['ks']}.{t['table']}"
+                vals = {col: self._field(expr, rec) for col, expr in t["mapping"] if not col.startswith("__")}
+                if rec.value is None:
+                    if t["deletes"]:
+                        pk = self._pk(t)
+                        self.session.execute(f"DELETE FROM {q} WHERE " + " AND ".join(f"{c} = ?" for c in pk),
+                                             [vals.get(c) for c in pk])
+                    continue
+                cols = [c for c, v in vals.items() if v is not None or not t["null_to_unset"]]
+                ttl = f" USING TTL {t['ttl']}" if t["ttl"] > 0 else ""
+                self.session.execute(f"INSERT INTO {q} ({', '.join(cols)}) VALUES ({', '.join('?' * len(cols))}){ttl}",
+                                     [vals[c] for c in cols])
+                self.written += 1
+
+    def stop(self):
+        self.session.close()
+
+
+class CassandraSinkConnector(Connector):
+    def task_class(self):
+        return CassandraSinkTask
+
+
 BUILTIN_CONNECTORS = {
     "org.apache.kafka.connect.file.FileStreamSinkConnector": FileStreamSinkConnector,
     "org.apache.kafka.connect.file.FileStreamSourceConnector": FileStreamSourceConnector,
+    "com.datastax.oss.kafka.sink.CassandraSinkConnector": CassandraSinkConnector,
 }
 
 

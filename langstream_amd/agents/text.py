@@ -429,54 +429,12 @@ class TextExtractorAgent(SingleRecordAgentProcessor):
 
 # ---------------------------------------------------------------- language detection
 # Character n-gram profiles (the technique of Tika's LanguageIdentifier, which the
-# reference uses: TXT/LanguageDetectorAgent.java:30-76): each language's profile is the
-# 1-3-gram distribution of a built-in sample text (word-boundary padded); a text is
-# scored by the naive-Bayes log-likelihood of its n-grams under each profile (add-k
+# reference uses: TXT/LanguageDetectorAgent.java:30-76, over Tika's legacy profile set of
+# 18 languages + en): each language's profile is the 1-3-gram distribution of original
+# generic training prose (agents/langid_data.py -- none of it is a test sentence); a text
+# is scored by the naive-Bayes log-likelihood of its n-grams under each profile (add-k
 # smoothed) and labelled with the best language, or "unknown" when it has no letters.
-_SAMPLES = {
-    "en": "the weather is nice today and we are going to the park with our friends. this is a simple "
-          "english sentence that shows how the language works. people in the city like to read books, "
-          "watch movies and talk about their work. what would you like to do this weekend? i think that "
-          "we should visit the museum because there is a new exhibition about history and science. "
-          "they have been waiting for the train since the morning, but it was late again. which one is "
-          "yours? she said that it was the best thing she had ever seen.",
-    "it": "questo è un esempio di testo in lingua italiana. oggi il tempo è bello e andiamo al parco con "
-          "gli amici. la gente della città ama leggere libri, guardare film e parlare del proprio lavoro. "
-          "che cosa vorresti fare questo fine settimana? penso che dovremmo visitare il museo perché c'è "
-          "una nuova mostra sulla storia e sulla scienza. aspettano il treno dalla mattina, ma era ancora "
-          "in ritardo. quale è il tuo? lei ha detto che era la cosa più bella che avesse mai visto. "
-          "questo libro è molto interessante e parla di italiano, cultura e tradizioni.",
-    "fr": "ceci est un exemple de texte en langue française. aujourd'hui il fait beau et nous allons au "
-          "parc avec nos amis. les gens de la ville aiment lire des livres, regarder des films et parler "
-          "de leur travail. qu'est-ce que vous voulez faire ce week-end? je pense que nous devrions "
-          "visiter le musée parce qu'il y a une nouvelle exposition sur l'histoire et la science. ils "
-          "attendent le train depuis le matin, mais il était encore en retard. parlez-vous français? "
-          "elle a dit que c'était la plus belle chose qu'elle ait jamais vue. voilà, ça va très bien.",
-    "de": "dies ist ein beispiel für einen text in deutscher sprache. heute ist das wetter schön und wir "
-          "gehen mit unseren freunden in den park. die menschen in der stadt lesen gerne bücher, sehen "
-          "filme und sprechen über ihre arbeit. was möchtest du an diesem wochenende machen? ich denke, "
-          "dass wir das museum besuchen sollten, weil es eine neue ausstellung über geschichte und "
-          "wissenschaft gibt. sie warten seit dem morgen auf den zug, aber er hatte wieder verspätung. "
-          "sie sagte, dass es das schönste war, was sie je gesehen hatte. sprechen sie deutsch?",
-    "es": "este es un ejemplo de texto en lengua española. hoy hace buen tiempo y vamos al parque con los "
-          "amigos. la gente de la ciudad disfruta leyendo libros, viendo películas y hablando de su "
-          "trabajo. ¿qué te gustaría hacer este fin de semana? creo que deberíamos visitar el museo "
-          "porque hay una nueva exposición sobre la historia y la ciencia. esperan el tren desde la "
-          "mañana, pero llegó tarde otra vez. ¿cuál es el tuyo? ella dijo que era lo más bonito que "
-          "había visto nunca. ¿hablas español? sí, un poco.",
-    "pt": "este é um exemplo de texto em língua portuguesa. hoje o tempo está bom e vamos ao parque com os "
-          "amigos. as pessoas da cidade gostam de ler livros, ver filmes e falar sobre o seu trabalho. o "
-          "que você gostaria de fazer neste fim de semana? acho que deveríamos visitar o museu porque há "
-          "uma nova exposição sobre a história e a ciência. eles esperam o comboio desde a manhã, mas "
-          "estava atrasado outra vez. ela disse que foi a coisa mais bonita que já tinha visto. você "
-          "fala português? não, ainda não. obrigado pela atenção.",
-    "nl": "dit is een voorbeeld van een tekst in de nederlandse taal. vandaag is het mooi weer en gaan we "
-          "met onze vrienden naar het park. de mensen in de stad lezen graag boeken, kijken films en "
-          "praten over hun werk. wat wil je dit weekend doen? ik denk dat we het museum moeten bezoeken "
-          "omdat er een nieuwe tentoonstelling is over geschiedenis en wetenschap. ze wachten sinds de "
-          "ochtend op de trein, maar hij was weer te laat. zij zei dat het het mooiste was dat ze ooit "
-          "had gezien. spreekt u nederlands? ja, een beetje.",
-}
+from .langid_data import SAMPLES as _SAMPLES  # noqa: E402
 _WORD = re.compile(r"[^\W\d_]+", re.UNICODE)
 
 

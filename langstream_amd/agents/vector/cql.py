@@ -258,14 +258,14 @@ class Prepared:
 class CqlSession:
     def __init__(self, contact_points: List[str], port: int = 9042, username: Optional[str] = None,
                  password: Optional[str] = None, keyspace: Optional[str] = None, use_tls: bool = False,
-                 consistency: str = "LOCAL_QUORUM", timeout: float = 30.0):
+                 consistency: str = "LOCAL_QUORUM", timeout: float = 30.0, ssl_context=None):
         last: Optional[Exception] = None
         for cp in contact_points:
             host, _, p = cp.partition(":")
             try:
                 s = socket.create_connection((host, int(p or port)), timeout=timeout)
-                if use_tls:
-                    s = ssl.create_default_context().wrap_socket(s, server_hostname=host)
+                if use_tls or ssl_context is not None:
+                    s = (ssl_context or ssl.create_default_context()).wrap_socket(s, server_hostname=host)
                 self.sock = s
                 break
             except OSError as e:

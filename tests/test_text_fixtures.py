@@ -114,3 +114,91 @@ def test_pdf_content_stream_text():
     pdf = (b"%PDF-1.4\n1 0 obj << /Length 10 /Filter /FlateDecode >>\nstream\n" + zlib.compress(content)
            + b"\nendstream\nendobj\n%%EOF")
     assert extract_text(pdf) == "Hello (PDF) world\nKern ed text\nHex string\noctAl"
+
+
+# Held-out sentences (food, technology, travel, sport, health): written for this test,
+# none of them (nor the reference fixtures) appears in agents/langid_data.py.
+HELD_OUT = {
+    "da": ["Jeg har glemt min adgangskode til computeren igen.", "Toget til lufthavnen er desværre forsinket i dag.",
+           "Hun løber fem kilometer hver tirsdag og torsdag.", "Lægen sagde, at jeg skal drikke mere vand.",
+           "Vi spiste rugbrød med ost og en kop kaffe til frokost."],
+    "de": ["Ich habe mein Passwort für den Computer schon wieder vergessen.",
+           "Der Zug zum Flughafen hat heute leider Verspätung.", "Sie läuft jeden Dienstag fünf Kilometer.",
+           "Der Arzt meinte, ich solle mehr Wasser trinken.", "Zum Mittagessen gab es Suppe mit frischem Gemüse."],
+    "el": ["Ξέχασα πάλι τον κωδικό του υπολογιστή μου.", "Το τρένο για το αεροδρόμιο έχει καθυστέρηση σήμερα.",
+           "Τρέχει πέντε χιλιόμετρα κάθε Τρίτη.", "Ο γιατρός είπε ότι πρέπει να πίνω περισσότερο νερό.",
+           "Για μεσημεριανό φάγαμε σαλάτα με τυρί φέτα."],
+    "en": ["I forgot the password for my laptop again.", "The train to the airport is delayed this morning.",
+           "She runs five kilometres every Tuesday evening.", "The doctor told me to drink more water.",
+           "We had soup and a sandwich for lunch."],
+    "es": ["Otra vez he olvidado la contraseña del ordenador.", "El tren al aeropuerto llega tarde esta mañana.",
+           "Ella corre cinco kilómetros todos los martes.", "El médico me dijo que bebiera más agua.",
+           "Para almorzar tomamos una sopa de verduras y pan."],
+    "et": ["Ma unustasin jälle oma arvuti parooli.", "Rong lennujaama hilineb täna hommikul.",
+           "Ta jookseb igal teisipäeval viis kilomeetrit.", "Arst ütles, et ma pean rohkem vett jooma.",
+           "Lõunaks sõime suppi ja musta leiba."],
+    "fi": ["Unohdin taas tietokoneeni salasanan.", "Juna lentokentälle on tänään myöhässä.",
+           "Hän juoksee viisi kilometriä joka tiistai.", "Lääkäri sanoi, että minun pitää juoda enemmän vettä.",
+           "Söimme lounaaksi keittoa ja ruisleipää."],
+    "fr": ["J'ai encore oublié le mot de passe de mon ordinateur.", "Le train pour l'aéroport a du retard ce matin.",
+           "Elle court cinq kilomètres tous les mardis.", "Le médecin m'a dit de boire plus d'eau.",
+           "Nous avons mangé une soupe et du fromage à midi."],
+    "hu": ["Megint elfelejtettem a számítógépem jelszavát.", "A repülőtérre tartó vonat ma reggel késik.",
+           "Minden kedden öt kilométert fut.", "Az orvos azt mondta, hogy több vizet kell innom.",
+           "Ebédre levest és friss kenyeret ettünk."],
+    "is": ["Ég gleymdi aftur lykilorðinu að tölvunni minni.", "Lestin út á flugvöll er sein í morgun.",
+           "Hún hleypur fimm kílómetra á hverjum þriðjudegi.", "Læknirinn sagði að ég þyrfti að drekka meira vatn.",
+           "Við borðuðum fiskisúpu og rúgbrauð í hádeginu."],
+    "it": ["Ho dimenticato di nuovo la password del computer.", "Il treno per l'aeroporto è in ritardo stamattina.",
+           "Lei corre cinque chilometri ogni martedì.", "Il medico mi ha detto di bere più acqua.",
+           "A pranzo abbiamo mangiato una minestra di verdure."],
+    "lt": ["Vėl pamiršau savo kompiuterio slaptažodį.", "Traukinys į oro uostą šį rytą vėluoja.",
+           "Ji kiekvieną antradienį nubėga penkis kilometrus.", "Gydytojas pasakė, kad turiu gerti daugiau vandens.",
+           "Pietums valgėme sriubą ir juodą duoną."],
+    "nl": ["Ik ben het wachtwoord van mijn computer weer vergeten.", "De trein naar het vliegveld heeft vandaag vertraging.",
+           "Ze loopt elke dinsdag vijf kilometer hard.", "De dokter zei dat ik meer water moet drinken.",
+           "Als lunch aten we soep met een broodje kaas."],
+    "no": ["Jeg har glemt passordet til datamaskinen min igjen.", "Toget til flyplassen er forsinket i dag.",
+           "Hun løper fem kilometer hver tirsdag.", "Legen sa at jeg må drikke mer vann.",
+           "Til lunsj spiste vi fiskesuppe og brødskiver med brunost."],
+    "pl": ["Znowu zapomniałem hasła do komputera.", "Pociąg na lotnisko jest dziś rano opóźniony.",
+           "Ona biega pięć kilometrów w każdy wtorek.", "Lekarz powiedział, że muszę pić więcej wody.",
+           "Na obiad zjedliśmy zupę pomidorową i chleb."],
+    "pt": ["Esqueci outra vez a palavra-passe do computador.", "O comboio para o aeroporto está atrasado hoje.",
+           "Ela corre cinco quilómetros todas as terças-feiras.", "O médico disse que eu devia beber mais água.",
+           "Ao almoço comemos uma sopa de legumes e pão."],
+    "ru": ["Я опять забыл пароль от своего компьютера.", "Поезд в аэропорт сегодня утром опаздывает.",
+           "Она бегает пять километров каждый вторник.", "Врач сказал, что мне нужно пить больше воды.",
+           "На обед мы ели суп и чёрный хлеб."],
+    "sv": ["Jag har glömt lösenordet till min dator igen.", "Tåget till flygplatsen är försenat i dag.",
+           "Hon springer fem kilometer varje tisdag.", "Läkaren sa att jag måste dricka mer vatten.",
+           "Till lunch åt vi ärtsoppa och pannkakor."],
+    "th": ["ฉันลืมรหัสผ่านคอมพิวเตอร์อีกแล้ว", "รถไฟไปสนามบินมาสายในเช้านี้", "เธอวิ่งห้ากิโลเมตรทุกวันอังคาร",
+           "หมอบอกว่าฉันควรดื่มน้ำให้มากขึ้น", "มื้อกลางวันเรากินข้าวผัดกับต้มยำกุ้ง"],
+}
+
+
+def test_language_detector_held_out_accuracy():
+    """Generalisation over Tika's legacy profile set (LanguageDetectorAgent.java:55):
+    >= 90 % of held-out sentences, none of which the profiles were built from."""
+    from langstream_amd.agents.langid_data import SAMPLES
+    from langstream_amd.agents.text import detect_language
+    assert set(HELD_OUT) == set(SAMPLES) and len(SAMPLES) == 19
+    corpus = " ".join(SAMPLES.values()).lower()
+    wrong, total = [], 0
+    for lang, sents in HELD_OUT.items():
+        assert len(sents) >= 5
+        for s in sents:
+            assert s.lower().rstrip(".") not in corpus          # truly held out
+            total += 1
+            got = detect_language(s)
+            if got != lang:
+                wrong.append((lang, got, s))
+    assert (total - len(wrong)) / total >= 0.90, wrong
+
+
+def test_language_samples_do_not_contain_fixture_phrases():
+    from langstream_amd.agents.langid_data import SAMPLES
+    corpus = " ".join(SAMPLES.values()).lower()
+    for phrase in ("this is a english", "questo é italiano", "parlez-vous français"):
+        assert phrase not in corpus
