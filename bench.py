@@ -354,6 +354,12 @@ def main():
                     help="stream: closed loop, --batch questions in flight per GPU, a new question as each "
                          "answer arrives, a step = --batch answers; burst: --batch questions at the start of "
                          "each step, the step ends when all are answered")
+    ap.add_argument("--config", choices=("rag", "embed", "chat"), default="rag",
+                    help="rag: BASELINE config 4 (the headline, default); embed: config 2 (compute-ai-embeddings "
+                         "agent on Kafka records); chat: config 3 (ai-chat-completions through the websocket "
+                         "gateway), and config 5 with --chat-model llama-3-70b --gpus 8 --tp 8")
+    ap.add_argument("--tp", type=int, default=0, help="chat: tensor-parallel degree (= --gpus)")
+    ap.add_argument("--embed-batch", type=int, default=64, help="embed: the agent's batch-size")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -361,6 +367,8 @@ def main():
     rank, world, local = _env_int("RANK", 0), _env_int("WORLD_SIZE", 1), _env_int("LOCAL_RANK", 0)
     if world != args.gpus:
         sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.config != "rag":
+        return _other_config(args, rank, world, local)
 
     import torch
     import torch.distributed as dist
@@ -640,6 +648,43 @@ def main():
     if rank == 0:
         unlink_shmlog(shm, size_mb=shm_mb)
     if multi:
+        dist.destroy_process_group()
+
+
+def _other_config(args, rank: int, world: int, local: int) -> None:
+    """BASELINE configs 2, 3 and 5 (langstream_amd/bench/)."""
+    import torch
+    import torch.distributed as dist
+    use_gpu = torch.cuda.is_available()
+    if use_gpu:
+        torch.cuda.set_device(local)
+    if args.config == "chat":
+        from langstream_amd.bench import chat
+        chat.run(args, rank, world, None)
+        if dist.is_initialized():
+            dist.destroy_process_group()
+        return
+    ctrl = None
+    if world > 1:
+        dist.init_process_group("gloo")
+        ctrl = dist.group.WORLD
+
+    def barrier():
+        if ctrl is not None:
+            dist.barrier(group=ctrl)
+        if use_gpu:
+            torch.cuda.synchronize()
+
+    def bcast(obj):
+        if world == 1:
+            return obj
+        box = [obj]
+        dist.broadcast_object_list(box, src=0, group=ctrl)
+        return box[0]
+
+    from langstream_amd.bench import embed
+    embed.run(args, rank, world, barrier, bcast)
+    if ctrl is not None:
         dist.destroy_process_group()
 
 

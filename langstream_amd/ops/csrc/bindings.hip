@@ -71,7 +71,8 @@ void decode_gemm(at::Tensor out, at::Tensor x, at::Tensor w, at::Tensor workspac
                  c10::optional<at::Tensor> norm_w, double eps, int64_t bn_force, int64_t splits_force);
 void decode_gemm_silu(at::Tensor out, at::Tensor x, at::Tensor w, at::Tensor workspace, at::Tensor tickets,
                       at::Tensor err, int64_t splits);
-void decode_gemm_ablate(at::Tensor x, at::Tensor w, at::Tensor workspace, int64_t abl, int64_t splits);
+void decode_gemm_ablate(at::Tensor x, at::Tensor w, at::Tensor workspace, int64_t abl, int64_t splits,
+                        int64_t split_outer);
 void bind_runners(pybind11::module_& m);
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {

@@ -106,6 +106,18 @@ static __device__ __forceinline__ void glds16(const bf16* src, char* lds_wave_ba
       : "memory");
 }
 
+// Same with the non-temporal hint (streamed-once operands: leave L2 to the re-read ones).
+static __device__ __forceinline__ void glds16_nt(const bf16* src, char* lds_wave_base) {
+  const unsigned dst = __builtin_amdgcn_readfirstlane(
+      (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)lds_wave_base);
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(src), "s"(dst)
+      : "memory");
+}
+
 template <int N>
 static __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");

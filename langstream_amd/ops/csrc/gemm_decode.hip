@@ -66,13 +66,14 @@ __device__ __forceinline__ int piece_chunk(int lane, int row) { return ((lane & 
 
 // XS / WS: ring slots of X / W; stage t of X is issued XS-1 steps ahead, of W WS-1 ahead.
 // ABL (timing-only ablations, wrong results; tools/dgemm_bench.py --ablate): bit 0 drops
-// the MFMAs, bit 1 the fragment reads, bit 2 the LDS-DMA issue, bit 3 the W DMA only.
+// the MFMAs, bit 1 the fragment reads, bit 2 the LDS-DMA issue, bit 3 the W DMA only;
+// bit 4 (a real variant, results valid) streams W with the non-temporal hint.
 template <int BN, int XS, int WS, int EPI, int ABL = 0>
 __global__ void __launch_bounds__(512) dgemm_kernel(const bf16* __restrict__ x, int64_t ldx,
                                                    const bf16* __restrict__ w, int M, int N, int K, int S,
                                                    bf16* __restrict__ out, int64_t ldo, float* __restrict__ part,
                                                    int F, unsigned* __restrict__ tickets, float* __restrict__ xchg,
-                                                   int* __restrict__ err) {
+                                                   int* __restrict__ err, int split_outer) {
   constexpr int WSTAGE = BN * BK * 2;
   constexpr int JT = BN / 32;              // 16-col tiles per wave (wave = 64 rows x BN/2 cols)
   constexpr int IT = 4;                    // 16-row tiles per wave
@@ -88,8 +89,13 @@ __global__ void __launch_bounds__(512) dgemm_kernel(const bf16* __restrict__ x, 
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   // the S splits of one tile are consecutive logical ids: same XCD (speed only)
+  // split_outer: consecutive logical ids (one XCD) share the K split, i.e. the same X
+  // slice, which then stays in that XCD's L2; otherwise the S splits of one tile are
+  // adjacent (the gate_up exchange pairs sit on one XCD).
   const int logical = xcd_remap(blockIdx.x, gridDim.x);
-  const int tile = logical / S, split = logical - tile * S;
+  const int ntiles = gridDim.x / S;
+  const int tile = split_outer ? logical % ntiles : logical / S;
+  const int split = split_outer ? logical / ntiles : logical - tile * S;
   const int nk = K / BK;
   const int kb = (int)(((int64_t)split * nk) / S), ke = (int)(((int64_t)(split + 1) * nk) / S);
   const int nks = ke - kb;
@@ -120,7 +126,10 @@ __global__ void __launch_bounds__(512) dgemm_kernel(const bf16* __restrict__ x, 
   auto issue_w = [&](int t) {
     char* dst = lw0 + (t % WS) * WSTAGE + (PW * wid) * 1024;
 #pragma unroll
-    for (int j = 0; j < PW; ++j) glds16(wsrc[j] + t * BK, dst + j * 1024);
+    for (int j = 0; j < PW; ++j) {
+      if constexpr ((ABL & 16) != 0) glds16_nt(wsrc[j] + t * BK, dst + j * 1024);
+      else glds16(wsrc[j] + t * BK, dst + j * 1024);
+    }
   };
 
   // ---- fragments
@@ -299,6 +308,11 @@ int pick_split(int tiles, int K, int min_steps) {
   return best;
 }
 
+int split_outer_default() {
+  static const int v = env_int("LS_DGEMM_SPLIT_OUTER", 1);
+  return v;
+}
+
 // ring shapes: BN = 128: X 3 slots (2 ahead) + W 4 slots (3 ahead) = 160 KB;
 // BN = 256: X 2 + W 3 = 160 KB.
 template <int BN, int EPI>
@@ -307,7 +321,8 @@ void dgemm_launch(int S, int tiles, hipStream_t st, const at::Tensor& x, const a
   constexpr int XS = BN == 128 ? 3 : 2, WS = BN == 128 ? 4 : 3;
   dgemm_kernel<BN, XS, WS, EPI><<<dim3(tiles * S), 512, 0, st>>>((const bf16*)x.data_ptr(), x.stride(0),
                                                                  (const bf16*)w.data_ptr(), M, N, K, S, out, ldo,
-                                                                 part, F, tickets, xchg, err);
+                                                                 part, F, tickets, xchg, err,
+                                                                 EPI == EPI_SILU2 ? 0 : split_outer_default());
 }
 
 void check_xw(const at::Tensor& x, const at::Tensor& w) {
@@ -415,7 +430,8 @@ void decode_gemm_silu(at::Tensor out, at::Tensor x, at::Tensor w, at::Tensor wor
 
 // Timing-only ablation builds of the plain split-K GEMM (EPI_PARTIAL, BN = 128): abl bits
 // as documented at dgemm_kernel.  Results are garbage by design.
-void decode_gemm_ablate(at::Tensor x, at::Tensor w, at::Tensor workspace, int64_t abl, int64_t splits) {
+void decode_gemm_ablate(at::Tensor x, at::Tensor w, at::Tensor workspace, int64_t abl, int64_t splits,
+                        int64_t split_outer) {
   check_xw(x, w);
   const int M = (int)x.size(0), K = (int)x.size(1), N = (int)w.size(0);
   const int tiles = N / 128;
@@ -429,10 +445,10 @@ void decode_gemm_ablate(at::Tensor x, at::Tensor w, at::Tensor workspace, int64_
     dgemm_kernel<128, 3, 4, EPI_PARTIAL, V><<<grid, 512, 0, st>>>((const bf16*)x.data_ptr(), x.stride(0), \
                                                                   (const bf16*)w.data_ptr(), M, N, K, S,  \
                                                                   nullptr, 0, part, 0, nullptr, nullptr, \
-                                                                  nullptr);                              \
+                                                                  nullptr, (int)split_outer);            \
     break;
   switch (abl) {
-    A_(0) A_(1) A_(2) A_(3) A_(4) A_(5) A_(7) A_(8) A_(9) A_(11)
+    A_(0) A_(1) A_(2) A_(3) A_(4) A_(5) A_(7) A_(8) A_(9) A_(11) A_(16) A_(17)
     default: TORCH_CHECK(false, "unsupported ablation ", abl);
   }
 #undef A_

@@ -26,3 +26,31 @@ def test_bench_two_ranks_consumer_group_dp(tmp_path):
         assert a[topic] and b[topic] and not set(a[topic]) & set(b[topic])
     assert all(n > 0 for n in d["knn_rounds_per_rank"])   # queries went through the sharded kNN
     assert d["config"]["crawl"] and d["ingest"]["chunks_per_s"] > 0
+
+
+def _run(args, tmp_path, timeout=600):
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], cwd=str(tmp_path), env=env,
+                       capture_output=True, text=True, timeout=timeout)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("{") and '"metric"' in ln]
+    assert len(line) == 1, r.stdout[-2000:]
+    return json.loads(line[0])
+
+
+def test_bench_config2_embeddings_agent_on_kafka_two_ranks(tmp_path):
+    """BASELINE config 2 shape: compute-ai-embeddings agent replicas (one per rank) as ONE
+    consumer group on a Kafka topic of the in-tree broker."""
+    d = _run(["--config", "embed", "--gpus", "2", "--steps", "2", "--warmup", "1", "--batch", "32"], tmp_path)
+    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp2" and d["value"] > 0
+    assert "Kafka" in d["metric"] and d["config"]["topics"].startswith("kafka")
+
+
+def test_bench_config5_shape_tensor_parallel_chat_gateway(tmp_path):
+    """BASELINE config 3/5 path: a TP=2 chat agent (rank 0 serves the websocket gateway +
+    scheduler, rank 1 mirrors every engine step) answering streamed chat sessions."""
+    d = _run(["--config", "chat", "--gpus", "2", "--tp", "2", "--steps", "1", "--warmup", "1", "--batch", "2",
+              "--max-tokens", "6"], tmp_path)
+    assert d["config"]["parallelism"] == "tp2" and d["answers"] == 2 and d["value"] > 0
+    assert d["ttft_p50_ms"] > 0 and d["unit"] == "tokens/s"
