@@ -354,6 +354,9 @@ def main():
                     help="stream: closed loop, --batch questions in flight per GPU, a new question as each "
                          "answer arrives, a step = --batch answers; burst: --batch questions at the start of "
                          "each step, the step ends when all are answered")
+    ap.add_argument("--no-persist", action="store_true",
+                    help="keep the vector store in HBM only (default: WAL + snapshots on local disk, the "
+                         "durable default of a vector-db-sink pod)")
     ap.add_argument("--config", choices=("rag", "embed", "chat"), default="rag",
                     help="rag: BASELINE config 4 (the headline, default); embed: config 2 (compute-ai-embeddings "
                          "agent on Kafka records); chat: config 3 (ai-chat-completions through the websocket "
@@ -425,6 +428,11 @@ def main():
 
     # ---- untimed setup: engines, corpus ingest into this rank's HBM shard
     t_setup = time.time()
+    persist_dir = None
+    if not args.no_persist:
+        import tempfile
+        persist_dir = tempfile.mkdtemp(prefix=f"rag-bench-store-r{rank}-")
+        VectorStoreRegistry.configure(persist_dir=persist_dir)   # every upsert WAL-logged before its ack
     emb = services.embedding_engine(embed_model, {"embeddings-model": embed_model})
     docs = [" ".join(corpus[(i * 7 + j) % len(corpus)] for j in range(4)) for i in range(args.corpus)]
     store = VectorStoreRegistry.get("documents", emb.dim, device=device)
@@ -624,6 +632,8 @@ def main():
                        "corpus_docs_per_gpu": args.corpus, "top_k": 20, "rerank": 5,
                        "crawled_pages_per_gpu_per_step": args.docs, "crawl": crawl,
                        "topics": "shm (cross-process consumer groups)",
+                       "vector_store": ("HBM shard, WAL + snapshots on local disk (fsync off)" if persist_dir
+                                        else "HBM shard, not persisted"),
                        "load": (f"closed loop, {args.batch} questions in flight per GPU; only questions sent "
                                 f"inside the timed window count, the window drains them"
                                 if args.load == "stream" else f"bursts of {args.batch} questions per GPU per step"),
@@ -647,6 +657,10 @@ def main():
     barrier()
     if rank == 0:
         unlink_shmlog(shm, size_mb=shm_mb)
+    if persist_dir:
+        import shutil
+        VectorStoreRegistry.reset()
+        shutil.rmtree(persist_dir, ignore_errors=True)
     if multi:
         dist.destroy_process_group()
 

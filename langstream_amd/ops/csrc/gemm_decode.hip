@@ -67,9 +67,15 @@ __device__ __forceinline__ int piece_chunk(int lane, int row) { return ((lane & 
 // XS / WS: ring slots of X / W; stage t of X is issued XS-1 steps ahead, of W WS-1 ahead.
 // ABL (timing-only ablations, wrong results; tools/dgemm_bench.py --ablate): bit 0 drops
 // the MFMAs, bit 1 the fragment reads, bit 2 the LDS-DMA issue, bit 3 the W DMA only;
-// bit 4 (a real variant, results valid) streams W with the non-temporal hint.
-template <int BN, int XS, int WS, int EPI, int ABL = 0>
-__global__ void __launch_bounds__(512) dgemm_kernel(const bf16* __restrict__ x, int64_t ldx,
+// bit 4 (a real variant, results valid) streams W with the non-temporal hint; bit 5 uses 4
+// dedicated loader waves; bit 6 skips the partial-slab stores.
+// LD: dedicated loader waves (0 or 4).  With LD = 4 the workgroup is 8 compute + 4
+// loader waves: only the loaders issue LDS-DMA.  Measured (tools/dgemm_bench.py
+// --ablate, profiles/dgemm_ablation_r3.log): with every wave issuing its share of the
+// stage right after the barrier, a full DMA queue blocks the issuing wave before its
+// MFMAs, so a step costs DMA + compute instead of max(DMA, compute).
+template <int BN, int XS, int WS, int EPI, int ABL = 0, int LD = 0>
+__global__ void __launch_bounds__(LD ? 768 : 512) dgemm_kernel(const bf16* __restrict__ x, int64_t ldx,
                                                    const bf16* __restrict__ w, int M, int N, int K, int S,
                                                    bf16* __restrict__ out, int64_t ldo, float* __restrict__ part,
                                                    int F, unsigned* __restrict__ tickets, float* __restrict__ xchg,
@@ -77,8 +83,9 @@ __global__ void __launch_bounds__(512) dgemm_kernel(const bf16* __restrict__ x, 
   constexpr int WSTAGE = BN * BK * 2;
   constexpr int JT = BN / 32;              // 16-col tiles per wave (wave = 64 rows x BN/2 cols)
   constexpr int IT = 4;                    // 16-row tiles per wave
-  constexpr int PX = 4;                    // X pieces per wave per stage (32 / 8 waves)
-  constexpr int PW = BN / 64;              // W pieces per wave per stage
+  constexpr int NLW = LD ? LD : 8;         // waves that issue the DMAs
+  constexpr int PX = 32 / NLW;             // X pieces per issuing wave per stage (32 per stage)
+  constexpr int PW = BN / 8 / NLW;         // W pieces per issuing wave per stage
   constexpr int XA = XS - 1, WA = WS - 1;  // stages issued ahead
   static_assert(XA >= 1 && WA >= XA, "W is issued at least as far ahead as X");
   static_assert(XS * XSTAGE + WS * WSTAGE <= LDS_MAX, "LDS budget");
@@ -88,6 +95,9 @@ __global__ void __launch_bounds__(512) dgemm_kernel(const bf16* __restrict__ x, 
 
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const bool loader = LD == 0 || wid >= 8;   // issues DMAs (every wave when LD == 0)
+  const bool computer = LD == 0 || wid < 8;
+  const int lw = LD ? (wid >= 8 ? wid - 8 : 0) : wid;   // index among the issuing waves
   // the S splits of one tile are consecutive logical ids: same XCD (speed only)
   // split_outer: consecutive logical ids (one XCD) share the K split, i.e. the same X
   // slice, which then stays in that XCD's L2; otherwise the S splits of one tile are
@@ -104,13 +114,13 @@ __global__ void __launch_bounds__(512) dgemm_kernel(const bf16* __restrict__ x, 
   const bf16* xsrc[PX];
 #pragma unroll
   for (int j = 0; j < PX; ++j) {
-    const int row = 32 * wid + 8 * j + (lane >> 3);
+    const int row = (8 * PX) * lw + 8 * j + (lane >> 3);
     xsrc[j] = x + (int64_t)min(row, M - 1) * ldx + (int64_t)kb * BK + piece_chunk(lane, row);  // rows >= M: never stored
   }
   const bf16* wsrc[PW];
 #pragma unroll
   for (int j = 0; j < PW; ++j) {
-    const int lr = (8 * PW) * wid + 8 * j + (lane >> 3);   // tile-local W row
+    const int lr = (8 * PW) * lw + 8 * j + (lane >> 3);    // tile-local W row
     int wrow;
     if constexpr (EPI == EPI_SILU || EPI == EPI_SILU2)
       wrow = lr < BN / 2 ? tile * (BN / 2) + lr : F + tile * (BN / 2) + (lr - BN / 2);
@@ -119,12 +129,12 @@ __global__ void __launch_bounds__(512) dgemm_kernel(const bf16* __restrict__ x, 
     wsrc[j] = w + (int64_t)wrow * K + (int64_t)kb * BK + piece_chunk(lane, lr);
   }
   auto issue_x = [&](int t) {
-    char* dst = lx0 + (t % XS) * XSTAGE + (PX * wid) * 1024;
+    char* dst = lx0 + (t % XS) * XSTAGE + (PX * lw) * 1024;
 #pragma unroll
     for (int j = 0; j < PX; ++j) glds16(xsrc[j] + t * BK, dst + j * 1024);
   };
   auto issue_w = [&](int t) {
-    char* dst = lw0 + (t % WS) * WSTAGE + (PW * wid) * 1024;
+    char* dst = lw0 + (t % WS) * WSTAGE + (PW * lw) * 1024;
 #pragma unroll
     for (int j = 0; j < PW; ++j) {
       if constexpr ((ABL & 16) != 0) glds16_nt(wsrc[j] + t * BK, dst + j * 1024);
@@ -133,7 +143,8 @@ __global__ void __launch_bounds__(512) dgemm_kernel(const bf16* __restrict__ x, 
   };
 
   // ---- fragments
-  const int wm = wid >> 1, wn = wid & 1;
+  const int cw = computer ? wid : 0;       // loaders: any valid layout, never used
+  const int wm = cw >> 1, wn = cw & 1;
   const int fr = lane & 15, h = lane >> 4;
   const int fsw = (fr >> 1) & 7;           // = (row >> 1) & 7 of every fragment row
   auto bcol = [&](int j) {                 // tile-local W row of this lane's B fragment
@@ -160,6 +171,7 @@ __global__ void __launch_bounds__(512) dgemm_kernel(const bf16* __restrict__ x, 
   // in between, X(t+1 .. t+XA-1) and W(t+WA-XA+1 .. t+WA-1): at the top of step t the
   // wait is vmcnt(that count), computed exactly (the tail skips issues).
   auto issue_step = [&](int u) {
+    if (!loader) return;
     if constexpr ((ABL & 4) == 0) {
       if (u + XA >= 0 && u + XA < nks) issue_x(u + XA);
       if constexpr ((ABL & 8) == 0)
@@ -170,11 +182,14 @@ __global__ void __launch_bounds__(512) dgemm_kernel(const bf16* __restrict__ x, 
   for (int t = 0; t < nks; ++t) {
     const int nx = max(0, min(t + XA - 1, nks - 1) - t);                       // X(t+1 .. t+XA-1)
     const int nw = max(0, min(t + WA - 1, nks - 1) - (t - XA + WA) + 1);       // W(t-XA+WA .. t+WA-1)
-    if constexpr ((ABL & 12) == 0) wait_vmcnt_dyn(PX * nx + PW * nw);
-    else if constexpr ((ABL & 4) == 0) wait_vmcnt_dyn(PX * nx);
+    if (loader) {
+      if constexpr ((ABL & 12) == 0) wait_vmcnt_dyn(PX * nx + PW * nw);
+      else if constexpr ((ABL & 4) == 0) wait_vmcnt_dyn(PX * nx);
+    }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // step t-1's fragment reads are done
     __builtin_amdgcn_s_barrier();                         // every wave: stage t landed, t-1 read
     issue_step(t);                                        // into the slots of stage t-1
+    if (!computer) continue;
     const char* lx = lx0 + (t % XS) * XSTAGE;
     const char* lw = lw0 + (t % WS) * WSTAGE;
 #pragma unroll
@@ -210,6 +225,7 @@ __global__ void __launch_bounds__(512) dgemm_kernel(const bf16* __restrict__ x, 
   // acc[i][j][r] = C[64wm + 16i + 4h + r][tile col of bcol(j)]
   const int rbase = 64 * wm + 4 * h;
   if constexpr (EPI == EPI_SILU2) {
+    static_assert(LD == 0, "the half exchange runs with every wave computing");
     // ---- in-launch combine of the two K halves (see the header)
     __syncthreads();                                      // ring reads done: LDS reusable
     unsigned* sh = reinterpret_cast<unsigned*>(lds);
@@ -266,29 +282,58 @@ __global__ void __launch_bounds__(512) dgemm_kernel(const bf16* __restrict__ x, 
     }
     return;
   }
+  // ---- LDS-staged epilogue: the tile goes through LDS as f32 rows of BN + 4 (the ring
+  // is dead now) and leaves in whole rows with 16-B stores -- every store instruction
+  // writes full 128-B lines instead of 4 x 64-B row pieces per wave.  BN = 128 stages all
+  // 256 rows at once (132 KB); BN = 256 in two passes of 128 rows.
+  constexpr int TP = BN + 4;
+  constexpr int PASS_ROWS = BM * TP * 4 <= XS * XSTAGE + WS * WSTAGE ? BM : BM / 2;
+  static_assert(PASS_ROWS * TP * 4 <= XS * XSTAGE + WS * WSTAGE, "epilogue pass must fit the ring's LDS");
+  constexpr int NT = LD ? 768 : 512;
+  float* T = reinterpret_cast<float*>(lds);
 #pragma unroll
-  for (int i = 0; i < IT; ++i)
+  for (int r0 = 0; r0 < BM; r0 += PASS_ROWS) {
+    __syncthreads();                                    // ring reads / the previous pass are done
+    if (computer && 64 * wm >= r0 && 64 * wm < r0 + PASS_ROWS) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int m = rbase + 16 * i + r;
-      if (m >= M) continue;
-      if constexpr (EPI == EPI_SILU) {
-        bf16* orow = out + (int64_t)m * ldo + tile * (BN / 2) + (BN / 4) * wn + fr;
+      for (int i = 0; i < IT; ++i)
 #pragma unroll
-        for (int j = 0; j < JT / 2; ++j) {
-          const float g = acc[i][j][r], u = acc[i][j + JT / 2][r];
-          orow[16 * j] = (bf16)(g / (1.f + __expf(-g)) * u);
+        for (int r = 0; r < 4; ++r) {
+          float* trow = T + (rbase + 16 * i + r - r0) * TP;
+#pragma unroll
+          for (int j = 0; j < JT; ++j) trow[bcol(j)] = acc[i][j][r];
         }
-      } else if constexpr (EPI == EPI_STORE) {
-        bf16* orow = out + (int64_t)m * ldo + tile * BN + (BN / 2) * wn + fr;
+    }
+    __syncthreads();
+    const int rows = min(PASS_ROWS, M - r0);
+    if constexpr (EPI == EPI_PARTIAL) {
+      // part[split][m][tile * BN + c]: BN / 4 float4 per row
+      for (int q = threadIdx.x; q < ((ABL & 64) ? 0 : rows * (BN / 4)); q += NT) {
+        const int m = q / (BN / 4), c = (q - m * (BN / 4)) * 4;
+        *reinterpret_cast<f32x4*>(part + ((int64_t)split * M + r0 + m) * N + tile * BN + c) =
+            *reinterpret_cast<const f32x4*>(T + m * TP + c);
+      }
+    } else if constexpr (EPI == EPI_STORE) {
+      for (int q = threadIdx.x; q < rows * (BN / 8); q += NT) {
+        const int m = q / (BN / 8), c = (q - m * (BN / 8)) * 8;
+        const float* src = T + m * TP + c;
+        float v[8];
 #pragma unroll
-        for (int j = 0; j < JT; ++j) orow[16 * j] = (bf16)acc[i][j][r];
-      } else {
-        float* prow = part + ((int64_t)split * M + m) * N + tile * BN + (BN / 2) * wn + fr;
+        for (int e = 0; e < 8; ++e) v[e] = src[e];
+        st16(out + (int64_t)(r0 + m) * ldo + tile * BN + c, pack8(v));
+      }
+    } else {
+      // EPI_SILU: tile columns [0, BN/2) are gate, [BN/2, BN) the matching up columns
+      for (int q = threadIdx.x; q < rows * (BN / 16); q += NT) {
+        const int m = q / (BN / 16), c = (q - m * (BN / 16)) * 8;
+        const float* g = T + m * TP + c;
+        float v[8];
 #pragma unroll
-        for (int j = 0; j < JT; ++j) prow[16 * j] = acc[i][j][r];
+        for (int e = 0; e < 8; ++e) v[e] = g[e] / (1.f + __expf(-g[e])) * g[BN / 2 + e];
+        st16(out + (int64_t)(r0 + m) * ldo + tile * (BN / 2) + c, pack8(v));
       }
     }
+  }
 }
 
 int env_int(const char* name, int dflt) {
@@ -319,7 +364,8 @@ template <int BN, int EPI>
 void dgemm_launch(int S, int tiles, hipStream_t st, const at::Tensor& x, const at::Tensor& w, int M, int N, int K,
                   bf16* out, int64_t ldo, float* part, int F, unsigned* tickets, float* xchg, int* err) {
   constexpr int XS = BN == 128 ? 3 : 2, WS = BN == 128 ? 4 : 3;
-  dgemm_kernel<BN, XS, WS, EPI><<<dim3(tiles * S), 512, 0, st>>>((const bf16*)x.data_ptr(), x.stride(0),
+  constexpr int LDW = BN == 128 ? 4 : 0;   // BN = 256 needs 200 VGPRs: no room for a third wave per SIMD
+  dgemm_kernel<BN, XS, WS, EPI, 0, LDW><<<dim3(tiles * S), LDW ? 768 : 512, 0, st>>>((const bf16*)x.data_ptr(), x.stride(0),
                                                                  (const bf16*)w.data_ptr(), M, N, K, S, out, ldo,
                                                                  part, F, tickets, xchg, err,
                                                                  EPI == EPI_SILU2 ? 0 : split_outer_default());
@@ -409,7 +455,10 @@ void decode_gemm_silu(at::Tensor out, at::Tensor x, at::Tensor w, at::Tensor wor
   TORCH_CHECK(decode_gemm_supported(w, true), "decode_gemm_silu: gate_up rows must be 2F with F % 128 == 0");
   TORCH_CHECK(out.scalar_type() == at::kBFloat16 && out.size(0) == M && out.size(1) == F && out.stride(1) == 1);
   const int tiles = F / 128;
-  static const int split_env = env_int("LS_DGEMM_SILU_SPLIT", 2);
+  // default 1: one launch of 128-column tiles (64 gate + 64 up) with loader waves, full K
+  // (66 us at M = 256 on Llama-3-8B, tools/dgemm_bench.py); 2: the 256-column tile with
+  // the in-launch K-half exchange (82 us: 8 waves that also issue their DMAs)
+  static const int split_env = env_int("LS_DGEMM_SILU_SPLIT", 1);
   const int sp = splits > 0 ? (int)splits : split_env;
   auto st = at::hip::getCurrentHIPStream();
   if (sp != 2 || K / BK < 8) {
@@ -442,13 +491,15 @@ void decode_gemm_ablate(at::Tensor x, at::Tensor w, at::Tensor workspace, int64_
   float* part = workspace.data_ptr<float>();
 #define A_(V)                                                                                          \
   case V:                                                                                              \
-    dgemm_kernel<128, 3, 4, EPI_PARTIAL, V><<<grid, 512, 0, st>>>((const bf16*)x.data_ptr(), x.stride(0), \
+    dgemm_kernel<128, 3, 4, EPI_PARTIAL, (V & ~32), (V & 32) ? 4 : 0><<<grid, (V & 32) ? 768 : 512, 0, st>>>( \
+        (const bf16*)x.data_ptr(), x.stride(0),                                                        \
                                                                   (const bf16*)w.data_ptr(), M, N, K, S,  \
                                                                   nullptr, 0, part, 0, nullptr, nullptr, \
                                                                   nullptr, (int)split_outer);            \
     break;
   switch (abl) {
     A_(0) A_(1) A_(2) A_(3) A_(4) A_(5) A_(7) A_(8) A_(9) A_(11) A_(16) A_(17)
+    A_(32) A_(33) A_(35) A_(36) A_(39) A_(48) A_(64) A_(71)
     default: TORCH_CHECK(false, "unsupported ablation ", abl);
   }
 #undef A_

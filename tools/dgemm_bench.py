@@ -68,9 +68,14 @@ def main():
             if a.ablate:
                 out = torch.empty(M, N, device=dev, dtype=bf)
                 ref = None
-                for abl, nm in ((0, "full"), (1, "no_mfma"), (2, "no_lds_read"), (3, "dma_only"), (4, "no_dma"),
-                                (8, "no_w_dma"), (9, "no_w_dma_no_mfma"), (7, "barrier_only")):
-                    variants[f"abl{abl}_{nm}"] = lambda i, abl=abl: h.decode_gemm_ablate(x, ws[i], wsp, abl, 0)
+                for abl, so, nm in ((0, 0, "full_split_inner"), (0, 1, "full_split_outer"), (16, 1, "w_nt"),
+                                    (1, 1, "no_mfma"), (2, 1, "no_lds_read"), (3, 1, "dma_only"), (4, 1, "no_dma"),
+                                    (8, 1, "no_w_dma"), (9, 1, "no_w_dma_no_mfma"), (7, 1, "barrier_only"),
+                                    (32, 1, "ld_full"), (33, 1, "ld_no_mfma"), (35, 1, "ld_dma_only"),
+                                    (36, 1, "ld_no_dma"), (39, 1, "ld_barrier_only"), (48, 1, "ld_w_nt"),
+                                    (64, 1, "no_slab_store"), (71, 1, "barrier_only_no_slab_store")):
+                    variants[f"abl{abl}_{nm}"] = (
+                        lambda i, abl=abl, so=so: h.decode_gemm_ablate(x, ws[i], wsp, abl, 0, so))
                 check = None
             elif name == "gate_up":
                 out = torch.empty(M, Fi, device=dev, dtype=bf)
