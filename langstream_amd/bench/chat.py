@@ -1,7 +1,7 @@
 """BASELINE configs 3 and 5: ai-chat-completions through the WebSocket chat gateway.
 
 Config 3 = Llama-3-8B TP=1 on one MI355X (``bench.py --config chat``); config 5 =
-Llama-3-70B TP=8 over xGMI (``bench.py --config chat --model llama-3-70b --gpus 8 --tp
+Llama-3-70B TP=8 over xGMI (``bench.py --config chat --chat-model llama-3-70b --gpus 8 --tp
 8``).  The chat application is the reference's chat-gateway shape
 (GW/websocket/handlers/ChatHandler.java:29-190: chat gateway -> questions topic ->
 ai-chat-completions streaming chunks to the answers topic, ChatCompletionsStep.java:

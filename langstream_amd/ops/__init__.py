@@ -153,13 +153,15 @@ def gemm_fused(x, w, bias=None, gelu=False, residual=None, ln_stats_in=None, ln_
     return r
 
 
-def gemm_prefill(x, w, silu=False, out=None):
+def gemm_prefill(x, w, silu=False, out=None, variant=-1):
     """Prefill-sized MFMA GEMM (ops/csrc/gemm_prefill.hip, 256 x 256 tiles): x . w^T, or with
-    ``silu`` the Llama SwiGLU of the fused gate_up weight [2F, K]: silu(x.g^T) * (x.u^T)."""
+    ``silu`` the Llama SwiGLU of the fused gate_up weight [2F, K]: silu(x.g^T) * (x.u^T).
+    ``variant``: -1 the configured kernel (LS_PGEMM_KERNEL), 0 the 32-deep ring kernel,
+    1 the ping-pong kernel (K % 128 == 0)."""
     if _gpu(x):
         n = w.shape[0] // 2 if silu else w.shape[0]
         out = torch.empty(x.shape[0], n, dtype=x.dtype, device=x.device) if out is None else out
-        hip().gemm_prefill(out, x, w, silu)
+        hip().gemm_prefill(out, x, w, silu, variant)
         return out
     y = x.float() @ w.float().t()
     r = (ref.silu_and_mul(y) if silu else y).to(x.dtype)

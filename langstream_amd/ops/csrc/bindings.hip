@@ -63,7 +63,7 @@ void gemm_fused(at::Tensor out, at::Tensor x, at::Tensor w, c10::optional<at::Te
                 c10::optional<at::Tensor> res_b, double eps, c10::optional<at::Tensor> stats_out);
 void skinny_gemm_add_rmsnorm(at::Tensor out, at::Tensor x, at::Tensor w, at::Tensor residual, at::Tensor norm_w,
                              double eps);
-void gemm_prefill(at::Tensor out, at::Tensor x, at::Tensor w, bool silu);
+void gemm_prefill(at::Tensor out, at::Tensor x, at::Tensor w, bool silu, int64_t variant);
 bool gemm_prefill_supported(const at::Tensor& w, bool silu);
 bool decode_gemm_supported(const at::Tensor& w, bool silu);
 int64_t decode_gemm_workspace(int64_t M, int64_t N, int64_t K, bool silu);
@@ -116,7 +116,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("res_g") = py::none(), py::arg("res_b") = py::none(), py::arg("eps") = 1e-12,
         py::arg("stats_out") = py::none());
   m.def("skinny_gemm_add_rmsnorm", &skinny_gemm_add_rmsnorm);
-  m.def("gemm_prefill", &gemm_prefill);
+  m.def("gemm_prefill", &gemm_prefill, py::arg("out"), py::arg("x"), py::arg("w"), py::arg("silu"), py::arg("variant") = -1);
   m.def("gemm_prefill_supported", &gemm_prefill_supported);
   m.def("decode_gemm_supported", &decode_gemm_supported);
   m.def("decode_gemm_workspace", &decode_gemm_workspace);

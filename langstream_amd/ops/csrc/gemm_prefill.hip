@@ -23,6 +23,7 @@
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
 #include "common.h"
+#include <type_traits>
 
 namespace {
 
@@ -351,18 +352,434 @@ __global__ void __launch_bounds__(512) gemm_prefill64_kernel(const bf16* __restr
     }
 }
 
+// ---------------------------------------------------------------------------------
+// Ping-pong kernel: 64-deep K tiles cut into four 16 KB HALF-TILES (128 LDS rows x 128 B)
+// -- A-q0 = tile rows {0..63, 128..191}, A-q1 = rows {64..127, 192..255}, B-q0 / B-q1 =
+// the first / second 32 of each wave's 64 columns -- in an 8-slot LDS ring (128 KB).
+// Every K tile is four PHASES, one C quadrant (qm, qn) of the wave's 128 x 64 each:
+//
+//   phase  quadrant  fragment reads        LDS-DMA issued            vmcnt before barrier
+//   0      (0, 0)    A-q0 -> a, B-q0 -> b0  B-q1 of tile t+1        8 (B-q1 of t landed)
+//   1      (0, 1)    B-q1 -> b1             A-q1 of tile t+1        8 (A-q1 of t)
+//   2      (1, 1)    A-q1 -> a              A-q0 of tile t+2        -
+//   3      (1, 0)    -                      B-q0 of tile t+2        8 (A-q0, B-q0 of t+1)
+//
+// A phase is { fragment reads, one half-tile of LDS-DMA (2 per lane), counted vmcnt } ->
+// s_barrier -> { lgkmcnt(0), 16 MFMA 16x16x32 } -> s_barrier, and the two wave groups that
+// share each SIMD (wm = 0: waves 0-3, wm = 1: waves 4-7) run one barrier apart, so one
+// group's MFMA cluster overlaps the other's LDS reads and DMA issue (cdna_hip_programming
+// §5 "256^2 8-phase template", T3-T5).  Hazards, by barrier count: a half-tile is waited
+// for (every wave, its own DMA) in the phase BEFORE its first read, and re-filled no
+// earlier than two phases after its last read (the staggered group finishes reading
+// one barrier late); each half-tile spends 4-5 phases in flight (4 half-tiles = 64 KB per CU).
+// LDS rows hold k-chunk c ^ ((row >> 1) & 7) at chunk c (source-side swizzle, conflict-free
+// ds_read_b128 for the 16 rows of a fragment lane group).
+constexpr int HT = 16384;
+
+template <int EPI>
+__global__ void __launch_bounds__(512) gemm_pp_kernel(const bf16* __restrict__ x, int64_t ldx,
+                                                      const bf16* __restrict__ w, int M, int K,
+                                                      bf16* __restrict__ out, int64_t ldo, int MT, int NTL, int F,
+                                                      int group_m) {
+  __shared__ __attribute__((aligned(1024))) char lds[8 * HT];
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int logical = xcd_remap(blockIdx.x, gridDim.x);
+  const int per_group = group_m * NTL;
+  const int grp = logical / per_group, first = grp * group_m;
+  const int gsz = min(MT - first, group_m);
+  const int rem = logical - grp * per_group;
+  const int mt = first + rem % gsz, nt = rem / gsz;
+  const int m0 = mt * TM;
+  const int nk = K / 64;
+
+  // LDS-DMA sources: wave w fills LDS rows 16w..16w+15 of every half-tile (2 pieces of
+  // 8 rows x 128 B); lane l loads row 8e + (l >> 3) of piece e, swizzled chunk l & 7.
+  const bf16* src[4][2];   // [A-q0, A-q1, B-q0, B-q1][piece]
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    const int r = 16 * wid + 8 * e + (lane >> 3);
+    const int koff = ((lane & 7) ^ ((r >> 1) & 7)) * 8;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int arow = m0 + (r & 63) + 128 * (r >> 6) + 64 * q;
+      src[q][e] = x + (int64_t)min(arow, M - 1) * ldx + koff;   // rows >= M: any valid row, never stored
+      int wrow;
+      if (EPI == EPI_SILU) wrow = (q == 0 ? 0 : F) + nt * 128 + r;
+      else wrow = nt * TN + 64 * (r >> 5) + 32 * q + (r & 31);
+      src[2 + q][e] = w + (int64_t)wrow * K + koff;
+    }
+  }
+  auto issue = [&](int type, int tile, int slot) {
+    const int ko = min(tile, nk - 1) * 64;   // past the end: re-load the last tile into a dead slot
+#pragma unroll
+    for (int e = 0; e < 2; ++e) glds16(src[type][e] + ko, lds + slot * HT + (2 * wid + e) * 1024);
+  };
+
+  const int wm = wid >> 2, wn = wid & 3;
+  const int fr = lane & 15, h = lane >> 4;
+  const int fsw = (fr >> 1) & 7;
+  // byte offsets of this lane's fragment rows for k-steps 0 / 1 inside a half-tile
+  const int aoff0 = (64 * wm + fr) * 128 + 16 * (h ^ fsw), aoff1 = (64 * wm + fr) * 128 + 16 * ((4 + h) ^ fsw);
+  const int boff0 = (32 * wn + fr) * 128 + 16 * (h ^ fsw), boff1 = (32 * wn + fr) * 128 + 16 * ((4 + h) ^ fsw);
+  bf16x8 a[4][2], b0[2][2], b1[2][2];
+  auto read_a = [&](int slot) {
+    const char* base = lds + slot * HT;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      a[i][0] = __builtin_bit_cast(bf16x8, ld16(base + aoff0 + i * 2048));
+      a[i][1] = __builtin_bit_cast(bf16x8, ld16(base + aoff1 + i * 2048));
+    }
+  };
+  auto read_b = [&](int slot, bf16x8 (&b)[2][2]) {
+    const char* base = lds + slot * HT;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      b[j][0] = __builtin_bit_cast(bf16x8, ld16(base + boff0 + j * 2048));
+      b[j][1] = __builtin_bit_cast(bf16x8, ld16(base + boff1 + j * 2048));
+    }
+  };
+  f32x4 acc[2][2][4][2];
+#pragma unroll
+  for (int qm = 0; qm < 2; ++qm)
+#pragma unroll
+    for (int qn = 0; qn < 2; ++qn)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[qm][qn][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto mfma = [&](f32x4 (&c)[4][2], const bf16x8 (&bb)[2][2]) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) c[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][ks], bb[j][ks], c[i][j], 0, 0, 0);
+  };
+  // the MFMA half of a phase: barrier -> wait this wave's fragment reads -> cluster -> barrier
+  auto compute = [&](f32x4 (&c)[4][2], const bf16x8 (&bb)[2][2]) {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+    mfma(c, bb);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  // one K tile t whose half-tiles sit in slots 4P..4P+3 (P = t & 1, compile-time)
+  auto ktile = [&](int t, auto Pc) {
+    constexpr int P = decltype(Pc)::value;
+    constexpr int Q = 1 - P;
+    read_a(4 * P + 0);
+    read_b(4 * P + 1, b0);
+    issue(3, t + 1, 4 * Q + 2);     // B-q1 of t+1
+    wait_vmcnt<8>();
+    compute(acc[0][0], b0);
+    read_b(4 * P + 2, b1);
+    issue(1, t + 1, 4 * Q + 3);     // A-q1 of t+1
+    wait_vmcnt<8>();
+    compute(acc[0][1], b1);
+    read_a(4 * P + 3);
+    issue(0, t + 2, 4 * P + 0);     // A-q0 of t+2
+    compute(acc[1][1], b1);
+    issue(2, t + 2, 4 * P + 1);     // B-q0 of t+2
+    wait_vmcnt<8>();
+    compute(acc[1][0], b0);
+  };
+
+  // prologue, in steady-state issue order: A-q0, B-q0, B-q1, A-q1 of tile 0, A-q0, B-q0 of tile 1
+  issue(0, 0, 0);
+  issue(2, 0, 1);
+  issue(3, 0, 2);
+  issue(1, 0, 3);
+  issue(0, 1, 4);
+  issue(2, 1, 5);
+  wait_vmcnt<8>();
+  __builtin_amdgcn_s_barrier();
+  if (wm == 1) __builtin_amdgcn_s_barrier();   // group 1 runs one barrier behind
+  for (int t = 0; t < nk; t += 2) {   // nk even
+    ktile(t, std::integral_constant<int, 0>());
+    ktile(t + 1, std::integral_constant<int, 1>());
+  }
+  if (wm == 0) __builtin_amdgcn_s_barrier();
+  wait_vmcnt<0>();  // no LDS-DMA may outlive the workgroup
+
+  // acc[qm][qn][i][j][r] = C[128 wm + 64 qm + 16 i + 4 h + r][64 wn + 32 qn + 16 j + fr] (tile-local;
+  // SILU: qn = 0 gate, qn = 1 up of feature nt*128 + 32 wn + 16 j + fr)
+#pragma unroll
+  for (int qm = 0; qm < 2; ++qm)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + 128 * wm + 64 * qm + 16 * i + 4 * h + r;
+        if (m >= M) continue;
+        bf16* orow = out + (int64_t)m * ldo;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          if (EPI == EPI_SILU) {
+            const float g = acc[qm][0][i][j][r], u = acc[qm][1][i][j][r];
+            orow[nt * 128 + 32 * wn + 16 * j + fr] = (bf16)(g / (1.f + __expf(-g)) * u);
+          } else {
+#pragma unroll
+            for (int qn = 0; qn < 2; ++qn) orow[nt * TN + 64 * wn + 32 * qn + 16 * j + fr] = (bf16)acc[qm][qn][i][j][r];
+          }
+        }
+      }
+}
+
+// ---------------------------------------------------------------------------------
+// Persistent form of the ping-pong kernel: one workgroup per CU walks its tiles (round r
+// of G = gridDim.x tiles: logical tile r*G + xcd_remap(blockIdx)) as ONE stream of K tiles,
+// so the ring's prefetch runs straight across tile boundaries -- the next tile's first
+// half-tiles are in flight while this tile finishes and stores -- and no tile pays a
+// cold prologue.  Operands are read by buffer_load ... lds through per-tile buffer
+// resources: the per-lane offsets are tile-independent (8 VGPRs instead of 8 pointers),
+// rows past M fall outside the X resource's range and read zeros, and the "tile" after
+// a workgroup's last one has an empty resource (its dummy prefetches move no bytes).
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ i32x4 make_rsrc(const void* p, uint32_t bytes) {
+  const uint64_t a = (uint64_t)(uintptr_t)p;
+  i32x4 r;
+  r[0] = __builtin_amdgcn_readfirstlane((int)(uint32_t)a);
+  r[1] = __builtin_amdgcn_readfirstlane((int)((a >> 32) & 0xffff));
+  r[2] = __builtin_amdgcn_readfirstlane((int)bytes);
+  r[3] = 0x00020000;
+  return r;
+}
+
+// 16 B per lane from rsrc + voff + soff into LDS at lds_wave_base + 16 * lane (M0-based,
+// as glds16; inline asm so hipcc does not drain vmcnt before the next ds_read)
+static __device__ __forceinline__ void blds16(i32x4 rsrc, int voff, int soff, unsigned lds_addr) {
+  const unsigned dst = __builtin_amdgcn_readfirstlane(lds_addr);
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(rsrc), "s"(dst), "s"(soff)
+      : "memory");
+}
+
+template <int EPI>
+__global__ void __launch_bounds__(512) gemm_pp2_kernel(const bf16* __restrict__ x, int64_t ldx,
+                                                       const bf16* __restrict__ w, int64_t w_elems, int M, int K,
+                                                       bf16* __restrict__ out, int64_t ldo, int MT, int NTL, int F,
+                                                       int group_m, int ntiles) {
+  __shared__ __attribute__((aligned(1024))) char lds[8 * HT];
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int G = gridDim.x;
+  const int g = xcd_remap(blockIdx.x, G);
+  const int my_n = g < ntiles ? (ntiles - 1 - g) / G + 1 : 0;
+  if (my_n == 0) return;
+  const int nk = K / 64;
+  const int per_group = group_m * NTL;
+  auto coords = [&](int j, int& m0, int& nt) {
+    const int logical = j * G + g;
+    const int grp = logical / per_group, first = grp * group_m;
+    const int gsz = min(MT - first, group_m);
+    const int rem = logical - grp * per_group;
+    m0 = (first + rem % gsz) * TM;
+    nt = rem / gsz;
+  };
+  constexpr int WROWS = EPI == EPI_SILU ? 128 : TN;   // W rows per tile from the tile's W base
+  auto rsrc_a = [&](int j) {
+    if (j >= my_n) return make_rsrc(x, 0);
+    int m0, nt;
+    coords(j, m0, nt);
+    return make_rsrc(x + (int64_t)m0 * ldx, (uint32_t)(((int64_t)(M - m0 - 1) * ldx + K) * 2));
+  };
+  auto rsrc_w = [&](int j) {
+    if (j >= my_n) return make_rsrc(w, 0);
+    int m0, nt;
+    coords(j, m0, nt);
+    const int64_t off = (int64_t)nt * WROWS * K;
+    return make_rsrc(w + off, (uint32_t)((w_elems - off) * 2));
+  };
+  // tile-independent per-lane byte offsets: [A-q0, A-q1, B-q0, B-q1][piece]
+  int voff[4][2];
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    const int r = 16 * wid + 8 * e + (lane >> 3);
+    const int kb = ((lane & 7) ^ ((r >> 1) & 7)) * 16;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      voff[q][e] = (int)(((r & 63) + 128 * (r >> 6) + 64 * q) * ldx * 2) + kb;
+      if (EPI == EPI_SILU) voff[2 + q][e] = (int)(((int64_t)(q == 0 ? 0 : F) + r) * K * 2) + kb;
+      else voff[2 + q][e] = (64 * (r >> 5) + 32 * q + (r & 31)) * K * 2 + kb;
+    }
+  }
+  i32x4 ra_cur = rsrc_a(0), rw_cur = rsrc_w(0), ra_nxt = rsrc_a(1), rw_nxt = rsrc_w(1);
+  const unsigned lds_u32 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)lds;
+  // K tile tr of the current tile (tr >= nk: tile tr - nk of the next one)
+  auto issue = [&](int type, int tr, int slot) {
+    const bool nxt = tr >= nk;
+    const int soff = (nxt ? tr - nk : tr) * 128;
+    const i32x4 rs = type < 2 ? (nxt ? ra_nxt : ra_cur) : (nxt ? rw_nxt : rw_cur);
+#pragma unroll
+    for (int e = 0; e < 2; ++e) blds16(rs, voff[type][e], soff, lds_u32 + slot * HT + (2 * wid + e) * 1024);
+  };
+
+  const int wm = wid >> 2, wn = wid & 3;
+  const int fr = lane & 15, h = lane >> 4;
+  const int fsw = (fr >> 1) & 7;
+  const int aoff0 = (64 * wm + fr) * 128 + 16 * (h ^ fsw), aoff1 = (64 * wm + fr) * 128 + 16 * ((4 + h) ^ fsw);
+  const int boff0 = (32 * wn + fr) * 128 + 16 * (h ^ fsw), boff1 = (32 * wn + fr) * 128 + 16 * ((4 + h) ^ fsw);
+  bf16x8 a[4][2], b0[2][2], b1[2][2];
+  auto read_a = [&](int slot) {
+    const char* base = lds + slot * HT;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      a[i][0] = __builtin_bit_cast(bf16x8, ld16(base + aoff0 + i * 2048));
+      a[i][1] = __builtin_bit_cast(bf16x8, ld16(base + aoff1 + i * 2048));
+    }
+  };
+  auto read_b = [&](int slot, bf16x8 (&b)[2][2]) {
+    const char* base = lds + slot * HT;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      b[j][0] = __builtin_bit_cast(bf16x8, ld16(base + boff0 + j * 2048));
+      b[j][1] = __builtin_bit_cast(bf16x8, ld16(base + boff1 + j * 2048));
+    }
+  };
+  f32x4 acc[2][2][4][2];
+  auto zero = [&]() {
+#pragma unroll
+    for (int qm = 0; qm < 2; ++qm)
+#pragma unroll
+      for (int qn = 0; qn < 2; ++qn)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[qm][qn][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  };
+  auto compute = [&](f32x4 (&c)[4][2], const bf16x8 (&bb)[2][2]) {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) c[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][ks], bb[j][ks], c[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  // same phase table as gemm_pp_kernel
+  auto ktile = [&](int t, auto Pc) {
+    constexpr int P = decltype(Pc)::value;
+    constexpr int Q = 1 - P;
+    read_a(4 * P + 0);
+    read_b(4 * P + 1, b0);
+    issue(3, t + 1, 4 * Q + 2);
+    wait_vmcnt<8>();
+    compute(acc[0][0], b0);
+    read_b(4 * P + 2, b1);
+    issue(1, t + 1, 4 * Q + 3);
+    wait_vmcnt<8>();
+    compute(acc[0][1], b1);
+    read_a(4 * P + 3);
+    issue(0, t + 2, 4 * P + 0);
+    compute(acc[1][1], b1);
+    issue(2, t + 2, 4 * P + 1);
+    wait_vmcnt<8>();
+    compute(acc[1][0], b0);
+  };
+
+  zero();
+  issue(0, 0, 0);
+  issue(2, 0, 1);
+  issue(3, 0, 2);
+  issue(1, 0, 3);
+  issue(0, 1, 4);
+  issue(2, 1, 5);
+  wait_vmcnt<8>();
+  __builtin_amdgcn_s_barrier();
+  if (wm == 1) __builtin_amdgcn_s_barrier();   // group 1 runs one barrier behind
+  for (int j = 0; j < my_n; ++j) {
+    for (int t = 0; t < nk; t += 2) {   // nk even
+      ktile(t, std::integral_constant<int, 0>());
+      ktile(t + 1, std::integral_constant<int, 1>());
+    }
+    int m0, nt;
+    coords(j, m0, nt);
+#pragma unroll
+    for (int qm = 0; qm < 2; ++qm)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = m0 + 128 * wm + 64 * qm + 16 * i + 4 * h + r;
+          if (m >= M) continue;
+          bf16* orow = out + (int64_t)m * ldo;
+#pragma unroll
+          for (int jj = 0; jj < 2; ++jj) {
+            if (EPI == EPI_SILU) {
+              const float gg = acc[qm][0][i][jj][r], u = acc[qm][1][i][jj][r];
+              orow[nt * 128 + 32 * wn + 16 * jj + fr] = (bf16)(gg / (1.f + __expf(-gg)) * u);
+            } else {
+#pragma unroll
+              for (int qn = 0; qn < 2; ++qn)
+                orow[nt * TN + 64 * wn + 32 * qn + 16 * jj + fr] = (bf16)acc[qm][qn][i][jj][r];
+            }
+          }
+        }
+    zero();
+    ra_cur = ra_nxt;
+    rw_cur = rw_nxt;
+    ra_nxt = rsrc_a(j + 2);
+    rw_nxt = rsrc_w(j + 2);
+  }
+  if (wm == 0) __builtin_amdgcn_s_barrier();
+  wait_vmcnt<0>();  // no LDS-DMA may outlive the workgroup
+}
+
+int num_cus() {
+  static const int n = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return 256;
+    return v > 0 ? v : 256;
+  }();
+  return n;
+}
+
 int env_int(const char* name, int dflt) {
   const char* v = getenv(name);
   return v ? atoi(v) : dflt;
 }
 
 template <int EPI>
-void launch(int ring, int nwv, bool sp, dim3 grid, hipStream_t st, const at::Tensor& x, const at::Tensor& w, int M, int K,
+void launch(int variant, int ring, int nwv, bool sp, dim3 grid, hipStream_t st, const at::Tensor& x, const at::Tensor& w, int M, int K,
             at::Tensor& out, int MT, int NTL, int F, int gm) {
 #define L(SV, NW, ...)                                                                                         \
   gemm_prefill_kernel<SV, EPI, NW, ##__VA_ARGS__><<<grid, NW * 64, 0, st>>>((const bf16*)x.data_ptr(), x.stride(0),                  \
                                                      (const bf16*)w.data_ptr(), M, K, (bf16*)out.data_ptr(),  \
                                                      out.stride(0), MT, NTL, F, gm)
+  if (variant == 2 && K % 128 == 0) {
+    const int ntiles = (int)grid.x;
+    const int G = std::min(ntiles, num_cus());
+    TORCH_CHECK((int64_t)x.size(0) * x.stride(0) * 2 < (1LL << 32) && w.numel() * 2 < (1LL << 32),
+                "gemm_prefill: operands over 4 GB (32-bit buffer ranges)");
+    gemm_pp2_kernel<EPI><<<G, 512, 0, st>>>((const bf16*)x.data_ptr(), x.stride(0), (const bf16*)w.data_ptr(),
+                                           w.numel(), M, K, (bf16*)out.data_ptr(), out.stride(0), MT, NTL, F, gm,
+                                           ntiles);
+    return;
+  }
+  if (variant == 1 && K % 128 == 0) {
+    gemm_pp_kernel<EPI><<<grid, 512, 0, st>>>((const bf16*)x.data_ptr(), x.stride(0), (const bf16*)w.data_ptr(), M, K,
+                                             (bf16*)out.data_ptr(), out.stride(0), MT, NTL, F, gm);
+    return;
+  }
   static const bool k64 = env_int("LS_PGEMM_K64", 0) != 0;   // measured equal, 2-slot ring: off
   if (k64 && K % 64 == 0) {
     gemm_prefill64_kernel<EPI><<<grid, 512, 0, st>>>((const bf16*)x.data_ptr(), x.stride(0),
@@ -408,7 +825,9 @@ bool gemm_prefill_supported(const at::Tensor& w, bool silu) {
 }
 
 // silu == false: out[M, N] = x . w^T;  silu == true: out[M, F] = silu(x . w[:F]^T) * (x . w[F:]^T)
-void gemm_prefill(at::Tensor out, at::Tensor x, at::Tensor w, bool silu) {
+// variant: -1 = LS_PGEMM_KERNEL (default 1); 0 = the 32-deep ring kernel; 1 = the ping-pong kernel;
+// 2 = its persistent form
+void gemm_prefill(at::Tensor out, at::Tensor x, at::Tensor w, bool silu, int64_t variant) {
   const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16, "x must be bf16 on the GPU");
   TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && x.stride(0) % 8 == 0, "x must be [M, K] with unit column stride");
@@ -429,6 +848,11 @@ void gemm_prefill(at::Tensor out, at::Tensor x, at::Tensor w, bool silu) {
   const int gm = std::max(1, std::min(gm_env, MT));
   auto stream = at::hip::getCurrentHIPStream();
   const dim3 grid((unsigned)(MT * NTL));
-  if (silu) launch<EPI_SILU>(ring, nwv, sp, grid, stream, x, w, (int)M, (int)K, out, MT, NTL, (int)(N / 2), gm);
-  else launch<EPI_STORE>(ring, nwv, sp, grid, stream, x, w, (int)M, (int)K, out, MT, NTL, 0, gm);
+  // default: the ping-pong kernel (1.48-1.50 PFLOP/s on the Llama-3-8B shapes at M = 16384,
+  // 1.23-1.30 for kernel 0; the persistent form 2 measured 1-5 % slower than 1:
+  // profiles/pgemm_ab_r3_pingpong_v1.log, pgemm_ab_r3_persistent_v2.log)
+  static const int var_env = env_int("LS_PGEMM_KERNEL", 1);
+  const int var = variant < 0 ? var_env : (int)variant;
+  if (silu) launch<EPI_SILU>(var, ring, nwv, sp, grid, stream, x, w, (int)M, (int)K, out, MT, NTL, (int)(N / 2), gm);
+  else launch<EPI_STORE>(var, ring, nwv, sp, grid, stream, x, w, (int)M, (int)K, out, MT, NTL, 0, gm);
 }

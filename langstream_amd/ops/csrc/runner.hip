@@ -101,7 +101,7 @@ void gemv_silu_norm(at::Tensor out, at::Tensor o, at::Tensor res, at::Tensor res
                     at::Tensor w);
 void skinny_gemm_add_rmsnorm(at::Tensor out, at::Tensor x, at::Tensor w, at::Tensor residual, at::Tensor norm_w,
                              double eps);
-void gemm_prefill(at::Tensor out, at::Tensor x, at::Tensor w, bool silu);
+void gemm_prefill(at::Tensor out, at::Tensor x, at::Tensor w, bool silu, int64_t variant);
 bool gemm_prefill_supported(const at::Tensor& w, bool silu);
 bool decode_gemm_supported(const at::Tensor& w, bool silu);
 int64_t decode_gemm_workspace(int64_t M, int64_t N, int64_t K, bool silu);
@@ -273,7 +273,7 @@ class LlamaRunner {
         decode_gemm(qkv, x, qkv_w_[l], dg_ws_, c10::nullopt, c10::nullopt, eps_, 0, 0);
       } else if (pgemm(T, qkv_w_[l], false)) {
         qkv = at::empty({T, qkv_w_[l].size(0)}, x.options());
-        gemm_prefill(qkv, x, qkv_w_[l], false);
+        gemm_prefill(qkv, x, qkv_w_[l], false, -1);
       } else {
         qkv = at::linear(x, qkv_w_[l]);
       }
@@ -318,7 +318,7 @@ class LlamaRunner {
       } else {
         if (pgemm(T, o_w_[l], false)) {
           o = at::empty_like(residual);
-          gemm_prefill(o, attn, o_w_[l], false);
+          gemm_prefill(o, attn, o_w_[l], false, -1);
         } else {
           o = at::linear(attn, o_w_[l]);
         }
@@ -336,7 +336,7 @@ class LlamaRunner {
       } else if (pgemm(T, gate_up_w_[l], true)) {
         // prefill: SwiGLU in the GEMM epilogue, the [T, 2F] product never reaches HBM
         a = at::empty({T, gate_up_w_[l].size(0) / 2}, o.options());
-        gemm_prefill(a, o, gate_up_w_[l], true);
+        gemm_prefill(a, o, gate_up_w_[l], true, -1);
       } else {
         at::Tensor gu = at::linear(o, gate_up_w_[l]);
         a = at::empty({T, gu.size(1) / 2}, gu.options());
@@ -370,7 +370,7 @@ class LlamaRunner {
       } else {
         if (pgemm(T, down_w_[l], false)) {
           dn = at::empty_like(residual);
-          gemm_prefill(dn, a, down_w_[l], false);
+          gemm_prefill(dn, a, down_w_[l], false, -1);
         } else {
           dn = at::linear(a, down_w_[l]);
         }
@@ -458,10 +458,12 @@ class LlamaRunner {
     }();
     return on;
   }
-  // Prefill-sized steps (T >= LS_PGEMM_MIN_T, default 8192) run the gate_up projection
-  // on the 256 x 256-tile hand-written GEMM (ops/csrc/gemm_prefill.hip) with SwiGLU in
-  // its epilogue (no [T, 2F] round trip, no silu_and_mul); qkv / o / down stay on
-  // hipBLASLt, which is faster on those plain shapes (profiles/pgemm_bench_*.log).
+  // Prefill-sized steps (T >= LS_PGEMM_MIN_T, default 1024) run the gate_up projection
+  // on the 256 x 256-tile ping-pong GEMM (ops/csrc/gemm_prefill.hip) with SwiGLU in its
+  // epilogue (no [T, 2F] round trip, no silu_and_mul): 2.57 vs 2.74 ms for hipBLASLt +
+  // silu_and_mul at T = 16384, 359 vs 375 us at T = 2048.  qkv / o / down stay on
+  // hipBLASLt, still 4-8 % faster on those plain shapes at T = 16384 and 20-30 % on o /
+  // down at T = 2048 (128 tiles for 256 CUs) (profiles/pgemm_ab_r3_*.log).
   // LS_PGEMM=0: gate_up on hipBLASLt + silu_and_mul too; LS_PGEMM=all: all four here.
   static bool pgemm(int64_t T, const at::Tensor& w, bool silu) {
     static const int mode = [] {
@@ -472,7 +474,7 @@ class LlamaRunner {
     }();
     static const int64_t min_t = [] {
       const char* e = getenv("LS_PGEMM_MIN_T");
-      return e ? (int64_t)atoll(e) : (int64_t)8192;
+      return e ? (int64_t)atoll(e) : (int64_t)1024;
     }();
     return mode > (silu ? 0 : 1) && T >= min_t && gemm_prefill_supported(w, silu);
   }

@@ -10,7 +10,9 @@
   engine scheduler, the other ranks mirror its steps in the native executor's worker
   loop (``LLMEngine.worker_loop``).  Column/row-parallel weights and the all-reduces
   after o_proj / down_proj live in ``models/llama.py`` + ``ops/csrc/runner.hip``; the
-  vocab-parallel LM head is gathered on the last dim.
+  LM head stays vocab-parallel: each rank works on its own vocab slice and only per-row
+  statistics, top-k/top-p histograms and candidates are all-reduced
+  (``ops/csrc/sampling.hip`` tp_sample_*), never the [T, vocab] logits.
 
 Reference: none -- the reference scales only by replica DP
 (``DEPL/agents/AgentResourcesFactory.java:525-540``); TP is the MI355X addition for

@@ -421,6 +421,49 @@ def test_gemm_prefill_silu(M, F, K):
     _close(out, torch.nn.functional.silu(gu[:, :F]) * gu[:, F:], 0.02, 0.02)
 
 
+@pytest.mark.parametrize("variant", [1, 2])
+@pytest.mark.parametrize("M", [1, 300, 2048, 3000, 70000])
+@pytest.mark.parametrize("N,K", [(256, 128), (768, 1024), (512, 2048)])
+def test_gemm_prefill_pingpong(M, N, K, variant):
+    """The ping-pong prefill GEMM (gemm_pp_kernel, variant 1) vs fp32: M tails, several
+    N tiles per group, the shortest K (one iteration of two K tiles)."""
+    torch.manual_seed(M + N + K + 1)
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=DEV) / K ** 0.5).to(torch.bfloat16)
+    out = ops.gemm_prefill(x, w, variant=variant)
+    _close(out, x.float() @ w.float().t(), 0.02, 0.02)
+
+
+@pytest.mark.parametrize("variant", [1, 2])
+@pytest.mark.parametrize("M,F,K", [(77, 128, 256), (1000, 384, 1024), (4096, 256, 512), (40000, 640, 256)])
+def test_gemm_prefill_pingpong_silu(M, F, K, variant):
+    torch.manual_seed(M + F + 1)
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(2 * F, K, device=DEV) / K ** 0.5).to(torch.bfloat16)
+    out = ops.gemm_prefill(x, w, silu=True, variant=variant)
+    gu = x.float().cpu() @ w.float().cpu().t()
+    _close(out, torch.nn.functional.silu(gu[:, :F]) * gu[:, F:], 0.02, 0.02)
+
+
+@pytest.mark.parametrize("name,N,K,silu", [("qkv", 6144, 4096, False), ("o", 4096, 4096, False),
+                                            ("gate_up", 28672, 4096, True), ("down", 4096, 14336, False)])
+@pytest.mark.parametrize("variant", [0, 1, 2])
+def test_gemm_prefill_llama_shapes(name, N, K, silu, variant):
+    """Llama-3-8B projection shapes at a ragged M = 16384 - 77 (edge M tile), against a
+    fp32 GEMM of the same bf16 operands on the GPU (torch.matmul in fp32)."""
+    M = 16384 - 77
+    torch.manual_seed(N + K)
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=DEV) / K ** 0.5).to(torch.bfloat16)
+    out = ops.gemm_prefill(x, w, silu=silu, variant=variant)
+    ref = x.float() @ w.float().t()
+    if silu:
+        ref = torch.nn.functional.silu(ref[:, : N // 2]) * ref[:, N // 2:]
+    err = (out.float() - ref).abs().max().item()
+    assert err <= 0.03 * ref.abs().max().item() + 0.03, (name, err)
+    del ref, out
+
+
 @pytest.mark.parametrize("M,K,N", [(5, 1024, 512), (128, 1024, 512), (256, 4096, 4096), (256, 8192, 256)])
 def test_skinny_gemm_add_rmsnorm(M, K, N):
     # split-K 2 / 2 / 8 (decode o_proj shape) / 16 (past the reduction's unrolled 8)

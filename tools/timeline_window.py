@@ -12,7 +12,7 @@ import sqlite3
 CATS = [("prefill_gemm", lambda n, g: "Cijk" in n and "MT256x256" in n),
         ("hipblaslt_other", lambda n, g: "Cijk" in n),
         ("gemm_prefill(hand)", lambda n, g: "gemm_prefill" in n),
-        ("skinny/gemv", lambda n, g: "skinny" in n or "gemv" in n or "splitk" in n),
+        ("skinny/gemv/dgemm", lambda n, g: "skinny" in n or "gemv" in n or "splitk" in n or "dgemm" in n),
         ("encoder_gemm", lambda n, g: "gemm_fused" in n),
         ("decode_attn", lambda n, g: "decode_attn" in n),
         ("prefill_attn", lambda n, g: "prefill_attn" in n),
