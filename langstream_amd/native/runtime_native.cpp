@@ -14,6 +14,7 @@ namespace py = pybind11;
 void bind_memlog(py::module_& m);
 void bind_shmlog(py::module_& m);
 void bind_tokenizer(py::module_& m);
+void bind_codec(py::module_& m);
 
 namespace {
 
@@ -59,7 +60,7 @@ class BlockAllocator {
 }  // namespace
 
 PYBIND11_MODULE(_lsnative, m) {
-  m.doc() = "langstream_amd native host runtime (memlog, shared-memory log, tokenizers, KV block allocator)";
+  m.doc() = "langstream_amd native host runtime (memlog, shared-memory log, tokenizers, KV block allocator, Kafka checksums)";
   py::class_<BlockAllocator>(m, "BlockAllocator")
       .def(py::init<int>())
       .def("num_free", &BlockAllocator::num_free)
@@ -72,4 +73,5 @@ PYBIND11_MODULE(_lsnative, m) {
   bind_memlog(m);
   bind_shmlog(m);
   bind_tokenizer(m);
+  bind_codec(m);
 }

@@ -268,7 +268,7 @@ def _crc32c_table():
 _CRC = _crc32c_table()
 
 
-def crc32c(data: bytes) -> int:
+def _crc32c_py(data: bytes) -> int:
     c = 0xFFFFFFFF
     t = _CRC
     for x in data:
@@ -276,7 +276,7 @@ def crc32c(data: bytes) -> int:
     return c ^ 0xFFFFFFFF
 
 
-def murmur2(data: bytes) -> int:
+def _murmur2_py(data: bytes) -> int:
     length = len(data)
     seed, m, r = 0x9747B28C, 0x5BD1E995, 24
     h = (seed ^ length) & 0xFFFFFFFF
@@ -300,6 +300,22 @@ def murmur2(data: bytes) -> int:
     h = (h * m) & 0xFFFFFFFF
     h ^= h >> 15
     return h - (1 << 32) if h >= 1 << 31 else h
+
+
+def _native():
+    try:
+        from ...native import lib
+        m = lib()
+        return m if hasattr(m, "crc32c") else None
+    except Exception:  # noqa: BLE001  (no toolchain: the Python loops below)
+        return None
+
+
+_NATIVE = _native()
+# record-batch checksums and the partitioner hash run per batch / per keyed record on
+# every produce and fetch: native (SSE4.2 crc32) when the host runtime is built
+crc32c = _NATIVE.crc32c if _NATIVE is not None else _crc32c_py
+murmur2 = _NATIVE.murmur2 if _NATIVE is not None else _murmur2_py
 
 
 def partition_for_key(key: bytes, num_partitions: int) -> int:

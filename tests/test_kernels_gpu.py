@@ -421,7 +421,7 @@ def test_gemm_prefill_silu(M, F, K):
     _close(out, torch.nn.functional.silu(gu[:, :F]) * gu[:, F:], 0.02, 0.02)
 
 
-@pytest.mark.parametrize("variant", [1, 2])
+@pytest.mark.parametrize("variant", [1, 2, 3])
 @pytest.mark.parametrize("M", [1, 300, 2048, 3000, 70000])
 @pytest.mark.parametrize("N,K", [(256, 128), (768, 1024), (512, 2048)])
 def test_gemm_prefill_pingpong(M, N, K, variant):
@@ -434,7 +434,7 @@ def test_gemm_prefill_pingpong(M, N, K, variant):
     _close(out, x.float() @ w.float().t(), 0.02, 0.02)
 
 
-@pytest.mark.parametrize("variant", [1, 2])
+@pytest.mark.parametrize("variant", [1, 2, 3])
 @pytest.mark.parametrize("M,F,K", [(77, 128, 256), (1000, 384, 1024), (4096, 256, 512), (40000, 640, 256)])
 def test_gemm_prefill_pingpong_silu(M, F, K, variant):
     torch.manual_seed(M + F + 1)
@@ -447,7 +447,7 @@ def test_gemm_prefill_pingpong_silu(M, F, K, variant):
 
 @pytest.mark.parametrize("name,N,K,silu", [("qkv", 6144, 4096, False), ("o", 4096, 4096, False),
                                             ("gate_up", 28672, 4096, True), ("down", 4096, 14336, False)])
-@pytest.mark.parametrize("variant", [0, 1, 2])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
 def test_gemm_prefill_llama_shapes(name, N, K, silu, variant):
     """Llama-3-8B projection shapes at a ragged M = 16384 - 77 (edge M tile), against a
     fp32 GEMM of the same bf16 operands on the GPU (torch.matmul in fp32)."""

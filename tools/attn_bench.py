@@ -46,6 +46,9 @@ def main():
                          "time the attention kernel with rocprofv3 in this mode")
     ap.add_argument("--pool-gb", type=float, default=0.0,
                     help="scatter the blocks over a KV pool of this size (TLB reach), like a real engine")
+    ap.add_argument("--rope", action="store_true",
+                    help="time the decode-only variant with RoPE + the KV write fused in "
+                         "(paged_decode_attention_rope over an un-rotated qkv buffer, as the engine runs it)")
     a = ap.parse_args()
     Hq, Hkv, D = 32, 8, 128
     dev, bf = "cuda", torch.bfloat16
@@ -84,20 +87,36 @@ def main():
             gx = torch.randn(B, 4096, device=dev, dtype=bf)
             gw = torch.randn(28672, 4096, device=dev, dtype=bf) * 0.02
 
+        if a.rope:
+            qkv = torch.randn(B, (Hq + 2 * Hkv) * D, device=dev, dtype=bf)
+            pos = (cl - 1).to(torch.int32)
+            half = torch.arange(0, D // 2, device=dev, dtype=torch.float32)
+            inv = 1.0 / (500000.0 ** (2 * half / D))
+            ang = torch.arange(0, 8192, device=dev, dtype=torch.float32)[:, None] * inv[None, :]
+            cos_sin = torch.cat([ang.cos(), ang.sin()], dim=1).contiguous()
+            # the new token's cache slot: its position inside the sequence's last block
+            lastblk = bt.gather(1, ((cl.long() - 1) // 64).view(-1, 1)).view(-1).long()
+            slots = lastblk * 64 + (cl.long() - 1) % 64
+
         def call():
             if a.interleave_gemm:
                 torch.nn.functional.linear(gx, gw)
             k_, v_ = kvs[it[0] % len(kvs)]
             it[0] += 1
-            ops.hip().paged_decode_attention(o, q, k_, v_, bt, cl, scale, nsplit, mbps, ws)
+            if a.rope:
+                ops.hip().paged_decode_attention_rope(o, qkv, pos, cos_sin, slots, k_, v_, bt, cl, scale, nsplit,
+                                                      mbps, ws)
+            else:
+                ops.hip().paged_decode_attention(o, q, k_, v_, bt, cl, scale, nsplit, mbps, ws)
         us = timeit(call)
-        ops.hip().paged_decode_attention(o, q, kc, vc, bt, cl, scale, nsplit, mbps, ws)
+        if not a.rope:
+            ops.hip().paged_decode_attention(o, q, kc, vc, bt, cl, scale, nsplit, mbps, ws)
         byts = int(ctxs.sum()) * Hkv * D * 2 * 2
         rec = {"B": B, "ctx": ctx, "us": round(us, 2), "TBps": round(byts / us / 1e6, 2),
                "kernel": "decode_attn_kernel", "wpp": os.environ.get("LS_ATTN_WPP", "auto"),
                "pipe": os.environ.get("LS_ATTN_PIPE", "1"),
-               "ragged": a.ragged, "pool_gb": a.pool_gb, "ring": a.ring}
-        if (B <= 16 or (a.check_all and B * ctx <= 256 * 1024)) and a.pool_gb == 0:
+               "ragged": a.ragged, "pool_gb": a.pool_gb, "ring": a.ring, "rope": a.rope}
+        if not a.rope and (B <= 16 or (a.check_all and B * ctx <= 256 * 1024)) and a.pool_gb == 0:
             exp = ref.paged_decode_attention(q.float().cpu().reshape(B, Hq, D), kc.float().cpu(), vc.float().cpu(),
                                              bt.cpu(), cl.cpu(), scale).reshape(B, Hq * D)
             rec["max_err"] = round(float((o.float().cpu() - exp).abs().max()), 4)

@@ -36,7 +36,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ms", default="2048,16384")
     ap.add_argument("--only", default="")
-    ap.add_argument("--variants", default="1,2")
+    ap.add_argument("--variants", default="1,3")
     ap.add_argument("--rounds", type=int, default=5)
     a = ap.parse_args()
     dev = "cuda"
