@@ -69,6 +69,9 @@ bool decode_gemm_supported(const at::Tensor& w, bool silu);
 int64_t decode_gemm_workspace(int64_t M, int64_t N, int64_t K, bool silu);
 void decode_gemm(at::Tensor out, at::Tensor x, at::Tensor w, at::Tensor workspace, c10::optional<at::Tensor> residual,
                  c10::optional<at::Tensor> norm_w, double eps, int64_t bn_force, int64_t splits_force);
+void decode_gemm_qkv_rope(at::Tensor qkv, at::Tensor x, at::Tensor w, at::Tensor workspace, at::Tensor pos,
+                          at::Tensor cos_sin, at::Tensor slots, at::Tensor k_cache, at::Tensor v_cache, int64_t Hq,
+                          int64_t Hkv);
 void decode_gemm_silu(at::Tensor out, at::Tensor x, at::Tensor w, at::Tensor workspace, at::Tensor tickets,
                       at::Tensor err, int64_t splits);
 void decode_gemm_ablate(at::Tensor x, at::Tensor w, at::Tensor workspace, int64_t abl, int64_t splits,
@@ -124,6 +127,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("residual") = py::none(), py::arg("norm_w") = py::none(), py::arg("eps") = 1e-5,
         py::arg("bn") = 0, py::arg("splits") = 0);
   m.def("decode_gemm_ablate", &decode_gemm_ablate);
+  m.def("decode_gemm_qkv_rope", &decode_gemm_qkv_rope);
   m.def("decode_gemm_silu", &decode_gemm_silu, py::arg("out"), py::arg("x"), py::arg("w"), py::arg("workspace"),
         py::arg("tickets"), py::arg("err"), py::arg("splits") = 0);
   bind_runners(m);

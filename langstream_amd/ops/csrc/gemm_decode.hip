@@ -445,6 +445,126 @@ void decode_gemm(at::Tensor out, at::Tensor x, at::Tensor w, at::Tensor workspac
     splitk_reduce_launch(part, S, M, N, (bf16*)out.data_ptr(), out.stride(0), st);
 }
 
+// ---------------------------------------------------------------------------------
+// qkv projection of a decode-only step: the split-K reduction fused with RoPE and the
+// paged KV-cache write.  One thread per (row m, head hd, 4-dim group c < D/8): it sums
+// the S partial slabs of dims 4c..4c+3 and D/2+4c..+3 (the RoPE pairs), rotates q and k
+// heads in f32 (cos / sin of position pos[m]), stores the bf16 row, and for k / v heads
+// writes the paged cache (K rows, V transposed: see rope.hip).  This replaces the plain
+// split-K reduce + the separate RoPE/cache pass (the attention then runs its un-fused
+// form: the fused-RoPE attention measured 91.6 vs 80.4 us at B = 256, ctx 410,
+// profiles/decode_attn_rope_isolated_r3.log).
+template <int D>
+__global__ void __launch_bounds__(256) splitk_reduce_rope_kernel(
+    const float* __restrict__ part, int S, int M, int N, bf16* __restrict__ out, int64_t ldo,
+    const int32_t* __restrict__ pos, const float* __restrict__ cos_sin, int max_pos,
+    const int64_t* __restrict__ slots, int64_t nslots, bf16* __restrict__ kc, bf16* __restrict__ vc, int Hq, int Hkv,
+    int BS) {
+  constexpr int HALF = D / 2, G4 = HALF / 4;
+  const int H = Hq + 2 * Hkv;
+  const int64_t tid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (tid >= (int64_t)M * H * G4) return;
+  const int c = (int)(tid % G4);
+  const int64_t rest = tid / G4;
+  const int hd = (int)(rest % H);
+  const int m = (int)(rest / H);
+  const int64_t MN = (int64_t)M * N;
+  const int64_t e0 = (int64_t)m * N + (int64_t)hd * D + 4 * c;
+  constexpr int SMAX = 8;
+  float4 lo[SMAX], hi[SMAX];
+#pragma unroll
+  for (int s = 0; s < SMAX; ++s)
+    if (s < S) {
+      lo[s] = *reinterpret_cast<const float4*>(part + s * MN + e0);
+      hi[s] = *reinterpret_cast<const float4*>(part + s * MN + e0 + HALF);
+    }
+  float a[4] = {lo[0].x, lo[0].y, lo[0].z, lo[0].w}, b[4] = {hi[0].x, hi[0].y, hi[0].z, hi[0].w};
+#pragma unroll
+  for (int s = 1; s < SMAX; ++s)
+    if (s < S) {
+      a[0] += lo[s].x; a[1] += lo[s].y; a[2] += lo[s].z; a[3] += lo[s].w;
+      b[0] += hi[s].x; b[1] += hi[s].y; b[2] += hi[s].z; b[3] += hi[s].w;
+    }
+  for (int s = SMAX; s < S; ++s) {
+    const float4 x = *reinterpret_cast<const float4*>(part + s * MN + e0);
+    const float4 y = *reinterpret_cast<const float4*>(part + s * MN + e0 + HALF);
+    a[0] += x.x; a[1] += x.y; a[2] += x.z; a[3] += x.w;
+    b[0] += y.x; b[1] += y.y; b[2] += y.z; b[3] += y.w;
+  }
+  if (hd < Hq + Hkv) {
+    const int p = min(max(pos[m], 0), max_pos - 1);
+    const float4 co = *reinterpret_cast<const float4*>(cos_sin + (int64_t)p * D + 4 * c);
+    const float4 si = *reinterpret_cast<const float4*>(cos_sin + (int64_t)p * D + HALF + 4 * c);
+    const float cv[4] = {co.x, co.y, co.z, co.w}, sv[4] = {si.x, si.y, si.z, si.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float x1 = a[j], x2 = b[j];
+      a[j] = x1 * cv[j] - x2 * sv[j];
+      b[j] = x2 * cv[j] + x1 * sv[j];
+    }
+  }
+  const bf16x4 va = {(bf16)a[0], (bf16)a[1], (bf16)a[2], (bf16)a[3]};
+  const bf16x4 vb = {(bf16)b[0], (bf16)b[1], (bf16)b[2], (bf16)b[3]};
+  bf16* orow = out + (int64_t)m * ldo + (int64_t)hd * D + 4 * c;
+  *reinterpret_cast<bf16x4*>(orow) = va;
+  *reinterpret_cast<bf16x4*>(orow + HALF) = vb;
+  if (hd < Hq) return;
+  const int64_t sl = slots[m];
+  if (sl < 0 || sl >= nslots) return;
+  const int64_t blk = sl / BS, off = sl - blk * BS;
+  if (hd < Hq + Hkv) {
+    bf16* kd = kc + ((blk * Hkv + (hd - Hq)) * BS + off) * D + 4 * c;
+    *reinterpret_cast<bf16x4*>(kd) = va;
+    *reinterpret_cast<bf16x4*>(kd + HALF) = vb;
+  } else {
+    bf16* vd = vc + ((blk * Hkv + (hd - Hq - Hkv)) * (int64_t)D) * BS + off;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      vd[(int64_t)(4 * c + j) * BS] = va[j];
+      vd[(int64_t)(HALF + 4 * c + j) * BS] = vb[j];
+    }
+  }
+}
+
+void rope_and_cache(at::Tensor qkv, at::Tensor pos, at::Tensor cos_sin, at::Tensor slots, at::Tensor k_cache,
+                    at::Tensor v_cache, int64_t Hq, int64_t Hkv, bool apply_rope);
+
+// qkv[M, (Hq + 2 Hkv) D] = RoPE(x . w^T) for q and k heads, with the step's K / V rows
+// written to the paged cache (the same contract as decode_gemm + rope_and_cache).
+void decode_gemm_qkv_rope(at::Tensor qkv, at::Tensor x, at::Tensor w, at::Tensor workspace, at::Tensor pos,
+                          at::Tensor cos_sin, at::Tensor slots, at::Tensor k_cache, at::Tensor v_cache, int64_t Hq,
+                          int64_t Hkv) {
+  check_xw(x, w);
+  const int M = (int)x.size(0), K = (int)x.size(1), N = (int)w.size(0);
+  const int D = (int)k_cache.size(3), BSZ = (int)k_cache.size(2);
+  TORCH_CHECK(N == (Hq + 2 * Hkv) * D && N % 128 == 0, "decode_gemm_qkv_rope: qkv width");
+  TORCH_CHECK(qkv.scalar_type() == at::kBFloat16 && qkv.size(0) == M && qkv.size(1) == N && qkv.stride(1) == 1);
+  TORCH_CHECK(pos.scalar_type() == at::kInt && pos.numel() >= M && slots.scalar_type() == at::kLong &&
+              slots.numel() >= M && cos_sin.scalar_type() == at::kFloat && cos_sin.is_contiguous() &&
+              cos_sin.size(1) == D, "decode_gemm_qkv_rope: pos / slots / cos_sin");
+  TORCH_CHECK(k_cache.is_contiguous() && v_cache.is_contiguous() && v_cache.size(2) == D && v_cache.size(3) == BSZ);
+  const int bn = pick_bn(N), tiles = N / bn;
+  const int S = pick_split(tiles, K, 4);
+  if (S == 1 || D != 128) {
+    decode_gemm(qkv, x, w, workspace, c10::nullopt, c10::nullopt, 1e-5, 0, 0);
+    rope_and_cache(qkv, pos, cos_sin, slots, k_cache, v_cache, Hq, Hkv, true);
+    return;
+  }
+  TORCH_CHECK(workspace.scalar_type() == at::kFloat && workspace.numel() >= (int64_t)S * M * N,
+              "decode_gemm_qkv_rope: workspace too small");
+  auto st = at::hip::getCurrentHIPStream();
+  float* part = workspace.data_ptr<float>();
+  if (bn == 256)
+    dgemm_launch<256, EPI_PARTIAL>(S, tiles, st, x, w, M, N, K, nullptr, 0, part, 0, nullptr, nullptr, nullptr);
+  else
+    dgemm_launch<128, EPI_PARTIAL>(S, tiles, st, x, w, M, N, K, nullptr, 0, part, 0, nullptr, nullptr, nullptr);
+  const int64_t threads = (int64_t)M * (Hq + 2 * Hkv) * (D / 8);
+  splitk_reduce_rope_kernel<128><<<(unsigned)((threads + 255) / 256), 256, 0, st>>>(
+      part, S, M, N, (bf16*)qkv.data_ptr(), qkv.stride(0), pos.data_ptr<int32_t>(), cos_sin.data_ptr<float>(),
+      (int)cos_sin.size(0), slots.data_ptr<int64_t>(), k_cache.size(0) * BSZ, (bf16*)k_cache.data_ptr(),
+      (bf16*)v_cache.data_ptr(), (int)Hq, (int)Hkv, BSZ);
+}
+
 // out[M, F] = silu(x . w[:F]^T) * (x . w[F:]^T).  tickets: int32 [2 * (F / 128)] zeros
 // once at allocation (monotonic, never reset); err: int32 [1].
 // splits: 0 = automatic (2 with the in-launch combine), 1 = one launch over full K.

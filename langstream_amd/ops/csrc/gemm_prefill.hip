@@ -531,144 +531,6 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(const bf16* __restrict__ x
       }
 }
 
-// The same ping-pong schedule on v_mfma_f32_32x32x16_bf16 (guide §5.4 rule 28: the chip
-// can hold a different clock on the two bf16 MFMA shapes at equal FLOP per cycle): per
-// phase 2 (M) x 1 (N) output tiles of 32 x 32, four 16-deep k-steps, 8 MFMAs.
-template <int EPI>
-__global__ void __launch_bounds__(512) gemm_pp32_kernel(const bf16* __restrict__ x, int64_t ldx,
-                                                        const bf16* __restrict__ w, int M, int K,
-                                                        bf16* __restrict__ out, int64_t ldo, int MT, int NTL, int F,
-                                                        int group_m) {
-  __shared__ __attribute__((aligned(1024))) char lds[8 * HT];
-  const int lane = threadIdx.x & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int logical = xcd_remap(blockIdx.x, gridDim.x);
-  const int per_group = group_m * NTL;
-  const int grp = logical / per_group, first = grp * group_m;
-  const int gsz = min(MT - first, group_m);
-  const int rem = logical - grp * per_group;
-  const int mt = first + rem % gsz, nt = rem / gsz;
-  const int m0 = mt * TM;
-  const int nk = K / 64;
-  const bf16* src[4][2];
-#pragma unroll
-  for (int e = 0; e < 2; ++e) {
-    const int r = 16 * wid + 8 * e + (lane >> 3);
-    const int koff = ((lane & 7) ^ ((r >> 1) & 7)) * 8;
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int arow = m0 + (r & 63) + 128 * (r >> 6) + 64 * q;
-      src[q][e] = x + (int64_t)min(arow, M - 1) * ldx + koff;
-      int wrow;
-      if (EPI == EPI_SILU) wrow = (q == 0 ? 0 : F) + nt * 128 + r;
-      else wrow = nt * TN + 64 * (r >> 5) + 32 * q + (r & 31);
-      src[2 + q][e] = w + (int64_t)wrow * K + koff;
-    }
-  }
-  auto issue = [&](int type, int tile, int slot) {
-    const int ko = min(tile, nk - 1) * 64;
-#pragma unroll
-    for (int e = 0; e < 2; ++e) glds16(src[type][e] + ko, lds + slot * HT + (2 * wid + e) * 1024);
-  };
-  const int wm = wid >> 2, wn = wid & 3;
-  const int fr = lane & 31, hh = lane >> 5;
-  const int fsw = (fr >> 1) & 7;
-  // 32x32x16 operand: lane holds row (lane & 31), k 8 (lane >> 5) .. +7 of a 16-deep k-step
-  int koffs[4];
-#pragma unroll
-  for (int ks = 0; ks < 4; ++ks) koffs[ks] = 16 * ((2 * ks + hh) ^ fsw);
-  const int arow = (64 * wm + fr) * 128, brow = (32 * wn + fr) * 128;
-  bf16x8 a[2][4], b0[4], b1[4];
-  auto read_a = [&](int slot) {
-    const char* base = lds + slot * HT + arow;
-#pragma unroll
-    for (int im = 0; im < 2; ++im)
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) a[im][ks] = __builtin_bit_cast(bf16x8, ld16(base + im * 4096 + koffs[ks]));
-  };
-  auto read_b = [&](int slot, bf16x8 (&b)[4]) {
-    const char* base = lds + slot * HT + brow;
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) b[ks] = __builtin_bit_cast(bf16x8, ld16(base + koffs[ks]));
-  };
-  f32x16 acc[2][2][2];
-#pragma unroll
-  for (int qm = 0; qm < 2; ++qm)
-#pragma unroll
-    for (int qn = 0; qn < 2; ++qn)
-#pragma unroll
-      for (int im = 0; im < 2; ++im)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) acc[qm][qn][im][i] = 0.f;
-  auto compute = [&](f32x16 (&c)[2], const bf16x8 (&bb)[4]) {
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks)
-#pragma unroll
-      for (int im = 0; im < 2; ++im) c[im] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[im][ks], bb[ks], c[im], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-  };
-  auto ktile = [&](int t, auto Pc) {
-    constexpr int P = decltype(Pc)::value;
-    constexpr int Q = 1 - P;
-    read_a(4 * P + 0);
-    read_b(4 * P + 1, b0);
-    issue(3, t + 1, 4 * Q + 2);
-    wait_vmcnt<8>();
-    compute(acc[0][0], b0);
-    read_b(4 * P + 2, b1);
-    issue(1, t + 1, 4 * Q + 3);
-    wait_vmcnt<8>();
-    compute(acc[0][1], b1);
-    read_a(4 * P + 3);
-    issue(0, t + 2, 4 * P + 0);
-    compute(acc[1][1], b1);
-    issue(2, t + 2, 4 * P + 1);
-    wait_vmcnt<8>();
-    compute(acc[1][0], b0);
-  };
-  issue(0, 0, 0);
-  issue(2, 0, 1);
-  issue(3, 0, 2);
-  issue(1, 0, 3);
-  issue(0, 1, 4);
-  issue(2, 1, 5);
-  wait_vmcnt<8>();
-  __builtin_amdgcn_s_barrier();
-  if (wm == 1) __builtin_amdgcn_s_barrier();
-  for (int t = 0; t < nk; t += 2) {
-    ktile(t, std::integral_constant<int, 0>());
-    ktile(t + 1, std::integral_constant<int, 1>());
-  }
-  if (wm == 0) __builtin_amdgcn_s_barrier();
-  wait_vmcnt<0>();
-  // acc[qm][qn][im][i] = C[128 wm + 64 qm + 32 im + 8 (i >> 2) + 4 hh + (i & 3)][64 wn + 32 qn + fr]
-#pragma unroll
-  for (int qm = 0; qm < 2; ++qm)
-#pragma unroll
-    for (int im = 0; im < 2; ++im)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int m = m0 + 128 * wm + 64 * qm + 32 * im + 8 * (i >> 2) + 4 * hh + (i & 3);
-        if (m >= M) continue;
-        bf16* orow = out + (int64_t)m * ldo;
-        if (EPI == EPI_SILU) {
-          const float g = acc[qm][0][im][i], u = acc[qm][1][im][i];
-          orow[nt * 128 + 32 * wn + fr] = (bf16)(g / (1.f + __expf(-g)) * u);
-        } else {
-#pragma unroll
-          for (int qn = 0; qn < 2; ++qn) orow[nt * TN + 64 * wn + 32 * qn + fr] = (bf16)acc[qm][qn][im][i];
-        }
-      }
-}
-
 // ---------------------------------------------------------------------------------
 // Persistent form of the ping-pong kernel: one workgroup per CU walks its tiles (round r
 // of G = gridDim.x tiles: logical tile r*G + xcd_remap(blockIdx)) as ONE stream of K tiles,
@@ -913,11 +775,6 @@ void launch(int variant, int ring, int nwv, bool sp, dim3 grid, hipStream_t st, 
                                            ntiles);
     return;
   }
-  if (variant == 3 && K % 128 == 0) {
-    gemm_pp32_kernel<EPI><<<grid, 512, 0, st>>>((const bf16*)x.data_ptr(), x.stride(0), (const bf16*)w.data_ptr(), M,
-                                               K, (bf16*)out.data_ptr(), out.stride(0), MT, NTL, F, gm);
-    return;
-  }
   if (variant == 1 && K % 128 == 0) {
     gemm_pp_kernel<EPI><<<grid, 512, 0, st>>>((const bf16*)x.data_ptr(), x.stride(0), (const bf16*)w.data_ptr(), M, K,
                                              (bf16*)out.data_ptr(), out.stride(0), MT, NTL, F, gm);
@@ -969,7 +826,8 @@ bool gemm_prefill_supported(const at::Tensor& w, bool silu) {
 
 // silu == false: out[M, N] = x . w^T;  silu == true: out[M, F] = silu(x . w[:F]^T) * (x . w[F:]^T)
 // variant: -1 = LS_PGEMM_KERNEL (default 1); 0 = the 32-deep ring kernel; 1 = the ping-pong kernel;
-// 2 = its persistent form; 3 = the ping-pong kernel on 32x32x16 MFMA
+// 2 = its persistent form (the same schedule on 32x32x16 MFMA measured 1.27-1.29 PFLOP/s,
+// 13-15 % below 16x16x32: profiles/pgemm_ab_r3_mfma32_v3.log, removed)
 void gemm_prefill(at::Tensor out, at::Tensor x, at::Tensor w, bool silu, int64_t variant) {
   const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16, "x must be bf16 on the GPU");

@@ -324,6 +324,161 @@ __global__ void __launch_bounds__(256) knn_filter_kernel(const bf16* __restrict_
   }
 }
 
+// Main pass for large query batches (Q >= 128, dim <= 512): 256 queries per workgroup,
+// 8 waves x 32 queries whose Q^T fragments stay in REGISTERS for the whole launch, and
+// the workgroup's row range streamed ONCE through a ring of LDS stages (64 rows each,
+// LDS-DMA) that all 8 waves read.  knn_filter_kernel instead re-reads every row from L2
+// per 64 queries straight into registers, which bounded it by the L2 -> CU path at
+// Q = 1024 (412 GB/s effective over 1M x 384; profiles/knn_filter64_r2i.log).
+//   * LDS image: row r's 16-B chunk p holds the row's chunk p ^ (r & 15) (rows are a
+//     multiple of 256 B, so without it the 16 rows of an A-fragment lane group would
+//     sit on the same banks); the LDS-DMA writes lane-linear, so the permutation is
+//     applied to the SOURCE address (cdna_hip_programming §5.4 rule 21);
+//   * per 64-row tile a wave reads 4 x KS A fragments and issues 8 x KS MFMAs (two
+//     16-query groups share each fragment);
+//   * scores above the query's sample threshold are appended exactly as in
+//     knn_filter_kernel (same candidate lists, counters and overflow flags).
+template <int DIM>
+__global__ void __launch_bounds__(512) knn_filter_q256_kernel(const bf16* __restrict__ X, int64_t N,
+                                                              const bf16* __restrict__ Qm, int Qn,
+                                                              float* __restrict__ cand_s, int32_t* __restrict__ cand_i,
+                                                              int* __restrict__ ctrl, int64_t cap, int64_t row_begin,
+                                                              int rows_per_wg, int nqb) {
+  constexpr int KS = DIM / 32;
+  constexpr int RB = DIM * 2;                    // bytes per row
+  constexpr int TR = 64;                         // rows per LDS stage
+  constexpr int SB = TR * RB;                    // stage bytes
+  constexpr int CAPW = 128;                      // per-wave LDS candidate buffer entries
+  constexpr int CBYTES = 8 * CAPW * 12;
+  constexpr int NST = 3 * SB + CBYTES <= 160 * 1024 ? 3 : 2;
+  constexpr int GPW = SB / (8 * 1024);           // LDS-DMA instructions per wave per stage
+  static_assert(RB % 256 == 0 && SB % 8192 == 0, "rows must be a multiple of 256 B");
+  __shared__ __attribute__((aligned(1024))) char lds[NST * SB + CBYTES];
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int fr = lane & 15, h = lane >> 4;
+  // candidates above the threshold go to this wave's LDS buffer (ballot-compacted, no
+  // atomics) and reach the global lists only in flush(): a returning global atomic inside
+  // the tile loop made hipcc drain vmcnt(0) every tile, i.e. the whole LDS-DMA ring
+  float* c_s = reinterpret_cast<float*>(lds + NST * SB) + wid * CAPW;
+  int* c_r = reinterpret_cast<int*>(lds + NST * SB + 8 * CAPW * 4) + wid * CAPW;
+  int* c_q = reinterpret_cast<int*>(lds + NST * SB + 8 * CAPW * 8) + wid * CAPW;
+  int ccount = 0;   // wave-uniform
+  auto flush = [&]() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (int e = lane; e < ccount; e += 64) {
+      const int qi = c_q[e];
+      const int slot = __hip_atomic_fetch_add(ctrl + qi, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (slot < cap) {
+        cand_s[(int64_t)qi * cap + slot] = c_s[e];
+        cand_i[(int64_t)qi * cap + slot] = c_r[e];
+      } else {
+        ctrl[2 * Qn + qi] = 1;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    ccount = 0;
+  };
+  // XCD-aware: the query blocks of one row range are consecutive logical ids
+  const int logical = xcd_remap(blockIdx.x, gridDim.x);
+  const int rb = logical / nqb, qb = logical - rb * nqb;
+  const int64_t r0 = row_begin + (int64_t)rb * rows_per_wg;
+  const int64_t r1 = min(N, r0 + rows_per_wg);
+  if (r0 >= r1) return;
+  const int ntile = (int)((r1 - r0 + TR - 1) / TR);
+
+  // this wave's 32 queries: groups g = 0, 1 of 16; lane (fr, h) holds query 16g + fr, dims 32ks + 8h..
+  const int q0 = qb * 256 + wid * 32;
+  bf16x8 qf[2][KS];
+  float thr[2];
+#pragma unroll
+  for (int g = 0; g < 2; ++g) {
+    const int qi = q0 + 16 * g + fr;
+    const bool ok = qi < Qn;
+    const bf16* qp = Qm + (int64_t)(ok ? qi : 0) * DIM + 8 * h;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+      qf[g][ks] = __builtin_bit_cast(bf16x8, ok ? ld16(qp + 32 * ks) : make_uint4(0, 0, 0, 0));
+    thr[g] = ok ? key2f(ctrl[Qn + qi]) : INFINITY;
+  }
+  // consume the query fragments here: otherwise hipcc places their vmcnt wait at the first
+  // MFMA inside the tile loop, where a vmcnt(0) also drains the LDS-DMA ring every tile
+#pragma unroll
+  for (int g = 0; g < 2; ++g) {
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) asm volatile("" ::"v"(qf[g][ks]));
+    asm volatile("" ::"v"(thr[g]));
+  }
+  // LDS-DMA: instruction j of wave w fills bytes [(w*GPW + j) * 1024, +1024) of a stage
+  int src_row[GPW], src_off[GPW];
+#pragma unroll
+  for (int j = 0; j < GPW; ++j) {
+    const int o = (wid * GPW + j) * 1024 + lane * 16;
+    const int r = o / RB, p = (o % RB) / 16;
+    src_row[j] = r;
+    src_off[j] = ((p ^ (r & 15)) * 16);
+  }
+  auto issue = [&](int t, int slot) {
+    const int64_t base = r0 + (int64_t)min(t, ntile - 1) * TR;   // past the end: reload the last tile (dead slot)
+#pragma unroll
+    for (int j = 0; j < GPW; ++j) {
+      const int64_t row = min(base + src_row[j], N - 1);
+      glds16((const bf16*)((const char*)X + row * RB + src_off[j]), lds + slot * SB + (wid * GPW + j) * 1024);
+    }
+  };
+  // A fragment of 16-row subtile i, k-step ks: row 16i + fr, chunk 4ks + h (swizzled)
+  int aoff[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) aoff[ks] = fr * RB + (((4 * ks + h) ^ fr) * 16);
+
+  for (int s = 0; s < NST - 1; ++s) issue(s, s);
+  for (int t = 0; t < ntile; ++t) {
+    wait_vmcnt<(NST - 2) * GPW>();   // this wave's DMA of tile t landed (tiles t+1.. may be in flight)
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();    // every wave's part of tile t landed; tile t-1's slot is free
+    __builtin_amdgcn_sched_barrier(0);
+    issue(t + NST - 1, (t + NST - 1) % NST);
+    const char* st = lds + (t % NST) * SB;
+    const int64_t trow = r0 + (int64_t)t * TR;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      bf16x8 af[KS];
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) af[ks] = __builtin_bit_cast(bf16x8, ld16(st + i * 16 * RB + aoff[ks]));
+      f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+        for (int g = 0; g < 2; ++g) acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks], qf[g][ks], acc[g], 0, 0, 0);
+      // acc[g][rr] = score(row trow + 16i + 4h + rr, query q0 + 16g + fr)
+#pragma unroll
+      for (int g = 0; g < 2; ++g)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+          const int64_t row = trow + 16 * i + 4 * h + rr;
+          const bool hit = acc[g][rr] > thr[g] && row < r1;
+          const uint64_t mask = __ballot(hit);
+          if (mask == 0) continue;
+          const int nh = __popcll(mask);
+          if (ccount + nh > CAPW) flush();   // rare: drains the DMA ring once
+          const int pos = ccount + __popcll(mask & ((1ull << lane) - 1ull));
+          if (hit) {
+            c_s[pos] = acc[g][rr];
+            c_r[pos] = (int)row;
+            c_q[pos] = q0 + 16 * g + fr;
+          }
+          ccount += nh;
+        }
+    }
+  }
+  wait_vmcnt<0>();   // no LDS-DMA may outlive the workgroup
+  flush();
+}
+
 __global__ void knn_init_kernel(int* __restrict__ ctrl, int Qn) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < Qn) {
@@ -448,7 +603,37 @@ void knn_topk(at::Tensor X, at::Tensor Q, int64_t K, at::Tensor out_s, at::Tenso
     DISPATCH_DIM(LAUNCH_E)
 #undef LAUNCH_E
   };
+  static const int q256_min = getenv("LS_KNN_Q256_MIN") ? atoi(getenv("LS_KNN_Q256_MIN")) : 128;
+  const bool q256 = Qn >= q256_min && (dim == 128 || dim == 256 || dim == 384 || dim == 512);
+  auto filter_q256 = [&](int c0, int nc) {
+    const int64_t row_begin = (int64_t)c0 * CH;
+    const int64_t rows = std::min<int64_t>(N, (int64_t)(c0 + nc) * CH) - row_begin;
+    if (rows <= 0) return;
+    const int nqb = (Qn + 255) / 256;
+    // ~1024 workgroups (4 per CU) over rows x query blocks, whole 64-row tiles per workgroup
+    const int64_t nrb_target = std::max<int64_t>(1, 1024 / nqb);
+    int64_t rpw = (rows + nrb_target - 1) / nrb_target;
+    rpw = std::max<int64_t>(256, (rpw + 63) / 64 * 64);
+    const int nrb = (int)((rows + rpw - 1) / rpw);
+    dim3 grid(nrb * nqb);
+#define LAUNCH_Q(DD)                                                                                                \
+  knn_filter_q256_kernel<DD><<<grid, 512, 0, stream>>>((const bf16*)X.data_ptr(), N, (const bf16*)Q.data_ptr(), Qn, \
+                                                       ws_s.data_ptr<float>(), ws_i.data_ptr<int32_t>(), ctrl, cap,  \
+                                                       row_begin, (int)rpw, nqb)
+    switch (dim) {
+      case 128: LAUNCH_Q(128); break;
+      case 256: LAUNCH_Q(256); break;
+      case 384: LAUNCH_Q(384); break;
+      case 512: LAUNCH_Q(512); break;
+      default: break;
+    }
+#undef LAUNCH_Q
+  };
   auto filter = [&](int c0, int nc) {
+    if (q256) {
+      filter_q256(c0, nc);
+      return;
+    }
     dim3 grid(nc * nqf);
 #define LAUNCH_F(DD)                                                                                            \
   knn_filter_kernel<DD><<<grid, 256, 0, stream>>>((const bf16*)X.data_ptr(), N, (const bf16*)Q.data_ptr(), Qn, \

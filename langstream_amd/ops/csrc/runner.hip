@@ -105,6 +105,9 @@ void gemm_prefill(at::Tensor out, at::Tensor x, at::Tensor w, bool silu, int64_t
 bool gemm_prefill_supported(const at::Tensor& w, bool silu);
 bool decode_gemm_supported(const at::Tensor& w, bool silu);
 int64_t decode_gemm_workspace(int64_t M, int64_t N, int64_t K, bool silu);
+void decode_gemm_qkv_rope(at::Tensor qkv, at::Tensor x, at::Tensor w, at::Tensor workspace, at::Tensor pos,
+                          at::Tensor cos_sin, at::Tensor slots, at::Tensor k_cache, at::Tensor v_cache, int64_t Hq,
+                          int64_t Hkv);
 void decode_gemm(at::Tensor out, at::Tensor x, at::Tensor w, at::Tensor workspace, c10::optional<at::Tensor> residual,
                  c10::optional<at::Tensor> norm_w, double eps, int64_t bn_force, int64_t splits_force);
 void decode_gemm_silu(at::Tensor out, at::Tensor x, at::Tensor w, at::Tensor workspace, at::Tensor tickets,
@@ -260,8 +263,10 @@ class LlamaRunner {
       fused_add_rmsnorm(dn, residual, final_norm_, eps_);
       x = dn;
     }
+    const bool decode_only = num_prefill == 0 && num_decode == T;
     for (int64_t l = 0; l < L && !fused; ++l) {
       at::Tensor qkv;
+      bool roped = false;   // RoPE + the K/V cache write already done by the qkv GEMM's reduction
       if (gv && gemv_supported(qkv_w_[l], false)) {
         qkv = at::empty({T, qkv_w_[l].size(0)}, x.options());
         gemv(qkv, x, qkv_w_[l]);
@@ -270,7 +275,12 @@ class LlamaRunner {
         skinny_gemm(qkv, x, qkv_w_[l]);
       } else if (dgemm(T, qkv_w_[l], false)) {
         qkv = at::empty({T, qkv_w_[l].size(0)}, x.options());
-        decode_gemm(qkv, x, qkv_w_[l], dg_ws_, c10::nullopt, c10::nullopt, eps_, 0, 0);
+        if (decode_only && qkv_rope_fused()) {
+          decode_gemm_qkv_rope(qkv, x, qkv_w_[l], dg_ws_, pos, cos_sin_, slots, kc_[l], vc_[l], hq_, hkv_);
+          roped = true;
+        } else {
+          decode_gemm(qkv, x, qkv_w_[l], dg_ws_, c10::nullopt, c10::nullopt, eps_, 0, 0);
+        }
       } else if (pgemm(T, qkv_w_[l], false)) {
         qkv = at::empty({T, qkv_w_[l].size(0)}, x.options());
         gemm_prefill(qkv, x, qkv_w_[l], false, -1);
@@ -279,7 +289,9 @@ class LlamaRunner {
       }
       at::Tensor attn = at::empty({T, hq_ * d_}, qkv.options());
       at::Tensor q = qkv.narrow(1, 0, hq_ * d_);
-      if (num_prefill == 0 && num_decode == T && rope_fused()) {
+      if (roped) {
+        paged_decode_attention(attn, q, kc_[l], vc_[l], d_bt, d_ctx, scale_, nsplit, bps, ws);
+      } else if (decode_only && rope_fused()) {
         // decode-only step: RoPE + K/V cache write inside the attention kernel
         paged_decode_attention_rope(attn, qkv, pos, cos_sin_, slots, kc_[l], vc_[l], d_bt, d_ctx, scale_, nsplit,
                                     bps, ws);
@@ -443,6 +455,15 @@ class LlamaRunner {
   }
 
   // LS_ATTN_ROPE=0: separate rope_cache launch before decode attention (A/B switch)
+  // Decode-only steps whose qkv runs on the split-K decode GEMM: RoPE + the K/V cache
+  // write inside its reduction (LS_QKV_ROPE=0: the attention kernel's fused form instead).
+  static bool qkv_rope_fused() {
+    static const bool on = [] {
+      const char* e = getenv("LS_QKV_ROPE");
+      return e == nullptr || e[0] != '0';
+    }();
+    return on;
+  }
   static bool rope_fused() {
     static const bool on = [] {
       const char* e = getenv("LS_ATTN_ROPE");

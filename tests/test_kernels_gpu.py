@@ -351,6 +351,33 @@ def test_knn_topk(N, Qn, k, dup):
                 assert not valid[q, j]
 
 
+@pytest.mark.parametrize("N,Qn,D,k,dup", [(300000, 1024, 384, 20, 0), (300000, 2048, 384, 20, 0),
+                                           (100000, 2048, 512, 10, 0), (50000, 1500, 256, 64, 0),
+                                           (100000, 700, 128, 20, 0), (60000, 300, 384, 20, 5)])
+def test_knn_topk_large_q(N, Qn, D, k, dup):
+    """The large-batch main pass (knn_filter_q256_kernel: 256 queries per workgroup, rows
+    through an LDS-DMA ring, per-wave LDS candidate buffers) against an fp32 top-k of the
+    same bf16 operands on the GPU; dup > 0 (massive ties) overflows the per-wave buffers
+    and the candidate lists and takes the exact rerun."""
+    torch.manual_seed(N + Qn + D)
+    X = torch.nn.functional.normalize(torch.randn(N, D, device=DEV), dim=-1)
+    if dup:
+        X = X[torch.arange(N, device=DEV) % dup]
+    X = X.to(torch.bfloat16)
+    Q = torch.nn.functional.normalize(torch.randn(Qn, D, device=DEV), dim=-1).to(torch.bfloat16)
+    s, i = ops.knn_topk(X, Q, k)
+    full = Q.float() @ X.float().t()
+    es, _ = full.topk(k, dim=1)
+    assert (s - es).abs().max().item() < 2e-3
+    assert (i >= 0).all()
+    got = full.gather(1, i.long())
+    assert (got - s).abs().max().item() < 2e-3
+    # no row twice in one answer
+    srt = i.sort(dim=1).values
+    assert (srt[:, 1:] != srt[:, :-1]).all()
+    del full
+
+
 def test_knn_topk_threshold_overflow_and_exact():
     """Rows get MORE similar to the queries further into the store, so the sample's
     K-th best is a weak threshold: candidate lists overflow and the search reruns
@@ -421,7 +448,7 @@ def test_gemm_prefill_silu(M, F, K):
     _close(out, torch.nn.functional.silu(gu[:, :F]) * gu[:, F:], 0.02, 0.02)
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3])
+@pytest.mark.parametrize("variant", [1, 2])
 @pytest.mark.parametrize("M", [1, 300, 2048, 3000, 70000])
 @pytest.mark.parametrize("N,K", [(256, 128), (768, 1024), (512, 2048)])
 def test_gemm_prefill_pingpong(M, N, K, variant):
@@ -434,7 +461,7 @@ def test_gemm_prefill_pingpong(M, N, K, variant):
     _close(out, x.float() @ w.float().t(), 0.02, 0.02)
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3])
+@pytest.mark.parametrize("variant", [1, 2])
 @pytest.mark.parametrize("M,F,K", [(77, 128, 256), (1000, 384, 1024), (4096, 256, 512), (40000, 640, 256)])
 def test_gemm_prefill_pingpong_silu(M, F, K, variant):
     torch.manual_seed(M + F + 1)
@@ -447,7 +474,7 @@ def test_gemm_prefill_pingpong_silu(M, F, K, variant):
 
 @pytest.mark.parametrize("name,N,K,silu", [("qkv", 6144, 4096, False), ("o", 4096, 4096, False),
                                             ("gate_up", 28672, 4096, True), ("down", 4096, 14336, False)])
-@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+@pytest.mark.parametrize("variant", [0, 1, 2])
 def test_gemm_prefill_llama_shapes(name, N, K, silu, variant):
     """Llama-3-8B projection shapes at a ragged M = 16384 - 77 (edge M tile), against a
     fp32 GEMM of the same bf16 operands on the GPU (torch.matmul in fp32)."""
@@ -814,3 +841,44 @@ def test_decode_gemm_silu(M, F, K, splits):
         ops.hip().decode_gemm_silu(out, x, w, ws, tickets, err, splits)
         _close(out, exp, 0.02, 0.02)
     assert err.item() == 0
+
+
+@pytest.mark.parametrize("M", [129, 256])
+@pytest.mark.parametrize("Hq,Hkv,K", [(32, 8, 4096), (8, 1, 8192)])   # Llama-3-8B; Llama-3-70B TP=8 shard
+def test_decode_gemm_qkv_rope(M, Hq, Hkv, K):
+    """qkv split-K GEMM with RoPE + the paged K/V write fused into its reduction, against
+    an fp32 projection rotated in fp32 and the same rows in the caches; rows with slot -1
+    are not cached."""
+    torch.manual_seed(M + Hq + K)
+    D, BS = 128, 64
+    N = (Hq + 2 * Hkv) * D
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=DEV) / K ** 0.5).to(torch.bfloat16)
+    pos = torch.randint(0, 4000, (M,), device=DEV, dtype=torch.int32)
+    half = torch.arange(0, D // 2, dtype=torch.float64)
+    inv = 1.0 / (500000.0 ** (2 * half / D))
+    ang = torch.arange(0, 4096, dtype=torch.float64)[:, None] * inv[None, :]
+    cos_sin = torch.cat([ang.cos(), ang.sin()], 1).float().to(DEV)
+    NB = 2 * M
+    kc = torch.zeros(NB, Hkv, BS, D, device=DEV, dtype=torch.bfloat16)
+    vc = torch.zeros(NB, Hkv, D, BS, device=DEV, dtype=torch.bfloat16)
+    slots = torch.randperm(NB * BS, device=DEV)[:M].long()
+    slots[5] = -1
+    qkv = torch.full((M, N), float("nan"), device=DEV, dtype=torch.bfloat16)
+    ops.hip().decode_gemm_qkv_rope(qkv, x, w, _dg_ws(M, N), pos, cos_sin, slots, kc, vc, Hq, Hkv)
+    y = (x.float() @ w.float().t()).view(M, Hq + 2 * Hkv, D)
+    cs = cos_sin[pos.long()]                                  # [M, D]
+    co, si = cs[:, None, : D // 2], cs[:, None, D // 2:]
+    a, b = y[:, : Hq + Hkv, : D // 2], y[:, : Hq + Hkv, D // 2:]
+    rot = torch.cat([a * co - b * si, b * co + a * si], -1)
+    exp = torch.cat([rot, y[:, Hq + Hkv:]], 1)
+    _close(qkv.view(M, -1, D), exp, 0.03, 0.03, "qkv")
+    got = qkv.view(M, -1, D)
+    for m in range(M):
+        s = int(slots[m])
+        if s < 0:
+            continue
+        blk, off = s // BS, s % BS
+        assert torch.equal(kc[blk, :, off, :], got[m, Hq: Hq + Hkv]), m
+        assert torch.equal(vc[blk, :, :, off], got[m, Hq + Hkv:]), m
+    assert int((kc != 0).any(-1).sum()) == (M - 1) * Hkv
