@@ -269,6 +269,21 @@ def balanced_key(prefix: str, target: int, parts: int) -> str:
         salt += 1
 
 
+def _stream_summary(gathered, args, world):
+    """The closed-loop window run after the burst window (--also-stream): records/s over
+    the slowest rank, p50 latency; None when it did not run."""
+    if not gathered or gathered[0].get("stream") is None:
+        return None
+    el = max(g["stream"]["elapsed"] for g in gathered)
+    lats = [x for g in gathered for x in g["stream"]["lats"]]
+    n = args.also_stream * args.batch * world
+    return {"value": round(n / el, 3), "unit": "records/s", "steps": args.also_stream,
+            "ms_per_step": round(1000 * el / args.also_stream, 2),
+            "p50_latency_s": round(statistics.median(lats), 3) if lats else None,
+            "load": f"closed loop, {args.batch} questions in flight per GPU; only questions sent inside the "
+                    f"window count, the window drains them"}
+
+
 def make_page(i: int, corpus) -> str:
     """A crawled page: ~12 paragraphs of corpus sentences."""
     return "\n\n".join(" ".join(corpus[(i * 31 + p * 7 + j) % len(corpus)] for j in range(5)) for p in range(12))
@@ -350,6 +365,9 @@ def main():
     ap.add_argument("--timeout", type=float, default=900.0)
     ap.add_argument("--prefill-chunk", type=int, default=16384,
                     help="engine max-prefill-tokens per step (chunked prefill)")
+    ap.add_argument("--also-stream", type=int, default=3,
+                    help="burst load: afterwards time this many steps' worth of questions under the closed-loop "
+                         "load too and report it as stream_load (0: skip)")
     ap.add_argument("--load", choices=("stream", "burst"), default="burst",
                     help="stream: closed loop, --batch questions in flight per GPU, a new question as each "
                          "answer arrives, a step = --batch answers; burst: --batch questions at the start of "
@@ -600,7 +618,15 @@ def main():
         if c is not None and hasattr(c, "get_info"):
             info = c.get_info()
             assign[info["topic"]] = info.get("assignment")
-    mine = {"elapsed": elapsed, "lats": my_lats, "chunks": chunks, "assign": assign,
+    stream_res = None
+    if args.load == "burst" and args.also_stream > 0:
+        # the same pipeline under the closed-loop load, reported beside the burst number
+        barrier()
+        ts0 = time.time()
+        s_lats = run_window(args.also_stream)
+        barrier()
+        stream_res = {"elapsed": time.time() - ts0, "lats": s_lats}
+    mine = {"elapsed": elapsed, "lats": my_lats, "chunks": chunks, "assign": assign, "stream": stream_res,
             "prefill_tokens": stats.get("prefill_tokens", 0), "requests": stats.get("requests", 0),
             "phases": phases, "gc": {"pause_ms": round(gc_t["ms"], 1), "collections_by_gen": gc_t["n"]},
             "knn_rounds": dist_knn.active().rounds if dist_knn.active() else 0,
@@ -646,6 +672,7 @@ def main():
             "setup_s": round(setup_s, 1),
             "engine_rank0": dict(stats, exec_ms=dict(zip(("upload", "enqueue", "download", "wait"),
                                                          (round(x, 1) for x in llm.exec.timings())))),
+            "stream_load": _stream_summary(gathered, args, world),
         }), flush=True)
     barrier()
     runner.stop(timeout=10)

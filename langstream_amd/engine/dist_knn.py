@@ -110,6 +110,7 @@ class ShardedKnn:
                       "header_s": 0.0}
         # LS_KNN_PROFILE=1: synchronise after each phase of a round's search (diagnosis only)
         self._prof = os.environ.get("LS_KNN_PROFILE") == "1" and self.device.type == "cuda"
+        self._replicate = max(1, int(os.environ.get("LS_KNN_REPLICATE", "1") or 1))
         if self._prof:
             self.stats.update(upload_s=0.0, gather_s=0.0, topk_s=0.0, a2a_s=0.0)
         self._thread = threading.Thread(target=self._loop, name="sharded-knn", daemon=True)
@@ -309,12 +310,16 @@ class ShardedKnn:
                 s = idx = None
                 if store is not None and store.dim == dim and len(store):
                     try:
+                        # LS_KNN_REPLICATE=R (diagnosis): search the gathered queries R times
+                        # over, i.e. the per-round load of R x W ranks, and keep the first copy
+                        qs = qall if self._replicate <= 1 else qall.repeat(self._replicate, 1)
                         if store.device.type == "cuda" and self.data_dev.type == "cpu":
-                            s, idx = to_host(*store.topk_rows(qall.pin_memory().to(
+                            s, idx = to_host(*store.topk_rows(qs.pin_memory().to(
                                 store.device, non_blocking=True).to(store.dtype), kmax))
                         else:
-                            s, idx = store.topk_rows(qall.to(store.device, store.dtype), kmax)
+                            s, idx = store.topk_rows(qs.to(store.device, store.dtype), kmax)
                             s, idx = s.to(self.data_dev), idx.to(self.data_dev)
+                        s, idx = s[: W * qmax], idx[: W * qmax]
                     except Exception as e:  # noqa: BLE001 - contribute nothing, keep the collectives
                         log.exception("sharded kNN: local search of %s failed", coll)
                         errs[coll] = e

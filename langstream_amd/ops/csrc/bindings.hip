@@ -72,6 +72,8 @@ void decode_gemm(at::Tensor out, at::Tensor x, at::Tensor w, at::Tensor workspac
 void decode_gemm_qkv_rope(at::Tensor qkv, at::Tensor x, at::Tensor w, at::Tensor workspace, at::Tensor pos,
                           at::Tensor cos_sin, at::Tensor slots, at::Tensor k_cache, at::Tensor v_cache, int64_t Hq,
                           int64_t Hkv);
+bool decode_gemm_f32_supported(const at::Tensor& w, int64_t M);
+void decode_gemm_f32(at::Tensor out, at::Tensor x, at::Tensor w, int64_t bn_force);
 void decode_gemm_silu(at::Tensor out, at::Tensor x, at::Tensor w, at::Tensor workspace, at::Tensor tickets,
                       at::Tensor err, int64_t splits);
 void decode_gemm_ablate(at::Tensor x, at::Tensor w, at::Tensor workspace, int64_t abl, int64_t splits,
@@ -128,6 +130,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("bn") = 0, py::arg("splits") = 0);
   m.def("decode_gemm_ablate", &decode_gemm_ablate);
   m.def("decode_gemm_qkv_rope", &decode_gemm_qkv_rope);
+  m.def("decode_gemm_f32_supported", &decode_gemm_f32_supported);
+  m.def("decode_gemm_f32", &decode_gemm_f32, py::arg("out"), py::arg("x"), py::arg("w"), py::arg("bn") = 0);
   m.def("decode_gemm_silu", &decode_gemm_silu, py::arg("out"), py::arg("x"), py::arg("w"), py::arg("workspace"),
         py::arg("tickets"), py::arg("err"), py::arg("splits") = 0);
   bind_runners(m);

@@ -544,7 +544,9 @@ void decode_gemm_qkv_rope(at::Tensor qkv, at::Tensor x, at::Tensor w, at::Tensor
               cos_sin.size(1) == D, "decode_gemm_qkv_rope: pos / slots / cos_sin");
   TORCH_CHECK(k_cache.is_contiguous() && v_cache.is_contiguous() && v_cache.size(2) == D && v_cache.size(3) == BSZ);
   const int bn = pick_bn(N), tiles = N / bn;
-  const int S = pick_split(tiles, K, 4);
+  // at most 4 K slices: the fused reduction reads every slab once more (qkv at M = 256:
+  // 27.5 us with 4 slices vs 28.1 with the 5 pick_split chooses, profiles/dgemm_bench_r3b.log)
+  const int S = std::min(4, pick_split(tiles, K, 4));
   if (S == 1 || D != 128) {
     decode_gemm(qkv, x, w, workspace, c10::nullopt, c10::nullopt, 1e-5, 0, 0);
     rope_and_cache(qkv, pos, cos_sin, slots, k_cache, v_cache, Hq, Hkv, true);
@@ -563,6 +565,32 @@ void decode_gemm_qkv_rope(at::Tensor qkv, at::Tensor x, at::Tensor w, at::Tensor
       part, S, M, N, (bf16*)qkv.data_ptr(), qkv.stride(0), pos.data_ptr<int32_t>(), cos_sin.data_ptr<float>(),
       (int)cos_sin.size(0), slots.data_ptr<int64_t>(), k_cache.size(0) * BSZ, (bf16*)k_cache.data_ptr(),
       (bf16*)v_cache.data_ptr(), (int)Hq, (int)Hkv, BSZ);
+}
+
+// f32 OUTPUT (the LM head: logits the sampler reads in f32): out[M, N] f32 contiguous =
+// x . w^T, no K split -- the EPI_PARTIAL epilogue with one split IS an f32 store.
+// bn: 128 or 256 (0 = LS_DGEMM_HEAD_BN, default 128).
+bool decode_gemm_f32_supported(const at::Tensor& w, int64_t M) {
+  return M >= 1 && M <= BM && w.dim() == 2 && w.scalar_type() == at::kBFloat16 && w.is_contiguous() &&
+         w.size(1) % BK == 0 && w.size(0) % 128 == 0;
+}
+
+void decode_gemm_f32(at::Tensor out, at::Tensor x, at::Tensor w, int64_t bn_force) {
+  check_xw(x, w);
+  const int M = (int)x.size(0), K = (int)x.size(1), N = (int)w.size(0);
+  TORCH_CHECK(decode_gemm_f32_supported(w, M), "decode_gemm_f32: shape");
+  TORCH_CHECK(out.scalar_type() == at::kFloat && out.is_contiguous() && out.size(0) == M && out.size(1) == N,
+              "decode_gemm_f32: out must be f32 [M, N] contiguous");
+  static const int bn_env = env_int("LS_DGEMM_HEAD_BN", 128);
+  int bn = bn_force > 0 ? (int)bn_force : bn_env;
+  if (bn != 256 || N % 256 != 0) bn = 128;
+  auto st = at::hip::getCurrentHIPStream();
+  if (bn == 256)
+    dgemm_launch<256, EPI_PARTIAL>(1, N / 256, st, x, w, M, N, K, nullptr, 0, out.data_ptr<float>(), 0, nullptr,
+                                   nullptr, nullptr);
+  else
+    dgemm_launch<128, EPI_PARTIAL>(1, N / 128, st, x, w, M, N, K, nullptr, 0, out.data_ptr<float>(), 0, nullptr,
+                                   nullptr, nullptr);
 }
 
 // out[M, F] = silu(x . w[:F]^T) * (x . w[F:]^T).  tickets: int32 [2 * (F / 128)] zeros

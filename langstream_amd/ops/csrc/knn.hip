@@ -389,7 +389,8 @@ __global__ void __launch_bounds__(512) knn_filter_q256_kernel(const bf16* __rest
   const int64_t r0 = row_begin + (int64_t)rb * rows_per_wg;
   const int64_t r1 = min(N, r0 + rows_per_wg);
   if (r0 >= r1) return;
-  const int ntile = (int)((r1 - r0 + TR - 1) / TR);
+  const int nrows = (int)(r1 - r0);
+  const int ntile = (nrows + TR - 1) / TR;
 
   // this wave's 32 queries: groups g = 0, 1 of 16; lane (fr, h) holds query 16g + fr, dims 32ks + 8h..
   const int q0 = qb * 256 + wid * 32;
@@ -443,24 +444,27 @@ __global__ void __launch_bounds__(512) knn_filter_q256_kernel(const bf16* __rest
     __builtin_amdgcn_sched_barrier(0);
     issue(t + NST - 1, (t + NST - 1) % NST);
     const char* st = lds + (t % NST) * SB;
-    const int64_t trow = r0 + (int64_t)t * TR;
+    const int tl0 = t * TR;   // tile's first row, relative to r0
+    // A fragments double-buffered across the tile's four 16-row subtiles: subtile i+1's
+    // LDS reads are in flight while subtile i's MFMAs run
+    bf16x8 fa[KS], fb[KS];
+    auto rd = [&](int i, bf16x8 (&f)[KS]) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      bf16x8 af[KS];
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) af[ks] = __builtin_bit_cast(bf16x8, ld16(st + i * 16 * RB + aoff[ks]));
+      for (int ks = 0; ks < KS; ++ks) f[ks] = __builtin_bit_cast(bf16x8, ld16(st + i * 16 * RB + aoff[ks]));
+    };
+    auto sub = [&](int i, const bf16x8 (&f)[KS]) {
       f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
-        for (int g = 0; g < 2; ++g) acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks], qf[g][ks], acc[g], 0, 0, 0);
-      // acc[g][rr] = score(row trow + 16i + 4h + rr, query q0 + 16g + fr)
+        for (int g = 0; g < 2; ++g) acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f[ks], qf[g][ks], acc[g], 0, 0, 0);
+      // acc[g][rr] = score(row r0 + tl0 + 16i + 4h + rr, query q0 + 16g + fr)
 #pragma unroll
       for (int g = 0; g < 2; ++g)
 #pragma unroll
         for (int rr = 0; rr < 4; ++rr) {
-          const int64_t row = trow + 16 * i + 4 * h + rr;
-          const bool hit = acc[g][rr] > thr[g] && row < r1;
+          const int lr = tl0 + 16 * i + 4 * h + rr;
+          const bool hit = acc[g][rr] > thr[g] && lr < nrows;
           const uint64_t mask = __ballot(hit);
           if (mask == 0) continue;
           const int nh = __popcll(mask);
@@ -468,12 +472,20 @@ __global__ void __launch_bounds__(512) knn_filter_q256_kernel(const bf16* __rest
           const int pos = ccount + __popcll(mask & ((1ull << lane) - 1ull));
           if (hit) {
             c_s[pos] = acc[g][rr];
-            c_r[pos] = (int)row;
+            c_r[pos] = (int)(r0 + lr);
             c_q[pos] = q0 + 16 * g + fr;
           }
           ccount += nh;
         }
-    }
+    };
+    rd(0, fa);
+    rd(1, fb);
+    sub(0, fa);
+    rd(2, fa);
+    sub(1, fb);
+    rd(3, fb);
+    sub(2, fa);
+    sub(3, fb);
   }
   wait_vmcnt<0>();   // no LDS-DMA may outlive the workgroup
   flush();

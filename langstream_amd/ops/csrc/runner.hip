@@ -108,6 +108,8 @@ int64_t decode_gemm_workspace(int64_t M, int64_t N, int64_t K, bool silu);
 void decode_gemm_qkv_rope(at::Tensor qkv, at::Tensor x, at::Tensor w, at::Tensor workspace, at::Tensor pos,
                           at::Tensor cos_sin, at::Tensor slots, at::Tensor k_cache, at::Tensor v_cache, int64_t Hq,
                           int64_t Hkv);
+bool decode_gemm_f32_supported(const at::Tensor& w, int64_t M);
+void decode_gemm_f32(at::Tensor out, at::Tensor x, at::Tensor w, int64_t bn_force);
 void decode_gemm(at::Tensor out, at::Tensor x, at::Tensor w, at::Tensor workspace, c10::optional<at::Tensor> residual,
                  c10::optional<at::Tensor> norm_w, double eps, int64_t bn_force, int64_t splits_force);
 void decode_gemm_silu(at::Tensor out, at::Tensor x, at::Tensor w, at::Tensor workspace, at::Tensor tickets,
@@ -182,6 +184,19 @@ class LlamaRunner {
   // logit tensor quantises logits to 2^-7 relative steps (0.125 at |logit| ~ 20), which
   // ties near-equal tokens and coarsens the log-probs FLARE and `logprobs` consume.
   at::Tensor lm_head(const at::Tensor& x) {
+    // decode batches of 129..256 rows: the 256-row decode GEMM with its f32 epilogue
+    // (LS_DGEMM_HEAD=0: hipBLASLt)
+    static const bool dg_head = [] {
+      const char* e = getenv("LS_DGEMM_HEAD");
+      return e == nullptr || e[0] != '0';
+    }();
+    const int64_t R = x.size(0);
+    if (dg_head && dgemm_enabled() && R >= dgemm_min_t() && decode_gemm_f32_supported(lm_head_, R) &&
+        x.stride(1) == 1 && x.is_contiguous()) {
+      at::Tensor out = at::empty({R, lm_head_.size(0)}, x.options().dtype(at::kFloat));
+      decode_gemm_f32(out, x, lm_head_, 0);
+      return out;
+    }
     if (f32_head_) {
       try {
         return at::mm(x, lm_head_.t(), at::kFloat);
@@ -512,12 +527,16 @@ class LlamaRunner {
     }();
     return on;
   }
-  bool dgemm(int64_t T, const at::Tensor& w, bool silu) const {
+  static int64_t dgemm_min_t() {
     static const int64_t min_t = [] {
       const char* e = getenv("LS_DGEMM_MIN_T");
       return e ? (int64_t)atoll(e) : (int64_t)129;
     }();
-    return dgemm_enabled() && dg_ws_.defined() && T >= min_t && T <= kDgemmMaxM && decode_gemm_supported(w, silu);
+    return min_t;
+  }
+  bool dgemm(int64_t T, const at::Tensor& w, bool silu) const {
+    return dgemm_enabled() && dg_ws_.defined() && T >= dgemm_min_t() && T <= kDgemmMaxM &&
+           decode_gemm_supported(w, silu);
   }
 
   void all_reduce(at::Tensor& t) {

@@ -882,3 +882,19 @@ def test_decode_gemm_qkv_rope(M, Hq, Hkv, K):
         assert torch.equal(kc[blk, :, off, :], got[m, Hq: Hq + Hkv]), m
         assert torch.equal(vc[blk, :, :, off], got[m, Hq + Hkv:]), m
     assert int((kc != 0).any(-1).sum()) == (M - 1) * Hkv
+
+
+@pytest.mark.parametrize("M", [129, 256])
+@pytest.mark.parametrize("bn", [128, 256])
+def test_decode_gemm_f32_lm_head(M, bn):
+    """The decode LM head: f32 logits straight from the 256-row decode GEMM at the
+    Llama-3 vocabulary (128256 = 1002 x 128 = 501 x 256), against fp32."""
+    torch.manual_seed(M + bn)
+    N, K = 128256, 4096
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=DEV) / K ** 0.5).to(torch.bfloat16)
+    assert ops.hip().decode_gemm_f32_supported(w, M)
+    out = torch.full((M, N), float("nan"), device=DEV)
+    ops.hip().decode_gemm_f32(out, x, w, bn)
+    ref = x.float() @ w.float().t()
+    assert (out - ref).abs().max().item() < 2e-3 * ref.abs().max().item() + 1e-3

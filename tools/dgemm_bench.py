@@ -50,7 +50,7 @@ def main():
     H, Fi = a.hidden, a.ffn
     dev, bf = "cuda", torch.bfloat16
     h = ops.hip()
-    shapes = {"qkv": (a.qkv, H), "o": (H, H), "gate_up": (2 * Fi, H), "down": (H, Fi)}
+    shapes = {"qkv": (a.qkv, H), "o": (H, H), "gate_up": (2 * Fi, H), "down": (H, Fi), "head": (128256, H)}
     tickets = torch.zeros(2 * (Fi // 128) + 2, device=dev, dtype=torch.int32)
     err = torch.zeros(1, device=dev, dtype=torch.int32)
     for name, (N, K) in shapes.items():
@@ -77,6 +77,13 @@ def main():
                     variants[f"abl{abl}_{nm}"] = (
                         lambda i, abl=abl, so=so: h.decode_gemm_ablate(x, ws[i], wsp, abl, 0, so))
                 check = None
+            elif name == "head":
+                out = torch.empty(M, N, device=dev, dtype=torch.float32)
+                ref = x.float() @ ws[0].float().t()
+                variants["hipblaslt_f32"] = lambda i: torch.mm(x, ws[i].t(), out_dtype=torch.float32, out=out)
+                variants["dgemm_f32_bn128"] = lambda i: h.decode_gemm_f32(out, x, ws[i], 128)
+                variants["dgemm_f32_bn256"] = lambda i: h.decode_gemm_f32(out, x, ws[i], 256)
+                check = lambda: out  # noqa: E731
             elif name == "gate_up":
                 out = torch.empty(M, Fi, device=dev, dtype=bf)
                 ref = F.silu(x.float() @ ws[0][:Fi].float().t()) * (x.float() @ ws[0][Fi:].float().t())
