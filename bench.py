@@ -269,6 +269,15 @@ def balanced_key(prefix: str, target: int, parts: int) -> str:
         salt += 1
 
 
+def _pcts(xs):
+    """min / p10 / p50 / p90 / p99 / max of a list (the decode attention launch ends with the longest context)."""
+    if not xs:
+        return None
+    xs = sorted(xs)
+    return {k: xs[min(len(xs) - 1, int(q * len(xs)))] for k, q in
+            (("min", 0.0), ("p10", 0.1), ("p50", 0.5), ("p90", 0.9), ("p99", 0.99), ("max", 1.0))}
+
+
 def _stream_summary(gathered, args, world):
     """The closed-loop window run after the burst window (--also-stream): records/s over
     the slowest rank, p50 latency; None when it did not run."""
@@ -673,6 +682,7 @@ def main():
             "engine_rank0": dict(stats, exec_ms=dict(zip(("upload", "enqueue", "download", "wait"),
                                                          (round(x, 1) for x in llm.exec.timings())))),
             "stream_load": _stream_summary(gathered, args, world),
+            "prompt_len_pcts_rank0": _pcts(list(llm.prompt_lens)),
         }), flush=True)
     barrier()
     runner.stop(timeout=10)

@@ -218,6 +218,8 @@ class LLMEngine:
         self.stats = {"prefill_steps": 0, "decode_steps": 0, "mixed_steps": 0, "prefill_tokens": 0,
                       "decode_tokens": 0, "preemptions": 0, "requests": 0, "finished": 0, "graph_steps": 0,
                       "host_ms": 0.0, "wait_ms": 0.0, "launch_ms": 0.0, "retire_ms": 0.0}
+        # prompt lengths of the most recent requests (decode attention cost follows the longest context)
+        self.prompt_lens: collections.deque = collections.deque(maxlen=8192)
         self.buckets = sorted(set(graph_buckets or [b for b in (1, 2, 4, 8, 16, 24, 32, 48, 64, 96, 128, 160, 192,
                                                                  224, 256, 320, 384, 448, 512) if b <= max_batch]
                                   + [max_batch]))
@@ -323,6 +325,7 @@ class LLMEngine:
                 break
             self.waiting.append(r)
             self.stats["requests"] += 1
+            self.prompt_lens.append(len(r.prompt_ids))
 
     def step(self) -> None:
         """Schedule + launch one step, then retire the previous in-flight step."""
