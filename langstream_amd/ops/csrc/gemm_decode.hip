@@ -74,10 +74,7 @@ __device__ __forceinline__ int piece_chunk(int lane, int row) { return ((lane & 
 // --ablate, profiles/dgemm_ablation_r3.log): with every wave issuing its share of the
 // stage right after the barrier, a full DMA queue blocks the issuing wave before its
 // MFMAs, so a step costs DMA + compute instead of max(DMA, compute).
-// SP (LD = 0 only): spread the stage's DMA issues through the MFMA stream -- one piece
-// after each (ks, 16-row) group of MFMAs -- instead of issuing them all right after the
-// barrier, where a full DMA queue stalls the issuing wave before its first MFMA.
-template <int BN, int XS, int WS, int EPI, int ABL = 0, int LD = 0, int SP = 0>
+template <int BN, int XS, int WS, int EPI, int ABL = 0, int LD = 0>
 __global__ void __launch_bounds__(LD ? 768 : 512) dgemm_kernel(const bf16* __restrict__ x, int64_t ldx,
                                                    const bf16* __restrict__ w, int M, int N, int K, int S,
                                                    bf16* __restrict__ out, int64_t ldo, float* __restrict__ part,
@@ -181,18 +178,6 @@ __global__ void __launch_bounds__(LD ? 768 : 512) dgemm_kernel(const bf16* __res
         if (u + WA >= 0 && u + WA < nks) issue_w(u + WA);
     }
   };
-  constexpr bool SPREAD = SP != 0 && LD == 0 && ABL == 0;
-  static_assert(!SPREAD || PX + PW <= 2 * IT, "one DMA piece per (ks, row group) slot");
-  // piece p of step u's issue set: X pieces first (stage u + XA), then W (stage u + WA)
-  auto issue_piece = [&](int u, int p) {
-    if (p < PX) {
-      const int st = u + XA;
-      if (st >= 0 && st < nks) glds16(xsrc[p] + st * BK, lx0 + (st % XS) * XSTAGE + (PX * lw + p) * 1024);
-    } else {
-      const int st = u + WA, q = p - PX;
-      if (st >= 0 && st < nks) glds16(wsrc[q] + st * BK, lw0 + (st % WS) * WSTAGE + (PW * lw + q) * 1024);
-    }
-  };
   for (int u = -WA; u < 0; ++u) issue_step(u);
   for (int t = 0; t < nks; ++t) {
     const int nx = max(0, min(t + XA - 1, nks - 1) - t);                       // X(t+1 .. t+XA-1)
@@ -203,7 +188,7 @@ __global__ void __launch_bounds__(LD ? 768 : 512) dgemm_kernel(const bf16* __res
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // step t-1's fragment reads are done
     __builtin_amdgcn_s_barrier();                         // every wave: stage t landed, t-1 read
-    if constexpr (!SPREAD) issue_step(t);                 // into the slots of stage t-1
+    issue_step(t);                                        // into the slots of stage t-1
     if (!computer) continue;
     const char* lx = lx0 + (t % XS) * XSTAGE;
     const char* lw = lw0 + (t % WS) * WSTAGE;
@@ -224,13 +209,9 @@ __global__ void __launch_bounds__(LD ? 768 : 512) dgemm_kernel(const bf16* __res
       }
       if constexpr ((ABL & 1) == 0) {
 #pragma unroll
-        for (int i = 0; i < IT; ++i) {
+        for (int i = 0; i < IT; ++i)
 #pragma unroll
           for (int j = 0; j < JT; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
-          if constexpr (SPREAD) {
-            if (ks * IT + i < PX + PW) issue_piece(t, ks * IT + i);
-          }
-        }
       } else {
 #pragma unroll
         for (int i = 0; i < IT; ++i) asm volatile("" ::"v"(a[i]));
@@ -377,12 +358,6 @@ int split_outer_default() {
   return v;
 }
 
-// LS_DGEMM_SPREAD=1: BN = 256 launches (no loader waves) spread their DMA issues (SP)
-int spread_default() {
-  static const int v = env_int("LS_DGEMM_SPREAD", 0);
-  return v;
-}
-
 // ring shapes: BN = 128: X 3 slots (2 ahead) + W 4 slots (3 ahead) = 160 KB;
 // BN = 256: X 2 + W 3 = 160 KB.
 template <int BN, int EPI>
@@ -390,16 +365,10 @@ void dgemm_launch(int S, int tiles, hipStream_t st, const at::Tensor& x, const a
                   bf16* out, int64_t ldo, float* part, int F, unsigned* tickets, float* xchg, int* err) {
   constexpr int XS = BN == 128 ? 3 : 2, WS = BN == 128 ? 4 : 3;
   constexpr int LDW = BN == 128 ? 4 : 0;   // BN = 256 needs 200 VGPRs: no room for a third wave per SIMD
-  const int so = EPI == EPI_SILU2 ? 0 : split_outer_default();
-  if (LDW == 0 && spread_default()) {
-    dgemm_kernel<BN, XS, WS, EPI, 0, LDW, 1><<<dim3(tiles * S), 512, 0, st>>>(
-        (const bf16*)x.data_ptr(), x.stride(0), (const bf16*)w.data_ptr(), M, N, K, S, out, ldo, part, F, tickets,
-        xchg, err, so);
-    return;
-  }
   dgemm_kernel<BN, XS, WS, EPI, 0, LDW><<<dim3(tiles * S), LDW ? 768 : 512, 0, st>>>((const bf16*)x.data_ptr(), x.stride(0),
                                                                  (const bf16*)w.data_ptr(), M, N, K, S, out, ldo,
-                                                                 part, F, tickets, xchg, err, so);
+                                                                 part, F, tickets, xchg, err,
+                                                                 EPI == EPI_SILU2 ? 0 : split_outer_default());
 }
 
 void check_xw(const at::Tensor& x, const at::Tensor& w) {

@@ -153,6 +153,20 @@ WORKER = textwrap.dedent('''
 ''')
 
 
+def _wait_started(proc):
+    """Read the worker's merged stdout/stderr up to its 'started' line (log lines such as the
+    restored store's kernel-path notice may come first)."""
+    seen = []
+    for _ in range(50):
+        line = proc.stdout.readline()
+        if not line:
+            break
+        if line.strip() == b"started":
+            return
+        seen.append(line)
+    raise AssertionError(f"worker did not start: {seen!r}")
+
+
 def test_kill_restart_replays_committed_offsets_without_loss(tmp_path):
     from langstream_amd.api.model import StreamingCluster
     from langstream_amd.api.record import SimpleRecord
@@ -169,7 +183,7 @@ def test_kill_restart_replays_committed_offsets_without_loss(tmp_path):
     n = 400
     try:
         a = subprocess.Popen([sys.executable, str(script)], stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
-        assert a.stdout.readline().strip() == b"started"
+        _wait_started(a)
         for i in range(n):
             prod.write(SimpleRecord.of(f"c{i}", {"vec": [float(i % 7 + 1), 1.0, float(i % 3)], "text": f"t{i}"})) \
                 .result(5)
@@ -181,7 +195,7 @@ def test_kill_restart_replays_committed_offsets_without_loss(tmp_path):
         done_at_kill = sum(rt.log.committed("chunks", group))
         assert 0 < done_at_kill
         b = subprocess.Popen([sys.executable, str(script)], stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
-        assert b.stdout.readline().strip() == b"started"
+        _wait_started(b)
         deadline = time.time() + 90
         while sum(rt.log.committed("chunks", group)) < n and time.time() < deadline:
             time.sleep(0.05)

@@ -46,6 +46,9 @@ def main():
     ap.add_argument("--qkv", type=int, default=6144)
     ap.add_argument("--ablate", action="store_true",
                     help="time the split-K kernel's ablation builds (no MFMA / no LDS reads / no DMA)")
+    ap.add_argument("--env-ab", default="",
+                    help="NAME: time every dgemm variant twice, with NAME=0 and NAME=1 in the environment "
+                         "(a switch the kernels read per launch), interleaved in the same rounds")
     a = ap.parse_args()
     H, Fi = a.hidden, a.ffn
     dev, bf = "cuda", torch.bfloat16
@@ -119,15 +122,41 @@ def main():
                         variants[f"dgemm_bn{bn}_s{sp}"] = (
                             lambda i, bn=bn, sp=sp: h.decode_gemm(out, x, ws[i], wsp, None, None, 1e-5, bn, sp))
                 check = lambda: out.float()  # noqa: E731
+                if name == "qkv" and N % 128 == 0:
+                    # decode-only step form: + RoPE + paged K/V write in the reduction pass; timed
+                    # only (RoPE changes the values), checked by tests/test_kernels_gpu.py
+                    D, Hkv = 128, 8
+                    Hq = N // D - 2 * Hkv
+                    rp_pos = torch.randint(0, 4000, (M,), device=dev, dtype=torch.int32)
+                    rp_cs = torch.randn(4096, D, device=dev)
+                    rp_kc = torch.zeros(2 * M, Hkv, 64, D, device=dev, dtype=bf)
+                    rp_vc = torch.zeros(2 * M, Hkv, D, 64, device=dev, dtype=bf)
+                    rp_slots = torch.randperm(2 * M * 64, device=dev)[:M].long()
+                    variants["qkvrope_pass"] = lambda i: h.decode_gemm_qkv_rope(
+                        out, x, ws[i], wsp, rp_pos, rp_cs, rp_slots, rp_kc, rp_vc, Hq, Hkv)
             # correctness of every variant on weight copy 0 (residual reset each time)
             errs = {}
             for k, fn in (variants.items() if check is not None else ()):
+                if k.startswith("qkvrope"):
+                    continue
                 res.copy_(res0)
                 out.zero_()
                 fn(0)
                 torch.cuda.synchronize()
                 d = (check() - ref).abs().max().item()
                 errs[k] = round(d / (ref.abs().max().item() + 1e-6), 4)
+            if a.env_ab:
+                ab = {}
+                for k, fn in variants.items():
+                    if not k.startswith("dgemm"):
+                        ab[k] = fn
+                        continue
+                    for v in ("0", "1"):
+                        def fn_env(i, fn=fn, v=v):
+                            os.environ[a.env_ab] = v
+                            fn(i)
+                        ab[f"{k}@{v}"] = fn_env
+                variants = ab
             times = {k: [] for k in variants}
             for k, fn in variants.items():   # warm
                 time_once(fn, ring, 3)
