@@ -542,8 +542,11 @@ def main():
                         send_question()   # closed loop: keep --batch questions in flight
         steps_done[0] += 1
         t_end = time.time()
-        # (first answer, last answer, step end incl. waiting for the crawled pages' indexing), s
-        phases.append([round((t_first or t_end) - t0, 3), round((t_all or t_end) - t0, 3), round(t_end - t0, 3)])
+        # (first answer, last answer, step end incl. waiting for the crawled pages' indexing,
+        # first / last prompt reaching the LLM scheduler), s
+        arr = [a for a in list(llm.arrival_log) if t0 <= a <= t_end]
+        phases.append([round((t_first or t_end) - t0, 3), round((t_all or t_end) - t0, 3), round(t_end - t0, 3),
+                       round(min(arr) - t0, 3) if arr else None, round(max(arr) - t0, 3) if arr else None])
         return t_end - t0, lats
 
     def run_window(k_steps):

@@ -188,7 +188,8 @@ class ShardedKnn:
     def _loop(self) -> None:
         try:
             if self.device.type == "cuda":
-                torch.cuda.set_device(self.device)
+                torch.cuda.set_device(self.device.index if self.device.index is not None
+                                      else torch.cuda.current_device())
                 # Every device op of a round -- the H2D query copy, the kNN kernel and the
                 # D2H copies (plus the RCCL collectives under LS_KNN_DATA=nccl, which order
                 # themselves after the CURRENT stream) -- runs on the one high-priority search

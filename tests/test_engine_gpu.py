@@ -276,3 +276,72 @@ def test_prefill_gate_up_gemm_in_model(monkeypatch):
     for i in range(len(lens)):
         assert _cos(fused[i], lib[i]) > 0.999
         assert _cos(native[i], lib[i]) > 0.999
+
+
+# ------------------------------------------------------------------ native TP, 2 ranks
+_TP_PROMPTS = [list(range(3, 3 + n)) for n in (5, 33, 64, 200)]
+
+
+def _tp_native_worker(rank, world, port, q):
+    """One TP rank on cuda:0 over a gloo process group: the NATIVE step executor (C++
+    forward, per-layer all-reduces through c10d, vocab-parallel sampling); rank 0 drives
+    the engine, the other ranks run StepExecutor::worker_loop (pure C++)."""
+    import os
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from langstream_amd.models.llama import TPInfo
+        from langstream_amd.models.loader import shard_llama
+        cfg = PRESETS["llama-small"]
+        full = LlamaModel(cfg, device="cpu", dtype=torch.float32, seed=9)
+        m = LlamaModel(cfg, device="cuda", tp=TPInfo(rank, world, None))
+        m.load_state_dict(shard_llama(full.state_dict(), cfg, rank, world))
+        eng = LLMEngine(m, None, num_blocks=128, max_model_len=1024, max_batch=8, use_graphs=False)
+        if rank == 0:
+            sp = SamplingParams(max_tokens=10, temperature=0.0, ignore_eos=True, logprobs=2)
+            out = _run_tops(eng, _TP_PROMPTS, sp)
+            stats = dict(eng.stats)
+            eng.stop()
+            q.put((out, stats))
+        else:
+            eng.worker_loop()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_native_executor_tp2_two_ranks_one_gpu():
+    """TP = 2 with two real ranks (two processes sharing cuda:0, gloo collectives on GPU
+    tensors): the native executor's worker loop, arena broadcast, per-layer all-reduces
+    and vocab-parallel sampling produce the TP = 1 engine's greedy tokens (up to genuine
+    near-ties) on the same full weights.  RCCL cannot put two ranks on one GPU; this is
+    the multi-rank run of the C++ TP path available on a 1-GPU box."""
+    import multiprocessing as mp
+    import socket
+    cfg = PRESETS["llama-small"]
+    full = LlamaModel(cfg, device="cpu", dtype=torch.float32, seed=9)
+    m0 = LlamaModel(cfg, device="cuda")
+    m0.load_state_dict(full.state_dict())
+    e0 = LLMEngine(m0, None, num_blocks=128, max_model_len=1024, max_batch=8, use_graphs=False)
+    ref = _run_tops(e0, _TP_PROMPTS, SamplingParams(max_tokens=10, temperature=0.0, ignore_eos=True, logprobs=2))
+    e0.stop()
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_tp_native_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    try:
+        got, stats = q.get(timeout=100)
+    finally:
+        for p in procs:
+            p.join(30)
+            if p.is_alive():
+                p.kill()
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    assert stats["decode_steps"] > 0
+    for a, b in zip(got, ref):
+        _same_or_near_tie(a, b)

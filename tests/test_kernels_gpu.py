@@ -145,13 +145,17 @@ def test_paged_decode_attention(G, nsplit, min_bps):
     _close(got, exp.reshape(B, Hq * D), 0.03, 0.03)
 
 
-def test_paged_decode_attention_wave_per_pair():
+@pytest.mark.parametrize("B,sort", [(256, False), (257, True)])
+def test_paged_decode_attention_wave_per_pair(B, sort):
     """B*Hkv >= 2048 takes the one-wave-per-(seq, kv-head) kernel; ragged contexts
-    exercise the masked tail-block loads."""
+    exercise the masked tail-block loads (rows in arrival order, and sorted longest
+    first as the engine schedules them, at an odd batch)."""
     Hkv, G, D = 8, 4, 128
     Hq = Hkv * G
     gen = torch.Generator().manual_seed(7)
-    ctx = torch.randint(1, 300, (256,), generator=gen).tolist()
+    ctx = torch.randint(1, 300, (B,), generator=gen).tolist()
+    if sort:
+        ctx.sort(reverse=True)
     B = len(ctx)
     kc, vc, bt = _random_paged(B, ctx, Hkv, D, DEV, seed=3)
     q = torch.randn(B, Hq * D, device=DEV, dtype=torch.bfloat16)

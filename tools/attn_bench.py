@@ -46,6 +46,11 @@ def main():
                          "time the attention kernel with rocprofv3 in this mode")
     ap.add_argument("--pool-gb", type=float, default=0.0,
                     help="scatter the blocks over a KV pool of this size (TLB reach), like a real engine")
+    ap.add_argument("--uniform-lo", type=int, default=0,
+                    help="per-sequence context drawn uniformly from [uniform-lo, ctx] (e.g. the RAG bench's "
+                         "prompt lengths 201..502 plus the tokens generated so far)")
+    ap.add_argument("--sorted", action="store_true",
+                    help="rows ordered by context length, longest first (as the engine schedules them)")
     ap.add_argument("--rope", action="store_true",
                     help="time the decode-only variant with RoPE + the KV write fused in "
                          "(paged_decode_attention_rope over an un-rotated qkv buffer, as the engine runs it)")
@@ -59,8 +64,12 @@ def main():
         if a.ragged > 0:
             lo, hi = int(ctx * (1 - a.ragged)), int(ctx * (1 + a.ragged))
             ctxs = torch.randint(max(1, lo), hi + 1, (B,), generator=g)
+        elif a.uniform_lo > 0:
+            ctxs = torch.randint(a.uniform_lo, ctx + 1, (B,), generator=g)
         else:
             ctxs = torch.full((B,), ctx)
+        if a.sorted:
+            ctxs = ctxs.sort(descending=True).values
         nb = int((ctxs.max() + 63) // 64)
         # blocks scattered over a pool 2x the live size (like a busy engine), or --pool-gb
         blk_bytes = Hkv * 64 * D * 2 * 2
@@ -115,8 +124,9 @@ def main():
         rec = {"B": B, "ctx": ctx, "us": round(us, 2), "TBps": round(byts / us / 1e6, 2),
                "kernel": "decode_attn_kernel", "wpp": os.environ.get("LS_ATTN_WPP", "auto"),
                "pipe": os.environ.get("LS_ATTN_PIPE", "1"),
-               "ragged": a.ragged, "pool_gb": a.pool_gb, "ring": a.ring, "rope": a.rope}
-        if not a.rope and (B <= 16 or (a.check_all and B * ctx <= 256 * 1024)) and a.pool_gb == 0:
+               "ragged": a.ragged, "pool_gb": a.pool_gb, "ring": a.ring, "rope": a.rope,
+               "uniform_lo": a.uniform_lo, "sorted": a.sorted}
+        if not a.rope and (B <= 16 or (a.check_all and B * ctx <= 512 * 1024)) and a.pool_gb == 0:
             exp = ref.paged_decode_attention(q.float().cpu().reshape(B, Hq, D), kc.float().cpu(), vc.float().cpu(),
                                              bt.cpu(), cl.cpu(), scale).reshape(B, Hq * D)
             rec["max_err"] = round(float((o.float().cpu() - exp).abs().max()), 4)
