@@ -49,6 +49,9 @@ def main():
     ap.add_argument("--uniform-lo", type=int, default=0,
                     help="per-sequence context drawn uniformly from [uniform-lo, ctx] (e.g. the RAG bench's "
                          "prompt lengths 201..502 plus the tokens generated so far)")
+    ap.add_argument("--seq-blocks", action="store_true",
+                    help="each sequence's blocks are consecutive ids (a fresh burst through the engine's "
+                         "block allocator) instead of scattered over the pool")
     ap.add_argument("--sorted", action="store_true",
                     help="rows ordered by context length, longest first (as the engine schedules them)")
     ap.add_argument("--rope", action="store_true",
@@ -74,7 +77,7 @@ def main():
         # blocks scattered over a pool 2x the live size (like a busy engine), or --pool-gb
         blk_bytes = Hkv * 64 * D * 2 * 2
         pool = max(2 * B * nb, int(a.pool_gb * 1e9 // blk_bytes))
-        perm = torch.randperm(pool, generator=g)[: B * nb].to(torch.int32)
+        perm = (torch.arange(B * nb) if a.seq_blocks else torch.randperm(pool, generator=g)[: B * nb]).to(torch.int32)
         bt = perm.view(B, nb).to(dev)
         if pool > 2 * B * nb:
             kc = torch.zeros(pool, Hkv, 64, D, device=dev, dtype=bf)
@@ -125,7 +128,8 @@ def main():
                "kernel": "decode_attn_kernel", "wpp": os.environ.get("LS_ATTN_WPP", "auto"),
                "pipe": os.environ.get("LS_ATTN_PIPE", "1"),
                "ragged": a.ragged, "pool_gb": a.pool_gb, "ring": a.ring, "rope": a.rope,
-               "uniform_lo": a.uniform_lo, "sorted": a.sorted}
+               "uniform_lo": a.uniform_lo, "sorted": a.sorted, "seq_blocks": a.seq_blocks,
+               "interleave_gemm": a.interleave_gemm}
         if not a.rope and (B <= 16 or (a.check_all and B * ctx <= 512 * 1024)) and a.pool_gb == 0:
             exp = ref.paged_decode_attention(q.float().cpu().reshape(B, Hq, D), kc.float().cpu(), vc.float().cpu(),
                                              bt.cpu(), cl.cpu(), scale).reshape(B, Hq * D)
