@@ -5,7 +5,7 @@ Replaces the remote completion services the reference calls from
 ``OpenAICompletionService.java:122-404``, ``OllamaProvider.java:273-311``) with a local
 engine:
 
-* paged KV cache (64-token blocks, V stored transposed; blocks managed by the native
+* paged KV cache (64-token blocks, V stored transposed in 8-key groups; blocks managed by the native
   ``BlockAllocator``), sized from the 288 GB HBM budget;
 * unified steps: every step carries one decode token per running sequence plus, when
   prompts are waiting, chunked-prefill tokens (``max_prefill_tokens`` per step), so new
@@ -194,9 +194,7 @@ class LLMEngine:
         self.num_blocks = int(num_blocks)
         self.kv_caches = []
         for _ in range(self.cfg.num_layers):
-            kc = torch.zeros(self.num_blocks, hkv, BLOCK, D, device=self.device, dtype=model.dtype)
-            vc = torch.zeros(self.num_blocks, hkv, D, BLOCK, device=self.device, dtype=model.dtype)
-            self.kv_caches.append((kc, vc))
+            self.kv_caches.append(ops.new_kv_cache(self.num_blocks, hkv, D, self.device, model.dtype))
         self.allocator = lib().BlockAllocator(self.num_blocks)
         self.nsplit, self.bps = ops.decode_splits(self.max_blocks_per_seq)
         # ---- step arena + executor

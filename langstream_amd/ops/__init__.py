@@ -25,6 +25,17 @@ import torch
 from . import reference as ref
 
 KV_BLOCK = 64
+
+
+def new_kv_cache(num_blocks: int, hkv: int, head_dim: int, device, dtype, zeros: bool = True):
+    """(K, V) paged caches of one layer: K [NB, Hkv, 64, D]; V^T in 8-key groups
+    [NB, Hkv, 8, D, 8] (element (d, key) of a block at [key // 8, d, key % 8]; see
+    ops/csrc/common.h vt_off)."""
+    mk = torch.zeros if zeros else torch.empty
+    return (mk(num_blocks, hkv, KV_BLOCK, head_dim, device=device, dtype=dtype),
+            mk(num_blocks, hkv, KV_BLOCK // 8, head_dim, 8, device=device, dtype=dtype))
+
+
 PREFILL_ROWS = 128  # query rows per prefill-attention workgroup (see attention_prefill.hip)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))

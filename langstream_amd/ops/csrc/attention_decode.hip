@@ -3,8 +3,8 @@
 // One query token per sequence.  Work unit = one (sequence, kv-head) pair; its G
 // query heads (G = Hq/Hkv <= 16) are the 16 MFMA "rows" (padded with zero rows).
 //
-// Layout trick (no LDS, no transposes): with the V cache stored transposed
-// ([NB, Hkv, D, BS]) and the scores computed SWAPPED (S^T = K * Q^T), every MFMA
+// Layout trick (no LDS, no transposes): with the V cache stored transposed in 8-key
+// groups ([NB, Hkv, BS/8, D, 8], common.h vt_off) and the scores computed SWAPPED (S^T = K * Q^T), every MFMA
 // operand of both products is one 16-B contiguous global load per lane and the
 // softmax statistics stay lane-local:
 //   S^T tile kt=(2*kg+e):  A = K rows, lane i=l&15 loads key 32kg + 8(i>>2) + 4e + (i&3)
@@ -159,7 +159,7 @@ __global__ void __launch_bounds__(64 * WPP) __attribute__((amdgpu_waves_per_eu(2
       const bool vok = 32 * kg + 8 * h < lim;
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) {
-        const int off = ((16 * dt + i16) * BS + 32 * kg + 8 * h) * 2;
+        const int off = (int)vt_off(16 * dt + i16, 32 * kg + 8 * h, D) * 2;
         vf[kg][dt] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(vrs, vok ? off : OOB, 0, AUX));
       }
     }
@@ -235,13 +235,13 @@ __global__ void __launch_bounds__(64 * WPP) __attribute__((amdgpu_waves_per_eu(2
           for (int ks = 0; ks < KS; ++ks) st16(kd + 32 * ks, __builtin_bit_cast(uint4, kn[ks]));
         }
         if (i16 < DT) {
-          // V^T: lane (i16, h) stores dims 16 i16 + 4h + r (each a 2-B store at stride BS)
-          bf16* vd = ra.vc + ((blk * Hkv + kvh) * (int64_t)D) * BS + off;
+          // V^T: lane (i16, h) stores dims 16 i16 + 4h + r (2-B stores at a 16-B stride)
+          bf16* vd = ra.vc + ((blk * Hkv + kvh) * (int64_t)D) * BS;
           bf16x4 vv = vn[0];
 #pragma unroll
           for (int dt = 1; dt < DT; ++dt) if (i16 == dt) vv = vn[dt];
 #pragma unroll
-          for (int r = 0; r < 4; ++r) vd[(int64_t)(16 * i16 + 4 * h + r) * BS] = vv[r];
+          for (int r = 0; r < 4; ++r) vd[vt_off(16 * i16 + 4 * h + r, (int)off, D)] = vv[r];
         }
       }
     }
@@ -444,9 +444,10 @@ static void decode_attention_launch(at::Tensor& out, const at::Tensor& q, const 
                                     const at::Tensor& workspace, const RopeArgs* ra) {
   TORCH_CHECK(q.is_cuda() && q.scalar_type() == at::kBFloat16 && out.scalar_type() == at::kBFloat16);
   TORCH_CHECK(out.is_contiguous() && q.stride(-1) == 1);
-  TORCH_CHECK(k_cache.dim() == 4 && v_cache.dim() == 4);
+  TORCH_CHECK(k_cache.dim() == 4 && v_cache.dim() == 5, "k_cache [NB, Hkv, 64, D], v_cache [NB, Hkv, 8, D, 8]");
   const int Hkv = k_cache.size(1), D = k_cache.size(3);
-  TORCH_CHECK(k_cache.size(2) == BS && v_cache.size(3) == BS && v_cache.size(2) == D, "KV block size must be 64");
+  TORCH_CHECK(k_cache.size(2) == BS && v_cache.size(1) == Hkv && v_cache.size(2) == BS / 8 && v_cache.size(3) == D &&
+              v_cache.size(4) == 8, "KV block size must be 64");
   const int B = ctx_lens.numel();
   TORCH_CHECK(out.numel() % ((int64_t)B * D) == 0);
   const int Hq = out.numel() / ((int64_t)B * D);

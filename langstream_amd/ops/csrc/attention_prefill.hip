@@ -4,7 +4,8 @@
 // as extra rows (row = token*G + g), so every staged K/V tile is reused by G heads.
 //
 //  * PAGED=true  (Llama prefill, incl. chunked prefill with a cached prefix):
-//      K from k_cache [NB, Hkv, 64, D], V^T from v_cache [NB, Hkv, D, 64], causal.
+//      K from k_cache [NB, Hkv, 64, D], V^T from v_cache [NB, Hkv, 8, D, 8] (8-key groups,
+//      common.h vt_off), causal.
 //  * PAGED=false (BERT encoder): K and V read from the packed QKV projection,
 //      bidirectional, keys limited to the sequence (padding-free varlen).
 //
@@ -130,10 +131,10 @@ __global__ void __launch_bounds__(256, 2) prefill_attn_kernel(
       *reinterpret_cast<uint4*>(&ks_lds[key * D + 8 * (c ^ kswz<D>(key))]) = kreg[i];
     }
     if constexpr (PAGED) {
-      // source already V^T: chunk qi = (d, c) with 8 chunks per 64-key row
+      // source already V^T in 8-key groups: chunk qi = (key group c, dim d)
 #pragma unroll
       for (int i = 0; i < VPT; ++i) {
-        const int qi = threadIdx.x + 256 * i, d = qi >> 3, c = qi & 7;
+        const int qi = threadIdx.x + 256 * i, c = qi / D, d = qi - c * D;
         *reinterpret_cast<uint4*>(&vs_lds[d * KVT + 8 * (c ^ vswz(d))]) = vreg[i];
       }
     } else {
@@ -255,9 +256,10 @@ void paged_prefill_attention(at::Tensor out, at::Tensor q, at::Tensor k_cache, a
                              at::Tensor block_tables, at::Tensor q_start, at::Tensor q_len, at::Tensor ctx_len,
                              at::Tensor tiles, int64_t Hq, double scale) {
   TORCH_CHECK(q.scalar_type() == at::kBFloat16 && out.scalar_type() == at::kBFloat16 && q.stride(-1) == 1);
-  TORCH_CHECK(k_cache.dim() == 4 && k_cache.size(2) == KVT && v_cache.size(3) == KVT, "KV block size must be 64");
+  TORCH_CHECK(k_cache.dim() == 4 && k_cache.size(2) == KVT && v_cache.dim() == 5 && v_cache.size(2) == KVT / 8 &&
+              v_cache.size(4) == 8, "KV block size must be 64 (v_cache [NB, Hkv, 8, D, 8])");
   const int Hkv = k_cache.size(1), D = k_cache.size(3);
-  TORCH_CHECK(Hq % Hkv == 0 && v_cache.size(2) == D);
+  TORCH_CHECK(Hq % Hkv == 0 && v_cache.size(3) == D);
   for (auto* t : {&block_tables, &q_start, &q_len, &ctx_len, &tiles})
     TORCH_CHECK(t->scalar_type() == at::kInt && t->is_contiguous());
   TORCH_CHECK(out.stride(-1) == 1 && q.stride(0) % 8 == 0 && out.stride(0) % 4 == 0);

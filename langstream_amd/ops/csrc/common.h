@@ -17,6 +17,15 @@ typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
+// Paged V cache: [NB, Hkv, BS/8, D, 8] -- V^T of a (block, kv-head) in 8-key groups, each
+// head dim's 8 keys one 16-B chunk.  The MFMA P.V operand (8 consecutive keys of one dim)
+// is still one 16-B load, the 16 dims of a fragment are 256 contiguous bytes, and the
+// step's new token lands as 2-B stores at a 16-B stride (16 lines per head instead of
+// D lines of a [D, BS] image).  Element (d, key) of the image at:
+__host__ __device__ __forceinline__ int64_t vt_off(int d, int key, int D) {
+  return ((int64_t)(key >> 3) * D + d) * 8 + (key & 7);
+}
+
 __device__ __forceinline__ float bf2f(bf16 x) { return (float)x; }
 __device__ __forceinline__ bf16 f2bf(float x) { return (bf16)x; }
 

@@ -74,10 +74,7 @@ __device__ __forceinline__ int piece_chunk(int lane, int row) { return ((lane & 
 // --ablate, profiles/dgemm_ablation_r3.log): with every wave issuing its share of the
 // stage right after the barrier, a full DMA queue blocks the issuing wave before its
 // MFMAs, so a step costs DMA + compute instead of max(DMA, compute).
-// SEP (LD = 4 only): loader waves 0-1 issue only X pieces, 2-3 only W pieces, so the
-// short-latency X (L2) loads never wait behind HBM-bound W loads in one wave's in-order
-// vector-memory queue; each loader waits only for its own stream.
-template <int BN, int XS, int WS, int EPI, int ABL = 0, int LD = 0, int SEP = 0>
+template <int BN, int XS, int WS, int EPI, int ABL = 0, int LD = 0>
 __global__ void __launch_bounds__(LD ? 768 : 512) dgemm_kernel(const bf16* __restrict__ x, int64_t ldx,
                                                    const bf16* __restrict__ w, int M, int N, int K, int S,
                                                    bf16* __restrict__ out, int64_t ldo, float* __restrict__ part,
@@ -87,9 +84,8 @@ __global__ void __launch_bounds__(LD ? 768 : 512) dgemm_kernel(const bf16* __res
   constexpr int JT = BN / 32;              // 16-col tiles per wave (wave = 64 rows x BN/2 cols)
   constexpr int IT = 4;                    // 16-row tiles per wave
   constexpr int NLW = LD ? LD : 8;         // waves that issue the DMAs
-  constexpr bool SEPL = SEP != 0 && LD == 4;
-  constexpr int PX = SEPL ? 16 : 32 / NLW;           // X pieces per issuing wave per stage (32 per stage)
-  constexpr int PW = SEPL ? BN / 16 : BN / 8 / NLW;  // W pieces per issuing wave per stage
+  constexpr int PX = 32 / NLW;             // X pieces per issuing wave per stage (32 per stage)
+  constexpr int PW = BN / 8 / NLW;         // W pieces per issuing wave per stage
   constexpr int XA = XS - 1, WA = WS - 1;  // stages issued ahead
   static_assert(XA >= 1 && WA >= XA, "W is issued at least as far ahead as X");
   static_assert(XS * XSTAGE + WS * WSTAGE <= LDS_MAX, "LDS budget");
@@ -101,9 +97,7 @@ __global__ void __launch_bounds__(LD ? 768 : 512) dgemm_kernel(const bf16* __res
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const bool loader = LD == 0 || wid >= 8;   // issues DMAs (every wave when LD == 0)
   const bool computer = LD == 0 || wid < 8;
-  const int lw0i = LD ? (wid >= 8 ? wid - 8 : 0) : wid;   // index among the issuing waves
-  const bool xload = !SEPL || lw0i < 2, wload = !SEPL || lw0i >= 2;
-  const int lw = SEPL ? (lw0i & 1) : lw0i;                 // index among the waves of its stream
+  const int lw = LD ? (wid >= 8 ? wid - 8 : 0) : wid;   // index among the issuing waves
   // the S splits of one tile are consecutive logical ids: same XCD (speed only)
   // split_outer: consecutive logical ids (one XCD) share the K split, i.e. the same X
   // slice, which then stays in that XCD's L2; otherwise the S splits of one tile are
@@ -135,13 +129,11 @@ __global__ void __launch_bounds__(LD ? 768 : 512) dgemm_kernel(const bf16* __res
     wsrc[j] = w + (int64_t)wrow * K + (int64_t)kb * BK + piece_chunk(lane, lr);
   }
   auto issue_x = [&](int t) {
-    if (!xload) return;
     char* dst = lx0 + (t % XS) * XSTAGE + (PX * lw) * 1024;
 #pragma unroll
     for (int j = 0; j < PX; ++j) glds16(xsrc[j] + t * BK, dst + j * 1024);
   };
   auto issue_w = [&](int t) {
-    if (!wload) return;
     char* dst = lw0 + (t % WS) * WSTAGE + (PW * lw) * 1024;
 #pragma unroll
     for (int j = 0; j < PW; ++j) {
@@ -191,10 +183,7 @@ __global__ void __launch_bounds__(LD ? 768 : 512) dgemm_kernel(const bf16* __res
     const int nx = max(0, min(t + XA - 1, nks - 1) - t);                       // X(t+1 .. t+XA-1)
     const int nw = max(0, min(t + WA - 1, nks - 1) - (t - XA + WA) + 1);       // W(t-XA+WA .. t+WA-1)
     if (loader) {
-      if constexpr (SEPL) {
-        if (xload) wait_vmcnt_dyn(PX * nx);
-        else wait_vmcnt_dyn(PW * max(0, min(t + WA - 1, nks - 1) - t));   // W(t+1 .. t+WA-1)
-      } else if constexpr ((ABL & 12) == 0) wait_vmcnt_dyn(PX * nx + PW * nw);
+      if constexpr ((ABL & 12) == 0) wait_vmcnt_dyn(PX * nx + PW * nw);
       else if constexpr ((ABL & 4) == 0) wait_vmcnt_dyn(PX * nx);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // step t-1's fragment reads are done
@@ -369,9 +358,6 @@ int split_outer_default() {
   return v;
 }
 
-// LS_DGEMM_SEP=1: separate X / W loader waves (SEP), read per launch (A/B in one process)
-int sep_default() { return env_int("LS_DGEMM_SEP", 0); }
-
 // ring shapes: BN = 128: X 3 slots (2 ahead) + W 4 slots (3 ahead) = 160 KB;
 // BN = 256: X 2 + W 3 = 160 KB.
 template <int BN, int EPI>
@@ -379,12 +365,6 @@ void dgemm_launch(int S, int tiles, hipStream_t st, const at::Tensor& x, const a
                   bf16* out, int64_t ldo, float* part, int F, unsigned* tickets, float* xchg, int* err) {
   constexpr int XS = BN == 128 ? 3 : 2, WS = BN == 128 ? 4 : 3;
   constexpr int LDW = BN == 128 ? 4 : 0;   // BN = 256 needs 200 VGPRs: no room for a third wave per SIMD
-  if (LDW == 4 && sep_default()) {
-    dgemm_kernel<BN, XS, WS, EPI, 0, LDW, 1><<<dim3(tiles * S), 768, 0, st>>>(
-        (const bf16*)x.data_ptr(), x.stride(0), (const bf16*)w.data_ptr(), M, N, K, S, out, ldo, part, F, tickets,
-        xchg, err, EPI == EPI_SILU2 ? 0 : split_outer_default());
-    return;
-  }
   dgemm_kernel<BN, XS, WS, EPI, 0, LDW><<<dim3(tiles * S), LDW ? 768 : 512, 0, st>>>((const bf16*)x.data_ptr(), x.stride(0),
                                                                  (const bf16*)w.data_ptr(), M, N, K, S, out, ldo,
                                                                  part, F, tickets, xchg, err,
@@ -537,11 +517,11 @@ __global__ void __launch_bounds__(256) splitk_reduce_rope_kernel(
     *reinterpret_cast<bf16x4*>(kd) = va;
     *reinterpret_cast<bf16x4*>(kd + HALF) = vb;
   } else {
-    bf16* vd = vc + ((blk * Hkv + (hd - Hq - Hkv)) * (int64_t)D) * BS + off;
+    bf16* vd = vc + ((blk * Hkv + (hd - Hq - Hkv)) * (int64_t)D) * BS;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      vd[(int64_t)(4 * c + j) * BS] = va[j];
-      vd[(int64_t)(HALF + 4 * c + j) * BS] = vb[j];
+      vd[vt_off(4 * c + j, (int)off, D)] = va[j];
+      vd[vt_off(HALF + 4 * c + j, (int)off, D)] = vb[j];
     }
   }
 }
@@ -562,7 +542,8 @@ void decode_gemm_qkv_rope(at::Tensor qkv, at::Tensor x, at::Tensor w, at::Tensor
   TORCH_CHECK(pos.scalar_type() == at::kInt && pos.numel() >= M && slots.scalar_type() == at::kLong &&
               slots.numel() >= M && cos_sin.scalar_type() == at::kFloat && cos_sin.is_contiguous() &&
               cos_sin.size(1) == D, "decode_gemm_qkv_rope: pos / slots / cos_sin");
-  TORCH_CHECK(k_cache.is_contiguous() && v_cache.is_contiguous() && v_cache.size(2) == D && v_cache.size(3) == BSZ);
+  TORCH_CHECK(k_cache.is_contiguous() && v_cache.is_contiguous() && v_cache.dim() == 5 && v_cache.size(2) == BSZ / 8 &&
+              v_cache.size(3) == D && v_cache.size(4) == 8, "decode_gemm_qkv_rope: v_cache [NB, Hkv, BS/8, D, 8]");
   const int bn = pick_bn(N), tiles = N / bn;
   // at most 4 K slices: the fused reduction reads every slab once more (qkv at M = 256:
   // 27.5 us with 4 slices vs 28.1 with the 5 pick_split chooses, profiles/dgemm_bench_r3b.log)

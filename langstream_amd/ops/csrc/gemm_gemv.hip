@@ -55,7 +55,7 @@ struct ProNorm {
 // EPI_QKV operands: W is the fused qkv projection [(Hq + 2 Hkv) * D, K]; each block owns
 // RB/2 rotary pairs (d, d + D/2) of one head, so the epilogue applies RoPE to q and k heads
 // and writes k to the paged K cache [NB, Hkv, BS, D] and v transposed to the V cache
-// [NB, Hkv, D, BS] -- the rope_cache kernel of rope.hip, fused (same bf16 rounding).
+// [NB, Hkv, BS/8, D, 8] -- the rope_cache kernel of rope.hip, fused (same bf16 rounding).
 struct QkvEpi {
   const int32_t* pos;
   const float* cos_sin;  // [max_pos, D]: cols [0, D/2) cos, [D/2, D) sin
@@ -250,9 +250,9 @@ __global__ void __launch_bounds__(256) gemv_kernel(const bf16* __restrict__ x, i
             kd[d1] = ab;
             kd[d2] = bb;
           } else {
-            bf16* vd = qe.vc + (blk * qe.Hkv + (qk_head - qe.Hq - qe.Hkv)) * (int64_t)qe.D * qe.BS + off;
-            vd[(int64_t)d1 * qe.BS] = ab;
-            vd[(int64_t)d2 * qe.BS] = bb;
+            bf16* vd = qe.vc + (blk * qe.Hkv + (qk_head - qe.Hq - qe.Hkv)) * (int64_t)qe.D * qe.BS;
+            vd[vt_off(d1, (int)off, qe.D)] = ab;
+            vd[vt_off(d2, (int)off, qe.D)] = bb;
           }
         }
       }
@@ -420,11 +420,11 @@ QkvEpi make_qkv(const at::Tensor& out, const at::Tensor& pos, const at::Tensor& 
                 const at::Tensor& kc, const at::Tensor& vc, int64_t Hq, int64_t Hkv, bool apply_rope) {
   TORCH_CHECK(pos.scalar_type() == at::kInt && slots.scalar_type() == at::kLong && cos_sin.scalar_type() == at::kFloat &&
                   cos_sin.is_contiguous(), "gemv_qkv: pos int32, slots int64, cos_sin f32");
-  TORCH_CHECK(kc.dim() == 4 && vc.dim() == 4 && kc.scalar_type() == at::kBFloat16 && vc.scalar_type() == at::kBFloat16,
-              "gemv_qkv: paged caches [NB, Hkv, BS, D] / [NB, Hkv, D, BS] bf16");
+  TORCH_CHECK(kc.dim() == 4 && vc.dim() == 5 && kc.scalar_type() == at::kBFloat16 && vc.scalar_type() == at::kBFloat16,
+              "gemv_qkv: paged caches [NB, Hkv, BS, D] / [NB, Hkv, BS/8, D, 8] bf16");
   const int D = kc.size(3), BS = kc.size(2);
-  TORCH_CHECK(kc.size(1) == Hkv && vc.size(1) == Hkv && vc.size(2) == D && vc.size(3) == BS && cos_sin.size(1) == D,
-              "gemv_qkv: cache / rope table shapes");
+  TORCH_CHECK(kc.size(1) == Hkv && vc.size(1) == Hkv && vc.size(2) == BS / 8 && vc.size(3) == D && vc.size(4) == 8 &&
+                  cos_sin.size(1) == D, "gemv_qkv: cache / rope table shapes");
   TORCH_CHECK(out.size(1) == (Hq + 2 * Hkv) * D && pos.numel() == out.size(0) && slots.numel() == out.size(0),
               "gemv_qkv: qkv / pos / slots shapes");
   return QkvEpi{pos.data_ptr<int32_t>(), cos_sin.data_ptr<float>(), slots.data_ptr<int64_t>(), (bf16*)kc.data_ptr(),

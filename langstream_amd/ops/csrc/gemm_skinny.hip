@@ -183,19 +183,21 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restr
 
 // One row per workgroup:  v = sum_s part[s, m, :] + residual[m, :];  residual = bf16(v);
 // out[m, :] = rmsnorm(bf16(v)) * w.  (Same rounding as fused_add_rmsnorm in norm.hip.)
-template <int NV, int SMAX = 8>
-__global__ void __launch_bounds__(256) splitk_add_rmsnorm_kernel(const float* __restrict__ part, int S, int M, int H,
+// NT threads per row: 512 at the decode width (H = 4096, NV = 1) puts the whole row's
+// partials (S x 16 KB) in flight at once -- one memory round trip per row instead of two.
+template <int NV, int SMAX = 8, int NT = 256>
+__global__ void __launch_bounds__(NT) splitk_add_rmsnorm_kernel(const float* __restrict__ part, int S, int M, int H,
                                                                  bf16* __restrict__ residual,
                                                                  const bf16* __restrict__ w, float eps,
                                                                  bf16* __restrict__ out) {
-  __shared__ float red[4];
+  __shared__ float red[NT / 64];
   const int m = blockIdx.x;
   const int64_t total = (int64_t)M * H;
   float v[NV][8];
   float ss = 0.f;
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
-    const int c = (threadIdx.x + 256 * i) * 8;
+    const int c = (threadIdx.x + NT * i) * 8;
     if (c < H) {
       const float* p = part + (int64_t)m * H + c;
       // Issue the first SMAX partials' loads together (independent, predicated), then
@@ -237,7 +239,7 @@ __global__ void __launch_bounds__(256) splitk_add_rmsnorm_kernel(const float* __
   const float inv = rsqrtf(ss / H + eps);
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
-    const int c = (threadIdx.x + 256 * i) * 8;
+    const int c = (threadIdx.x + NT * i) * 8;
     if (c < H) {
       float wf[8], o[8];
       unpack8(ld16(w + c), wf);
@@ -499,6 +501,11 @@ void splitk_add_rmsnorm_launch(const float* part, int S, int M, int N, bf16* res
                                bf16* out, hipStream_t st) {
   const int nv = (N / 8 + 255) / 256;
   TORCH_CHECK(nv <= 8, "splitk_add_rmsnorm: N <= 16384");
+  const char* e = getenv("LS_NORM_NT512");   // 0: the 256-thread form (read per launch, A/B in one process)
+  if ((e ? atoi(e) : 1) != 0 && N / 8 <= 512) {
+    splitk_add_rmsnorm_kernel<1, 8, 512><<<M, 512, 0, st>>>(part, S, M, N, residual, norm_w, eps, out);
+    return;
+  }
 #define RED(NV) splitk_add_rmsnorm_kernel<NV><<<M, 256, 0, st>>>(part, S, M, N, residual, norm_w, eps, out)
   if (nv <= 1) RED(1);
   else if (nv <= 2) RED(2);

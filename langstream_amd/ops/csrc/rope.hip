@@ -6,8 +6,9 @@
 //            includes any rope scaling; no device trig -- guide App. B "element-wise")
 // slots    : [T] int64 cache slot = block * BS + offset (-1 = do not cache)
 // k_cache  : [NB, Hkv, BS, D]   (token-major rows: 256-B contiguous per token & head)
-// v_cache  : [NB, Hkv, D, BS]   (TRANSPOSED: keys contiguous, so attention reads V^T
-//            MFMA fragments with one 16-B load per lane -- see attention kernels)
+// v_cache  : [NB, Hkv, BS/8, D, 8]   (TRANSPOSED in 8-key groups: 8 keys of one dim are
+//            16 contiguous bytes, so attention reads V^T MFMA fragments with one 16-B load
+//            per lane; a token's V lands at a 16-B stride -- common.h vt_off)
 //
 // Grid: x = tiles of TOK tokens, y = head groups.  y < nq: rotate HG query heads;
 // nq <= y < nq+nk: rotate HG key heads and store them to the K cache; the last Hkv
@@ -98,8 +99,8 @@ __global__ void __launch_bounds__(256) rope_cache_kernel(bf16* __restrict__ qkv,
   if (s < 0 || s >= nslots) return;
   const int64_t blk = s / BS, off = s - blk * BS;
   const bf16* src = qkv + t * row_elems + (Hq + Hkv + hv) * D;
-  bf16* vd = vc + ((blk * Hkv + hv) * (int64_t)D) * BS + off;
-  for (int d = dr; d < D; d += 256 / TOK) vd[(int64_t)d * BS] = src[d];
+  bf16* vd = vc + ((blk * Hkv + hv) * (int64_t)D) * BS;
+  for (int d = dr; d < D; d += 256 / TOK) vd[vt_off(d, (int)off, D)] = src[d];
 }
 
 }  // namespace
@@ -110,10 +111,11 @@ void rope_and_cache(at::Tensor qkv, at::Tensor pos, at::Tensor cos_sin, at::Tens
   TORCH_CHECK(pos.scalar_type() == at::kInt && slots.scalar_type() == at::kLong);
   TORCH_CHECK(cos_sin.scalar_type() == at::kFloat && cos_sin.is_contiguous());
   TORCH_CHECK(k_cache.scalar_type() == at::kBFloat16 && v_cache.scalar_type() == at::kBFloat16);
-  TORCH_CHECK(k_cache.dim() == 4 && v_cache.dim() == 4);
+  TORCH_CHECK(k_cache.dim() == 4 && v_cache.dim() == 5, "k_cache [NB, Hkv, BS, D], v_cache [NB, Hkv, BS/8, D, 8]");
   const int D = k_cache.size(3);
   const int BS = k_cache.size(2);
-  TORCH_CHECK(k_cache.size(1) == Hkv && v_cache.size(1) == Hkv && v_cache.size(2) == D && v_cache.size(3) == BS);
+  TORCH_CHECK(k_cache.size(1) == Hkv && v_cache.size(1) == Hkv && v_cache.size(2) == BS / 8 && v_cache.size(3) == D &&
+              v_cache.size(4) == 8);
   TORCH_CHECK(qkv.size(-1) == (Hq + 2 * Hkv) * D);
   const int64_t T = qkv.numel() / qkv.size(-1);
   TORCH_CHECK(pos.numel() == T && slots.numel() == T);

@@ -128,7 +128,7 @@ def rope_and_cache(qkv, pos, cos_sin, slots, k_cache, v_cache, Hq, Hkv, apply_ro
             continue
         blk, off = divmod(s, BS)
         k_cache[blk, :, off, :] = v[t, Hq: Hq + Hkv]
-        v_cache[blk, :, :, off] = v[t, Hq + Hkv:]
+        v_cache[blk, :, off // 8, :, off % 8] = v[t, Hq + Hkv:]    # [NB, Hkv, BS/8, D, 8]
 
 
 def gather_kv(k_cache, v_cache, block_table, n):
@@ -136,7 +136,8 @@ def gather_kv(k_cache, v_cache, block_table, n):
     BS = k_cache.shape[2]
     nb = (n + BS - 1) // BS
     ks = [k_cache[int(block_table[i])] for i in range(nb)]           # [Hkv, BS, D]
-    vs = [v_cache[int(block_table[i])].transpose(1, 2) for i in range(nb)]  # [Hkv, BS, D]
+    # V blocks [Hkv, BS/8, D, 8] -> [Hkv, BS, D]
+    vs = [v_cache[int(block_table[i])].permute(0, 1, 3, 2).reshape(v_cache.shape[1], BS, -1) for i in range(nb)]
     K = torch.cat(ks, dim=1)[:, :n].transpose(0, 1)
     V = torch.cat(vs, dim=1)[:, :n].transpose(0, 1)
     return K, V

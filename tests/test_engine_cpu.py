@@ -22,7 +22,7 @@ def _greedy_reference(model, prompt, n):
     kv = []
     nb = 16
     for _ in range(cfg.num_layers):
-        kv.append((torch.zeros(nb, model.hkv, 64, cfg.head_dim), torch.zeros(nb, model.hkv, cfg.head_dim, 64)))
+        kv.append(ops.new_kv_cache(nb, model.hkv, cfg.head_dim, "cpu", torch.float32))
     ids = list(prompt)
     out = []
     for _ in range(n):

@@ -53,9 +53,7 @@ def test_native_runner_matches_python_forward():
     logits must agree to bf16 rounding on a two-sequence prefill."""
     cfg = PRESETS["llama-small"]
     model = LlamaModel(cfg, device="cuda")
-    kv = [(torch.zeros(16, model.hkv, 64, cfg.head_dim, device="cuda", dtype=model.dtype),
-           torch.zeros(16, model.hkv, cfg.head_dim, 64, device="cuda", dtype=model.dtype))
-          for _ in range(cfg.num_layers)]
+    kv = [ops.new_kv_cache(16, model.hkv, cfg.head_dim, "cuda", model.dtype) for _ in range(cfg.num_layers)]
     lens = [70, 100]
     T = sum(lens)
     ids = torch.randint(5, 1000, (T,), dtype=torch.int32, device="cuda")
@@ -251,9 +249,7 @@ def test_prefill_gate_up_gemm_in_model(monkeypatch):
     bps = (max(lens) + 63) // 64
     nblk = bps * len(lens)
     assert max(lens) <= cfg.max_position
-    kv = [(torch.zeros(nblk, model.hkv, 64, cfg.head_dim, device="cuda", dtype=model.dtype),
-           torch.zeros(nblk, model.hkv, cfg.head_dim, 64, device="cuda", dtype=model.dtype))
-          for _ in range(cfg.num_layers)]
+    kv = [ops.new_kv_cache(nblk, model.hkv, cfg.head_dim, "cuda", model.dtype) for _ in range(cfg.num_layers)]
     ids = torch.randint(5, 1000, (n,), dtype=torch.int32, device="cuda")
     pos = torch.cat([torch.arange(m, dtype=torch.int32) for m in lens]).cuda()
     bt = torch.arange(nblk, dtype=torch.int32, device="cuda").view(len(lens), bps)

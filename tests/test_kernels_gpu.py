@@ -84,8 +84,7 @@ def test_silu_mul_and_gelu():
 
 
 def _alloc_cache(nb, Hkv, D, dev):
-    return (torch.zeros(nb, Hkv, ops.KV_BLOCK, D, device=dev, dtype=torch.bfloat16),
-            torch.zeros(nb, Hkv, D, ops.KV_BLOCK, device=dev, dtype=torch.bfloat16))
+    return ops.new_kv_cache(nb, Hkv, D, dev, torch.bfloat16)
 
 
 @pytest.mark.parametrize("T,D", [(150, 128), (2600, 128), (37, 64)])
@@ -115,7 +114,7 @@ def _random_paged(B, ctx, Hkv, D, dev, seed=0):
     nblk = [(c + ops.KV_BLOCK - 1) // ops.KV_BLOCK for c in ctx]
     NB = sum(nblk) + 3
     kc = torch.randn(NB, Hkv, ops.KV_BLOCK, D, device=dev, dtype=torch.bfloat16)
-    vc = torch.randn(NB, Hkv, D, ops.KV_BLOCK, device=dev, dtype=torch.bfloat16)
+    vc = torch.randn(NB, Hkv, ops.KV_BLOCK // 8, D, 8, device=dev, dtype=torch.bfloat16)
     perm = torch.randperm(NB)
     maxb = max(nblk)
     bt = torch.zeros(B, maxb, dtype=torch.int32)
@@ -590,7 +589,7 @@ def test_gemv_qkv_rope_cache(T, K, prologue):
     ang = torch.arange(512).float()[:, None] * inv[None]
     cos_sin = torch.cat([ang.cos(), ang.sin()], 1).to(DEV)
     kc = torch.zeros(NB, Hkv, BS, D, device=DEV, dtype=torch.bfloat16)
-    vc = torch.zeros(NB, Hkv, D, BS, device=DEV, dtype=torch.bfloat16)
+    vc = torch.zeros(NB, Hkv, BS // 8, D, 8, device=DEV, dtype=torch.bfloat16)
     out = torch.empty(T, N, device=DEV, dtype=torch.bfloat16)
     if prologue:
         o, res = x, torch.randn(T, K, device=DEV).to(torch.bfloat16)
@@ -618,7 +617,7 @@ def test_gemv_qkv_rope_cache(T, K, prologue):
             continue
         blk, off = divmod(sl, BS)
         _close(kcc[blk, :, off], exp[t, Hq: Hq + Hkv], 0.05, 0.02)
-        _close(vcc[blk, :, :, off], exp[t, Hq + Hkv:], 0.05, 0.02)
+        _close(vcc[blk, :, off // 8, :, off % 8], exp[t, Hq + Hkv:], 0.05, 0.02)
 
 
 def _ln_stats(x):
@@ -865,7 +864,7 @@ def test_decode_gemm_qkv_rope(M, Hq, Hkv, K):
     cos_sin = torch.cat([ang.cos(), ang.sin()], 1).float().to(DEV)
     NB = 2 * M
     kc = torch.zeros(NB, Hkv, BS, D, device=DEV, dtype=torch.bfloat16)
-    vc = torch.zeros(NB, Hkv, D, BS, device=DEV, dtype=torch.bfloat16)
+    vc = torch.zeros(NB, Hkv, BS // 8, D, 8, device=DEV, dtype=torch.bfloat16)
     slots = torch.randperm(NB * BS, device=DEV)[:M].long()
     slots[5] = -1
     qkv = torch.full((M, N), float("nan"), device=DEV, dtype=torch.bfloat16)
@@ -884,7 +883,7 @@ def test_decode_gemm_qkv_rope(M, Hq, Hkv, K):
             continue
         blk, off = s // BS, s % BS
         assert torch.equal(kc[blk, :, off, :], got[m, Hq: Hq + Hkv]), m
-        assert torch.equal(vc[blk, :, :, off], got[m, Hq + Hkv:]), m
+        assert torch.equal(vc[blk, :, off // 8, :, off % 8], got[m, Hq + Hkv:]), m
     assert int((kc != 0).any(-1).sum()) == (M - 1) * Hkv
 
 

@@ -41,6 +41,9 @@ def main():
     ap.add_argument("--ring", type=int, default=1,
                     help="rotate over this many KV pools per call (> 256 MB Infinity Cache in total: cold "
                          "caches, as in an engine step that streams 32 layers between two calls)")
+    ap.add_argument("--interleave-copy", action="store_true",
+                    help="copy 235 MB (the decode gate_up weight bytes, no MFMA) before every call: separates "
+                         "the cache / TLB effect of an interleaved GEMM from its power / clock effect")
     ap.add_argument("--interleave-gemm", action="store_true",
                     help="run a decode-sized gate_up GEMM before every call (engine-like power / cache state); "
                          "time the attention kernel with rocprofv3 in this mode")
@@ -81,13 +84,13 @@ def main():
         bt = perm.view(B, nb).to(dev)
         if pool > 2 * B * nb:
             kc = torch.zeros(pool, Hkv, 64, D, device=dev, dtype=bf)
-            vc = torch.zeros(pool, Hkv, D, 64, device=dev, dtype=bf)
+            vc = torch.zeros(pool, Hkv, 8, D, 8, device=dev, dtype=bf)
             idx = perm.long().to(dev)
             kc[idx] = torch.randn(len(idx), Hkv, 64, D, device=dev, dtype=bf)
-            vc[idx] = torch.randn(len(idx), Hkv, D, 64, device=dev, dtype=bf)
+            vc[idx] = torch.randn(len(idx), Hkv, 8, D, 8, device=dev, dtype=bf)
         else:
             kc = torch.randn(pool, Hkv, 64, D, device=dev, dtype=bf)
-            vc = torch.randn(pool, Hkv, D, 64, device=dev, dtype=bf)
+            vc = torch.randn(pool, Hkv, 8, D, 8, device=dev, dtype=bf)
         kvs = [(kc, vc)] + [(torch.randn_like(kc), torch.randn_like(vc)) for _ in range(a.ring - 1)]
         cl = ctxs.to(torch.int32).to(dev)
         q = torch.randn(B, Hq * D, device=dev, dtype=bf)
@@ -95,6 +98,9 @@ def main():
         o = torch.empty(B, Hq * D, device=dev, dtype=bf)
         scale = 1 / math.sqrt(D)
         it = [0]
+        if a.interleave_copy:
+            csrc = torch.empty(235 * 2 ** 20 // 2, device=dev, dtype=bf)
+            cdst = torch.empty_like(csrc)
         if a.interleave_gemm:
             gx = torch.randn(B, 4096, device=dev, dtype=bf)
             gw = torch.randn(28672, 4096, device=dev, dtype=bf) * 0.02
@@ -113,6 +119,8 @@ def main():
         def call():
             if a.interleave_gemm:
                 torch.nn.functional.linear(gx, gw)
+            if a.interleave_copy:
+                cdst.copy_(csrc)
             k_, v_ = kvs[it[0] % len(kvs)]
             it[0] += 1
             if a.rope:

@@ -64,7 +64,7 @@ def main():
     nb = (ctx + 63) // 64
     nblocks = B * nb
     kc = torch.randn(nblocks, Hkv, 64, D, device=dev, dtype=bf)
-    vc = torch.randn(nblocks, Hkv, D, 64, device=dev, dtype=bf)
+    vc = torch.randn(nblocks, Hkv, 8, D, 8, device=dev, dtype=bf)
     bt = torch.arange(nblocks, device=dev, dtype=torch.int32).view(B, nb)
     ctx_l = torch.full((B,), ctx, device=dev, dtype=torch.int32)
     qkv = torch.randn(B, (Hq + 2 * Hkv) * D, device=dev, dtype=bf)

@@ -130,7 +130,7 @@ def main():
                     rp_pos = torch.randint(0, 4000, (M,), device=dev, dtype=torch.int32)
                     rp_cs = torch.randn(4096, D, device=dev)
                     rp_kc = torch.zeros(2 * M, Hkv, 64, D, device=dev, dtype=bf)
-                    rp_vc = torch.zeros(2 * M, Hkv, D, 64, device=dev, dtype=bf)
+                    rp_vc = torch.zeros(2 * M, Hkv, 8, D, 8, device=dev, dtype=bf)
                     rp_slots = torch.randperm(2 * M * 64, device=dev)[:M].long()
                     variants["qkvrope_pass"] = lambda i: h.decode_gemm_qkv_rope(
                         out, x, ws[i], wsp, rp_pos, rp_cs, rp_slots, rp_kc, rp_vc, Hq, Hkv)

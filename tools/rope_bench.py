@@ -47,7 +47,7 @@ def main():
     ang = torch.arange(8192, device=dev).float()[:, None] * inv[None]
     cos_sin = torch.cat([ang.cos(), ang.sin()], -1).contiguous()
     kc = torch.zeros(a.blocks, Hkv, BS, D, device=dev, dtype=torch.bfloat16)
-    vc = torch.zeros(a.blocks, Hkv, D, BS, device=dev, dtype=torch.bfloat16)
+    vc = torch.zeros(a.blocks, Hkv, BS // 8, D, 8, device=dev, dtype=torch.bfloat16)
     blk = torch.randperm(a.blocks, device=dev)[:B].long()
     slots = blk * BS + torch.randint(0, BS, (B,), device=dev)
     none = torch.full_like(slots, -1)
