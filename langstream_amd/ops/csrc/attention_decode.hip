@@ -80,7 +80,7 @@ struct RopeArgs {
   bf16* vc;
 };
 
-template <int D, int WPP, bool PIPE, bool ROPE>
+template <int D, int WPP, bool PIPE, bool ROPE, int AUX = 0>
 __global__ void __launch_bounds__(64 * WPP) __attribute__((amdgpu_waves_per_eu(2, 2))) decode_attn_kernel(
     bf16* __restrict__ out, const bf16* __restrict__ q, int64_t q_stride, const bf16* __restrict__ kc,
     const bf16* __restrict__ vc, const int32_t* __restrict__ block_tables, int max_blocks,
@@ -132,7 +132,11 @@ __global__ void __launch_bounds__(64 * WPP) __attribute__((amdgpu_waves_per_eu(2
   // gets an out-of-range offset.  (A select on the loaded data instead made every
   // load wait before the next one issued: 139 vs 90 us at B=256.)
   constexpr int OOB = 1 << 30;
-  constexpr int AUX = 0;            // default cache policy (nt measured slower, see above)
+  // AUX: buffer-load cache policy, 0 or 2 (nt).  KV bytes have no reuse within a decode
+  // step: in the RAG bench nt loads take the in-engine kernel from 84.5 to 73.5 us per
+  // layer (the activations and split-K slabs stay cached; profiles/nt_r3c/).  Back-to-back
+  // isolated calls over one pool re-read the same cache and measure nt slower, so
+  // tools/attn_bench.py runs with a ring of pools.  LS_ATTN_NT=0 turns it off.
   const int kbyte = 8 * h * 2;
 
   auto issue_k = [&](int bi, uint4(&kf)[4][KS]) {
@@ -477,12 +481,16 @@ static void decode_attention_launch(at::Tensor& out, const at::Tensor& q, const 
   static const int env_wpp = getenv("LS_ATTN_WPP") ? atoi(getenv("LS_ATTN_WPP")) : 0;
   static const bool pipe = getenv("LS_ATTN_PIPE") ? atoi(getenv("LS_ATTN_PIPE")) != 0 : true;
   const bool rope = ra != nullptr;
+  const char* ent = getenv("LS_ATTN_NT");   // read per launch (A/B inside one process)
+  const bool attn_nt = !ent || atoi(ent) != 0;
   const RopeArgs rargs = rope ? *ra : RopeArgs{};
   const int wpp = env_wpp == 1 || env_wpp == 4 ? env_wpp : ((int64_t)B * Hkv >= WAVE_SLOTS && ns == 1 ? 1 : 4);
   dim3 grid(B * Hkv, ns);
   const float sl2 = (float)scale * LOG2E;
 #define LAUNCH_R(DD, W, P, R)                                                                                 \
-  decode_attn_kernel<DD, W, P, R><<<grid, 64 * W, 0, stream>>>(                                               \
+  if (attn_nt) LAUNCH_A(DD, W, P, R, 2); else LAUNCH_A(DD, W, P, R, 0)
+#define LAUNCH_A(DD, W, P, R, A)                                                                              \
+  decode_attn_kernel<DD, W, P, R, A><<<grid, 64 * W, 0, stream>>>(                                            \
       (bf16*)out.data_ptr(), (const bf16*)q.data_ptr(), q_stride, (const bf16*)k_cache.data_ptr(),            \
       (const bf16*)v_cache.data_ptr(), block_tables.data_ptr<int32_t>(), (int)block_tables.size(1),          \
       ctx_lens.data_ptr<int32_t>(), Hkv, G, (int)k_cache.size(0), sl2, (int)min_bps, po, pml, rargs)
@@ -503,6 +511,7 @@ static void decode_attention_launch(at::Tensor& out, const at::Tensor& q, const 
 #undef LAUNCH_K
 #undef LAUNCH_P
 #undef LAUNCH_R
+#undef LAUNCH_A
 #undef LAUNCH
 }
 

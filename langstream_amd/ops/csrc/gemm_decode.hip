@@ -68,7 +68,8 @@ __device__ __forceinline__ int piece_chunk(int lane, int row) { return ((lane & 
 // ABL (timing-only ablations, wrong results; tools/dgemm_bench.py --ablate): bit 0 drops
 // the MFMAs, bit 1 the fragment reads, bit 2 the LDS-DMA issue, bit 3 the W DMA only;
 // bit 4 (a real variant, results valid) streams W with the non-temporal hint; bit 5 uses 4
-// dedicated loader waves; bit 6 skips the partial-slab stores.
+// dedicated loader waves; bit 6 skips the partial-slab stores; bit 7 (a real variant)
+// writes the partial slabs with non-temporal stores.
 // LD: dedicated loader waves (0 or 4).  With LD = 4 the workgroup is 8 compute + 4
 // loader waves: only the loaders issue LDS-DMA.  Measured (tools/dgemm_bench.py
 // --ablate, profiles/dgemm_ablation_r3.log): with every wave issuing its share of the
@@ -310,8 +311,10 @@ __global__ void __launch_bounds__(LD ? 768 : 512) dgemm_kernel(const bf16* __res
       // part[split][m][tile * BN + c]: BN / 4 float4 per row
       for (int q = threadIdx.x; q < ((ABL & 64) ? 0 : rows * (BN / 4)); q += NT) {
         const int m = q / (BN / 4), c = (q - m * (BN / 4)) * 4;
-        *reinterpret_cast<f32x4*>(part + ((int64_t)split * M + r0 + m) * N + tile * BN + c) =
-            *reinterpret_cast<const f32x4*>(T + m * TP + c);
+        f32x4* dst = reinterpret_cast<f32x4*>(part + ((int64_t)split * M + r0 + m) * N + tile * BN + c);
+        const f32x4 v = *reinterpret_cast<const f32x4*>(T + m * TP + c);
+        if constexpr ((ABL & 128) != 0) __builtin_nontemporal_store(v, dst);
+        else *dst = v;
       }
     } else if constexpr (EPI == EPI_STORE) {
       for (int q = threadIdx.x; q < rows * (BN / 8); q += NT) {
@@ -358,6 +361,13 @@ int split_outer_default() {
   return v;
 }
 
+// Cache policy of the decode GEMMs in an engine step (profiles/nt_r3c/, full RAG bench,
+// per-layer kernel times): W loads non-temporal (LS_DGEMM_WNT, gate_up 66.5 -> 64.5 us)
+// and the f32 split-K slabs stored non-temporally (LS_DGEMM_NTST); with the attention's
+// nt KV loads the layer drops 256.8 -> 240.6 us.  Both default on; read per launch.
+int wnt_default() { return env_int("LS_DGEMM_WNT", 1); }
+int ntst_default() { return env_int("LS_DGEMM_NTST", 1); }
+
 // ring shapes: BN = 128: X 3 slots (2 ahead) + W 4 slots (3 ahead) = 160 KB;
 // BN = 256: X 2 + W 3 = 160 KB.
 template <int BN, int EPI>
@@ -365,10 +375,23 @@ void dgemm_launch(int S, int tiles, hipStream_t st, const at::Tensor& x, const a
                   bf16* out, int64_t ldo, float* part, int F, unsigned* tickets, float* xchg, int* err) {
   constexpr int XS = BN == 128 ? 3 : 2, WS = BN == 128 ? 4 : 3;
   constexpr int LDW = BN == 128 ? 4 : 0;   // BN = 256 needs 200 VGPRs: no room for a third wave per SIMD
+  const int so = EPI == EPI_SILU2 ? 0 : split_outer_default();
+  // cache-policy variants (ABL bits 4 and 7, real variants): weights streamed with the
+  // non-temporal hint -- 16 GB of weights per decode step have no reuse and should not
+  // evict the activations and the split-K workspace -- and / or the f32 partial slabs
+  // written non-temporally, so they do not sit dirty in L2 for the kernel-end write-back
+  const int pol = LDW == 4 ? (wnt_default() ? 16 : 0) | (ntst_default() ? 128 : 0) : 0;
+#define POL_(A)                                                                                                  \
+  case A:                                                                                                        \
+    dgemm_kernel<BN, XS, WS, EPI, A, LDW><<<dim3(tiles * S), 768, 0, st>>>(                                      \
+        (const bf16*)x.data_ptr(), x.stride(0), (const bf16*)w.data_ptr(), M, N, K, S, out, ldo, part, F, tickets, \
+        xchg, err, so);                                                                                          \
+    return;
+  switch (pol) { POL_(16) POL_(128) POL_(144) default: break; }
+#undef POL_
   dgemm_kernel<BN, XS, WS, EPI, 0, LDW><<<dim3(tiles * S), LDW ? 768 : 512, 0, st>>>((const bf16*)x.data_ptr(), x.stride(0),
                                                                  (const bf16*)w.data_ptr(), M, N, K, S, out, ldo,
-                                                                 part, F, tickets, xchg, err,
-                                                                 EPI == EPI_SILU2 ? 0 : split_outer_default());
+                                                                 part, F, tickets, xchg, err, so);
 }
 
 void check_xw(const at::Tensor& x, const at::Tensor& w) {
