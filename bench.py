@@ -686,6 +686,7 @@ def main():
                                                          (round(x, 1) for x in llm.exec.timings())))),
             "stream_load": _stream_summary(gathered, args, world),
             "prompt_len_pcts_rank0": _pcts(list(llm.prompt_lens)),
+            "prefill_step_tokens_rank0": list(llm.prefill_step_tokens)[-40:],
         }), flush=True)
     barrier()
     runner.stop(timeout=10)

@@ -227,6 +227,8 @@ class LLMEngine:
         self.prompt_lens: collections.deque = collections.deque(maxlen=8192)
         # wall-clock (time.time) times at which requests reached the scheduler
         self.arrival_log: collections.deque = collections.deque(maxlen=8192)
+        # token counts of the recent steps that carried prefill work
+        self.prefill_step_tokens: collections.deque = collections.deque(maxlen=4096)
         self.buckets = sorted(set(graph_buckets or [b for b in (1, 2, 4, 8, 16, 24, 32, 48, 64, 96, 128, 160, 192,
                                                                  224, 256, 320, 384, 448, 512) if b <= max_batch]
                                   + [max_batch]))
@@ -429,7 +431,27 @@ class LLMEngine:
             if n < remaining:
                 break
             self.waiting.pop(0)
+        self._align_step(chosen, n_decode)
         return chosen
+
+    def _align_step(self, chosen, n_decode: int) -> None:
+        """Trim the step's last prefill chunk so the step's token count (decode rows +
+        prefill tokens) is a multiple of 256 when prompt work is left over anyway: the
+        prefill GEMMs then run whole 256-row tiles, and hipBLASLt keeps its large-tile
+        kernels (an M of 16384 + decode rows picked kernels ~25 % slower in the RAG bench).
+        The trimmed tokens go first in the next step; nothing is trimmed when this step
+        would drain the queue (that would cost a step)."""
+        if not chosen:
+            return
+        T = n_decode + sum(n for _, n in chosen)
+        cut = T % 256
+        r, n = chosen[-1]
+        more = bool(self.waiting)
+        if T < 4096 or cut == 0 or n <= cut or not more:
+            return
+        chosen[-1] = (r, n - cut)
+        if not self.waiting or self.waiting[0] is not r:
+            self.waiting.insert(0, r)   # its last chunk no longer completes the prompt
 
     def _preempt_one(self, exclude: Optional[Request] = None) -> bool:
         for victim in reversed(self.running):
@@ -580,6 +602,8 @@ class LLMEngine:
         else:
             self.stats["mixed_steps" if nd and npf else ("prefill_steps" if npf else "decode_steps")] += 1
         self.stats["prefill_tokens"] += npf
+        if npf:
+            self.prefill_step_tokens.append(nd + npf)
         self.stats["decode_tokens"] += nd
         return _InFlight(sample_reqs, slot, n_top, self._step_id)
 
