@@ -283,6 +283,14 @@ class GroupConsumer:
         self._hb: Optional[threading.Thread] = None
         self._lock = threading.RLock()
         self._commit_error: Optional[BaseException] = None
+        # asynchronous offset commits (the reference's commitAsync, KafkaConsumerWrapper
+        # .java:266): commit() records the new contiguous prefix and returns; one committer
+        # thread sends the latest offsets per partition, coalescing the calls made while a
+        # request was in flight.  flush_commits() sends synchronously (rebalance, close).
+        self._pending: Dict[int, int] = {}
+        self._commit_cv = threading.Condition(threading.Lock())
+        self._commit_send = threading.Lock()
+        self._committer: Optional[threading.Thread] = None
 
     # -------------------------------------------------------------- membership
     def _coordinator(self) -> KafkaConnection:
@@ -295,6 +303,7 @@ class GroupConsumer:
         return self._coord
 
     def _join(self) -> None:
+        self.flush_commits()   # offsets of the partitions about to be revoked, old generation
         coord = self._coordinator()
         meta = P.encode(P.SUBSCRIPTION, {"version": 0, "topics": [self.topic], "user_data": None})
         while True:
@@ -366,9 +375,16 @@ class GroupConsumer:
         self._join()
         self._hb = threading.Thread(target=self._heartbeat_loop, daemon=True, name=f"kafka-hb-{self.group}")
         self._hb.start()
+        self._committer = threading.Thread(target=self._commit_loop, daemon=True, name=f"kafka-commit-{self.group}")
+        self._committer.start()
 
     def close(self) -> None:
         self._stop.set()
+        with self._commit_cv:
+            self._commit_cv.notify_all()
+        if self._committer is not None:
+            self._committer.join(5)
+        self.flush_commits()
         try:
             self._coordinator().request(P.LEAVE_GROUP, {"group_id": self.group, "member_id": self.member_id})
         except Exception:  # noqa: BLE001
@@ -419,19 +435,41 @@ class GroupConsumer:
                     to_commit[p] = c
         if not to_commit:
             return
-        try:
-            r = self._coordinator().request(P.OFFSET_COMMIT, {
-                "group_id": self.group, "generation": self.generation, "member_id": self.member_id,
-                "retention": -1, "topics": [{"name": self.topic, "partitions": [
-                    {"partition": p, "offset": o, "metadata": None} for p, o in to_commit.items()]}]})
-            for t in r["topics"]:
-                for pr in t["partitions"]:
-                    if pr["error"] in (P.REBALANCE_IN_PROGRESS, P.ILLEGAL_GENERATION, P.UNKNOWN_MEMBER_ID):
-                        self._need_rejoin = True
-                    elif pr["error"] != P.NONE:
-                        self._commit_error = KafkaError(pr["error"], "offset commit")
-        except Exception as e:  # noqa: BLE001
-            self._commit_error = e
+        with self._commit_cv:
+            self._pending.update(to_commit)
+            self._commit_cv.notify()
+        if self._committer is None:   # not started (tests driving the consumer directly)
+            self.flush_commits()
+
+    def _commit_loop(self) -> None:
+        while True:
+            with self._commit_cv:
+                while not self._pending and not self._stop.is_set():
+                    self._commit_cv.wait()
+                if self._stop.is_set():
+                    return
+            self.flush_commits()
+
+    def flush_commits(self) -> None:
+        """Send the pending offsets now (synchronous)."""
+        with self._commit_send:
+            with self._commit_cv:
+                batch, self._pending = self._pending, {}
+            if not batch:
+                return
+            try:
+                r = self._coordinator().request(P.OFFSET_COMMIT, {
+                    "group_id": self.group, "generation": self.generation, "member_id": self.member_id,
+                    "retention": -1, "topics": [{"name": self.topic, "partitions": [
+                        {"partition": p, "offset": o, "metadata": None} for p, o in sorted(batch.items())]}]})
+                for t in r["topics"]:
+                    for pr in t["partitions"]:
+                        if pr["error"] in (P.REBALANCE_IN_PROGRESS, P.ILLEGAL_GENERATION, P.UNKNOWN_MEMBER_ID):
+                            self._need_rejoin = True
+                        elif pr["error"] != P.NONE:
+                            self._commit_error = KafkaError(pr["error"], "offset commit")
+            except Exception as e:  # noqa: BLE001
+                self._commit_error = e
 
     def committed(self) -> Dict[int, int]:
         with self._lock:
