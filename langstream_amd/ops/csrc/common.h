@@ -127,6 +127,41 @@ static __device__ __forceinline__ void glds16_nt(const bf16* src, char* lds_wave
       : "memory");
 }
 
+// Raw buffer resource over `bytes` bytes from p (stride 0): loads at or past `bytes`
+// (voffset + instruction offset) return zeros without touching memory.
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ i32x4 make_rsrc(const void* p, uint32_t bytes) {
+  const uint64_t a = (uint64_t)(uintptr_t)p;
+  i32x4 r;
+  r[0] = __builtin_amdgcn_readfirstlane((int)(uint32_t)a);
+  r[1] = __builtin_amdgcn_readfirstlane((int)((a >> 32) & 0xffff));
+  r[2] = __builtin_amdgcn_readfirstlane((int)bytes);
+  r[3] = 0x00020000;
+  return r;
+}
+
+// 16 B per lane from rsrc + voff + soff into LDS at lds_wave_base + 16 * lane (M0-based,
+// as glds16; inline asm so hipcc does not drain vmcnt before the next ds_read).  The
+// range check applies to voff only.  NT: the non-temporal hint.
+template <bool NT = false>
+static __device__ __forceinline__ void blds16(i32x4 rsrc, int voff, int soff, unsigned lds_addr) {
+  const unsigned dst = __builtin_amdgcn_readfirstlane(lds_addr);
+  unsigned keep;
+  if constexpr (NT)
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen nt lds\n\ts_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(voff), "s"(rsrc), "s"(dst), "s"(soff)
+        : "memory");
+  else
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(voff), "s"(rsrc), "s"(dst), "s"(soff)
+        : "memory");
+}
+
 template <int N>
 static __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");

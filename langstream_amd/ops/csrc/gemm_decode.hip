@@ -111,36 +111,43 @@ __global__ void __launch_bounds__(LD ? 768 : 512) dgemm_kernel(const bf16* __res
   const int kb = (int)(((int64_t)split * nk) / S), ke = (int)(((int64_t)(split + 1) * nk) / S);
   const int nks = ke - kb;
 
-  // ---- LDS-DMA sources
-  const bf16* xsrc[PX];
+  // ---- LDS-DMA sources: buffer resources from this split's first K column (X rows at
+  // or past M fall outside the X resource and read zeros; they are never stored).  X
+  // pieces keep one per-lane byte offset each (the row decides the range check); a W
+  // piece is 8 consecutive rows, so its row base and the K stage go in the scalar
+  // offset and only two per-lane offsets remain (the swizzle depends on the piece's row
+  // parity) -- 64-bit pointers per piece cost BN = 256 its third wave per SIMD.
+  const i32x4 xrs = make_rsrc(x + (int64_t)kb * BK, (uint32_t)((((int64_t)(M - 1) * ldx + K) - (int64_t)kb * BK) * 2));
+  const i32x4 wrs = make_rsrc(w + (int64_t)kb * BK, (uint32_t)(((int64_t)N * K - (int64_t)kb * BK) * 2));
+  int xvo[PX];
 #pragma unroll
   for (int j = 0; j < PX; ++j) {
     const int row = (8 * PX) * lw + 8 * j + (lane >> 3);
-    xsrc[j] = x + (int64_t)min(row, M - 1) * ldx + (int64_t)kb * BK + piece_chunk(lane, row);  // rows >= M: never stored
+    xvo[j] = (row * (int)ldx + piece_chunk(lane, row)) * 2;
   }
-  const bf16* wsrc[PW];
+  int wvo[2];
 #pragma unroll
-  for (int j = 0; j < PW; ++j) {
-    const int lr = (8 * PW) * lw + 8 * j + (lane >> 3);    // tile-local W row
-    int wrow;
+  for (int p = 0; p < 2; ++p)
+    wvo[p] = ((lane >> 3) * K + (((lane & 7) ^ ((4 * p + (lane >> 4)) & 7)) * 8)) * 2;
+  auto wrow0 = [&](int j) -> uint32_t {   // first W row of piece j (uniform)
+    const int lr = (8 * PW) * lw + 8 * j;
     if constexpr (EPI == EPI_SILU || EPI == EPI_SILU2)
-      wrow = lr < BN / 2 ? tile * (BN / 2) + lr : F + tile * (BN / 2) + (lr - BN / 2);
-    else
-      wrow = tile * BN + lr;
-    wsrc[j] = w + (int64_t)wrow * K + (int64_t)kb * BK + piece_chunk(lane, lr);
-  }
+      return lr < BN / 2 ? tile * (BN / 2) + lr : F + tile * (BN / 2) + (lr - BN / 2);
+    return tile * BN + lr;
+  };
+  const unsigned lxa = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)lx0;
+  const unsigned lwa = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)lw0;
   auto issue_x = [&](int t) {
-    char* dst = lx0 + (t % XS) * XSTAGE + (PX * lw) * 1024;
+    const unsigned dst = lxa + (t % XS) * XSTAGE + (PX * lw) * 1024;
 #pragma unroll
-    for (int j = 0; j < PX; ++j) glds16(xsrc[j] + t * BK, dst + j * 1024);
+    for (int j = 0; j < PX; ++j) blds16<false>(xrs, xvo[j], t * BK * 2, dst + j * 1024);
   };
   auto issue_w = [&](int t) {
-    char* dst = lw0 + (t % WS) * WSTAGE + (PW * lw) * 1024;
+    const unsigned dst = lwa + (t % WS) * WSTAGE + (PW * lw) * 1024;
 #pragma unroll
-    for (int j = 0; j < PW; ++j) {
-      if constexpr ((ABL & 16) != 0) glds16_nt(wsrc[j] + t * BK, dst + j * 1024);
-      else glds16(wsrc[j] + t * BK, dst + j * 1024);
-    }
+    for (int j = 0; j < PW; ++j)
+      blds16<(ABL & 16) != 0>(wrs, wvo[(PW * lw + j) & 1], (int)(wrow0(j) * (uint32_t)K * 2u + (uint32_t)(t * BK * 2)),
+                              dst + j * 1024);
   };
 
   // ---- fragments
@@ -226,8 +233,9 @@ __global__ void __launch_bounds__(LD ? 768 : 512) dgemm_kernel(const bf16* __res
   // acc[i][j][r] = C[64wm + 16i + 4h + r][tile col of bcol(j)]
   const int rbase = 64 * wm + 4 * h;
   if constexpr (EPI == EPI_SILU2) {
-    static_assert(LD == 0, "the half exchange runs with every wave computing");
-    // ---- in-launch combine of the two K halves (see the header)
+    // ---- in-launch combine of the two K halves (see the header); with loader waves
+    // (LD = 4) only the 512 compute threads hold accumulators, the loaders only join
+    // the workgroup barriers
     __syncthreads();                                      // ring reads done: LDS reusable
     unsigned* sh = reinterpret_cast<unsigned*>(lds);
     if (threadIdx.x == 0) sh[0] = __hip_atomic_fetch_add(&tickets[2 * tile], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -237,11 +245,13 @@ __global__ void __launch_bounds__(LD ? 768 : 512) dgemm_kernel(const bf16* __res
     float* xb = xchg + (int64_t)tile * (BM * BN);
     if ((tk & 1u) == 0) {
       // first half: publish the accumulators in a thread-linear, coalesced layout
+      if (computer) {
 #pragma unroll
-      for (int i = 0; i < IT; ++i)
+        for (int i = 0; i < IT; ++i)
 #pragma unroll
-        for (int j = 0; j < JT; ++j)
-          *reinterpret_cast<f32x4*>(xb + ((int64_t)(i * JT + j) * 512 + threadIdx.x) * 4) = acc[i][j];
+          for (int j = 0; j < JT; ++j)
+            *reinterpret_cast<f32x4*>(xb + ((int64_t)(i * JT + j) * 512 + threadIdx.x) * 4) = acc[i][j];
+      }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (threadIdx.x == 0) {
@@ -264,20 +274,23 @@ __global__ void __launch_bounds__(LD ? 768 : 512) dgemm_kernel(const bf16* __res
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
+    if (!computer) return;
     // combine + SwiGLU + store one 16-row tile at a time (bounded live registers)
 #pragma unroll
     for (int i = 0; i < IT; ++i) {
-      f32x4 g[JT];
 #pragma unroll
-      for (int j = 0; j < JT; ++j)
-        g[j] = acc[i][j] + *reinterpret_cast<const f32x4*>(xb + ((int64_t)(i * JT + j) * 512 + threadIdx.x) * 4);
+      for (int j = 0; j < JT / 2; ++j) {
+        // gate column j and its up column j + JT/2, one pair at a time (bounded registers)
+        const f32x4 g = acc[i][j] + *reinterpret_cast<const f32x4*>(xb + ((int64_t)(i * JT + j) * 512 + threadIdx.x) * 4);
+        const f32x4 u = acc[i][j + JT / 2] +
+                        *reinterpret_cast<const f32x4*>(xb + ((int64_t)(i * JT + j + JT / 2) * 512 + threadIdx.x) * 4);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = rbase + 16 * i + r;
-        if (m >= M) continue;
-        bf16* orow = out + (int64_t)m * ldo + tile * (BN / 2) + (BN / 4) * wn + fr;
-#pragma unroll
-        for (int j = 0; j < JT / 2; ++j) orow[16 * j] = (bf16)(g[j][r] / (1.f + __expf(-g[j][r])) * g[j + JT / 2][r]);
+        for (int r = 0; r < 4; ++r) {
+          const int m = rbase + 16 * i + r;
+          if (m < M)
+            out[(int64_t)m * ldo + tile * (BN / 2) + (BN / 4) * wn + fr + 16 * j] =
+                (bf16)(g[r] / (1.f + __expf(-g[r])) * u[r]);
+        }
       }
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -374,7 +387,11 @@ template <int BN, int EPI>
 void dgemm_launch(int S, int tiles, hipStream_t st, const at::Tensor& x, const at::Tensor& w, int M, int N, int K,
                   bf16* out, int64_t ldo, float* part, int F, unsigned* tickets, float* xchg, int* err) {
   constexpr int XS = BN == 128 ? 3 : 2, WS = BN == 128 ? 4 : 3;
-  constexpr int LDW = BN == 128 ? 4 : 0;   // BN = 256 needs 200 VGPRs: no room for a third wave per SIMD
+  // BN = 256: 8 compute waves need 128 accumulator VGPRs each, no room for a third wave
+  // per SIMD.  (Streaming the B fragments one at a time fits 168 VGPRs with 4 loader
+  // waves, but the gate_up K-half exchange form then measured 90 vs 82 us:
+  // profiles/dgemm_r3c/silu2_loaders.log.)
+  constexpr int LDW = BN == 128 ? 4 : 0;
   const int so = EPI == EPI_SILU2 ? 0 : split_outer_default();
   // cache-policy variants (ABL bits 4 and 7, real variants): weights streamed with the
   // non-temporal hint -- 16 GB of weights per decode step have no reuse and should not

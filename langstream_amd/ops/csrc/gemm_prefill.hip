@@ -540,29 +540,7 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(const bf16* __restrict__ x
 // resources: the per-lane offsets are tile-independent (8 VGPRs instead of 8 pointers),
 // rows past M fall outside the X resource's range and read zeros, and the "tile" after
 // a workgroup's last one has an empty resource (its dummy prefetches move no bytes).
-typedef int i32x4 __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ i32x4 make_rsrc(const void* p, uint32_t bytes) {
-  const uint64_t a = (uint64_t)(uintptr_t)p;
-  i32x4 r;
-  r[0] = __builtin_amdgcn_readfirstlane((int)(uint32_t)a);
-  r[1] = __builtin_amdgcn_readfirstlane((int)((a >> 32) & 0xffff));
-  r[2] = __builtin_amdgcn_readfirstlane((int)bytes);
-  r[3] = 0x00020000;
-  return r;
-}
-
-// 16 B per lane from rsrc + voff + soff into LDS at lds_wave_base + 16 * lane (M0-based,
-// as glds16; inline asm so hipcc does not drain vmcnt before the next ds_read)
-static __device__ __forceinline__ void blds16(i32x4 rsrc, int voff, int soff, unsigned lds_addr) {
-  const unsigned dst = __builtin_amdgcn_readfirstlane(lds_addr);
-  unsigned keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(voff), "s"(rsrc), "s"(dst), "s"(soff)
-      : "memory");
-}
+// (make_rsrc / blds16: common.h)
 
 template <int EPI>
 __global__ void __launch_bounds__(512) gemm_pp2_kernel(const bf16* __restrict__ x, int64_t ldx,
