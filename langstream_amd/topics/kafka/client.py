@@ -288,6 +288,10 @@ class GroupConsumer:
         # thread sends the latest offsets per partition, coalescing the calls made while a
         # request was in flight.  flush_commits() sends synchronously (rebalance, close).
         self._pending: Dict[int, int] = {}
+        # records fetched beyond max.poll.records, served by the next polls (a fetch
+        # response carries up to 1000 records per partition; re-fetching the surplus made
+        # the broker encode every record twice)
+        self._buf: Dict[int, List[tuple]] = {}
         self._commit_cv = threading.Condition(threading.Lock())
         self._commit_send = threading.Lock()
         self._committer: Optional[threading.Thread] = None
@@ -345,6 +349,7 @@ class GroupConsumer:
 
     def _init_positions(self) -> None:
         self.positions = {}
+        self._buf = {}
         self._acked = {p: set() for p in self.assigned}
         if not self.assigned:
             return
@@ -400,6 +405,12 @@ class GroupConsumer:
         if self._need_rejoin:
             self._join()
         with self._lock:
+            if any(self._buf.values()):
+                out = []
+                for p, recs in self._buf.items():
+                    out.extend((p,) + r for r in recs[: self.max_poll])
+                    self._buf[p] = recs[self.max_poll:]
+                return out
             pos = dict(self.positions)
         if not pos:
             time.sleep(timeout_ms / 1000.0)
@@ -408,12 +419,13 @@ class GroupConsumer:
         out = []
         with self._lock:
             for p, (_hw, recs) in res.items():
-                if p not in self.positions:
-                    continue
-                for r in recs[: self.max_poll]:
-                    out.append((p,) + r)
+                if p not in self.positions or self.positions[p] != pos.get(p):
+                    continue   # reassigned or moved while the fetch was in flight
+                out.extend((p,) + r for r in recs[: self.max_poll])
+                if len(recs) > self.max_poll:
+                    self._buf[p] = list(recs[self.max_poll:])
                 if recs:
-                    self.positions[p] = recs[: self.max_poll][-1][0] + 1
+                    self.positions[p] = recs[-1][0] + 1
         return out
 
     def commit(self, offsets: List[Tuple[int, int]]) -> None:
