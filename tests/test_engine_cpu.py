@@ -128,3 +128,24 @@ def test_prefill_tiles_np_matches_torch():
             w = lambda t: pre[t[0]] + (min(t[1] + ops.PREFILL_ROWS, q[t[0]] * G) - 1) // G  # noqa: E731
             ws = [w(t) for t in b.tolist()]
             assert ws == sorted(ws, reverse=True)
+
+
+def test_full_prefill_steps_are_256_aligned(model):
+    """A step whose prefill budget is used up carries decode rows + prefill tokens in a
+    multiple of 256 (the prefill GEMMs run whole 256-row tiles), and the outputs equal an
+    engine with a small unaligned budget (chunking does not change greedy tokens)."""
+    V = model.cfg.vocab_size
+    prompts = [[3 + (7 * i + n) % (V - 3) for i in range(n)] for n in (300, 700, 650, 1500, 1800, 1700, 1200, 40, 510)]
+    sp = SamplingParams(max_tokens=6, temperature=0.0, ignore_eos=True)
+    eng = LLMEngine(model, None, num_blocks=256, max_model_len=2048, max_batch=16, max_prefill_tokens=4608)
+    reqs = [eng.submit(p, sp) for p in prompts[:3]]
+    for _ in range(3):       # some decode rows running before the large prompts arrive
+        eng.step()
+    reqs += [eng.submit(p, sp) for p in prompts[3:]]
+    while not all(r.finished for r in reqs):
+        eng.step()
+    eng._flush()
+    full = [t for t in eng.prefill_step_tokens if t > 4608 - 256]
+    assert full and all(t % 256 == 0 for t in full), list(eng.prefill_step_tokens)
+    ref = LLMEngine(model, None, num_blocks=256, max_model_len=2048, max_batch=16, max_prefill_tokens=333)
+    assert [r.output_ids for r in reqs] == [r.output_ids for r in ref.generate(prompts, sp)]
