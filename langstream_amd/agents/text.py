@@ -392,21 +392,70 @@ def _pdf_text(data: bytes) -> str:
     return re.sub(r"\n{2,}", "\n", text).strip()
 
 
+def _email_text(s: str) -> str:
+    """RFC 822 / MIME message: subject + the text/plain parts (text/html parts as text
+    when there is no plain part)."""
+    import email
+    from email import policy
+    msg = email.message_from_string(s, policy=policy.default)
+    plain, htmls = [], []
+    for part in (msg.walk() if msg.is_multipart() else [msg]):
+        ctype = part.get_content_type()
+        if part.get_content_maintype() == "multipart" or part.get_filename():
+            continue
+        try:
+            body = part.get_content()
+        except Exception:  # noqa: BLE001 - undecodable part
+            continue
+        if not isinstance(body, str):
+            continue
+        if ctype == "text/plain":
+            plain.append(body.strip())
+        elif ctype == "text/html":
+            htmls.append(html_to_text(body).strip())
+    head = str(msg.get("subject") or "").strip()
+    return "\n".join([head] + (plain or htmls) if head else (plain or htmls)).strip()
+
+
+_EMAIL_HEAD = re.compile(r"^(?:(?:From|To|Subject|Date|Message-ID|MIME-Version|Received|Return-Path)"
+                         r":[^\n]*\n)+", re.I)
+
+
 def extract_text(data: Any) -> str:
+    """Text of a document (the reference runs Tika's AutoDetectParser,
+    TikaTextExtractorAgent.java:36-58): PDF, OOXML (docx / pptx / xlsx), ODF, EPUB, RTF,
+    HTML / XHTML / XML, MIME e-mail, gzip-wrapped content and UTF-8/16 text (BOMs)."""
     if isinstance(data, str):
-        s = data.lstrip()
+        s = data.lstrip("\ufeff").lstrip()
         if s[:1] == "<" and re.search(r"<(html|body|p|div)\b", s[:2000], re.I):
-            return html_to_text(data)
-        return data
+            return html_to_text(s)
+        if s[:5] == "<?xml" or (s[:1] == "<" and re.match(r"<[A-Za-z_][\w:.-]*[\s>/]", s)):
+            # generic XML: element text, elements separated by a space
+            t = html.unescape(re.sub(r"<[^>]+>", "", re.sub(r"</[^>]+>", " ", s)))
+            return re.sub(r"[ \t]+", " ", re.sub(r"\s*\n\s*", "\n", t)).strip()
+        if _EMAIL_HEAD.match(s):
+            return _email_text(s)
+        return s
     if not isinstance(data, (bytes, bytearray)):
         return to_text(data)
     b = bytes(data)
     if b[:4] == b"%PDF":
         return _pdf_text(b)
+    if b[:2] == b"\x1f\x8b":
+        import gzip
+        try:
+            return extract_text(gzip.decompress(b))
+        except OSError:
+            pass
+    if b[:2] in (b"\xff\xfe", b"\xfe\xff"):
+        return extract_text(b.decode("utf-16"))
     if b[:2] == b"PK":
         try:
             with zipfile.ZipFile(io.BytesIO(b)) as z:
                 names = z.namelist()
+                if "META-INF/container.xml" in names and any(n.endswith((".xhtml", ".html", ".htm")) for n in names):
+                    # EPUB: the content documents in spine order (the OPF manifest / spine)
+                    return _epub_text(z, names)
                 parts = [n for n in names if n in ("word/document.xml", "content.xml")]
                 parts += sorted(n for n in names if re.match(r"ppt/slides/slide\d+\.xml", n))
                 parts += [n for n in names if n == "xl/sharedStrings.xml"]
@@ -419,6 +468,26 @@ def extract_text(data: Any) -> str:
         return s.strip()
     s = b.decode("utf-8", errors="replace")
     return extract_text(s)
+
+
+def _epub_text(z: "zipfile.ZipFile", names) -> str:
+    import posixpath
+    order = []
+    try:
+        cont = z.read("META-INF/container.xml").decode("utf-8", "replace")
+        opf = re.search(r'full-path="([^"]+)"', cont).group(1)
+        o = z.read(opf).decode("utf-8", "replace")
+        base = posixpath.dirname(opf)
+        items = dict(re.findall(r'<item\b[^>]*?id="([^"]+)"[^>]*?href="([^"]+)"', o))
+        items.update({i: h for h, i in re.findall(r'<item\b[^>]*?href="([^"]+)"[^>]*?id="([^"]+)"', o)})
+        for idref in re.findall(r'<itemref\b[^>]*?idref="([^"]+)"', o):
+            if idref in items:
+                order.append(posixpath.normpath(posixpath.join(base, items[idref])))
+    except Exception:  # noqa: BLE001 - no usable OPF: document order
+        order = []
+    if not order:
+        order = sorted(n for n in names if n.endswith((".xhtml", ".html", ".htm")))
+    return "\n".join(html_to_text(z.read(n).decode("utf-8", "replace")).strip() for n in order if n in names).strip()
 
 
 @register_agent("text-extractor")

@@ -202,3 +202,30 @@ def test_language_samples_do_not_contain_fixture_phrases():
     corpus = " ".join(SAMPLES.values()).lower()
     for phrase in ("this is a english", "questo é italiano", "parlez-vous français"):
         assert phrase not in corpus
+
+
+def test_extractor_more_formats():
+    """EPUB (spine order), gzip-wrapped, UTF-16 with BOM, generic XML, MIME e-mail."""
+    import gzip
+    import io
+    import zipfile
+    from langstream_amd.agents.text import extract_text
+    buf = io.BytesIO()
+    with zipfile.ZipFile(buf, "w") as z:
+        z.writestr("mimetype", "application/epub+zip")
+        z.writestr("META-INF/container.xml",
+                   '<container><rootfiles><rootfile full-path="OEBPS/content.opf"/></rootfiles></container>')
+        z.writestr("OEBPS/content.opf",
+                   '<package><manifest><item id="c2" href="ch2.xhtml"/><item id="c1" href="ch1.xhtml"/></manifest>'
+                   '<spine><itemref idref="c1"/><itemref idref="c2"/></spine></package>')
+        z.writestr("OEBPS/ch1.xhtml", "<html><body><p>Chapter one.</p></body></html>")
+        z.writestr("OEBPS/ch2.xhtml", "<html><body><p>Chapter two.</p></body></html>")
+    t = extract_text(buf.getvalue())
+    assert t.index("Chapter one.") < t.index("Chapter two.")
+    assert extract_text(gzip.compress("<html><body><p>zipped &amp; fine</p></body></html>".encode())) == "zipped & fine"
+    assert extract_text("﻿hello world".encode("utf-16")) == "hello world"
+    assert extract_text(b'<?xml version="1.0"?><note><to>Tove</to><msg>there &lt;3</msg></note>') == "Tove there <3"
+    mail = ("From: a@example.com\nTo: b@example.com\nSubject: Quarterly report\nMIME-Version: 1.0\n"
+            "Content-Type: multipart/alternative; boundary=XX\n\n--XX\nContent-Type: text/plain\n\n"
+            "Numbers are up.\n--XX\nContent-Type: text/html\n\n<p>Numbers are <b>up</b>.</p>\n--XX--\n")
+    assert extract_text(mail.encode()) == "Quarterly report\nNumbers are up."
