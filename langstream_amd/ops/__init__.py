@@ -57,9 +57,28 @@ def _load():
         loader.exec_module(mod)
         sys.modules["langstream_amd.ops._hip_ops"] = mod
         _ext = mod
+        _load_pgemm_route(mod)
     except BaseException as e:  # noqa: BLE001 - remember and re-raise on GPU use
         _ext_err = e
     return _ext
+
+
+def _load_pgemm_route(mod, path: Optional[str] = None) -> int:
+    """Load ops/pgemm_route_gfx950.csv (tools/pgemm_route_tune.py: N,K,M,lib_us,pp_us per
+    256-row M bucket) into the runner's prefill routing table: the plain projections run on
+    gemm_prefill where it measured >= 3 % faster than hipBLASLt.  LS_PGEMM_ROUTE=0: off."""
+    path = path or os.path.join(_HERE, "pgemm_route_gfx950.csv")
+    if os.environ.get("LS_PGEMM_ROUTE", "1") == "0" or not os.path.exists(path):
+        return 0
+    import csv
+    rows = {}
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            key = (int(r["N"]), int(r["K"]))
+            rows.setdefault(key, {})[int(r["M"]) // 256] = float(r["pp_us"]) < 0.97 * float(r["lib_us"])
+    for (n, k), d in rows.items():
+        mod.set_pgemm_route(n, k, [int(d.get(b, False)) for b in range(max(d) + 1)])
+    return len(rows)
 
 
 _TUNED = None

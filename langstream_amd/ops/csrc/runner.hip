@@ -43,6 +43,28 @@
 
 namespace py = pybind11;
 
+// Prefill routing of the plain projections (qkv / o / down): hipBLASLt's kernel choice is
+// erratic across M -- 1.55 PFLOP/s at M = 8192 or 16384, 0.9-1.1 at some M in between --
+// while gemm_pp_kernel holds 1.25-1.43 (profiles/pgemm_m2_r3c.log).  A per-(N, K) table of
+// 256-row M buckets, measured on the target by tools/pgemm_route_tune.py and loaded at
+// import (ops/pgemm_route_gfx950.csv), says where gemm_prefill is the faster one.
+namespace pgemm_route {
+std::mutex mu;
+std::map<std::pair<int64_t, int64_t>, std::vector<uint8_t>> table;   // (N, K) -> use_pp per M/256
+void set(int64_t N, int64_t K, std::vector<int64_t> use_pp) {
+  std::lock_guard<std::mutex> lk(mu);
+  std::vector<uint8_t> v(use_pp.begin(), use_pp.end());
+  table[{N, K}] = std::move(v);
+}
+bool use_pp(int64_t T, int64_t N, int64_t K) {
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = table.find({N, K});
+  if (it == table.end()) return false;
+  const int64_t b = (T + 128) / 256;
+  return b >= 0 && b < (int64_t)it->second.size() && it->second[b] != 0;
+}
+}  // namespace pgemm_route
+
 void rmsnorm(at::Tensor out, at::Tensor x, at::Tensor w, double eps);
 void fused_add_rmsnorm(at::Tensor x, at::Tensor residual, at::Tensor w, double eps);
 void layernorm(at::Tensor out, at::Tensor x, c10::optional<at::Tensor> bias, c10::optional<at::Tensor> residual,
@@ -512,7 +534,9 @@ class LlamaRunner {
       const char* e = getenv("LS_PGEMM_MIN_T");
       return e ? (int64_t)atoll(e) : (int64_t)1024;
     }();
-    return mode > (silu ? 0 : 1) && T >= min_t && gemm_prefill_supported(w, silu);
+    if (!gemm_prefill_supported(w, silu) || T < min_t) return false;
+    if (silu || mode == 2) return mode > 0;
+    return mode == 1 && pgemm_route::use_pp(T, w.size(0), w.size(1));
   }
   static bool skinny_shape(const at::Tensor& w) { return w.size(0) % 128 == 0 && w.size(1) % 64 == 0; }
 
@@ -1162,6 +1186,8 @@ class StepExecutor {
 }  // namespace
 
 void bind_runners(py::module_& m) {
+  m.def("set_pgemm_route", &pgemm_route::set, "prefill routing table: use_pp[b] for M in [256 b - 128, 256 b + 128)");
+  m.def("pgemm_route_uses_pp", &pgemm_route::use_pp);
   py::class_<LlamaRunner, std::shared_ptr<LlamaRunner>>(m, "LlamaRunner")
       .def(py::init<at::Tensor, std::vector<at::Tensor>, std::vector<at::Tensor>, std::vector<at::Tensor>,
                     std::vector<at::Tensor>, std::vector<at::Tensor>, std::vector<at::Tensor>, at::Tensor, at::Tensor,
