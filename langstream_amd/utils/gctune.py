@@ -14,7 +14,9 @@ GC pause per 9.7 s, 3 full collections; `bench.py` reports `gc_rank0`).
   * thresholds (50000, 20, 100): young collections every 50k net allocations, full
     collections rarely.
 Cycles are still collected.  LANGSTREAM_GC=default keeps CPython's policy;
-LANGSTREAM_GC_GEN0 overrides the young-generation threshold.
+LANGSTREAM_GC_GEN0 overrides the young-generation threshold.  (Round 3, one box,
+alternating runs: 400000 removes the two ~30 ms young collections of 3 RAG steps but
+measured 118.3 / 119.0 records/s against 122.0 / 121.3 at 50000 -- profiles/gc_r3c/.)
 """
 from __future__ import annotations
 
