@@ -428,6 +428,7 @@ def main():
 
     from langstream_amd.engine import dist_knn
     from langstream_amd.engine.vector_store import VectorStoreRegistry
+    from langstream_amd.runtime import composite as _composite
     from langstream_amd.runtime.local import LocalApplicationRunner
     from langstream_amd.services import ServiceRegistry
     from langstream_amd.tokenizers import builtin_corpus
@@ -472,6 +473,8 @@ def main():
     if multi:
         dist_knn.start(device=device)
     only = None if rank == 0 else ["query", "ingest"]   # the crawler runs once (rank 0)
+    if os.environ.get("LS_STAGE_TRACE", "0") != "0":
+        _composite.STAGE_TRACE = []
     runner = LocalApplicationRunner.from_yaml(files, instance=INSTANCE.format(**fmt), application_id="rag-bench",
                                               services=services, agents=only)
     runner.start()
@@ -500,6 +503,7 @@ def main():
 
     sent = {}
     phases = []
+    stage_trace = []
 
     def publish_pages(step):
         if args.docs <= 0:
@@ -516,9 +520,10 @@ def main():
         step = steps_done[0]
         t0 = time.time()
         publish_pages(step)
+        step_keys = set()
         if args.load == "burst" or step == 0:
             for _ in range(args.batch):
-                send_question()
+                step_keys.add(send_question())
         expect_docs = (step + 1) * args.docs * world
         lats = []
         t_first = t_all = None
@@ -547,6 +552,15 @@ def main():
         arr = [a for a in list(llm.arrival_log) if t0 <= a <= t_end]
         phases.append([round((t_first or t_end) - t0, 3), round((t_all or t_end) - t0, 3), round(t_end - t0, 3),
                        round(min(arr) - t0, 3) if arr else None, round(max(arr) - t0, 3) if arr else None])
+        if _composite.STAGE_TRACE is not None:
+            # per stage of the fused question chain: [p10, p50, max] of entry time - t0, s
+            by = {}
+            for k, name, t in list(_composite.STAGE_TRACE):
+                if k in step_keys and t >= t0:
+                    by.setdefault(name, []).append(t - t0)
+            stage_trace.append({n: [round(sorted(v)[min(len(v) - 1, int(q * len(v)))], 3) for q in (0.1, 0.5, 1.0)]
+                                for n, v in by.items()})
+            _composite.STAGE_TRACE.clear()
         return t_end - t0, lats
 
     def run_window(k_steps):
@@ -640,7 +654,7 @@ def main():
         stream_res = {"elapsed": time.time() - ts0, "lats": s_lats}
     mine = {"elapsed": elapsed, "lats": my_lats, "chunks": chunks, "assign": assign, "stream": stream_res,
             "prefill_tokens": stats.get("prefill_tokens", 0), "requests": stats.get("requests", 0),
-            "phases": phases, "gc": {"pause_ms": round(gc_t["ms"], 1), "collections_by_gen": gc_t["n"]},
+            "phases": phases, "stage_trace": stage_trace, "gc": {"pause_ms": round(gc_t["ms"], 1), "collections_by_gen": gc_t["n"]},
             "knn_rounds": dist_knn.active().rounds if dist_knn.active() else 0,
             "knn_stats": ({k: (round(v, 3) if isinstance(v, float) else v) for k, v in dist_knn.active().stats.items()}
                           if dist_knn.active() else None)}
@@ -678,7 +692,8 @@ def main():
                        "parallelism": f"dp{world}"},
             "ingest": {"pages_per_s": round(args.docs * args.steps * world / elapsed, 2),
                        "chunks_per_s": round(sum(g["chunks"] for g in gathered) / elapsed, 2)},
-            "latency_samples": len(all_lats), "step_phases_rank0_s": gathered[0]["phases"], "gc_rank0": gathered[0]["gc"], "knn_rounds_per_rank": [g["knn_rounds"] for g in gathered],
+            "latency_samples": len(all_lats), "step_phases_rank0_s": gathered[0]["phases"],
+            **({"stage_trace_rank0_s": gathered[0]["stage_trace"]} if gathered[0]["stage_trace"] else {}), "gc_rank0": gathered[0]["gc"], "knn_rounds_per_rank": [g["knn_rounds"] for g in gathered],
             "knn_stats_rank0": gathered[0]["knn_stats"],
             "partitions_per_rank": [g["assign"] for g in gathered],
             "setup_s": round(setup_s, 1),

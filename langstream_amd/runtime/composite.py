@@ -10,12 +10,18 @@ from __future__ import annotations
 
 import logging
 import threading
+import time
 from typing import Any, Dict, List, Optional
 
 from ..api.agent import AgentProcessor, AgentSink, AgentSource, AgentStatusResponse
 from ..api.record import Record, RecordSink, SourceRecordAndResult
 
 log = logging.getLogger(__name__)
+
+# Optional stage tracer (benchmarks): when a list, every record entering processor i of a
+# composite appends (source key, agent type of processor i, time.time()); the chain's end
+# appends (key, "end", t).  Off (None) by default: one attribute test per step.
+STAGE_TRACE: Optional[list] = None
 
 
 class CompositeAgentProcessor(AgentProcessor):
@@ -84,6 +90,9 @@ class CompositeAgentProcessor(AgentProcessor):
 
     def _invoke(self, index: int, current: List[Record], initial: Record, final: RecordSink) -> None:
         proc = self.processors[index]
+        tr = STAGE_TRACE
+        if tr is not None:
+            tr.append((initial.key(), f"{index}:{proc._agent_id}", time.time()))
         state = {"results": [], "failed": False}
         lock = threading.Lock()
         n = len(current)
@@ -113,6 +122,8 @@ class CompositeAgentProcessor(AgentProcessor):
                 final(SourceRecordAndResult(initial, [], None))
             elif index == len(self.processors) - 1:
                 self.processed(0, len(out))
+                if tr is not None:
+                    tr.append((initial.key(), "end", time.time()))
                 final(SourceRecordAndResult(initial, out, None))
             else:
                 self._invoke(index + 1, out, initial, final)
