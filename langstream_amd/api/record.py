@@ -22,7 +22,8 @@ class Header:
         if isinstance(v, str):
             return v
         if isinstance(v, (dict, list)):
-            return json.dumps(v)
+            from ..utils import fastjson
+            return fastjson.dumps(v)
         return str(v)
 
 

@@ -1,0 +1,263 @@
+// json_dumps(obj) -> str: byte-identical to Python's json.dumps(obj) with its default
+// options (", " / ": " separators, ensure_ascii, allow_nan, insertion-ordered keys),
+// for dict / list / tuple / str / int / float / bool / None trees.
+//
+// Why native: records leaving an embeddings agent carry a 384..1024-float vector, and
+// json.dumps spends ~0.7 us per float in float.__repr__ + str building (263 us for one
+// bge-small record, measured) -- the whole per-record budget of the Kafka embeddings
+// pipeline (BASELINE config 2).  Floats here go through std::to_chars (shortest
+// round-trip digits, the digits repr() picks) laid out by repr's rules: positional for
+// decimal exponents -4..15 with a ".0" for integral values, else d.ddde+XX.
+//
+// Anything else (numpy scalars, objects with a `default`, cycles deeper than the
+// limit) raises _lsnative.JsonUnsupported and the Python wrapper falls back to
+// json.dumps, so errors and extensions behave exactly as before.
+#include <Python.h>
+#include <pybind11/pybind11.h>
+
+#include <charconv>
+#include <cmath>
+#include <cstring>
+#include <string>
+
+namespace py = pybind11;
+
+namespace {
+
+PyObject* g_unsupported = nullptr;
+
+struct Unsupported {};
+
+const char HEX[] = "0123456789abcdef";
+
+void put_u16(std::string& o, unsigned c) {
+  char b[6] = {'\\', 'u', HEX[(c >> 12) & 15], HEX[(c >> 8) & 15], HEX[(c >> 4) & 15], HEX[c & 15]};
+  o.append(b, 6);
+}
+
+void put_str(std::string& o, PyObject* s) {
+  if (PyUnicode_READY(s) < 0) throw Unsupported{};
+  const Py_ssize_t n = PyUnicode_GET_LENGTH(s);
+  const int kind = PyUnicode_KIND(s);
+  const void* d = PyUnicode_DATA(s);
+  o.push_back('"');
+  if (kind == PyUnicode_1BYTE_KIND) {
+    const unsigned char* p = (const unsigned char*)d;
+    Py_ssize_t i = 0;
+    while (i < n) {
+      // copy the run of characters that need no escape in one append
+      Py_ssize_t j = i;
+      while (j < n && p[j] >= 0x20 && p[j] < 0x7f && p[j] != '"' && p[j] != '\\') ++j;
+      if (j > i) o.append((const char*)p + i, j - i);
+      if (j >= n) break;
+      unsigned c = p[j];
+      switch (c) {
+        case '"': o.append("\\\""); break;
+        case '\\': o.append("\\\\"); break;
+        case '\n': o.append("\\n"); break;
+        case '\r': o.append("\\r"); break;
+        case '\t': o.append("\\t"); break;
+        case '\b': o.append("\\b"); break;
+        case '\f': o.append("\\f"); break;
+        default: put_u16(o, c);
+      }
+      i = j + 1;
+    }
+  } else {
+    for (Py_ssize_t i = 0; i < n; ++i) {
+      Py_UCS4 c = PyUnicode_READ(kind, d, i);
+      if (c >= 0x20 && c < 0x7f && c != '"' && c != '\\') {
+        o.push_back((char)c);
+        continue;
+      }
+      switch (c) {
+        case '"': o.append("\\\""); break;
+        case '\\': o.append("\\\\"); break;
+        case '\n': o.append("\\n"); break;
+        case '\r': o.append("\\r"); break;
+        case '\t': o.append("\\t"); break;
+        case '\b': o.append("\\b"); break;
+        case '\f': o.append("\\f"); break;
+        default:
+          if (c >= 0x10000) {
+            Py_UCS4 v = c - 0x10000;
+            put_u16(o, 0xd800 | ((v >> 10) & 0x3ff));
+            put_u16(o, 0xdc00 | (v & 0x3ff));
+          } else {
+            put_u16(o, c);
+          }
+      }
+    }
+  }
+  o.push_back('"');
+}
+
+// float.__repr__ layout over the shortest round-trip digits
+void put_float(std::string& o, double x) {
+  if (std::isnan(x)) { o.append("NaN"); return; }
+  if (std::isinf(x)) { o.append(x > 0 ? "Infinity" : "-Infinity"); return; }
+  if (x == 0.0) { o.append(std::signbit(x) ? "-0.0" : "0.0"); return; }
+  char buf[64];
+  auto r = std::to_chars(buf, buf + sizeof buf, x, std::chars_format::scientific);
+  if (r.ec != std::errc()) throw Unsupported{};
+  // buf = [-]d[.ddd]e(+|-)XX
+  const char* p = buf;
+  const char* end = r.ptr;
+  bool neg = false;
+  if (*p == '-') { neg = true; ++p; }
+  char dig[32];
+  int nd = 0;
+  const char* q = p;
+  for (; q < end && *q != 'e'; ++q)
+    if (*q != '.') dig[nd++] = *q;
+  int e = 0;
+  std::from_chars(q + 1 + (q[1] == '+' ? 1 : 0), end, e);
+  if (neg) o.push_back('-');
+  if (e >= -4 && e < 16) {
+    if (e < 0) {
+      o.append("0.");
+      o.append(-e - 1, '0');
+      o.append(dig, nd);
+    } else if (nd <= e + 1) {
+      o.append(dig, nd);
+      o.append(e + 1 - nd, '0');
+      o.append(".0");
+    } else {
+      o.append(dig, e + 1);
+      o.push_back('.');
+      o.append(dig + e + 1, nd - e - 1);
+    }
+  } else {
+    o.push_back(dig[0]);
+    if (nd > 1) {
+      o.push_back('.');
+      o.append(dig + 1, nd - 1);
+    }
+    o.push_back('e');
+    o.push_back(e < 0 ? '-' : '+');
+    int a = e < 0 ? -e : e;
+    if (a < 10) o.push_back('0');
+    o.append(std::to_string(a));
+  }
+}
+
+void put_int(std::string& o, PyObject* v) {
+  int overflow = 0;
+  long long x = PyLong_AsLongLongAndOverflow(v, &overflow);
+  if (overflow == 0) {
+    if (x == -1 && PyErr_Occurred()) { PyErr_Clear(); throw Unsupported{}; }
+    char b[24];
+    auto r = std::to_chars(b, b + sizeof b, x);
+    o.append(b, r.ptr - b);
+    return;
+  }
+  PyObject* s = PyObject_Str(v);   // int.__str__ is int.__repr__
+  if (!s) { PyErr_Clear(); throw Unsupported{}; }
+  Py_ssize_t n;
+  const char* c = PyUnicode_AsUTF8AndSize(s, &n);
+  if (c) o.append(c, n);
+  Py_DECREF(s);
+  if (!c) { PyErr_Clear(); throw Unsupported{}; }
+}
+
+void put(std::string& o, PyObject* v, int depth);
+
+void put_key(std::string& o, PyObject* k) {
+  if (PyUnicode_Check(k)) { put_str(o, k); return; }
+  // json.dumps coerces these key types to strings
+  o.push_back('"');
+  if (k == Py_True) o.append("true");
+  else if (k == Py_False) o.append("false");
+  else if (k == Py_None) o.append("null");
+  else if (PyFloat_Check(k)) put_float(o, PyFloat_AS_DOUBLE(k));
+  else if (PyLong_Check(k)) put_int(o, k);
+  else throw Unsupported{};
+  o.push_back('"');
+}
+
+void put(std::string& o, PyObject* v, int depth) {
+  if (depth > 200) throw Unsupported{};   // let json.dumps report recursion / cycles
+  if (PyUnicode_Check(v)) { put_str(o, v); return; }
+  if (v == Py_None) { o.append("null"); return; }
+  if (v == Py_True) { o.append("true"); return; }
+  if (v == Py_False) { o.append("false"); return; }
+  if (PyFloat_Check(v)) {
+    // a float subclass with its own __repr__ would differ; json.dumps uses float.__repr__
+    put_float(o, PyFloat_AS_DOUBLE(v));
+    return;
+  }
+  if (PyLong_Check(v)) {
+    if (!PyLong_CheckExact(v)) throw Unsupported{};   // IntEnum etc.: json's own rules
+    put_int(o, v);
+    return;
+  }
+  if (PyList_Check(v) || PyTuple_Check(v)) {
+    PyObject* seq = v;
+    const bool lst = PyList_Check(v);
+    Py_ssize_t n = lst ? PyList_GET_SIZE(seq) : PyTuple_GET_SIZE(seq);
+    o.push_back('[');
+    for (Py_ssize_t i = 0; i < n; ++i) {
+      if (i) o.append(", ");
+      PyObject* it = lst ? PyList_GET_ITEM(seq, i) : PyTuple_GET_ITEM(seq, i);
+      Py_INCREF(it);
+      try {
+        put(o, it, depth + 1);
+      } catch (...) {
+        Py_DECREF(it);
+        throw;
+      }
+      Py_DECREF(it);
+      if (lst) n = PyList_GET_SIZE(seq);
+    }
+    o.push_back(']');
+    return;
+  }
+  if (PyDict_Check(v)) {
+    if (!PyDict_CheckExact(v)) throw Unsupported{};   // OrderedDict & co: json's own path
+    o.push_back('{');
+    Py_ssize_t pos = 0;
+    PyObject *k, *x;
+    bool first = true;
+    while (PyDict_Next(v, &pos, &k, &x)) {
+      if (!first) o.append(", ");
+      first = false;
+      put_key(o, k);
+      o.append(": ");
+      Py_INCREF(x);
+      try {
+        put(o, x, depth + 1);
+      } catch (...) {
+        Py_DECREF(x);
+        throw;
+      }
+      Py_DECREF(x);
+    }
+    o.push_back('}');
+    return;
+  }
+  throw Unsupported{};
+}
+
+py::object json_dumps(py::handle obj) {
+  std::string o;
+  o.reserve(256);
+  try {
+    put(o, obj.ptr(), 0);
+  } catch (const Unsupported&) {
+    PyErr_SetString(g_unsupported, "json_dumps: type outside the native encoder");
+    throw py::error_already_set();
+  }
+  // output is pure ASCII (ensure_ascii)
+  PyObject* s = PyUnicode_FromStringAndSize(o.data(), (Py_ssize_t)o.size());
+  if (!s) throw py::error_already_set();
+  return py::reinterpret_steal<py::object>(s);
+}
+
+}  // namespace
+
+void bind_jsonenc(py::module_& m) {
+  g_unsupported = PyErr_NewException("_lsnative.JsonUnsupported", PyExc_TypeError, nullptr);
+  m.attr("JsonUnsupported") = py::handle(g_unsupported);
+  m.def("json_dumps", &json_dumps, py::arg("obj"),
+        "json.dumps(obj) with default options; raises JsonUnsupported for other types");
+}

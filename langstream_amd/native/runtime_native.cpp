@@ -15,6 +15,7 @@ void bind_memlog(py::module_& m);
 void bind_shmlog(py::module_& m);
 void bind_tokenizer(py::module_& m);
 void bind_codec(py::module_& m);
+void bind_jsonenc(py::module_& m);
 
 namespace {
 
@@ -60,7 +61,7 @@ class BlockAllocator {
 }  // namespace
 
 PYBIND11_MODULE(_lsnative, m) {
-  m.doc() = "langstream_amd native host runtime (memlog, shared-memory log, tokenizers, KV block allocator, Kafka checksums)";
+  m.doc() = "langstream_amd native host runtime (memlog, shared-memory log, tokenizers, KV block allocator, Kafka checksums, JSON encoder)";
   py::class_<BlockAllocator>(m, "BlockAllocator")
       .def(py::init<int>())
       .def("num_free", &BlockAllocator::num_free)
@@ -74,4 +75,5 @@ PYBIND11_MODULE(_lsnative, m) {
   bind_shmlog(m);
   bind_tokenizer(m);
   bind_codec(m);
+  bind_jsonenc(m);
 }

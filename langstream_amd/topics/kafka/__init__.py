@@ -25,7 +25,6 @@ Parity:
 """
 from __future__ import annotations
 
-import json
 import logging
 import threading
 import time
@@ -37,6 +36,7 @@ from ...api.topics import (TopicAdmin, TopicConnectionsRuntime, TopicConnections
                            TopicOffsetPosition, TopicProducer, TopicReader, TopicReadResult, decode_offsets,
                            encode_offsets)
 from . import codecs
+from ...utils import fastjson
 from .client import GroupConsumer, KafkaClient, PartitionReader, Producer
 from .security import SecurityConfig
 
@@ -53,7 +53,7 @@ def serialize(v: Any) -> Optional[bytes]:
     if isinstance(v, bool):
         return b"true" if v else b"false"
     if isinstance(v, (dict, list)):
-        return json.dumps(v).encode()
+        return fastjson.dumps(v).encode()
     return str(v).encode()
 
 

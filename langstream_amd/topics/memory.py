@@ -15,7 +15,6 @@ One log instance per ``configuration.name`` (default ``default``) per process.
 from __future__ import annotations
 
 import itertools
-import json
 import atexit
 import logging
 import threading
@@ -30,6 +29,7 @@ from ..api.topics import (TopicAdmin, TopicConnectionsRuntime, TopicConnectionsR
                           TopicOffsetPosition, TopicProducer, TopicReader, TopicReadResult, decode_offsets,
                           encode_offsets)
 from ..native import lib
+from ..utils import fastjson
 
 log = logging.getLogger(__name__)
 
@@ -71,7 +71,7 @@ def _key_hash(key: Any) -> int:
 
 def serialize_value(v: Any) -> Any:
     if isinstance(v, (dict, list)):
-        return json.dumps(v)
+        return fastjson.dumps(v)
     return v
 
 
