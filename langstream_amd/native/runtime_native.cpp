@@ -16,6 +16,7 @@ void bind_shmlog(py::module_& m);
 void bind_tokenizer(py::module_& m);
 void bind_codec(py::module_& m);
 void bind_jsonenc(py::module_& m);
+void bind_kafka_records(py::module_& m);
 
 namespace {
 
@@ -76,4 +77,5 @@ PYBIND11_MODULE(_lsnative, m) {
   bind_tokenizer(m);
   bind_codec(m);
   bind_jsonenc(m);
+  bind_kafka_records(m);
 }

@@ -316,6 +316,9 @@ _NATIVE = _native()
 # every produce and fetch: native (SSE4.2 crc32) when the host runtime is built
 crc32c = _NATIVE.crc32c if _NATIVE is not None else _crc32c_py
 murmur2 = _NATIVE.murmur2 if _NATIVE is not None else _murmur2_py
+# records sections of every produced / fetched batch (native/kafka_records.cpp)
+_ENC = getattr(_NATIVE, "kafka_encode_records", None)
+_DEC = getattr(_NATIVE, "kafka_decode_records", None)
 
 
 def partition_for_key(key: bytes, num_partitions: int) -> int:
@@ -329,6 +332,22 @@ def encode_batch(base_offset: int, records: List[Tuple[Optional[bytes], Optional
     (topics/kafka/codecs.py) applied to the records section."""
     first_ts = records[0][3] if records else 0
     max_ts = max((r[3] for r in records), default=0)
+    if _ENC is not None:
+        body = _ENC(records, first_ts)
+    else:
+        body = _encode_records_py(records, first_ts)
+    if codec:
+        from . import codecs
+        body = codecs.compress(codec, bytes(body))
+    tail = struct.pack(">hiqqqhii", codec & 0x07, len(records) - 1, first_ts, max_ts, -1, -1, -1,
+                       len(records)) + bytes(body)
+    crc = crc32c(tail)
+    head = struct.pack(">ib", -1, 2) + struct.pack(">I", crc)  # partitionLeaderEpoch, magic, crc
+    batch_len = len(head) + len(tail)
+    return struct.pack(">qi", base_offset, batch_len) + head + tail
+
+
+def _encode_records_py(records, first_ts: int) -> bytearray:
     body = bytearray()
     for i, (k, v, hs, ts) in enumerate(records):
         rec = bytearray(b"\x00")
@@ -348,15 +367,7 @@ def encode_batch(base_offset: int, records: List[Tuple[Optional[bytes], Optional
             else:
                 rec += zigzag_varint(len(hv)) + hv
         body += zigzag_varint(len(rec)) + rec
-    if codec:
-        from . import codecs
-        body = codecs.compress(codec, bytes(body))
-    tail = struct.pack(">hiqqqhii", codec & 0x07, len(records) - 1, first_ts, max_ts, -1, -1, -1,
-                       len(records)) + bytes(body)
-    crc = crc32c(tail)
-    head = struct.pack(">ib", -1, 2) + struct.pack(">I", crc)  # partitionLeaderEpoch, magic, crc
-    batch_len = len(head) + len(tail)
-    return struct.pack(">qi", base_offset, batch_len) + head + tail
+    return body
 
 
 def decode_batches(data: Optional[bytes], verify_crc: bool = False):
@@ -390,6 +401,12 @@ def decode_batches(data: Optional[bytes], verify_crc: bool = False):
 
 def _records(data, p: int, count: int, base: int, first_ts: int):
     """Records of one (decompressed) batch starting at byte ``p``."""
+    if _DEC is not None:
+        return _DEC(data, p, count, base, first_ts)
+    return _records_py(data, p, count, base, first_ts)
+
+
+def _records_py(data, p: int, count: int, base: int, first_ts: int):
     for _ in range(count):
         _ln, p = read_varint(data, p)
         p += 1  # attributes

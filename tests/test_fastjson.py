@@ -40,3 +40,22 @@ def test_unsupported_falls_back_to_json_errors():
     cyc.append(cyc)
     with pytest.raises(ValueError):
         fastjson.dumps(cyc)
+
+
+def test_kafka_native_records_match_python():
+    from langstream_amd.topics.kafka import protocol as P
+    if P._ENC is None:
+        pytest.skip("native runtime not built")
+    rnd = random.Random(3)
+    recs = []
+    for i in range(300):
+        k = None if i % 7 == 0 else bytes(rnd.getrandbits(8) for _ in range(rnd.randint(0, 40)))
+        v = None if i % 11 == 0 else bytes(rnd.getrandbits(8) for _ in range(rnd.randint(0, 3000)))
+        hs = [("h%d" % j, None if j == 1 else b"x" * j) for j in range(i % 4)]
+        hs += [("ünï", b"\x00\xff")] if i % 5 == 0 else []
+        recs.append((k, v, hs, 1700000000000 + rnd.randint(-5000, 5000)))
+    assert P._ENC(recs, recs[0][3]) == bytes(P._encode_records_py(recs, recs[0][3]))
+    batch = P.encode_batch(100, recs)
+    native = list(P.decode_batches(batch, verify_crc=True))
+    assert native == list(P._records_py(batch, 61, len(recs), 100, recs[0][3]))
+    assert [(x[2], x[3], x[4]) for x in native] == [(r[0], r[1], [tuple(h) for h in r[2]]) for r in recs]
