@@ -22,6 +22,7 @@ from __future__ import annotations
 
 import gc
 import os
+import sys
 
 _done = False
 
@@ -33,5 +34,10 @@ def tune() -> bool:
     gc.collect()
     gc.freeze()
     gc.set_threshold(int(os.environ.get("LANGSTREAM_GC_GEN0", "50000")), 20, 100)
+    sw = os.environ.get("LANGSTREAM_SWITCH_MS")
+    if sw:
+        # GIL hand-off interval: a thread coming back from a GIL-released native call
+        # (a GPU step, a socket read) waits up to this long for a Python-busy thread
+        sys.setswitchinterval(float(sw) / 1000.0)
     _done = True
     return True
