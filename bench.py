@@ -482,6 +482,8 @@ def main():
     only = None if rank == 0 else ["query", "ingest"]   # the crawler runs once (rank 0)
     if os.environ.get("LS_STAGE_TRACE", "0") != "0":
         _composite.STAGE_TRACE = []
+        from langstream_amd.engine import vector_store as _vs
+        _vs.SEARCH_TRACE = []
     runner = LocalApplicationRunner.from_yaml(files, instance=INSTANCE.format(**fmt), application_id="rag-bench",
                                               services=services, agents=only)
     runner.start()
@@ -568,6 +570,13 @@ def main():
             stage_trace.append({n: [round(sorted(v)[min(len(v) - 1, int(q * len(v)))], 3) for q in (0.1, 0.5, 1.0)]
                                 for n, v in by.items()})
             _composite.STAGE_TRACE.clear()
+            from langstream_amd.engine import vector_store as _vs
+            if _vs.SEARCH_TRACE is not None:
+                # searches of this step: [start, lock wait, lock->host top-k, results build, n] (s, ms, ms, ms)
+                stage_trace[-1]["searches"] = [[round(a - t0, 3), round(1e3 * (b - a), 1), round(1e3 * (c - b), 1),
+                                                round(1e3 * (d - c), 1), n] for a, b, c, d, n in list(_vs.SEARCH_TRACE)
+                                               if a >= t0]
+                _vs.SEARCH_TRACE.clear()
         return t_end - t0, lats
 
     def run_window(k_steps):

@@ -42,8 +42,51 @@ class DataSource:
         pass
 
 
+_SENT = "\u0000ls-param-"
+_TEMPLATES: Dict[str, Any] = {}
+
+
 def _bind_json(query: str, params: List[Any]) -> Any:
-    """Replace bare ``?`` placeholders (outside strings) with JSON-encoded params."""
+    """Replace bare ``?`` placeholders (outside strings) with the params.  The query is
+    parsed once per distinct text with sentinel strings in the placeholders' places and
+    bound by substitution: JSON-encoding a 384-float query vector into the text and
+    parsing it back cost ~0.4 ms per record."""
+    tpl = _TEMPLATES.get(query)
+    if tpl is None:
+        n = [0]
+
+        def sent(_):
+            n[0] += 1
+            return json.dumps(f"{_SENT}{n[0] - 1}")
+        try:
+            tpl = (json.loads(_bind_text(query, None, sent)), n[0])
+        except ValueError:
+            tpl = (None, 0)
+        if len(_TEMPLATES) < 256:
+            _TEMPLATES[query] = tpl
+    obj, nph = tpl
+    if obj is None:
+        return json.loads(_bind_text(query, params, None))
+    if nph > len(params):
+        raise ValueError("not enough parameters for query")
+    return _subst(obj, params)
+
+
+def _subst(o: Any, params: List[Any]) -> Any:
+    if isinstance(o, str):
+        if o.startswith(_SENT):
+            v = params[int(o[len(_SENT):])]
+            # JSON types as the text binding produced them (tuples -> lists, keys -> str)
+            return v if isinstance(v, (str, int, float, bool, type(None), list)) else json.loads(json.dumps(v))
+        return o
+    if isinstance(o, dict):
+        return {k: _subst(v, params) for k, v in o.items()}
+    if isinstance(o, list):
+        return [_subst(v, params) for v in o]
+    return o
+
+
+def _bind_text(query: str, params: Optional[List[Any]], sent) -> str:
     out, i, pi, in_str = [], 0, 0, None
     while i < len(query):
         c = query[i]
@@ -58,14 +101,17 @@ def _bind_json(query: str, params: List[Any]) -> Any:
             in_str = c
             out.append(c)
         elif c == "?":
-            if pi >= len(params):
-                raise ValueError("not enough parameters for query")
-            out.append(json.dumps(params[pi]))
+            if sent is not None:
+                out.append(sent(pi))
+            else:
+                if pi >= len(params):
+                    raise ValueError("not enough parameters for query")
+                out.append(json.dumps(params[pi]))
             pi += 1
         else:
             out.append(c)
         i += 1
-    return json.loads("".join(out))
+    return "".join(out)
 
 
 class LocalVectorDataSource(DataSource):

@@ -31,6 +31,7 @@ import logging
 import os
 import re
 import threading
+import time
 from typing import Any, Dict, List, Optional, Sequence, Tuple
 
 import msgpack
@@ -190,6 +191,11 @@ class _Persistence:
         if self._wal is not None:
             self._wal.close()
             self._wal = None
+
+
+# Optional search tracer (benchmarks): when a list, every search appends (enter, lock
+# taken, top-k on the host, results built, number of queries) as time.time() stamps.
+SEARCH_TRACE: Optional[list] = None
 
 
 class VectorStore:
@@ -400,11 +406,18 @@ class VectorStore:
         {"id", "similarity", **metadata} sorted by decreasing cosine similarity."""
         if k < 1:
             raise ValueError("top-k must be >= 1")
+        tr = SEARCH_TRACE
+        t_in = time.time() if tr is not None else 0.0
         with on_search(self.device), self.lock:
+            t_lk = time.time() if tr is not None else 0.0
             q = self._normalize(queries)
             s, idx = self.topk_rows(q, k)
             s, idx = (t.tolist() for t in to_host(s, idx))
-            return self.rows_to_results(s, idx, with_vectors)
+            t_gpu = time.time() if tr is not None else 0.0
+            out = self.rows_to_results(s, idx, with_vectors)
+            if tr is not None:
+                tr.append((t_in, t_lk, t_gpu, time.time(), len(out)))
+            return out
 
     def rows_to_results(self, scores, rows, with_vectors: bool) -> List[List[Dict[str, Any]]]:
         """Host results for row indices (caller holds ``lock``)."""
