@@ -80,11 +80,7 @@ def mmr(docs: List[Any], texts: List[str], embs: np.ndarray, query: str, max_: i
     qc = Counter(q)
     terms = list(qc)
     qw = np.array([qc[t] for t in terms], dtype=np.float64)
-    tf = np.zeros((n, len(terms)), dtype=np.float64)
-    for i, d in enumerate(toks):
-        c = Counter(d)
-        for j, t in enumerate(terms):
-            tf[i, j] = c.get(t, 0)
+    tf = np.array([[c.get(t, 0) for t in terms] for c in map(Counter, toks)], dtype=np.float64).reshape(n, len(terms))
     dl = np.array([len(d) for d in toks], dtype=np.float64)
     remaining = np.ones(n, dtype=bool)
     selected: List[int] = []
@@ -95,7 +91,7 @@ def mmr(docs: List[Any], texts: List[str], embs: np.ndarray, query: str, max_: i
         avgdl = dl[idx].mean()
         df = (tf[idx] > 0).sum(0)
         idf = np.log((N - df + 0.5) / (df + 0.5) + 1.0)
-        denom = tf[idx] + k1 * (1 - b + b * (dl[idx] / avgdl if avgdl else 1.0))[:, None]
+        denom = tf[idx] + k1 * (1 - b + b * (dl[idx] / avgdl if avgdl else np.ones(N)))[:, None]
         with np.errstate(divide="ignore", invalid="ignore"):
             part = np.where(denom > 0, tf[idx] * (k1 + 1) / denom, 0.0)
         rel = (part * idf[None, :] * qw[None, :]).sum(1)
