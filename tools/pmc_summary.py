@@ -19,7 +19,7 @@ def main():
         name = row["Kernel_Name"]
         if filt and filt not in name:
             continue
-        short = name.split("(")[0][-60:]
+        short = name.replace("(anonymous namespace)::", "").split("(")[0][-60:]
         sums[short][row["Counter_Name"]] += float(row["Counter_Value"])
         disp[short].add(row["Dispatch_Id"])
     for k, c in sums.items():
