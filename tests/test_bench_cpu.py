@@ -54,3 +54,18 @@ def test_bench_config5_shape_tensor_parallel_chat_gateway(tmp_path):
               "--max-tokens", "6"], tmp_path)
     assert d["config"]["parallelism"] == "tp2" and d["answers"] == 2 and d["value"] > 0
     assert d["ttft_p50_ms"] > 0 and d["unit"] == "tokens/s"
+
+
+def test_bench_stage_trace(tmp_path, monkeypatch):
+    """LS_STAGE_TRACE=1: per-step entry times of every processor of the fused question
+    chain and the per-batch kNN search timings come back in the JSON line."""
+    monkeypatch.setenv("LS_STAGE_TRACE", "1")
+    d = _run(["--steps", "1", "--warmup", "1", "--batch", "8", "--max-tokens", "4", "--corpus", "1000",
+              "--docs", "2"], tmp_path)
+    st = d["stage_trace_rank0_s"]
+    assert len(st) == 2
+    for step in st:
+        assert any("query-vector-db" in k for k in step) and "end" in step
+        p10, p50, mx = step["end"]
+        assert 0 <= p10 <= p50 <= mx
+        assert step["searches"] and sum(s[4] for s in step["searches"]) >= 8
