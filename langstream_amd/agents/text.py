@@ -376,11 +376,27 @@ def _pdf_content_text(buf: bytes) -> str:
 
 
 def _pdf_text(data: bytes) -> str:
+    """PDF text through the object-level extractor (agents/pdf.py: page tree, object
+    streams, font encodings and ToUnicode CMaps); a damaged file it cannot parse falls
+    back to the literal strings of every text-drawing stream."""
+    from .pdf import pdf_text
+    try:
+        text = pdf_text(data)
+        if text:
+            return text
+    except DecompressionBombError:
+        raise
+    except Exception:  # noqa: BLE001 - damaged structure: the stream scan below
+        pass
+    return _pdf_text_streams(data)
+
+
+def _pdf_text_streams(data: bytes) -> str:
     out = []
     for m in re.finditer(rb"stream\r?\n(.*?)\r?\nendstream", data, re.S):
         raw = m.group(1)
         try:
-            raw = zlib.decompress(raw)
+            raw = bounded_inflate(raw)
         except zlib.error:
             pass
         if b"BT" not in raw:                            # images, fonts, xref streams
@@ -421,10 +437,80 @@ _EMAIL_HEAD = re.compile(r"^(?:(?:From|To|Subject|Date|Message-ID|MIME-Version|R
                          r":[^\n]*\n)+", re.I)
 
 
-def extract_text(data: Any) -> str:
+# Decompression-bomb guard.  Tika's AutoDetectParser runs under SecureContentHandler,
+# which rejects a document whose output exceeds 100x its input once past 1M characters
+# (the reference's TikaTextExtractorAgent.java:41 inherits it).  Every inflate here --
+# gzip wrappers, zip members (OOXML / ODF / EPUB), PDF FlateDecode streams -- goes
+# through a bounded streaming decompressor with the same shape of limit plus a hard
+# ceiling, and nested gzip wrappers are limited in depth.
+MAX_EXPANSION_RATIO = 100
+MIN_EXPANSION_ALLOWANCE = 1 << 20
+MAX_INFLATED_BYTES = 256 << 20
+MAX_NESTING = 3
+
+
+class DecompressionBombError(ValueError):
+    pass
+
+
+def inflate_limit(compressed_len: int) -> int:
+    return min(MAX_INFLATED_BYTES, max(MIN_EXPANSION_ALLOWANCE, MAX_EXPANSION_RATIO * compressed_len))
+
+
+def bounded_inflate(data: bytes, wbits: int = zlib.MAX_WBITS, limit: Optional[int] = None) -> bytes:
+    """zlib / raw-deflate / gzip (wbits 15 / -15 / 31) decompression that stops with
+    DecompressionBombError once the output passes ``limit`` (default inflate_limit)."""
+    limit = inflate_limit(len(data)) if limit is None else limit
+    d = zlib.decompressobj(wbits)
+    out = bytearray()
+    buf = data
+    while buf:
+        chunk = d.decompress(buf, limit + 1 - len(out))
+        out += chunk
+        if len(out) > limit:
+            raise DecompressionBombError(f"decompressed size exceeds {limit} bytes "
+                                         f"({len(data)} compressed)")
+        buf = d.unconsumed_tail
+        if d.eof:
+            # gzip members may be concatenated: continue with the next one
+            rest = d.unused_data
+            if wbits == 31 and rest[:2] == b"\x1f\x8b":
+                d = zlib.decompressobj(wbits)
+                buf = rest
+                continue
+            break
+        if not chunk and not buf:
+            break
+    out += d.flush()
+    if len(out) > limit:
+        raise DecompressionBombError(f"decompressed size exceeds {limit} bytes")
+    return bytes(out)
+
+
+def _zip_read(z: "zipfile.ZipFile", name: str, budget: List[int]) -> bytes:
+    """One zip member, refused when its declared size or its actual inflated size would
+    exceed the document's remaining budget (shared by all members)."""
+    info = z.getinfo(name)
+    if info.file_size > budget[0]:
+        raise DecompressionBombError(f"zip member {name}: {info.file_size} bytes over the budget")
+    out = bytearray()
+    with z.open(info) as f:
+        while True:
+            chunk = f.read(1 << 16)
+            if not chunk:
+                break
+            out += chunk
+            if len(out) > budget[0]:
+                raise DecompressionBombError(f"zip member {name} inflates past the budget")
+    budget[0] -= len(out)
+    return bytes(out)
+
+
+def extract_text(data: Any, _depth: int = 0) -> str:
     """Text of a document (the reference runs Tika's AutoDetectParser,
     TikaTextExtractorAgent.java:36-58): PDF, OOXML (docx / pptx / xlsx), ODF, EPUB, RTF,
-    HTML / XHTML / XML, MIME e-mail, gzip-wrapped content and UTF-8/16 text (BOMs)."""
+    HTML / XHTML / XML, MIME e-mail, gzip-wrapped content and UTF-8/16 text (BOMs).
+    Compressed content is inflated under the bomb guard above (DecompressionBombError)."""
     if isinstance(data, str):
         s = data.lstrip("\ufeff").lstrip()
         if s[:1] == "<" and re.search(r"<(html|body|p|div)\b", s[:2000], re.I):
@@ -442,24 +528,28 @@ def extract_text(data: Any) -> str:
     if b[:4] == b"%PDF":
         return _pdf_text(b)
     if b[:2] == b"\x1f\x8b":
-        import gzip
+        if _depth >= MAX_NESTING:
+            raise DecompressionBombError(f"gzip nested deeper than {MAX_NESTING} levels")
         try:
-            return extract_text(gzip.decompress(b))
-        except OSError:
-            pass
+            inner = bounded_inflate(b, 31)
+        except zlib.error:
+            inner = None
+        if inner is not None:
+            return extract_text(inner, _depth + 1)
     if b[:2] in (b"\xff\xfe", b"\xfe\xff"):
-        return extract_text(b.decode("utf-16"))
+        return extract_text(b.decode("utf-16"), _depth)
     if b[:2] == b"PK":
         try:
             with zipfile.ZipFile(io.BytesIO(b)) as z:
                 names = z.namelist()
+                budget = [inflate_limit(len(b))]
                 if "META-INF/container.xml" in names and any(n.endswith((".xhtml", ".html", ".htm")) for n in names):
                     # EPUB: the content documents in spine order (the OPF manifest / spine)
-                    return _epub_text(z, names)
+                    return _epub_text(z, names, budget)
                 parts = [n for n in names if n in ("word/document.xml", "content.xml")]
                 parts += sorted(n for n in names if re.match(r"ppt/slides/slide\d+\.xml", n))
                 parts += [n for n in names if n == "xl/sharedStrings.xml"]
-                return "\n".join(_xml_text(z.read(n)) for n in parts).strip()
+                return "\n".join(_xml_text(_zip_read(z, n, budget)) for n in parts).strip()
         except zipfile.BadZipFile:
             pass
     if b[:5] == b"{\\rtf":
@@ -467,27 +557,30 @@ def extract_text(data: Any) -> str:
         s = re.sub(r"\\[a-z]+-?\d* ?|[{}]", "", s)
         return s.strip()
     s = b.decode("utf-8", errors="replace")
-    return extract_text(s)
+    return extract_text(s, _depth)
 
 
-def _epub_text(z: "zipfile.ZipFile", names) -> str:
+def _epub_text(z: "zipfile.ZipFile", names, budget: List[int]) -> str:
     import posixpath
     order = []
     try:
-        cont = z.read("META-INF/container.xml").decode("utf-8", "replace")
+        cont = _zip_read(z, "META-INF/container.xml", budget).decode("utf-8", "replace")
         opf = re.search(r'full-path="([^"]+)"', cont).group(1)
-        o = z.read(opf).decode("utf-8", "replace")
+        o = _zip_read(z, opf, budget).decode("utf-8", "replace")
         base = posixpath.dirname(opf)
         items = dict(re.findall(r'<item\b[^>]*?id="([^"]+)"[^>]*?href="([^"]+)"', o))
         items.update({i: h for h, i in re.findall(r'<item\b[^>]*?href="([^"]+)"[^>]*?id="([^"]+)"', o)})
         for idref in re.findall(r'<itemref\b[^>]*?idref="([^"]+)"', o):
             if idref in items:
                 order.append(posixpath.normpath(posixpath.join(base, items[idref])))
+    except DecompressionBombError:
+        raise
     except Exception:  # noqa: BLE001 - no usable OPF: document order
         order = []
     if not order:
         order = sorted(n for n in names if n.endswith((".xhtml", ".html", ".htm")))
-    return "\n".join(html_to_text(z.read(n).decode("utf-8", "replace")).strip() for n in order if n in names).strip()
+    return "\n".join(html_to_text(_zip_read(z, n, budget).decode("utf-8", "replace")).strip()
+                     for n in order if n in names).strip()
 
 
 @register_agent("text-extractor")

@@ -1,0 +1,238 @@
+"""PDF extraction parity beyond the reference's simple.pdf fixture (TextExtractorTest.java:55;
+the reference extracts through Tika / PDFBox, TikaTextExtractorAgent.java:41).
+
+The fixtures are built here, byte by byte, in the shapes the two common producers write:
+* Word ("Save as PDF"): PDF 1.7, every dictionary packed in an object stream, an XRef
+  stream instead of a classic table, subset TrueType fonts as Type0 / Identity-H composite
+  fonts whose two-byte glyph ids mean nothing without the /ToUnicode CMap;
+* pdfTeX: Type1 subset fonts (ABCDEF+CMR10) with an /Encoding /Differences array that
+  puts ligatures and accented glyphs at arbitrary codes (\\002 = fi, \\016 = ffi), no
+  ToUnicode, kerned TJ arrays.
+Plus the page tree order, Form XObjects, the ASCII85 / LZW / hex filters and the
+decompression-bomb guard (gzip without a size limit)."""
+import gzip
+import zlib
+
+import pytest
+
+from langstream_amd.agents.pdf import glyph_to_unicode, pdf_text
+from langstream_amd.agents.text import DecompressionBombError, bounded_inflate, extract_text
+
+
+def _stream(d: str, data: bytes, flate: bool = True) -> bytes:
+    if flate:
+        data = zlib.compress(data)
+        d = d + " /Filter /FlateDecode"
+    return b"<< " + d.encode() + b" /Length %d >>\nstream\n" % len(data) + data + b"\nendstream"
+
+
+def build_pdf(objs, root: int, objstm=(), version=b"1.7") -> bytes:
+    """objs: {num: bytes (object body)}; numbers in ``objstm`` (non-stream objects) are
+    packed into one /Type /ObjStm, the rest written as top-level objects (in reverse
+    numeric order, so file order never matches page order)."""
+    out = bytearray(b"%PDF-" + version + b"\n%\xe2\xe3\xcf\xd3\n")
+    packed = [n for n in sorted(objs) if n in objstm]
+    nxt = max(objs) + 1
+    if packed:
+        head, body = [], bytearray()
+        for n in packed:
+            head.append(b"%d %d" % (n, len(body)))
+            body += objs[n] + b"\n"
+        hb = b" ".join(head) + b"\n"
+        objs = {n: v for n, v in objs.items() if n not in objstm}
+        objs[nxt] = _stream("/Type /ObjStm /N %d /First %d" % (len(packed), len(hb)), hb + bytes(body))
+        nxt += 1
+    for n in sorted(objs, reverse=True):
+        out += b"%d 0 obj\n" % n + objs[n] + b"\nendobj\n"
+    if packed:
+        out += b"%d 0 obj\n" % nxt + _stream("/Type /XRef /Root %d 0 R /Size %d /W [1 4 2]" % (root, nxt + 1),
+                                             b"\x00" * 7) + b"\nendobj\n"
+        out += b"startxref\n0\n%%EOF\n"
+    else:
+        out += b"trailer\n<< /Root %d 0 R >>\nstartxref\n0\n%%%%EOF\n" % root
+    return bytes(out)
+
+
+def _to_unicode_cmap(char_to_gid):
+    chars = sorted(char_to_gid.items(), key=lambda kv: kv[1])
+    bfchar = b"\n".join(b"<%04X> <%04X>" % (g, ord(c)) for c, g in chars if not c.isdigit())
+    return (b"/CIDInit /ProcSet findresource begin 12 dict begin begincmap\n"
+            b"/CIDSystemInfo << /Registry (Adobe) /Ordering (UCS) /Supplement 0 >> def\n"
+            b"/CMapName /Adobe-Identity-UCS def /CMapType 2 def\n"
+            b"1 begincodespacerange\n<0000> <FFFF>\nendcodespacerange\n"
+            b"%d beginbfchar\n" % sum(1 for c, _ in chars if not c.isdigit()) + bfchar + b"\nendbfchar\n"
+            b"1 beginbfrange\n<0010> <0019> <0030>\nendbfrange\n"
+            b"endcmap\nCMapName currentdict /CMap defineresource pop\nend\nend\n")
+
+
+def word_like_pdf():
+    lines = ["Quarterly “results” – up 5%", "Ünïcödé naïve café, 2024"]
+    gids = {}
+    for ch in "".join(lines):
+        if ch.isdigit():
+            gids[ch] = 0x10 + int(ch)                   # the bfrange: <0010>..<0019> -> '0'..'9'
+        elif ch not in gids:
+            gids[ch] = 0x24 + len([c for c in gids if not c.isdigit()]) * 3   # sparse subset gids
+    content = b""
+    for i, ln in enumerate(lines):
+        hexs = b"".join(b"%04X" % gids[c] for c in ln)
+        # Word: one Tm per line, TJ arrays with small kerning, hex glyph-id strings
+        content += b"BT\n/F1 11.04 Tf\n1 0 0 1 72.024 %.3f Tm\n[<%s> 3]TJ\nET\n" % (720 - 14 * i, hexs)
+    objs = {
+        1: b"<< /Type /Catalog /Pages 2 0 R /Lang (en-US) >>",
+        2: b"<< /Type /Pages /Count 1 /Kids [3 0 R] >>",
+        3: b"<< /Type /Page /Parent 2 0 R /Resources << /Font << /F1 5 0 R >> >> /MediaBox [0 0 612 792] "
+           b"/Contents 4 0 R >>",
+        4: _stream("", content),
+        5: b"<< /Type /Font /Subtype /Type0 /BaseFont /BCDEEE+Calibri /Encoding /Identity-H "
+           b"/DescendantFonts [6 0 R] /ToUnicode 7 0 R >>",
+        6: b"<< /Type /Font /Subtype /CIDFontType2 /BaseFont /BCDEEE+Calibri "
+           b"/CIDSystemInfo << /Registry (Adobe) /Ordering (Identity) /Supplement 0 >> /DW 1000 >>",
+        7: _stream("", _to_unicode_cmap(gids)),
+    }
+    return build_pdf(objs, 1, objstm=(1, 2, 3, 5, 6)), "\n".join(lines)
+
+
+def latex_like_pdf():
+    # pdfTeX: CMR10 subset, Differences put fi at \002, ffi at \016, quoteright at \047,
+    # eacute at \351; kerning inside TJ; Td line moves
+    page1 = (b"BT\n/F8 9.9626 Tf 91.925 759.927 Td [(The)-333(\\002rst)-334(o)-27(\\016ce)-333(is)-334"
+             b"(Alice\\047s.)]TJ 0 -11.955 Td [(Caf\\351)-333(menu)]TJ\nET\n")
+    page2 = b"BT\n/F8 9.9626 Tf 91.925 759.927 Td [(P)28(age)-333(t)28(w)28(o)]TJ\nET\n"
+    form = b"BT /F8 9.9626 Tf 100 100 Td (Footnote) Tj ET"
+    objs = {
+        1: b"<< /Type /Catalog /Pages 2 0 R >>",
+        2: b"<< /Type /Pages /Count 2 /Kids [3 0 R 10 0 R] /Resources << /Font << /F8 5 0 R >> "
+           b"/XObject << /Fm1 9 0 R >> >> >>",
+        3: b"<< /Type /Page /Parent 2 0 R /Contents [4 0 R 8 0 R] >>",
+        4: _stream("", page1[:40]),                      # a content array split mid-token range
+        8: _stream("", page1[40:] + b"q /Fm1 Do Q\n"),
+        5: b"<< /Type /Font /Subtype /Type1 /BaseFont /ZKLQQW+CMR10 /FirstChar 2 /LastChar 233 "
+           b"/Encoding 6 0 R /FontDescriptor 7 0 R >>",
+        6: b"<< /Type /Encoding /Differences [ 2 /fi 14 /ffi 39 /quoteright 233 /eacute ] >>",
+        7: b"<< /Type /FontDescriptor /FontName /ZKLQQW+CMR10 /Flags 4 >>",
+        9: _stream("/Type /XObject /Subtype /Form /BBox [0 0 200 200]", form),
+        10: b"<< /Type /Page /Parent 2 0 R /Contents 11 0 R >>",
+        11: _stream("", page2),
+    }
+    return build_pdf(objs, 1, objstm=(1, 2, 3, 5, 6, 7, 10), version=b"1.5")
+
+
+def test_word_like_type0_identity_h_with_tounicode():
+    pdf, expected = word_like_pdf()
+    assert b"Quarterly" not in pdf                      # nothing readable without decoding
+    assert extract_text(pdf) == expected
+
+
+def test_latex_like_type1_differences_and_page_order():
+    t = extract_text(latex_like_pdf())
+    assert t == "The first office is Alice’s.\nCafé menu\nFootnote\nPage two", t
+
+
+def test_simple_fonts_named_encodings():
+    content = b"BT /F1 12 Tf 72 700 Td (\\223Smart\\224 quotes \\226 and \\200uro) Tj ET"
+    content2 = b"BT /F2 12 Tf 72 680 Td (Mac \\216t\\216) Tj ET"
+    objs = {
+        1: b"<< /Type /Catalog /Pages 2 0 R >>",
+        2: b"<< /Type /Pages /Count 1 /Kids [3 0 R] >>",
+        3: b"<< /Type /Page /Parent 2 0 R /Contents [4 0 R 7 0 R] /Resources << /Font << /F1 5 0 R /F2 6 0 R >> >> >>",
+        4: _stream("", content),
+        5: b"<< /Type /Font /Subtype /TrueType /BaseFont /Arial /Encoding /WinAnsiEncoding >>",
+        6: b"<< /Type /Font /Subtype /Type1 /BaseFont /Times-Roman /Encoding /MacRomanEncoding >>",
+        7: _stream("", content2),
+    }
+    assert extract_text(build_pdf(objs, 1)) == "“Smart” quotes – and €uro\nMac été"
+
+
+def test_filters_ascii85_lzw_hex():
+    content = b"BT /F1 12 Tf 72 700 Td (Filtered text) Tj ET"
+    import base64
+    a85 = base64.a85encode(content, adobe=True)
+
+    def lzw_encode(data: bytes) -> bytes:
+        table = {bytes([i]): i for i in range(256)}
+        codes, w, nxt = [256], b"", 258
+        width, bits, out = 9, [], bytearray()
+        for c in data:
+            wc = w + bytes([c])
+            if wc in table:
+                w = wc
+            else:
+                codes.append(table[w])
+                table[wc] = nxt
+                nxt += 1
+                w = bytes([c])
+        codes.append(table[w])
+        codes.append(257)
+        # widths follow the decoder's EarlyChange=1 schedule
+        size = 258
+        acc, nb = 0, 0
+        for i, code in enumerate(codes):
+            acc = (acc << width) | code
+            nb += width
+            while nb >= 8:
+                nb -= 8
+                out.append((acc >> nb) & 0xFF)
+            if i > 0 and code not in (256, 257):
+                size += 1
+                if size + 1 >= (1 << width) and width < 12:
+                    width += 1
+        if nb:
+            out.append((acc << (8 - nb)) & 0xFF)
+        _ = bits
+        return bytes(out)
+
+    for filt, data in (("/ASCII85Decode", a85), ("/ASCIIHexDecode", content.hex().encode() + b">"),
+                       ("/LZWDecode", lzw_encode(content)),
+                       ("[/ASCIIHexDecode /FlateDecode]", zlib.compress(content).hex().encode() + b">")):
+        objs = {1: b"<< /Type /Catalog /Pages 2 0 R >>", 2: b"<< /Type /Pages /Count 1 /Kids [3 0 R] >>",
+                3: b"<< /Type /Page /Parent 2 0 R /Contents 4 0 R >>",
+                4: b"<< /Filter " + filt.encode() + b" /Length %d >>\nstream\n" % len(data) + data + b"\nendstream"}
+        assert pdf_text(build_pdf(objs, 1)) == "Filtered text", filt
+
+
+def test_glyph_names():
+    assert glyph_to_unicode("uni00E9") == "é"
+    assert glyph_to_unicode("u1F600") == "\U0001F600"
+    assert glyph_to_unicode("f_f_i") == "ffi"
+    assert glyph_to_unicode("a.sc") == "a"
+    assert glyph_to_unicode("Zcaron") == "Ž"
+    assert glyph_to_unicode("odieresis") == "ö"
+    assert glyph_to_unicode("g123") == ""
+
+
+def test_gzip_bomb_is_rejected():
+    bomb = gzip.compress(b"\0" * (64 << 20))            # 64 MB of zeros in ~64 KB
+    assert len(bomb) < (1 << 17)
+    with pytest.raises(DecompressionBombError):
+        extract_text(bomb)
+    # nested wrappers are limited in depth too
+    nested = b"hello"
+    for _ in range(5):
+        nested = gzip.compress(nested)
+    with pytest.raises(DecompressionBombError):
+        extract_text(nested)
+    assert extract_text(gzip.compress(gzip.compress(b"two levels"))) == "two levels"
+
+
+def test_zip_and_pdf_bombs_are_rejected():
+    import io
+    import zipfile
+    buf = io.BytesIO()
+    with zipfile.ZipFile(buf, "w", zipfile.ZIP_DEFLATED) as z:
+        z.writestr("word/document.xml", b"<w:t>" + b" " * (200 << 20) + b"</w:t>")
+    with pytest.raises(DecompressionBombError):
+        extract_text(buf.getvalue())
+    huge = zlib.compress(b"BT (x) Tj ET " + b" " * (300 << 20))
+    pdf = b"%%PDF-1.4\n1 0 obj << /Length %d /Filter /FlateDecode >>\nstream\n" % len(huge) + huge + \
+        b"\nendstream\nendobj\n%%EOF"
+    with pytest.raises(DecompressionBombError):
+        extract_text(pdf)
+
+
+def test_bounded_inflate_roundtrip_and_limit():
+    data = b"abc" * 1000
+    assert bounded_inflate(zlib.compress(data)) == data
+    assert bounded_inflate(gzip.compress(data) + gzip.compress(b"tail"), 31) == data + b"tail"
+    with pytest.raises(DecompressionBombError):
+        bounded_inflate(zlib.compress(data), limit=100)

@@ -9,10 +9,12 @@ import argparse
 import collections
 import sqlite3
 
-CATS = [("prefill_gemm", lambda n, g: "Cijk" in n and "MT256x256" in n),
-        ("hipblaslt_other", lambda n, g: "Cijk" in n),
-        ("gemm_prefill(hand)", lambda n, g: "gemm_prefill" in n),
-        ("skinny/gemv/dgemm", lambda n, g: "skinny" in n or "gemv" in n or "splitk" in n or "dgemm" in n),
+# Library kernels (hipBLASLt / Tensile "Cijk_*") and hand-written kernels are kept in
+# separate categories so a summary can never credit one for the other.
+CATS = [("hipblaslt_MT256x256", lambda n, g: "Cijk" in n and "MT256x256" in n),
+        ("hipblaslt_other", lambda n, g: "Cijk" in n or "hipblaslt" in n.lower()),
+        ("gemm_pp(hand,prefill)", lambda n, g: "gemm_pp" in n or "gemm_prefill" in n),
+        ("dgemm/skinny(hand,decode)", lambda n, g: "skinny" in n or "gemv" in n or "splitk" in n or "dgemm" in n),
         ("encoder_gemm", lambda n, g: "gemm_fused" in n),
         ("decode_attn", lambda n, g: "decode_attn" in n),
         ("prefill_attn", lambda n, g: "prefill_attn" in n),
