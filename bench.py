@@ -467,6 +467,10 @@ def main():
     if not args.no_persist:
         import tempfile
         persist_dir = tempfile.mkdtemp(prefix=f"rag-bench-store-r{rank}-")
+        import atexit
+        import shutil
+        # removed on every exit path (a failed or interrupted run too), not only at the end
+        atexit.register(shutil.rmtree, persist_dir, True)
         VectorStoreRegistry.configure(persist_dir=persist_dir)   # every upsert WAL-logged before its ack
     emb = services.embedding_engine(embed_model, {"embeddings-model": embed_model})
     docs = [" ".join(corpus[(i * 7 + j) % len(corpus)] for j in range(4)) for i in range(args.corpus)]

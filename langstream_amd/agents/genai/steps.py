@@ -19,6 +19,7 @@ from concurrent.futures import Future
 from typing import Any, Callable, Dict, List, Optional
 
 from ...api.util import OrderedAsyncBatchExecutor
+from ...api.types import Float32, Int8, Int16, Int32
 from .el import eval_expression, eval_predicate
 from .mustache import compile_template
 from .mutable import MutableRecord
@@ -94,8 +95,9 @@ _CASTS: Dict[str, Callable[[Any], Any]] = {
     "string": lambda v: v if isinstance(v, str) else (json.dumps(v) if isinstance(v, (dict, list)) else (
         "true" if v is True else "false" if v is False else str(v))),
     "boolean": lambda v: v if isinstance(v, bool) else str(v).strip().lower() == "true",
-    "int8": lambda v: int(float(v)), "int16": lambda v: int(float(v)), "int32": lambda v: int(float(v)),
-    "int64": lambda v: int(float(v)), "float": lambda v: float(v), "double": lambda v: float(v),
+    "int8": lambda v: Int8(int(float(v))), "int16": lambda v: Int16(int(float(v))),
+    "int32": lambda v: Int32(int(float(v))),
+    "int64": lambda v: int(float(v)), "float": lambda v: Float32(float(v)), "double": lambda v: float(v),
     "bytes": lambda v: v if isinstance(v, bytes) else str(v).encode(),
 }
 
@@ -141,9 +143,11 @@ class DropStep(Step):
 
 _COMPUTE_TYPES = {
     "STRING": lambda v: None if v is None else _CASTS["string"](v),
-    "INT8": lambda v: None if v is None else int(v), "INT16": lambda v: None if v is None else int(v),
-    "INT32": lambda v: None if v is None else int(v), "INT64": lambda v: None if v is None else int(v),
-    "FLOAT": lambda v: None if v is None else float(v), "DOUBLE": lambda v: None if v is None else float(v),
+    # width-tagged (api/types.py): a topic receives them as 1 / 2 / 4 / 8-byte and 4 / 8-byte
+    # Java-serialised numbers, like the reference's Byte / Short / Integer / Long / Float / Double
+    "INT8": lambda v: None if v is None else Int8(int(v)), "INT16": lambda v: None if v is None else Int16(int(v)),
+    "INT32": lambda v: None if v is None else Int32(int(v)), "INT64": lambda v: None if v is None else int(v),
+    "FLOAT": lambda v: None if v is None else Float32(float(v)), "DOUBLE": lambda v: None if v is None else float(v),
     "BOOLEAN": lambda v: None if v is None else _CASTS["boolean"](v),
     "BYTES": lambda v: None if v is None else _CASTS["bytes"](v),
     "DATE": lambda v: None if v is None else _to_date(v), "TIME": lambda v: v,

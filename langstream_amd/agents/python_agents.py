@@ -27,6 +27,34 @@ from ..runtime.registry import register_agent
 log = logging.getLogger(__name__)
 
 
+def _to_user(v: Any) -> Any:
+    """Avro records reach Python agents as ``langstream.AvroValue(schema, value)`` -- the
+    schema as its JSON dict, the value as plain dicts (the reference decodes them with
+    fastavro.schemaless_reader: RTPY/langstream_grpc/grpc_service.py:239-248)."""
+    from ..api.avro import AvroRecord
+    if isinstance(v, AvroRecord) and v.schema is not None:
+        from langstream import AvroValue
+        return AvroValue(schema=v.schema.to_json(), value=_plain(v))
+    return v
+
+
+def _plain(v: Any) -> Any:
+    if isinstance(v, dict):
+        return {k: _plain(x) for k, x in v.items()}
+    if isinstance(v, list):
+        return [_plain(x) for x in v]
+    return v
+
+
+def _from_user(v: Any) -> Any:
+    """``AvroValue`` results become AvroRecords (encoded with their schema downstream,
+    grpc_service.py:294-305's schemaless_writer path)."""
+    if type(v).__name__ == "AvroValue" and hasattr(v, "schema") and hasattr(v, "value"):
+        from ..api.avro import AvroRecord
+        return AvroRecord(v.value, v.schema)
+    return v
+
+
 class _UserRecord:
     """Runtime Record viewed through the user API (key(), value(), headers() as tuples)."""
 
@@ -34,10 +62,10 @@ class _UserRecord:
         self._r = r
 
     def key(self):
-        return self._r.key()
+        return _to_user(self._r.key())
 
     def value(self):
-        return self._r.value()
+        return _to_user(self._r.value())
 
     def origin(self):
         return self._r.origin()
@@ -57,19 +85,21 @@ def to_runtime_record(x: Any) -> Record:
         return x._r
     if isinstance(x, Record):
         return x
+    f = _from_user
     if isinstance(x, dict):
-        return SimpleRecord.of(x.get("key"), x.get("value"), [Header(k, v) for k, v in (x.get("headers") or [])],
-                               x.get("origin"), x.get("timestamp"))
+        return SimpleRecord.of(f(x.get("key")), f(x.get("value")),
+                               [Header(k, f(v)) for k, v in (x.get("headers") or [])], x.get("origin"),
+                               x.get("timestamp"))
     if isinstance(x, (tuple, list)):
         vals = list(x) + [None] * (5 - len(x))
         value, key, headers, origin, ts = vals[:5]
-        return SimpleRecord.of(key, value, [Header(k, v) for k, v in (headers or [])], origin, ts)
+        return SimpleRecord.of(f(key), f(value), [Header(k, f(v)) for k, v in (headers or [])], origin, ts)
     if hasattr(x, "value") and callable(x.value):
-        hs = [Header(k, v) for k, v in (x.headers() or [])] if hasattr(x, "headers") else []
-        return SimpleRecord.of(x.key() if hasattr(x, "key") else None, x.value(), hs,
+        hs = [Header(k, f(v)) for k, v in (x.headers() or [])] if hasattr(x, "headers") else []
+        return SimpleRecord.of(f(x.key()) if hasattr(x, "key") else None, f(x.value()), hs,
                                x.origin() if hasattr(x, "origin") else None,
                                x.timestamp() if hasattr(x, "timestamp") else None)
-    return SimpleRecord.of(None, x)
+    return SimpleRecord.of(None, f(x))
 
 
 class _Ctx:

@@ -71,10 +71,10 @@ def pod_configuration(plan: ExecutionPlan, node: AgentNode, tenant: str = "defau
     sc = inst.streaming_cluster if inst is not None else None
     inp: Dict[str, Any] = {}
     if node.input is not None:
-        inp["topic"] = node.input.name
+        inp = node.input.consumer_configuration()
         if node.input.deadletter is not None:
-            inp["deadLetterTopicProducer"] = {"topic": node.input.deadletter.name}
-    out: Dict[str, Any] = {"topic": node.output.name} if node.output is not None else {}
+            inp["deadLetterTopicProducer"] = node.input.deadletter.producer_configuration()
+    out: Dict[str, Any] = node.output.producer_configuration() if node.output is not None else {}
     errors = {"retries": node.errors.retries or 0, "onFailure": node.errors.on_failure or "fail"}
     return RuntimePodConfiguration(
         agent_id=node.id, agent_type=node.agent_type, component_type=node.component_type.value,

@@ -51,12 +51,12 @@ def agent_pod_configuration(plan: ExecutionPlan, node: AgentNode, tenant: str) -
     sc = inst.streaming_cluster if inst is not None else None
     inp: Dict[str, Any] = {}
     if node.input is not None:
-        inp["topic"] = node.input.name
+        inp = node.input.consumer_configuration()
         if node.input.deadletter is not None:
-            inp["deadLetterTopicProducer"] = {"topic": node.input.deadletter.name}
+            inp["deadLetterTopicProducer"] = node.input.deadletter.producer_configuration()
     return {
         "input": inp,
-        "output": {"topic": node.output.name} if node.output is not None else {},
+        "output": node.output.producer_configuration() if node.output is not None else {},
         "agent": {"componentType": node.component_type.value, "tenant": tenant, "agentId": node.id,
                   "applicationId": plan.application_id, "agentType": node.agent_type,
                   "configuration": node.configuration,

@@ -49,6 +49,41 @@ class Topic:
                 "deletion-mode": self.deletion_mode, "implicit": self.implicit,
                 "deadletter": self.deadletter.name if self.deadletter else None, "config": self.config}
 
+    def _schemas(self) -> Dict[str, Any]:
+        out = {}
+        for k, s in (("keySchema", self.definition.key_schema if self.definition else None),
+                     ("valueSchema", self.definition.value_schema if self.definition else None)):
+            if s is not None:
+                out[k] = {"type": s.type, "schema": s.schema, "name": s.name}
+        return out
+
+    def consumer_configuration(self) -> Dict[str, Any]:
+        """What an agent's input connection carries (KAFKA/KafkaTopic.java:62-88): the topic,
+        the key / value deserializer its schemas select, the schemas themselves, and the
+        ``consumer.*`` options (prefix stripped)."""
+        from ..topics.kafka.serde import deserializer_for_schema
+        sch = self._schemas()
+        cfg: Dict[str, Any] = {"topic": self.name,
+                               "key.deserializer": deserializer_for_schema(sch.get("keySchema")),
+                               "value.deserializer": deserializer_for_schema(sch.get("valueSchema")), **sch}
+        for k, v in (self.options or {}).items():
+            if k.startswith("consumer."):
+                cfg[k[len("consumer."):]] = v
+        return cfg
+
+    def producer_configuration(self) -> Dict[str, Any]:
+        """Output connection (KAFKA/KafkaTopic.java:123-138): serializers + schemas +
+        ``producer.*`` options."""
+        from ..topics.kafka.serde import serializer_for_schema
+        sch = self._schemas()
+        cfg: Dict[str, Any] = {"topic": self.name,
+                               "key.serializer": serializer_for_schema(sch.get("keySchema")),
+                               "value.serializer": serializer_for_schema(sch.get("valueSchema")), **sch}
+        for k, v in (self.options or {}).items():
+            if k.startswith("producer."):
+                cfg[k[len("producer."):]] = v
+        return cfg
+
 
 @dataclass
 class AgentNode:

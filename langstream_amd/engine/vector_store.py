@@ -226,6 +226,24 @@ class VectorStore:
     def __len__(self) -> int:
         return self._n
 
+    @property
+    def persistent(self) -> bool:
+        return self._persist is not None
+
+    def attach_persistence(self, persist_dir: str, fsync: bool = False) -> bool:
+        """Make a store created without persistence durable: restore what the directory
+        holds and WAL-log every later write.  Only an EMPTY store can be attached (its
+        in-memory rows would otherwise exist in no WAL); returns False when it is not."""
+        with on_search(self.device), self.lock:
+            if self._persist is not None:
+                return True
+            if self._n:
+                return False
+            self._persist = _Persistence(persist_dir, fsync)
+            self._restore()
+            self._mark_written()
+            return True
+
     # ------------------------------------------------------------------ mutation
     def _grow(self, need: int) -> None:
         cap = self._vecs.shape[0]
@@ -483,11 +501,25 @@ class VectorStoreRegistry:
 
     @classmethod
     def configure(cls, persist_dir: Optional[str] = None, fsync: Optional[bool] = None) -> None:
+        """Set the persistence directory (and fsync policy) for collections.  Collections
+        that already exist without persistence -- e.g. a query agent that started before
+        the sink -- are made durable when still empty, and reported otherwise; a collection
+        already persisted elsewhere keeps its directory (with a warning)."""
         with cls._lock:
-            if persist_dir:
-                cls.persist_dir = persist_dir
             if fsync is not None:
                 cls.fsync = bool(fsync)
+            if not persist_dir or persist_dir == cls.persist_dir:
+                return
+            old = cls.persist_dir
+            cls.persist_dir = persist_dir
+            for name, s in cls._stores.items():
+                if s.persistent:
+                    log.warning("vector collection %s keeps its persistence directory under %s; the new "
+                                "directory %s applies to collections created from now on", name, old, persist_dir)
+                elif not s.attach_persistence(os.path.join(persist_dir, _safe(name)), cls.fsync):
+                    log.warning("vector collection %s was created without persistence and already holds "
+                                "%d rows: they are NOT durable (configure persistence before the first write)",
+                                name, len(s))
 
     @classmethod
     def _persisted_dim(cls, name: str) -> Optional[int]:

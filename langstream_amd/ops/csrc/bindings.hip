@@ -78,6 +78,15 @@ void decode_gemm_silu(at::Tensor out, at::Tensor x, at::Tensor w, at::Tensor wor
                       at::Tensor err, int64_t splits);
 void decode_gemm_ablate(at::Tensor x, at::Tensor w, at::Tensor workspace, int64_t abl, int64_t splits,
                         int64_t split_outer);
+int64_t decode_gemm_cmb_splits(int64_t N, int64_t K);
+void decode_gemm_res(at::Tensor y_out, at::Tensor x, at::Tensor w, at::Tensor workspace, at::Tensor counters,
+                     at::Tensor residual, at::Tensor norm_g, at::Tensor sumsq_out, at::Tensor err);
+void decode_gemm_qkv_cmb(at::Tensor qkv, at::Tensor x, at::Tensor w, at::Tensor workspace, at::Tensor counters,
+                         at::Tensor sumsq_in, double eps, at::Tensor pos, at::Tensor cos_sin, at::Tensor slots,
+                         at::Tensor k_cache, at::Tensor v_cache, int64_t Hq, int64_t Hkv, at::Tensor err);
+void decode_gemm_silu_r(at::Tensor out, at::Tensor x, at::Tensor w, at::Tensor sumsq_in, double eps);
+void rms_prep(at::Tensor y, at::Tensor sumsq, at::Tensor h, at::Tensor g);
+void rows_rms_scale(at::Tensor out, at::Tensor y, at::Tensor sumsq, double eps);
 void bind_runners(pybind11::module_& m);
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -134,5 +143,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("decode_gemm_f32", &decode_gemm_f32, py::arg("out"), py::arg("x"), py::arg("w"), py::arg("bn") = 0);
   m.def("decode_gemm_silu", &decode_gemm_silu, py::arg("out"), py::arg("x"), py::arg("w"), py::arg("workspace"),
         py::arg("tickets"), py::arg("err"), py::arg("splits") = 0);
+  m.def("decode_gemm_cmb_splits", &decode_gemm_cmb_splits);
+  m.def("decode_gemm_res", &decode_gemm_res);
+  m.def("decode_gemm_qkv_cmb", &decode_gemm_qkv_cmb);
+  m.def("decode_gemm_silu_r", &decode_gemm_silu_r);
+  m.def("rms_prep", &rms_prep);
+  m.def("rows_rms_scale", &rows_rms_scale);
   bind_runners(m);
 }

@@ -58,7 +58,49 @@ __device__ __forceinline__ void wait_vmcnt_dyn(int n) {
   }
 }
 
-enum { EPI_STORE = 0, EPI_PARTIAL = 1, EPI_SILU = 2, EPI_SILU2 = 3 };
+enum { EPI_STORE = 0, EPI_PARTIAL = 1, EPI_SILU = 2, EPI_SILU2 = 3, EPI_CMB_RES = 4, EPI_CMB_QKV = 5,
+       EPI_SILU_R = 6 };
+
+// ---- the norm-deferred decode layer (TP = 1, 129..256 rows; LlamaRunner::forward_dgemm)
+//
+// RMSNorm needs whole rows, which is what forced a separate split-K reduce kernel (with
+// its launch and its slab round trip) behind o / down.  Here the norm is split in two:
+//   rmsnorm(h) . W^T = r_m * ((h * g) . W^T),   r_m = 1 / sqrt(mean_k h[m,k]^2 + eps)
+// The producer's combine writes y = bf16(h * g) -- elementwise, no row dependency -- and
+// per-(row, tile) partial sums of h^2; the consumer GEMM runs on y and multiplies its
+// output rows by r_m (gate_up: in its SwiGLU epilogue; qkv: in its combine, before RoPE).
+// With that, the split-K reduction of qkv / o / down happens INSIDE the GEMM launch:
+// the S K-slices of a tile write their f32 partial tiles, meet at a per-tile counter
+// (all tiles x S <= CUs workgroups are co-resident: one 160 KB-LDS workgroup per CU), and
+// each slice then reduces 1/S of the tile's rows (cdna_hip_programming "Projection GEMM
+// at M = 256", item 2: plain slab stores -> agent release -> counter; counter poll ->
+// agent acquire -> plain loads).  Counters are 64-bit and monotonic per call site
+// (never reset; a launch advances each of its tiles by exactly S).
+struct DgArgs {
+  unsigned long long* counters = nullptr;  // [tiles] per call site
+  int* err = nullptr;                      // set when a rendezvous times out
+  bf16* residual = nullptr;                // CMB_RES: h, updated in place (h += x . w^T)
+  const bf16* norm_g = nullptr;            // CMB_RES: the next RMSNorm's weight [N]
+  bf16* y_out = nullptr;                   // CMB_RES: bf16(h * g) [M, N]
+  float* sumsq_out = nullptr;              // CMB_RES: [M][tiles] partial sums of h^2
+  const float* sumsq_in = nullptr;         // CMB_QKV / SILU_R: the producer's partials [M][npart]
+  int npart = 0;
+  float eps = 1e-5f, inv_h = 0.f;          // inv_h = 1 / hidden size (the mean of h^2)
+  const int32_t* pos = nullptr;            // CMB_QKV: RoPE + paged KV write
+  const float* cos_sin = nullptr;
+  int max_pos = 0;
+  const int64_t* slots = nullptr;
+  int64_t nslots = 0;
+  bf16* kc = nullptr;
+  bf16* vc = nullptr;
+  int Hq = 0, Hkv = 0, BS = 0;
+};
+
+__device__ __forceinline__ float rms_scale(const float* __restrict__ part, int npart, float inv_h, float eps) {
+  float s = 0.f;
+  for (int t = 0; t < npart; ++t) s += part[t];
+  return rsqrtf(s * inv_h + eps);
+}
 
 // 8-row x 128-B piece p of an image: lane l fills row 8p + (l >> 3), LDS chunk l & 7
 // with global chunk (l & 7) ^ ((row >> 1) & 7).
@@ -80,8 +122,11 @@ __global__ void __launch_bounds__(LD ? 768 : 512) dgemm_kernel(const bf16* __res
                                                    const bf16* __restrict__ w, int M, int N, int K, int S,
                                                    bf16* __restrict__ out, int64_t ldo, float* __restrict__ part,
                                                    int F, unsigned* __restrict__ tickets, float* __restrict__ xchg,
-                                                   int* __restrict__ err, int split_outer) {
+                                                   int* __restrict__ err, int split_outer, DgArgs ga) {
   constexpr int WSTAGE = BN * BK * 2;
+  constexpr bool CMB = EPI == EPI_CMB_RES || EPI == EPI_CMB_QKV;
+  constexpr bool SILU_LIKE = EPI == EPI_SILU || EPI == EPI_SILU_R;
+  static_assert(!(CMB || EPI == EPI_SILU_R) || (BN == 128 && LD == 4), "fused epilogues: BN 128 + loader waves");
   constexpr int JT = BN / 32;              // 16-col tiles per wave (wave = 64 rows x BN/2 cols)
   constexpr int IT = 4;                    // 16-row tiles per wave
   constexpr int NLW = LD ? LD : 8;         // waves that issue the DMAs
@@ -131,7 +176,7 @@ __global__ void __launch_bounds__(LD ? 768 : 512) dgemm_kernel(const bf16* __res
     wvo[p] = ((lane >> 3) * K + (((lane & 7) ^ ((4 * p + (lane >> 4)) & 7)) * 8)) * 2;
   auto wrow0 = [&](int j) -> uint32_t {   // first W row of piece j (uniform)
     const int lr = (8 * PW) * lw + 8 * j;
-    if constexpr (EPI == EPI_SILU || EPI == EPI_SILU2)
+    if constexpr (EPI == EPI_SILU || EPI == EPI_SILU2 || EPI == EPI_SILU_R)
       return lr < BN / 2 ? tile * (BN / 2) + lr : F + tile * (BN / 2) + (lr - BN / 2);
     return tile * BN + lr;
   };
@@ -156,7 +201,7 @@ __global__ void __launch_bounds__(LD ? 768 : 512) dgemm_kernel(const bf16* __res
   const int fr = lane & 15, h = lane >> 4;
   const int fsw = (fr >> 1) & 7;           // = (row >> 1) & 7 of every fragment row
   auto bcol = [&](int j) {                 // tile-local W row of this lane's B fragment
-    if constexpr (EPI == EPI_SILU || EPI == EPI_SILU2)
+    if constexpr (EPI == EPI_SILU || EPI == EPI_SILU2 || EPI == EPI_SILU_R)
       return (j < JT / 2 ? (BN / 4) * wn + 16 * j : BN / 2 + (BN / 4) * wn + 16 * (j - JT / 2)) + fr;
     return (BN / 2) * wn + 16 * j + fr;
   };
@@ -305,6 +350,9 @@ __global__ void __launch_bounds__(LD ? 768 : 512) dgemm_kernel(const bf16* __res
   static_assert(PASS_ROWS * TP * 4 <= XS * XSTAGE + WS * WSTAGE, "epilogue pass must fit the ring's LDS");
   constexpr int NT = LD ? 768 : 512;
   float* T = reinterpret_cast<float*>(lds);
+  // SILU_R: the row scales 1/rms(h) after T (LDS past 256 x 132 floats is free)
+  float* rbuf = reinterpret_cast<float*>(lds + PASS_ROWS * TP * 4);
+  if constexpr (EPI == EPI_SILU_R) static_assert(PASS_ROWS == BM && BM * TP * 4 + BM * 4 <= LDS_MAX, "r buffer");
 #pragma unroll
   for (int r0 = 0; r0 < BM; r0 += PASS_ROWS) {
     __syncthreads();                                    // ring reads / the previous pass are done
@@ -318,9 +366,17 @@ __global__ void __launch_bounds__(LD ? 768 : 512) dgemm_kernel(const bf16* __res
           for (int j = 0; j < JT; ++j) trow[bcol(j)] = acc[i][j][r];
         }
     }
+    if constexpr (EPI == EPI_SILU_R) {
+      // the loader waves (idle now) reduce the producer's per-tile partial sums of h^2
+      // while the compute waves stage the tile
+      if (!computer) {
+        const int m = threadIdx.x - 512;
+        if (m < M) rbuf[m] = rms_scale(ga.sumsq_in + (int64_t)m * ga.npart, ga.npart, ga.inv_h, ga.eps);
+      }
+    }
     __syncthreads();
     const int rows = min(PASS_ROWS, M - r0);
-    if constexpr (EPI == EPI_PARTIAL) {
+    if constexpr (EPI == EPI_PARTIAL || CMB) {
       // part[split][m][tile * BN + c]: BN / 4 float4 per row
       for (int q = threadIdx.x; q < ((ABL & 64) ? 0 : rows * (BN / 4)); q += NT) {
         const int m = q / (BN / 4), c = (q - m * (BN / 4)) * 4;
@@ -339,14 +395,136 @@ __global__ void __launch_bounds__(LD ? 768 : 512) dgemm_kernel(const bf16* __res
         st16(out + (int64_t)(r0 + m) * ldo + tile * BN + c, pack8(v));
       }
     } else {
-      // EPI_SILU: tile columns [0, BN/2) are gate, [BN/2, BN) the matching up columns
+      // EPI_SILU(_R): tile columns [0, BN/2) are gate, [BN/2, BN) the matching up columns
       for (int q = threadIdx.x; q < rows * (BN / 16); q += NT) {
         const int m = q / (BN / 16), c = (q - m * (BN / 16)) * 8;
         const float* g = T + m * TP + c;
+        const float rs = EPI == EPI_SILU_R ? rbuf[r0 + m] : 1.f;
         float v[8];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = g[e] / (1.f + __expf(-g[e])) * g[BN / 2 + e];
+        for (int e = 0; e < 8; ++e) {
+          const float gg = g[e] * rs, uu = g[BN / 2 + e] * rs;
+          v[e] = gg / (1.f + __expf(-gg)) * uu;
+        }
         st16(out + (int64_t)(r0 + m) * ldo + tile * (BN / 2) + c, pack8(v));
+      }
+    }
+  }
+  if constexpr (CMB) {
+    // ---- rendezvous of the tile's S slices: publish this slab, wait for the others
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's slab stores are done
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      unsigned long long* cnt = ga.counters + tile;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const unsigned long long old = __hip_atomic_fetch_add(cnt, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned long long target = old - old % (unsigned long long)S + (unsigned long long)S;
+      int spins = 0;
+      while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > (1 << 23)) {   // ~1 s: a slice never arrived -- flag it, never hang
+          __hip_atomic_store(ga.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          break;
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    // ---- this slice reduces rows [rr0, rr0 + nr) of the tile over the S slabs
+    const int R = (M + S - 1) / S;
+    const int rr0 = split * R, nr = min(R, M - rr0);
+    if (nr <= 0) return;
+    const int64_t MN = (int64_t)M * N;
+    if constexpr (EPI == EPI_CMB_RES) {
+      // h += sum; residual <- bf16(h); y <- bf16(bf16(h) * g); sumsq[m][tile] = sum_c h^2.
+      // Thread = 8 consecutive columns of one row; the 16 threads of a row are 16
+      // consecutive lanes of one wave (NT and 16 | 64), reduced with width-16 shuffles.
+      const int ntiles = N / BN;
+      for (int q = threadIdx.x; q < nr * (BN / 8); q += NT) {
+        const int m = rr0 + q / (BN / 8), c = tile * BN + (q % (BN / 8)) * 8;
+        const float* p = part + (int64_t)m * N + c;
+        f32x4 a0 = *reinterpret_cast<const f32x4*>(p), a1 = *reinterpret_cast<const f32x4*>(p + 4);
+        for (int s = 1; s < S; ++s) {
+          a0 += *reinterpret_cast<const f32x4*>(p + s * MN);
+          a1 += *reinterpret_cast<const f32x4*>(p + s * MN + 4);
+        }
+        bf16* rp = ga.residual + (int64_t)m * N + c;
+        float h[8], y[8], g[8];
+        unpack8(ld16(rp), h);
+        unpack8(ld16(ga.norm_g + c), g);
+        float ss = 0.f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float hv = (float)(bf16)(h[e] + (e < 4 ? a0[e] : a1[e - 4]));   // the bf16 residual stream
+          h[e] = hv;
+          y[e] = hv * g[e];
+          ss += hv * hv;
+        }
+        st16(rp, pack8(h));
+        st16(ga.y_out + (int64_t)m * N + c, pack8(y));
+#pragma unroll
+        for (int o = 8; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 16);
+        if ((q & 15) == 0) ga.sumsq_out[(int64_t)m * ntiles + tile] = ss;
+      }
+    } else {
+      // qkv: the tile is one head (BN = D = 128).  Row scale r_m from the producer's
+      // partials, then RoPE on q / k heads, the paged K / V write for k / v heads.
+      constexpr int D = 128, HALF = 64, G4 = 16;
+      float* rrow = reinterpret_cast<float*>(lds);   // LDS is free after the slab stores
+      for (int i = threadIdx.x; i < nr; i += NT)
+        rrow[i] = rms_scale(ga.sumsq_in + (int64_t)(rr0 + i) * ga.npart, ga.npart, ga.inv_h, ga.eps);
+      __syncthreads();
+      const int hd = tile;
+      for (int q = threadIdx.x; q < nr * G4; q += NT) {
+        const int i = q / G4, c4 = q % G4, m = rr0 + i;
+        const int64_t e0 = (int64_t)m * N + (int64_t)hd * D + 4 * c4;
+        f32x4 lo = *reinterpret_cast<const f32x4*>(part + e0), hi = *reinterpret_cast<const f32x4*>(part + e0 + HALF);
+        for (int s = 1; s < S; ++s) {
+          lo += *reinterpret_cast<const f32x4*>(part + s * MN + e0);
+          hi += *reinterpret_cast<const f32x4*>(part + s * MN + e0 + HALF);
+        }
+        const float rs = rrow[i];
+        float a[4], b[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          a[j] = lo[j] * rs;
+          b[j] = hi[j] * rs;
+        }
+        if (hd < ga.Hq + ga.Hkv) {
+          const int pp = min(max(ga.pos[m], 0), ga.max_pos - 1);
+          const float4 co = *reinterpret_cast<const float4*>(ga.cos_sin + (int64_t)pp * D + 4 * c4);
+          const float4 si = *reinterpret_cast<const float4*>(ga.cos_sin + (int64_t)pp * D + HALF + 4 * c4);
+          const float cv[4] = {co.x, co.y, co.z, co.w}, sv[4] = {si.x, si.y, si.z, si.w};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float x1 = a[j], x2 = b[j];
+            a[j] = x1 * cv[j] - x2 * sv[j];
+            b[j] = x2 * cv[j] + x1 * sv[j];
+          }
+        }
+        const bf16x4 va = {(bf16)a[0], (bf16)a[1], (bf16)a[2], (bf16)a[3]};
+        const bf16x4 vb = {(bf16)b[0], (bf16)b[1], (bf16)b[2], (bf16)b[3]};
+        bf16* orow = out + (int64_t)m * ldo + (int64_t)hd * D + 4 * c4;
+        *reinterpret_cast<bf16x4*>(orow) = va;
+        *reinterpret_cast<bf16x4*>(orow + HALF) = vb;
+        if (hd < ga.Hq) continue;
+        const int64_t sl = ga.slots[m];
+        if (sl < 0 || sl >= ga.nslots) continue;
+        const int64_t blk = sl / ga.BS, off = sl - blk * ga.BS;
+        if (hd < ga.Hq + ga.Hkv) {
+          bf16* kd = ga.kc + ((blk * ga.Hkv + (hd - ga.Hq)) * ga.BS + off) * D + 4 * c4;
+          *reinterpret_cast<bf16x4*>(kd) = va;
+          *reinterpret_cast<bf16x4*>(kd + HALF) = vb;
+        } else {
+          bf16* vd = ga.vc + ((blk * ga.Hkv + (hd - ga.Hq - ga.Hkv)) * (int64_t)D) * ga.BS;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            vd[vt_off(4 * c4 + j, (int)off, D)] = va[j];
+            vd[vt_off(HALF + 4 * c4 + j, (int)off, D)] = vb[j];
+          }
+        }
       }
     }
   }
@@ -385,14 +563,16 @@ int ntst_default() { return env_int("LS_DGEMM_NTST", 1); }
 // BN = 256: X 2 + W 3 = 160 KB.
 template <int BN, int EPI>
 void dgemm_launch(int S, int tiles, hipStream_t st, const at::Tensor& x, const at::Tensor& w, int M, int N, int K,
-                  bf16* out, int64_t ldo, float* part, int F, unsigned* tickets, float* xchg, int* err) {
+                  bf16* out, int64_t ldo, float* part, int F, unsigned* tickets, float* xchg, int* err,
+                  DgArgs ga = DgArgs()) {
   constexpr int XS = BN == 128 ? 3 : 2, WS = BN == 128 ? 4 : 3;
   // BN = 256: 8 compute waves need 128 accumulator VGPRs each, no room for a third wave
   // per SIMD.  (Streaming the B fragments one at a time fits 168 VGPRs with 4 loader
   // waves, but the gate_up K-half exchange form then measured 90 vs 82 us:
   // profiles/dgemm_r3c/silu2_loaders.log.)
   constexpr int LDW = BN == 128 ? 4 : 0;
-  const int so = EPI == EPI_SILU2 ? 0 : split_outer_default();
+  // the gate_up exchange pairs and the in-launch combine slices of a tile sit on one XCD
+  const int so = (EPI == EPI_SILU2 || EPI == EPI_CMB_RES || EPI == EPI_CMB_QKV) ? 0 : split_outer_default();
   // cache-policy variants (ABL bits 4 and 7, real variants): weights streamed with the
   // non-temporal hint -- 16 GB of weights per decode step have no reuse and should not
   // evict the activations and the split-K workspace -- and / or the f32 partial slabs
@@ -402,13 +582,13 @@ void dgemm_launch(int S, int tiles, hipStream_t st, const at::Tensor& x, const a
   case A:                                                                                                        \
     dgemm_kernel<BN, XS, WS, EPI, A, LDW><<<dim3(tiles * S), 768, 0, st>>>(                                      \
         (const bf16*)x.data_ptr(), x.stride(0), (const bf16*)w.data_ptr(), M, N, K, S, out, ldo, part, F, tickets, \
-        xchg, err, so);                                                                                          \
+        xchg, err, so, ga);                                                                                      \
     return;
   switch (pol) { POL_(16) POL_(128) POL_(144) default: break; }
 #undef POL_
   dgemm_kernel<BN, XS, WS, EPI, 0, LDW><<<dim3(tiles * S), LDW ? 768 : 512, 0, st>>>((const bf16*)x.data_ptr(), x.stride(0),
                                                                  (const bf16*)w.data_ptr(), M, N, K, S, out, ldo,
-                                                                 part, F, tickets, xchg, err, so);
+                                                                 part, F, tickets, xchg, err, so, ga);
 }
 
 void check_xw(const at::Tensor& x, const at::Tensor& w) {
@@ -684,7 +864,7 @@ void decode_gemm_ablate(at::Tensor x, at::Tensor w, at::Tensor workspace, int64_
         (const bf16*)x.data_ptr(), x.stride(0),                                                        \
                                                                   (const bf16*)w.data_ptr(), M, N, K, S,  \
                                                                   nullptr, 0, part, 0, nullptr, nullptr, \
-                                                                  nullptr, (int)split_outer);            \
+                                                                  nullptr, (int)split_outer, DgArgs());  \
     break;
   switch (abl) {
     A_(0) A_(1) A_(2) A_(3) A_(4) A_(5) A_(7) A_(8) A_(9) A_(11) A_(16) A_(17)
@@ -692,4 +872,190 @@ void decode_gemm_ablate(at::Tensor x, at::Tensor w, at::Tensor workspace, int64_
     default: TORCH_CHECK(false, "unsupported ablation ", abl);
   }
 #undef A_
+}
+
+// ---------------------------------------------------------------------------------
+// Norm-deferred decode layer entry points (see DgArgs).  The combine path needs every
+// workgroup of the launch co-resident (tiles x S <= CUs; one workgroup per CU by LDS).
+namespace {
+int device_cus() {
+  static const int n = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return 0;
+    return v;
+  }();
+  return n;
+}
+
+void check_cmb_common(const at::Tensor& x, const at::Tensor& w, const at::Tensor& workspace, const at::Tensor& counters,
+                      const at::Tensor& err, int S) {
+  check_xw(x, w);
+  const int64_t M = x.size(0), N = w.size(0);
+  TORCH_CHECK(N % 128 == 0, "combine path: N % 128 == 0");
+  TORCH_CHECK(S >= 1 && (N / 128) * S <= device_cus(), "combine path: tiles x splits exceeds the CU count");
+  TORCH_CHECK(workspace.scalar_type() == at::kFloat && workspace.is_cuda() && workspace.numel() >= S * M * N,
+              "combine path: workspace too small");
+  TORCH_CHECK(counters.scalar_type() == at::kLong && counters.is_cuda() && counters.numel() >= N / 128,
+              "combine path: counters int64 [tiles]");
+  TORCH_CHECK(err.scalar_type() == at::kInt && err.is_cuda() && err.numel() >= 1, "combine path: err int32 [1]");
+}
+}  // namespace
+
+// K splits of the combine path for an [N, K] weight (0: not supported on this device).
+int64_t decode_gemm_cmb_splits(int64_t N, int64_t K) {
+  if (N % 128 != 0 || K % BK != 0) return 0;
+  const int tiles = (int)(N / 128), cus = device_cus();
+  if (cus <= 0 || tiles > cus) return 0;
+  int best = 0;
+  for (int s = 1; s <= 16; ++s) {
+    if (tiles * s > cus || (K / BK) / s < 4) break;
+    best = s;
+  }
+  return best;
+}
+
+// residual[M, N] += x . w^T  (in place, bf16 residual stream);  y_out = bf16(residual * norm_g);
+// sumsq_out[M][N / 128] = per-tile sums of residual^2 (for the consumer's 1/rms).
+void decode_gemm_res(at::Tensor y_out, at::Tensor x, at::Tensor w, at::Tensor workspace, at::Tensor counters,
+                     at::Tensor residual, at::Tensor norm_g, at::Tensor sumsq_out, at::Tensor err) {
+  const int M = (int)x.size(0), K = (int)x.size(1), N = (int)w.size(0);
+  const int S = (int)decode_gemm_cmb_splits(N, K);
+  check_cmb_common(x, w, workspace, counters, err, S);
+  TORCH_CHECK(residual.scalar_type() == at::kBFloat16 && residual.is_contiguous() && residual.numel() == (int64_t)M * N,
+              "decode_gemm_res: residual bf16 [M, N] contiguous");
+  TORCH_CHECK(y_out.scalar_type() == at::kBFloat16 && y_out.is_contiguous() && y_out.numel() == (int64_t)M * N,
+              "decode_gemm_res: y_out bf16 [M, N] contiguous");
+  TORCH_CHECK(norm_g.scalar_type() == at::kBFloat16 && norm_g.is_contiguous() && norm_g.numel() == N,
+              "decode_gemm_res: norm weight bf16 [N]");
+  TORCH_CHECK(sumsq_out.scalar_type() == at::kFloat && sumsq_out.is_contiguous() &&
+              sumsq_out.numel() >= (int64_t)M * (N / 128), "decode_gemm_res: sumsq_out f32 [M, N / 128]");
+  DgArgs ga;
+  ga.counters = reinterpret_cast<unsigned long long*>(counters.data_ptr<int64_t>());
+  ga.err = err.data_ptr<int>();
+  ga.residual = (bf16*)residual.data_ptr();
+  ga.norm_g = (const bf16*)norm_g.data_ptr();
+  ga.y_out = (bf16*)y_out.data_ptr();
+  ga.sumsq_out = sumsq_out.data_ptr<float>();
+  dgemm_launch<128, EPI_CMB_RES>(S, N / 128, at::hip::getCurrentHIPStream(), x, w, M, N, K, nullptr, 0,
+                                 workspace.data_ptr<float>(), 0, nullptr, nullptr, nullptr, ga);
+}
+
+// qkv = RoPE(r_m * (x . w^T)) with the step's K / V rows written to the paged cache;
+// r_m from sumsq_in [M, npart] (the producer's partials) over hidden size K.
+void decode_gemm_qkv_cmb(at::Tensor qkv, at::Tensor x, at::Tensor w, at::Tensor workspace, at::Tensor counters,
+                         at::Tensor sumsq_in, double eps, at::Tensor pos, at::Tensor cos_sin, at::Tensor slots,
+                         at::Tensor k_cache, at::Tensor v_cache, int64_t Hq, int64_t Hkv, at::Tensor err) {
+  const int M = (int)x.size(0), K = (int)x.size(1), N = (int)w.size(0);
+  const int S = (int)decode_gemm_cmb_splits(N, K);
+  check_cmb_common(x, w, workspace, counters, err, S);
+  const int D = (int)k_cache.size(3), BSZ = (int)k_cache.size(2);
+  TORCH_CHECK(D == 128 && N == (Hq + 2 * Hkv) * D, "decode_gemm_qkv_cmb: head dim 128, qkv width");
+  TORCH_CHECK(qkv.scalar_type() == at::kBFloat16 && qkv.size(0) == M && qkv.size(1) == N && qkv.stride(1) == 1);
+  TORCH_CHECK(sumsq_in.scalar_type() == at::kFloat && sumsq_in.is_contiguous() && sumsq_in.dim() == 2 &&
+              sumsq_in.size(0) >= M, "decode_gemm_qkv_cmb: sumsq_in f32 [M, npart]");
+  TORCH_CHECK(pos.scalar_type() == at::kInt && pos.numel() >= M && slots.scalar_type() == at::kLong &&
+              slots.numel() >= M && cos_sin.scalar_type() == at::kFloat && cos_sin.is_contiguous() &&
+              cos_sin.size(1) == D, "decode_gemm_qkv_cmb: pos / slots / cos_sin");
+  TORCH_CHECK(k_cache.is_contiguous() && v_cache.is_contiguous() && v_cache.dim() == 5 && v_cache.size(2) == BSZ / 8 &&
+              v_cache.size(3) == D && v_cache.size(4) == 8, "decode_gemm_qkv_cmb: v_cache [NB, Hkv, BS/8, D, 8]");
+  DgArgs ga;
+  ga.counters = reinterpret_cast<unsigned long long*>(counters.data_ptr<int64_t>());
+  ga.err = err.data_ptr<int>();
+  ga.sumsq_in = sumsq_in.data_ptr<float>();
+  ga.npart = (int)sumsq_in.size(1);
+  ga.eps = (float)eps;
+  ga.inv_h = 1.f / (float)K;
+  ga.pos = pos.data_ptr<int32_t>();
+  ga.cos_sin = cos_sin.data_ptr<float>();
+  ga.max_pos = (int)cos_sin.size(0);
+  ga.slots = slots.data_ptr<int64_t>();
+  ga.nslots = k_cache.size(0) * BSZ;
+  ga.kc = (bf16*)k_cache.data_ptr();
+  ga.vc = (bf16*)v_cache.data_ptr();
+  ga.Hq = (int)Hq;
+  ga.Hkv = (int)Hkv;
+  ga.BS = BSZ;
+  dgemm_launch<128, EPI_CMB_QKV>(S, N / 128, at::hip::getCurrentHIPStream(), x, w, M, N, K,
+                                 (bf16*)qkv.data_ptr(), qkv.stride(0), workspace.data_ptr<float>(), 0, nullptr,
+                                 nullptr, nullptr, ga);
+}
+
+// out[M, F] = silu(r_m * x . w[:F]^T) * (r_m * x . w[F:]^T), r_m from sumsq_in [M, npart].
+void decode_gemm_silu_r(at::Tensor out, at::Tensor x, at::Tensor w, at::Tensor sumsq_in, double eps) {
+  check_xw(x, w);
+  const int M = (int)x.size(0), K = (int)x.size(1), F = (int)(w.size(0) / 2);
+  TORCH_CHECK(decode_gemm_supported(w, true), "decode_gemm_silu_r: gate_up rows must be 2F with F % 128 == 0");
+  TORCH_CHECK(out.scalar_type() == at::kBFloat16 && out.size(0) == M && out.size(1) == F && out.stride(1) == 1);
+  TORCH_CHECK(sumsq_in.scalar_type() == at::kFloat && sumsq_in.is_contiguous() && sumsq_in.dim() == 2 &&
+              sumsq_in.size(0) >= M, "decode_gemm_silu_r: sumsq_in f32 [M, npart]");
+  DgArgs ga;
+  ga.sumsq_in = sumsq_in.data_ptr<float>();
+  ga.npart = (int)sumsq_in.size(1);
+  ga.eps = (float)eps;
+  ga.inv_h = 1.f / (float)K;
+  dgemm_launch<128, EPI_SILU_R>(1, F / 64, at::hip::getCurrentHIPStream(), x, w, M, 2 * F, K, (bf16*)out.data_ptr(),
+                                out.stride(0), nullptr, F, nullptr, nullptr, nullptr, ga);
+}
+
+// ---------------------------------------------------------------------------------
+// Row helpers of the norm-deferred layer: the first layer's input (y = bf16(h * g),
+// sumsq[m] = sum h^2, one partial) and the final norm (out = bf16(y * r_m)).
+namespace {
+__global__ void __launch_bounds__(256) rms_prep_kernel(bf16* __restrict__ y, float* __restrict__ sumsq,
+                                                       const bf16* __restrict__ h, const bf16* __restrict__ g, int N) {
+  __shared__ float red[4];
+  const int m = blockIdx.x;
+  float ss = 0.f;
+  for (int c = threadIdx.x * 8; c < N; c += 256 * 8) {
+    float hv[8], gv[8], yv[8];
+    unpack8(ld16(h + (int64_t)m * N + c), hv);
+    unpack8(ld16(g + c), gv);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      ss += hv[e] * hv[e];
+      yv[e] = hv[e] * gv[e];
+    }
+    st16(y + (int64_t)m * N + c, pack8(yv));
+  }
+  ss = block_sum(ss, red);
+  if (threadIdx.x == 0) sumsq[m] = ss;
+}
+
+__global__ void __launch_bounds__(256) rows_rms_scale_kernel(bf16* __restrict__ out, const bf16* __restrict__ y,
+                                                             const float* __restrict__ sumsq, int npart, float inv_h,
+                                                             float eps, int N) {
+  const int m = blockIdx.x;
+  const float r = rms_scale(sumsq + (int64_t)m * npart, npart, inv_h, eps);
+  for (int c = threadIdx.x * 8; c < N; c += 256 * 8) {
+    float v[8];
+    unpack8(ld16(y + (int64_t)m * N + c), v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] *= r;
+    st16(out + (int64_t)m * N + c, pack8(v));
+  }
+}
+}  // namespace
+
+void rms_prep(at::Tensor y, at::Tensor sumsq, at::Tensor h, at::Tensor g) {
+  const int64_t M = h.size(0), N = h.size(1);
+  TORCH_CHECK(h.is_contiguous() && y.is_contiguous() && h.scalar_type() == at::kBFloat16 &&
+              y.scalar_type() == at::kBFloat16 && y.numel() == M * N && N % 8 == 0, "rms_prep: bf16 [M, N]");
+  TORCH_CHECK(g.numel() == N && g.scalar_type() == at::kBFloat16 && sumsq.scalar_type() == at::kFloat &&
+              sumsq.numel() >= M, "rms_prep: g [N] bf16, sumsq f32 [M]");
+  if (M == 0) return;
+  rms_prep_kernel<<<(unsigned)M, 256, 0, at::hip::getCurrentHIPStream()>>>(
+      (bf16*)y.data_ptr(), sumsq.data_ptr<float>(), (const bf16*)h.data_ptr(), (const bf16*)g.data_ptr(), (int)N);
+}
+
+void rows_rms_scale(at::Tensor out, at::Tensor y, at::Tensor sumsq, double eps) {
+  const int64_t M = y.size(0), N = y.size(1);
+  TORCH_CHECK(y.is_contiguous() && out.is_contiguous() && y.scalar_type() == at::kBFloat16 &&
+              out.scalar_type() == at::kBFloat16 && out.numel() == M * N && N % 8 == 0, "rows_rms_scale: bf16 [M, N]");
+  TORCH_CHECK(sumsq.scalar_type() == at::kFloat && sumsq.is_contiguous() && sumsq.dim() == 2 && sumsq.size(0) >= M,
+              "rows_rms_scale: sumsq f32 [M, npart]");
+  if (M == 0) return;
+  rows_rms_scale_kernel<<<(unsigned)M, 256, 0, at::hip::getCurrentHIPStream()>>>(
+      (bf16*)out.data_ptr(), (const bf16*)y.data_ptr(), sumsq.data_ptr<float>(), (int)sumsq.size(1), 1.f / (float)N,
+      (float)eps, (int)N);
 }

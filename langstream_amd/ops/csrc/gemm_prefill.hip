@@ -376,12 +376,21 @@ __global__ void __launch_bounds__(512) gemm_prefill64_kernel(const bf16* __restr
 // ds_read_b128 for the 16 rows of a fragment lane group).
 constexpr int HT = 16384;
 
-template <int EPI>
+// Epilogue forms of the ping-pong kernel (EPS):
+//   0: each lane stores its accumulators as 2-byte scalars straight from the MFMA layout
+//      (a wave-instruction writes 4 rows x 32 B: partial lines);
+//   1: the tile goes through LDS as bf16 rows (the ring is dead after the K loop) and
+//      leaves in 16-B stores of whole 512-B rows -- full 128-B lines per instruction;
+//   2: timing ablation, no stores at all (results garbage; LS_PGEMM_KERNEL=4).
+constexpr int EPI_ROW = 256 + 8;          // staged row pitch in bf16 (528 B: 4-bank shift per row)
+constexpr int PP_LDS = 256 * EPI_ROW * 2 > 8 * HT ? 256 * EPI_ROW * 2 : 8 * HT;
+
+template <int EPI, int EPS = 0>
 __global__ void __launch_bounds__(512) gemm_pp_kernel(const bf16* __restrict__ x, int64_t ldx,
                                                       const bf16* __restrict__ w, int M, int K,
                                                       bf16* __restrict__ out, int64_t ldo, int MT, int NTL, int F,
                                                       int group_m) {
-  __shared__ __attribute__((aligned(1024))) char lds[8 * HT];
+  __shared__ __attribute__((aligned(1024))) char lds[EPS == 1 ? PP_LDS : 8 * HT];
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int logical = xcd_remap(blockIdx.x, gridDim.x);
@@ -506,6 +515,53 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(const bf16* __restrict__ x
   }
   if (wm == 0) __builtin_amdgcn_s_barrier();
   wait_vmcnt<0>();  // no LDS-DMA may outlive the workgroup
+
+  if constexpr (EPS == 2) {
+#pragma unroll
+    for (int qm = 0; qm < 2; ++qm)
+#pragma unroll
+      for (int qn = 0; qn < 2; ++qn)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) asm volatile("" ::"v"(acc[qm][qn][i][j]));
+    return;
+  }
+  if constexpr (EPS == 1) {
+    // stage: every wave's fragments -> bf16 rows of the tile image (OC columns wide),
+    // then whole rows leave with 16-B stores
+    constexpr int OC = EPI == EPI_SILU ? 128 : 256;          // output columns of the tile
+    constexpr int RP = EPI == EPI_SILU ? 128 + 8 : EPI_ROW;  // row pitch (bf16)
+    bf16* T = reinterpret_cast<bf16*>(lds);
+    __syncthreads();                                         // every wave's ring reads are done
+#pragma unroll
+    for (int qm = 0; qm < 2; ++qm)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          bf16* trow = T + (128 * wm + 64 * qm + 16 * i + 4 * h + r) * RP;
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            if constexpr (EPI == EPI_SILU) {
+              const float g = acc[qm][0][i][j][r], u = acc[qm][1][i][j][r];
+              trow[32 * wn + 16 * j + fr] = (bf16)(g / (1.f + __expf(-g)) * u);
+            } else {
+#pragma unroll
+              for (int qn = 0; qn < 2; ++qn) trow[64 * wn + 32 * qn + 16 * j + fr] = (bf16)acc[qm][qn][i][j][r];
+            }
+          }
+        }
+    __syncthreads();
+    constexpr int CPR = OC / 8;                              // 16-B chunks per row
+    const int rows = min(256, M - m0);
+    const int col0 = EPI == EPI_SILU ? nt * 128 : nt * TN;
+    for (int q = threadIdx.x; q < rows * CPR; q += 512) {
+      const int rr = q / CPR, c = (q - rr * CPR) * 8;
+      st16(out + (int64_t)(m0 + rr) * ldo + col0 + c, ld16(reinterpret_cast<const char*>(T + rr * RP + c)));
+    }
+    return;
+  }
 
   // acc[qm][qn][i][j][r] = C[128 wm + 64 qm + 16 i + 4 h + r][64 wn + 32 qn + 16 j + fr] (tile-local;
   // SILU: qn = 0 gate, qn = 1 up of feature nt*128 + 32 wn + 16 j + fr)
@@ -753,9 +809,16 @@ void launch(int variant, int ring, int nwv, bool sp, dim3 grid, hipStream_t st, 
                                            ntiles);
     return;
   }
-  if (variant == 1 && K % 128 == 0) {
-    gemm_pp_kernel<EPI><<<grid, 512, 0, st>>>((const bf16*)x.data_ptr(), x.stride(0), (const bf16*)w.data_ptr(), M, K,
-                                             (bf16*)out.data_ptr(), out.stride(0), MT, NTL, F, gm);
+  if ((variant == 1 || variant == 3 || variant == 4) && K % 128 == 0) {
+    auto* xp = (const bf16*)x.data_ptr();
+    auto* wp = (const bf16*)w.data_ptr();
+    auto* op = (bf16*)out.data_ptr();
+    if (variant == 3)
+      gemm_pp_kernel<EPI, 1><<<grid, 512, 0, st>>>(xp, x.stride(0), wp, M, K, op, out.stride(0), MT, NTL, F, gm);
+    else if (variant == 4)
+      gemm_pp_kernel<EPI, 2><<<grid, 512, 0, st>>>(xp, x.stride(0), wp, M, K, op, out.stride(0), MT, NTL, F, gm);
+    else
+      gemm_pp_kernel<EPI, 0><<<grid, 512, 0, st>>>(xp, x.stride(0), wp, M, K, op, out.stride(0), MT, NTL, F, gm);
     return;
   }
   static const bool k64 = env_int("LS_PGEMM_K64", 0) != 0;   // measured equal, 2-slot ring: off

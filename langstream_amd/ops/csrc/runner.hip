@@ -137,6 +137,15 @@ void decode_gemm(at::Tensor out, at::Tensor x, at::Tensor w, at::Tensor workspac
 void decode_gemm_silu(at::Tensor out, at::Tensor x, at::Tensor w, at::Tensor workspace, at::Tensor tickets,
                       at::Tensor err, int64_t splits);
 const int* oneshot_allreduce_err(const std::shared_ptr<OneShotAllReduce>& ar);
+int64_t decode_gemm_cmb_splits(int64_t N, int64_t K);
+void decode_gemm_res(at::Tensor y_out, at::Tensor x, at::Tensor w, at::Tensor workspace, at::Tensor counters,
+                     at::Tensor residual, at::Tensor norm_g, at::Tensor sumsq_out, at::Tensor err);
+void decode_gemm_qkv_cmb(at::Tensor qkv, at::Tensor x, at::Tensor w, at::Tensor workspace, at::Tensor counters,
+                         at::Tensor sumsq_in, double eps, at::Tensor pos, at::Tensor cos_sin, at::Tensor slots,
+                         at::Tensor k_cache, at::Tensor v_cache, int64_t Hq, int64_t Hkv, at::Tensor err);
+void decode_gemm_silu_r(at::Tensor out, at::Tensor x, at::Tensor w, at::Tensor sumsq_in, double eps);
+void rms_prep(at::Tensor y, at::Tensor sumsq, at::Tensor h, at::Tensor g);
+void rows_rms_scale(at::Tensor out, at::Tensor y, at::Tensor sumsq, double eps);
 
 #define HIP_OK(x)                                                                  \
   do {                                                                             \
@@ -188,8 +197,33 @@ class LlamaRunner {
           fmax = std::max(fmax, gate_up_w_[l].size(0) / 2);
         }
       }
+      // the norm-deferred layer (forward_dgemm): combine-path splits must exist for qkv /
+      // o / down, the head dim must be 128 (one head per 128-column tile)
+      bool fz = !pg_ && head_dim == 128 && fused_env();
+      const int64_t H = embed_.size(1);
+      for (size_t l = 0; l < L && fz; ++l) {
+        const at::Tensor* ws[3] = {&qkv_w_[l], &o_w_[l], &down_w_[l]};
+        for (auto* w : ws) {
+          const int64_t S = decode_gemm_cmb_splits(w->size(0), w->size(1));
+          fz = fz && S > 0 && decode_gemm_supported(*w, false);
+          if (S > 0) wsz = std::max(wsz, S * kDgemmMaxM * w->size(0) * 4);
+        }
+        fz = fz && decode_gemm_supported(gate_up_w_[l], true) && o_w_[l].size(0) == H && down_w_[l].size(0) == H;
+      }
       dg_ws_ = at::empty({(wsz + 3) / 4}, dev.dtype(at::kFloat));
       dg_tickets_ = at::zeros({std::max<int64_t>(2, 2 * (fmax / 128))}, dev.dtype(at::kInt));
+      if (fz) {
+        auto bf = dev.dtype(at::kBFloat16);
+        y_in_ = at::zeros({kDgemmMaxM, H}, bf);
+        y_post_ = at::zeros({kDgemmMaxM, H}, bf);
+        ss_in_ = at::zeros({kDgemmMaxM, H / 128}, dev.dtype(at::kFloat));
+        ss_post_ = at::zeros({kDgemmMaxM, H / 128}, dev.dtype(at::kFloat));
+        ss0_ = at::zeros({kDgemmMaxM, 1}, dev.dtype(at::kFloat));
+        const int64_t maxt = std::max<int64_t>(qkv_w_[0].size(0), H) / 128;
+        cnt_qkv_ = at::zeros({maxt}, dev.dtype(at::kLong));
+        cnt_o_ = at::zeros({maxt}, dev.dtype(at::kLong));
+        cnt_down_ = at::zeros({maxt}, dev.dtype(at::kLong));
+      }
     }
   }
 
@@ -197,7 +231,9 @@ class LlamaRunner {
   // half-exchange of gemm_decode.hip timed out; the one-shot all-reduce's sticky timeout
   // word.  The step executor copies them next to every step's results and fails the step.
   std::vector<const int*> status_ptrs() const {
-    std::vector<const int*> v{status_.data_ptr<int>()};
+    // [0] gate_up half exchange, [1] combine rendezvous (forward_dgemm), then the
+    // one-shot all-reduce's word
+    std::vector<const int*> v{status_.data_ptr<int>(), status_.data_ptr<int>() + 1};
     if (oneshot_) v.push_back(oneshot_allreduce_err(oneshot_));
     return v;
   }
@@ -236,6 +272,8 @@ class LlamaRunner {
                           const at::Tensor& q_len, const at::Tensor& ctx_len, const at::Tensor& tiles,
                           const c10::optional<at::Tensor>& rows, bool gather_logits = true) {
     const int64_t T = ids.size(0);
+    if (num_prefill == 0 && num_decode == T && fused_ready(T))
+      return forward_dgemm(ids, pos, slots, d_bt, d_ctx, nsplit, bps, ws, rows);
     at::Tensor h = embed(ids);
     at::Tensor residual = h;
     at::Tensor x = at::empty_like(h);
@@ -448,6 +486,41 @@ class LlamaRunner {
     return lg;
   }
 
+  // Decode-only steps of 129..256 rows at TP = 1: the norm-deferred layer of
+  // gemm_decode.hip (DgArgs).  Per layer 5 launches -- qkv (+ in-launch split-K combine,
+  // 1/rms, RoPE, KV write), attention, o (+ combine, residual add, y = h * g, row sums of
+  // h^2), gate_up (+ 1/rms, SwiGLU), down (+ combine ...) -- instead of 8.  The residual
+  // stream h is updated in place; y_in_ / y_post_ hold bf16(h * g) for the next GEMM and
+  // ss_in_ / ss_post_ the per-tile sums of h^2 its epilogue turns into 1/rms.
+  at::Tensor forward_dgemm(const at::Tensor& ids, const at::Tensor& pos, const at::Tensor& slots,
+                           const at::Tensor& d_bt, const at::Tensor& d_ctx, int64_t nsplit, int64_t bps,
+                           const at::Tensor& ws, const c10::optional<at::Tensor>& rows) {
+    const int64_t T = ids.size(0);
+    at::Tensor h = embed(ids).contiguous();
+    const int64_t L = qkv_w_.size();
+    at::Tensor y = y_in_.narrow(0, 0, T), y2 = y_post_.narrow(0, 0, T);
+    at::Tensor ss_in = ss_in_.narrow(0, 0, T), ss_post = ss_post_.narrow(0, 0, T), ss0 = ss0_.narrow(0, 0, T);
+    at::Tensor err = status_.narrow(0, 1, 1);
+    rms_prep(y, ss0, h, in_norm_[0]);
+    for (int64_t l = 0; l < L; ++l) {
+      at::Tensor qkv = at::empty({T, qkv_w_[l].size(0)}, h.options());
+      decode_gemm_qkv_cmb(qkv, y, qkv_w_[l], dg_ws_, cnt_qkv_, l == 0 ? ss0 : ss_in, eps_, pos, cos_sin_, slots,
+                          kc_[l], vc_[l], hq_, hkv_, err);
+      at::Tensor attn = at::empty({T, hq_ * d_}, h.options());
+      paged_decode_attention(attn, qkv.narrow(1, 0, hq_ * d_), kc_[l], vc_[l], d_bt, d_ctx, scale_, nsplit, bps, ws);
+      decode_gemm_res(y2, attn, o_w_[l], dg_ws_, cnt_o_, h, post_norm_[l], ss_post, err);
+      at::Tensor a = at::empty({T, gate_up_w_[l].size(0) / 2}, h.options());
+      decode_gemm_silu_r(a, y2, gate_up_w_[l], ss_post, eps_);
+      decode_gemm_res(y, a, down_w_[l], dg_ws_, cnt_down_, h, l + 1 < L ? in_norm_[l + 1] : final_norm_, ss_in, err);
+    }
+    at::Tensor x = at::empty_like(h);
+    rows_rms_scale(x, y, ss_in, eps_);
+    at::Tensor sel = rows.has_value() ? x.index_select(0, *rows) : x;
+    at::Tensor lg = lm_head(sel);
+    if (lg.size(1) != vocab_) lg = lg.narrow(1, 0, vocab_).contiguous();
+    return lg;
+  }
+
   at::Tensor forward(at::Tensor ids, at::Tensor pos, at::Tensor slots, int64_t num_decode,
                      c10::optional<at::Tensor> d_bt, c10::optional<at::Tensor> d_ctx, int64_t nsplit, int64_t bps,
                      c10::optional<at::Tensor> ws, int64_t num_prefill, c10::optional<at::Tensor> p_bt,
@@ -481,6 +554,18 @@ class LlamaRunner {
     h.masked_fill_(mask.unsqueeze(1), 0);
     all_reduce(h);
     return h;
+  }
+
+  // LS_DGEMM_FUSED=0: the unfused 129..256-row decode path (split-K reduce kernels)
+  static bool fused_env() {
+    static const bool on = [] {
+      const char* e = getenv("LS_DGEMM_FUSED");
+      return e == nullptr || e[0] != '0';
+    }();
+    return on;
+  }
+  bool fused_ready(int64_t T) const {
+    return cnt_qkv_.defined() && dgemm_enabled() && T >= dgemm_min_t() && T <= kDgemmMaxM;
   }
 
   static bool gemv_enabled() {
@@ -578,6 +663,7 @@ class LlamaRunner {
 
   bool f32_head_ = true;
   at::Tensor status_, dg_ws_, dg_tickets_;
+  at::Tensor y_in_, y_post_, ss_in_, ss_post_, ss0_, cnt_qkv_, cnt_o_, cnt_down_;   // forward_dgemm
   at::Tensor embed_;
   std::vector<at::Tensor> qkv_w_, o_w_, gate_up_w_, down_w_, in_norm_, post_norm_;
   at::Tensor final_norm_, lm_head_;
@@ -1104,10 +1190,25 @@ class StepExecutor {
     for (size_t k = 0; k < status_ptrs_.size(); ++k)
       HIP_OK(hipMemcpyAsync(dst + k, status_ptrs_[k], sizeof(int), hipMemcpyDeviceToHost, stream()));
   }
-  static void check_status(const int* st) {
-    TORCH_CHECK(st[0] == 0, "decode GEMM: the gate_up K-half exchange timed out (partner workgroup never "
-                "published); this step's results are invalid");
-    for (int k = 1; k < kStatusWords; ++k)
+  void check_status(const int* st) {
+    if (st[1] != 0) {
+      // per step, like [0] below: clear and report once
+      HIP_OK(hipMemsetAsync(const_cast<int*>(status_ptrs_[1]), 0, sizeof(int), stream()));
+      TORCH_CHECK(false, "decode GEMM: a split-K combine rendezvous timed out (a K-slice workgroup never "
+                  "arrived); this step's results are invalid");
+    }
+    if (st[0] != 0) {
+      // the gate_up exchange word is per step: clear it (in stream order, after this
+      // step) so the failed step is reported once and later steps run normally -- the
+      // exchange's monotonic tickets stay consistent after a timeout.  The one-shot
+      // all-reduce words below stay sticky: a peer that never arrived desynchronises
+      // its epochs for good.
+      if (!status_ptrs_.empty())
+        HIP_OK(hipMemsetAsync(const_cast<int*>(status_ptrs_[0]), 0, sizeof(int), stream()));
+      TORCH_CHECK(false, "decode GEMM: the gate_up K-half exchange timed out (partner workgroup never "
+                  "published); this step's results are invalid");
+    }
+    for (int k = 2; k < kStatusWords; ++k)
       TORCH_CHECK(st[k] == 0, "one-shot all-reduce timed out: a tensor-parallel peer never arrived; this step's "
                   "results are invalid");
   }

@@ -122,8 +122,15 @@ class LocalApplicationRunner:
         self.stop()
 
     # ------------------------------------------------------------------ topic helpers (tests / CLI)
+    def _conn(self, topic: str, producer: bool) -> Dict[str, Any]:
+        """The plan topic's connection configuration (schemas / serde), as an agent gets it."""
+        t = self.plan.get_topic(topic)
+        if t is None:
+            return {"topic": topic}
+        return t.producer_configuration() if producer else t.consumer_configuration()
+
     def producer(self, topic: str):
-        p = self.topic_runtime.create_producer("local-client", self.streaming_cluster, {"topic": topic})
+        p = self.topic_runtime.create_producer("local-client", self.streaming_cluster, self._conn(topic, True))
         p.start()
         return p
 
@@ -132,7 +139,7 @@ class LocalApplicationRunner:
         self.producer(topic).write(SimpleRecord.of(key, value, hs)).result(10)
 
     def reader(self, topic: str, position: TopicOffsetPosition = TopicOffsetPosition.EARLIEST):
-        r = self.topic_runtime.create_reader(self.streaming_cluster, {"topic": topic}, position)
+        r = self.topic_runtime.create_reader(self.streaming_cluster, self._conn(topic, False), position)
         r.start()
         return r
 

@@ -11,9 +11,16 @@ Parity:
 * consumer (``KafkaConsumerWrapper.java``): poll -> records; out-of-order commit
   tracking advancing only the contiguous prefix per partition; a failed commit is
   raised by the next read().
-* producer (``KafkaProducerWrapper.java:58-270``): key/value/header serialisation by
-  Python type -- str -> UTF-8, bytes as is, dict/list -> JSON, bool/int/float -> their
-  string form; the consumer deserialises UTF-8 back to str (bytes when not UTF-8).
+* producer / consumer serde (``KafkaProducerWrapper.java:57-270``, ``KafkaTopic.java:90-126``,
+  ``serde.py``): topic ``keySchema`` / ``valueSchema`` force String / ByteArray / Avro
+  (Confluent wire format, schemas registered in the schema registry); without a schema
+  the Java type of each key / value / header picks the Kafka binary serializer
+  (Boolean 1 B, Short / Integer / Long 2 / 4 / 8 B, Float / Double IEEE-754, UUID, JSON
+  for maps and lists, Avro for AvroRecord values); consumers use StringDeserializer
+  (bytes when not UTF-8) unless the schema says bytes / avro.
+* schema registry (``KafkaTopicConnectionsRuntime.java:232-325``): on deploy, Avro key /
+  value schemas of ``create-if-not-exists`` topics are registered under
+  ``<topic>-key`` / ``<topic>-value`` at ``admin.schema.registry.url``.
 * reader (``KafkaReaderWrapper.java``): assign-all, latest / earliest / absolute
   (``{partition: offset}`` JSON, base64 in the gateway API).
 * admin (``KafkaTopicConnectionsRuntime.java:166-291``): create-if-not-exists topics
@@ -35,7 +42,7 @@ from ...api.record import Header, Record
 from ...api.topics import (TopicAdmin, TopicConnectionsRuntime, TopicConnectionsRuntimeRegistry, TopicConsumer,
                            TopicOffsetPosition, TopicProducer, TopicReader, TopicReadResult, decode_offsets,
                            encode_offsets)
-from . import codecs
+from . import codecs, serde
 from ...utils import fastjson
 from .client import GroupConsumer, KafkaClient, PartitionReader, Producer
 from .security import SecurityConfig
@@ -44,20 +51,12 @@ log = logging.getLogger(__name__)
 
 
 def serialize(v: Any) -> Optional[bytes]:
-    if v is None:
-        return None
-    if isinstance(v, bytes):
-        return v
-    if isinstance(v, str):
-        return v.encode()
-    if isinstance(v, bool):
-        return b"true" if v else b"false"
-    if isinstance(v, (dict, list)):
-        return fastjson.dumps(v).encode()
-    return str(v).encode()
+    """Reflection serialisation (no topic schema): serde.serialize_typed without Avro."""
+    return serde.serialize_typed(v)
 
 
 def deserialize(b: Optional[bytes]) -> Any:
+    """StringDeserializer (bytes when the payload is not UTF-8)."""
     if b is None:
         return None
     try:
@@ -66,13 +65,35 @@ def deserialize(b: Optional[bytes]) -> Any:
         return b
 
 
+_STRING = serde.ValueDeserializer(serde.STRING_DESER, None)
+
+
 class KafkaRecord(Record):
     __slots__ = ("topic", "partition", "offset")
 
-    def __init__(self, topic: str, partition: int, offset: int, ts: int, key, value, headers):
-        super().__init__(deserialize(key), deserialize(value), topic, ts,
+    def __init__(self, topic: str, partition: int, offset: int, ts: int, key, value, headers,
+                 kdes=None, vdes=None):
+        super().__init__((kdes or deserialize)(key), (vdes or deserialize)(value), topic, ts,
                          [Header(k, deserialize(v)) for k, v in headers])
         self.topic, self.partition, self.offset = topic, partition, offset
+
+
+def _serdes(configuration: Dict[str, Any], registry_cfgs, topic: str, producer: bool):
+    """(key, value) serializers or deserializers for a consumer / producer configuration
+    (the KafkaTopic configuration: key/value (de)serializer class + the topic schemas)."""
+    ks, vs = configuration.get("keySchema"), configuration.get("valueSchema")
+    registry = None
+    if (ks and ks.get("type") == "avro") or (vs and vs.get("type") == "avro") or producer:
+        registry = serde.SchemaRegistryClient.from_config(*registry_cfgs)
+    if producer:
+        kcls = configuration.get("key.serializer") or serde.serializer_for_schema(ks)
+        vcls = configuration.get("value.serializer") or serde.serializer_for_schema(vs)
+        auto = str(configuration.get("auto.register.schemas", "true")).lower() != "false"
+        return (serde.ValueSerializer(kcls, serde.AvroSerializer(registry, topic, True, serde.topic_schema(ks), auto)),
+                serde.ValueSerializer(vcls, serde.AvroSerializer(registry, topic, False, serde.topic_schema(vs), auto)))
+    kcls = configuration.get("key.deserializer") or serde.deserializer_for_schema(ks)
+    vcls = configuration.get("value.deserializer") or serde.deserializer_for_schema(vs)
+    return serde.ValueDeserializer(kcls, registry), serde.ValueDeserializer(vcls, registry)
 
 
 def _bootstrap(streaming_cluster) -> str:
@@ -86,10 +107,11 @@ def _bootstrap(streaming_cluster) -> str:
 
 class KafkaConsumer(TopicConsumer):
     def __init__(self, bootstrap: str, topic: str, group: str, reset: str, max_records: int, poll_ms: int,
-                 security: Optional[SecurityConfig] = None):
+                 security: Optional[SecurityConfig] = None, deserializers=None):
         self.client = KafkaClient(bootstrap, client_id=f"consumer-{group}", security=security)
         self.c = GroupConsumer(self.client, topic, group, reset, max_poll_records=max_records)
         self.topic, self.group, self.poll_ms = topic, group, poll_ms
+        self.kdes, self.vdes = deserializers or (None, None)
         self._out = 0
 
     def start(self) -> None:
@@ -101,7 +123,8 @@ class KafkaConsumer(TopicConsumer):
 
     def read(self) -> List[Record]:
         recs = self.c.poll(self.poll_ms)
-        out = [KafkaRecord(self.topic, p, off, ts, k, v, hs) for p, off, ts, k, v, hs in recs]
+        kd, vd = self.kdes, self.vdes
+        out = [KafkaRecord(self.topic, p, off, ts, k, v, hs, kd, vd) for p, off, ts, k, v, hs in recs]
         self._out += len(out)
         return out
 
@@ -127,8 +150,10 @@ class KafkaProducer(TopicProducer):
     MAX_BATCH_RECORDS = 1000
     MAX_BATCH_BYTES = 900 * 1024   # under the broker's default message.max.bytes (1 MiB)
 
-    def __init__(self, bootstrap: str, topic: str, security: Optional[SecurityConfig] = None, codec: int = 0):
+    def __init__(self, bootstrap: str, topic: str, security: Optional[SecurityConfig] = None, codec: int = 0,
+                 serializers=None):
         self.client = KafkaClient(bootstrap, client_id=f"producer-{topic}", security=security)
+        self.kser, self.vser = serializers or (serialize, serialize)
         self.p = Producer(self.client, topic, codec=codec)
         self.topic = topic
         self._in = 0
@@ -150,7 +175,7 @@ class KafkaProducer(TopicProducer):
         f: Future = Future()
         try:
             hs = [(h.key, serialize(h.value)) for h in record.headers()]
-            item = (serialize(record.key()), serialize(record.value()), hs,
+            item = (self.kser(record.key()), self.vser(record.value()), hs,
                     int(record.timestamp() or time.time() * 1000))
         except Exception as e:  # noqa: BLE001
             f.set_exception(e)
@@ -207,9 +232,10 @@ class KafkaProducer(TopicProducer):
 
 class KafkaReader(TopicReader):
     def __init__(self, bootstrap: str, topic: str, position: TopicOffsetPosition, poll_ms: int = 500,
-                 security: Optional[SecurityConfig] = None):
+                 security: Optional[SecurityConfig] = None, deserializers=None):
         self.client = KafkaClient(bootstrap, client_id=f"reader-{topic}", security=security)
         self.topic, self.position, self.poll_ms = topic, position, poll_ms
+        self.kdes, self.vdes = deserializers or (None, None)
         self.r: Optional[PartitionReader] = None
 
     def start(self) -> None:
@@ -223,7 +249,8 @@ class KafkaReader(TopicReader):
 
     def read(self) -> TopicReadResult:
         recs = self.r.read(self.poll_ms)
-        out = [KafkaRecord(self.topic, p, off, ts, k, v, hs) for p, off, ts, k, v, hs in recs]
+        kd, vd = self.kdes, self.vdes
+        out = [KafkaRecord(self.topic, p, off, ts, k, v, hs, kd, vd) for p, off, ts, k, v, hs in recs]
         return TopicReadResult(out, encode_offsets(dict(self.r.positions)))
 
 
@@ -246,8 +273,24 @@ class KafkaTopicConnectionsRuntime(TopicConnectionsRuntime):
                 if t.creation_mode == "create-if-not-exists":
                     rf = int((t.options or {}).get("replication-factor", 1))
                     client.create_topic(t.name, max(1, t.partitions), rf, t.config or {})
+                    self._enforce_schema(t)
         finally:
             client.close()
+
+    def _enforce_schema(self, t) -> None:
+        """Register the topic's Avro key / value schemas (TopicNameStrategy subjects),
+        KafkaTopicConnectionsRuntime.java:232-281; a missing registry url is an error
+        only when a topic actually declares an Avro schema."""
+        d = getattr(t, "definition", None)
+        pairs = [(True, getattr(d, "key_schema", None)), (False, getattr(d, "value_schema", None))]
+        pairs = [(k, s) for k, s in pairs if s is not None and s.type == "avro" and s.schema]
+        if not pairs:
+            return
+        reg = serde.SchemaRegistryClient.from_config(self.admin_cfg)
+        if reg is None:
+            raise ValueError("Missing 'schema.registry.url' property in streaming cluster configuration admin section")
+        for is_key, s in pairs:
+            reg.register(serde.subject_name(t.name, is_key), s.schema)
 
     def delete(self, plan) -> None:
         client = KafkaClient(self.bootstrap, client_id="langstream-admin", security=self.security)
@@ -263,15 +306,18 @@ class KafkaTopicConnectionsRuntime(TopicConnectionsRuntime):
         return KafkaConsumer(self.bootstrap, configuration["topic"], group,
                              str(configuration.get("auto.offset.reset", "earliest")),
                              int(configuration.get("max.poll.records", 500)),
-                             int(configuration.get("poll.timeout.ms", 500)), self.consumer_security)
+                             int(configuration.get("poll.timeout.ms", 500)), self.consumer_security,
+                             _serdes(configuration, (self.admin_cfg, self.consumer_cfg), configuration["topic"], False))
 
     def create_producer(self, agent_id, streaming_cluster, configuration) -> TopicProducer:
         ctype = configuration.get("compression.type", self.producer_cfg.get("compression.type"))
-        return KafkaProducer(self.bootstrap, configuration["topic"], self.producer_security, codecs.codec_of(ctype))
+        return KafkaProducer(self.bootstrap, configuration["topic"], self.producer_security, codecs.codec_of(ctype),
+                             _serdes(configuration, (self.admin_cfg, self.producer_cfg), configuration["topic"], True))
 
     def create_reader(self, streaming_cluster, configuration, initial_position) -> TopicReader:
         return KafkaReader(self.bootstrap, configuration["topic"], initial_position,
-                           int(configuration.get("poll.timeout.ms", 500)), self.consumer_security)
+                           int(configuration.get("poll.timeout.ms", 500)), self.consumer_security,
+                           _serdes(configuration, (self.admin_cfg, self.consumer_cfg), configuration["topic"], False))
 
     def create_topic_admin(self, agent_id, streaming_cluster, configuration) -> TopicAdmin:
         return TopicAdmin()

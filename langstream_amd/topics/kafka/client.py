@@ -404,12 +404,17 @@ class GroupConsumer:
             raise e
         if self._need_rejoin:
             self._join()
+        # max.poll.records caps ONE poll across all partitions (KafkaConsumer semantics);
+        # what a fetch returned beyond it waits in _buf, in per-partition order
         with self._lock:
             if any(self._buf.values()):
                 out = []
                 for p, recs in self._buf.items():
-                    out.extend((p,) + r for r in recs[: self.max_poll])
-                    self._buf[p] = recs[self.max_poll:]
+                    room = self.max_poll - len(out)
+                    if room <= 0:
+                        break
+                    out.extend((p,) + r for r in recs[:room])
+                    self._buf[p] = recs[room:]
                 return out
             pos = dict(self.positions)
         if not pos:
@@ -421,9 +426,10 @@ class GroupConsumer:
             for p, (_hw, recs) in res.items():
                 if p not in self.positions or self.positions[p] != pos.get(p):
                     continue   # reassigned or moved while the fetch was in flight
-                out.extend((p,) + r for r in recs[: self.max_poll])
-                if len(recs) > self.max_poll:
-                    self._buf[p] = list(recs[self.max_poll:])
+                room = max(0, self.max_poll - len(out))
+                out.extend((p,) + r for r in recs[:room])
+                if len(recs) > room:
+                    self._buf[p] = list(recs[room:])
                 if recs:
                     self.positions[p] = recs[-1][0] + 1
         return out

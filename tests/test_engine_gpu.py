@@ -341,3 +341,23 @@ def test_native_executor_tp2_two_ranks_one_gpu():
     assert stats["decode_steps"] > 0
     for a, b in zip(got, ref):
         _same_or_near_tie(a, b)
+
+
+def test_norm_deferred_decode_layer_matches_python_executor():
+    """Decode batches of 129..256 rows run the norm-deferred layer (LlamaRunner::
+    forward_dgemm: in-launch split-K combines, 1/rms in the consumer epilogues): greedy
+    tokens against the Python executor's op-by-op path over 160 concurrent sequences."""
+    from langstream_amd.engine.arena import PyStepExecutor
+    from langstream_amd.engine.llm_engine import NSLOTS
+    cfg = PRESETS["llama-small"]
+    model = LlamaModel(cfg, device="cuda")
+    prompts = [list(range(3 + i % 50, 3 + i % 50 + 5 + i % 37)) for i in range(160)]
+    sp = SamplingParams(max_tokens=6, temperature=0.0, ignore_eos=True)
+    e1 = LLMEngine(model, None, num_blocks=512, max_model_len=512, max_batch=256)
+    out1 = _run_tops(e1, prompts, sp)
+    assert e1.stats["graph_steps"] > 0
+    e2 = LLMEngine(model, None, num_blocks=512, max_model_len=512, max_batch=256, use_graphs=False)
+    e2.exec = PyStepExecutor(model, e2.kv_caches, e2.layout, NSLOTS, e2.nsplit, e2.bps, e2.device)
+    out2 = _run_tops(e2, prompts, SamplingParams(max_tokens=6, temperature=0.0, ignore_eos=True, logprobs=2))
+    for a, b in zip(out1, out2):
+        _same_or_near_tie(a, b)

@@ -901,3 +901,121 @@ def test_decode_gemm_f32_lm_head(M, bn):
     ops.hip().decode_gemm_f32(out, x, w, bn)
     ref = x.float() @ w.float().t()
     assert (out - ref).abs().max().item() < 2e-3 * ref.abs().max().item() + 1e-3
+
+
+# ------------------------------------------------------------------ norm-deferred decode layer
+# gemm_decode.hip DgArgs: split-K combine inside the launch (rendezvous of a tile's K
+# slices), y = bf16(h * g) + per-tile sums of h^2 from the producer, 1/rms applied by the
+# consumer's epilogue.  Repeated calls exercise the monotonic 64-bit counters.
+def _rms_ref(h, g, eps=1e-5):
+    return h * torch.rsqrt(h.pow(2).mean(-1, keepdim=True) + eps) * g
+
+
+@pytest.mark.parametrize("M", [129, 200, 256])
+@pytest.mark.parametrize("name,N,K", [("o8b", 4096, 4096), ("down8b", 4096, 14336), ("o70b", 8192, 8192)])
+def test_decode_gemm_res_combine(M, name, N, K):
+    torch.manual_seed(M + N + K)
+    S = ops.hip().decode_gemm_cmb_splits(N, K)
+    assert S > 1 and (N // 128) * S <= 256
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=DEV) / K ** 0.5).to(torch.bfloat16)
+    g = (1 + 0.1 * torch.randn(N, device=DEV)).to(torch.bfloat16)
+    cnt = torch.zeros(N // 128, device=DEV, dtype=torch.int64)
+    err = torch.zeros(1, device=DEV, dtype=torch.int32)
+    ws = torch.empty(S * M * N, device=DEV, dtype=torch.float32)
+    res = torch.randn(M, N, device=DEV).to(torch.bfloat16)
+    for it in range(3):
+        h_exp = (res.float() + x.float() @ w.float().t()).to(torch.bfloat16)
+        y = torch.full((M, N), float("nan"), device=DEV, dtype=torch.bfloat16)
+        ss = torch.full((M, N // 128), float("nan"), device=DEV)
+        ops.hip().decode_gemm_res(y, x, w, ws, cnt, res, g, ss, err)
+        torch.cuda.synchronize()
+        _close(res, h_exp.float().cpu(), 0.03, 0.03, f"residual it{it}")
+        hf = res.float()
+        _close(y, (hf * g.float()).cpu(), 0.01, 0.01, "y")
+        assert torch.allclose(ss.sum(1), hf.pow(2).sum(1), rtol=1e-3), "sumsq"
+        assert torch.allclose(ss[:, 3], hf[:, 384:512].pow(2).sum(1), rtol=1e-3)
+    assert err.item() == 0 and int(cnt[0]) == 3 * S
+
+
+@pytest.mark.parametrize("M", [129, 256])
+@pytest.mark.parametrize("F,K", [(14336, 4096), (3584, 1024)])
+def test_decode_gemm_silu_r(M, F, K):
+    """gate_up on y = h * g with the producer's per-tile sums of h^2: silu(r g) * (r u)
+    equals SwiGLU of the RMS-normed input."""
+    torch.manual_seed(M + F)
+    h = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    gnorm = (1 + 0.1 * torch.randn(K, device=DEV)).to(torch.bfloat16)
+    w = (torch.randn(2 * F, K, device=DEV) / K ** 0.5).to(torch.bfloat16)
+    y = (h.float() * gnorm.float()).to(torch.bfloat16)
+    parts = h.float().pow(2).view(M, K // 128, 128).sum(-1).contiguous()
+    out = torch.full((M, F), float("nan"), device=DEV, dtype=torch.bfloat16)
+    ops.hip().decode_gemm_silu_r(out, y, w, parts, 1e-5)
+    xn = _rms_ref(h.float(), gnorm.float())
+    gu = xn @ w.float().t()
+    _close(out, torch.nn.functional.silu(gu[:, :F]) * gu[:, F:], 0.03, 0.03)
+
+
+@pytest.mark.parametrize("M", [129, 256])
+@pytest.mark.parametrize("Hq,Hkv,K", [(32, 8, 4096), (64, 8, 8192)])   # Llama-3-8B; Llama-3-70B at TP=1
+def test_decode_gemm_qkv_combine(M, Hq, Hkv, K):
+    """qkv on y = h * g: in-launch combine, 1/rms from the producer's partials, RoPE,
+    paged K / V write (slot -1 rows not cached), against fp32 rmsnorm -> projection ->
+    rotation."""
+    torch.manual_seed(M + Hq + K)
+    D, BS = 128, 64
+    N = (Hq + 2 * Hkv) * D
+    S = ops.hip().decode_gemm_cmb_splits(N, K)
+    assert S >= 1
+    h = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    gnorm = (1 + 0.1 * torch.randn(K, device=DEV)).to(torch.bfloat16)
+    y = (h.float() * gnorm.float()).to(torch.bfloat16)
+    parts = h.float().pow(2).view(M, K // 128, 128).sum(-1).contiguous()
+    w = (torch.randn(N, K, device=DEV) / K ** 0.5).to(torch.bfloat16)
+    pos = torch.randint(0, 4000, (M,), device=DEV, dtype=torch.int32)
+    half = torch.arange(0, D // 2, dtype=torch.float64)
+    inv = 1.0 / (500000.0 ** (2 * half / D))
+    ang = torch.arange(0, 4096, dtype=torch.float64)[:, None] * inv[None, :]
+    cos_sin = torch.cat([ang.cos(), ang.sin()], 1).float().to(DEV)
+    NB = 2 * M
+    kc = torch.zeros(NB, Hkv, BS, D, device=DEV, dtype=torch.bfloat16)
+    vc = torch.zeros(NB, Hkv, BS // 8, D, 8, device=DEV, dtype=torch.bfloat16)
+    slots = torch.randperm(NB * BS, device=DEV)[:M].long()
+    slots[5] = -1
+    cnt = torch.zeros(N // 128, device=DEV, dtype=torch.int64)
+    err = torch.zeros(1, device=DEV, dtype=torch.int32)
+    ws = torch.empty(S * M * N, device=DEV, dtype=torch.float32)
+    xn = _rms_ref(h.float(), gnorm.float())
+    yp = (xn @ w.float().t()).view(M, Hq + 2 * Hkv, D)
+    cs = cos_sin[pos.long()]
+    co, si = cs[:, None, : D // 2], cs[:, None, D // 2:]
+    a, b = yp[:, : Hq + Hkv, : D // 2], yp[:, : Hq + Hkv, D // 2:]
+    exp = torch.cat([torch.cat([a * co - b * si, b * co + a * si], -1), yp[:, Hq + Hkv:]], 1)
+    for _ in range(2):
+        qkv = torch.full((M, N), float("nan"), device=DEV, dtype=torch.bfloat16)
+        ops.hip().decode_gemm_qkv_cmb(qkv, y, w, ws, cnt, parts, 1e-5, pos, cos_sin, slots, kc, vc, Hq, Hkv, err)
+        _close(qkv.view(M, -1, D), exp, 0.03, 0.03, "qkv")
+    got = qkv.view(M, -1, D)
+    for m in range(0, M, 7):
+        s = int(slots[m])
+        if s < 0:
+            continue
+        blk, off = s // BS, s % BS
+        assert torch.equal(kc[blk, :, off, :], got[m, Hq: Hq + Hkv]), m
+        assert torch.equal(vc[blk, :, off // 8, :, off % 8], got[m, Hq + Hkv:]), m
+    assert err.item() == 0
+
+
+def test_rms_prep_and_rows_rms_scale():
+    torch.manual_seed(3)
+    M, N = 200, 4096
+    h = torch.randn(M, N, device=DEV).to(torch.bfloat16)
+    g = (1 + 0.1 * torch.randn(N, device=DEV)).to(torch.bfloat16)
+    y = torch.empty_like(h)
+    ss = torch.empty(M, 1, device=DEV)
+    ops.hip().rms_prep(y, ss, h, g)
+    assert torch.allclose(ss[:, 0], h.float().pow(2).sum(1), rtol=1e-4)
+    _close(y, (h.float() * g.float()).cpu(), 0.01, 0.01)
+    out = torch.empty_like(h)
+    ops.hip().rows_rms_scale(out, y, ss, 1e-5)
+    _close(out, _rms_ref(h.float(), g.float()).cpu(), 0.02, 0.02)

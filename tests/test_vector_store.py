@@ -98,6 +98,29 @@ def test_registry_restores_collection_after_restart(tmp_path):
         VectorStoreRegistry.persist_dir = None
 
 
+def test_query_agent_created_before_sink_becomes_durable(tmp_path, caplog):
+    """a collection created (empty, non-persistent) by a query agent before the
+    sink configures persistence is attached to the WAL when persistence is configured;
+    one that already holds rows is reported as not durable."""
+    VectorStoreRegistry.reset()
+    VectorStoreRegistry.persist_dir = None
+    try:
+        q = VectorStoreRegistry.get("docs", 8, device="cpu")           # the query agent, first
+        early = VectorStoreRegistry.get("early", 8, device="cpu")
+        early.upsert(["x"], [[1.0] * 8])
+        assert not q.persistent
+        with caplog.at_level("WARNING"):
+            VectorStoreRegistry.configure(persist_dir=str(tmp_path))   # the sink's set_context
+        assert q.persistent and not early.persistent
+        assert any("early" in r.getMessage() and "NOT durable" in r.getMessage() for r in caplog.records)
+        q.upsert(["a"], [[1.0] * 8], [{"text": "kept"}])
+        VectorStoreRegistry.reset()                                      # "process restart"
+        assert VectorStoreRegistry.get("docs", device="cpu").get("a") == {"text": "kept"}
+    finally:
+        VectorStoreRegistry.reset()
+        VectorStoreRegistry.persist_dir = None
+
+
 WORKER = textwrap.dedent('''
     import sys, time
     sys.path.insert(0, {root!r})
