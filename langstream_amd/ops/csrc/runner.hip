@@ -238,21 +238,25 @@ class LlamaRunner {
     return v;
   }
 
-  // LM head with f32 OUTPUT straight from the GEMM (hipBLASLt bf16 x bf16 -> f32): a bf16
-  // logit tensor quantises logits to 2^-7 relative steps (0.125 at |logit| ~ 20), which
-  // ties near-equal tokens and coarsens the log-probs FLARE and `logprobs` consume.
+  // LM head with f32 OUTPUT straight from the GEMM (bf16 x bf16 -> f32): a bf16 logit
+  // tensor quantises logits to 2^-7 relative steps (0.125 at |logit| ~ 20), which ties
+  // near-equal tokens and coarsens the log-probs FLARE and `logprobs` consume.  Every row
+  // count runs on the 256-row decode GEMM's f32 epilogue (gemm_decode.hip), in blocks of
+  // 256 rows; only shapes it cannot take (vocab % 128, hidden % 64) fall back to the
+  // library GEMM (LS_DGEMM_HEAD=0 forces the library).
   at::Tensor lm_head(const at::Tensor& x) {
-    // decode batches of 129..256 rows: the 256-row decode GEMM with its f32 epilogue
-    // (LS_DGEMM_HEAD=0: hipBLASLt)
     static const bool dg_head = [] {
       const char* e = getenv("LS_DGEMM_HEAD");
       return e == nullptr || e[0] != '0';
     }();
     const int64_t R = x.size(0);
-    if (dg_head && dgemm_enabled() && R >= dgemm_min_t() && decode_gemm_f32_supported(lm_head_, R) &&
-        x.stride(1) == 1 && x.is_contiguous()) {
+    if (dg_head && dgemm_enabled() && R >= 1 && decode_gemm_f32_supported(lm_head_, std::min<int64_t>(R, kDgemmMaxM))) {
+      at::Tensor xc = x.contiguous();
       at::Tensor out = at::empty({R, lm_head_.size(0)}, x.options().dtype(at::kFloat));
-      decode_gemm_f32(out, x, lm_head_, 0);
+      for (int64_t r0 = 0; r0 < R; r0 += kDgemmMaxM) {
+        const int64_t n = std::min<int64_t>(kDgemmMaxM, R - r0);
+        decode_gemm_f32(out.narrow(0, r0, n), xc.narrow(0, r0, n), lm_head_, 0);
+      }
       return out;
     }
     if (f32_head_) {
@@ -263,6 +267,44 @@ class LlamaRunner {
       }
     }
     return at::linear(x, lm_head_).to(at::kFloat);
+  }
+
+  // x . w^T on the hand-written kernels for any row count: the ping-pong prefill GEMM
+  // (256 x 256 tiles) from LS_PGEMM_MIN_T rows, the 256-row decode GEMM (split-K, in
+  // blocks of 256 rows) below that.  The library GEMM remains only for shapes neither
+  // kernel takes (tiny test models: N % 128 or K % 64 != 0) or LS_PGEMM=lib.
+  at::Tensor proj(const at::Tensor& x, const at::Tensor& w) {
+    const int64_t T = x.size(0);
+    at::Tensor out = at::empty({T, w.size(0)}, x.options());
+    if (pgemm(T, w, false)) {
+      gemm_prefill(out, x, w, false, -1);
+    } else if (dgemm_blocks_ok(w, false) && x.stride(1) == 1) {
+      for (int64_t r0 = 0; r0 < T; r0 += kDgemmMaxM) {
+        const int64_t n = std::min<int64_t>(kDgemmMaxM, T - r0);
+        decode_gemm(out.narrow(0, r0, n), x.narrow(0, r0, n), w, dg_ws_, c10::nullopt, c10::nullopt, eps_, 0, 0);
+      }
+    } else {
+      out = at::linear(x, w);
+    }
+    return out;
+  }
+
+  // silu(x . w[:F]^T) * (x . w[F:]^T) for any row count (same routing as proj)
+  at::Tensor proj_silu(const at::Tensor& x, const at::Tensor& w) {
+    const int64_t T = x.size(0);
+    at::Tensor a = at::empty({T, w.size(0) / 2}, x.options());
+    if (pgemm(T, w, true)) {
+      gemm_prefill(a, x, w, true, -1);
+    } else if (dgemm_blocks_ok(w, true) && x.stride(1) == 1) {
+      for (int64_t r0 = 0; r0 < T; r0 += kDgemmMaxM) {
+        const int64_t n = std::min<int64_t>(kDgemmMaxM, T - r0);
+        decode_gemm_silu(a.narrow(0, r0, n), x.narrow(0, r0, n), w, dg_ws_, dg_tickets_, status_.narrow(0, 0, 1), 0);
+      }
+    } else {
+      at::Tensor gu = at::linear(x, w);
+      silu_and_mul(a, gu);
+    }
+    return a;
   }
 
   // f32 logits [rows or T, vocab]; decode rows are [0, num_decode), prefill rows after.
@@ -345,7 +387,7 @@ class LlamaRunner {
       if (gv && gemv_supported(qkv_w_[l], false)) {
         qkv = at::empty({T, qkv_w_[l].size(0)}, x.options());
         gemv(qkv, x, qkv_w_[l]);
-      } else if (sk && T <= 32 && skinny_shape(qkv_w_[l])) {
+      } else if (sk && T <= skinny_qkv_max() && skinny_shape(qkv_w_[l])) {
         qkv = at::empty({T, qkv_w_[l].size(0)}, x.options());
         skinny_gemm(qkv, x, qkv_w_[l]);
       } else if (dgemm(T, qkv_w_[l], false)) {
@@ -356,11 +398,8 @@ class LlamaRunner {
         } else {
           decode_gemm(qkv, x, qkv_w_[l], dg_ws_, c10::nullopt, c10::nullopt, eps_, 0, 0);
         }
-      } else if (pgemm(T, qkv_w_[l], false)) {
-        qkv = at::empty({T, qkv_w_[l].size(0)}, x.options());
-        gemm_prefill(qkv, x, qkv_w_[l], false, -1);
       } else {
-        qkv = at::linear(x, qkv_w_[l]);
+        qkv = proj(x, qkv_w_[l]);
       }
       at::Tensor attn = at::empty({T, hq_ * d_}, qkv.options());
       at::Tensor q = qkv.narrow(1, 0, hq_ * d_);
@@ -403,12 +442,7 @@ class LlamaRunner {
           fused_add_rmsnorm(o, residual, post_norm_[l], eps_);
         }
       } else {
-        if (pgemm(T, o_w_[l], false)) {
-          o = at::empty_like(residual);
-          gemm_prefill(o, attn, o_w_[l], false, -1);
-        } else {
-          o = at::linear(attn, o_w_[l]);
-        }
+        o = proj(attn, o_w_[l]);
         all_reduce(o);
         fused_add_rmsnorm(o, residual, post_norm_[l], eps_);
       }
@@ -420,14 +454,8 @@ class LlamaRunner {
         // decode batch: SwiGLU in the epilogue after the in-launch combine of the K halves
         a = at::empty({T, gate_up_w_[l].size(0) / 2}, o.options());
         decode_gemm_silu(a, o, gate_up_w_[l], dg_ws_, dg_tickets_, status_.narrow(0, 0, 1), 0);
-      } else if (pgemm(T, gate_up_w_[l], true)) {
-        // prefill: SwiGLU in the GEMM epilogue, the [T, 2F] product never reaches HBM
-        a = at::empty({T, gate_up_w_[l].size(0) / 2}, o.options());
-        gemm_prefill(a, o, gate_up_w_[l], true, -1);
       } else {
-        at::Tensor gu = at::linear(o, gate_up_w_[l]);
-        a = at::empty({T, gu.size(1) / 2}, gu.options());
-        silu_and_mul(a, gu);
+        a = proj_silu(o, gate_up_w_[l]);
       }
       const at::Tensor& nxt = l + 1 < L ? in_norm_[l + 1] : final_norm_;
       at::Tensor dn;
@@ -455,12 +483,7 @@ class LlamaRunner {
           fused_add_rmsnorm(dn, residual, nxt, eps_);
         }
       } else {
-        if (pgemm(T, down_w_[l], false)) {
-          dn = at::empty_like(residual);
-          gemm_prefill(dn, a, down_w_[l], false, -1);
-        } else {
-          dn = at::linear(a, down_w_[l]);
-        }
+        dn = proj(a, down_w_[l]);
         all_reduce(dn);
         fused_add_rmsnorm(dn, residual, nxt, eps_);
       }
@@ -601,27 +624,43 @@ class LlamaRunner {
     }();
     return on;
   }
-  // Prefill-sized steps (T >= LS_PGEMM_MIN_T, default 1024) run the gate_up projection
-  // on the 256 x 256-tile ping-pong GEMM (ops/csrc/gemm_prefill.hip) with SwiGLU in its
-  // epilogue (no [T, 2F] round trip, no silu_and_mul): 2.57 vs 2.74 ms for hipBLASLt +
-  // silu_and_mul at T = 16384, 359 vs 375 us at T = 2048.  qkv / o / down stay on
-  // hipBLASLt, still 4-8 % faster on those plain shapes at T = 16384 and 20-30 % on o /
-  // down at T = 2048 (128 tiles for 256 CUs) (profiles/pgemm_ab_r3_*.log).
-  // LS_PGEMM=0: gate_up on hipBLASLt + silu_and_mul too; LS_PGEMM=all: all four here.
+  // Prefill-sized steps (T >= LS_PGEMM_MIN_T, default 1024) run all four projections on
+  // the 256 x 256-tile ping-pong GEMM (ops/csrc/gemm_prefill.hip), gate_up with SwiGLU in
+  // its epilogue (no [T, 2F] round trip).  LS_PGEMM=lib: the library GEMM instead (A/B
+  // switch); LS_PGEMM=route: qkv / o / down by the measured per-M-bucket table of round 3
+  // (ops/pgemm_route_gfx950.csv), gate_up always here.
   static bool pgemm(int64_t T, const at::Tensor& w, bool silu) {
     static const int mode = [] {
       const char* e = getenv("LS_PGEMM");
-      if (e == nullptr) return 1;
-      if (std::string(e) == "all") return 2;
-      return e[0] == '0' ? 0 : 1;
+      if (e == nullptr) return 2;
+      const std::string v(e);
+      if (v == "lib" || v == "0") return 0;
+      if (v == "route" || v == "1") return 1;
+      return 2;
     }();
     static const int64_t min_t = [] {
       const char* e = getenv("LS_PGEMM_MIN_T");
       return e ? (int64_t)atoll(e) : (int64_t)1024;
     }();
-    if (!gemm_prefill_supported(w, silu) || T < min_t) return false;
-    if (silu || mode == 2) return mode > 0;
-    return mode == 1 && pgemm_route::use_pp(T, w.size(0), w.size(1));
+    if (mode == 0 || !gemm_prefill_supported(w, silu) || T < min_t) return false;
+    if (silu || mode == 2) return true;
+    return pgemm_route::use_pp(T, w.size(0), w.size(1));
+  }
+  // rows below the prefill threshold: the decode GEMM in 256-row blocks
+  bool dgemm_blocks_ok(const at::Tensor& w, bool silu) const {
+    static const bool lib = [] {
+      const char* e = getenv("LS_PGEMM");
+      return e != nullptr && (std::string(e) == "lib" || std::string(e) == "0");
+    }();
+    return !lib && dgemm_enabled() && dg_ws_.defined() && decode_gemm_supported(w, silu);
+  }
+  // qkv rows on the skinny ring (measured faster than the 256-row decode GEMM at small T)
+  static int64_t skinny_qkv_max() {
+    static const int64_t v = [] {
+      const char* e = getenv("LS_SKINNY_QKV_MAX");
+      return e ? (int64_t)atoll(e) : (int64_t)32;
+    }();
+    return v;
   }
   static bool skinny_shape(const at::Tensor& w) { return w.size(0) % 128 == 0 && w.size(1) % 64 == 0; }
 

@@ -69,3 +69,23 @@ def test_bench_stage_trace(tmp_path, monkeypatch):
         p10, p50, mx = step["end"]
         assert 0 <= p10 <= p50 <= mx
         assert step["searches"] and sum(s[4] for s in step["searches"]) >= 8
+
+
+def test_bench_eight_ranks_dp8_disjoint_partitions(tmp_path):
+    """World 8 (the driver's scaling size) on CPU: bench.py --gpus 8 self-launches 8
+    ranks whose replicas consume DISJOINT partitions of the question and document topics
+    (one consumer group), every rank owns partitions, and every query went through the
+    8-shard kNN service (global top-k: tests/test_distributed_cpu.py at world 8)."""
+    d = _run(["--gpus", "8", "--steps", "1", "--warmup", "1", "--batch", "2", "--max-tokens", "2",
+              "--corpus", "400", "--docs", "1"], tmp_path, timeout=900)
+    assert d["n_gpus"] == 8 and d["config"]["parallelism"] == "dp8" and d["value"] > 0
+    assert d["latency_samples"] == 8 * 2
+    parts = d["partitions_per_rank"]
+    assert len(parts) == 8
+    for topic in ("questions-topic", "documents-topic"):
+        owned = [set(p[topic]) for p in parts]
+        assert all(owned), (topic, owned)
+        for i in range(8):
+            for j in range(i + 1, 8):
+                assert not owned[i] & owned[j], (topic, i, j)
+    assert all(n > 0 for n in d["knn_rounds_per_rank"])
