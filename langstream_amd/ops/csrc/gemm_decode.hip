@@ -96,9 +96,29 @@ struct DgArgs {
   int Hq = 0, Hkv = 0, BS = 0;
 };
 
+// 1 / rms of one row from its npart partial sums of squares.  The partials were written by
+// the previous launch from every XCD, so each load is a MALL / cross-XCD round trip: the
+// loads go out together as float4s (a dependent scalar loop cost ~1 us per partial).
 __device__ __forceinline__ float rms_scale(const float* __restrict__ part, int npart, float inv_h, float eps) {
   float s = 0.f;
-  for (int t = 0; t < npart; ++t) s += part[t];
+  int t = 0;
+  if ((npart & 3) == 0 && (reinterpret_cast<uintptr_t>(part) & 15) == 0) {
+    const float4* p4 = reinterpret_cast<const float4*>(part);
+    const int n4 = npart >> 2;
+    for (; t + 8 <= n4; t += 8) {
+      float4 v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = p4[t + j];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += (v[j].x + v[j].y) + (v[j].z + v[j].w);
+    }
+    for (; t < n4; ++t) {
+      const float4 v = p4[t];
+      s += (v.x + v.y) + (v.z + v.w);
+    }
+    t = npart;
+  }
+  for (; t < npart; ++t) s += part[t];
   return rsqrtf(s * inv_h + eps);
 }
 
@@ -345,6 +365,14 @@ __global__ void __launch_bounds__(LD ? 768 : 512) dgemm_kernel(const bf16* __res
   // is dead now) and leaves in whole rows with 16-B stores -- every store instruction
   // writes full 128-B lines instead of 4 x 64-B row pieces per wave.  BN = 128 stages all
   // 256 rows at once (132 KB); BN = 256 in two passes of 128 rows.
+  // CMB_QKV: this thread's row scale, fetched now so its latency hides behind the slab
+  // stores and the rendezvous (nr <= NT rows per slice: thread i takes row rr0 + i)
+  float r_pre = 1.f;
+  if constexpr (EPI == EPI_CMB_QKV) {
+    const int R = (M + S - 1) / S, rr0 = split * R;
+    if ((int)threadIdx.x < min(R, M - rr0))
+      r_pre = rms_scale(ga.sumsq_in + (int64_t)(rr0 + threadIdx.x) * ga.npart, ga.npart, ga.inv_h, ga.eps);
+  }
   constexpr int TP = BN + 4;
   constexpr int PASS_ROWS = BM * TP * 4 <= XS * XSTAGE + WS * WSTAGE ? BM : BM / 2;
   static_assert(PASS_ROWS * TP * 4 <= XS * XSTAGE + WS * WSTAGE, "epilogue pass must fit the ring's LDS");
@@ -376,7 +404,19 @@ __global__ void __launch_bounds__(LD ? 768 : 512) dgemm_kernel(const bf16* __res
     }
     __syncthreads();
     const int rows = min(PASS_ROWS, M - r0);
-    if constexpr (EPI == EPI_PARTIAL || CMB) {
+    if constexpr (CMB) {
+      // slab stores WRITE-THROUGH (sc1): the K slices of this tile read them in this launch,
+      // and a plain store would need an agent release fence that writes back every dirty
+      // L2 line of the XCD (128 KB per workgroup here) -- MI355X_MICROARCH publish-large
+      const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
+          part, 0, (int)((int64_t)S * M * N * 4), 0x00020000);
+      for (int q = threadIdx.x; q < rows * (BN / 4); q += NT) {
+        const int m = q / (BN / 4), c = (q - m * (BN / 4)) * 4;
+        const int off = (int)((((int64_t)split * M + r0 + m) * N + tile * BN + c) * 4);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, *reinterpret_cast<const f32x4*>(T + m * TP + c)),
+                                               prs, off, 0, 16);
+      }
+    } else if constexpr (EPI == EPI_PARTIAL) {
       // part[split][m][tile * BN + c]: BN / 4 float4 per row
       for (int q = threadIdx.x; q < ((ABL & 64) ? 0 : rows * (BN / 4)); q += NT) {
         const int m = q / (BN / 4), c = (q - m * (BN / 4)) * 4;
@@ -415,9 +455,8 @@ __global__ void __launch_bounds__(LD ? 768 : 512) dgemm_kernel(const bf16* __res
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's slab stores are done
     __syncthreads();
     if (threadIdx.x == 0) {
+      // every storing wave drained its sc1 stores before the barrier above: no release
       unsigned long long* cnt = ga.counters + tile;
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       const unsigned long long old = __hip_atomic_fetch_add(cnt, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const unsigned long long target = old - old % (unsigned long long)S + (unsigned long long)S;
       int spins = 0;
@@ -473,8 +512,7 @@ __global__ void __launch_bounds__(LD ? 768 : 512) dgemm_kernel(const bf16* __res
       // partials, then RoPE on q / k heads, the paged K / V write for k / v heads.
       constexpr int D = 128, HALF = 64, G4 = 16;
       float* rrow = reinterpret_cast<float*>(lds);   // LDS is free after the slab stores
-      for (int i = threadIdx.x; i < nr; i += NT)
-        rrow[i] = rms_scale(ga.sumsq_in + (int64_t)(rr0 + i) * ga.npart, ga.npart, ga.inv_h, ga.eps);
+      if (threadIdx.x < nr) rrow[threadIdx.x] = r_pre;
       __syncthreads();
       const int hd = tile;
       for (int q = threadIdx.x; q < nr * G4; q += NT) {

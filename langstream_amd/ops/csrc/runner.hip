@@ -321,12 +321,13 @@ class LlamaRunner {
     at::Tensor x = at::empty_like(h);
     rmsnorm(x, h, in_norm_[0], eps_);
     const int64_t L = qkv_w_.size();
-    // Decode-sized steps use the hand-written skinny MFMA GEMM (ops/csrc/gemm_skinny.hip)
-    // where it measured faster than hipBLASLt on MI355X (profiles/skinny_gemm_v2.log):
-    // qkv at T <= 32, o_proj at T <= 192 and down_proj at 48 <= T <= 256, the last two
-    // with the residual add + RMSNorm fused into the split-K reduction at TP=1; under TP
-    // the row-parallel partial sums are all-reduced first, so o/down store the plain
-    // GEMM and the residual add + RMSNorm runs after the all-reduce.
+    // Decode-sized steps (5..256 rows) run on the 256-row decode GEMM (gemm_decode.hip,
+    // dgemm()); the skinny ring (gemm_skinny.hip) remains the path for LS_DGEMM=0 or
+    // shapes the decode GEMM does not take: qkv at T <= 32, o_proj at T <= 192 and
+    // down_proj at 48 <= T <= 256, the last two with the residual add + RMSNorm fused into
+    // the split-K reduction at TP=1; under TP the row-parallel partial sums are
+    // all-reduced first, so o/down store the plain GEMM and the residual add + RMSNorm
+    // runs after the all-reduce.
     const bool sk = skinny_enabled();
     // T <= 4 (single-stream / low-concurrency chat): the register-streaming GEMV
     // (ops/csrc/gemm_gemv.hip) for all four projections, gate_up with silu*up fused; it
@@ -387,9 +388,6 @@ class LlamaRunner {
       if (gv && gemv_supported(qkv_w_[l], false)) {
         qkv = at::empty({T, qkv_w_[l].size(0)}, x.options());
         gemv(qkv, x, qkv_w_[l]);
-      } else if (sk && T <= skinny_qkv_max() && skinny_shape(qkv_w_[l])) {
-        qkv = at::empty({T, qkv_w_[l].size(0)}, x.options());
-        skinny_gemm(qkv, x, qkv_w_[l]);
       } else if (dgemm(T, qkv_w_[l], false)) {
         qkv = at::empty({T, qkv_w_[l].size(0)}, x.options());
         if (decode_only && qkv_rope_fused()) {
@@ -398,6 +396,9 @@ class LlamaRunner {
         } else {
           decode_gemm(qkv, x, qkv_w_[l], dg_ws_, c10::nullopt, c10::nullopt, eps_, 0, 0);
         }
+      } else if (sk && T <= skinny_qkv_max() && skinny_shape(qkv_w_[l])) {
+        qkv = at::empty({T, qkv_w_[l].size(0)}, x.options());
+        skinny_gemm(qkv, x, qkv_w_[l]);
       } else {
         qkv = proj(x, qkv_w_[l]);
       }
@@ -588,7 +589,8 @@ class LlamaRunner {
     return on;
   }
   bool fused_ready(int64_t T) const {
-    return cnt_qkv_.defined() && dgemm_enabled() && T >= dgemm_min_t() && T <= kDgemmMaxM;
+    return cnt_qkv_.defined() && dgemm_enabled() && T >= std::max(dgemm_min_t(), fused_min_t()) &&
+           T <= kDgemmMaxM;
   }
 
   static bool gemv_enabled() {
@@ -664,7 +666,7 @@ class LlamaRunner {
   }
   static bool skinny_shape(const at::Tensor& w) { return w.size(0) % 128 == 0 && w.size(1) % 64 == 0; }
 
-  // Decode batches of LS_DGEMM_MIN_T (default 129) .. 256 rows run all four projections
+  // Decode batches of LS_DGEMM_MIN_T (default 5) .. 256 rows run all four projections
   // on the 256-row decode GEMM (ops/csrc/gemm_decode.hip) instead of hipBLASLt / the
   // skinny ring.  LS_DGEMM=0 turns it off (A/B switch).
   static constexpr int64_t kDgemmMaxM = 256;
@@ -675,12 +677,24 @@ class LlamaRunner {
     }();
     return on;
   }
+  // From 5 rows (the GEMV takes 1..4): measured against hipBLASLt and the skinny ring at
+  // 5..128 rows on the Llama-3-8B shapes (profiles/dgemm_smallm_r4.log): qkv 17-24.5 us
+  // vs 28.8-31.1 (hipBLASLt) / 18.3-27.5 (skinny), gate_up + SwiGLU 52.4-54.3 vs
+  // 53.8-62.7 / 57.7-59.3, down 30.5-37.8 vs 34.3-84.0 / 35.0-45.4.
   static int64_t dgemm_min_t() {
     static const int64_t min_t = [] {
       const char* e = getenv("LS_DGEMM_MIN_T");
-      return e ? (int64_t)atoll(e) : (int64_t)129;
+      return e ? (int64_t)atoll(e) : (int64_t)5;
     }();
     return min_t;
+  }
+  // the norm-deferred layer from this many rows (LS_DGEMM_FUSED_MIN_T)
+  static int64_t fused_min_t() {
+    static const int64_t v = [] {
+      const char* e = getenv("LS_DGEMM_FUSED_MIN_T");
+      return e ? (int64_t)atoll(e) : (int64_t)129;
+    }();
+    return v;
   }
   bool dgemm(int64_t T, const at::Tensor& w, bool silu) const {
     return dgemm_enabled() && dg_ws_.defined() && T >= dgemm_min_t() && T <= kDgemmMaxM &&
