@@ -745,24 +745,32 @@ def _other_config(args, rank: int, world: int, local: int) -> None:
     """BASELINE configs 2, 3 and 5 (langstream_amd/bench/)."""
     import torch
     import torch.distributed as dist
-    use_gpu = torch.cuda.is_available()
-    if use_gpu:
-        torch.cuda.set_device(local)
     if args.config == "chat":
+        if torch.cuda.is_available():
+            torch.cuda.set_device(local)
         from langstream_amd.bench import chat
         chat.run(args, rank, world, None)
         if dist.is_initialized():
             dist.destroy_process_group()
         return
+    # config 2 starts its broker and load-generator processes before anything touches
+    # the GPU (gloo needs no GPU), then initialises the device
     ctrl = None
     if world > 1:
         dist.init_process_group("gloo")
         ctrl = dist.group.WORLD
+    gpu = [False]
+
+    def gpu_init() -> bool:
+        gpu[0] = torch.cuda.is_available()
+        if gpu[0]:
+            torch.cuda.set_device(local)
+        return gpu[0]
 
     def barrier():
         if ctrl is not None:
             dist.barrier(group=ctrl)
-        if use_gpu:
+        if gpu[0]:
             torch.cuda.synchronize()
 
     def bcast(obj):
@@ -773,7 +781,7 @@ def _other_config(args, rank: int, world: int, local: int) -> None:
         return box[0]
 
     from langstream_amd.bench import embed
-    embed.run(args, rank, world, barrier, bcast)
+    embed.run(args, rank, world, barrier, bcast, gpu_init)
     if ctrl is not None:
         dist.destroy_process_group()
 

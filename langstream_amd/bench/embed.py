@@ -8,6 +8,9 @@ writing ``output-topic`` of the in-tree Kafka-protocol broker (streaming type
 ``kafka``; rank 0 hosts the broker, every rank's agent replica joins the consumer group
 ``langstream-agent-embed`` -- replica DP as the reference scales).  A step = B records
 per GPU produced at once; the step ends when all of them are committed by the group.
+The broker and the clients that feed and count the topics (bench/embed_load.py) run in
+their own processes, as Kafka and the applications around an agent pod do; set
+``LS_EMBED_INPROC=1`` to put all of them in the agent's interpreter instead.
 """
 from __future__ import annotations
 
@@ -61,19 +64,26 @@ instance:
 METRIC = "records/sec (whole node), compute-ai-embeddings agent on Kafka records, bge-small-en"
 
 
-def run(args, rank: int, world: int, barrier, bcast) -> None:
+def run(args, rank: int, world: int, barrier, bcast, gpu_init=None) -> None:
+    broker = None
+    inproc = bool(os.environ.get("LS_EMBED_INPROC"))
+    if rank == 0:
+        # the broker runs in its own interpreter, as the reference's Kafka runs in its
+        # own JVM; like the load generator it starts before anything touches the GPU
+        from ..topics.kafka.broker import BrokerProcess, KafkaBroker
+        parts0 = max(2, 2 * world)
+        broker = KafkaBroker(default_partitions=parts0).start() if inproc else BrokerProcess(partitions=parts0)
+    bootstrap = bcast(broker.bootstrap if broker else None)
+    B = args.batch
+    load = None
+    if not inproc:
+        from .embed_load import LoadProcess
+        load = LoadProcess(bootstrap, rank, world, B, read=rank == 0, timeout=args.timeout)
     import torch
-    from ..api.record import SimpleRecord
     from ..runtime.local import LocalApplicationRunner
     from ..services import ServiceRegistry
-    from ..tokenizers import builtin_corpus
-    use_gpu = torch.cuda.is_available()
+    use_gpu = gpu_init() if gpu_init is not None else torch.cuda.is_available()
     model = args.embed_model if use_gpu else "bert-tiny"
-    broker = None
-    if rank == 0:
-        from ..topics.kafka.broker import KafkaBroker
-        broker = KafkaBroker(default_partitions=max(2, 2 * world)).start()
-    bootstrap = bcast(broker.bootstrap if broker else None)
     parts = max(2, 2 * world)
     services = ServiceRegistry({"device": f"cuda:{int(os.environ.get('LOCAL_RANK', '0') or 0)}" if use_gpu else "cpu"})
     ServiceRegistry.set_default(services)
@@ -82,25 +92,34 @@ def run(args, rank: int, world: int, barrier, bcast) -> None:
              "configuration.yaml": CONFIG.format(model=model)}
     runner = LocalApplicationRunner.from_yaml(files, instance=INSTANCE.format(bootstrap=bootstrap),
                                               application_id="embed-bench", services=services).start()
-    corpus = builtin_corpus(20000)
-    prod = runner.producer("input-topic")
-    reader = runner.reader("output-topic") if rank == 0 else None   # rank 0 counts every replica's output
-    B = args.batch
+    if inproc:
+        # LS_EMBED_INPROC=1: clients and broker share the agent's interpreter (GIL)
+        from ..tokenizers import builtin_corpus
+        from .embed_load import make_records
+        corpus = builtin_corpus(20000)
+        prod = runner.producer("input-topic")
+        reader = runner.reader("output-topic") if rank == 0 else None   # rank 0 counts every replica's output
     seen = [0]
 
     def step(i):
-        futs = []
-        for j in range(B):
-            g = (i * world + rank) * B + j
-            text = " ".join(corpus[(g * 7 + k) % len(corpus)] for k in range(3))
-            futs.append(prod.write(SimpleRecord.of(f"r{rank}-{g}", json.dumps({"text": text}))))
+        if load is not None:
+            load.produce(i)
+            return
+        futs = [prod.write(r) for r in make_records(corpus, rank, world, B, i)]
         for f in futs:
             f.result(60)
 
     def wait_all(total):
-        if reader is None:
+        if rank != 0:
             return
         deadline = time.time() + args.timeout
+        if load is not None:
+            seen[0] = load.wait(total)
+            if runner.errors:
+                raise runner.errors[0]
+            if seen[0] < total:
+                raise TimeoutError(f"embed bench: {seen[0]} of {total} embedded records")
+            return
         while seen[0] < total:
             if runner.errors:
                 raise runner.errors[0]
@@ -127,10 +146,12 @@ def run(args, rank: int, world: int, barrier, bcast) -> None:
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "bf16" if use_gpu else "fp32", "data": "synthetic text records (builtin corpus), random-init weights",
             "config": {"model": model, "records_per_gpu_per_step": B, "batch-size": args.embed_batch,
-                       "concurrency": 4, "topics": "kafka (in-tree broker)", "parallelism": f"dp{world}"}}),
+                       "concurrency": 4, "topics": "kafka (in-tree broker, own process)", "parallelism": f"dp{world}"}}),
               flush=True)
     barrier()
     runner.stop(10)
     services.shutdown()
+    if load is not None:
+        load.close()
     if broker is not None:
         broker.stop()

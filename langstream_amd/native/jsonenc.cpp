@@ -17,8 +17,10 @@
 
 #include <charconv>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <string>
+#include <vector>
 
 namespace py = pybind11;
 
@@ -92,53 +94,70 @@ void put_str(std::string& o, PyObject* s) {
   o.push_back('"');
 }
 
-// float.__repr__ layout over the shortest round-trip digits
-void put_float(std::string& o, double x) {
-  if (std::isnan(x)) { o.append("NaN"); return; }
-  if (std::isinf(x)) { o.append(x > 0 ? "Infinity" : "-Infinity"); return; }
-  if (x == 0.0) { o.append(std::signbit(x) ? "-0.0" : "0.0"); return; }
-  char buf[64];
+// float.__repr__ layout over the shortest round-trip digits, built in one stack buffer
+// (appending piecewise to the std::string cost as much as the digit generation)
+inline int format_float(char* out, double x) {
+  char* w = out;
+  if (std::isnan(x)) { std::memcpy(w, "NaN", 3); return 3; }
+  if (std::isinf(x)) {
+    if (x > 0) { std::memcpy(w, "Infinity", 8); return 8; }
+    std::memcpy(w, "-Infinity", 9); return 9;
+  }
+  if (x == 0.0) {
+    if (std::signbit(x)) { std::memcpy(w, "-0.0", 4); return 4; }
+    std::memcpy(w, "0.0", 3); return 3;
+  }
+  char buf[40];
   auto r = std::to_chars(buf, buf + sizeof buf, x, std::chars_format::scientific);
   if (r.ec != std::errc()) throw Unsupported{};
   // buf = [-]d[.ddd]e(+|-)XX
   const char* p = buf;
   const char* end = r.ptr;
-  bool neg = false;
-  if (*p == '-') { neg = true; ++p; }
-  char dig[32];
+  if (*p == '-') { *w++ = '-'; ++p; }
+  char dig[24];
   int nd = 0;
-  const char* q = p;
-  for (; q < end && *q != 'e'; ++q)
-    if (*q != '.') dig[nd++] = *q;
+  dig[nd++] = *p++;
+  if (*p == '.') {
+    ++p;
+    while (*p != 'e') dig[nd++] = *p++;
+  }
+  // exponent: e, sign, 2..3 digits
+  const bool eneg = p[1] == '-';
   int e = 0;
-  std::from_chars(q + 1 + (q[1] == '+' ? 1 : 0), end, e);
-  if (neg) o.push_back('-');
+  for (const char* q = p + 2; q < end; ++q) e = e * 10 + (*q - '0');
+  if (eneg) e = -e;
   if (e >= -4 && e < 16) {
     if (e < 0) {
-      o.append("0.");
-      o.append(-e - 1, '0');
-      o.append(dig, nd);
+      *w++ = '0'; *w++ = '.';
+      for (int i = 0; i < -e - 1; ++i) *w++ = '0';
+      std::memcpy(w, dig, nd); w += nd;
     } else if (nd <= e + 1) {
-      o.append(dig, nd);
-      o.append(e + 1 - nd, '0');
-      o.append(".0");
+      std::memcpy(w, dig, nd); w += nd;
+      for (int i = 0; i < e + 1 - nd; ++i) *w++ = '0';
+      *w++ = '.'; *w++ = '0';
     } else {
-      o.append(dig, e + 1);
-      o.push_back('.');
-      o.append(dig + e + 1, nd - e - 1);
+      std::memcpy(w, dig, e + 1); w += e + 1;
+      *w++ = '.';
+      std::memcpy(w, dig + e + 1, nd - e - 1); w += nd - e - 1;
     }
   } else {
-    o.push_back(dig[0]);
+    *w++ = dig[0];
     if (nd > 1) {
-      o.push_back('.');
-      o.append(dig + 1, nd - 1);
+      *w++ = '.';
+      std::memcpy(w, dig + 1, nd - 1); w += nd - 1;
     }
-    o.push_back('e');
-    o.push_back(e < 0 ? '-' : '+');
+    *w++ = 'e';
+    *w++ = e < 0 ? '-' : '+';
     int a = e < 0 ? -e : e;
-    if (a < 10) o.push_back('0');
-    o.append(std::to_string(a));
+    if (a >= 100) { *w++ = char('0' + a / 100); a %= 100; *w++ = char('0' + a / 10); *w++ = char('0' + a % 10); }
+    else { *w++ = char('0' + a / 10); *w++ = char('0' + a % 10); }
   }
+  return int(w - out);
+}
+
+void put_float(std::string& o, double x) {
+  char b[48];
+  o.append(b, format_float(b, x));
 }
 
 void put_int(std::string& o, PyObject* v) {
@@ -161,6 +180,54 @@ void put_int(std::string& o, PyObject* v) {
 }
 
 void put(std::string& o, PyObject* v, int depth);
+
+// LS_JSON_NOGIL=1: a long all-float list (an embedding vector) is formatted with the GIL
+// released (the doubles are copied out first; the list is never touched without the
+// GIL).  Off by default: measured on the config-2 agent (bench/embed.py, null embedder)
+// it LOST 20-30% -- the releasing thread then waits a switch interval to get the GIL
+// back from the agent's CPU-bound threads, which costs more than the ~25 us/record of
+// formatting it overlaps.
+constexpr Py_ssize_t kFloatRunMin = 64;
+
+bool float_run_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("LS_JSON_NOGIL");
+    return e != nullptr && e[0] == '1';
+  }();
+  return on;
+}
+
+bool put_float_run(std::string& o, PyObject* seq, bool lst, Py_ssize_t n) {
+  thread_local std::vector<double> xs;
+  thread_local std::string tmp;
+  xs.resize(n);
+  for (Py_ssize_t i = 0; i < n; ++i) {
+    PyObject* it = lst ? PyList_GET_ITEM(seq, i) : PyTuple_GET_ITEM(seq, i);
+    if (!PyFloat_CheckExact(it)) return false;
+    xs[i] = PyFloat_AS_DOUBLE(it);
+  }
+  // ", " + at most 25 chars per float, + brackets
+  tmp.resize(size_t(n) * 28 + 2);
+  size_t len = 0;
+  bool ok = true;
+  Py_BEGIN_ALLOW_THREADS
+  try {
+    char* w = &tmp[0];
+    *w++ = '[';
+    for (Py_ssize_t i = 0; i < n; ++i) {
+      if (i) { *w++ = ','; *w++ = ' '; }
+      w += format_float(w, xs[i]);
+    }
+    *w++ = ']';
+    len = size_t(w - &tmp[0]);
+  } catch (...) {
+    ok = false;
+  }
+  Py_END_ALLOW_THREADS
+  if (!ok) throw Unsupported{};
+  o.append(tmp.data(), len);
+  return true;
+}
 
 void put_key(std::string& o, PyObject* k) {
   if (PyUnicode_Check(k)) { put_str(o, k); return; }
@@ -195,6 +262,7 @@ void put(std::string& o, PyObject* v, int depth) {
     PyObject* seq = v;
     const bool lst = PyList_Check(v);
     Py_ssize_t n = lst ? PyList_GET_SIZE(seq) : PyTuple_GET_SIZE(seq);
+    if (n >= kFloatRunMin && float_run_enabled() && put_float_run(o, seq, lst, n)) return;
     o.push_back('[');
     for (Py_ssize_t i = 0; i < n; ++i) {
       if (i) o.append(", ");

@@ -436,6 +436,41 @@ __global__ void __launch_bounds__(512) knn_filter_q256_kernel(const bf16* __rest
 #pragma unroll
   for (int ks = 0; ks < KS; ++ks) aoff[ks] = fr * RB + (((4 * ks + h) ^ fr) * 16);
 
+  // Score epilogues run one subtile behind the MFMAs that produce them: subtile i's
+  // compare / ballot / append is issued after subtile i+1's MFMAs, so the wave never waits
+  // on an MFMA result it has just requested (two accumulator sets alternate; the last
+  // subtile of a tile is checked after the next tile's first MFMAs).
+  auto mm = [&](const bf16x8 (&f)[KS], f32x4 (&acc)[2]) {
+    acc[0] = f32x4{0.f, 0.f, 0.f, 0.f};
+    acc[1] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int g = 0; g < 2; ++g) acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f[ks], qf[g][ks], acc[g], 0, 0, 0);
+  };
+  // acc[g][rr] = score(row r0 + sr0 + 4h + rr, query q0 + 16g + fr); sr0 = subtile's first row
+  auto epi = [&](int sr0, const f32x4 (&acc)[2]) {
+#pragma unroll
+    for (int g = 0; g < 2; ++g)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int lr = sr0 + 4 * h + rr;
+        const bool hit = acc[g][rr] > thr[g] && lr < nrows;
+        const uint64_t mask = __ballot(hit);
+        if (mask == 0) continue;
+        const int nh = __popcll(mask);
+        if (ccount + nh > CAPW) flush();   // rare: drains the DMA ring once
+        const int pos = ccount + __popcll(mask & ((1ull << lane) - 1ull));
+        if (hit) {
+          c_s[pos] = acc[g][rr];
+          c_r[pos] = (int)(r0 + lr);
+          c_q[pos] = q0 + 16 * g + fr;
+        }
+        ccount += nh;
+      }
+  };
+  f32x4 accA[2], accB[2];
+  int pend = -1;   // first row of the subtile whose scores wait in accB (-1: none)
   for (int s = 0; s < NST - 1; ++s) issue(s, s);
   for (int t = 0; t < ntile; ++t) {
     wait_vmcnt<(NST - 2) * GPW>();   // this wave's DMA of tile t landed (tiles t+1.. may be in flight)
@@ -452,41 +487,21 @@ __global__ void __launch_bounds__(512) knn_filter_q256_kernel(const bf16* __rest
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) f[ks] = __builtin_bit_cast(bf16x8, ld16(st + i * 16 * RB + aoff[ks]));
     };
-    auto sub = [&](int i, const bf16x8 (&f)[KS]) {
-      f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks)
-#pragma unroll
-        for (int g = 0; g < 2; ++g) acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f[ks], qf[g][ks], acc[g], 0, 0, 0);
-      // acc[g][rr] = score(row r0 + tl0 + 16i + 4h + rr, query q0 + 16g + fr)
-#pragma unroll
-      for (int g = 0; g < 2; ++g)
-#pragma unroll
-        for (int rr = 0; rr < 4; ++rr) {
-          const int lr = tl0 + 16 * i + 4 * h + rr;
-          const bool hit = acc[g][rr] > thr[g] && lr < nrows;
-          const uint64_t mask = __ballot(hit);
-          if (mask == 0) continue;
-          const int nh = __popcll(mask);
-          if (ccount + nh > CAPW) flush();   // rare: drains the DMA ring once
-          const int pos = ccount + __popcll(mask & ((1ull << lane) - 1ull));
-          if (hit) {
-            c_s[pos] = acc[g][rr];
-            c_r[pos] = (int)(r0 + lr);
-            c_q[pos] = q0 + 16 * g + fr;
-          }
-          ccount += nh;
-        }
-    };
     rd(0, fa);
     rd(1, fb);
-    sub(0, fa);
+    mm(fa, accA);                       // subtile 0
+    if (pend >= 0) epi(pend, accB);     // the previous tile's subtile 3
     rd(2, fa);
-    sub(1, fb);
+    mm(fb, accB);                       // subtile 1
+    epi(tl0, accA);
     rd(3, fb);
-    sub(2, fa);
-    sub(3, fb);
+    mm(fa, accA);                       // subtile 2
+    epi(tl0 + 16, accB);
+    mm(fb, accB);                       // subtile 3
+    epi(tl0 + 32, accA);
+    pend = tl0 + 48;
   }
+  if (pend >= 0) epi(pend, accB);
   wait_vmcnt<0>();   // no LDS-DMA may outlive the workgroup
   flush();
 }

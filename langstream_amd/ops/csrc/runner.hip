@@ -580,11 +580,14 @@ class LlamaRunner {
     return h;
   }
 
-  // LS_DGEMM_FUSED=0: the unfused 129..256-row decode path (split-K reduce kernels)
+  // LS_DGEMM_FUSED=1: the norm-deferred fused 129..256-row decode layer (in-launch
+  // split-K combine).  Off by default: measured 9.43 vs 8.80 ms per B=256 decode step
+  // (profiles/eng2_fused_r4.log) -- the 32 MB of slab writes + reads after the
+  // rendezvous cost more than the reduce launches they replace.
   static bool fused_env() {
     static const bool on = [] {
       const char* e = getenv("LS_DGEMM_FUSED");
-      return e == nullptr || e[0] != '0';
+      return e != nullptr && e[0] == '1';
     }();
     return on;
   }

@@ -24,14 +24,15 @@ class _Counter:
     def __init__(self, c, labels):
         self._c = c
         self._labels = labels
+        self._child = c.labels(**labels) if c is not None else None   # resolved once, not per inc
         self.value = 0.0
         self._lock = threading.Lock()
 
     def inc(self, n: float = 1.0) -> None:
         with self._lock:
             self.value += n
-        if self._c is not None:
-            self._c.labels(**self._labels).inc(n)
+        if self._child is not None:
+            self._child.inc(n)
 
     def count(self) -> float:
         return self.value

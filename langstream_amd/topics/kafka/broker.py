@@ -437,3 +437,68 @@ class KafkaBroker:
                     for m in dead:
                         del g.members[m]
                     self._start_rebalance(g)
+
+
+def main(argv=None) -> int:
+    """Standalone broker process (``python -m langstream_amd.topics.kafka.broker``): the
+    single-node Kafka of the reference's docker mode in its own interpreter, so broker
+    work never contends for the agents' GIL.  Prints ``bootstrap=<host:port>`` once
+    listening and serves until stdin closes or SIGTERM."""
+    import argparse
+    import signal
+    import sys
+    ap = argparse.ArgumentParser(prog="langstream_amd.topics.kafka.broker")
+    ap.add_argument("--host", default="127.0.0.1")
+    ap.add_argument("--port", type=int, default=0)
+    ap.add_argument("--partitions", type=int, default=1, help="partitions of auto-created topics")
+    ap.add_argument("--no-auto-create", action="store_true")
+    a = ap.parse_args(argv)
+    b = KafkaBroker(a.host, a.port, auto_create_topics=not a.no_auto_create,
+                    default_partitions=a.partitions).start()
+    done = threading.Event()
+    signal.signal(signal.SIGTERM, lambda *_: done.set())
+    print(f"bootstrap={b.bootstrap}", flush=True)
+
+    def watch_stdin():
+        try:
+            sys.stdin.read()
+        except Exception:  # noqa: BLE001
+            pass
+        done.set()
+    threading.Thread(target=watch_stdin, daemon=True).start()
+    done.wait()
+    b.stop()
+    return 0
+
+
+class BrokerProcess:
+    """A broker in a child interpreter; the parent holds its stdin, so the broker also
+    ends when the parent dies."""
+
+    def __init__(self, partitions: int = 1, host: str = "127.0.0.1"):
+        import os
+        import subprocess
+        import sys
+        root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+        env = dict(os.environ, PYTHONPATH=os.pathsep.join([root, os.environ.get("PYTHONPATH", "")]).rstrip(os.pathsep))
+        self.proc = subprocess.Popen(
+            [sys.executable, "-m", "langstream_amd.topics.kafka.broker", "--host", host,
+             "--partitions", str(partitions)],
+            stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True, env=env)
+        line = self.proc.stdout.readline().strip()
+        if not line.startswith("bootstrap="):
+            self.proc.kill()
+            raise RuntimeError(f"broker process failed to start: {line!r}")
+        self.bootstrap = line.split("=", 1)[1]
+
+    def stop(self) -> None:
+        if self.proc.poll() is None:
+            self.proc.stdin.close()
+            try:
+                self.proc.wait(10)
+            except Exception:  # noqa: BLE001
+                self.proc.kill()
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())
