@@ -39,6 +39,8 @@ pipeline:
       batch-size: {batch_size}
       concurrency: 4
       flush-interval: 5
+    resources:
+      parallelism: {replicas}
 """
 
 CONFIG = """
@@ -71,7 +73,7 @@ def run(args, rank: int, world: int, barrier, bcast, gpu_init=None) -> None:
         # the broker runs in its own interpreter, as the reference's Kafka runs in its
         # own JVM; like the load generator it starts before anything touches the GPU
         from ..topics.kafka.broker import BrokerProcess, KafkaBroker
-        parts0 = max(2, 2 * world)
+        parts0 = max(2, 2 * world * args.embed_replicas)
         broker = KafkaBroker(default_partitions=parts0).start() if inproc else BrokerProcess(partitions=parts0)
     bootstrap = bcast(broker.bootstrap if broker else None)
     B = args.batch
@@ -82,16 +84,24 @@ def run(args, rank: int, world: int, barrier, bcast, gpu_init=None) -> None:
     import torch
     from ..runtime.local import LocalApplicationRunner
     from ..services import ServiceRegistry
-    use_gpu = gpu_init() if gpu_init is not None else torch.cuda.is_available()
+    R = args.embed_replicas
+    if R > 1:
+        # the replicas are agent-pod processes with their own engines: this process never
+        # touches the GPU (so it may start them), it only counts devices
+        use_gpu = torch.cuda.device_count() > 0
+    else:
+        use_gpu = gpu_init() if gpu_init is not None else torch.cuda.is_available()
     model = args.embed_model if use_gpu else "bert-tiny"
-    parts = max(2, 2 * world)
+    parts = max(2, 2 * world * R)
     services = ServiceRegistry({"device": f"cuda:{int(os.environ.get('LOCAL_RANK', '0') or 0)}" if use_gpu else "cpu"})
     ServiceRegistry.set_default(services)
-    services.embedding_engine(model, {"embeddings-model": model})
-    files = {"pipeline.yaml": PIPE.format(model=model, parts=parts, batch_size=args.embed_batch),
+    if R == 1:
+        services.embedding_engine(model, {"embeddings-model": model})
+    files = {"pipeline.yaml": PIPE.format(model=model, parts=parts, batch_size=args.embed_batch, replicas=R),
              "configuration.yaml": CONFIG.format(model=model)}
     runner = LocalApplicationRunner.from_yaml(files, instance=INSTANCE.format(bootstrap=bootstrap),
-                                              application_id="embed-bench", services=services).start()
+                                              application_id="embed-bench", services=services,
+                                              replica_processes=True).start(wait=600.0)
     if inproc:
         # LS_EMBED_INPROC=1: clients and broker share the agent's interpreter (GIL)
         from ..tokenizers import builtin_corpus
@@ -146,7 +156,8 @@ def run(args, rank: int, world: int, barrier, bcast, gpu_init=None) -> None:
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "bf16" if use_gpu else "fp32", "data": "synthetic text records (builtin corpus), random-init weights",
             "config": {"model": model, "records_per_gpu_per_step": B, "batch-size": args.embed_batch,
-                       "concurrency": 4, "topics": "kafka (in-tree broker, own process)", "parallelism": f"dp{world}"}}),
+                       "concurrency": 4, "topics": "kafka (in-tree broker, own process)",
+                       "agent_replicas_per_gpu": R, "parallelism": f"dp{world}"}}),
               flush=True)
     barrier()
     runner.stop(10)

@@ -7,6 +7,13 @@ an agent gets its own runner thread and they share the agent's consumer group, s
 ``resources.parallelism`` is honoured (replica data-parallelism over partitions).
 The GPU services (LLM / embedding engines, vector store) are process-wide singletons
 shared by all agents (``langstream_amd.services``).
+
+``replica_processes=True`` (or ``LANGSTREAM_REPLICA_PROCESSES=1``) runs each replica of
+an agent with ``parallelism`` > 1 as its own agent-pod process instead
+(``python -m langstream_amd.runtime.pod``, the process a StatefulSet replica runs), when
+the streaming cluster is reachable from other processes (kafka / pulsar / shm): each
+replica then has its own interpreter -- and GIL -- and its own engines on the same GPU,
+which is what scales a host-bound agent (per-record Python work) on one device.
 """
 from __future__ import annotations
 
@@ -32,7 +39,7 @@ log = logging.getLogger(__name__)
 class LocalApplicationRunner:
     def __init__(self, application: Application, application_id: str = "app", tenant: str = "default",
                  code_directory: str = "", state_dir: Optional[str] = None, services=None,
-                 agents: Optional[List[str]] = None):
+                 agents: Optional[List[str]] = None, replica_processes: Optional[bool] = None):
         if application.instance is None or application.instance.streaming_cluster is None:
             g = application.instance.globals if application.instance else {}
             application.instance = Instance(StreamingCluster("memory", {}), ComputeCluster("none", {}), g)
@@ -52,6 +59,10 @@ class LocalApplicationRunner:
         self.threads: List[threading.Thread] = []
         self.errors: List[BaseException] = []
         self._topic_rt = None
+        if replica_processes is None:
+            replica_processes = os.environ.get("LANGSTREAM_REPLICA_PROCESSES", "") == "1"
+        self.replica_processes = replica_processes
+        self.processes: List["_PodProcess"] = []
 
     # ------------------------------------------------------------------ construction helpers
     @staticmethod
@@ -84,6 +95,10 @@ class LocalApplicationRunner:
             if self.only_agents and node.id not in self.only_agents:
                 continue
             replicas = max(1, int(node.resources.parallelism or 1))
+            if replicas > 1 and self.replica_processes and self._cross_process():
+                for rep in range(replicas):
+                    self.processes.append(_PodProcess(self, node, rep))
+                continue
             for rep in range(replicas):
                 pod = pod_configuration(self.plan, node, self.tenant, self.code_directory,
                                         os.path.join(self.state_dir, node.id), rep)
@@ -98,6 +113,11 @@ class LocalApplicationRunner:
         deadline = time.time() + wait
         for r in self.runners:
             r.started.wait(max(0.0, deadline - time.time()))
+        for p in self.processes:
+            # engines load in every replica process: allow them longer than a thread
+            p.wait_started(max(wait, 300.0))
+        if self.processes:
+            threading.Thread(target=self._watch_processes, name="replica-watch", daemon=True).start()
         gctune.tune()   # startup heap -> permanent generation, rare full collections
         return self
 
@@ -108,12 +128,29 @@ class LocalApplicationRunner:
             log.exception("agent %s failed", runner.pod.agent_id)
             self.errors.append(e)
 
+    def _cross_process(self) -> bool:
+        sc = self.streaming_cluster
+        return sc is not None and sc.type in ("kafka", "pulsar", "shm")
+
+    def _watch_processes(self) -> None:
+        while self.processes and not all(p.stopping for p in self.processes):
+            for p in self.processes:
+                rc = p.proc.poll()
+                if rc is not None and not p.stopping and not p.reported:
+                    p.reported = True
+                    self.errors.append(RuntimeError(f"agent {p.agent_id} replica {p.replica} exited with {rc}"))
+            time.sleep(0.5)
+
     def stop(self, timeout: float = 30.0) -> None:
         for r in self.runners:
             r.stop()
+        for p in self.processes:
+            p.terminate()
         deadline = time.time() + timeout
         for t in self.threads:
             t.join(max(0.1, deadline - time.time()))
+        for p in self.processes:
+            p.join(max(0.1, deadline - time.time()))
 
     def __enter__(self):
         return self.start()
@@ -156,3 +193,55 @@ class LocalApplicationRunner:
 
     def agent_info(self) -> Dict[str, Any]:
         return {f"{r.pod.agent_id}-{r.pod.replica}": r.agent_info() for r in self.runners}
+
+
+class _PodProcess:
+    """One agent replica as an agent-pod process (runtime/pod.py) on this host."""
+
+    def __init__(self, owner: LocalApplicationRunner, node, replica: int):
+        import json
+        import subprocess
+        import sys
+        from ..core.k8s import agent_pod_configuration
+        self.agent_id, self.replica = node.id, replica
+        self.stopping = self.reported = False
+        d = os.path.join(owner.state_dir, node.id, f"replica-{replica}")
+        os.makedirs(d, exist_ok=True)
+        cfg = os.path.join(d, "pod-configuration.json")
+        with open(cfg, "w") as f:
+            json.dump(agent_pod_configuration(owner.plan, node, owner.tenant), f, default=str)
+        self.ready = os.path.join(d, "started")
+        if os.path.exists(self.ready):
+            os.remove(self.ready)
+        root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        env = dict(os.environ,
+                   PYTHONPATH=os.pathsep.join([root, os.environ.get("PYTHONPATH", "")]).rstrip(os.pathsep),
+                   HOSTNAME=f"{node.id}-{replica}",              # the StatefulSet ordinal
+                   LANGSTREAM_AGENT_HTTP_PORT="0",
+                   LANGSTREAM_AGENT_READY_FILE=self.ready,
+                   LANGSTREAM_FATAL_WAIT_S="0",
+                   LANGSTREAM_AGENT_RUNNER_CODE_PATH=owner.code_directory or "",
+                   LANGSTREAM_AGENT_RUNNER_PERSISTENT_STATE_DIRECTORY=d)
+        env.pop("WORLD_SIZE", None)   # torchrun's ranks are not this pod's TP group
+        self.proc = subprocess.Popen([sys.executable, "-m", "langstream_amd.runtime.pod", cfg], env=env)
+
+    def wait_started(self, timeout: float) -> None:
+        deadline = time.time() + timeout
+        while not os.path.exists(self.ready):
+            if self.proc.poll() is not None:
+                raise RuntimeError(f"agent {self.agent_id} replica {self.replica} exited with {self.proc.returncode}")
+            if time.time() > deadline:
+                raise TimeoutError(f"agent {self.agent_id} replica {self.replica} did not start in {timeout:.0f}s")
+            time.sleep(0.05)
+
+    def terminate(self) -> None:
+        self.stopping = True
+        if self.proc.poll() is None:
+            self.proc.terminate()
+
+    def join(self, timeout: float) -> None:
+        try:
+            self.proc.wait(timeout)
+        except Exception:  # noqa: BLE001
+            self.proc.kill()
+            self.proc.wait(5)

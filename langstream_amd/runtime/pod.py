@@ -164,7 +164,15 @@ def main(argv: Optional[List[str]] = None) -> int:
     except (ValueError, OSError):
         pass
     from ..utils import gctune
-    threading.Thread(target=lambda: runner.started.wait() and gctune.tune(), name="gc-tune", daemon=True).start()
+    ready = os.environ.get("LANGSTREAM_AGENT_READY_FILE")
+
+    def on_started():
+        runner.started.wait()
+        if ready:
+            # the local runner's replica processes wait for this (runtime/local.py)
+            open(ready, "w").close()
+        gctune.tune()
+    threading.Thread(target=on_started, name="gc-tune", daemon=True).start()
     try:
         runner.run()
         return 0
