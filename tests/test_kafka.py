@@ -147,3 +147,55 @@ instance:
         assert vals == [2 * i for i in range(10)]
     finally:
         app.stop(10)
+
+
+def test_pipeline_replicas_as_pod_processes(tmp_path):
+    """resources.parallelism: 2 with replica_processes: two agent-pod processes
+    (runtime/pod.py) join one consumer group on a broker in its own process."""
+    from langstream_amd.runtime.local import LocalApplicationRunner
+    from langstream_amd.topics.kafka.broker import BrokerProcess
+    b = BrokerProcess(partitions=2)
+    tin, tout = "in-" + uuid.uuid4().hex[:6], "out-" + uuid.uuid4().hex[:6]
+    pipe = f"""
+topics:
+  - name: {tin}
+    creation-mode: create-if-not-exists
+    partitions: 4
+  - name: {tout}
+    creation-mode: create-if-not-exists
+pipeline:
+  - name: c
+    id: twice
+    type: compute
+    input: {tin}
+    output: {tout}
+    resources:
+      parallelism: 2
+    configuration:
+      fields:
+        - name: "value.n2"
+          expression: "value.n * 2"
+"""
+    instance = f"""
+instance:
+  streamingCluster:
+    type: kafka
+    configuration:
+      admin:
+        bootstrap.servers: "{b.bootstrap}"
+"""
+    app = LocalApplicationRunner.from_yaml({"pipeline.yaml": pipe}, instance=instance, state_dir=str(tmp_path),
+                                           replica_processes=True).start(wait=120)
+    try:
+        assert len(app.processes) == 2 and not app.runners
+        assert all(p.proc.poll() is None for p in app.processes)
+        for i in range(40):
+            app.produce(tin, json.dumps({"n": i}), key=f"k{i}")
+        out = app.consume(tout, 40, timeout=60)
+        vals = sorted(json.loads(r.value())["n2"] for r in out)
+        assert vals == [2 * i for i in range(40)]
+        assert not app.errors
+    finally:
+        app.stop(20)
+        b.stop()
+    assert all(p.proc.returncode == 0 for p in app.processes)
