@@ -338,12 +338,20 @@ __global__ void __launch_bounds__(256) knn_filter_kernel(const bf16* __restrict_
 //     16-query groups share each fragment);
 //   * scores above the query's sample threshold are appended exactly as in
 //     knn_filter_kernel (same candidate lists, counters and overflow flags).
-template <int DIM>
+//
+// MODE 0: append scores > thr (the rows after an exact sample, see above);
+// MODE 1: append scores >= thr over the WHOLE store (thr from a MODE 2 pass: a lower
+//         bound attained by K distinct rows, so every row of the answer is >= thr);
+// MODE 2: no appends -- the running max of every (lane, accumulator register) slot,
+//         i.e. of 16 disjoint row groups per query per workgroup, written to
+//         gmax[q * G + 16 * rb + 4h + rr] (knn_group_thr_kernel turns them into thr).
+template <int DIM, int MODE>
 __global__ void __launch_bounds__(512) knn_filter_q256_kernel(const bf16* __restrict__ X, int64_t N,
                                                               const bf16* __restrict__ Qm, int Qn,
                                                               float* __restrict__ cand_s, int32_t* __restrict__ cand_i,
                                                               int* __restrict__ ctrl, int64_t cap, int64_t row_begin,
-                                                              int rows_per_wg, int nqb) {
+                                                              int rows_per_wg, int nqb, float* __restrict__ gmax,
+                                                              int G) {
   constexpr int KS = DIM / 32;
   constexpr int RB = DIM * 2;                    // bytes per row
   constexpr int TR = 64;                         // rows per LDS stage
@@ -404,7 +412,7 @@ __global__ void __launch_bounds__(512) knn_filter_q256_kernel(const bf16* __rest
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks)
       qf[g][ks] = __builtin_bit_cast(bf16x8, ok ? ld16(qp + 32 * ks) : make_uint4(0, 0, 0, 0));
-    thr[g] = ok ? key2f(ctrl[Qn + qi]) : INFINITY;
+    thr[g] = MODE == 2 ? -INFINITY : ok ? key2f(ctrl[Qn + qi]) : INFINITY;
   }
   // consume the query fragments here: otherwise hipcc places their vmcnt wait at the first
   // MFMA inside the tile loop, where a vmcnt(0) also drains the LDS-DMA ring every tile
@@ -414,22 +422,24 @@ __global__ void __launch_bounds__(512) knn_filter_q256_kernel(const bf16* __rest
     for (int ks = 0; ks < KS; ++ks) asm volatile("" ::"v"(qf[g][ks]));
     asm volatile("" ::"v"(thr[g]));
   }
-  // LDS-DMA: instruction j of wave w fills bytes [(w*GPW + j) * 1024, +1024) of a stage
-  int src_row[GPW], src_off[GPW];
+  // LDS-DMA: instruction j of wave w fills bytes [(w*GPW + j) * 1024, +1024) of a stage,
+  // through a buffer resource over this workgroup's rows: the per-lane offsets are
+  // tile-invariant (a tile adds t * SB), no 64-bit address math per load, and rows past
+  // the range read as zeros (their scores are masked by lr < nrows).
+  const i32x4 rsrc = make_rsrc((const char*)X + r0 * RB, (uint32_t)nrows * RB);
+  int voff[GPW];
 #pragma unroll
   for (int j = 0; j < GPW; ++j) {
     const int o = (wid * GPW + j) * 1024 + lane * 16;
     const int r = o / RB, p = (o % RB) / 16;
-    src_row[j] = r;
-    src_off[j] = ((p ^ (r & 15)) * 16);
+    voff[j] = r * RB + ((p ^ (r & 15)) * 16);
   }
+  const unsigned lds_base = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)lds;
   auto issue = [&](int t, int slot) {
-    const int64_t base = r0 + (int64_t)min(t, ntile - 1) * TR;   // past the end: reload the last tile (dead slot)
+    const int toff = min(t, ntile - 1) * SB;   // past the end: reload the last tile (dead slot)
 #pragma unroll
-    for (int j = 0; j < GPW; ++j) {
-      const int64_t row = min(base + src_row[j], N - 1);
-      glds16((const bf16*)((const char*)X + row * RB + src_off[j]), lds + slot * SB + (wid * GPW + j) * 1024);
-    }
+    for (int j = 0; j < GPW; ++j)
+      blds16(rsrc, voff[j] + toff, 0, lds_base + slot * SB + (wid * GPW + j) * 1024);
   };
   // A fragment of 16-row subtile i, k-step ks: row 16i + fr, chunk 4ks + h (swizzled)
   int aoff[KS];
@@ -448,14 +458,34 @@ __global__ void __launch_bounds__(512) knn_filter_q256_kernel(const bf16* __rest
 #pragma unroll
       for (int g = 0; g < 2; ++g) acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f[ks], qf[g][ks], acc[g], 0, 0, 0);
   };
-  // acc[g][rr] = score(row r0 + sr0 + 4h + rr, query q0 + 16g + fr); sr0 = subtile's first row
+  // acc[g][rr] = score(row r0 + sr0 + 4h + rr, query q0 + 16g + fr); sr0 = subtile's first row.
+  // Fast test first: one ballot over the subtile's 8 scores per lane (hits are rare -- only
+  // rows above the query's sample threshold), the per-score ballots only when it fires.
+  float gm[2][4];   // MODE 2: running max per (query group, accumulator register)
+#pragma unroll
+  for (int g = 0; g < 2; ++g)
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) gm[g][rr] = -INFINITY;
+  auto pass = [&](float v, float t) { return MODE == 0 ? v > t : v >= t; };
   auto epi = [&](int sr0, const f32x4 (&acc)[2]) {
+    if constexpr (MODE == 2) {
+      const bool tail = sr0 + 16 > nrows;   // wave-uniform
+#pragma unroll
+      for (int g = 0; g < 2; ++g)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr)
+          gm[g][rr] = fmaxf(gm[g][rr], tail && sr0 + 4 * h + rr >= nrows ? -INFINITY : acc[g][rr]);
+      return;
+    }
+    const float m0 = fmaxf(fmaxf(acc[0][0], acc[0][1]), fmaxf(acc[0][2], acc[0][3]));
+    const float m1 = fmaxf(fmaxf(acc[1][0], acc[1][1]), fmaxf(acc[1][2], acc[1][3]));
+    if (__ballot(pass(m0, thr[0]) || pass(m1, thr[1])) == 0) return;
 #pragma unroll
     for (int g = 0; g < 2; ++g)
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) {
         const int lr = sr0 + 4 * h + rr;
-        const bool hit = acc[g][rr] > thr[g] && lr < nrows;
+        const bool hit = pass(acc[g][rr], thr[g]) && lr < nrows;
         const uint64_t mask = __ballot(hit);
         if (mask == 0) continue;
         const int nh = __popcll(mask);
@@ -487,23 +517,59 @@ __global__ void __launch_bounds__(512) knn_filter_q256_kernel(const bf16* __rest
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) f[ks] = __builtin_bit_cast(bf16x8, ld16(st + i * 16 * RB + aoff[ks]));
     };
+    // sched_barriers pin each subtile's reads ahead of the previous subtile's MFMAs:
+    // left alone, hipcc sinks every read to just before its MFMA behind an lgkmcnt wait
+#define KNN_SB __builtin_amdgcn_sched_barrier(0)
     rd(0, fa);
     rd(1, fb);
+    KNN_SB;
     mm(fa, accA);                       // subtile 0
     if (pend >= 0) epi(pend, accB);     // the previous tile's subtile 3
+    KNN_SB;
     rd(2, fa);
+    KNN_SB;
     mm(fb, accB);                       // subtile 1
     epi(tl0, accA);
+    KNN_SB;
     rd(3, fb);
+    KNN_SB;
     mm(fa, accA);                       // subtile 2
     epi(tl0 + 16, accB);
+    KNN_SB;
     mm(fb, accB);                       // subtile 3
     epi(tl0 + 32, accA);
+#undef KNN_SB
     pend = tl0 + 48;
   }
   if (pend >= 0) epi(pend, accB);
   wait_vmcnt<0>();   // no LDS-DMA may outlive the workgroup
+  if constexpr (MODE == 2) {
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      const int qi = q0 + 16 * g + fr;
+      if (qi < Qn)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) gmax[(int64_t)qi * G + 16 * rb + 4 * h + rr] = gm[g][rr];
+    }
+    return;
+  }
   flush();
+}
+
+// thr[q] = the K-th largest of 64 group maxima (lane l: max over groups l, l+64, ...):
+// K disjoint row groups each hold a row scoring >= thr, so the answer's K-th best is
+// >= thr (a lower bound attained by K distinct rows).  One wave per query.
+__global__ void __launch_bounds__(256) knn_group_thr_kernel(const float* __restrict__ gmax, int G, int Qn, int K,
+                                                            int* __restrict__ ctrl) {
+  const int lane = threadIdx.x & 63;
+  const int qi = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (qi >= Qn) return;
+  float m = -INFINITY;
+  for (int j = lane; j < G; j += 64) m = fmaxf(m, gmax[(int64_t)qi * G + j]);
+  int idx = lane;
+  wave_sort_desc(m, idx, lane);
+  const float t = __shfl(m, K - 1, 64);
+  if (lane == 0) ctrl[Qn + qi] = f2key(t);
 }
 
 __global__ void knn_init_kernel(int* __restrict__ ctrl, int Qn) {
@@ -632,33 +698,44 @@ void knn_topk(at::Tensor X, at::Tensor Q, int64_t K, at::Tensor out_s, at::Tenso
   };
   static const int q256_min = getenv("LS_KNN_Q256_MIN") ? atoi(getenv("LS_KNN_Q256_MIN")) : 128;
   const bool q256 = Qn >= q256_min && (dim == 128 || dim == 256 || dim == 384 || dim == 512);
-  auto filter_q256 = [&](int c0, int nc) {
-    const int64_t row_begin = (int64_t)c0 * CH;
-    const int64_t rows = std::min<int64_t>(N, (int64_t)(c0 + nc) * CH) - row_begin;
+  // MODE: 0 strict filter after an exact sample, 1 non-strict filter over the whole store,
+  // 2 group-max sample pass (gmax = ws_s scratch, G groups per query)
+  auto filter_q256 = [&](int mode, int64_t row_begin, int64_t rows, int64_t nrb_target, int64_t min_rpw,
+                         int* G_out) {
     if (rows <= 0) return;
     const int nqb = (Qn + 255) / 256;
-    // ~1024 workgroups (4 per CU) over rows x query blocks, whole 64-row tiles per workgroup
-    const int64_t nrb_target = std::max<int64_t>(1, 1024 / nqb);
     int64_t rpw = (rows + nrb_target - 1) / nrb_target;
-    rpw = std::max<int64_t>(256, (rpw + 63) / 64 * 64);
+    rpw = std::max<int64_t>(min_rpw, (rpw + 63) / 64 * 64);
     const int nrb = (int)((rows + rpw - 1) / rpw);
+    const int G = 16 * nrb;
+    if (G_out) *G_out = G;
     dim3 grid(nrb * nqb);
-#define LAUNCH_Q(DD)                                                                                                \
-  knn_filter_q256_kernel<DD><<<grid, 512, 0, stream>>>((const bf16*)X.data_ptr(), N, (const bf16*)Q.data_ptr(), Qn, \
-                                                       ws_s.data_ptr<float>(), ws_i.data_ptr<int32_t>(), ctrl, cap,  \
-                                                       row_begin, (int)rpw, nqb)
+#define LAUNCH_Q(DD, MM)                                                                                         \
+  knn_filter_q256_kernel<DD, MM><<<grid, 512, 0, stream>>>(                                                      \
+      (const bf16*)X.data_ptr(), N, (const bf16*)Q.data_ptr(), Qn, ws_s.data_ptr<float>(),                      \
+      ws_i.data_ptr<int32_t>(), ctrl, cap, row_begin, (int)rpw, nqb, ws_s.data_ptr<float>(), G)
+#define LAUNCH_QM(DD)                     \
+  switch (mode) {                         \
+    case 0: LAUNCH_Q(DD, 0); break;       \
+    case 1: LAUNCH_Q(DD, 1); break;       \
+    default: LAUNCH_Q(DD, 2); break;      \
+  }
     switch (dim) {
-      case 128: LAUNCH_Q(128); break;
-      case 256: LAUNCH_Q(256); break;
-      case 384: LAUNCH_Q(384); break;
-      case 512: LAUNCH_Q(512); break;
+      case 128: LAUNCH_QM(128); break;
+      case 256: LAUNCH_QM(256); break;
+      case 384: LAUNCH_QM(384); break;
+      case 512: LAUNCH_QM(512); break;
       default: break;
     }
+#undef LAUNCH_QM
 #undef LAUNCH_Q
   };
   auto filter = [&](int c0, int nc) {
     if (q256) {
-      filter_q256(c0, nc);
+      // ~1024 workgroups (4 per CU) over rows x query blocks, whole 64-row tiles per workgroup
+      const int64_t row_begin = (int64_t)c0 * CH;
+      filter_q256(0, row_begin, std::min<int64_t>(N, (int64_t)(c0 + nc) * CH) - row_begin,
+                  std::max(1, 1024 / ((Qn + 255) / 256)), 256, nullptr);
       return;
     }
     dim3 grid(nc * nqf);
@@ -676,6 +753,24 @@ void knn_topk(at::Tensor X, at::Tensor Q, int64_t K, at::Tensor out_s, at::Tenso
                                                         out_i.data_ptr<int32_t>(), write_thr);
   };
   const int ns = sample <= 0 ? nchunks : (int)std::min<int64_t>(nchunks, sample);
+  // Large batches: the thresholds come from a group-max pass over the sample rows (an
+  // MFMA pass with a running-max epilogue, ~10x cheaper than the exact per-chunk top-K
+  // of the sample) and the filter then covers the whole store with scores >= thr.
+  const int64_t S = (int64_t)ns * CH;
+  if (q256 && ns < nchunks && K <= 64 && N >= 2 * S && !getenv("LS_KNN_EXACT_SAMPLE")) {
+    const int nqb = (Qn + 255) / 256;
+    const int64_t nrb_target = std::min<int64_t>(256, std::max<int64_t>(32, 256 / nqb));
+    const int64_t rpw = std::max<int64_t>(64, ((S + nrb_target - 1) / nrb_target + 63) / 64 * 64);
+    const int64_t G = 16 * ((S + rpw - 1) / rpw);
+    if ((int64_t)Qn * G <= ws_s.numel()) {
+      int Gk = 0;
+      filter_q256(2, 0, S, nrb_target, 64, &Gk);
+      knn_group_thr_kernel<<<(Qn + 3) / 4, 256, 0, stream>>>(ws_s.data_ptr<float>(), Gk, Qn, (int)K, ctrl);
+      filter_q256(1, 0, N, std::max(1, 1024 / nqb), 256, nullptr);
+      select(0);
+      return;
+    }
+  }
   exact(ns);
   if (ns < nchunks) {
     select(1);

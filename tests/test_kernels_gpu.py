@@ -381,6 +381,26 @@ def test_knn_topk_large_q(N, Qn, D, k, dup):
     del full
 
 
+@pytest.mark.parametrize("N,Qn,dup", [(140_000, 300, 0), (140_000, 2048, 70_000), (200_000, 1024, 0)])
+def test_knn_group_max_threshold_path_equals_exact(N, Qn, dup, monkeypatch):
+    """Q >= 128 over >= 64k rows: thresholds from the group-max sample pass
+    (knn_filter_q256_kernel MODE 2 + knn_group_thr_kernel) and a non-strict filter over
+    the whole store give the same answers, ties included (dup: every row twice), as the
+    exact-sample path and the all-exact search."""
+    torch.manual_seed(N + Qn)
+    X = torch.nn.functional.normalize(torch.randn(N, 384, device=DEV), dim=-1)
+    if dup:
+        X = X[torch.arange(N, device=DEV) % dup]
+    X = X.to(torch.bfloat16)
+    Q = torch.nn.functional.normalize(torch.randn(Qn, 384, device=DEV), dim=-1).to(torch.bfloat16)
+    s, i = ops.knn_topk(X, Q, 20)
+    s0, i0 = ops.knn_topk(X, Q, 20, sample_chunks=0)
+    assert torch.equal(s, s0) and torch.equal(i, i0)
+    monkeypatch.setenv("LS_KNN_EXACT_SAMPLE", "1")
+    s1, i1 = ops.knn_topk(X, Q, 20)
+    assert torch.equal(s1, s0) and torch.equal(i1, i0)
+
+
 def test_knn_topk_threshold_overflow_and_exact():
     """Rows get MORE similar to the queries further into the store, so the sample's
     K-th best is a weak threshold: candidate lists overflow and the search reruns
