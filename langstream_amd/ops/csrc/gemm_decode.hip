@@ -137,27 +137,41 @@ __device__ __forceinline__ int piece_chunk(int lane, int row) { return ((lane & 
 // --ablate, profiles/dgemm_ablation_r3.log): with every wave issuing its share of the
 // stage right after the barrier, a full DMA queue blocks the issuing wave before its
 // MFMAs, so a step costs DMA + compute instead of max(DMA, compute).
-template <int BN, int XS, int WS, int EPI, int ABL = 0, int LD = 0>
+template <int BN, int XS, int WS, int EPI, int ABL = 0, int LD = 0, int BMT = BM, int SPB = 1>
 __global__ void __launch_bounds__(LD ? 768 : 512) dgemm_kernel(const bf16* __restrict__ x, int64_t ldx,
                                                    const bf16* __restrict__ w, int M, int N, int K, int S,
                                                    bf16* __restrict__ out, int64_t ldo, float* __restrict__ part,
                                                    int F, unsigned* __restrict__ tickets, float* __restrict__ xchg,
                                                    int* __restrict__ err, int split_outer, DgArgs ga) {
   constexpr int WSTAGE = BN * BK * 2;
+  // BMT: rows of the tile (256, or 128 / 64 for small batches: rows past M are zeros the
+  // DMA still moves and the MFMAs still multiply, so a 64-row batch in a 256-row tile
+  // pays the 256-row X stream).  8 compute waves as WM x WN, IT x 16 rows each.
+  constexpr int IT = BMT == 64 ? 2 : 4;    // 16-row tiles per wave
+  constexpr int WM = BMT / (16 * IT);      // wave rows
+  constexpr int WN = 8 / WM;               // wave columns
+  constexpr int XST = BMT * BK * 2;        // X stage bytes
+  static_assert(BMT == 256 || BMT == 128 || BMT == 64, "tile rows");
   constexpr bool CMB = EPI == EPI_CMB_RES || EPI == EPI_CMB_QKV;
+  static_assert(BMT == 256 || !(CMB || EPI == EPI_SILU2 || EPI == EPI_SILU_R), "fused paths: 256-row tiles");
   constexpr bool SILU_LIKE = EPI == EPI_SILU || EPI == EPI_SILU_R;
   static_assert(!(CMB || EPI == EPI_SILU_R) || (BN == 128 && LD == 4), "fused epilogues: BN 128 + loader waves");
-  constexpr int JT = BN / 32;              // 16-col tiles per wave (wave = 64 rows x BN/2 cols)
-  constexpr int IT = 4;                    // 16-row tiles per wave
+  constexpr int JT = BN / (16 * WN);       // 16-col tiles per wave (wave = 16 IT rows x BN / WN cols)
+  static_assert(JT >= 2 || !(EPI == EPI_SILU || EPI == EPI_SILU2 || EPI == EPI_SILU_R), "SwiGLU pairs");
   constexpr int NLW = LD ? LD : 8;         // waves that issue the DMAs
-  constexpr int PX = 32 / NLW;             // X pieces per issuing wave per stage (32 per stage)
+  constexpr int PX = BMT / 8 / NLW;        // X pieces per issuing wave per stage (BMT / 8 per stage)
   constexpr int PW = BN / 8 / NLW;         // W pieces per issuing wave per stage
-  constexpr int XA = XS - 1, WA = WS - 1;  // stages issued ahead
+  // SPB: 64-deep K stages per barrier.  At small M a stage is a few MFMAs per wave and the
+  // barrier + LDS-read round trip per stage sets the rate; SPB = 2 halves the barriers
+  // (the ring then keeps SPB stages being read, so XS - SPB / WS - SPB are issued ahead).
+  constexpr int XA = XS - SPB, WA = WS - SPB;  // stages issued ahead
+  static_assert(SPB == 1 || SPB == 2, "stages per barrier");
+  static_assert(SPB == 1 || (ABL & ~(16 | 128)) == 0, "ablations: one stage per barrier");
   static_assert(XA >= 1 && WA >= XA, "W is issued at least as far ahead as X");
-  static_assert(XS * XSTAGE + WS * WSTAGE <= LDS_MAX, "LDS budget");
-  __shared__ __attribute__((aligned(1024))) char lds[XS * XSTAGE + WS * WSTAGE];
+  static_assert(XS * XST + WS * WSTAGE <= LDS_MAX, "LDS budget");
+  __shared__ __attribute__((aligned(1024))) char lds[XS * XST + WS * WSTAGE];
   char* const lx0 = lds;
-  char* const lw0 = lds + XS * XSTAGE;
+  char* const lw0 = lds + XS * XST;
 
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -203,7 +217,7 @@ __global__ void __launch_bounds__(LD ? 768 : 512) dgemm_kernel(const bf16* __res
   const unsigned lxa = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)lx0;
   const unsigned lwa = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)lw0;
   auto issue_x = [&](int t) {
-    const unsigned dst = lxa + (t % XS) * XSTAGE + (PX * lw) * 1024;
+    const unsigned dst = lxa + (t % XS) * XST + (PX * lw) * 1024;
 #pragma unroll
     for (int j = 0; j < PX; ++j) blds16<false>(xrs, xvo[j], t * BK * 2, dst + j * 1024);
   };
@@ -217,17 +231,17 @@ __global__ void __launch_bounds__(LD ? 768 : 512) dgemm_kernel(const bf16* __res
 
   // ---- fragments
   const int cw = computer ? wid : 0;       // loaders: any valid layout, never used
-  const int wm = cw >> 1, wn = cw & 1;
+  const int wm = cw / WN, wn = cw % WN;
   const int fr = lane & 15, h = lane >> 4;
   const int fsw = (fr >> 1) & 7;           // = (row >> 1) & 7 of every fragment row
   auto bcol = [&](int j) {                 // tile-local W row of this lane's B fragment
     if constexpr (EPI == EPI_SILU || EPI == EPI_SILU2 || EPI == EPI_SILU_R)
-      return (j < JT / 2 ? (BN / 4) * wn + 16 * j : BN / 2 + (BN / 4) * wn + 16 * (j - JT / 2)) + fr;
-    return (BN / 2) * wn + 16 * j + fr;
+      return (j < JT / 2 ? (BN / (2 * WN)) * wn + 16 * j : BN / 2 + (BN / (2 * WN)) * wn + 16 * (j - JT / 2)) + fr;
+    return (BN / WN) * wn + 16 * j + fr;
   };
   int aoff[IT], boff[JT];
 #pragma unroll
-  for (int i = 0; i < IT; ++i) aoff[i] = (64 * wm + 16 * i + fr) * 128;
+  for (int i = 0; i < IT; ++i) aoff[i] = (16 * IT * wm + 16 * i + fr) * 128;
 #pragma unroll
   for (int j = 0; j < JT; ++j) boff[j] = bcol(j) * 128;
 
@@ -252,19 +266,33 @@ __global__ void __launch_bounds__(LD ? 768 : 512) dgemm_kernel(const bf16* __res
     }
   };
   for (int u = -WA; u < 0; ++u) issue_step(u);
-  for (int t = 0; t < nks; ++t) {
-    const int nx = max(0, min(t + XA - 1, nks - 1) - t);                       // X(t+1 .. t+XA-1)
-    const int nw = max(0, min(t + WA - 1, nks - 1) - (t - XA + WA) + 1);       // W(t-XA+WA .. t+WA-1)
+  for (int t = 0; t < nks; t += SPB) {
     if (loader) {
-      if constexpr ((ABL & 12) == 0) wait_vmcnt_dyn(PX * nx + PW * nw);
-      else if constexpr ((ABL & 4) == 0) wait_vmcnt_dyn(PX * nx);
+      if constexpr (SPB == 1) {
+        const int nx = max(0, min(t + XA - 1, nks - 1) - t);                       // X(t+1 .. t+XA-1)
+        const int nw = max(0, min(t + WA - 1, nks - 1) - (t - XA + WA) + 1);       // W(t-XA+WA .. t+WA-1)
+        if constexpr ((ABL & 12) == 0) wait_vmcnt_dyn(PX * nx + PW * nw);
+        else if constexpr ((ABL & 4) == 0) wait_vmcnt_dyn(PX * nx);
+      } else {
+        // stages t .. t+SPB-1 must have landed: the last of their DMAs is X(t+SPB-1),
+        // issued by step u0; count what was issued after it (W(u0+WA), steps u0+1 .. t-1)
+        const int u0 = t + SPB - 1 - XA;
+        int cnt = (u0 + WA >= 0 && u0 + WA < nks) ? PW : 0;
+        for (int u = u0 + 1; u < t; ++u)
+          cnt += ((u + XA >= 0 && u + XA < nks) ? PX : 0) + ((u + WA >= 0 && u + WA < nks) ? PW : 0);
+        wait_vmcnt_dyn(cnt);
+      }
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // step t-1's fragment reads are done
-    __builtin_amdgcn_s_barrier();                         // every wave: stage t landed, t-1 read
-    issue_step(t);                                        // into the slots of stage t-1
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the previous stages' fragment reads are done
+    __builtin_amdgcn_s_barrier();                         // every wave: stages t.. landed, t-SPB.. read
+#pragma unroll
+    for (int sp = 0; sp < SPB; ++sp) issue_step(t + sp);  // into the slots of stages t-SPB ..
     if (!computer) continue;
-    const char* lx = lx0 + (t % XS) * XSTAGE;
-    const char* lw = lw0 + (t % WS) * WSTAGE;
+#pragma unroll
+    for (int sp = 0; sp < SPB; ++sp) {
+    if (t + sp >= nks) break;
+    const char* lx = lx0 + ((t + sp) % XS) * XST;
+    const char* lw = lw0 + ((t + sp) % WS) * WSTAGE;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const int off = 16 * ((4 * ks + h) ^ fsw);
@@ -292,11 +320,12 @@ __global__ void __launch_bounds__(LD ? 768 : 512) dgemm_kernel(const bf16* __res
         for (int j = 0; j < JT; ++j) asm volatile("" ::"v"(b[j]));
       }
     }
+    }
   }
   wait_vmcnt<0>();  // no LDS-DMA may outlive the workgroup
 
-  // acc[i][j][r] = C[64wm + 16i + 4h + r][tile col of bcol(j)]
-  const int rbase = 64 * wm + 4 * h;
+  // acc[i][j][r] = C[16 IT wm + 16i + 4h + r][tile col of bcol(j)]
+  const int rbase = 16 * IT * wm + 4 * h;
   if constexpr (EPI == EPI_SILU2) {
     // ---- in-launch combine of the two K halves (see the header); with loader waves
     // (LD = 4) only the 512 compute threads hold accumulators, the loaders only join
@@ -353,7 +382,7 @@ __global__ void __launch_bounds__(LD ? 768 : 512) dgemm_kernel(const bf16* __res
         for (int r = 0; r < 4; ++r) {
           const int m = rbase + 16 * i + r;
           if (m < M)
-            out[(int64_t)m * ldo + tile * (BN / 2) + (BN / 4) * wn + fr + 16 * j] =
+            out[(int64_t)m * ldo + tile * (BN / 2) + (BN / (2 * WN)) * wn + fr + 16 * j] =
                 (bf16)(g[r] / (1.f + __expf(-g[r])) * u[r]);
         }
       }
@@ -374,17 +403,17 @@ __global__ void __launch_bounds__(LD ? 768 : 512) dgemm_kernel(const bf16* __res
       r_pre = rms_scale(ga.sumsq_in + (int64_t)(rr0 + threadIdx.x) * ga.npart, ga.npart, ga.inv_h, ga.eps);
   }
   constexpr int TP = BN + 4;
-  constexpr int PASS_ROWS = BM * TP * 4 <= XS * XSTAGE + WS * WSTAGE ? BM : BM / 2;
-  static_assert(PASS_ROWS * TP * 4 <= XS * XSTAGE + WS * WSTAGE, "epilogue pass must fit the ring's LDS");
+  constexpr int PASS_ROWS = BMT * TP * 4 <= XS * XST + WS * WSTAGE ? BMT : BMT / 2;
+  static_assert(PASS_ROWS * TP * 4 <= XS * XST + WS * WSTAGE, "epilogue pass must fit the ring's LDS");
   constexpr int NT = LD ? 768 : 512;
   float* T = reinterpret_cast<float*>(lds);
   // SILU_R: the row scales 1/rms(h) after T (LDS past 256 x 132 floats is free)
   float* rbuf = reinterpret_cast<float*>(lds + PASS_ROWS * TP * 4);
-  if constexpr (EPI == EPI_SILU_R) static_assert(PASS_ROWS == BM && BM * TP * 4 + BM * 4 <= LDS_MAX, "r buffer");
+  if constexpr (EPI == EPI_SILU_R) static_assert(PASS_ROWS == BMT && BMT * TP * 4 + BMT * 4 <= LDS_MAX, "r buffer");
 #pragma unroll
-  for (int r0 = 0; r0 < BM; r0 += PASS_ROWS) {
+  for (int r0 = 0; r0 < BMT; r0 += PASS_ROWS) {
     __syncthreads();                                    // ring reads / the previous pass are done
-    if (computer && 64 * wm >= r0 && 64 * wm < r0 + PASS_ROWS) {
+    if (computer && 16 * IT * wm >= r0 && 16 * IT * wm < r0 + PASS_ROWS) {
 #pragma unroll
       for (int i = 0; i < IT; ++i)
 #pragma unroll
@@ -599,11 +628,15 @@ int ntst_default() { return env_int("LS_DGEMM_NTST", 1); }
 
 // ring shapes: BN = 128: X 3 slots (2 ahead) + W 4 slots (3 ahead) = 160 KB;
 // BN = 256: X 2 + W 3 = 160 KB.
-template <int BN, int EPI>
-void dgemm_launch(int S, int tiles, hipStream_t st, const at::Tensor& x, const at::Tensor& w, int M, int N, int K,
-                  bf16* out, int64_t ldo, float* part, int F, unsigned* tickets, float* xchg, int* err,
-                  DgArgs ga = DgArgs()) {
-  constexpr int XS = BN == 128 ? 3 : 2, WS = BN == 128 ? 4 : 3;
+template <int BN, int EPI, int BMT>
+void dgemm_launch_bm(int S, int tiles, hipStream_t st, const at::Tensor& x, const at::Tensor& w, int M, int N, int K,
+                     bf16* out, int64_t ldo, float* part, int F, unsigned* tickets, float* xchg, int* err,
+                     const DgArgs& ga) {
+  // small tiles: two stages per barrier and the LDS they leave as a deeper W ring (8 / 6
+  // slots at 64 / 128 rows: 96 / 64 KB of weights issued ahead)
+  constexpr int SPB = BMT == BM ? 1 : 2;
+  constexpr int XS = BN != 128 ? 2 : BMT == BM ? 3 : 4;
+  constexpr int WS = BN != 128 ? 3 : BMT == 64 ? 8 : BMT == 128 ? 6 : 4;
   // BN = 256: 8 compute waves need 128 accumulator VGPRs each, no room for a third wave
   // per SIMD.  (Streaming the B fragments one at a time fits 168 VGPRs with 4 loader
   // waves, but the gate_up K-half exchange form then measured 90 vs 82 us:
@@ -618,15 +651,42 @@ void dgemm_launch(int S, int tiles, hipStream_t st, const at::Tensor& x, const a
   const int pol = LDW == 4 ? (wnt_default() ? 16 : 0) | (ntst_default() ? 128 : 0) : 0;
 #define POL_(A)                                                                                                  \
   case A:                                                                                                        \
-    dgemm_kernel<BN, XS, WS, EPI, A, LDW><<<dim3(tiles * S), 768, 0, st>>>(                                      \
+    dgemm_kernel<BN, XS, WS, EPI, A, LDW, BMT, SPB><<<dim3(tiles * S), 768, 0, st>>>(                                 \
         (const bf16*)x.data_ptr(), x.stride(0), (const bf16*)w.data_ptr(), M, N, K, S, out, ldo, part, F, tickets, \
         xchg, err, so, ga);                                                                                      \
     return;
-  switch (pol) { POL_(16) POL_(128) POL_(144) default: break; }
+  if constexpr (BMT == BM) {
+    switch (pol) { POL_(16) POL_(128) POL_(144) default: break; }
+  } else {
+    switch (pol) { POL_(144) default: break; }
+  }
 #undef POL_
-  dgemm_kernel<BN, XS, WS, EPI, 0, LDW><<<dim3(tiles * S), LDW ? 768 : 512, 0, st>>>((const bf16*)x.data_ptr(), x.stride(0),
-                                                                 (const bf16*)w.data_ptr(), M, N, K, S, out, ldo,
-                                                                 part, F, tickets, xchg, err, so, ga);
+  dgemm_kernel<BN, XS, WS, EPI, 0, LDW, BMT, SPB><<<dim3(tiles * S), LDW ? 768 : 512, 0, st>>>(
+      (const bf16*)x.data_ptr(), x.stride(0), (const bf16*)w.data_ptr(), M, N, K, S, out, ldo, part, F, tickets, xchg,
+      err, so, ga);
+}
+
+// Tile rows by batch: 64- and 128-row tiles for M <= 64 / <= 128 (BN = 128, plain /
+// split-K / SwiGLU epilogues; LS_DGEMM_SMALL_BM=0 keeps every batch on 256-row tiles).
+int small_bm_default() { return env_int("LS_DGEMM_SMALL_BM", 1); }
+
+template <int BN, int EPI>
+void dgemm_launch(int S, int tiles, hipStream_t st, const at::Tensor& x, const at::Tensor& w, int M, int N, int K,
+                  bf16* out, int64_t ldo, float* part, int F, unsigned* tickets, float* xchg, int* err,
+                  DgArgs ga = DgArgs()) {
+  if constexpr (BN == 128 && (EPI == EPI_STORE || EPI == EPI_PARTIAL || EPI == EPI_SILU)) {
+    if (small_bm_default()) {
+      if (M <= 64) {
+        dgemm_launch_bm<BN, EPI, 64>(S, tiles, st, x, w, M, N, K, out, ldo, part, F, tickets, xchg, err, ga);
+        return;
+      }
+      if (M <= 128) {
+        dgemm_launch_bm<BN, EPI, 128>(S, tiles, st, x, w, M, N, K, out, ldo, part, F, tickets, xchg, err, ga);
+        return;
+      }
+    }
+  }
+  dgemm_launch_bm<BN, EPI, BM>(S, tiles, st, x, w, M, N, K, out, ldo, part, F, tickets, xchg, err, ga);
 }
 
 void check_xw(const at::Tensor& x, const at::Tensor& w) {

@@ -644,6 +644,64 @@ __global__ void __launch_bounds__(256) knn_select_kernel(const float* __restrict
   }
 }
 
+// Long candidate lists (the group-max path: ~K * N / sample-rows per query): one
+// WORKGROUP per query, its 4 waves each keep the best 64 of every 4th batch (the loop of
+// knn_select_kernel), then wave 0 merges the four sorted lists from LDS.  A quarter of
+// the serial batch chain per wave, and 4x the waves in flight.
+__global__ void __launch_bounds__(256) knn_select4_kernel(const float* __restrict__ cand_s,
+                                                          const int32_t* __restrict__ cand_i,
+                                                          const int* __restrict__ ctrl, int Qn, int64_t cap, int K,
+                                                          float* __restrict__ out_s, int32_t* __restrict__ out_i) {
+  __shared__ float lv[4][64];
+  __shared__ int lr[4][64];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int qi = blockIdx.x;
+  const int n = (int)min((int64_t)ctrl[qi], cap);
+  const float* cs = cand_s + (int64_t)qi * cap;
+  const int32_t* ci = cand_i + (int64_t)qi * cap;
+  float bv = -INFINITY;
+  int br = INT_MAX;
+  float nv = -INFINITY;
+  int nr = INT_MAX;
+  if (wid * 64 + lane < n) {
+    nv = cs[wid * 64 + lane];
+    nr = ci[wid * 64 + lane];
+  }
+  for (int base = wid * 64; base < n; base += 256) {
+    float v = nv;
+    int r = nr < 0 || v == -INFINITY ? INT_MAX : nr;
+    nv = -INFINITY;
+    nr = INT_MAX;
+    if (base + 256 + lane < n) {
+      nv = cs[base + 256 + lane];
+      nr = ci[base + 256 + lane];
+    }
+    const float kv = __shfl(bv, K - 1, 64);
+    const int kr = __shfl(br, K - 1, 64);
+    if (__ballot(v > kv || (v == kv && r < kr)) == 0) continue;
+    wave_sort_desc(v, r, lane);
+    const float ov = __shfl(v, 63 - lane, 64);
+    const int orr = __shfl(r, 63 - lane, 64);
+    if (ov > bv || (ov == bv && orr < br)) { bv = ov; br = orr; }
+    wave_merge_desc(bv, br, lane);
+  }
+  lv[wid][lane] = bv;
+  lr[wid][lane] = br;
+  __syncthreads();
+  if (wid != 0) return;
+#pragma unroll
+  for (int w = 1; w < 4; ++w) {
+    const float ov = lv[w][63 - lane];
+    const int orr = lr[w][63 - lane];
+    if (ov > bv || (ov == bv && orr < br)) { bv = ov; br = orr; }
+    wave_merge_desc(bv, br, lane);
+  }
+  if (lane < K) {
+    out_s[(int64_t)qi * K + lane] = bv;
+    out_i[(int64_t)qi * K + lane] = bv > -INFINITY && br != INT_MAX ? br : -1;
+  }
+}
+
 }  // namespace
 
 // X: [N, dim] bf16 (rows L2-normalised), Q: [Qn, dim] bf16.  Returns via out tensors
@@ -767,7 +825,8 @@ void knn_topk(at::Tensor X, at::Tensor Q, int64_t K, at::Tensor out_s, at::Tenso
       filter_q256(2, 0, S, nrb_target, 64, &Gk);
       knn_group_thr_kernel<<<(Qn + 3) / 4, 256, 0, stream>>>(ws_s.data_ptr<float>(), Gk, Qn, (int)K, ctrl);
       filter_q256(1, 0, N, std::max(1, 1024 / nqb), 256, nullptr);
-      select(0);
+      knn_select4_kernel<<<Qn, 256, 0, stream>>>(ws_s.data_ptr<float>(), ws_i.data_ptr<int32_t>(), ctrl, Qn, cap,
+                                                 (int)K, out_s.data_ptr<float>(), out_i.data_ptr<int32_t>());
       return;
     }
   }

@@ -48,6 +48,53 @@ def test_llama_prefill_logits_match_cpu():
         assert len(set(t for t, _ in g.top) & set(cmap)) >= 10
 
 
+def _step_tops(e: LLMEngine, prompts, n_gen: int, n_top=10):
+    """Per prompt, the top-n (id, logprob) alternatives of each generated token."""
+    events = {}
+    reqs = [e.submit(p, SamplingParams(max_tokens=n_gen, temperature=0.0, ignore_eos=True, logprobs=n_top),
+                     callback=lambda ev, i=i: events.setdefault(i, []).append(ev)) for i, p in enumerate(prompts)]
+    while not all(r.finished for r in reqs):
+        e.step()
+    e._flush()
+    return [events[i] for i in range(len(prompts))]
+
+
+def _close_tops(g, c, tol=0.05):
+    cmap = dict(c.top)
+    assert g.token_id in cmap and cmap[g.token_id] >= c.top[0][1] - tol
+    assert abs(g.top[0][1] - c.top[0][1]) < tol
+
+
+@pytest.mark.parametrize("M", [5, 33, 64, 100, 128, 300, 700])
+def test_runner_projection_routing_at_m_rows_matches_fp32(M):
+    """Every projection route of LlamaRunner at M rows against the same weights in fp32 on
+    the CPU: a prefill step of M tokens (one prompt) and a decode-only step of M rows (M
+    sequences).  5..128 rows run the 256-row decode GEMM (rows past M read as zeros) and
+    the skinny kernels, 300 / 700 the decode GEMM in 256-row blocks; no library GEMM."""
+    cfg = PRESETS["llama-small"]
+    gpu = LlamaModel(cfg, device="cuda")
+    cpu = _cpu_copy(gpu)
+    torch.manual_seed(M)
+    # prefill of M rows
+    prompt = [[int(t) for t in torch.randint(5, 30000, (M,))]]
+    kw = dict(num_blocks=2048, max_model_len=1024, max_batch=1024, max_prefill_tokens=4096)
+    g = _first_token_tops(LLMEngine(gpu, None, **kw), prompt)[0]
+    c = _first_token_tops(LLMEngine(cpu, None, **kw), prompt)[0]
+    _close_tops(g, c)
+    # decode-only step of M rows: M prompts of 3 tokens prefilled together, then every
+    # sequence decodes its second token in one step
+    prompts = [[int(t) for t in torch.randint(5, 30000, (3,))] for _ in range(M)]
+    eg = _step_tops(LLMEngine(gpu, None, use_graphs=False, **kw), prompts, 2)
+    ec = _step_tops(LLMEngine(cpu, None, **kw), prompts, 2)
+    same = 0
+    for a, b in zip(eg, ec):
+        _close_tops(a[0], b[0])
+        if a[0].token_id == b[0].token_id:   # else a near-tie split the inputs of step 2
+            _close_tops(a[1], b[1])
+            same += 1
+    assert same >= 0.8 * M
+
+
 def test_native_runner_matches_python_forward():
     """The C++ LlamaRunner and the Python op-by-op forward issue the same kernels:
     logits must agree to bf16 rounding on a two-sequence prefill."""
