@@ -222,10 +222,11 @@ class ShardedKnn:
                 hdr = {"s": stopping, "r": [[r.coll, int(r.q.shape[0]), r.k, r.inc, int(r.q.shape[1])] for r in take]}
                 t_h = time.perf_counter()
                 hdrs = [json.loads(b) for b in self._allgather_bytes(json.dumps(hdr).encode())]
-                self.stats["header_s"] += time.perf_counter() - t_h
+                dt_h = time.perf_counter() - t_h
                 if all(h["s"] for h in hdrs):
                     return
                 if not any(h["r"] for h in hdrs):
+                    self.stats["idle_header_s"] = self.stats.get("idle_header_s", 0.0) + dt_h
                     # idle: back off (tick, 2 tick, ... up to max_idle_s) so an idle service
                     # does not run a collective every millisecond next to the engines; a
                     # local request wakes this rank at once, remote ones within the backoff
@@ -235,6 +236,7 @@ class ShardedKnn:
                             self._cv.wait(min(self.max_idle_s, self.tick_s * (1 << min(idle, 10))))
                     continue
                 idle = 0
+                self.stats["header_s"] += dt_h   # rounds with work only (idle polls: idle_header_s)
                 self.rounds += 1
                 self.stats["rounds"] += 1
                 self.stats["queries"] += sum(int(r.q.shape[0]) for r in take)
@@ -364,24 +366,27 @@ class ShardedKnn:
             # this rank owns are served directly (no serialisation, no exchange)
             t_p = time.perf_counter()
 
-            def serve(asked):
+            def serve(asked, as_bytes=True):
+                # vectors: one gathered float32 block per collection; remote askers get each
+                # row's bytes, this rank's own results keep the numpy row (no round trip)
                 ans = {}
                 for coll, rws in asked.items():
                     st = stores.get(coll)
                     if st is None:
                         continue
                     try:
-                        rws = sorted(rws)
-                        vecs = st.row_vectors(rws) if coll in vec_colls else {}
-                        ans[coll] = {rw: (st.row_payload(rw),
-                                          np.asarray(vecs[rw], np.float32).tobytes() if rw in vecs else None)
-                                     for rw in rws if 0 <= rw < len(st)}
+                        rws = [rw for rw in sorted(rws) if 0 <= rw < len(st)]
+                        vecs = {}
+                        if coll in vec_colls and rws:
+                            flat, arr = st.row_vectors_array(rws)
+                            vecs = {rw: (arr[i].tobytes() if as_bytes else arr[i]) for i, rw in enumerate(flat)}
+                        ans[coll] = {rw: (st.row_payload(rw), vecs.get(rw)) for rw in rws}
                     except Exception as e:  # noqa: BLE001 - tell the asker instead of skipping the exchange
                         log.exception("sharded kNN: payloads of %s failed", coll)
                         ans.setdefault("__errors__", {})[coll] = f"{type(e).__name__}: {e}"
                 return ans
 
-            local = serve(need[me])
+            local = serve(need[me], as_bytes=False)
             asks = [b"" if d == me else msgpack.packb({c: sorted(v) for c, v in need[d].items()}) for d in range(W)]
             got_asks = [msgpack.unpackb(b, strict_map_key=False) if b else {} for b in self._alltoall_bytes(asks)]
             answers = [b"" if src == me else msgpack.packb(serve(got_asks[src]), use_bin_type=True)
@@ -412,7 +417,8 @@ class ShardedKnn:
                     d = dict(p[0])
                     d["similarity"] = sc
                     if r.inc and p[1] is not None:
-                        d["vector"] = np.frombuffer(p[1], np.float32).tolist()
+                        v = p[1]
+                        d["vector"] = (v if isinstance(v, np.ndarray) else np.frombuffer(v, np.float32)).tolist()
                     res.append(d)
                 out.append(res)
             r.fut.set_result(out)

@@ -460,13 +460,19 @@ class VectorStore:
         return d
 
     def row_vectors(self, rows) -> Dict[int, List[float]]:
+        flat, arr = self.row_vectors_array(rows)
+        return dict(zip(flat, arr.tolist())) if flat else {}
+
+    def row_vectors_array(self, rows):
+        """(sorted rows, float32 numpy [n, dim]): one device gather + one D2H copy, no
+        per-float Python objects (the sharded kNN ships these rows as bytes)."""
         flat = sorted(rows)
         if not flat:
-            return {}
+            return flat, np.zeros((0, self.dim), np.float32)
         with on_search(self.device):
             self._order_read()
-            vv = to_host(self._vecs[torch.tensor(flat, device=self.device)].float())[0].tolist()
-        return dict(zip(flat, vv))
+            arr = to_host(self._vecs[torch.tensor(flat, device=self.device)].float())[0].numpy()
+        return flat, arr
 
 
 def _exact_topk(X: torch.Tensor, q: torch.Tensor, k: int, chunk: int = 1 << 20):
