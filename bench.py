@@ -293,69 +293,7 @@ def _stream_summary(gathered, args, world):
                     f"window count, the window drains them"}
 
 
-def make_page(i: int, corpus) -> str:
-    """A crawled page: ~12 paragraphs of corpus sentences."""
-    return "\n\n".join(" ".join(corpus[(i * 31 + p * 7 + j) % len(corpus)] for j in range(5)) for p in range(12))
-
-
-class Site:
-    """Local HTTP site the crawler walks: /step/<n>/index.html lists that step's pages
-    and links the next step's index, which long-polls until the step is published."""
-
-    def __init__(self, corpus, per_step: int):
-        import http.server
-        self.corpus, self.per_step = corpus, per_step
-        self.published = -1
-        self.cv = threading.Condition()
-        site = self
-
-        class H(http.server.BaseHTTPRequestHandler):
-            protocol_version = "HTTP/1.1"
-            # headers and body leave in separate writes: with Nagle on, the body waits for
-            # the client's delayed ACK of the headers (~40 ms per page on loopback)
-            disable_nagle_algorithm = True
-
-            def log_message(self, *a):
-                pass
-
-            def do_GET(self):
-                parts = self.path.strip("/").split("/")
-                if len(parts) != 3 or parts[0] != "step":
-                    return self._send(404, b"")
-                step = int(parts[1])
-                with site.cv:
-                    site.cv.wait_for(lambda: site.published >= step, timeout=1800)
-                if site.published < step:
-                    return self._send(503, b"")
-                if parts[2] == "index.html":
-                    links = "".join(f'<a href="/step/{step}/{d}.html">p{d}</a>' for d in range(site.per_step))
-                    body = f'<html><body>{links}<a href="/step/{step + 1}/index.html">next</a></body></html>'
-                else:
-                    d = int(parts[2].split(".")[0])
-                    text = make_page(step * site.per_step + d, site.corpus)
-                    body = "<html><body>" + "".join(f"<p>{p}</p>" for p in text.split("\n\n")) + "</body></html>"
-                self._send(200, body.encode())
-
-            def _send(self, code, body):
-                self.send_response(code)
-                self.send_header("Content-Type", "text/html; charset=utf-8")
-                self.send_header("Content-Length", str(len(body)))
-                self.end_headers()
-                self.wfile.write(body)
-
-        self.httpd = http.server.ThreadingHTTPServer(("127.0.0.1", 0), H)
-        self.httpd.daemon_threads = True
-        self.url = f"http://127.0.0.1:{self.httpd.server_address[1]}"
-        threading.Thread(target=self.httpd.serve_forever, daemon=True).start()
-
-    def publish(self, step: int) -> None:
-        with self.cv:
-            self.published = step
-            self.cv.notify_all()
-
-    def close(self) -> None:
-        self.publish(1 << 30)
-        self.httpd.shutdown()
+from langstream_amd.bench.site import Site, SiteProcess, make_page  # noqa: E402
 
 
 def main():
@@ -409,6 +347,17 @@ def main():
         sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     if args.config != "rag":
         return _other_config(args, rank, world, local)
+    corpus_sentences = max(4000, args.corpus // 4 + 1)
+    crawl = args.docs > 0 and not args.no_crawl
+    site = None
+    if crawl and rank == 0:
+        # the crawl target runs in its own process (started before the GPU is touched);
+        # LS_BENCH_SITE_INPROC=1 serves it from this rank's interpreter as before
+        if os.environ.get("LS_BENCH_SITE_INPROC") == "1":
+            from langstream_amd.tokenizers import builtin_corpus as _bc
+            site = Site(_bc(corpus_sentences), args.docs * world)
+        else:
+            site = SiteProcess(args.docs * world, corpus_sentences)
 
     import torch
     import torch.distributed as dist
@@ -454,9 +403,7 @@ def main():
     fmt = dict(chat_model=chat_model, embed_model=embed_model, max_tokens=args.max_tokens,
                max_batch=max(args.batch, 1), max_len=4096, prefill=args.prefill_chunk, q_parts=q_parts, d_parts=d_parts,
                shm=shm, shm_mb=shm_mb)
-    corpus = builtin_corpus(max(4000, args.corpus // 4 + 1))
-    crawl = args.docs > 0 and not args.no_crawl
-    site = Site(corpus, args.docs * world) if crawl and rank == 0 else None
+    corpus = builtin_corpus(corpus_sentences)
     files = {"pipeline.yaml": APP.format(**fmt), "ingest.yaml": INGEST.format(**fmt),
              "configuration.yaml": CONFIGURATION.format(**fmt)}
     if crawl:
