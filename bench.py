@@ -358,6 +358,13 @@ def main():
             site = Site(_bc(corpus_sentences), args.docs * world)
         else:
             site = SiteProcess(args.docs * world, corpus_sentences)
+    # the webcrawler source (once, on rank 0) in an interpreter of its own, as its own pod
+    # would be: pre-started here, before the GPU is touched, and handed the app later;
+    # LS_BENCH_CRAWLER_INPROC=1 runs it as a thread of rank 0's runner instead
+    crawler_host = None
+    if crawl and rank == 0 and os.environ.get("LS_BENCH_CRAWLER_INPROC") != "1":
+        from langstream_amd.runtime.agent_host import AgentHostProcess
+        crawler_host = AgentHostProcess()
 
     import torch
     import torch.distributed as dist
@@ -433,7 +440,8 @@ def main():
                                            "max-model-len": 4096, "max-prefill-tokens": args.prefill_chunk})
     if multi:
         dist_knn.start(device=device)
-    only = None if rank == 0 else ["query", "ingest"]   # the crawler runs once (rank 0)
+    # the crawler runs once (rank 0), in its own process unless LS_BENCH_CRAWLER_INPROC=1
+    only = None if rank == 0 and crawler_host is None else ["query", "ingest"]
     if os.environ.get("LS_STAGE_TRACE", "0") != "0":
         _composite.STAGE_TRACE = []
         from langstream_amd.engine import vector_store as _vs
@@ -441,6 +449,10 @@ def main():
     runner = LocalApplicationRunner.from_yaml(files, instance=INSTANCE.format(**fmt), application_id="rag-bench",
                                               services=services, agents=only)
     runner.start()
+    if crawler_host is not None:
+        import tempfile
+        crawler_host.start(files, INSTANCE.format(**fmt), "rag-bench", ["crawler"],
+                           state_dir=tempfile.mkdtemp(prefix="rag-bench-crawler-"))
     log = runner.topic_runtime.log
     barrier()
     prod = runner.producer("questions-topic")
@@ -496,6 +508,8 @@ def main():
                 t_all = time.time()
             if runner.errors:
                 raise runner.errors[0]
+            if crawler_host is not None and not crawler_host.alive():
+                raise RuntimeError("the crawler agent process exited")
             if time.time() > deadline:
                 raise TimeoutError(f"rank {rank}: {args.batch - len(lats)} answers missing; documents end "
                                    f"{log.end_offsets('documents-topic')} committed "
@@ -674,6 +688,8 @@ def main():
             "prefill_step_tokens_rank0": list(llm.prefill_step_tokens)[-40:],
         }), flush=True)
     barrier()
+    if crawler_host is not None:
+        crawler_host.stop()
     runner.stop(timeout=10)
     if multi:
         dist_knn.stop()
