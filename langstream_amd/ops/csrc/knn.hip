@@ -338,6 +338,11 @@ __global__ void __launch_bounds__(256) knn_filter_kernel(const bf16* __restrict_
 //     16-query groups share each fragment);
 //   * scores above the query's sample threshold are appended exactly as in
 //     knn_filter_kernel (same candidate lists, counters and overflow flags).
+// Measured at Q = 2048 over 1M x 384 (profiles/knn_pmc_*, r4): MFMA busy ~41 %, waves
+// parked in waitcnt / barrier ~49 %, L2 hit 85 %, LDS array ~23 % busy.  Dead ends: a
+// one-ballot epilogue test + buffer-resource DMA addressing + pinned fragment reads (VALU
+// per MFMA 5.7 -> ~1.5 in the loop: no change in time), moving the barrier to mid-tile
+// so the next tile's first fragments load under this tile's last MFMAs (1.607 vs 1.598 ms).
 //
 // MODE 0: append scores > thr (the rows after an exact sample, see above);
 // MODE 1: append scores >= thr over the WHOLE store (thr from a MODE 2 pass: a lower
@@ -517,6 +522,23 @@ __global__ void __launch_bounds__(512) knn_filter_q256_kernel(const bf16* __rest
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) f[ks] = __builtin_bit_cast(bf16x8, ld16(st + i * 16 * RB + aoff[ks]));
     };
+    if constexpr (DIM > 384) {
+      // one fragment set: two of them beside the query fragments exceed 256 VGPRs
+      rd(0, fa);
+      mm(fa, accA);
+      if (pend >= 0) epi(pend, accB);
+      rd(1, fa);
+      mm(fa, accB);
+      epi(tl0, accA);
+      rd(2, fa);
+      mm(fa, accA);
+      epi(tl0 + 16, accB);
+      rd(3, fa);
+      mm(fa, accB);
+      epi(tl0 + 32, accA);
+      pend = tl0 + 48;
+      continue;
+    }
     // sched_barriers pin each subtile's reads ahead of the previous subtile's MFMAs:
     // left alone, hipcc sinks every read to just before its MFMA behind an lgkmcnt wait
 #define KNN_SB __builtin_amdgcn_sched_barrier(0)
@@ -543,6 +565,7 @@ __global__ void __launch_bounds__(512) knn_filter_q256_kernel(const bf16* __rest
   }
   if (pend >= 0) epi(pend, accB);
   wait_vmcnt<0>();   // no LDS-DMA may outlive the workgroup
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   if constexpr (MODE == 2) {
 #pragma unroll
     for (int g = 0; g < 2; ++g) {
