@@ -71,16 +71,10 @@ def main(argv=None) -> int:
 
 class LoadProcess:
     def __init__(self, bootstrap: str, rank: int, world: int, batch: int, read: bool, timeout: float):
-        import os
-        import subprocess
-        root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-        env = dict(os.environ, PYTHONPATH=os.pathsep.join([root, os.environ.get("PYTHONPATH", "")]).rstrip(os.pathsep),
-                   CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
-        cmd = [sys.executable, "-m", "langstream_amd.bench.embed_load", "--bootstrap", bootstrap,
-               "--rank", str(rank), "--world", str(world), "--batch", str(batch), "--timeout", str(timeout)]
-        if read:
-            cmd.append("--read")
-        self.proc = subprocess.Popen(cmd, stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True, env=env)
+        from ..utils.procs import spawn_module
+        args = ["--bootstrap", bootstrap, "--rank", str(rank), "--world", str(world), "--batch", str(batch),
+                "--timeout", str(timeout)] + (["--read"] if read else [])
+        self.proc = spawn_module("langstream_amd.bench.embed_load", args)
         self._expect("ready")
 
     def _expect(self, prefix: str) -> str:
@@ -104,10 +98,11 @@ class LoadProcess:
         if self.proc.poll() is None:
             try:
                 self.proc.stdin.write("quit\n")
-                self.proc.stdin.close()
-                self.proc.wait(30)
+                self.proc.stdin.flush()
             except Exception:  # noqa: BLE001
-                self.proc.kill()
+                pass
+        from ..utils.procs import close_stdin_and_wait
+        close_stdin_and_wait(self.proc, 30.0)
 
 
 if __name__ == "__main__":

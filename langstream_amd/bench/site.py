@@ -99,31 +99,18 @@ class SiteProcess:
     """``Site`` in a child interpreter (started before the parent touches the GPU)."""
 
     def __init__(self, per_step: int, corpus_sentences: int):
-        import os
-        import subprocess
-        root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-        env = dict(os.environ, PYTHONPATH=os.pathsep.join([root, os.environ.get("PYTHONPATH", "")]).rstrip(os.pathsep),
-                   CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
-        self.proc = subprocess.Popen([sys.executable, "-m", "langstream_amd.bench.site", "--per-step", str(per_step),
-                                      "--corpus-sentences", str(corpus_sentences)],
-                                     stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True, env=env)
-        line = self.proc.stdout.readline().strip()
-        if not line.startswith("url="):
-            self.proc.kill()
-            raise RuntimeError(f"bench site process failed to start: {line!r}")
-        self.url = line.split("=", 1)[1]
+        from ..utils.procs import read_tagged, spawn_module
+        self.proc = spawn_module("langstream_amd.bench.site",
+                                 ["--per-step", str(per_step), "--corpus-sentences", str(corpus_sentences)])
+        self.url = read_tagged(self.proc, "url=", "bench site process")
 
     def publish(self, step: int) -> None:
         self.proc.stdin.write(f"publish {step}\n")
         self.proc.stdin.flush()
 
     def close(self) -> None:
-        if self.proc.poll() is None:
-            try:
-                self.proc.stdin.close()
-                self.proc.wait(10)
-            except Exception:  # noqa: BLE001
-                self.proc.kill()
+        from ..utils.procs import close_stdin_and_wait
+        close_stdin_and_wait(self.proc)
 
 
 if __name__ == "__main__":

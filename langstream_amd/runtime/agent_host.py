@@ -17,7 +17,6 @@ Protocol on stdin / stdout, one JSON line each way:
 from __future__ import annotations
 
 import json
-import os
 import sys
 import threading
 from typing import Dict, List, Optional
@@ -57,15 +56,8 @@ def main() -> int:
 
 class AgentHostProcess:
     def __init__(self, env: Optional[Dict[str, str]] = None):
-        import subprocess
-        root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-        e = dict(os.environ, PYTHONPATH=os.pathsep.join([root, os.environ.get("PYTHONPATH", "")]).rstrip(os.pathsep),
-                 CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
-        e.update(env or {})
-        for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
-            e.pop(k, None)   # not a rank of the parent's process group
-        self.proc = subprocess.Popen([sys.executable, "-m", "langstream_amd.runtime.agent_host"],
-                                     stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True, env=e)
+        from ..utils.procs import spawn_module
+        self.proc = spawn_module("langstream_amd.runtime.agent_host", env=env)
 
     def start(self, files: Dict[str, str], instance: Optional[str], application_id: str, agents: List[str],
               state_dir: Optional[str] = None, wait: float = 60.0) -> None:
@@ -81,12 +73,8 @@ class AgentHostProcess:
         return self.proc.poll() is None
 
     def stop(self, timeout: float = 20.0) -> None:
-        if self.proc.poll() is None:
-            try:
-                self.proc.stdin.close()
-                self.proc.wait(timeout)
-            except Exception:  # noqa: BLE001
-                self.proc.kill()
+        from ..utils.procs import close_stdin_and_wait
+        close_stdin_and_wait(self.proc, timeout)
 
 
 if __name__ == "__main__":

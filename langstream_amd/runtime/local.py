@@ -200,8 +200,6 @@ class _PodProcess:
 
     def __init__(self, owner: LocalApplicationRunner, node, replica: int):
         import json
-        import subprocess
-        import sys
         from ..core.k8s import agent_pod_configuration
         self.agent_id, self.replica = node.id, replica
         self.stopping = self.reported = False
@@ -213,17 +211,17 @@ class _PodProcess:
         self.ready = os.path.join(d, "started")
         if os.path.exists(self.ready):
             os.remove(self.ready)
-        root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-        env = dict(os.environ,
-                   PYTHONPATH=os.pathsep.join([root, os.environ.get("PYTHONPATH", "")]).rstrip(os.pathsep),
-                   HOSTNAME=f"{node.id}-{replica}",              # the StatefulSet ordinal
-                   LANGSTREAM_AGENT_HTTP_PORT="0",
-                   LANGSTREAM_AGENT_READY_FILE=self.ready,
-                   LANGSTREAM_FATAL_WAIT_S="0",
-                   LANGSTREAM_AGENT_RUNNER_CODE_PATH=owner.code_directory or "",
-                   LANGSTREAM_AGENT_RUNNER_PERSISTENT_STATE_DIRECTORY=d)
-        env.pop("WORLD_SIZE", None)   # torchrun's ranks are not this pod's TP group
-        self.proc = subprocess.Popen([sys.executable, "-m", "langstream_amd.runtime.pod", cfg], env=env)
+        from ..utils.procs import spawn_module
+        # a replica pod uses the GPU (its own engines on the parent's device); torchrun's
+        # ranks of the parent are not this pod's TP group
+        self.proc = spawn_module("langstream_amd.runtime.pod", [cfg], gpu=True, pipes=False, env={
+            "HOSTNAME": f"{node.id}-{replica}",              # the StatefulSet ordinal
+            "LANGSTREAM_AGENT_HTTP_PORT": "0",
+            "LANGSTREAM_AGENT_READY_FILE": self.ready,
+            "LANGSTREAM_FATAL_WAIT_S": "0",
+            "LANGSTREAM_AGENT_RUNNER_CODE_PATH": owner.code_directory or "",
+            "LANGSTREAM_AGENT_RUNNER_PERSISTENT_STATE_DIRECTORY": d,
+            "LOCAL_RANK": os.environ.get("LOCAL_RANK", "0")})
 
     def wait_started(self, timeout: float) -> None:
         deadline = time.time() + timeout

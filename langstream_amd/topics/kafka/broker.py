@@ -476,28 +476,14 @@ class BrokerProcess:
     ends when the parent dies."""
 
     def __init__(self, partitions: int = 1, host: str = "127.0.0.1"):
-        import os
-        import subprocess
-        import sys
-        root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
-        env = dict(os.environ, PYTHONPATH=os.pathsep.join([root, os.environ.get("PYTHONPATH", "")]).rstrip(os.pathsep))
-        self.proc = subprocess.Popen(
-            [sys.executable, "-m", "langstream_amd.topics.kafka.broker", "--host", host,
-             "--partitions", str(partitions)],
-            stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True, env=env)
-        line = self.proc.stdout.readline().strip()
-        if not line.startswith("bootstrap="):
-            self.proc.kill()
-            raise RuntimeError(f"broker process failed to start: {line!r}")
-        self.bootstrap = line.split("=", 1)[1]
+        from ...utils.procs import read_tagged, spawn_module
+        self.proc = spawn_module("langstream_amd.topics.kafka.broker",
+                                 ["--host", host, "--partitions", str(partitions)])
+        self.bootstrap = read_tagged(self.proc, "bootstrap=", "broker process")
 
     def stop(self) -> None:
-        if self.proc.poll() is None:
-            self.proc.stdin.close()
-            try:
-                self.proc.wait(10)
-            except Exception:  # noqa: BLE001
-                self.proc.kill()
+        from ...utils.procs import close_stdin_and_wait
+        close_stdin_and_wait(self.proc)
 
 
 if __name__ == "__main__":
