@@ -8,10 +8,14 @@ usage: python tools/prefill_attn_bench.py [--chunk 16384] [--iters 20]
 """
 import argparse
 import json
+import os
 import random
+import sys
 import time
 
 import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from langstream_amd import ops
 from langstream_amd.ops import reference as ref
