@@ -635,13 +635,14 @@ void dgemm_launch_bm(int S, int tiles, hipStream_t st, const at::Tensor& x, cons
   // small tiles: two stages per barrier and the LDS they leave as a deeper W ring (8 / 6
   // slots at 64 / 128 rows: 96 / 64 KB of weights issued ahead)
   constexpr int SPB = BMT == BM ? 1 : 2;
-  constexpr int XS = BN != 128 ? 2 : BMT == BM ? 3 : 4;
-  constexpr int WS = BN != 128 ? 3 : BMT == 64 ? 8 : BMT == 128 ? 6 : 4;
+  // BN = 64 (256-row tiles only): 8 KB W stages, so the W ring runs 5 stages ahead
+  constexpr int XS = BN == 256 ? 2 : BMT == BM ? 3 : 4;
+  constexpr int WS = BN == 256 ? 3 : BN == 64 ? 6 : BMT == 64 ? 8 : BMT == 128 ? 6 : 4;
   // BN = 256: 8 compute waves need 128 accumulator VGPRs each, no room for a third wave
   // per SIMD.  (Streaming the B fragments one at a time fits 168 VGPRs with 4 loader
   // waves, but the gate_up K-half exchange form then measured 90 vs 82 us:
   // profiles/dgemm_r3c/silu2_loaders.log.)
-  constexpr int LDW = BN == 128 ? 4 : 0;
+  constexpr int LDW = BN <= 128 ? 4 : 0;
   // the gate_up exchange pairs and the in-launch combine slices of a tile sit on one XCD
   const int so = (EPI == EPI_SILU2 || EPI == EPI_CMB_RES || EPI == EPI_CMB_QKV) ? 0 : split_outer_default();
   // cache-policy variants (ABL bits 4 and 7, real variants): weights streamed with the
@@ -703,7 +704,7 @@ void check_xw(const at::Tensor& x, const at::Tensor& w) {
 
 int pick_bn(int N) {
   static const int env = env_int("LS_DGEMM_BN", 0);
-  if (env == 128 || env == 256) return N % env == 0 ? env : 128;
+  if (env == 64 || env == 128 || env == 256) return N % env == 0 ? env : 128;
   return 128;
 }
 
@@ -736,7 +737,13 @@ void decode_gemm(at::Tensor out, at::Tensor x, at::Tensor w, at::Tensor workspac
   const bool norm = residual.has_value();
   TORCH_CHECK(!norm || (norm_w.has_value() && residual->is_contiguous() && residual->numel() == (int64_t)M * N &&
                         out.is_contiguous() && norm_w->numel() == N), "decode_gemm: residual/norm shapes");
-  const int bn = (bn_force == 128 || bn_force == 256) && N % bn_force == 0 ? (int)bn_force : pick_bn(N);
+  int bn = (bn_force == 64 || bn_force == 128 || bn_force == 256) && N % bn_force == 0 ? (int)bn_force : pick_bn(N);
+  // o-shaped projections with the residual + RMSNorm reduction (K <= 4096): 64-column
+  // tiles, half the K splits (4 instead of 8) and half the f32 slab bytes the reduction
+  // reads -- 27.1 vs 31.4 us at M = 256 including the reduction (profiles/dgemm_bn64_r4r.log);
+  // qkv and down stay on 128 (29.8 vs 32.9, 45.3 vs 51.8)
+  static const int o_bn64 = env_int("LS_DGEMM_O_BN64", 1);
+  if (bn_force == 0 && o_bn64 && norm && K <= 4096 && N % 64 == 0 && M > 128) bn = 64;
   const int tiles = N / bn;
   const int S = splits_force > 0 ? (int)std::min<int64_t>(splits_force, K / BK) : pick_split(tiles, K, 4);
   auto st = at::hip::getCurrentHIPStream();
@@ -744,6 +751,9 @@ void decode_gemm(at::Tensor out, at::Tensor x, at::Tensor w, at::Tensor workspac
     if (bn == 256)
       dgemm_launch<256, EPI_STORE>(1, tiles, st, x, w, M, N, K, (bf16*)out.data_ptr(), out.stride(0), nullptr, 0,
                                    nullptr, nullptr, nullptr);
+    else if (bn == 64)
+      dgemm_launch<64, EPI_STORE>(1, tiles, st, x, w, M, N, K, (bf16*)out.data_ptr(), out.stride(0), nullptr, 0,
+                                  nullptr, nullptr, nullptr);
     else
       dgemm_launch<128, EPI_STORE>(1, tiles, st, x, w, M, N, K, (bf16*)out.data_ptr(), out.stride(0), nullptr, 0,
                                    nullptr, nullptr, nullptr);
@@ -754,6 +764,8 @@ void decode_gemm(at::Tensor out, at::Tensor x, at::Tensor w, at::Tensor workspac
   float* part = workspace.data_ptr<float>();
   if (bn == 256)
     dgemm_launch<256, EPI_PARTIAL>(S, tiles, st, x, w, M, N, K, nullptr, 0, part, 0, nullptr, nullptr, nullptr);
+  else if (bn == 64)
+    dgemm_launch<64, EPI_PARTIAL>(S, tiles, st, x, w, M, N, K, nullptr, 0, part, 0, nullptr, nullptr, nullptr);
   else
     dgemm_launch<128, EPI_PARTIAL>(S, tiles, st, x, w, M, N, K, nullptr, 0, part, 0, nullptr, nullptr, nullptr);
   if (norm)

@@ -815,7 +815,7 @@ def _dg_ws(M, N):
 
 @pytest.mark.parametrize("M", [129, 200, 256])
 @pytest.mark.parametrize("name,N,K", _DG_SHAPES)
-@pytest.mark.parametrize("bn,splits", [(0, 0), (128, 1), (128, 5), (256, 3)])
+@pytest.mark.parametrize("bn,splits", [(0, 0), (128, 1), (128, 5), (256, 3), (64, 0), (64, 3)])
 def test_decode_gemm(M, name, N, K, bn, splits):
     if bn == 256 and N % 256:
         pytest.skip("N not a multiple of 256")
@@ -828,7 +828,7 @@ def test_decode_gemm(M, name, N, K, bn, splits):
     _close(out, x.float().cpu() @ w.float().cpu().t(), 0.02, 0.02, name)
 
 
-@pytest.mark.parametrize("M", [129, 256])
+@pytest.mark.parametrize("M", [129, 200, 256])   # o8b above 128 rows: 64-column tiles, 4 K splits
 @pytest.mark.parametrize("name,N,K", [("o8b", 4096, 4096), ("down8b", 4096, 14336), ("o70b_tp8", 8192, 1024)])
 def test_decode_gemm_add_rmsnorm(M, name, N, K):
     torch.manual_seed(M + K)

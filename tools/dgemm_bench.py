@@ -107,7 +107,7 @@ def main():
                     out.copy_(o)
                 variants["hipblaslt+norm"] = base
                 variants["skinny"] = lambda i: h.skinny_gemm_add_rmsnorm(out, x, ws[i], res, g, 1e-5)
-                for bn in (128, 256):
+                for bn in (64, 128, 256):
                     for sp in (0, 4, 8, 16):
                         variants[f"dgemm_bn{bn}_s{sp}"] = (
                             lambda i, bn=bn, sp=sp: h.decode_gemm(out, x, ws[i], wsp, res, g, 1e-5, bn, sp))
@@ -117,7 +117,7 @@ def main():
                 ref = x.float() @ ws[0].float().t()
                 variants["hipblaslt"] = lambda i: out.copy_(F.linear(x, ws[i]))
                 variants["skinny"] = lambda i: h.skinny_gemm(out, x, ws[i])
-                for bn in (128, 256):
+                for bn in (64, 128, 256):
                     for sp in (0, 2, 4, 6, 8):
                         variants[f"dgemm_bn{bn}_s{sp}"] = (
                             lambda i, bn=bn, sp=sp: h.decode_gemm(out, x, ws[i], wsp, None, None, 1e-5, bn, sp))
