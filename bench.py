@@ -328,7 +328,7 @@ def main():
                          "gateway), and config 5 with --chat-model llama-3-70b --gpus 8 --tp 8")
     ap.add_argument("--tp", type=int, default=0, help="chat: tensor-parallel degree (= --gpus)")
     ap.add_argument("--embed-batch", type=int, default=64, help="embed: the agent's batch-size")
-    ap.add_argument("--embed-replicas", type=int, default=2,
+    ap.add_argument("--embed-replicas", type=int, default=3,
                     help="embed: agent replicas per GPU (resources.parallelism); > 1 runs each as its own "
                          "agent-pod process sharing the GPU")
     args = ap.parse_args()

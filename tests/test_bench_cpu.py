@@ -40,12 +40,12 @@ def _run(args, tmp_path, timeout=600):
 
 
 def test_bench_config2_embeddings_agent_on_kafka_two_ranks(tmp_path):
-    """BASELINE config 2 shape: compute-ai-embeddings agent replicas (2 agent-pod processes
+    """BASELINE config 2 shape: compute-ai-embeddings agent replicas (3 agent-pod processes
     per rank, the bench default) as ONE consumer group on a Kafka topic of the in-tree
     broker (its own process); the load clients run in their own processes too."""
     d = _run(["--config", "embed", "--gpus", "2", "--steps", "2", "--warmup", "1", "--batch", "32"], tmp_path)
     assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp2" and d["value"] > 0
-    assert d["config"]["agent_replicas_per_gpu"] == 2
+    assert d["config"]["agent_replicas_per_gpu"] == 3
     assert "Kafka" in d["metric"] and d["config"]["topics"].startswith("kafka")
 
 
