@@ -350,8 +350,12 @@ __global__ void __launch_bounds__(256) knn_filter_kernel(const bf16* __restrict_
 // MODE 2: no appends -- the running max of every (lane, accumulator register) slot,
 //         i.e. of 16 disjoint row groups per query per workgroup, written to
 //         gmax[q * G + 16 * rb + 4h + rr] (knn_group_thr_kernel turns them into thr).
-template <int DIM, int MODE>
-__global__ void __launch_bounds__(512) knn_filter_q256_kernel(const bf16* __restrict__ X, int64_t N,
+// NW: waves per workgroup -- 8 (two per SIMD, 32 queries per wave; launched) or 4 (one
+// per SIMD, 64 queries per wave: each A fragment feeds 4 query groups, half the LDS reads
+// per MFMA, up to 512 registers).  NW = 4 measured 2.62 vs 1.61 ms at Q = 2048: with one
+// wave per SIMD nothing covers a wave's waits (profiles/knn_nw_r4v/).
+template <int DIM, int MODE, int NW = 8>
+__global__ void __launch_bounds__(NW * 64, 1) knn_filter_q256_kernel(const bf16* __restrict__ X, int64_t N,
                                                               const bf16* __restrict__ Qm, int Qn,
                                                               float* __restrict__ cand_s, int32_t* __restrict__ cand_i,
                                                               int* __restrict__ ctrl, int64_t cap, int64_t row_begin,
@@ -362,9 +366,11 @@ __global__ void __launch_bounds__(512) knn_filter_q256_kernel(const bf16* __rest
   constexpr int TR = 64;                         // rows per LDS stage
   constexpr int SB = TR * RB;                    // stage bytes
   constexpr int CAPW = 128;                      // per-wave LDS candidate buffer entries
-  constexpr int CBYTES = 8 * CAPW * 12;
+  constexpr int QGW = 256 / NW / 16;             // 16-query groups per wave
+  constexpr int CBYTES = NW * CAPW * 12;
   constexpr int NST = 3 * SB + CBYTES <= 160 * 1024 ? 3 : 2;
-  constexpr int GPW = SB / (8 * 1024);           // LDS-DMA instructions per wave per stage
+  constexpr int GPW = SB / (NW * 1024);          // LDS-DMA instructions per wave per stage
+  static_assert(NW == 8 || NW == 4, "waves per workgroup");
   static_assert(RB % 256 == 0 && SB % 8192 == 0, "rows must be a multiple of 256 B");
   __shared__ __attribute__((aligned(1024))) char lds[NST * SB + CBYTES];
   const int lane = threadIdx.x & 63;
@@ -374,8 +380,8 @@ __global__ void __launch_bounds__(512) knn_filter_q256_kernel(const bf16* __rest
   // atomics) and reach the global lists only in flush(): a returning global atomic inside
   // the tile loop made hipcc drain vmcnt(0) every tile, i.e. the whole LDS-DMA ring
   float* c_s = reinterpret_cast<float*>(lds + NST * SB) + wid * CAPW;
-  int* c_r = reinterpret_cast<int*>(lds + NST * SB + 8 * CAPW * 4) + wid * CAPW;
-  int* c_q = reinterpret_cast<int*>(lds + NST * SB + 8 * CAPW * 8) + wid * CAPW;
+  int* c_r = reinterpret_cast<int*>(lds + NST * SB + NW * CAPW * 4) + wid * CAPW;
+  int* c_q = reinterpret_cast<int*>(lds + NST * SB + NW * CAPW * 8) + wid * CAPW;
   int ccount = 0;   // wave-uniform
   auto flush = [&]() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -405,12 +411,12 @@ __global__ void __launch_bounds__(512) knn_filter_q256_kernel(const bf16* __rest
   const int nrows = (int)(r1 - r0);
   const int ntile = (nrows + TR - 1) / TR;
 
-  // this wave's 32 queries: groups g = 0, 1 of 16; lane (fr, h) holds query 16g + fr, dims 32ks + 8h..
-  const int q0 = qb * 256 + wid * 32;
-  bf16x8 qf[2][KS];
-  float thr[2];
+  // this wave's 16 QGW queries: groups g of 16; lane (fr, h) holds query 16g + fr, dims 32ks + 8h..
+  const int q0 = qb * 256 + wid * (16 * QGW);
+  bf16x8 qf[QGW][KS];
+  float thr[QGW];
 #pragma unroll
-  for (int g = 0; g < 2; ++g) {
+  for (int g = 0; g < QGW; ++g) {
     const int qi = q0 + 16 * g + fr;
     const bool ok = qi < Qn;
     const bf16* qp = Qm + (int64_t)(ok ? qi : 0) * DIM + 8 * h;
@@ -422,7 +428,7 @@ __global__ void __launch_bounds__(512) knn_filter_q256_kernel(const bf16* __rest
   // consume the query fragments here: otherwise hipcc places their vmcnt wait at the first
   // MFMA inside the tile loop, where a vmcnt(0) also drains the LDS-DMA ring every tile
 #pragma unroll
-  for (int g = 0; g < 2; ++g) {
+  for (int g = 0; g < QGW; ++g) {
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) asm volatile("" ::"v"(qf[g][ks]));
     asm volatile("" ::"v"(thr[g]));
@@ -455,38 +461,40 @@ __global__ void __launch_bounds__(512) knn_filter_q256_kernel(const bf16* __rest
   // compare / ballot / append is issued after subtile i+1's MFMAs, so the wave never waits
   // on an MFMA result it has just requested (two accumulator sets alternate; the last
   // subtile of a tile is checked after the next tile's first MFMAs).
-  auto mm = [&](const bf16x8 (&f)[KS], f32x4 (&acc)[2]) {
-    acc[0] = f32x4{0.f, 0.f, 0.f, 0.f};
-    acc[1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto mm = [&](const bf16x8 (&f)[KS], f32x4 (&acc)[QGW]) {
+#pragma unroll
+    for (int g = 0; g < QGW; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
-      for (int g = 0; g < 2; ++g) acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f[ks], qf[g][ks], acc[g], 0, 0, 0);
+      for (int g = 0; g < QGW; ++g) acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f[ks], qf[g][ks], acc[g], 0, 0, 0);
   };
   // acc[g][rr] = score(row r0 + sr0 + 4h + rr, query q0 + 16g + fr); sr0 = subtile's first row.
   // Fast test first: one ballot over the subtile's 8 scores per lane (hits are rare -- only
   // rows above the query's sample threshold), the per-score ballots only when it fires.
-  float gm[2][4];   // MODE 2: running max per (query group, accumulator register)
+  float gm[QGW][4];   // MODE 2: running max per (query group, accumulator register)
 #pragma unroll
-  for (int g = 0; g < 2; ++g)
+  for (int g = 0; g < QGW; ++g)
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) gm[g][rr] = -INFINITY;
   auto pass = [&](float v, float t) { return MODE == 0 ? v > t : v >= t; };
-  auto epi = [&](int sr0, const f32x4 (&acc)[2]) {
+  auto epi = [&](int sr0, const f32x4 (&acc)[QGW]) {
     if constexpr (MODE == 2) {
       const bool tail = sr0 + 16 > nrows;   // wave-uniform
 #pragma unroll
-      for (int g = 0; g < 2; ++g)
+      for (int g = 0; g < QGW; ++g)
 #pragma unroll
         for (int rr = 0; rr < 4; ++rr)
           gm[g][rr] = fmaxf(gm[g][rr], tail && sr0 + 4 * h + rr >= nrows ? -INFINITY : acc[g][rr]);
       return;
     }
-    const float m0 = fmaxf(fmaxf(acc[0][0], acc[0][1]), fmaxf(acc[0][2], acc[0][3]));
-    const float m1 = fmaxf(fmaxf(acc[1][0], acc[1][1]), fmaxf(acc[1][2], acc[1][3]));
-    if (__ballot(pass(m0, thr[0]) || pass(m1, thr[1])) == 0) return;
+    bool any = false;
 #pragma unroll
-    for (int g = 0; g < 2; ++g)
+    for (int g = 0; g < QGW; ++g)
+      any |= pass(fmaxf(fmaxf(acc[g][0], acc[g][1]), fmaxf(acc[g][2], acc[g][3])), thr[g]);
+    if (__ballot(any) == 0) return;
+#pragma unroll
+    for (int g = 0; g < QGW; ++g)
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) {
         const int lr = sr0 + 4 * h + rr;
@@ -504,7 +512,7 @@ __global__ void __launch_bounds__(512) knn_filter_q256_kernel(const bf16* __rest
         ccount += nh;
       }
   };
-  f32x4 accA[2], accB[2];
+  f32x4 accA[QGW], accB[QGW];
   int pend = -1;   // first row of the subtile whose scores wait in accB (-1: none)
   for (int s = 0; s < NST - 1; ++s) issue(s, s);
   for (int t = 0; t < ntile; ++t) {
@@ -568,7 +576,7 @@ __global__ void __launch_bounds__(512) knn_filter_q256_kernel(const bf16* __rest
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   if constexpr (MODE == 2) {
 #pragma unroll
-    for (int g = 0; g < 2; ++g) {
+    for (int g = 0; g < QGW; ++g) {
       const int qi = q0 + 16 * g + fr;
       if (qi < Qn)
 #pragma unroll
@@ -792,7 +800,7 @@ void knn_topk(at::Tensor X, at::Tensor Q, int64_t K, at::Tensor out_s, at::Tenso
     if (G_out) *G_out = G;
     dim3 grid(nrb * nqb);
 #define LAUNCH_Q(DD, MM)                                                                                         \
-  knn_filter_q256_kernel<DD, MM><<<grid, 512, 0, stream>>>(                                                      \
+  knn_filter_q256_kernel<DD, MM, 8><<<grid, 512, 0, stream>>>(                                                   \
       (const bf16*)X.data_ptr(), N, (const bf16*)Q.data_ptr(), Qn, ws_s.data_ptr<float>(),                      \
       ws_i.data_ptr<int32_t>(), ctrl, cap, row_begin, (int)rpw, nqb, ws_s.data_ptr<float>(), G)
 #define LAUNCH_QM(DD)                     \
