@@ -338,6 +338,11 @@ __global__ void __launch_bounds__(256) knn_filter_kernel(const bf16* __restrict_
 //     16-query groups share each fragment);
 //   * scores above the query's sample threshold are appended exactly as in
 //     knn_filter_kernel (same candidate lists, counters and overflow flags).
+// Ablations at Q = 2048 (profiles/knn_ablation_r4.txt): with reads pinned ahead of each
+// subtile, dropping the MFMAs left 523 of 1625 us (reads and MFMAs ran in phases, not
+// overlapped); interleaved (below) the pass takes 1572 us and 1337 without MFMAs -- the
+// fragment-read stream, not the MFMA pipe or the DMA / barrier (1378 without them), now
+// bounds it.
 // Measured at Q = 2048 over 1M x 384 (profiles/knn_pmc_*, r4): MFMA busy ~41 %, waves
 // parked in waitcnt / barrier ~49 %, L2 hit 85 %, LDS array ~23 % busy.  Dead ends: a
 // one-ballot epilogue test + buffer-resource DMA addressing + pinned fragment reads (VALU
@@ -354,13 +359,15 @@ __global__ void __launch_bounds__(256) knn_filter_kernel(const bf16* __restrict_
 // per SIMD, 64 queries per wave: each A fragment feeds 4 query groups, half the LDS reads
 // per MFMA, up to 512 registers).  NW = 4 measured 2.62 vs 1.61 ms at Q = 2048: with one
 // wave per SIMD nothing covers a wave's waits (profiles/knn_nw_r4v/).
-template <int DIM, int MODE, int NW = 8>
+// ABL (timing-only diagnosis, wrong results): 1 drops the in-loop vmcnt wait + barrier,
+// 2 also the LDS-DMA issue, 3 drops the MFMAs instead.
+template <int DIM, int MODE, int NW = 8, int ABL = 0>
 __global__ void __launch_bounds__(NW * 64, 1) knn_filter_q256_kernel(const bf16* __restrict__ X, int64_t N,
                                                               const bf16* __restrict__ Qm, int Qn,
                                                               float* __restrict__ cand_s, int32_t* __restrict__ cand_i,
                                                               int* __restrict__ ctrl, int64_t cap, int64_t row_begin,
                                                               int rows_per_wg, int nqb, float* __restrict__ gmax,
-                                                              int G) {
+                                                              int G, int prio) {
   constexpr int KS = DIM / 32;
   constexpr int RB = DIM * 2;                    // bytes per row
   constexpr int TR = 64;                         // rows per LDS stage
@@ -376,6 +383,10 @@ __global__ void __launch_bounds__(NW * 64, 1) knn_filter_q256_kernel(const bf16*
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int fr = lane & 15, h = lane >> 4;
+  // prio 1: the second half of the waves (one per SIMD) at raised priority for the whole
+  // launch, so the two waves of a SIMD drift out of lockstep; prio 2: MFMA clusters at
+  // raised priority (cdna_hip_programming T5)
+  if (prio == 1 && wid >= NW / 2) __builtin_amdgcn_s_setprio(1);
   // candidates above the threshold go to this wave's LDS buffer (ballot-compacted, no
   // atomics) and reach the global lists only in flush(): a returning global atomic inside
   // the tile loop made hipcc drain vmcnt(0) every tile, i.e. the whole LDS-DMA ring
@@ -462,12 +473,20 @@ __global__ void __launch_bounds__(NW * 64, 1) knn_filter_q256_kernel(const bf16*
   // on an MFMA result it has just requested (two accumulator sets alternate; the last
   // subtile of a tile is checked after the next tile's first MFMAs).
   auto mm = [&](const bf16x8 (&f)[KS], f32x4 (&acc)[QGW]) {
+    if (prio == 2) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int g = 0; g < QGW; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
-      for (int g = 0; g < QGW; ++g) acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f[ks], qf[g][ks], acc[g], 0, 0, 0);
+      for (int g = 0; g < QGW; ++g) {
+        if constexpr (ABL == 3) {
+          asm volatile("" ::"v"(f[ks]));
+        } else {
+          acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f[ks], qf[g][ks], acc[g], 0, 0, 0);
+        }
+      }
+    if (prio == 2) __builtin_amdgcn_s_setprio(0);
   };
   // acc[g][rr] = score(row r0 + sr0 + 4h + rr, query q0 + 16g + fr); sr0 = subtile's first row.
   // Fast test first: one ballot over the subtile's 8 scores per lane (hits are rare -- only
@@ -516,11 +535,13 @@ __global__ void __launch_bounds__(NW * 64, 1) knn_filter_q256_kernel(const bf16*
   int pend = -1;   // first row of the subtile whose scores wait in accB (-1: none)
   for (int s = 0; s < NST - 1; ++s) issue(s, s);
   for (int t = 0; t < ntile; ++t) {
-    wait_vmcnt<(NST - 2) * GPW>();   // this wave's DMA of tile t landed (tiles t+1.. may be in flight)
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();    // every wave's part of tile t landed; tile t-1's slot is free
-    __builtin_amdgcn_sched_barrier(0);
-    issue(t + NST - 1, (t + NST - 1) % NST);
+    if constexpr (ABL != 1 && ABL != 2) {
+      wait_vmcnt<(NST - 2) * GPW>();   // this wave's DMA of tile t landed (tiles t+1.. may be in flight)
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();    // every wave's part of tile t landed; tile t-1's slot is free
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if constexpr (ABL != 2) issue(t + NST - 1, (t + NST - 1) % NST);
     const char* st = lds + (t % NST) * SB;
     const int tl0 = t * TR;   // tile's first row, relative to r0
     // A fragments double-buffered across the tile's four 16-row subtiles: subtile i+1's
@@ -543,6 +564,42 @@ __global__ void __launch_bounds__(NW * 64, 1) knn_filter_q256_kernel(const bf16*
       epi(tl0 + 16, accB);
       rd(3, fa);
       mm(fa, accB);
+      epi(tl0 + 32, accA);
+      pend = tl0 + 48;
+      continue;
+    }
+    if constexpr (DIM <= 384) {
+      // instruction-level interleave: the next subtile's fragment reads ride between this
+      // subtile's MFMAs (per k-step one ds_read, QGW MFMAs), so a wave is never in an
+      // all-read or all-MFMA phase (sched_group_barrier, one sync group).  Q = 2048: 1.585
+      // vs 1.635 ms for reads pinned ahead of each subtile (profiles/knn_ilv_r4y/, with the
+      // MFMA clusters at raised priority)
+      auto mmrd = [&](const bf16x8 (&f)[KS], f32x4 (&acc)[QGW], bf16x8 (&nf)[KS], int inext) {
+        if (prio == 2) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int g = 0; g < QGW; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          nf[ks] = __builtin_bit_cast(bf16x8, ld16(st + inext * 16 * RB + aoff[ks]));
+#pragma unroll
+          for (int g = 0; g < QGW; ++g)
+            acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f[ks], qf[g][ks], acc[g], 0, 0, 0);
+        }
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);     // 1 ds_read
+          __builtin_amdgcn_sched_group_barrier(0x008, QGW, 0);   // QGW MFMAs
+        }
+        if (prio == 2) __builtin_amdgcn_s_setprio(0);
+      };
+      rd(0, fa);
+      mmrd(fa, accA, fb, 1);              // subtile 0, reads 1
+      if (pend >= 0) epi(pend, accB);
+      mmrd(fb, accB, fa, 2);              // subtile 1, reads 2
+      epi(tl0, accA);
+      mmrd(fa, accA, fb, 3);              // subtile 2, reads 3
+      epi(tl0 + 16, accB);
+      mm(fb, accB);                       // subtile 3
       epi(tl0 + 32, accA);
       pend = tl0 + 48;
       continue;
@@ -601,6 +658,34 @@ __global__ void __launch_bounds__(256) knn_group_thr_kernel(const float* __restr
   wave_sort_desc(m, idx, lane);
   const float t = __shfl(m, K - 1, 64);
   if (lane == 0) ctrl[Qn + qi] = f2key(t);
+}
+
+template <int DD, int MM>
+void launch_q256(int abl, dim3 grid, hipStream_t stream, const bf16* X, int64_t N, const bf16* Q, int Qn, float* ws_s,
+                 int32_t* ws_i, int* ctrl, int64_t cap, int64_t row_begin, int rpw, int nqb, int G) {
+  // LS_KNN_PRIO: 2 (default) MFMA clusters at raised priority, 1 half the waves raised, 0 none
+  static const int prio = getenv("LS_KNN_PRIO") ? atoi(getenv("LS_KNN_PRIO")) : 2;
+  // the timing-only ablations exist for the bench's shape (384 dims, main pass) only
+  if constexpr (DD == 384 && MM == 1) {
+    switch (abl) {
+      case 1:
+        knn_filter_q256_kernel<DD, MM, 8, 1><<<grid, 512, 0, stream>>>(X, N, Q, Qn, ws_s, ws_i, ctrl, cap, row_begin,
+                                                                       rpw, nqb, ws_s, G, prio);
+        return;
+      case 2:
+        knn_filter_q256_kernel<DD, MM, 8, 2><<<grid, 512, 0, stream>>>(X, N, Q, Qn, ws_s, ws_i, ctrl, cap, row_begin,
+                                                                       rpw, nqb, ws_s, G, prio);
+        return;
+      case 3:
+        knn_filter_q256_kernel<DD, MM, 8, 3><<<grid, 512, 0, stream>>>(X, N, Q, Qn, ws_s, ws_i, ctrl, cap, row_begin,
+                                                                       rpw, nqb, ws_s, G, prio);
+        return;
+      default:
+        break;
+    }
+  }
+  knn_filter_q256_kernel<DD, MM, 8><<<grid, 512, 0, stream>>>(X, N, Q, Qn, ws_s, ws_i, ctrl, cap, row_begin, rpw, nqb,
+                                                              ws_s, G, prio);
 }
 
 __global__ void knn_init_kernel(int* __restrict__ ctrl, int Qn) {
@@ -798,11 +883,14 @@ void knn_topk(at::Tensor X, at::Tensor Q, int64_t K, at::Tensor out_s, at::Tenso
     const int nrb = (int)((rows + rpw - 1) / rpw);
     const int G = 16 * nrb;
     if (G_out) *G_out = G;
+    // LS_KNN_ABL (diagnosis only, wrong results): the main pass without its sync (1),
+    // without sync and DMA (2), without MFMAs (3); MODE 1 only
+    const char* ae = getenv("LS_KNN_ABL");
+    const int abl = ae != nullptr && mode == 1 && dim == 384 ? atoi(ae) : 0;
     dim3 grid(nrb * nqb);
 #define LAUNCH_Q(DD, MM)                                                                                         \
-  knn_filter_q256_kernel<DD, MM, 8><<<grid, 512, 0, stream>>>(                                                   \
-      (const bf16*)X.data_ptr(), N, (const bf16*)Q.data_ptr(), Qn, ws_s.data_ptr<float>(),                      \
-      ws_i.data_ptr<int32_t>(), ctrl, cap, row_begin, (int)rpw, nqb, ws_s.data_ptr<float>(), G)
+  launch_q256<DD, MM>(abl, grid, stream, (const bf16*)X.data_ptr(), N, (const bf16*)Q.data_ptr(), Qn,            \
+                      ws_s.data_ptr<float>(), ws_i.data_ptr<int32_t>(), ctrl, cap, row_begin, (int)rpw, nqb, G)
 #define LAUNCH_QM(DD)                     \
   switch (mode) {                         \
     case 0: LAUNCH_Q(DD, 0); break;       \
