@@ -106,8 +106,26 @@ __global__ void __launch_bounds__(256) gemv_kernel(const bf16* __restrict__ x, i
   if constexpr (PRO) {
     // ---- prologue: x = rmsnorm(o + residual) * norm_w, recomputed by every block from
     // the L2-resident [T, K] operands (16 KB per token at K = 4096 against >= 64 KB of W
-    // per block); block 0 also writes the new residual stream.  W loads go out first so
-    // they are in flight during the norm; a raw s_barrier keeps them outstanding.
+    // per block); block 0 also writes the new residual stream.  Load order matters: vmcnt
+    // retires loads in issue order, so the o / residual / norm_w fragments are all loaded
+    // BEFORE the W stream is issued -- an operand loaded after W cannot be waited for
+    // without draining every W load first (that order, with the residual store inside the
+    // loop, measured 67 us for gate_up at T = 4 against 42 us without a prologue).
+    u32x4 ov[TR][KCH], rv[TR][KCH];
+    uint4 nv[KCH];
+#pragma unroll
+    for (int m = 0; m < TR; ++m) {
+      const int64_t mo = (int64_t)min(m, T - 1) * K;
+#pragma unroll
+      for (int c = 0; c < KCH; ++c) {
+        const int off = (min(c * 4 + wv, nchunk - 1) << 9) + lane * 8;
+        ov[m][c] = *reinterpret_cast<const u32x4*>(pro.o + mo + off);
+        rv[m][c] = *reinterpret_cast<const u32x4*>(pro.res + mo + off);
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < KCH; ++c) nv[c] = ld16(pro.norm_w + (min(c * 4 + wv, nchunk - 1) << 9) + lane * 8);
+    asm volatile("" ::: "memory");
 #pragma unroll
     for (int r = 0; r < RB; ++r) {
       const int row = w_row(r);
@@ -117,21 +135,24 @@ __global__ void __launch_bounds__(256) gemv_kernel(const bf16* __restrict__ x, i
         wr[r][c] =
             __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(wrow + (min(c * 4 + wv, nchunk - 1) << 9)));
     }
+    // pin the issue order: the scheduler otherwise hoists the norm arithmetic (and with it
+    // the wait for o / residual) above the W loads, exposing one L2 round trip per block;
+    // the empty asm "redefines" the fragments after the W stream is out
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int m = 0; m < TR; ++m)
+#pragma unroll
+      for (int c = 0; c < KCH; ++c) asm volatile("" : "+v"(ov[m][c]), "+v"(rv[m][c]));
     __shared__ float pro_red[4][TR];
     float ss[TR];
 #pragma unroll
     for (int m = 0; m < TR; ++m) {
-      const int mm = min(m, T - 1);
-      const bf16* om = pro.o + (int64_t)mm * K;
-      const bf16* rm = pro.res + (int64_t)mm * K;
       ss[m] = 0.f;
 #pragma unroll
       for (int c = 0; c < KCH; ++c) {
-        const int g = c * 4 + wv;
-        const int off = (min(g, nchunk - 1) << 9) + lane * 8;
         float a[8], b[8];
-        unpack8(ld16(om + off), a);
-        unpack8(ld16(rm + off), b);
+        unpack8(__builtin_bit_cast(uint4, ov[m][c]), a);
+        unpack8(__builtin_bit_cast(uint4, rv[m][c]), b);
 #pragma unroll
         for (int j = 0; j < 8; ++j) a[j] += b[j];
         const uint4 packed = pack8(a);  // the residual stream stays bf16: round once
@@ -139,15 +160,27 @@ __global__ void __launch_bounds__(256) gemv_kernel(const bf16* __restrict__ x, i
         float s = 0.f;
 #pragma unroll
         for (int j = 0; j < 8; ++j) s += a[j] * a[j];
-        ss[m] += g < nchunk ? s : 0.f;
+        ss[m] += c * 4 + wv < nchunk ? s : 0.f;
         xr[m][c] = __builtin_bit_cast(u32x4, packed);
-        if (blockIdx.x == 0 && g < nchunk && m < T) st16(pro.res_out + (int64_t)m * K + off, packed);
       }
-      ss[m] = wave_sum(ss[m]);
     }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+      for (int m = 0; m < TR; ++m) ss[m] += __shfl_xor(ss[m], o, 64);
     if (lane == 0) {
 #pragma unroll
       for (int m = 0; m < TR; ++m) pro_red[wv][m] = ss[m];
+    }
+    if (blockIdx.x == 0) {
+#pragma unroll
+      for (int m = 0; m < TR; ++m)
+#pragma unroll
+        for (int c = 0; c < KCH; ++c) {
+          const int g = c * 4 + wv;
+          if (m < T && g < nchunk)
+            st16(pro.res_out + (int64_t)m * K + (g << 9) + lane * 8, __builtin_bit_cast(uint4, xr[m][c]));
+        }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -158,7 +191,7 @@ __global__ void __launch_bounds__(256) gemv_kernel(const bf16* __restrict__ x, i
     for (int c = 0; c < KCH; ++c) {
       const int g = c * 4 + wv;
       float wf[8];
-      unpack8(ld16(pro.norm_w + (min(g, nchunk - 1) << 9) + lane * 8), wf);
+      unpack8(nv[c], wf);
 #pragma unroll
       for (int m = 0; m < TR; ++m) {
         float a[8];
@@ -177,9 +210,7 @@ __global__ void __launch_bounds__(256) gemv_kernel(const bf16* __restrict__ x, i
       for (int c = 0; c < KCH; ++c) {
         // branch-free tail: a chunk past K reloads the last one and is zeroed by a select, so
         // no load sits behind control flow (which made the compiler drain vmcnt per row)
-        const int g = c * 4 + wv;
-        const u32x4 v = *reinterpret_cast<const u32x4*>(xm + (min(g, nchunk - 1) << 9) + lane * 8);
-        xr[m][c] = g < nchunk ? v : u32x4{0, 0, 0, 0};
+        xr[m][c] = *reinterpret_cast<const u32x4*>(xm + (min(c * 4 + wv, nchunk - 1) << 9) + lane * 8);
       }
     }
     // ---- W rows of this block
@@ -192,6 +223,25 @@ __global__ void __launch_bounds__(256) gemv_kernel(const bf16* __restrict__ x, i
         wr[r][c] =
             __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(wrow + (min(c * 4 + wv, nchunk - 1) << 9)));
     }
+    // Left alone, the scheduler interleaves the dots with the W loads (a rolling window of
+    // ~4-8 loads per wave behind the TR x fragments), which at TR = 4 halves the bytes in
+    // flight: qkv / o at T = 4 ran at ~3 TB/s.  Where x + W fit in ~128 VGPRs, every W load
+    // is issued before the first dot (the empty asm "redefines" the fragments after them).
+    if constexpr ((RB + TR) * KCH * 4 <= 128) {
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int r = 0; r < RB; ++r)
+#pragma unroll
+        for (int c = 0; c < KCH; ++c) asm volatile("" : "+v"(wr[r][c]));
+#pragma unroll
+      for (int m = 0; m < TR; ++m)
+#pragma unroll
+        for (int c = 0; c < KCH; ++c) asm volatile("" : "+v"(xr[m][c]));
+    }
+#pragma unroll
+    for (int m = 0; m < TR; ++m)
+#pragma unroll
+      for (int c = 0; c < KCH; ++c) xr[m][c] = c * 4 + wv < nchunk ? xr[m][c] : u32x4{0, 0, 0, 0};
   }
   float acc[RB][TR];
 #pragma unroll

@@ -372,9 +372,14 @@ class LlamaRunner {
         at::Tensor o = at::empty_like(residual);
         gemv(o, attn, o_w_[l]);
         at::Tensor a = at::empty({T, gate_up_w_[l].size(0) / 2}, o.options());
-        at::Tensor rn = at::empty_like(residual);
-        gemv_silu_norm(a, o, residual, rn, post_norm_[l], eps_, gate_up_w_[l]);
-        residual = rn;
+        if (T <= gemv_pro_max_t()) {
+          at::Tensor rn = at::empty_like(residual);
+          gemv_silu_norm(a, o, residual, rn, post_norm_[l], eps_, gate_up_w_[l]);
+          residual = rn;
+        } else {
+          fused_add_rmsnorm(o, residual, post_norm_[l], eps_);
+          gemv_silu(a, o, gate_up_w_[l]);
+        }
         dn = at::empty_like(residual);
         gemv(dn, a, down_w_[l]);
       }
@@ -602,6 +607,19 @@ class LlamaRunner {
       return !(v && std::string(v) == "0");
     }();
     return on;
+  }
+
+  // Largest T whose gate_up GEMV recomputes the add + RMSNorm in its prologue.  Each
+  // block re-reads o and the residual (2 T K bf16 from L2), which at T = 4 equals the
+  // block's 64 KB of weights: gate_up measured 62 us with the prologue against 41 us
+  // plain + a separate fused_add_rmsnorm launch; batch-4 decode step 4.59 -> 4.15 ms
+  // (tools/gemv_bench.py, tools/engine_bench.py; profiles/gemv_r4/gemv_ab_r4h.log).
+  static int gemv_pro_max_t() {
+    static const int t = [] {
+      const char* e = getenv("LS_GEMV_PRO_MAX_T");
+      return e ? atoi(e) : 2;
+    }();
+    return t;
   }
 
   // LS_ATTN_ROPE=0: separate rope_cache launch before decode attention (A/B switch)

@@ -60,8 +60,16 @@ def main():
                     h.gemv(out, x, w)
             b, g = timed(base, ring), timed(mine, ring)
             gb = N * K * 2 / 1e9
-            print(json.dumps({"gemm": name, "T": T, "N": N, "K": K, "hipblaslt_us": round(b, 1), "gemv_us": round(g, 1),
-                              "speedup": round(b / g, 2), "gemv_TBps": round(gb / g * 1e3, 2)}), flush=True)
+            row = {"gemm": name, "T": T, "N": N, "K": K, "hipblaslt_us": round(b, 1), "gemv_us": round(g, 1),
+                   "speedup": round(b / g, 2), "gemv_TBps": round(gb / g * 1e3, 2)}
+            if K <= 4096:
+                # prologue-fused form (input = rmsnorm(o + res) * norm_w, computed in the kernel)
+                o_, res = torch.randn(T, K, device=dev).to(torch.bfloat16), torch.randn(T, K, device=dev).to(torch.bfloat16)
+                res_out, nw = torch.empty_like(res), torch.ones(K, device=dev, dtype=torch.bfloat16)
+                fn = h.gemv_silu_norm if silu else h.gemv_norm
+                p = timed(lambda w: fn(out, o_, res, res_out, nw, 1e-5, w), ring)
+                row.update(pro_us=round(p, 1), pro_TBps=round(gb / p * 1e3, 2))
+            print(json.dumps(row), flush=True)
         del ring
 
 
