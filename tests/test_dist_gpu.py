@@ -100,3 +100,57 @@ def test_oneshot_allreduce_world1_rccl(rccl_world1):
     ref = t.clone()
     assert ops.hip().oneshot_allreduce_selftest(dist.group.WORLD, t) == 0
     assert torch.equal(t, ref)
+
+
+def _oneshot_rank(rank, world, port, q):
+    """One process of the one-shot all-reduce over real IPC-mapped buffers: ranks share
+    cuda:0 (RCCL refuses two ranks on one GPU, so the handle exchange runs over gloo)."""
+    import os
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from langstream_amd import ops
+        n = 8192 * 5 + 7
+        ts = [(torch.arange(n, dtype=torch.float32) % 61 - 30.0 + 0.25 * r) for r in range(world)]
+        t = ts[rank].to("cuda", torch.bfloat16)
+        errs = [ops.hip().oneshot_allreduce_selftest(dist.group.WORLD, t) for _ in range(3)]
+        # after each in-place call every rank holds bf16(f32 sum over ranks, rank order)
+        ref = [x.to(torch.bfloat16) for x in ts]
+        for _ in range(3):
+            acc = ref[0].float()
+            for x in ref[1:]:
+                acc = acc + x.float()
+            s = acc.to(torch.bfloat16)
+            ref = [s] * world
+        q.put((rank, errs, float((t.float().cpu() - ref[0].float()).abs().max())))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("W", [2, 3])
+def test_oneshot_allreduce_processes_sharing_one_gpu(W):
+    """The one-shot all-reduce (allreduce.hip) between W real processes: IPC handle
+    exchange, system-scope flag protocol and the W-way sum across process boundaries,
+    three back-to-back calls (both buffer halves), every rank bit-identical to the
+    host sum."""
+    import multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_oneshot_rank, args=(r, W, port, q)) for r in range(W)]
+    for p in procs:
+        p.start()
+    try:
+        res = [q.get(timeout=100) for _ in range(W)]
+    finally:
+        for p in procs:
+            p.join(30)
+            if p.is_alive():
+                p.kill()
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    for rank, errs, diff in res:
+        assert errs == [0, 0, 0], (rank, errs)
+        assert diff == 0.0, (rank, diff)

@@ -325,13 +325,15 @@ def test_prefill_gate_up_gemm_in_model(monkeypatch):
 _TP_PROMPTS = [list(range(3, 3 + n)) for n in (5, 33, 64, 200)]
 
 
-def _tp_native_worker(rank, world, port, q):
+def _tp_native_worker(rank, world, port, q, oneshot=False):
     """One TP rank on cuda:0 over a gloo process group: the NATIVE step executor (C++
     forward, per-layer all-reduces through c10d, vocab-parallel sampling); rank 0 drives
     the engine, the other ranks run StepExecutor::worker_loop (pure C++)."""
     import os
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    if oneshot:
+        os.environ["LS_ONESHOT_AR"] = "1"   # read when the runner is built
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -354,12 +356,15 @@ def _tp_native_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_native_executor_tp2_two_ranks_one_gpu():
+@pytest.mark.parametrize("oneshot", [False, True])
+def test_native_executor_tp2_two_ranks_one_gpu(oneshot):
     """TP = 2 with two real ranks (two processes sharing cuda:0, gloo collectives on GPU
     tensors): the native executor's worker loop, arena broadcast, per-layer all-reduces
     and vocab-parallel sampling produce the TP = 1 engine's greedy tokens (up to genuine
     near-ties) on the same full weights.  RCCL cannot put two ranks on one GPU; this is
-    the multi-rank run of the C++ TP path available on a 1-GPU box."""
+    the multi-rank run of the C++ TP path available on a 1-GPU box.  oneshot: the
+    per-layer all-reduces run allreduce.hip between the two processes (IPC-mapped
+    buffers, the xGMI one-shot protocol) instead of c10d."""
     import multiprocessing as mp
     import socket
     cfg = PRESETS["llama-small"]
@@ -374,7 +379,7 @@ def test_native_executor_tp2_two_ranks_one_gpu():
         port = s.getsockname()[1]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_tp_native_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_tp_native_worker, args=(r, 2, port, q, oneshot)) for r in range(2)]
     for p in procs:
         p.start()
     try:
