@@ -132,6 +132,90 @@ __global__ void __launch_bounds__(kThreads) oneshot_ar_kernel(IOTable io, int64_
   if (tid == 0) epoch[b] = e;
 }
 
+// The same protocol for the other collectives of a tensor-parallel decode step -- the
+// vocab-parallel sampler's int64 histogram all-reduce (MODE 1) and its f32 row-statistics
+// and candidate all-gathers (MODE 2, 4-byte words) -- so a TP decode step needs no c10d
+// call and can be captured whole into a graph without RCCL (and without its ring hops).
+// Units: MODE 1 int64 (2 per 16-B vector), MODE 2 32-bit words (4 per vector).  `n` is
+// the per-rank unit count; MODE 2 writes rank w's units at out + w * n (word stores: the
+// segments are not 16-B aligned in general).  A timed-out wait writes all-ones / NaN words.
+template <int MODE>
+__global__ void __launch_bounds__(kThreads) oneshot_x_kernel(const void* in_, void* out_, int* epoch, int* err, int64_t n,
+                                                             int64_t half_bytes, int rank, int W, PeerTable tbl) {
+  __shared__ int timed_out;
+  constexpr int U = MODE == 1 ? 8 : 4;   // bytes per unit
+  constexpr int VU = 16 / U;             // units per 16-B vector
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const char* in = (const char*)in_;
+  const int e = epoch[b] + 1;
+  const int64_t half = (int64_t)(e & 1) * half_bytes;   // byte offset of this call's buffer half
+  const int64_t nvec = n / VU;
+  const int64_t per = (nvec + kBlocks - 1) / kBlocks;
+  const int64_t v0 = b * per, v1 = min(nvec, v0 + per);
+  char* mine = (char*)tbl.data[rank] + half;
+  for (int64_t v = v0 + tid; v < v1; v += kThreads) st16(mine + v * 16, ld16(in + v * 16));
+  if (b == 0)
+    for (int64_t i = nvec * VU + tid; i < n; i += kThreads) {
+      if constexpr (U == 8) reinterpret_cast<int64_t*>(mine)[i] = reinterpret_cast<const int64_t*>(in)[i];
+      else reinterpret_cast<uint32_t*>(mine)[i] = reinterpret_cast<const uint32_t*>(in)[i];
+    }
+  if (tid == 0) timed_out = 0;
+  __threadfence_system();
+  __syncthreads();
+  if (tid < W) __hip_atomic_store(tbl.flags[tid] + rank * kBlocks + b, e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (tid < W) {
+    const int* f = tbl.flags[rank] + tid * kBlocks + b;
+    long long spins = 0;
+    while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < e) {
+      if (++spins > kSpinLimit) {
+        __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        timed_out = 1;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  __syncthreads();
+  __threadfence_system();
+  // this workgroup's units: vectors [v0, v1) plus (block 0) the ragged tail
+  auto for_units = [&](auto&& f) {
+    for (int64_t i = v0 * VU + tid; i < v1 * VU; i += kThreads) f(i);
+    if (b == 0)
+      for (int64_t i = nvec * VU + tid; i < n; i += kThreads) f(i);
+  };
+  if constexpr (MODE == 1) {
+    int64_t* out = (int64_t*)out_;
+    if (timed_out) {
+      for_units([&](int64_t i) { out[i] = -1; });
+    } else {
+      for (int64_t v = v0 + tid; v < v1; v += kThreads) {
+        int64_t a0 = 0, a1 = 0;
+        for (int w = 0; w < W; ++w) {
+          const uint4 x = ld16((const char*)tbl.data[w] + half + v * 16);
+          a0 += (int64_t)(((uint64_t)x.y << 32) | x.x);
+          a1 += (int64_t)(((uint64_t)x.w << 32) | x.z);
+        }
+        out[v * 2] = a0;
+        out[v * 2 + 1] = a1;
+      }
+      if (b == 0)
+        for (int64_t i = nvec * VU + tid; i < n; i += kThreads) {
+          int64_t a = 0;
+          for (int w = 0; w < W; ++w) a += reinterpret_cast<const int64_t*>((const char*)tbl.data[w] + half)[i];
+          out[i] = a;
+        }
+    }
+  } else {
+    uint32_t* out = (uint32_t*)out_;
+    for (int w = 0; w < W; ++w) {
+      const uint32_t* src = reinterpret_cast<const uint32_t*>((const char*)tbl.data[w] + half);
+      for_units([&](int64_t i) { out[w * n + i] = timed_out ? 0x7FC00000u : src[i]; });
+    }
+  }
+  __syncthreads();
+  if (tid == 0) epoch[b] = e;
+}
+
 void launch_oneshot(const IOTable& io, int ranks_in_grid, int64_t n, int64_t cap, int rank0, int W,
                     const PeerTable& tbl, hipStream_t stream, int stall_rank = -1) {
   oneshot_ar_kernel<<<dim3(kBlocks, ranks_in_grid), kThreads, 0, stream>>>(io, n, cap, rank0, W, tbl, stall_rank);
@@ -204,6 +288,23 @@ class OneShotAllReduce {
     launch_oneshot(io, 1, t.numel(), cap_, rank_, W_, tbl_, at::hip::getCurrentHIPStream().stream());
   }
 
+  // t = sum over ranks of t (int64, contiguous, up to 2 * capacity() / 8 elements).
+  void run_sum_i64(at::Tensor& t) {
+    TORCH_CHECK(t.scalar_type() == at::kLong && t.is_contiguous() && t.numel() * 8 <= 2 * cap_,
+                "one-shot all-reduce: contiguous int64 up to ", 2 * cap_ / 8, " elements");
+    oneshot_x_kernel<1><<<kBlocks, kThreads, 0, at::hip::getCurrentHIPStream().stream()>>>(
+        t.data_ptr(), t.data_ptr(), epoch_, err_, t.numel(), cap_ * (int64_t)sizeof(bf16), rank_, W_, tbl_);
+  }
+
+  // out[w * n : (w + 1) * n] = rank w's `in` (4-byte elements, n = in.numel()).
+  void run_gather32(const at::Tensor& in, at::Tensor& out) {
+    TORCH_CHECK(in.element_size() == 4 && in.is_contiguous() && in.numel() * 4 <= 2 * cap_ && out.is_contiguous() &&
+                    out.element_size() == 4 && out.numel() == W_ * in.numel() && out.data_ptr() != in.data_ptr(),
+                "one-shot all-gather: contiguous 4-byte elements up to ", 2 * cap_ / 4, " per rank");
+    oneshot_x_kernel<2><<<kBlocks, kThreads, 0, at::hip::getCurrentHIPStream().stream()>>>(
+        in.data_ptr(), out.data_ptr(), epoch_, err_, in.numel(), cap_ * (int64_t)sizeof(bf16), rank_, W_, tbl_);
+  }
+
   // Device word that becomes non-zero (and stays so) when a wait timed out.
   const int* err_ptr() const { return err_; }
 
@@ -231,6 +332,13 @@ std::shared_ptr<OneShotAllReduce> make_oneshot_allreduce(c10::intrusive_ptr<::c1
 }
 
 void oneshot_allreduce_run(const std::shared_ptr<OneShotAllReduce>& ar, at::Tensor t) { ar->run(t); }
+void oneshot_allreduce_i64(const std::shared_ptr<OneShotAllReduce>& ar, at::Tensor t) { ar->run_sum_i64(t); }
+void oneshot_allgather32(const std::shared_ptr<OneShotAllReduce>& ar, const at::Tensor& in, at::Tensor out) {
+  ar->run_gather32(in, out);
+}
+int64_t oneshot_capacity_bytes(const std::shared_ptr<OneShotAllReduce>& ar) {
+  return 2 * ar->capacity() * (int64_t)sizeof(bf16);
+}
 const int* oneshot_allreduce_err(const std::shared_ptr<OneShotAllReduce>& ar) { return ar->err_ptr(); }
 
 // Single-GPU rehearsal of the protocol: W simulated ranks with their own buffers, flag
@@ -275,4 +383,21 @@ int64_t oneshot_allreduce_selftest(py::object process_group, at::Tensor t) {
   ar->run(t);
   AR_OK(hipStreamSynchronize(at::hip::getCurrentHIPStream().stream()));
   return ar->error();
+}
+
+// The int64 all-reduce and 32-bit all-gather forms, interleaved on ONE instance the way
+// the vocab-parallel sampler calls them (bf16 sum, gather, int64 sum, gather): returns
+// [bf16 result, gather result, int64 result, gather result] and the error flag.
+std::vector<at::Tensor> oneshot_collectives_selftest(py::object process_group, at::Tensor bf, at::Tensor g32,
+                                                     at::Tensor i64, int64_t cap) {
+  auto pg = py::cast<c10::intrusive_ptr<::c10d::ProcessGroup>>(process_group);
+  auto ar = make_oneshot_allreduce(pg, cap);
+  const int64_t W = pg->getSize();
+  at::Tensor g1 = at::empty({W * g32.numel()}, g32.options()), g2 = at::empty_like(g1);
+  ar->run(bf);
+  ar->run_gather32(g32, g1);
+  ar->run_sum_i64(i64);
+  ar->run_gather32(g32, g2);
+  AR_OK(hipStreamSynchronize(at::hip::getCurrentHIPStream().stream()));
+  return {bf, g1, i64, g2, at::full({1}, ar->error(), i64.options())};
 }

@@ -104,6 +104,9 @@ class OneShotAllReduce;
 std::shared_ptr<OneShotAllReduce> make_oneshot_allreduce(c10::intrusive_ptr<::c10d::ProcessGroup> pg,
                                                          int64_t max_elems);
 void oneshot_allreduce_run(const std::shared_ptr<OneShotAllReduce>& ar, at::Tensor t);
+void oneshot_allreduce_i64(const std::shared_ptr<OneShotAllReduce>& ar, at::Tensor t);
+void oneshot_allgather32(const std::shared_ptr<OneShotAllReduce>& ar, const at::Tensor& in, at::Tensor out);
+int64_t oneshot_capacity_bytes(const std::shared_ptr<OneShotAllReduce>& ar);
 
 void skinny_gemm(at::Tensor out, at::Tensor x, at::Tensor w);
 void gemm_fused(at::Tensor out, at::Tensor x, at::Tensor w, c10::optional<at::Tensor> bias, bool gelu,
@@ -571,6 +574,29 @@ class LlamaRunner {
   int64_t vocab() const { return vocab_; }
   int64_t vocab_start() const { return vocab_start_; }
   c10::intrusive_ptr<::c10d::ProcessGroup> pg() const { return pg_; }
+
+  // The sampler's collectives on the one-shot buffers when LS_ONESHOT_AR=1 (and the
+  // message fits), c10d otherwise: int64 sum in place, 32-bit all-gather.
+  void allreduce_i64(at::Tensor t) {
+    if (oneshot_ && t.numel() * 8 <= oneshot_capacity_bytes(oneshot_)) {
+      oneshot_allreduce_i64(oneshot_, t);
+      return;
+    }
+    std::vector<at::Tensor> v{t};
+    pg_->allreduce(v)->wait();
+  }
+  void allgather32(const at::Tensor& src, const at::Tensor& dst) {
+    const int64_t W = pg_->getSize(), per = src.numel();
+    if (oneshot_ && per * 4 <= oneshot_capacity_bytes(oneshot_)) {
+      oneshot_allgather32(oneshot_, src, dst);
+      return;
+    }
+    std::vector<at::Tensor> parts;
+    for (int64_t w = 0; w < W; ++w) parts.push_back(dst.narrow(0, w * per, per));
+    std::vector<std::vector<at::Tensor>> outs{parts};
+    std::vector<at::Tensor> ins{src};
+    pg_->allgather(outs, ins)->wait();
+  }
 
  private:
   at::Tensor embed(const at::Tensor& ids) {
@@ -1207,22 +1233,16 @@ class StepExecutor {
   void sample_vocab_parallel(const at::Tensor& lg, const at::Tensor& temp, const at::Tensor& topk,
                              const at::Tensor& topp, const at::Tensor& seeds, const at::Tensor& steps, int64_t R,
                              int64_t ntop) {
-    auto pg = r_->pg();
-    const int64_t W = pg->getSize(), cw = 3 + 2 * ntop;
+    const int64_t W = r_->pg()->getSize(), cw = 3 + 2 * ntop;
     auto gather = [&](const at::Tensor& src, const at::Tensor& dst, int64_t per) {
-      std::vector<at::Tensor> parts;
-      for (int64_t w = 0; w < W; ++w) parts.push_back(dst.narrow(0, w * per, per));
-      std::vector<std::vector<at::Tensor>> outs{parts};
-      std::vector<at::Tensor> ins{src.narrow(0, 0, per)};
-      pg->allgather(outs, ins)->wait();
+      r_->allgather32(src.narrow(0, 0, per), dst);
     };
     at::Tensor stats = tp_stats_.narrow(0, 0, R * 4), stats_all = tp_stats_all_.narrow(0, 0, W * R * 4);
     tp_sample_stats(lg, r_->vocab_start(), stats);
     gather(tp_stats_, stats_all, R * 4);
     at::Tensor hist = tp_hist_.narrow(0, 0, R * 2 * 1024);
     tp_sample_hist(lg, r_->vocab(), temp, topk, topp, stats_all, W, hist);
-    std::vector<at::Tensor> hv{hist};
-    pg->allreduce(hv)->wait();
+    r_->allreduce_i64(hist);
     at::Tensor cand_all = tp_cand_all_.narrow(0, 0, W * R * cw);
     tp_sample_pick(lg, r_->vocab_start(), r_->vocab(), temp, topk, topp, seeds, steps, stats_all, W, hist, ntop,
                    tp_cand_);

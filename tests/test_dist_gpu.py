@@ -154,3 +154,50 @@ def test_oneshot_allreduce_processes_sharing_one_gpu(W):
     for rank, errs, diff in res:
         assert errs == [0, 0, 0], (rank, errs)
         assert diff == 0.0, (rank, diff)
+
+
+def _collectives_rank(rank, world, port, q):
+    import os
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from langstream_amd import ops
+        bf = torch.full((1000,), float(rank + 1)).to("cuda", torch.bfloat16)
+        g32 = (torch.arange(2051, dtype=torch.float32) + 10000 * rank).cuda()
+        i64 = (torch.arange(4099, dtype=torch.int64) * (rank + 1) + (1 << 40)).cuda()
+        out = ops.hip().oneshot_collectives_selftest(dist.group.WORLD, bf, g32, i64, 20000)
+        q.put((rank, [t.cpu().tolist() for t in out]))   # plain lists: a queued tensor's storage dies with this process
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("W", [2, 3])
+def test_oneshot_gather_and_int64_sum_processes_sharing_one_gpu(W):
+    """The vocab-parallel sampler's collectives on the one-shot buffers (32-bit
+    all-gather with ragged sizes, int64 sum past 2^32), interleaved with a bf16 sum on one
+    instance, between W real processes."""
+    import multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_collectives_rank, args=(r, W, port, q)) for r in range(W)]
+    for p in procs:
+        p.start()
+    try:
+        res = [q.get(timeout=100) for _ in range(W)]
+    finally:
+        for p in procs:
+            p.join(30)
+            if p.is_alive():
+                p.kill()
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    want_g = torch.cat([torch.arange(2051, dtype=torch.float32) + 10000 * r for r in range(W)])
+    want_i = sum(torch.arange(4099, dtype=torch.int64) * (r + 1) + (1 << 40) for r in range(W))
+    for rank, (bf, g1, i64, g2, err) in res:
+        assert err == [0], rank
+        assert bf == [float(W * (W + 1) // 2)] * 1000, rank
+        assert g1 == want_g.tolist() and g2 == want_g.tolist(), rank
+        assert i64 == want_i.tolist(), rank

@@ -325,7 +325,7 @@ def test_prefill_gate_up_gemm_in_model(monkeypatch):
 _TP_PROMPTS = [list(range(3, 3 + n)) for n in (5, 33, 64, 200)]
 
 
-def _tp_native_worker(rank, world, port, q, oneshot=False):
+def _tp_native_worker(rank, world, port, q, oneshot=False, graphs=False):
     """One TP rank on cuda:0 over a gloo process group: the NATIVE step executor (C++
     forward, per-layer all-reduces through c10d, vocab-parallel sampling); rank 0 drives
     the engine, the other ranks run StepExecutor::worker_loop (pure C++)."""
@@ -343,9 +343,10 @@ def _tp_native_worker(rank, world, port, q, oneshot=False):
         full = LlamaModel(cfg, device="cpu", dtype=torch.float32, seed=9)
         m = LlamaModel(cfg, device="cuda", tp=TPInfo(rank, world, None))
         m.load_state_dict(shard_llama(full.state_dict(), cfg, rank, world))
-        eng = LLMEngine(m, None, num_blocks=128, max_model_len=1024, max_batch=8, use_graphs=False)
+        eng = LLMEngine(m, None, num_blocks=128, max_model_len=1024, max_batch=8, use_graphs=graphs)
         if rank == 0:
-            sp = SamplingParams(max_tokens=10, temperature=0.0, ignore_eos=True, logprobs=2)
+            # decode graphs serve logprobs == 0 steps only (the reference run keeps top-2)
+            sp = SamplingParams(max_tokens=10, temperature=0.0, ignore_eos=True, logprobs=0 if graphs else 2)
             out = _run_tops(eng, _TP_PROMPTS, sp)
             stats = dict(eng.stats)
             eng.stop()
@@ -356,15 +357,17 @@ def _tp_native_worker(rank, world, port, q, oneshot=False):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("oneshot", [False, True])
-def test_native_executor_tp2_two_ranks_one_gpu(oneshot):
+@pytest.mark.parametrize("oneshot,graphs", [(False, False), (True, False), (True, True)])
+def test_native_executor_tp2_two_ranks_one_gpu(oneshot, graphs):
     """TP = 2 with two real ranks (two processes sharing cuda:0, gloo collectives on GPU
     tensors): the native executor's worker loop, arena broadcast, per-layer all-reduces
     and vocab-parallel sampling produce the TP = 1 engine's greedy tokens (up to genuine
     near-ties) on the same full weights.  RCCL cannot put two ranks on one GPU; this is
     the multi-rank run of the C++ TP path available on a 1-GPU box.  oneshot: the
     per-layer all-reduces run allreduce.hip between the two processes (IPC-mapped
-    buffers, the xGMI one-shot protocol) instead of c10d."""
+    buffers, the xGMI one-shot protocol) instead of c10d, and so do the sampler's
+    all-gathers and histogram all-reduce; with graphs, whole TP decode steps -- every
+    collective included -- are captured and replayed on both ranks."""
     import multiprocessing as mp
     import socket
     cfg = PRESETS["llama-small"]
@@ -379,7 +382,7 @@ def test_native_executor_tp2_two_ranks_one_gpu(oneshot):
         port = s.getsockname()[1]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_tp_native_worker, args=(r, 2, port, q, oneshot)) for r in range(2)]
+    procs = [ctx.Process(target=_tp_native_worker, args=(r, 2, port, q, oneshot, graphs)) for r in range(2)]
     for p in procs:
         p.start()
     try:
@@ -391,6 +394,8 @@ def test_native_executor_tp2_two_ranks_one_gpu(oneshot):
                 p.kill()
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     assert stats["decode_steps"] > 0
+    if graphs:
+        assert stats["graph_steps"] > 0, stats
     for a, b in zip(got, ref):
         _same_or_near_tie(a, b)
 
