@@ -450,9 +450,12 @@ def main():
                                               services=services, agents=only)
     runner.start()
     if crawler_host is not None:
+        import atexit
+        import shutil
         import tempfile
-        crawler_host.start(files, INSTANCE.format(**fmt), "rag-bench", ["crawler"],
-                           state_dir=tempfile.mkdtemp(prefix="rag-bench-crawler-"))
+        crawler_state = tempfile.mkdtemp(prefix="rag-bench-crawler-")
+        atexit.register(shutil.rmtree, crawler_state, True)
+        crawler_host.start(files, INSTANCE.format(**fmt), "rag-bench", ["crawler"], state_dir=crawler_state)
     log = runner.topic_runtime.log
     barrier()
     prod = runner.producer("questions-topic")
