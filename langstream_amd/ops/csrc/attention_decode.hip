@@ -17,7 +17,9 @@
 // Grid: (B*Hkv, S splits).  WPP waves per workgroup stride over the split's KV blocks:
 // WPP = 1 (one wave owns a (seq, kv-head) pair, writes straight from its accumulators)
 // once the pairs alone fill every wave slot of the chip (B*Hkv >= 2048, no split);
-// otherwise WPP = 4, merged through LDS, and with S > 1 a second kernel merges splits.
+// otherwise WPP = 4, merged through LDS, and with S > 1 a second kernel merges splits
+// (a sequence whose context fits in one split is finished by split 0 and skipped by
+// the merge: short chats at small batch pay no partial round trip).
 //
 // Split policy (decided per launch, so it is fixed inside a captured HIP graph):
 // S = min(nsplit_max, ceil(TARGET_WG / (B*Hkv))).  At large batch the (seq, kv-head)
@@ -53,7 +55,8 @@
 namespace {
 
 constexpr int BS = 64;            // tokens per KV block (engine-wide constant)
-constexpr int TARGET_WG = 1024;   // ~4 workgroups per CU before contexts are split
+constexpr int TARGET_WG = 512;    // ~2 workgroups per CU before contexts are split (1024 measured
+                                  // 13-17 % slower at B = 32-64, ctx 600: profiles/attn_split_r4l.log)
 constexpr int WAVE_SLOTS = 2048;  // 256 CUs x 4 SIMDs x 2 waves/SIMD
 constexpr float LOG2E = 1.4426950408889634f;
 
@@ -107,6 +110,9 @@ __global__ void __launch_bounds__(64 * WPP) __attribute__((amdgpu_waves_per_eu(2
   // splits past this sequence's context exit at once; the merge kernel only reads
   // the ceil(nblk / bps) splits that exist.
   if (split > 0 && bstart >= nblk) return;
+  // a context that fits in one split (short chats at small batch) is finished here:
+  // split 0 writes the normalised bf16 row and the merge kernel skips it
+  const bool single = nsplit == 1 || nblk <= bps;
 
   // Q^T fragments (B operand): lane holds Q[head kvh*G + i16][32ks + 8h .. +7]
   bf16x8 qf[KS];
@@ -328,7 +334,7 @@ __global__ void __launch_bounds__(64 * WPP) __attribute__((amdgpu_waves_per_eu(2
     // one wave owns the (pair, split): write straight from the accumulators
     if (i16 < G) {
       const int64_t row = (int64_t)b * Hkv * G + kvh * G + i16;
-      if (nsplit == 1) {
+      if (single) {
         const float inv = l > 0.f ? 1.f / l : 0.f;
         bf16* op = out + row * D + 4 * h;
 #pragma unroll
@@ -383,7 +389,7 @@ __global__ void __launch_bounds__(64 * WPP) __attribute__((amdgpu_waves_per_eu(2
       acc[c] = a;
     }
     const int head = kvh * G + row;
-    if (nsplit == 1) {
+    if (single) {
       const float inv = lt > 0.f ? 1.f / lt : 0.f;
       bf16* op = out + ((int64_t)b * Hkv * G + head) * D + dc * CH;
 #pragma unroll
@@ -417,6 +423,7 @@ __global__ void __launch_bounds__(256) decode_merge_kernel(bf16* __restrict__ ou
   const int nblk = min((max(ctx_lens[row / Hq] - ctx_adj, 0) + BS - 1) / BS, max_blocks);
   const int bps = split_blocks(nblk, nsplit_grid, min_bps);
   const int nsplit = max(1, min(nsplit_grid, (nblk + bps - 1) / bps));
+  if (nblk <= bps) return;   // one split: the attention kernel wrote the row itself
   const float* ml = part_ml + (int64_t)row * nsplit_grid * 2;
   float mstar = -1e30f;
   for (int s = 0; s < nsplit; ++s) mstar = fmaxf(mstar, ml[2 * s]);
@@ -434,8 +441,9 @@ __global__ void __launch_bounds__(256) decode_merge_kernel(bf16* __restrict__ ou
 
 // Number of KV splits a decode launch over B sequences uses (<= nsplit_max).
 int64_t decode_nsplit(int64_t B, int64_t Hkv, int64_t nsplit_max) {
+  static const int64_t target = getenv("LS_ATTN_TARGET_WG") ? atoll(getenv("LS_ATTN_TARGET_WG")) : TARGET_WG;
   const int64_t pairs = std::max<int64_t>(1, B * Hkv);
-  return std::max<int64_t>(1, std::min<int64_t>(nsplit_max, (TARGET_WG + pairs - 1) / pairs));
+  return std::max<int64_t>(1, std::min<int64_t>(nsplit_max, (target + pairs - 1) / pairs));
 }
 
 // q: [B, Hq*D] view (row stride q_stride elements), out: [B, Hq, D] contiguous.
