@@ -169,6 +169,32 @@ def test_native_executor_matches_python_executor():
         _same_or_near_tie(a, b)
 
 
+@pytest.mark.parametrize("n", [1, 2, 3, 4])
+def test_batch_le4_fused_gemv_decode_matches_python_executor(n):
+    """Decode batches of 1-4 rows take the runner's fused GEMV layer (gemm_gemv.hip: qkv
+    with RoPE + KV write, o, gate_up with SwiGLU, down; the add + RMSNorm in the next
+    GEMV's prologue up to 2 rows, a separate fused_add_rmsnorm above): greedy tokens of
+    the native executor (graphs) against the Python executor.  The model's dimensions are
+    multiples of 512 (llama-small's 2816-wide MLP is not, so it never reaches this path)."""
+    from langstream_amd.engine.arena import PyStepExecutor
+    from langstream_amd.engine.llm_engine import NSLOTS
+    from langstream_amd.models.llama import LlamaConfig
+    cfg = LlamaConfig(name="llama-gemv", vocab_size=32000, hidden_size=1024, intermediate_size=3072, num_layers=4,
+                      num_heads=8, num_kv_heads=2, head_dim=128, max_position=4096, bos_token_id=1, eos_token_ids=(2,))
+    model = LlamaModel(cfg, device="cuda")
+    prompts = [list(range(3 + 7 * i, 3 + 7 * i + n_tok)) for i, n_tok in enumerate((5, 70, 129, 300)[:n])]
+    sp = SamplingParams(max_tokens=12, temperature=0.0, ignore_eos=True)
+    sp_ref = SamplingParams(max_tokens=12, temperature=0.0, ignore_eos=True, logprobs=2)
+    e1 = LLMEngine(model, None, num_blocks=128, max_model_len=1024, max_batch=8)
+    out1 = _run_tops(e1, prompts, sp)
+    assert e1.stats["graph_steps"] > 0
+    e2 = LLMEngine(model, None, num_blocks=128, max_model_len=1024, max_batch=8, use_graphs=False)
+    e2.exec = PyStepExecutor(model, e2.kv_caches, e2.layout, NSLOTS, e2.nsplit, e2.bps, e2.device)
+    out2 = _run_tops(e2, prompts, sp_ref)
+    for a, b in zip(out1, out2):
+        _same_or_near_tie(a, b)
+
+
 def test_llama_graph_decode_matches_eager():
     cfg = PRESETS["llama-small"]
     model = LlamaModel(cfg, device="cuda")
