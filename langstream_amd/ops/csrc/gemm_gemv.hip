@@ -404,9 +404,11 @@ struct Extra {
 template <int TR, int KCH, int EPI, bool PRO>
 void launch_rb(const at::Tensor& x, const at::Tensor& w, at::Tensor& out, int T, int N, int K, hipStream_t st,
                const Extra& ex) {
-  // the compiler streams W through a rolling window of ~8 loads per wave, so RB sets the
-  // rows sharing one x fetch + reduction, not the VGPR count (RB = 2 at K = 14336, T = 4
-  // measured 0.7x hipBLASLt; profiles/gemv_bench.log)
+  // RB sets the rows sharing one x fetch + reduction.  Where x + W fit in ~128 VGPRs
+  // (K <= 4096 at T <= 4) every W load is pinned ahead of the dots (see the kernel); at
+  // larger K the compiler streams W through a rolling window of loads per wave instead,
+  // so RB does not set the VGPR count there (RB = 2 at K = 14336, T = 4 measured 0.7x
+  // hipBLASLt; profiles/gemv_bench.log)
   constexpr int RB = KCH <= 3 ? 8 : 4;
   const int rows_per_block = EPI == EPI_SILU ? RB / 2 : RB;
   const int nrows = EPI == EPI_SILU ? N / 2 : N;
