@@ -365,11 +365,15 @@ class LlamaRunner {
         if (l == 0) {
           gemv_qkv(qkv, x, qkv_w_[l], pos, cos_sin_, slots, kc_[l], vc_[l], hq_, hkv_, true, c10::nullopt,
                    c10::nullopt, c10::nullopt, c10::nullopt, eps_);
-        } else {
+        } else if (T <= gemv_pro_max_t()) {
           at::Tensor rn = at::empty_like(residual);
           gemv_qkv(qkv, x, qkv_w_[l], pos, cos_sin_, slots, kc_[l], vc_[l], hq_, hkv_, true, dn, residual, rn,
                    in_norm_[l], eps_);
           residual = rn;
+        } else {
+          fused_add_rmsnorm(dn, residual, in_norm_[l], eps_);
+          gemv_qkv(qkv, dn, qkv_w_[l], pos, cos_sin_, slots, kc_[l], vc_[l], hq_, hkv_, true, c10::nullopt,
+                   c10::nullopt, c10::nullopt, c10::nullopt, eps_);
         }
         at::Tensor attn = attend(l, qkv, true);
         at::Tensor o = at::empty_like(residual);
@@ -635,7 +639,7 @@ class LlamaRunner {
     return on;
   }
 
-  // Largest T whose gate_up GEMV recomputes the add + RMSNorm in its prologue.  Each
+  // Largest T whose qkv / gate_up GEMVs recompute the add + RMSNorm in their prologue.  Each
   // block re-reads o and the residual (2 T K bf16 from L2), which at T = 4 equals the
   // block's 64 KB of weights: gate_up measured 62 us with the prologue against 41 us
   // plain + a separate fused_add_rmsnorm launch; batch-4 decode step 4.59 -> 4.15 ms
