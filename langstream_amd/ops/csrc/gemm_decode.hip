@@ -134,7 +134,7 @@ __device__ __forceinline__ int piece_chunk(int lane, int row) { return ((lane & 
 // writes the partial slabs with non-temporal stores.
 // LD: dedicated loader waves (0 or 4).  With LD = 4 the workgroup is 8 compute + 4
 // loader waves: only the loaders issue LDS-DMA.  Measured (tools/dgemm_bench.py
-// --ablate, profiles/dgemm_ablation_r3.log): with every wave issuing its share of the
+// --ablate, profiles/dgemm_ablation_r3a.log, dgemm_ablation_r3b_loaders.log): with every wave issuing its share of the
 // stage right after the barrier, a full DMA queue blocks the issuing wave before its
 // MFMAs, so a step costs DMA + compute instead of max(DMA, compute).
 template <int BN, int XS, int WS, int EPI, int ABL = 0, int LD = 0, int BMT = BM, int SPB = 1>

@@ -343,7 +343,7 @@ __global__ void __launch_bounds__(256) knn_filter_kernel(const bf16* __restrict_
 // overlapped); interleaved (below) the pass takes 1572 us and 1337 without MFMAs -- the
 // fragment-read stream, not the MFMA pipe or the DMA / barrier (1378 without them), now
 // bounds it.
-// Measured at Q = 2048 over 1M x 384 (profiles/knn_pmc_*, r4): MFMA busy ~41 %, waves
+// Measured at Q = 2048 over 1M x 384 (profiles/knn_pmc_r4/): MFMA busy ~41 %, waves
 // parked in waitcnt / barrier ~49 %, L2 hit 85 %, LDS array ~23 % busy.  Dead ends: a
 // one-ballot epilogue test + buffer-resource DMA addressing + pinned fragment reads (VALU
 // per MFMA 5.7 -> ~1.5 in the loop: no change in time), moving the barrier to mid-tile
