@@ -322,8 +322,9 @@ def main():
     ap.add_argument("--no-persist", action="store_true",
                     help="keep the vector store in HBM only (default: WAL + snapshots on local disk, the "
                          "durable default of a vector-db-sink pod)")
-    ap.add_argument("--config", choices=("rag", "embed", "chat"), default="rag",
-                    help="rag: BASELINE config 4 (the headline, default); embed: config 2 (compute-ai-embeddings "
+    ap.add_argument("--config", choices=("rag", "embed", "chat", "split"), default="rag",
+                    help="rag: BASELINE config 4 (the headline, default); split: config 1 (text-splitter on an "
+                         "in-memory topic, CPU only); embed: config 2 (compute-ai-embeddings "
                          "agent on Kafka records); chat: config 3 (ai-chat-completions through the websocket "
                          "gateway), and config 5 with --chat-model llama-3-70b --gpus 8 --tp 8")
     ap.add_argument("--tp", type=int, default=0, help="chat: tensor-parallel degree (= --gpus)")
@@ -345,6 +346,9 @@ def main():
     rank, world, local = _env_int("RANK", 0), _env_int("WORLD_SIZE", 1), _env_int("LOCAL_RANK", 0)
     if world != args.gpus:
         sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.config == "split":
+        from langstream_amd.bench import split
+        return split.run(args)
     if args.config != "rag":
         return _other_config(args, rank, world, local)
     corpus_sentences = max(4000, args.corpus // 4 + 1)

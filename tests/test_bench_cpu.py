@@ -91,3 +91,12 @@ def test_bench_eight_ranks_dp8_disjoint_partitions(tmp_path):
             for j in range(i + 1, 8):
                 assert not owned[i] & owned[j], (topic, i, j)
     assert all(n > 0 for n in d["knn_rounds_per_rank"])
+
+
+def test_bench_config1_text_splitter_on_memory_topic(tmp_path):
+    """BASELINE config 1 (CPU only): the text-splitter agent on the in-memory streaming
+    cluster; every chunk the agent's own splitter predicts is read back per step."""
+    d = _run(["--config", "split", "--steps", "2", "--warmup", "1", "--batch", "16"], tmp_path, timeout=300)
+    assert d["n_gpus"] == 0 and d["value"] > 0 and d["steps"] == 2
+    assert d["config"]["agent"] == "text-splitter" and d["config"]["streaming"] == "memory"
+    assert d["chunks_per_document"] > 1 and d["chunks_per_s"] > d["value"]
