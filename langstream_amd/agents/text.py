@@ -22,7 +22,7 @@ import json
 import re
 import zipfile
 import zlib
-from typing import Any, Callable, Dict, List, Optional
+from typing import Any, Callable, Dict, List, Optional, Tuple
 
 from ..api.agent import SingleRecordAgentProcessor
 from ..api.record import Header, SimpleRecord
@@ -78,13 +78,15 @@ class RecursiveCharacterTextSplitter:
         t = sep.join(docs).strip()
         return t or None
 
-    def _merge(self, splits: List[str], sep: str) -> List[str]:
+    def _merge(self, splits: List[Tuple[str, int]], sep: str) -> List[str]:
+        """``splits``: (piece, length) pairs -- each piece's length is computed once by
+        the caller (the length function is a BPE count: the dominant cost of a split)."""
         docs: List[str] = []
         cur: List[str] = []
+        cur_len: List[int] = []
         total = 0
-        sep_len = self.length(sep)
-        for d in splits:
-            ln = self.length(d)
+        sep_len = self.length(sep) if sep else 0
+        for d, ln in splits:
             if total + ln + (sep_len if cur else 0) > self.chunk_size:
                 if cur:
                     doc = self._join(cur, sep)
@@ -92,9 +94,11 @@ class RecursiveCharacterTextSplitter:
                         docs.append(doc)
                     while total > self.chunk_overlap or (
                             total + ln + (sep_len if cur else 0) > self.chunk_size and total > 0):
-                        total -= self.length(cur[0]) + (sep_len if len(cur) > 1 else 0)
+                        total -= cur_len[0] + (sep_len if len(cur) > 1 else 0)
                         cur.pop(0)
+                        cur_len.pop(0)
             cur.append(d)
+            cur_len.append(ln)
             total += ln + (sep_len if len(cur) > 1 else 0)
         doc = self._join(cur, sep)
         if doc is not None:
@@ -114,11 +118,12 @@ class RecursiveCharacterTextSplitter:
                 new_seps = separators[i + 1:]
                 break
         splits = self._split_regex(text, separator, self.keep_separator)
-        good: List[str] = []
+        good: List[Tuple[str, int]] = []
         sep_use = "" if self.keep_separator else separator
         for s in splits:
-            if self.length(s) < self.chunk_size:
-                good.append(s)
+            ln = self.length(s)
+            if ln < self.chunk_size:
+                good.append((s, ln))
             else:
                 if good:
                     final.extend(self._merge(good, sep_use))
