@@ -241,12 +241,14 @@ def rope_and_cache(qkv, pos, cos_sin, slots, k_cache, v_cache, Hq: int, Hkv: int
 
 
 # ---------------------------------------------------------------- attention
-def decode_splits(max_blocks: int, min_blocks_per_split: int = 4) -> tuple[int, int]:
+def decode_splits(max_blocks: int, min_blocks_per_split: int = 0) -> tuple[int, int]:
     """Split-KV plan for decode: (nsplit_max, min_blocks_per_split).  The kernel picks
     the split count per launch from the batch (no split once B*Hkv workgroups fill the
     chip; see attention_decode.hip), and each sequence spreads its own context evenly
     over the splits (at least `min_blocks_per_split` blocks each, one per wave), so one
     captured graph serves every context length.  The workspace is sized for nsplit_max."""
+    if min_blocks_per_split <= 0:
+        min_blocks_per_split = int(os.environ.get("LS_ATTN_MIN_BPS", "4"))
     bps = max(1, min_blocks_per_split)
     nsplit = max(1, (max_blocks + bps - 1) // bps)
     return nsplit, bps
