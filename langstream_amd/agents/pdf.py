@@ -615,10 +615,19 @@ class _Font:
 
 class _Doc:
     def __init__(self, data: bytes):
+        from .text import inflate_limit
         self.data = data
         self.objs: Dict[int, Any] = {}
+        # file offset of the definition each object number currently resolves to: a later
+        # definition (an incremental update appended to the file) supersedes an earlier one,
+        # whether either sits at the top level or inside an object stream
+        self._pos: Dict[int, int] = {}
         self.streams: Dict[int, Tuple[Dict[str, Any], int, int]] = {}
         self._fonts: Dict[int, _Font] = {}
+        # ONE decompression budget for the whole document (Tika-style 100x of the file,
+        # at least 1 MiB), shared by every FlateDecode / LZW stream like text._zip_read's
+        self._budget = inflate_limit(len(data))
+        self._decoded: Dict[int, bytes] = {}
         self._scan()
 
     # -- object table
@@ -652,8 +661,11 @@ class _Doc:
                 self.streams[num] = (obj, s, e)
             else:
                 self.objs[num] = obj
-        # objects inside object streams (later definitions win, like incremental updates)
-        for num, (d, _, _) in list(self.streams.items()):
+            self._pos[num] = m.start()
+        # objects inside object streams, in file order: an entry replaces a definition
+        # that comes EARLIER in the file (an update appended an object stream), never a
+        # later one (an update appended a top-level object)
+        for num, (d, _, _) in sorted(self.streams.items(), key=lambda kv: self._pos.get(kv[0], 0)):
             if d.get("Type") == "ObjStm":
                 try:
                     self._load_objstm(num, d)
@@ -677,13 +689,15 @@ class _Doc:
             if k1 != "num" or k2 != "num":
                 break
             pairs.append((int(onum), int(off)))
+        here = self._pos.get(num, 0)
         for onum, off in pairs:
-            if onum in self.objs:
+            if onum == num or self._pos.get(onum, -1) > here:
                 continue
             try:
                 self.objs[onum] = _Lexer(raw, first + off).parse()
             except Exception:  # noqa: BLE001
                 continue
+            self._pos[onum] = here
 
     def resolve(self, v: Any, depth: int = 0) -> Any:
         while isinstance(v, Ref) and depth < 32:
@@ -697,12 +711,24 @@ class _Doc:
             return self.streams[v[1]][0]
         return None
 
+    def _spend(self, n: int):
+        from .text import DecompressionBombError
+        self._budget -= n
+        if self._budget < 0:
+            raise DecompressionBombError("PDF streams inflate past the document's budget")
+
     def stream_data(self, v: Any) -> bytes:
-        from .text import bounded_inflate
         v = self.resolve(v)
         if not (isinstance(v, tuple) and v[0] == "stream"):
             return b""
-        d, s, e = self.streams[v[1]]
+        num = v[1]
+        if num not in self._decoded:
+            self._decoded[num] = self._decode(num)
+        return self._decoded[num]
+
+    def _decode(self, num: int) -> bytes:
+        from .text import bounded_inflate
+        d, s, e = self.streams[num]
         raw = self.data[s:e]
         filters = self.resolve(d.get("Filter"))
         parms = self.resolve(d.get("DecodeParms"))
@@ -715,12 +741,13 @@ class _Doc:
             p = self.resolve(p) or {}
             if f in ("FlateDecode", "Fl"):
                 try:
-                    raw = bounded_inflate(raw)
+                    raw = bounded_inflate(raw, limit=max(0, self._budget))
                 except Exception as ex:  # noqa: BLE001 - truncated streams: salvage what inflates
                     from .text import DecompressionBombError
                     if isinstance(ex, DecompressionBombError):
                         raise
-                    raw = _inflate_partial(raw)
+                    raw = _inflate_partial(raw, max(0, self._budget))
+                self._spend(len(raw))
                 pred = int(self.resolve(p.get("Predictor", 1)) or 1) if isinstance(p, dict) else 1
                 if pred >= 10:
                     raw = _png_unpredict(raw, int(self.resolve(p.get("Columns", 1)) or 1),
@@ -731,9 +758,9 @@ class _Doc:
             elif f in ("ASCII85Decode", "A85"):
                 raw = _ascii85(raw)
             elif f in ("LZWDecode", "LZW"):
-                from .text import inflate_limit
                 early = int(self.resolve(p.get("EarlyChange", 1))) if isinstance(p, dict) else 1
-                raw = _lzw(raw, early, inflate_limit(len(raw)))
+                raw = _lzw(raw, early, max(0, self._budget))
+                self._spend(len(raw))
             elif f in ("RunLengthDecode", "RL"):
                 raw = _run_length(raw)
             else:                                  # image codecs, Crypt: no text
@@ -785,12 +812,11 @@ class _Doc:
         return out
 
 
-def _inflate_partial(raw: bytes) -> bytes:
+def _inflate_partial(raw: bytes, limit: int) -> bytes:
     import zlib
-    from .text import inflate_limit
     d = zlib.decompressobj()
     try:
-        return d.decompress(raw, inflate_limit(len(raw)))
+        return d.decompress(raw, limit)
     except zlib.error:
         return b""
 

@@ -488,7 +488,7 @@ def l2_normalize_rows(x):
     return torch.nn.functional.normalize(x.float(), dim=-1, eps=1e-12).to(x.dtype)
 
 
-def knn_topk(X, Q, k: int, sample_chunks: Optional[int] = None):
+def knn_topk(X, Q, k: int, sample_chunks: Optional[int] = None, _ablate: int = 0):
     """Top-k rows of X by dot product with each query row.  Returns (scores f32 [Q,k], idx int32 [Q,k]).
     GPU: the first ``sample_chunks`` x 1024 rows are searched exactly and set a per-query
     threshold for the rest (0 = search every chunk exactly); ties go to the lower row."""
@@ -504,6 +504,9 @@ def knn_topk(X, Q, k: int, sample_chunks: Optional[int] = None):
             sample_chunks = 16 if Qn >= 1024 else 32
         ws_s = torch.empty(max(1, Qn * nchunks * k), dtype=torch.float32, device=dev)
         ws_i = torch.empty(Qn * nchunks * k + 3 * Qn, dtype=torch.int32, device=dev)
+        if _ablate:   # tools/engine_bench.py --knn-ablate only: timing ablations, wrong results
+            hip().knn_topk_ablate(X, Q, k, out_s, out_i, ws_s, ws_i, sample_chunks, _ablate)
+            return out_s, out_i
         hip().knn_topk(X, Q, k, out_s, out_i, ws_s, ws_i, sample_chunks)
         if sample_chunks > 0 and nchunks > sample_chunks and bool(ws_i[-Qn:].any()):
             # a candidate list overflowed (many rows above the sample's K-th best): exact rerun

@@ -336,8 +336,41 @@ void oneshot_allreduce_i64(const std::shared_ptr<OneShotAllReduce>& ar, at::Tens
 void oneshot_allgather32(const std::shared_ptr<OneShotAllReduce>& ar, const at::Tensor& in, at::Tensor out) {
   ar->run_gather32(in, out);
 }
+// Bytes ONE call may move (one buffer half: run_sum_i64 / run_gather32 accept up to
+// capacity() bf16 elements' worth; the other half is the next call's).
 int64_t oneshot_capacity_bytes(const std::shared_ptr<OneShotAllReduce>& ar) {
-  return 2 * ar->capacity() * (int64_t)sizeof(bf16);
+  return ar->capacity() * (int64_t)sizeof(bf16);
+}
+
+// The sampler's int64 sum: on the one-shot buffers when the message fits one call, c10d
+// otherwise.  Returns true when the one-shot path ran.
+bool oneshot_route_sum_i64(const std::shared_ptr<OneShotAllReduce>& ar,
+                           const c10::intrusive_ptr<::c10d::ProcessGroup>& pg, at::Tensor t) {
+  if (ar && t.numel() * 8 <= oneshot_capacity_bytes(ar)) {
+    ar->run_sum_i64(t);
+    return true;
+  }
+  std::vector<at::Tensor> v{t};
+  pg->allreduce(v)->wait();
+  return false;
+}
+
+// The sampler's 32-bit all-gather (dst = W x src), routed the same way.
+bool oneshot_route_gather32(const std::shared_ptr<OneShotAllReduce>& ar,
+                            const c10::intrusive_ptr<::c10d::ProcessGroup>& pg, const at::Tensor& src,
+                            const at::Tensor& dst) {
+  const int64_t W = pg->getSize(), per = src.numel();
+  if (ar && per * 4 <= oneshot_capacity_bytes(ar)) {
+    at::Tensor d = dst;
+    ar->run_gather32(src, d);
+    return true;
+  }
+  std::vector<at::Tensor> parts;
+  for (int64_t w = 0; w < W; ++w) parts.push_back(dst.narrow(0, w * per, per));
+  std::vector<std::vector<at::Tensor>> outs{parts};
+  std::vector<at::Tensor> ins{src};
+  pg->allgather(outs, ins)->wait();
+  return false;
 }
 const int* oneshot_allreduce_err(const std::shared_ptr<OneShotAllReduce>& ar) { return ar->err_ptr(); }
 
@@ -400,4 +433,18 @@ std::vector<at::Tensor> oneshot_collectives_selftest(py::object process_group, a
   ar->run_gather32(g32, g2);
   AR_OK(hipStreamSynchronize(at::hip::getCurrentHIPStream().stream()));
   return {bf, g1, i64, g2, at::full({1}, ar->error(), i64.options())};
+}
+
+// The runner's routing of the sampler collectives: returns {summed i64, gathered g32,
+// [one-shot used for the sum, for the gather]}.  Messages past one call's capacity must
+// fall back to c10d instead of failing the one-shot size check.
+std::vector<at::Tensor> oneshot_route_selftest(py::object process_group, at::Tensor g32, at::Tensor i64, int64_t cap) {
+  auto pg = py::cast<c10::intrusive_ptr<::c10d::ProcessGroup>>(process_group);
+  auto ar = make_oneshot_allreduce(pg, cap);
+  at::Tensor g = at::empty({pg->getSize() * g32.numel()}, g32.options());
+  const bool a = oneshot_route_sum_i64(ar, pg, i64);
+  const bool b = oneshot_route_gather32(ar, pg, g32, g);
+  AR_OK(hipStreamSynchronize(at::hip::getCurrentHIPStream().stream()));
+  at::Tensor used = at::tensor({(int64_t)a, (int64_t)b, ar->error()}, at::kLong);
+  return {i64, g, used};
 }

@@ -41,8 +41,11 @@ std::vector<at::Tensor> oneshot_allreduce_sim(std::vector<at::Tensor> inputs, in
 int64_t oneshot_allreduce_selftest(py::object process_group, at::Tensor t);
 std::vector<at::Tensor> oneshot_collectives_selftest(py::object process_group, at::Tensor bf, at::Tensor g32,
                                                      at::Tensor i64, int64_t cap);
+std::vector<at::Tensor> oneshot_route_selftest(py::object process_group, at::Tensor g32, at::Tensor i64, int64_t cap);
 void knn_topk(at::Tensor X, at::Tensor Q, int64_t K, at::Tensor out_s, at::Tensor out_i, at::Tensor ws_s,
               at::Tensor ws_i, int64_t sample);
+void knn_topk_ablate(at::Tensor X, at::Tensor Q, int64_t K, at::Tensor out_s, at::Tensor out_i, at::Tensor ws_s,
+                     at::Tensor ws_i, int64_t sample, int64_t abl);
 int64_t knn_default_sample();
 void skinny_gemm(at::Tensor out, at::Tensor x, at::Tensor w);
 void gemv(at::Tensor out, at::Tensor x, at::Tensor w);
@@ -87,6 +90,7 @@ void decode_gemm_qkv_cmb(at::Tensor qkv, at::Tensor x, at::Tensor w, at::Tensor 
                          at::Tensor sumsq_in, double eps, at::Tensor pos, at::Tensor cos_sin, at::Tensor slots,
                          at::Tensor k_cache, at::Tensor v_cache, int64_t Hq, int64_t Hkv, at::Tensor err);
 void decode_gemm_silu_r(at::Tensor out, at::Tensor x, at::Tensor w, at::Tensor sumsq_in, double eps);
+pybind11::dict decode_gemm_launch_counts(bool reset);
 void rms_prep(at::Tensor y, at::Tensor sumsq, at::Tensor h, at::Tensor g);
 void rows_rms_scale(at::Tensor out, at::Tensor y, at::Tensor sumsq, double eps);
 void bind_runners(pybind11::module_& m);
@@ -113,11 +117,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("stall_rank") = -1);
   m.def("oneshot_allreduce_selftest", &oneshot_allreduce_selftest);
   m.def("oneshot_collectives_selftest", &oneshot_collectives_selftest);
+  m.def("oneshot_route_selftest", &oneshot_route_selftest);
   m.def("tp_sample_stats", &tp_sample_stats);
   m.def("tp_sample_hist", &tp_sample_hist);
   m.def("tp_sample_pick", &tp_sample_pick);
   m.def("tp_sample_final", &tp_sample_final);
   m.def("knn_default_sample", &knn_default_sample);
+  m.def("knn_topk_ablate", &knn_topk_ablate);
   m.def("skinny_gemm", &skinny_gemm);
   m.def("gemv", &gemv);
   m.def("gemv_supported", &gemv_supported);
@@ -150,6 +156,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("decode_gemm_res", &decode_gemm_res);
   m.def("decode_gemm_qkv_cmb", &decode_gemm_qkv_cmb);
   m.def("decode_gemm_silu_r", &decode_gemm_silu_r);
+  m.def("decode_gemm_launch_counts", &decode_gemm_launch_counts, py::arg("reset") = false);
   m.def("rms_prep", &rms_prep);
   m.def("rows_rms_scale", &rows_rms_scale);
   bind_runners(m);

@@ -35,6 +35,8 @@
 // err[0] and the host checks it (ops.decode_gemm_error).
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
+#include <atomic>
+#include <string>
 #include "common.h"
 
 void splitk_reduce_launch(const float* part, int S, int M, int N, bf16* out, int64_t ldo, hipStream_t st);
@@ -626,12 +628,21 @@ int split_outer_default() {
 int wnt_default() { return env_int("LS_DGEMM_WNT", 1); }
 int ntst_default() { return env_int("LS_DGEMM_NTST", 1); }
 
+// Host-side launch census per (BN, epilogue, tile rows, K splits): the tests read it to
+// prove which kernel variant a shape was routed to (decode_gemm_launch_counts).
+// Relaxed atomics on the host only; one increment per launch.
+constexpr int kCensusBn = 3, kCensusEpi = 7, kCensusBm = 3, kCensusS = 17;
+std::atomic<int64_t> g_census[kCensusBn][kCensusEpi][kCensusBm][kCensusS];
+constexpr int census_bn(int bn) { return bn == 64 ? 0 : bn == 128 ? 1 : 2; }
+constexpr int census_bm(int bm) { return bm == 64 ? 0 : bm == 128 ? 1 : 2; }
+
 // ring shapes: BN = 128: X 3 slots (2 ahead) + W 4 slots (3 ahead) = 160 KB;
 // BN = 256: X 2 + W 3 = 160 KB.
 template <int BN, int EPI, int BMT>
 void dgemm_launch_bm(int S, int tiles, hipStream_t st, const at::Tensor& x, const at::Tensor& w, int M, int N, int K,
                      bf16* out, int64_t ldo, float* part, int F, unsigned* tickets, float* xchg, int* err,
                      const DgArgs& ga) {
+  g_census[census_bn(BN)][EPI][census_bm(BMT)][std::min(S, kCensusS - 1)].fetch_add(1, std::memory_order_relaxed);
   // small tiles: two stages per barrier and the LDS they leave as a deeper W ring (8 / 6
   // slots at 64 / 128 rows: 96 / 64 KB of weights issued ahead)
   constexpr int SPB = BMT == BM ? 1 : 2;
@@ -709,6 +720,24 @@ int pick_bn(int N) {
 }
 
 }  // namespace
+
+// The launch census since the last reset: {"bn128_partial_bm64_s3": n, ...}.
+pybind11::dict decode_gemm_launch_counts(bool reset) {
+  static const char* epi_names[kCensusEpi] = {"store", "partial", "silu", "silu2", "cmb_res", "cmb_qkv", "silu_r"};
+  static const int bns[kCensusBn] = {64, 128, 256}, bms[kCensusBm] = {64, 128, 256};
+  pybind11::dict d;
+  for (int a = 0; a < kCensusBn; ++a)
+    for (int e = 0; e < kCensusEpi; ++e)
+      for (int b = 0; b < kCensusBm; ++b)
+        for (int s = 0; s < kCensusS; ++s) {
+          const int64_t n = reset ? g_census[a][e][b][s].exchange(0) : g_census[a][e][b][s].load();
+          if (n == 0) continue;
+          const std::string key = "bn" + std::to_string(bns[a]) + "_" + epi_names[e] + "_bm" + std::to_string(bms[b]) +
+                                  "_s" + std::to_string(s);
+          d[pybind11::str(key)] = n;
+        }
+  return d;
+}
 
 // Shapes: K % 64 == 0, N % 128 == 0; silu: the fused [2F, K] gate_up weight, F % 128 == 0.
 bool decode_gemm_supported(const at::Tensor& w, bool silu) {

@@ -829,8 +829,9 @@ __global__ void __launch_bounds__(256) knn_select4_kernel(const float* __restric
 // (K-th best of the sample -> threshold); thresholded main pass over the rest; select
 // (answer).  sample <= 0 or >= nchunks: every chunk is searched exactly.  The caller
 // checks the overflow flags (ws_i tail) and reruns exactly if any is set.
-void knn_topk(at::Tensor X, at::Tensor Q, int64_t K, at::Tensor out_s, at::Tensor out_i, at::Tensor ws_s,
-              at::Tensor ws_i, int64_t sample) {
+namespace {
+void knn_topk_impl(at::Tensor X, at::Tensor Q, int64_t K, at::Tensor out_s, at::Tensor out_i, at::Tensor ws_s,
+                   at::Tensor ws_i, int64_t sample, int abl_req) {
   TORCH_CHECK(X.scalar_type() == at::kBFloat16 && Q.scalar_type() == at::kBFloat16);
   TORCH_CHECK(X.is_contiguous() && Q.is_contiguous() && X.dim() == 2 && Q.dim() == 2);
   const int dim = X.size(1);
@@ -883,10 +884,10 @@ void knn_topk(at::Tensor X, at::Tensor Q, int64_t K, at::Tensor out_s, at::Tenso
     const int nrb = (int)((rows + rpw - 1) / rpw);
     const int G = 16 * nrb;
     if (G_out) *G_out = G;
-    // LS_KNN_ABL (diagnosis only, wrong results): the main pass without its sync (1),
-    // without sync and DMA (2), without MFMAs (3); MODE 1 only
-    const char* ae = getenv("LS_KNN_ABL");
-    const int abl = ae != nullptr && mode == 1 && dim == 384 ? atoi(ae) : 0;
+    // abl_req (knn_topk_ablate only -- diagnosis, wrong results): the main pass without
+    // its sync (1), without sync and DMA (2), without MFMAs (3); MODE 1, 384 dims only.
+    // The serving entry point (knn_topk) always passes 0.
+    const int abl = mode == 1 && dim == 384 ? abl_req : 0;
     dim3 grid(nrb * nqb);
 #define LAUNCH_Q(DD, MM)                                                                                         \
   launch_q256<DD, MM>(abl, grid, stream, (const bf16*)X.data_ptr(), N, (const bf16*)Q.data_ptr(), Qn,            \
@@ -955,6 +956,21 @@ void knn_topk(at::Tensor X, at::Tensor Q, int64_t K, at::Tensor out_s, at::Tenso
     filter(ns, nchunks - ns);
   }
   select(0);
+}
+}  // namespace
+
+void knn_topk(at::Tensor X, at::Tensor Q, int64_t K, at::Tensor out_s, at::Tensor out_i, at::Tensor ws_s,
+              at::Tensor ws_i, int64_t sample) {
+  knn_topk_impl(X, Q, K, out_s, out_i, ws_s, ws_i, sample, 0);
+}
+
+// Timing-only ablations of the large-batch main pass (tools/engine_bench.py --knn-ablate):
+// the results are WRONG by design, so this is a separate entry point the serving path
+// never calls (no environment switch on knn_topk).
+void knn_topk_ablate(at::Tensor X, at::Tensor Q, int64_t K, at::Tensor out_s, at::Tensor out_i, at::Tensor ws_s,
+                     at::Tensor ws_i, int64_t sample, int64_t abl) {
+  TORCH_CHECK(abl >= 0 && abl <= 3, "knn_topk_ablate: abl 0..3");
+  knn_topk_impl(X, Q, K, out_s, out_i, ws_s, ws_i, sample, (int)abl);
 }
 
 int64_t knn_default_sample() { return SAMPLE_CHUNKS; }

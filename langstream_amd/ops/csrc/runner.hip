@@ -107,6 +107,11 @@ void oneshot_allreduce_run(const std::shared_ptr<OneShotAllReduce>& ar, at::Tens
 void oneshot_allreduce_i64(const std::shared_ptr<OneShotAllReduce>& ar, at::Tensor t);
 void oneshot_allgather32(const std::shared_ptr<OneShotAllReduce>& ar, const at::Tensor& in, at::Tensor out);
 int64_t oneshot_capacity_bytes(const std::shared_ptr<OneShotAllReduce>& ar);
+bool oneshot_route_sum_i64(const std::shared_ptr<OneShotAllReduce>& ar,
+                           const c10::intrusive_ptr<::c10d::ProcessGroup>& pg, at::Tensor t);
+bool oneshot_route_gather32(const std::shared_ptr<OneShotAllReduce>& ar,
+                            const c10::intrusive_ptr<::c10d::ProcessGroup>& pg, const at::Tensor& src,
+                            const at::Tensor& dst);
 
 void skinny_gemm(at::Tensor out, at::Tensor x, at::Tensor w);
 void gemm_fused(at::Tensor out, at::Tensor x, at::Tensor w, c10::optional<at::Tensor> bias, bool gelu,
@@ -581,26 +586,8 @@ class LlamaRunner {
 
   // The sampler's collectives on the one-shot buffers when LS_ONESHOT_AR=1 (and the
   // message fits), c10d otherwise: int64 sum in place, 32-bit all-gather.
-  void allreduce_i64(at::Tensor t) {
-    if (oneshot_ && t.numel() * 8 <= oneshot_capacity_bytes(oneshot_)) {
-      oneshot_allreduce_i64(oneshot_, t);
-      return;
-    }
-    std::vector<at::Tensor> v{t};
-    pg_->allreduce(v)->wait();
-  }
-  void allgather32(const at::Tensor& src, const at::Tensor& dst) {
-    const int64_t W = pg_->getSize(), per = src.numel();
-    if (oneshot_ && per * 4 <= oneshot_capacity_bytes(oneshot_)) {
-      oneshot_allgather32(oneshot_, src, dst);
-      return;
-    }
-    std::vector<at::Tensor> parts;
-    for (int64_t w = 0; w < W; ++w) parts.push_back(dst.narrow(0, w * per, per));
-    std::vector<std::vector<at::Tensor>> outs{parts};
-    std::vector<at::Tensor> ins{src};
-    pg_->allgather(outs, ins)->wait();
-  }
+  void allreduce_i64(at::Tensor t) { oneshot_route_sum_i64(oneshot_, pg_, t); }
+  void allgather32(const at::Tensor& src, const at::Tensor& dst) { oneshot_route_gather32(oneshot_, pg_, src, dst); }
 
  private:
   at::Tensor embed(const at::Tensor& ids) {
@@ -707,7 +694,11 @@ class LlamaRunner {
     }();
     return !lib && dgemm_enabled() && dg_ws_.defined() && decode_gemm_supported(w, silu);
   }
-  // qkv rows on the skinny ring (measured faster than the 256-row decode GEMM at small T)
+  // Fallback routing when the decode GEMM does not take a step (LS_DGEMM=0, or T below
+  // LS_DGEMM_MIN_T): qkv rows up to this many go to the skinny ring.  With the default
+  // routing the decode GEMM is tried FIRST and takes every qkv from 5 rows (it measured
+  // faster than the skinny ring at every M from 5, profiles/dgemm_smallm_r4.log), so this
+  // knob only matters for those A/B runs.
   static int64_t skinny_qkv_max() {
     static const int64_t v = [] {
       const char* e = getenv("LS_SKINNY_QKV_MAX");

@@ -201,3 +201,53 @@ def test_oneshot_gather_and_int64_sum_processes_sharing_one_gpu(W):
         assert bf == [float(W * (W + 1) // 2)] * 1000, rank
         assert g1 == want_g.tolist() and g2 == want_g.tolist(), rank
         assert i64 == want_i.tolist(), rank
+
+
+def _route_rank(rank, world, port, q, n_i64, n_g32):
+    import os
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from langstream_amd import ops
+        g32 = (torch.arange(n_g32, dtype=torch.float32) + 10000 * rank).cuda()
+        i64 = (torch.arange(n_i64, dtype=torch.int64) * (rank + 1) + (1 << 40)).cuda()
+        out = ops.hip().oneshot_route_selftest(dist.group.WORLD, g32, i64, 2000)
+        q.put((rank, [t.cpu().tolist() for t in out]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("n_i64,n_g32,want_used", [
+    (700, 600, [0, 1]),     # int64 message between one buffer half (4000 B) and both (8000 B): c10d
+    (400, 1500, [1, 0]),    # gather past one half: c10d; the int64 sum fits: one-shot
+    (500, 1000, [1, 1]),    # both exactly at one call's capacity
+])
+def test_oneshot_routing_falls_back_to_c10d_past_one_call(n_i64, n_g32, want_used):
+    """Sampler collectives with LS_ONESHOT_AR=1 (runner.hip allreduce_i64 / allgather32):
+    a message larger than ONE call's half of the IPC buffer must go to c10d, not fail the
+    one-shot size check (the round-4 advisor case: R * 2048 int64 histograms)."""
+    import multiprocessing as mp
+    W = 2
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_route_rank, args=(r, W, port, q, n_i64, n_g32)) for r in range(W)]
+    for p in procs:
+        p.start()
+    try:
+        res = [q.get(timeout=100) for _ in range(W)]
+    finally:
+        for p in procs:
+            p.join(30)
+            if p.is_alive():
+                p.kill()
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    want_g = torch.cat([torch.arange(n_g32, dtype=torch.float32) + 10000 * r for r in range(W)])
+    want_i = sum(torch.arange(n_i64, dtype=torch.int64) * (r + 1) + (1 << 40) for r in range(W))
+    for rank, (i64, g, used) in res:
+        assert used == want_used + [0], (rank, used)
+        assert i64 == want_i.tolist(), rank
+        assert g == want_g.tolist(), rank

@@ -813,7 +813,42 @@ def _dg_ws(M, N):
     return torch.empty(64 * M * N + 4 * 256 * 256, device=DEV, dtype=torch.float32)
 
 
-@pytest.mark.parametrize("M", [129, 200, 256])
+# Every decode-GEMM test also proves which kernel variant ran: the dispatcher keeps a
+# host-side launch census per (BN, epilogue, tile rows, K splits).  _dg_* mirror the
+# dispatcher's routing rules (gemm_decode.hip pick_split / dgemm_launch / decode_gemm).
+_DG_SMALL_M = [5, 17, 64, 100, 128]
+_DG_ALL_M = _DG_SMALL_M + [129, 200, 256]
+
+
+def _dg_split(tiles, K, min_steps=4):
+    best = 1
+    for s in range(1, 65):
+        if tiles * s > 264 or (K // 64) // s < min_steps:
+            break
+        best = s
+    return best
+
+
+def _dg_bm(M, bn, epi):
+    if bn == 128 and epi in ("store", "partial", "silu"):
+        return 64 if M <= 64 else 128 if M <= 128 else 256
+    return 256
+
+
+def _dg_key(M, bn, epi, s):
+    return f"bn{bn}_{epi}_bm{_dg_bm(M, bn, epi)}_s{s}"
+
+
+def _dg_census_reset():
+    ops.hip().decode_gemm_launch_counts(True)
+
+
+def _dg_census_check(*keys):
+    got = dict(ops.hip().decode_gemm_launch_counts(True))
+    assert got == {k: 1 for k in keys}, (got, keys)
+
+
+@pytest.mark.parametrize("M", _DG_ALL_M)
 @pytest.mark.parametrize("name,N,K", _DG_SHAPES)
 @pytest.mark.parametrize("bn,splits", [(0, 0), (128, 1), (128, 5), (256, 3), (64, 0), (64, 3)])
 def test_decode_gemm(M, name, N, K, bn, splits):
@@ -824,29 +859,38 @@ def test_decode_gemm(M, name, N, K, bn, splits):
     w = (torch.randn(N, K, device=DEV) / K ** 0.5).to(torch.bfloat16)
     out = torch.full((M, N), float("nan"), device=DEV, dtype=torch.bfloat16)
     assert ops.hip().decode_gemm_supported(w, False)
+    _dg_census_reset()
     ops.hip().decode_gemm(out, x, w, _dg_ws(M, N), None, None, 1e-5, bn, splits)
+    bn_eff = bn or 128
+    S = min(splits, K // 64) if splits else _dg_split(N // bn_eff, K)
+    _dg_census_check(_dg_key(M, bn_eff, "store" if S == 1 else "partial", S))
     _close(out, x.float().cpu() @ w.float().cpu().t(), 0.02, 0.02, name)
 
 
-@pytest.mark.parametrize("M", [129, 200, 256])   # o8b above 128 rows: 64-column tiles, 4 K splits
-@pytest.mark.parametrize("name,N,K", [("o8b", 4096, 4096), ("down8b", 4096, 14336), ("o70b_tp8", 8192, 1024)])
+@pytest.mark.parametrize("M", _DG_ALL_M)   # o8b above 128 rows: 64-column tiles, 4 K splits
+@pytest.mark.parametrize("name,N,K", [("o8b", 4096, 4096), ("down8b", 4096, 14336), ("o70b_tp8", 8192, 1024),
+                                      ("o70b", 8192, 8192), ("down70b", 8192, 28672)])
 def test_decode_gemm_add_rmsnorm(M, name, N, K):
     torch.manual_seed(M + K)
     x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
     w = (torch.randn(N, K, device=DEV) / K ** 0.5).to(torch.bfloat16)
     res = torch.randn(M, N, device=DEV).to(torch.bfloat16)
     g = (1 + 0.1 * torch.randn(N, device=DEV)).to(torch.bfloat16)
-    res_exp = res.float().cpu() + x.float().cpu() @ w.float().cpu().t()
+    res_exp = (res.float() + x.float() @ w.float().t()).cpu()   # fp32 reference (gfx950 has no xf32)
     out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    _dg_census_reset()
     ops.hip().decode_gemm(out, x, w, _dg_ws(M, N), res, g, 1e-5)
+    bn = 64 if (K <= 4096 and M > 128) else 128
+    _dg_census_check(_dg_key(M, bn, "partial", _dg_split(N // bn, K)))
     _close(res, res_exp, 0.03, 0.03, "residual")
     rb = res_exp.to(torch.bfloat16).float()
     exp = rb * torch.rsqrt(rb.pow(2).mean(-1, keepdim=True) + 1e-5) * g.float().cpu()
     _close(out, exp, 0.05, 0.05, "normed")
 
 
-@pytest.mark.parametrize("M", [129, 256])
-@pytest.mark.parametrize("F,K,splits", [(14336, 4096, 2), (14336, 4096, 1), (3584, 8192, 2), (384, 1024, 2)])
+@pytest.mark.parametrize("M", _DG_SMALL_M + [129, 256])
+@pytest.mark.parametrize("F,K,splits", [(14336, 4096, 2), (14336, 4096, 1), (3584, 8192, 2), (3584, 8192, 1),
+                                        (384, 1024, 2), (28672, 8192, 1)])
 def test_decode_gemm_silu(M, F, K, splits):
     """gate_up + SwiGLU: the 2-way K split with the in-launch combine (ticket parity,
     release/acquire hand-off) and the single-launch form; repeated calls exercise the
@@ -857,17 +901,19 @@ def test_decode_gemm_silu(M, F, K, splits):
     tickets = torch.zeros(2 * (F // 128), device=DEV, dtype=torch.int32)
     err = torch.zeros(1, device=DEV, dtype=torch.int32)
     ws = torch.empty((F // 128) * 256 * 256, device=DEV, dtype=torch.float32)
-    gu = x.float().cpu() @ w.float().cpu().t()
+    gu = (x.float() @ w.float().t()).cpu()
     exp = torch.nn.functional.silu(gu[:, :F]) * gu[:, F:]
     for _ in range(3):
         out = torch.full((M, F), float("nan"), device=DEV, dtype=torch.bfloat16)
+        _dg_census_reset()
         ops.hip().decode_gemm_silu(out, x, w, ws, tickets, err, splits)
+        _dg_census_check(_dg_key(M, 256, "silu2", 2) if splits == 2 else _dg_key(M, 128, "silu", 1))
         _close(out, exp, 0.02, 0.02)
     assert err.item() == 0
 
 
-@pytest.mark.parametrize("M", [129, 256])
-@pytest.mark.parametrize("Hq,Hkv,K", [(32, 8, 4096), (8, 1, 8192)])   # Llama-3-8B; Llama-3-70B TP=8 shard
+@pytest.mark.parametrize("M", _DG_SMALL_M + [129, 256])
+@pytest.mark.parametrize("Hq,Hkv,K", [(32, 8, 4096), (8, 1, 8192), (64, 8, 8192)])   # 8B; 70B TP=8 shard; 70B
 def test_decode_gemm_qkv_rope(M, Hq, Hkv, K):
     """qkv split-K GEMM with RoPE + the paged K/V write fused into its reduction, against
     an fp32 projection rotated in fp32 and the same rows in the caches; rows with slot -1
@@ -886,9 +932,12 @@ def test_decode_gemm_qkv_rope(M, Hq, Hkv, K):
     kc = torch.zeros(NB, Hkv, BS, D, device=DEV, dtype=torch.bfloat16)
     vc = torch.zeros(NB, Hkv, BS // 8, D, 8, device=DEV, dtype=torch.bfloat16)
     slots = torch.randperm(NB * BS, device=DEV)[:M].long()
-    slots[5] = -1
+    slots[M // 2] = -1
     qkv = torch.full((M, N), float("nan"), device=DEV, dtype=torch.bfloat16)
+    _dg_census_reset()
     ops.hip().decode_gemm_qkv_rope(qkv, x, w, _dg_ws(M, N), pos, cos_sin, slots, kc, vc, Hq, Hkv)
+    S = min(4, _dg_split(N // 128, K))
+    _dg_census_check(_dg_key(M, 128, "partial" if S > 1 else "store", S))
     y = (x.float() @ w.float().t()).view(M, Hq + 2 * Hkv, D)
     cs = cos_sin[pos.long()]                                  # [M, D]
     co, si = cs[:, None, : D // 2], cs[:, None, D // 2:]
@@ -907,7 +956,7 @@ def test_decode_gemm_qkv_rope(M, Hq, Hkv, K):
     assert int((kc != 0).any(-1).sum()) == (M - 1) * Hkv
 
 
-@pytest.mark.parametrize("M", [129, 256])
+@pytest.mark.parametrize("M", _DG_SMALL_M + [129, 256])
 @pytest.mark.parametrize("bn", [128, 256])
 def test_decode_gemm_f32_lm_head(M, bn):
     """The decode LM head: f32 logits straight from the 256-row decode GEMM at the
@@ -918,7 +967,9 @@ def test_decode_gemm_f32_lm_head(M, bn):
     w = (torch.randn(N, K, device=DEV) / K ** 0.5).to(torch.bfloat16)
     assert ops.hip().decode_gemm_f32_supported(w, M)
     out = torch.full((M, N), float("nan"), device=DEV)
+    _dg_census_reset()
     ops.hip().decode_gemm_f32(out, x, w, bn)
+    _dg_census_check(_dg_key(M, bn, "partial", 1))
     ref = x.float() @ w.float().t()
     assert (out - ref).abs().max().item() < 2e-3 * ref.abs().max().item() + 1e-3
 
@@ -931,7 +982,7 @@ def _rms_ref(h, g, eps=1e-5):
     return h * torch.rsqrt(h.pow(2).mean(-1, keepdim=True) + eps) * g
 
 
-@pytest.mark.parametrize("M", [129, 200, 256])
+@pytest.mark.parametrize("M", _DG_ALL_M)
 @pytest.mark.parametrize("name,N,K", [("o8b", 4096, 4096), ("down8b", 4096, 14336), ("o70b", 8192, 8192)])
 def test_decode_gemm_res_combine(M, name, N, K):
     torch.manual_seed(M + N + K)
@@ -1001,7 +1052,7 @@ def test_decode_gemm_qkv_combine(M, Hq, Hkv, K):
     kc = torch.zeros(NB, Hkv, BS, D, device=DEV, dtype=torch.bfloat16)
     vc = torch.zeros(NB, Hkv, BS // 8, D, 8, device=DEV, dtype=torch.bfloat16)
     slots = torch.randperm(NB * BS, device=DEV)[:M].long()
-    slots[5] = -1
+    slots[M // 2] = -1
     cnt = torch.zeros(N // 128, device=DEV, dtype=torch.int64)
     err = torch.zeros(1, device=DEV, dtype=torch.int32)
     ws = torch.empty(S * M * N, device=DEV, dtype=torch.float32)

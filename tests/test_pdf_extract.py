@@ -236,3 +236,61 @@ def test_bounded_inflate_roundtrip_and_limit():
     assert bounded_inflate(gzip.compress(data) + gzip.compress(b"tail"), 31) == data + b"tail"
     with pytest.raises(DecompressionBombError):
         bounded_inflate(zlib.compress(data), limit=100)
+
+
+def _page_pdf_objs(text: bytes):
+    return {
+        1: b"<< /Type /Catalog /Pages 2 0 R >>",
+        2: b"<< /Type /Pages /Kids [3 0 R] /Count 1 >>",
+        3: b"<< /Type /Page /Parent 2 0 R /Resources << /Font << /F1 4 0 R >> >> /Contents 5 0 R >>",
+        4: b"<< /Type /Font /Subtype /Type1 /BaseFont /Helvetica /Encoding /WinAnsiEncoding >>",
+        5: _stream("", b"BT /F1 12 Tf 72 720 Td (" + text + b") Tj ET"),
+    }
+
+
+def test_incremental_update_in_object_stream_supersedes_body_object():
+    """An update appended as an object stream (Word / Acrobat 'save' with compressed
+    xrefs) redefines the page object: the LATER definition wins (ADVICE r4:
+    object-stream entries were skipped when the number already had a body definition)."""
+    base = build_pdf(_page_pdf_objs(b"Caf\xe9 old"), root=1, version=b"1.5")
+    # the update: page object 3 again, inside an object stream, pointing at a NEW content stream 7
+    upd_objs = {3: b"<< /Type /Page /Parent 2 0 R /Resources << /Font << /F1 4 0 R >> >> /Contents 7 0 R >>"}
+    head = b"3 0\n"
+    body = upd_objs[3] + b"\n"
+    objstm = _stream("/Type /ObjStm /N 1 /First %d" % len(head), head + body)
+    update = (b"7 0 obj\n" + _stream("", b"BT /F1 12 Tf 72 720 Td (new text) Tj ET") + b"\nendobj\n"
+              b"8 0 obj\n" + objstm + b"\nendobj\n"
+              b"trailer\n<< /Root 1 0 R /Prev 0 >>\nstartxref\n0\n%%EOF\n")
+    text = pdf_text(base + update)
+    assert "new text" in text and "old" not in text
+
+
+def test_incremental_update_body_object_supersedes_older_object_stream():
+    # the original file packs the page in an object stream; the update rewrites it at top level
+    objs = _page_pdf_objs(b"old text")
+    objs[7] = _stream("", b"BT /F1 12 Tf 72 720 Td (new text) Tj ET")
+    base = build_pdf(objs, root=1, objstm=(1, 2, 3, 4))
+    update = (b"3 0 obj\n<< /Type /Page /Parent 2 0 R /Resources << /Font << /F1 4 0 R >> >> /Contents 7 0 R >>"
+              b"\nendobj\ntrailer\n<< /Root 1 0 R >>\nstartxref\n0\n%%EOF\n")
+    text = pdf_text(base + update)
+    assert "new text" in text and "old text" not in text
+
+
+def test_pdf_many_small_streams_share_one_inflate_budget():
+    """Each stream alone is under its own 1 MiB floor, together they pass the document's
+    budget (the guard was per stream only)."""
+    chunk = zlib.compress(b" " * (900 << 10))           # ~1 KB each -> 900 KiB inflated
+    parts = [b"%PDF-1.4\n"]
+    kids = []
+    for i in range(40):
+        n = 10 + i
+        parts.append(b"%d 0 obj\n<< /Length %d /Filter /FlateDecode >>\nstream\n" % (n, len(chunk)) + chunk +
+                     b"\nendstream\nendobj\n")
+        kids.append(n)
+    contents = b"[" + b" ".join(b"%d 0 R" % n for n in kids) + b"]"
+    parts.append(b"1 0 obj << /Type /Catalog /Pages 2 0 R >> endobj\n"
+                 b"2 0 obj << /Type /Pages /Kids [3 0 R] /Count 1 >> endobj\n"
+                 b"3 0 obj << /Type /Page /Parent 2 0 R /Contents " + contents + b" >> endobj\n"
+                 b"trailer << /Root 1 0 R >>\n%%EOF\n")
+    with pytest.raises(DecompressionBombError):
+        extract_text(b"".join(parts))

@@ -106,11 +106,11 @@ def bench_knn(args):
     for nq in str(args.queries).split(","):
         Q = torch.nn.functional.normalize(torch.randn(int(nq), 384, device="cuda"), dim=-1).bfloat16()
         for _ in range(3):
-            ops.knn_topk(X, Q, 20)
+            ops.knn_topk(X, Q, 20, _ablate=args.knn_ablate)
         sync()
         t0 = time.time()
         for _ in range(20):
-            ops.knn_topk(X, Q, 20)
+            ops.knn_topk(X, Q, 20, _ablate=args.knn_ablate)
         sync()
         dt = (time.time() - t0) / 20
         print(json.dumps({"test": "knn", "rows": args.rows, "queries": int(nq), "ms": round(dt * 1000, 3),
@@ -130,6 +130,8 @@ if __name__ == "__main__":
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--rows", type=int, default=1_000_000)
     ap.add_argument("--queries", default="64", help="comma-separated query counts (knn)")
+    ap.add_argument("--knn-ablate", type=int, default=0,
+                    help="kNN main-pass timing ablation 1-3 (diagnosis only: WRONG results)")
     a = ap.parse_args()
     for w in a.what.split(","):
         {"llm": bench_llm, "embed": bench_embed, "knn": bench_knn}[w](a)
