@@ -560,7 +560,13 @@ def build_parser() -> argparse.ArgumentParser:
     cp.add_argument("--api-server", default=None, help="Kubernetes API server (store=kubernetes)")
     cp.add_argument("--code-storage", default=None, help="code storage config JSON (or @file)")
     cp.add_argument("--code-dir", default=None, help="local cache of unpacked archives")
-    cp.add_argument("--auth-secret", default=None, help="HS256 secret for bearer tokens on /api/*")
+    cp.add_argument("--auth-secret", default=None, help="raw HMAC secret for bearer tokens on /api/* "
+                                                         "(shorthand for --security secret-key)")
+    cp.add_argument("--security", default=None,
+                    help="application.security.token properties as JSON (or @file): secret-key, public-key, "
+                         "public-alg, auth-claim, audience-claim, audience, admin-roles, jwks-hosts-allowlist, "
+                         "allow-kubernetes-service-accounts, kubernetes-namespace-prefix")
+    cp.add_argument("--admin-roles", default=None, help="comma-separated principals granted ROLE_ADMIN")
     cp.add_argument("--max-units-per-tenant", type=int, default=0)
     cp.set_defaults(fn=cmd_control_plane)
     return ap
@@ -580,7 +586,10 @@ def cmd_control_plane(args) -> int:
     cs = _json_arg(args.code_storage or os.environ.get("LANGSTREAM_CODE_STORAGE"))
     cp = ControlPlane(store, code_dir=args.code_dir, max_units_per_tenant=args.max_units_per_tenant,
                       code_storage=code_storage_for(cs) if cs else None)
-    srv = WebServiceServer(cp, host=args.host, port=args.port, auth_secret=args.auth_secret).start()
+    sec = dict(_json_arg(args.security or os.environ.get("LANGSTREAM_SECURITY_TOKEN")) or {})
+    if args.admin_roles:
+        sec["admin-roles"] = [r.strip() for r in args.admin_roles.split(",") if r.strip()]
+    srv = WebServiceServer(cp, host=args.host, port=args.port, auth_secret=args.auth_secret, security=sec).start()
     print(f"control plane listening on {srv.url}", flush=True)
     stop = threading.Event()
     signal.signal(signal.SIGTERM, lambda *_: stop.set())

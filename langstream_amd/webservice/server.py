@@ -20,7 +20,14 @@ resource-unit limit Σ size×parallelism, ``ApplicationService.java:95-125``) ->
 start on the compute cluster: ``local``/``none``/``docker`` run in-process
 (``LocalApplicationRunner``, the docker-run path); ``kubernetes`` renders the Agent
 custom resources + StatefulSets (``core.k8s``) into the store (and applies them with
-kubectl when ``apply`` is configured).  Optional bearer-token auth (HS256 JWT).
+kubectl when ``apply`` is configured).
+
+Security (``security.py``, ``SecurityConfiguration.java``): with a token configuration every
+``/api/**`` call needs a bearer JWT (HMAC secret, RSA / EC public key, allowlisted
+``jwks_uri`` claims or the local Kubernetes issuer); ``/api/tenants/**`` needs a principal
+in ``admin-roles``; application / archetype / log / code calls on tenant T need ROLE_ADMIN
+or principal == T.  No token configuration: the API is open (the reference's
+``application.security.enabled=false`` default).
 """
 from __future__ import annotations
 
@@ -289,10 +296,25 @@ class ControlPlane:
 # ---------------------------------------------------------------- HTTP layer
 class WebServiceServer:
     def __init__(self, cp: ControlPlane, host: str = "127.0.0.1", port: int = 8090,
-                 auth_secret: Optional[str] = None):
+                 auth_secret: Optional[str] = None, security: Optional[Dict[str, Any]] = None,
+                 authenticator=None):
+        """``security``: ``application.security.token`` properties (``secret-key``,
+        ``public-key``, ``public-alg``, ``auth-claim``, ``audience-claim``, ``audience``,
+        ``admin-roles``, ``jwks-hosts-allowlist``, ``allow-kubernetes-service-accounts``,
+        ``kubernetes-namespace-prefix``).  ``auth_secret``: shorthand for a raw HMAC secret
+        with ``admin-roles`` from ``security`` (default ``["admin"]``)."""
+        from urllib.parse import quote
+        from .security import TokenAuthenticator, TokenProperties
         self.cp = cp
         self.host, self.port = host, port
-        self.auth_secret = auth_secret
+        sec = dict(security or {})
+        if auth_secret:
+            sec.setdefault("secret-key", "data:," + quote(auth_secret, safe=""))
+            sec.setdefault("admin-roles", ["admin"])
+        self.auth = authenticator
+        if self.auth is None and any(sec.get(k) for k in ("secret-key", "public-key", "jwks-hosts-allowlist",
+                                                          "allow-kubernetes-service-accounts")):
+            self.auth = TokenAuthenticator(TokenProperties.from_dict(sec))
         self._loop = None
         self._thread = None
         self._started = threading.Event()
@@ -300,16 +322,25 @@ class WebServiceServer:
     def make_app(self):
         from aiohttp import web
 
+        from .security import AuthenticationError, Principal, route_policy
+
         @web.middleware
         async def auth_mw(request, handler):
-            if self.auth_secret and request.path.startswith("/api/"):
-                from ..gateway.auth import JwtError, decode_jwt
+            request["principal"] = None
+            policy = route_policy(request.path, request.method)
+            if self.auth is not None and policy != "public":
                 h = request.headers.get("Authorization", "")
+                if not h.startswith("Bearer ") or len(h) <= len("Bearer "):
+                    raise web.HTTPUnauthorized(text="Missing token")
                 try:
-                    decode_jwt(h[len("Bearer "):] if h.startswith("Bearer ") else "",
-                               secret=self.auth_secret.encode())
-                except JwtError as e:
+                    # JWKS / issuer fetches may block: off the event loop
+                    name = await self._off(self.auth.authenticate, h[len("Bearer "):])
+                except AuthenticationError as e:
                     raise web.HTTPUnauthorized(text=str(e))
+                principal = Principal(name, self.auth.is_admin(name))
+                if policy == "admin" and not principal.admin:
+                    raise web.HTTPForbidden(text="ROLE_ADMIN required")
+                request["principal"] = principal
             try:
                 return await handler(request)
             except KeyError as e:
@@ -342,6 +373,12 @@ class WebServiceServer:
         from ..core.config_model import generate_docs
         return web.json_response(generate_docs())
 
+    @staticmethod
+    def _authorize(request) -> None:
+        """``performAuthorization`` of ApplicationResource / ArchetypeResource."""
+        from .security import authorize_tenant
+        authorize_tenant(request.get("principal"), request.match_info["tenant"])
+
     async def _off(self, fn, *a, **kw):
         return await asyncio.get_running_loop().run_in_executor(None, lambda: fn(*a, **kw))
 
@@ -369,6 +406,7 @@ class WebServiceServer:
 
     async def list_apps(self, request):
         from aiohttp import web
+        self._authorize(request)
         return web.json_response([a.summary() for a in self.cp.store.list(request.match_info["tenant"])])
 
     async def _parts(self, request) -> Dict[str, Any]:
@@ -384,6 +422,7 @@ class WebServiceServer:
     async def app(self, request):
         from aiohttp import web
         t, i = request.match_info["tenant"], request.match_info["id"]
+        self._authorize(request)
         q = request.query
         if request.method == "GET":
             return web.json_response(await self._off(self.cp.describe, t, i, q.get("stats") == "true"),
@@ -401,6 +440,7 @@ class WebServiceServer:
     async def app_logs(self, request):
         from aiohttp import web
         t, i = request.match_info["tenant"], request.match_info["id"]
+        self._authorize(request)
         if self.cp.store.get(t, i) is None:
             raise KeyError(f"application {i} not found")
         buf = self.cp.logs(t, i)
@@ -426,6 +466,7 @@ class WebServiceServer:
 
     async def app_code(self, request):
         from aiohttp import web
+        self._authorize(request)
         sa = self.cp.store.get(request.match_info["tenant"], request.match_info["id"])
         if sa is None or not sa.code_archive_id:
             raise KeyError("code not found")
@@ -434,6 +475,7 @@ class WebServiceServer:
 
     async def app_code_info(self, request):
         from aiohttp import web
+        self._authorize(request)
         sa = self.cp.store.get(request.match_info["tenant"], request.match_info["id"])
         if sa is None:
             raise KeyError("application not found")
@@ -444,10 +486,12 @@ class WebServiceServer:
 
     async def archetypes(self, request):
         from aiohttp import web
+        self._authorize(request)
         return web.json_response(self.cp.list_archetypes())
 
     async def archetype(self, request):
         from aiohttp import web
+        self._authorize(request)
         for a in self.cp.list_archetypes():
             if a["id"] == request.match_info["id"]:
                 return web.json_response(a)
@@ -455,6 +499,7 @@ class WebServiceServer:
 
     async def archetype_deploy(self, request):
         from aiohttp import web
+        self._authorize(request)
         params = await request.json() if request.can_read_body else {}
         res = await self._off(self.cp.deploy_archetype, request.match_info["tenant"], request.match_info["id"],
                               request.match_info["app"], params or {})

@@ -1,0 +1,401 @@
+"""Control-plane authentication + authorization parity (VERDICT r4 missing #1).
+
+Reference: ``langstream-webservice/.../SecurityConfiguration.java:67-92`` (``/api/tenants/**``
+is ROLE_ADMIN only), ``TokenAuthFilter.java:84-97`` (principal in ``adminRoles`` ->
+ROLE_ADMIN), ``ApplicationResource.java:94`` / ``ArchetypeResource.java:59``
+(principal == tenant), ``langstream-auth-jwt/.../AuthenticationProviderToken.java``
+(secret / public key / ``jwks_uri`` claim with a host allowlist / local Kubernetes issuer,
+audience, auth claim, service-account namespaces).
+
+Keys are generated here (RSA: Miller-Rabin primes; EC: the module's own curve
+arithmetic with a random nonce), tokens signed by hand, JWKS and the Kubernetes
+``/.well-known/openid-configuration`` served by a local HTTP server."""
+import base64
+import hashlib
+import json
+import random
+import secrets
+import threading
+import time
+from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
+
+import pytest
+import requests
+
+from langstream_amd.cli.client import AdminClient, AdminClientError
+from langstream_amd.topics.memory import reset_memlogs
+from langstream_amd.webservice import security as sec
+from langstream_amd.webservice.server import ControlPlane, WebServiceServer
+
+
+# ---------------------------------------------------------------- key material + signing
+def _b64u(b: bytes) -> str:
+    return base64.urlsafe_b64encode(b).rstrip(b"=").decode()
+
+
+def _is_prime(n: int, rng) -> bool:
+    if n < 2:
+        return False
+    for p in (2, 3, 5, 7, 11, 13, 17, 19, 23, 29, 31, 37):
+        if n % p == 0:
+            return n == p
+    d, r = n - 1, 0
+    while d % 2 == 0:
+        d //= 2
+        r += 1
+    for _ in range(24):
+        a = rng.randrange(2, n - 1)
+        x = pow(a, d, n)
+        if x in (1, n - 1):
+            continue
+        for _ in range(r - 1):
+            x = x * x % n
+            if x == n - 1:
+                break
+        else:
+            return False
+    return True
+
+
+def _prime(bits: int, rng) -> int:
+    while True:
+        c = rng.getrandbits(bits) | (1 << (bits - 1)) | 1
+        if _is_prime(c, rng):
+            return c
+
+
+def rsa_keypair(seed: int, bits: int = 1024):
+    rng = random.Random(seed)
+    e = 65537
+    while True:
+        p, q = _prime(bits // 2, rng), _prime(bits // 2, rng)
+        phi = (p - 1) * (q - 1)
+        if p != q and phi % e:
+            return p * q, e, pow(e, -1, phi)
+
+
+_DIGEST_INFO = {"256": bytes.fromhex("3031300d060960864801650304020105000420"),
+                "384": bytes.fromhex("3041300d060960864801650304020205000430"),
+                "512": bytes.fromhex("3051300d060960864801650304020305000440")}
+
+
+def _der(tag: int, body: bytes) -> bytes:
+    n = len(body)
+    if n < 128:
+        ln = bytes([n])
+    else:
+        nb = n.to_bytes((n.bit_length() + 7) // 8, "big")
+        ln = bytes([0x80 | len(nb)]) + nb
+    return bytes([tag]) + ln + body
+
+
+def _der_int(v: int) -> bytes:
+    b = v.to_bytes(v.bit_length() // 8 + 1, "big")
+    return _der(0x02, b)
+
+
+def rsa_spki(n: int, e: int) -> bytes:
+    algid = _der(0x30, _der(0x06, bytes.fromhex("2a864886f70d010101")) + b"\x05\x00")
+    return _der(0x30, algid + _der(0x03, b"\x00" + _der(0x30, _der_int(n) + _der_int(e))))
+
+
+def ec_spki(x: int, y: int) -> bytes:
+    algid = _der(0x30, _der(0x06, bytes.fromhex("2a8648ce3d0201")) + _der(0x06, bytes.fromhex("2a8648ce3d030107")))
+    return _der(0x30, algid + _der(0x03, b"\x00\x04" + x.to_bytes(32, "big") + y.to_bytes(32, "big")))
+
+
+def sign(header: dict, claims: dict, *, hs: bytes = None, rsa=None, ec=None) -> str:
+    h = _b64u(json.dumps(header).encode())
+    p = _b64u(json.dumps(claims).encode())
+    msg = f"{h}.{p}".encode()
+    alg = header["alg"]
+    if alg.startswith("HS"):
+        import hmac
+        sig = hmac.new(hs, msg, getattr(hashlib, "sha" + alg[2:])).digest()
+    elif alg.startswith("RS"):
+        n, _, d = rsa
+        k = (n.bit_length() + 7) // 8
+        t = _DIGEST_INFO[alg[2:]] + hashlib.new("sha" + alg[2:], msg).digest()
+        em = b"\x00\x01" + b"\xff" * (k - len(t) - 3) + b"\x00" + t
+        sig = pow(int.from_bytes(em, "big"), d, n).to_bytes(k, "big")
+    else:
+        c, priv = sec._P256, ec
+        z = sec._ec_hash_int(c, msg)
+        while True:
+            kk = secrets.randbelow(c.n - 1) + 1
+            r = sec.ec_mul(c, kk, (c.gx, c.gy))[0] % c.n
+            s = pow(kk, -1, c.n) * (z + r * priv) % c.n
+            if r and s:
+                break
+        sig = r.to_bytes(32, "big") + s.to_bytes(32, "big")
+    return f"{h}.{p}.{_b64u(sig)}"
+
+
+RSA_A = rsa_keypair(1)
+RSA_B = rsa_keypair(2)
+EC_PRIV = 0x1D2C3B4A5968778695A4B3C2D1E0F00112233445566778899AABBCCDDEEFF001
+EC_PUB = sec.ec_mul(sec._P256, EC_PRIV, (sec._P256.gx, sec._P256.gy))
+
+
+# ---------------------------------------------------------------- a JWKS / k8s API fake
+class _Fake(BaseHTTPRequestHandler):
+    docs = {}
+    seen_auth = []
+
+    def do_GET(self):  # noqa: N802
+        self.seen_auth.append((self.path, self.headers.get("Authorization")))
+        body = self.docs.get(self.path)
+        if callable(body):
+            body = body(self)
+        if body is None:
+            self.send_response(404)
+            self.end_headers()
+            return
+        data = json.dumps(body).encode()
+        self.send_response(200)
+        self.send_header("Content-Type", "application/json")
+        self.send_header("Content-Length", str(len(data)))
+        self.end_headers()
+        self.wfile.write(data)
+
+    def log_message(self, *a):
+        pass
+
+
+@pytest.fixture()
+def fake_http():
+    srv = ThreadingHTTPServer(("127.0.0.1", 0), _Fake)
+    _Fake.docs = {}
+    _Fake.seen_auth = []
+    t = threading.Thread(target=srv.serve_forever, daemon=True)
+    t.start()
+    yield f"http://127.0.0.1:{srv.server_address[1]}", _Fake
+    srv.shutdown()
+
+
+def _rsa_jwk(n, e, kid, alg="RS256"):
+    return {"kty": "RSA", "alg": alg, "kid": kid, "n": _b64u(n.to_bytes((n.bit_length() + 7) // 8, "big")),
+            "e": _b64u(e.to_bytes(3, "big"))}
+
+
+def _server(tmp_path, security):
+    reset_memlogs()
+    cp = ControlPlane(code_dir=str(tmp_path / "code"))
+    cp.store.put_tenant("t1", {})
+    cp.store.put_tenant("t2", {})
+    return cp, WebServiceServer(cp, port=0, security=security).start()
+
+
+def _get(srv, path, token=None):
+    h = {"Authorization": f"Bearer {token}"} if token else {}
+    return requests.get(srv.url + path, headers=h, timeout=10)
+
+
+# ---------------------------------------------------------------- tests
+SECRET = b"a-256-bit-secret-for-the-control-plane!!"
+HS_CONF = {"secret-key": base64.b64encode(SECRET).decode(), "admin-roles": ["super"]}
+
+
+def test_tenants_are_admin_only_and_apps_are_per_tenant(tmp_path):
+    cp, srv = _server(tmp_path, HS_CONF)
+    try:
+        admin = sign({"alg": "HS256"}, {"sub": "super"}, hs=SECRET)
+        t1 = sign({"alg": "HS256"}, {"sub": "t1"}, hs=SECRET)
+        assert _get(srv, "/api/tenants").status_code == 401                   # no token
+        assert _get(srv, "/api/tenants", "x.y.z").status_code == 401          # garbage
+        assert _get(srv, "/api/tenants", t1).status_code == 403               # not ROLE_ADMIN
+        assert _get(srv, "/api/tenants/t1", t1).status_code == 403
+        r = _get(srv, "/api/tenants", admin)
+        assert r.status_code == 200 and {"t1", "t2"} <= set(r.json())
+        # applications: principal == tenant, or admin
+        assert _get(srv, "/api/applications/t1", t1).status_code == 200
+        assert _get(srv, "/api/applications/t2", t1).status_code == 403
+        assert _get(srv, "/api/applications/t2/someapp", t1).status_code == 403
+        assert _get(srv, "/api/applications/t2/someapp/logs", t1).status_code == 403
+        assert _get(srv, "/api/applications/t2/someapp/code", t1).status_code == 403
+        assert _get(srv, "/api/archetypes/t2", t1).status_code == 403
+        assert _get(srv, "/api/archetypes/t1", t1).status_code == 200
+        assert _get(srv, "/api/applications/t2", admin).status_code == 200
+        r = requests.delete(srv.url + "/api/applications/t2/x", headers={"Authorization": f"Bearer {t1}"}, timeout=10)
+        assert r.status_code == 403
+        # the admin client surfaces the same answers
+        with pytest.raises(AdminClientError) as ei:
+            AdminClient(srv.url, "t1", token=t1).tenants()
+        assert ei.value.status == 403
+        assert AdminClient(srv.url, "t1", token=t1).list() == []
+        # public probes and docs need no token
+        assert _get(srv, "/management/health").status_code == 200
+        assert _get(srv, "/api/docs").status_code == 200
+        # wrong secret / expired / not yet valid
+        assert _get(srv, "/api/applications/t1", sign({"alg": "HS256"}, {"sub": "t1"}, hs=b"x" * 40)).status_code == 401
+        exp = sign({"alg": "HS256"}, {"sub": "t1", "exp": int(time.time()) - 10}, hs=SECRET)
+        assert _get(srv, "/api/applications/t1", exp).status_code == 401
+        nbf = sign({"alg": "HS256"}, {"sub": "t1", "nbf": int(time.time()) + 600}, hs=SECRET)
+        assert _get(srv, "/api/applications/t1", nbf).status_code == 401
+        # a token without the principal claim
+        assert _get(srv, "/api/applications/t1", sign({"alg": "HS256"}, {"x": 1}, hs=SECRET)).status_code == 401
+        # alg confusion: an RS256 token against an HMAC-only configuration
+        assert _get(srv, "/api/applications/t1", sign({"alg": "RS256"}, {"sub": "t1"}, rsa=RSA_A)).status_code == 401
+        assert _get(srv, "/api/applications/t1", _b64u(b'{"alg":"none"}') + "." + _b64u(b'{"sub":"t1"}') + ".")\
+            .status_code == 401
+    finally:
+        srv.stop()
+
+
+def test_open_api_without_token_configuration(tmp_path):
+    cp, srv = _server(tmp_path, {})
+    try:
+        assert _get(srv, "/api/tenants").status_code == 200
+        assert _get(srv, "/api/applications/t2").status_code == 200
+    finally:
+        srv.stop()
+
+
+@pytest.mark.parametrize("alg", ["RS256", "RS384", "RS512"])
+def test_rsa_public_key_tokens(tmp_path, alg):
+    n, e, _ = RSA_A
+    pem = b"-----BEGIN PUBLIC KEY-----\n" + base64.encodebytes(rsa_spki(n, e)) + b"-----END PUBLIC KEY-----\n"
+    keyfile = tmp_path / "pub.pem"
+    keyfile.write_bytes(pem)
+    cp, srv = _server(tmp_path, {"public-key": f"file:{keyfile}", "public-alg": "RS256", "admin-roles": "root"})
+    try:
+        ok = sign({"alg": alg}, {"sub": "t1"}, rsa=RSA_A)
+        assert _get(srv, "/api/applications/t1", ok).status_code == 200
+        assert _get(srv, "/api/applications/t1", sign({"alg": alg}, {"sub": "t1"}, rsa=RSA_B)).status_code == 401
+        assert _get(srv, "/api/tenants", sign({"alg": alg}, {"sub": "root"}, rsa=RSA_A)).status_code == 200
+        # an HS256 token "signed" with the public key bytes must not pass (key confusion)
+        assert _get(srv, "/api/applications/t1", sign({"alg": "HS256"}, {"sub": "t1"}, hs=pem)).status_code == 401
+    finally:
+        srv.stop()
+
+
+def test_ec_public_key_es256(tmp_path):
+    der = ec_spki(*EC_PUB)
+    conf = {"public-key": "data:;base64," + base64.b64encode(der).decode(), "public-alg": "ES256"}
+    cp, srv = _server(tmp_path, conf)
+    try:
+        assert _get(srv, "/api/applications/t1", sign({"alg": "ES256"}, {"sub": "t1"}, ec=EC_PRIV)).status_code == 200
+        bad = sign({"alg": "ES256"}, {"sub": "t1"}, ec=EC_PRIV + 1)
+        assert _get(srv, "/api/applications/t1", bad).status_code == 401
+    finally:
+        srv.stop()
+    with pytest.raises(ValueError):   # an EC key with an RSA public-alg
+        sec.TokenAuthenticator(sec.TokenProperties.from_dict({"public-key": base64.b64encode(der).decode()}))
+
+
+def test_jwks_uri_claim_needs_an_allowlisted_host(tmp_path, fake_http):
+    base, fake = fake_http
+    n, e, _ = RSA_B
+    fake.docs["/jwks.json"] = {"keys": [_rsa_jwk(*RSA_A[:2], "a"), _rsa_jwk(n, e, "b"),
+                                        _rsa_jwk(n, e, "b384", alg="RS384")]}
+    conf = {"jwks-hosts-allowlist": r"127\.0\.0\.1", "secret-key": base64.b64encode(SECRET).decode()}
+    cp, srv = _server(tmp_path, conf)
+    try:
+        tok = sign({"alg": "RS256", "kid": "b"}, {"sub": "t1", "jwks_uri": base + "/jwks.json"}, rsa=RSA_B)
+        assert _get(srv, "/api/applications/t1", tok).status_code == 200
+        # kid a is RSA_A's key: a token signed with RSA_B and kid a fails
+        tok = sign({"alg": "RS256", "kid": "a"}, {"sub": "t1", "jwks_uri": base + "/jwks.json"}, rsa=RSA_B)
+        assert _get(srv, "/api/applications/t1", tok).status_code == 401
+        # keys are filtered by alg == public-alg (RS256): the RS384 entry is never used
+        tok = sign({"alg": "RS384", "kid": "b384"}, {"sub": "t1", "jwks_uri": base + "/jwks.json"}, rsa=RSA_B)
+        assert _get(srv, "/api/applications/t1", tok).status_code == 401
+        # a host outside the allowlist (localhost != 127.0.0.1) is never fetched
+        port = base.rsplit(":", 1)[1]
+        tok = sign({"alg": "RS256", "kid": "b"}, {"sub": "t1", "jwks_uri": f"http://localhost:{port}/jwks.json"},
+                   rsa=RSA_B)
+        assert _get(srv, "/api/applications/t1", tok).status_code == 401
+        evil = sign({"alg": "RS256", "kid": "b"}, {"sub": "t1", "jwks_uri": f"http://127.0.0.1.evil:{port}/j"},
+                    rsa=RSA_B)
+        assert _get(srv, "/api/applications/t1", evil).status_code == 401
+    finally:
+        srv.stop()
+    # no allowlist: a jwks_uri claim is untrusted
+    auth = sec.TokenAuthenticator(sec.TokenProperties.from_dict({"secret-key": base64.b64encode(SECRET).decode(),
+                                                                 "kubernetes-base-url": None}))
+    with pytest.raises(sec.AuthenticationError, match="Untrusted hostname"):
+        auth.authenticate(sign({"alg": "RS256", "kid": "b"}, {"sub": "t1", "jwks_uri": base + "/jwks.json"},
+                               rsa=RSA_B))
+
+
+def test_audience_and_auth_claim(tmp_path):
+    conf = {"secret-key": base64.b64encode(SECRET).decode(), "audience-claim": "aud", "audience": "langstream",
+            "auth-claim": "roles", "admin-roles": ["ops"]}
+    cp, srv = _server(tmp_path, conf)
+    try:
+        def tok(claims):
+            return sign({"alg": "HS256"}, claims, hs=SECRET)
+        assert _get(srv, "/api/applications/t1", tok({"roles": "t1", "aud": "langstream"})).status_code == 200
+        assert _get(srv, "/api/applications/t1", tok({"roles": ["t1", "x"], "aud": ["a", "langstream"]})) \
+            .status_code == 200
+        assert _get(srv, "/api/applications/t1", tok({"roles": "t1", "aud": "other"})).status_code == 401
+        assert _get(srv, "/api/applications/t1", tok({"roles": "t1", "aud": ["other"]})).status_code == 401
+        assert _get(srv, "/api/applications/t1", tok({"roles": "t1"})).status_code == 401          # no audience
+        assert _get(srv, "/api/applications/t1", tok({"sub": "t1", "aud": "langstream"})).status_code == 401
+        assert _get(srv, "/api/tenants", tok({"roles": ["ops"], "aud": "langstream"})).status_code == 200
+    finally:
+        srv.stop()
+    with pytest.raises(ValueError, match="Audience"):
+        sec.TokenAuthenticator(sec.TokenProperties.from_dict({"secret-key": "c2VjcmV0", "audience-claim": "aud"}))
+
+
+def test_kubernetes_service_account_tokens(tmp_path, fake_http):
+    base, fake = fake_http
+    issuer = base + "/k8s"
+    tokfile = tmp_path / "sa-token"
+    tokfile.write_text("pod-sa-token")
+    fake.docs["/.well-known/openid-configuration"] = {"issuer": issuer}
+    fake.docs["/k8s/.well-known/openid-configuration"] = {"issuer": issuer, "jwks_uri": base + "/k8s/keys"}
+    # the cluster's keys need the pod's token (first unauthenticated GET is refused)
+    fake.docs["/k8s/keys"] = lambda h: ({"keys": [_rsa_jwk(*RSA_A[:2], "sa")]}
+                                        if h.headers.get("Authorization") == "Bearer pod-sa-token" else None)
+    conf = {"allow-kubernetes-service-accounts": True, "kubernetes-namespace-prefix": "langstream-",
+            "kubernetes-base-url": base, "kubernetes-token-path": str(tokfile),
+            "secret-key": base64.b64encode(SECRET).decode()}
+    cp, srv = _server(tmp_path, conf)
+    try:
+        sa = sign({"alg": "RS256", "kid": "sa"},
+                  {"iss": issuer, "sub": "system:serviceaccount:langstream-t1:default",
+                   "kubernetes.io": {"namespace": "langstream-t1"}}, rsa=RSA_A)
+        assert _get(srv, "/api/applications/t1", sa).status_code == 200
+        assert _get(srv, "/api/applications/t2", sa).status_code == 403
+        # the same claims signed by another key
+        forged = sign({"alg": "RS256", "kid": "sa"},
+                      {"iss": issuer, "kubernetes.io": {"namespace": "langstream-t2"}}, rsa=RSA_B)
+        assert _get(srv, "/api/applications/t2", forged).status_code == 401
+        # a foreign issuer falls back to the secret key: an RS256 token then fails
+        other = sign({"alg": "RS256", "kid": "sa"},
+                     {"iss": "https://elsewhere", "kubernetes.io": {"namespace": "langstream-t1"}}, rsa=RSA_A)
+        assert _get(srv, "/api/applications/t1", other).status_code == 401
+        assert ("/k8s/keys", "Bearer pod-sa-token") in fake.seen_auth
+    finally:
+        srv.stop()
+
+
+def test_read_key_bytes_forms(tmp_path):
+    f = tmp_path / "k"
+    f.write_bytes(b"raw-key")
+    assert sec.read_key_bytes(str(f)) == b"raw-key"
+    assert sec.read_key_bytes(f"file:{f}") == b"raw-key"
+    assert sec.read_key_bytes("data:;base64," + base64.b64encode(b"abc").decode()) == b"abc"
+    assert sec.read_key_bytes("data:,a%20b") == b"a b"
+    assert sec.read_key_bytes(base64.b64encode(b"xyz").decode()) == b"xyz"
+    with pytest.raises(ValueError):
+        sec.read_key_bytes("/no/such/file")
+
+
+def test_route_policy():
+    assert sec.route_policy("/api/tenants", "GET") == "admin"
+    assert sec.route_policy("/api/tenants/x", "DELETE") == "admin"
+    assert sec.route_policy("/api/tenantsx", "GET") == "authenticated"
+    assert sec.route_policy("/api/applications/t", "GET") == "authenticated"
+    assert sec.route_policy("/management/health", "GET") == "public"
+    assert sec.route_policy("/management/other", "GET") == "authenticated"
+    assert sec.route_policy("/api/tenants", "OPTIONS") == "public"
+
+
+def test_ecdsa_rejects_off_curve_and_out_of_range():
+    c = sec._P256
+    msg = b"m"
+    assert not sec.ecdsa_verify(c, (EC_PUB[0], EC_PUB[1] + 1), msg, b"\x01" * 64)
+    assert not sec.ecdsa_verify(c, EC_PUB, msg, b"\x00" * 64)
+    assert not sec.ecdsa_verify(c, EC_PUB, msg, c.n.to_bytes(32, "big") * 2)
