@@ -24,31 +24,26 @@ class AssetManager:
 
 
 class JdbcTableManager(AssetManager):
+    """``jdbc-table`` (``JdbcAssetsManagerProvider.java``): existence from the database's
+    table catalogue (name as given, upper- and lower-case), ``create-statements`` on
+    deploy, ``delete-statements`` on delete -- only when the table exists, and nothing
+    else (no implicit DROP)."""
+
     def _ds(self):
-        from .vector.datasources import SqliteDataSource
-        return SqliteDataSource.shared(self.cfg["datasource"])
+        from .vector.datasources import jdbc_datasource
+        return jdbc_datasource(self.cfg["datasource"])
 
     def asset_exists(self) -> bool:
-        ds = self._ds()
-        with ds.lock:
-            r = ds.conn.execute("SELECT name FROM sqlite_master WHERE type='table' AND lower(name)=lower(?)",
-                                [self.cfg["table-name"]]).fetchone()
-        return r is not None
+        return self._ds().table_exists(self.cfg["table-name"])
 
     def deploy_asset(self) -> None:
-        ds = self._ds()
-        with ds.lock:
-            for stmt in self.cfg.get("create-statements") or []:
-                ds.conn.execute(stmt)
-            ds.conn.commit()
+        self._ds().script(list(self.cfg.get("create-statements") or []))
 
     def delete_asset_if_exists(self) -> None:
-        ds = self._ds()
-        stmts = self.cfg.get("delete-statements") or [f"DROP TABLE IF EXISTS {self.cfg['table-name']}"]
-        with ds.lock:
-            for stmt in stmts:
-                ds.conn.execute(stmt)
-            ds.conn.commit()
+        if not self.asset_exists():
+            log.info("table %s does not exist, skipping the delete statements", self.cfg["table-name"])
+            return
+        self._ds().script(list(self.cfg.get("delete-statements") or []))
 
 
 class VectorCollectionManager(AssetManager):

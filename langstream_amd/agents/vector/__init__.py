@@ -21,7 +21,7 @@ from ...runtime.registry import register_agent
 from ..genai.el import eval_expression
 from ..genai.mutable import MutableRecord
 from ..genai.steps import QueryStep
-from .datasources import LocalVectorDataSource, SqliteDataSource, datasource_for
+from .datasources import LocalVectorDataSource, SqliteDataSource, datasource_for, jdbc_datasource
 
 
 @register_agent("query-vector-db")
@@ -146,7 +146,7 @@ class _LocalWriter:
 
 class _JdbcWriter:
     def __init__(self, cfg: Dict[str, Any]):
-        self.ds: SqliteDataSource = SqliteDataSource.shared(cfg["datasource"])
+        self.ds = jdbc_datasource(cfg["datasource"])
         self.table = cfg.get("table-name") or cfg.get("table")
         if not self.table:
             raise ValueError("vector-db-sink (jdbc): table-name is required")
@@ -159,6 +159,9 @@ class _JdbcWriter:
     def upsert(self, mr: MutableRecord) -> None:
         ctx = mr.el_context()
         vals = {f["name"]: eval_expression(f["expression"], ctx) for f in self.fields}
+        if not isinstance(self.ds, SqliteDataSource):
+            self._upsert_generic(mr, vals)
+            return
         enc = lambda v: json.dumps(v) if isinstance(v, (list, dict)) else v  # noqa: E731
         ds = self.ds
         with ds.lock:
@@ -180,6 +183,25 @@ class _JdbcWriter:
             ds.conn.commit()
             rowid = ds.conn.execute(f"SELECT rowid FROM {self.table} WHERE {where}", pkv).fetchone()[0]
         self._mirror_upsert(rowid, vals)
+
+    def _upsert_generic(self, mr: MutableRecord, vals: Dict[str, Any]) -> None:
+        """JdbcWriter.upsert on a server database: prepared UPDATE, INSERT when it matched
+        no row, DELETE for a null value (one statement at a time, autocommit)."""
+        ds = self.ds
+        where = " AND ".join(f"{c}=?" for c in self.pk)
+        pkv = [vals[c] for c in self.pk]
+        if mr.value is None:
+            ds.execute_statement(f"DELETE FROM {self.table} WHERE {where}", [], pkv)
+            return
+        n = 0
+        if self.cols:
+            sets = "=?, ".join(self.cols) + " = ?"
+            n = ds.execute_statement(f"UPDATE {self.table} SET {sets} WHERE {where}", [],
+                                     [vals[c] for c in self.cols] + pkv)["count"]
+        if n == 0:
+            allc = self.pk + self.cols
+            ds.execute_statement(f"INSERT INTO {self.table} ({', '.join(allc)}) VALUES ({','.join('?' * len(allc))})",
+                                 [], [vals[c] for c in allc])
 
     def _mirror_upsert(self, rowid, vals) -> None:
         for (table, col), name in list(self.ds.vector_cols.items()):

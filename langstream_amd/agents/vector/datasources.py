@@ -7,12 +7,20 @@ MI355X-native services:
 * ``local`` / ``local-gpu``: HBM vector collections (engine/vector_store.py) with a JSON
   query language -- ``{"collection-name": "docs", "vector": ?, "top-k": 5,
   "filter": {"field": ?}, "include-vector": false}`` (``?`` = positional params).
-* ``jdbc`` / ``sqlite``: SQL on SQLite (stdlib) with a ``cosine_similarity`` UDF; the
-  RAG pattern ``... ORDER BY cosine_similarity(<vector col>, ?) DESC LIMIT k`` is
-  executed as a GPU kNN over an HBM mirror of the vector column (the reference
-  example ``EX/docker-chatbot/chatbot.yaml:36`` runs exactly this query on HerdDB).
-* cassandra / astra / astra-vector-db / milvus / opensearch / pinecone / solr: their
-  client libraries are not part of this image -> a datasource that fails loudly.
+* ``jdbc`` by URL (``JdbcDataSourceProvider.java:147-160`` picks the driver the same way):
+  - ``jdbc:postgresql://...``: a real server through the in-tree v3 wire client
+    (``pgwire.py``: SCRAM-SHA-256 / MD5 auth, prepared statements, typed results);
+  - ``jdbc:sqlite:<path>`` (or ``service: sqlite``): SQLite (stdlib) with a
+    ``cosine_similarity`` UDF; the RAG pattern ``... ORDER BY cosine_similarity(<vector
+    col>, ?) DESC LIMIT k`` runs as a GPU kNN over an HBM mirror of the vector column
+    (the reference example ``EX/docker-chatbot/chatbot.yaml:36`` runs that query on HerdDB);
+  - ``jdbc:herddb:local`` (HerdDB's embedded, in-process mode) -> an in-process SQLite
+    database shared by the process's agents;
+  - any other URL (``jdbc:herddb:server:...``, ``jdbc:mysql:...``) fails at init: no
+    driver for it ships in this build, and a silent stand-in would not share data
+    between pods.
+* cassandra / astra / astra-vector-db / milvus / opensearch / pinecone / solr: the REST /
+  CQL clients of ``remote.py`` / ``cql.py``.
 """
 from __future__ import annotations
 
@@ -204,10 +212,11 @@ class SqliteDataSource(DataSource):
     def __init__(self, cfg: Dict[str, Any]):
         url = str(cfg.get("url") or cfg.get("path") or "memory")
         m = re.match(r"^jdbc:sqlite:(.+)$", url)
-        self.path = m.group(1) if m else None
+        self.path = m.group(1) if m else (url if cfg.get("path") else None)
         self.name = url
-        if self.path is None:
-            # any other JDBC url (e.g. herddb) -> a process-wide in-memory database per url
+        if self.path is None or self.path == ":memory:":
+            # an in-process database shared by this process's agents (jdbc:herddb:local,
+            # jdbc:sqlite::memory:, service sqlite without a path)
             self.conn = sqlite3.connect(f"file:{re.sub(r'[^A-Za-z0-9]', '_', url)}?mode=memory&cache=shared",
                                         uri=True, check_same_thread=False)
         else:
@@ -264,8 +273,8 @@ class SqliteDataSource(DataSource):
             cur = self.conn.execute(query, [self._sql_param(p) for p in params])
             self.conn.commit()
             res = {"count": cur.rowcount}
-            if generated_keys:
-                res["generated-keys"] = {generated_keys[0]: cur.lastrowid}
+            if generated_keys:   # the key name JdbcDataSourceProvider.executeStatement returns
+                res["generatedKeys"] = {generated_keys[0]: cur.lastrowid}
             self._invalidate_mirrors_for(query)
             return res
 
@@ -290,6 +299,20 @@ class SqliteDataSource(DataSource):
         if ids:
             store.upsert(ids, vecs)
         self.vector_cols[key] = name
+
+    def script(self, statements: Sequence[str]) -> None:
+        with self.lock:
+            for stmt in statements:
+                self.conn.executescript(stmt)
+            self.conn.commit()
+        for stmt in statements:
+            self._invalidate_mirrors_for(stmt)
+
+    def table_exists(self, table: str) -> bool:
+        with self.lock:
+            r = self.conn.execute("SELECT name FROM sqlite_master WHERE type='table' AND lower(name)=lower(?)",
+                                  [table]).fetchone()
+        return r is not None
 
     def _invalidate_mirrors_for(self, query: str) -> None:
         ql = query.lower()
@@ -324,6 +347,39 @@ class UnavailableDataSource(DataSource):
     execute_statement = _fail
 
 
+_pg_lock = threading.Lock()
+_pg: Dict[tuple, Any] = {}
+
+
+def jdbc_datasource(cfg: Dict[str, Any]):
+    """The JDBC datasource for ``cfg['url']`` (see the module docstring); unsupported URLs
+    raise at init."""
+    url = str(cfg.get("url") or "")
+    svc = cfg.get("service", "jdbc")
+    if svc == "sqlite" or url.startswith("jdbc:sqlite:") or url.startswith("jdbc:herddb:local") or \
+            (not url and cfg.get("path")):
+        return SqliteDataSource.shared(cfg)
+    if url.startswith("jdbc:postgresql:"):
+        from .pgwire import PostgresDataSource
+        key = (url, str(cfg.get("user")), str(cfg.get("password")))
+        with _pg_lock:
+            ds = _pg.get(key)
+            if ds is None:
+                ds = _pg[key] = PostgresDataSource(cfg)
+            return ds
+    raise ValueError(f"JDBC URL {url or '(none)'!r} is not supported by this build: it speaks "
+                     f"jdbc:postgresql:// (wire protocol), jdbc:sqlite:<path> and jdbc:herddb:local "
+                     f"(in-process); set one of those")
+
+
+def reset_jdbc_datasources() -> None:
+    """Close the shared PostgreSQL connections (tests)."""
+    with _pg_lock:
+        for ds in _pg.values():
+            ds.close()
+        _pg.clear()
+
+
 def datasource_for(cfg: Optional[Dict[str, Any]]) -> DataSource:
     if cfg is None:
         raise ValueError("datasource is required")
@@ -331,7 +387,7 @@ def datasource_for(cfg: Optional[Dict[str, Any]]) -> DataSource:
     if svc in ("local", "local-gpu"):
         return LocalVectorDataSource(cfg)
     if svc in ("jdbc", "sqlite"):
-        return SqliteDataSource.shared(cfg)
+        return jdbc_datasource(cfg)
     from .remote import DATASOURCES
     if svc in DATASOURCES:
         return DATASOURCES[svc](cfg)

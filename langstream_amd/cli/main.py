@@ -353,6 +353,27 @@ def cmd_pravega_standalone(args) -> int:
     return pravega_main(["--host", args.host, "--port", str(args.port)])
 
 
+def cmd_pg_standalone(args) -> int:
+    """The PostgreSQL v3 protocol stand-in over SQLite (agents/vector/pg_standalone.py)."""
+    import signal
+    from ..agents.vector.pg_standalone import PgStandalone
+    users = {}
+    for u in args.user or ["postgres:password"]:
+        name, _, pw = u.partition(":")
+        users[name] = pw
+    srv = PgStandalone(args.host, args.port, users=users, auth=args.auth, db_path=args.db).start()
+    print(f"pg-standalone listening on {srv.host}:{srv.port} ({srv.url})", flush=True)
+    stop = threading.Event()
+    signal.signal(signal.SIGTERM, lambda *_: stop.set())
+    try:
+        while not stop.wait(1.0):
+            pass
+    except KeyboardInterrupt:
+        pass
+    srv.stop()
+    return 0
+
+
 def cmd_operator(args) -> int:
     from ..operator import main as operator_main
     argv = ["--resync", str(args.resync)] + (["--in-process"] if args.in_process else [])
@@ -520,6 +541,15 @@ def build_parser() -> argparse.ArgumentParser:
     pv.add_argument("--host", default="127.0.0.1")
     pv.add_argument("--port", type=int, default=9090)
     pv.set_defaults(fn=cmd_pravega_standalone)
+
+    pg = sub.add_parser("pg-standalone",
+                        help="run the in-tree PostgreSQL wire-protocol stand-in (SQL on SQLite) for jdbc:postgresql://")
+    pg.add_argument("--host", default="127.0.0.1")
+    pg.add_argument("--port", type=int, default=5432)
+    pg.add_argument("--user", action="append", help="user:password (repeatable; default postgres:password)")
+    pg.add_argument("--auth", choices=("scram-sha-256", "md5", "password", "trust"), default="scram-sha-256")
+    pg.add_argument("--db", default=None, help="SQLite file (default: in memory)")
+    pg.set_defaults(fn=cmd_pg_standalone)
 
     opr = sub.add_parser("operator", help="run the Kubernetes operator (Application / Agent CRs)")
     opr.add_argument("--api-server", default=None)

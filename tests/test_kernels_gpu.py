@@ -836,7 +836,7 @@ def _dg_bm(M, bn, epi):
 
 
 def _dg_key(M, bn, epi, s):
-    return f"bn{bn}_{epi}_bm{_dg_bm(M, bn, epi)}_s{s}"
+    return f"bn{bn}_{epi}_bm{_dg_bm(M, bn, epi)}_s{min(s, 16)}"   # the census caps splits at 16
 
 
 def _dg_census_reset():

@@ -1,0 +1,254 @@
+"""JDBC against a real database protocol (VERDICT r4 missing #2).
+
+``jdbc:postgresql://`` goes through the in-tree v3 wire client (``pgwire.py``) -- the
+reference opens ``DriverManager.getConnection(url, props)`` with the PostgreSQL driver its
+example ships (``JdbcDataSourceProvider.java:147-160``,
+``examples/applications/query-postgresql-chat-history``).  The server here is the in-tree
+protocol stand-in (``pg_standalone.py``: the v3 protocol over SQLite); live-PostgreSQL
+parity stays unpinned.  Unsupported JDBC URLs must fail at init instead of becoming an
+in-memory SQLite."""
+import json
+import os
+import threading
+import time
+from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
+
+import pytest
+
+from langstream_amd.agents.vector import pgwire
+from langstream_amd.agents.vector.datasources import jdbc_datasource, reset_jdbc_datasources
+from langstream_amd.agents.vector.pg_standalone import PgStandalone
+
+REF_APP = "/root/reference/examples/applications/query-postgresql-chat-history"
+
+
+@pytest.fixture()
+def pg():
+    srv = PgStandalone(users={"postgres": "password", "alice": "s3cr3t"}).start()
+    yield srv
+    reset_jdbc_datasources()
+    srv.stop()
+
+
+@pytest.mark.parametrize("auth", ["scram-sha-256", "md5", "password", "trust"])
+def test_authentication_methods(auth):
+    srv = PgStandalone(users={"alice": "s3cr3t"}, auth=auth).start()
+    try:
+        c = pgwire.PgConnection.from_jdbc(f"jdbc:postgresql://127.0.0.1:{srv.port}/db",
+                                          {"user": "alice", "password": "s3cr3t"})
+        rows, n, tag = c.execute("SELECT 1 AS one, 'x' AS s")
+        assert rows == [{"one": 1, "s": "x"}] and tag == "SELECT 1"
+        c.close()
+        if auth != "trust":
+            with pytest.raises(pgwire.PgError) as ei:
+                pgwire.PgConnection.from_jdbc(f"jdbc:postgresql://127.0.0.1:{srv.port}/db",
+                                              {"user": "alice", "password": "wrong"})
+            assert ei.value.sqlstate == "28P01"
+    finally:
+        srv.stop()
+
+
+def test_scram_rejects_a_server_that_does_not_know_the_password(pg):
+    # the stand-in holds "password" for postgres; the client's proof of "nope" fails
+    with pytest.raises(pgwire.PgError):
+        pgwire.PgConnection.from_jdbc(pg.url, {"user": "postgres", "password": "nope"})
+
+
+def test_jdbc_placeholders_and_url():
+    assert pgwire.jdbc_to_pg_sql("SELECT * FROM t WHERE a=? AND b = ?") == ("SELECT * FROM t WHERE a=$1 AND b = $2", 2)
+    assert pgwire.jdbc_to_pg_sql("SELECT '?' , \"col?\" , ? -- x?\n, ?")[1] == 2
+    assert pgwire.jdbc_to_pg_sql("SELECT $$a?b$$, ?, ?? ")[0] == "SELECT $$a?b$$, $1, ? "
+    assert pgwire.jdbc_to_pg_sql("/* ? */ SELECT ?") == ("/* ? */ SELECT $1", 1)
+    c = pgwire.parse_jdbc_url("jdbc:postgresql://host.docker.internal:5432/", {"user": "postgres", "password": "p"})
+    assert (c["host"], c["port"], c["database"], c["user"]) == ("host.docker.internal", 5432, "postgres", "postgres")
+    c = pgwire.parse_jdbc_url("jdbc:postgresql://db:6543/app?user=u&sslmode=require", {"user": "x"})
+    assert (c["host"], c["port"], c["database"], c["user"], c["sslmode"]) == ("db", 6543, "app", "u", "require")
+    c = pgwire.parse_jdbc_url("jdbc:postgresql://[::1]:7000/d")
+    assert (c["host"], c["port"]) == ("::1", 7000)
+
+
+def test_codecs():
+    assert pgwire.decode_value("{1,2,NULL}", 1007) == [1, 2, None]
+    assert pgwire.decode_value('{"a b","c\\"d"}', 1009) == ["a b", 'c"d']
+    assert pgwire.decode_value("{{1.5,2},{3,4}}", 1022) == [[1.5, 2.0], [3.0, 4.0]]
+    assert pgwire.decode_value("[0.1,0.2]", 16385) == [0.1, 0.2]        # pgvector
+    assert pgwire.decode_value("[not a list]", 25) == "[not a list]"
+    assert pgwire.decode_value('{"k": [1]}', 3802) == {"k": [1]}
+    assert pgwire.decode_value("12.50", 1700) == 12.5 and pgwire.decode_value("7", 1700) == 7
+    assert pgwire.decode_value("\\x00ff", 17) == b"\x00\xff"
+    assert pgwire.encode_param([1, 2.5], 1022) == b"{1,2.5}"
+    assert pgwire.encode_param(["a", None], 1009) == b'{"a",NULL}'
+    assert pgwire.encode_param([0.1, 0.2], 16385) == b"[0.1, 0.2]"
+    assert pgwire.encode_param({"a": 1}, 3802) == b'{"a": 1}'
+    assert pgwire.encode_param(None, 25) is None and pgwire.encode_param(True, 16) == b"t"
+
+
+def test_query_and_execute_through_the_datasource(pg):
+    ds = jdbc_datasource({"service": "jdbc", "url": pg.url, "user": "postgres", "password": "password"})
+    ds.script(["CREATE TABLE docs (id INTEGER PRIMARY KEY, name TEXT, score REAL, tags TEXT)"])
+    assert ds.table_exists("docs") and ds.table_exists("DOCS") and not ds.table_exists("nope")
+    for i in range(5):
+        r = ds.execute_statement("INSERT INTO docs(id, name, score, tags) VALUES (?, ?, ?, ?)", [],
+                                 [i, f"doc-{i}", i / 2, None])
+        assert r == {"count": 1}
+    rows = ds.fetch_data("SELECT id, name, score FROM docs WHERE score >= ? ORDER BY id", [1.0])
+    assert rows == [{"id": 2, "name": "doc-2", "score": 1.0}, {"id": 3, "name": "doc-3", "score": 1.5},
+                    {"id": 4, "name": "doc-4", "score": 2.0}]
+    assert ds.execute_statement("UPDATE docs SET name = ? WHERE id > ?", [], ["x", 2]) == {"count": 2}
+    assert ds.execute_statement("DELETE FROM docs WHERE id = ?", [], [0]) == {"count": 1}
+    # generated keys like PgJDBC: RETURNING the requested columns
+    r = ds.execute_statement("INSERT INTO docs(id, name) VALUES (?, ?)", ["id"], [42, "k"])
+    assert r == {"count": 1, "generatedKeys": {"id": 42}}
+    # a server error is raised and the connection recovers (skip-to-Sync)
+    with pytest.raises(pgwire.PgError):
+        ds.fetch_data("SELECT nope FROM missing_table WHERE x = ?", [1])
+    assert ds.fetch_data("SELECT count(*) AS n FROM docs", []) == [{"n": 5}]
+    # NULL parameters and values
+    assert ds.fetch_data("SELECT tags FROM docs WHERE id = ?", [1]) == [{"tags": None}]
+    # prepared statements are cached per query text
+    conn = ds.conn()
+    n = len(conn._stmts)
+    ds.fetch_data("SELECT count(*) AS n FROM docs", [])
+    assert len(conn._stmts) == n
+
+
+def test_unsupported_jdbc_urls_fail_at_init():
+    for url in ("jdbc:herddb:server:herddb:7000", "jdbc:mysql://db/app", ""):
+        with pytest.raises(ValueError, match="not supported"):
+            jdbc_datasource({"service": "jdbc", "url": url})
+    # HerdDB's embedded mode is an in-process database: served by SQLite
+    ds = jdbc_datasource({"service": "jdbc", "url": "jdbc:herddb:local"})
+    ds.execute_statement("CREATE TABLE IF NOT EXISTS t (a INT)", [], [])
+    assert ds.fetch_data("SELECT count(*) AS n FROM t", []) == [{"n": 0}]
+
+
+def test_query_agent_start_fails_on_unreachable_or_unsupported_jdbc():
+    from langstream_amd.agents.genai.agent import GenAIToolKitAgent
+    with pytest.raises(OSError):
+        jdbc_datasource({"service": "jdbc", "url": "jdbc:postgresql://127.0.0.1:1/db", "user": "u",
+                         "password": "p"})
+    a = GenAIToolKitAgent()
+    a.init({"steps": [{"type": "query", "query": "SELECT 1", "fields": [], "output-field": "value.x"}],
+            "datasource": {"service": "jdbc", "url": "jdbc:herddb:server:localhost:7000"}})
+    with pytest.raises(ValueError, match="not supported"):
+        a.start()
+
+
+def test_vector_db_sink_upsert_and_delete_on_postgres(pg):
+    from langstream_amd.agents.vector import VectorDBSinkAgent
+    from langstream_amd.api.record import SimpleRecord
+    ds_cfg = {"service": "jdbc", "url": pg.url, "user": "postgres", "password": "password"}
+    jdbc_datasource(ds_cfg).script(["CREATE TABLE vecs (id TEXT PRIMARY KEY, body TEXT, v JSONB)"])
+    sink = VectorDBSinkAgent()
+    sink.init({"datasource": ds_cfg, "table-name": "vecs",
+               "fields": [{"name": "id", "expression": "key", "primary-key": True},
+                          {"name": "body", "expression": "value.text"},
+                          {"name": "v", "expression": "value.embeddings"}]})
+    for k, t in (("a", "one"), ("b", "two"), ("a", "uno")):
+        sink.write(SimpleRecord.of(key=k, value=json.dumps({"text": t, "embeddings": [0.5, 1.0]}))).result(10)
+    rows = jdbc_datasource(ds_cfg).fetch_data("SELECT id, body, v FROM vecs ORDER BY id", [])
+    assert rows == [{"id": "a", "body": "uno", "v": [0.5, 1.0]}, {"id": "b", "body": "two", "v": [0.5, 1.0]}]
+    sink.write(SimpleRecord.of(key="a", value=None)).result(10)
+    assert [r["id"] for r in jdbc_datasource(ds_cfg).fetch_data("SELECT id FROM vecs", [])] == ["b"]
+
+
+# ---------------------------------------------------------------- the reference example, end to end
+class _FakeOpenAI(BaseHTTPRequestHandler):
+    """Streams 'ANSWER(<n history rows>): <question>' as OpenAI chat SSE."""
+    prompts = []
+
+    def do_POST(self):  # noqa: N802
+        body = json.loads(self.rfile.read(int(self.headers["Content-Length"])))
+        msgs = body["messages"]
+        self.prompts.append(msgs)
+        system = msgs[0]["content"]
+        n_hist = system.count("Question:")
+        answer = f"ANSWER({n_hist}): {msgs[-1]['content']}"
+        self.send_response(200)
+        self.send_header("Content-Type", "text/event-stream")
+        self.end_headers()
+        for i in range(0, len(answer), 4):
+            ev = {"choices": [{"delta": {"content": answer[i:i + 4]}, "finish_reason": None}]}
+            self.wfile.write(b"data: " + json.dumps(ev).encode() + b"\n\n")
+        self.wfile.write(b'data: {"choices": [{"delta": {}, "finish_reason": "stop"}]}\n\n')
+        self.wfile.write(b"data: [DONE]\n\n")
+
+    def log_message(self, *a):
+        pass
+
+
+@pytest.mark.skipif(not os.path.isdir(REF_APP), reason="reference example not present")
+def test_reference_query_postgresql_chat_history_example(pg):
+    """The reference's own example application, files unchanged except the datasource host
+    (host.docker.internal:5432 -> the stand-in's port): jdbc-table asset creation, the
+    history lookup (``SELECT ... LIMIT 20`` by session), ai-chat-completions with the
+    history in the system prompt, the ``INSERT ... NOW()`` write, and the
+    ``clean-history`` pipeline's ``DELETE ... WHERE TIMESTAMP <= ?`` timer job."""
+    from langstream_amd.runtime.local import LocalApplicationRunner
+    from langstream_amd.topics.memory import reset_memlogs
+    oa = ThreadingHTTPServer(("127.0.0.1", 0), _FakeOpenAI)
+    _FakeOpenAI.prompts = []
+    threading.Thread(target=oa.serve_forever, daemon=True).start()
+    files = {}
+    for f in os.listdir(REF_APP):
+        if f.endswith(".yaml"):
+            with open(os.path.join(REF_APP, f)) as fh:
+                files[f] = fh.read()
+    assert "jdbc:postgresql://host.docker.internal:5432/" in files["configuration.yaml"]
+    files["configuration.yaml"] = files["configuration.yaml"].replace(
+        "host.docker.internal:5432", f"127.0.0.1:{pg.port}")
+    secrets = f"""
+secrets:
+  - id: open-ai
+    data:
+      url: http://127.0.0.1:{oa.server_address[1]}
+      access-key: test
+      provider: openai
+      chat-completions-model: gpt-test
+"""
+    reset_memlogs()
+    app = LocalApplicationRunner.from_yaml(files, secrets=secrets).start(wait=20)
+    try:
+        rd = app.reader("output-topic")
+        for i, q in enumerate(["first question", "second question"]):
+            app.produce("input-topic", q, headers={"client_session_id": "s1"})
+            # the streamed chunks on output-topic, up to the one marked stream-last-message
+            chunks, last = [], False
+            deadline = time.time() + 30
+            while not last and time.time() < deadline:
+                for r in rd.read().records:
+                    hdr = {h.key: h.value for h in (r.headers() or [])}
+                    chunks.append(r.value())
+                    last = last or str(hdr.get("stream-last-message")).lower() == "true"
+            assert last and "".join(map(str, chunks)) == f"ANSWER({i}): {q}"
+            # the history row is written after the answer: wait for it
+            deadline = time.time() + 20
+            while time.time() < deadline:
+                n = jdbc_datasource({"service": "jdbc", "url": pg.url, "user": "postgres", "password": "password"}) \
+                    .fetch_data("SELECT count(*) AS n FROM chat_history", [])[0]["n"]
+                if n == i + 1:
+                    break
+                time.sleep(0.2)
+            assert n == i + 1
+        ds = jdbc_datasource({"service": "jdbc", "url": pg.url, "user": "postgres", "password": "password"})
+        rows = ds.fetch_data("SELECT session_id, question, answer, timestamp FROM chat_history ORDER BY timestamp", [])
+        assert [r["question"] for r in rows] == ["first question", "second question"]
+        assert rows[0]["answer"] == "ANSWER(0): first question"
+        # the second prompt carried the first exchange: the history came back from PostgreSQL
+        assert rows[1]["answer"] == "ANSWER(1): second question"
+        assert "Question: first question" in _FakeOpenAI.prompts[1][0]["content"]
+        assert all(r["session_id"] == "s1" for r in rows)
+        # the clean-history job deletes rows older than one hour: none here
+        assert ds.fetch_data("SELECT count(*) AS n FROM chat_history", [])[0]["n"] == 2
+        ds.execute_statement("UPDATE chat_history SET timestamp = ? WHERE question = ?", [],
+                             ["2000-01-01T00:00:00+00:00", "first question"])
+        deadline = time.time() + 30        # timer-source period: 10 s
+        while time.time() < deadline:
+            if ds.fetch_data("SELECT count(*) AS n FROM chat_history", [])[0]["n"] == 1:
+                break
+            time.sleep(0.5)
+        assert [r["question"] for r in ds.fetch_data("SELECT question FROM chat_history", [])] == ["second question"]
+    finally:
+        app.stop()
+        oa.shutdown()
+        reset_memlogs()
