@@ -63,9 +63,7 @@ class Topic:
         ``consumer.*`` options (prefix stripped)."""
         from ..topics.kafka.serde import deserializer_for_schema
         sch = self._schemas()
-        cfg: Dict[str, Any] = {"topic": self.name,
-                               "key.deserializer": deserializer_for_schema(sch.get("keySchema")),
-                               "value.deserializer": deserializer_for_schema(sch.get("valueSchema")), **sch}
+        cfg: Dict[str, Any] = {"topic": self.name, **_serde_keys(deserializer_for_schema, sch, "deserializer"), **sch}
         for k, v in (self.options or {}).items():
             if k.startswith("consumer."):
                 cfg[k[len("consumer."):]] = v
@@ -76,13 +74,25 @@ class Topic:
         ``producer.*`` options."""
         from ..topics.kafka.serde import serializer_for_schema
         sch = self._schemas()
-        cfg: Dict[str, Any] = {"topic": self.name,
-                               "key.serializer": serializer_for_schema(sch.get("keySchema")),
-                               "value.serializer": serializer_for_schema(sch.get("valueSchema")), **sch}
+        cfg: Dict[str, Any] = {"topic": self.name, **_serde_keys(serializer_for_schema, sch, "serializer"), **sch}
         for k, v in (self.options or {}).items():
             if k.startswith("producer."):
                 cfg[k[len("producer."):]] = v
         return cfg
+
+
+def _serde_keys(pick, sch: Dict[str, Any], kind: str) -> Dict[str, Any]:
+    """Kafka key / value (de)serializer classes for the topic's schemas.  A schema type the
+    Kafka mapping has no class for (``int32``, ``json``: Pulsar schema types) leaves the
+    key out: the Kafka adapter then raises 'Unsupported schema type' when it builds the
+    consumer / producer, other streaming types use the schema themselves."""
+    out: Dict[str, Any] = {}
+    for which, k in (("key", "keySchema"), ("value", "valueSchema")):
+        try:
+            out[f"{which}.{kind}"] = pick(sch.get(k))
+        except ValueError:
+            pass
+    return out
 
 
 @dataclass

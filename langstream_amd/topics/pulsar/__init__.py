@@ -11,8 +11,12 @@ PulsarTopicConnectionsRuntimeProvider.java``):
 * consumer: subscription ``langstream-agent-<agentId>`` (``subscriptionName`` overrides),
   **Failover** subscription type (one active consumer per partition: replica data
   parallelism), initial position Earliest, ``commit`` = per-message acknowledge;
-* producer: key / value / header serialisation like the Kafka adapter (str, bytes,
-  JSON for dict/list, str() for scalars) into payload + properties + key;
+* schemas (``schema.py``): deploy registers a topic's ``valueSchema`` (KeyValue SEPARATED
+  with a ``keySchema``) through the admin API; producers encode with the topic's schema
+  (configured, registered, or inferred from the first record's types and then
+  registered, like the Java client); consumers and readers decode with the topic's
+  registered schema (``AUTO_CONSUME``), KeyValue messages into key + value;
+* producer: headers as message properties (text);
 * reader (gateways): latest / earliest / absolute; the offset token is a JSON map
   ``{partition-topic: messageId}`` so a reader resumes each partition after the last
   message it returned (``PulsarTopicReader`` keeps the same map).
@@ -39,6 +43,7 @@ from ...api.topics import (TopicAdmin, TopicConnectionsRuntime, TopicConnections
                            TopicOffsetPosition, TopicProducer, TopicReader, TopicReadResult)
 from ...utils.wsclient import WebSocket, WebSocketClosed
 from ..kafka import serialize
+from .schema import TopicSchema, infer
 
 log = logging.getLogger(__name__)
 
@@ -46,14 +51,18 @@ log = logging.getLogger(__name__)
 class PulsarRecord(Record):
     __slots__ = ("message_id", "partition_topic")
 
-    def __init__(self, topic: str, d: Dict[str, Any]):
+    def __init__(self, topic: str, d: Dict[str, Any], schema: Optional[TopicSchema] = None):
         payload = base64.b64decode(d.get("payload") or "")
-        try:
-            value: Any = payload.decode()
-        except UnicodeDecodeError:
-            value = payload
+        key: Any = d.get("key")
+        if schema is not None:
+            key, value = schema.decode_message(key, payload)
+        else:
+            try:
+                value = payload.decode()
+            except UnicodeDecodeError:
+                value = payload
         props = d.get("properties") or {}
-        super().__init__(d.get("key"), value, topic, _publish_ms(d.get("publishTime")),
+        super().__init__(key, value, topic, _publish_ms(d.get("publishTime")),
                          [Header(k, v) for k, v in props.items()])
         self.message_id = d["messageId"]
         self.partition_topic = topic
@@ -117,6 +126,30 @@ class PulsarConfig:
         r = self.admin("GET", self.rest_path(full) + "/partitions")
         return int(r.json().get("partitions", 0)) if r.ok else 0
 
+    # ---------------------------------------------------------------- schemas
+    @staticmethod
+    def base_topic(full: str) -> str:
+        """The partitioned topic a ``-partition-N`` topic belongs to (schemas live there)."""
+        import re as _re
+        return _re.sub(r"-partition-\d+$", "", full)
+
+    def schema_path(self, full: str) -> str:
+        _, rest = self.base_topic(full).split("://", 1)
+        return "schemas/" + "/".join(quote(p, safe="") for p in rest.split("/")) + "/schema"
+
+    def get_schema(self, full: str) -> Optional[TopicSchema]:
+        r = self.admin("GET", self.schema_path(full))
+        if r.status_code == 404:
+            return None
+        if not r.ok:
+            raise RuntimeError(f"reading the schema of {full}: {r.status_code} {r.text}")
+        return TopicSchema.from_rest(r.json())
+
+    def post_schema(self, full: str, ts: TopicSchema) -> None:
+        r = self.admin("POST", self.schema_path(full), json=ts.rest_payload())
+        if r.status_code not in (200, 204):
+            raise RuntimeError(f"registering the schema of {full}: {r.status_code} {r.text}")
+
     def topic_exists(self, full: str) -> bool:
         if self.partitions(full) > 0:
             return True
@@ -134,8 +167,10 @@ class PulsarConsumer(TopicConsumer):
         self.max_records, self.poll_s = max_records, poll_s
         self.ws: Optional[WebSocket] = None
         self._out = 0
+        self.schema = _SchemaCache(cfg, self.topic)
 
     def start(self) -> None:
+        self.schema.get()
         self.ws = self.cfg.ws("consumer", self.topic, "/" + quote(self.subscription, safe=""),
                               {"subscriptionType": self.sub_type, "subscriptionInitialPosition": "Earliest",
                                "receiverQueueSize": 1000})
@@ -156,7 +191,7 @@ class PulsarConsumer(TopicConsumer):
                 if d.get("result", "ok") != "ok":
                     raise RuntimeError(f"pulsar consumer error: {d}")
                 continue
-            out.append(PulsarRecord(self.topic, d))
+            out.append(PulsarRecord(self.topic, d, self.schema.get()))
             timeout = 0.001
         self._out += len(out)
         return out
@@ -173,9 +208,30 @@ class PulsarConsumer(TopicConsumer):
         return {"topic": self.topic, "subscription": self.subscription, "type": self.sub_type}
 
 
-class PulsarProducer(TopicProducer):
+class _SchemaCache:
+    """A topic's registered schema for readers (AUTO_CONSUME): fetched at start and, while
+    the topic has none, at most once a second (a producer may register one later)."""
+
     def __init__(self, cfg: PulsarConfig, topic: str):
+        self.cfg, self.topic = cfg, topic
+        self.schema: Optional[TopicSchema] = None
+        self._last = 0.0
+
+    def get(self) -> Optional[TopicSchema]:
+        if self.schema is None and time.monotonic() - self._last > 1.0:
+            self._last = time.monotonic()
+            try:
+                self.schema = self.cfg.get_schema(self.topic)
+            except (requests.RequestException, RuntimeError) as e:
+                log.warning("cannot read the schema of %s: %s", self.topic, e)
+        return self.schema
+
+
+class PulsarProducer(TopicProducer):
+    def __init__(self, cfg: PulsarConfig, topic: str, schema: Optional[TopicSchema] = None):
         self.cfg, self.topic = cfg, cfg.full(topic)
+        self.schema = schema          # configured (topic keySchema / valueSchema)
+        self._schema_lock = threading.Lock()
         self.ws: Optional[WebSocket] = None
         self._pending: Dict[str, Future] = {}
         self._lock = threading.Lock()
@@ -187,6 +243,10 @@ class PulsarProducer(TopicProducer):
     def start(self) -> None:
         if self._started:
             return
+        if self.schema is None:
+            self.schema = self.cfg.get_schema(self.topic)
+        elif self.cfg.get_schema(self.topic) is None:
+            self.cfg.post_schema(self.topic, self.schema)      # the Java client registers on create
         self.ws = self.cfg.ws("producer", self.topic)
         self._reader = threading.Thread(target=self._receipts, name=f"pulsar-producer-{self.topic}", daemon=True)
         self._reader.start()
@@ -225,13 +285,27 @@ class PulsarProducer(TopicProducer):
             self.start()
         f: Future = Future()
         ctx = str(next(self._ctx))
-        msg: Dict[str, Any] = {"payload": base64.b64encode(serialize(record.value()) or b"").decode(),
+        try:
+            if self.schema is None:
+                with self._schema_lock:
+                    if self.schema is None:
+                        # no configured / registered schema: infer one from this record's
+                        # types and register it (PulsarTopicProducer.write, BASE_SCHEMAS)
+                        inferred = infer(record.key(), record.value())
+                        existing = self.cfg.get_schema(self.topic)
+                        if existing is None:
+                            self.cfg.post_schema(self.topic, inferred)
+                        self.schema = existing or inferred
+            key, payload = self.schema.encode_message(record.key(), record.value())
+        except Exception as e:  # noqa: BLE001 - a value the schema cannot carry
+            f.set_exception(e)
+            return f
+        msg: Dict[str, Any] = {"payload": base64.b64encode(payload).decode(),
                                "properties": {h.key: (serialize(h.value) or b"").decode(errors="replace")
-                                              for h in record.headers()},
+                                              for h in record.headers() if h.value is not None},
                                "context": ctx}
-        if record.key() is not None:
-            k = serialize(record.key())
-            msg["key"] = k.decode(errors="replace") if isinstance(k, bytes) else str(k)
+        if key is not None:
+            msg["key"] = key
         with self._lock:
             self._pending[ctx] = f
         try:
@@ -256,8 +330,10 @@ class PulsarReader(TopicReader):
         self.cfg, self.topic, self.position, self.poll_s = cfg, cfg.full(topic), position, poll_s
         self.readers: Dict[str, WebSocket] = {}
         self.ids: Dict[str, str] = {}
+        self.schema = _SchemaCache(cfg, self.topic)
 
     def start(self) -> None:
+        self.schema.get()
         n = self.cfg.partitions(self.topic)
         names = [f"{self.topic}-partition-{i}" for i in range(n)] if n > 0 else [self.topic]
         if self.position.position == "absolute" and self.position.offset:
@@ -282,7 +358,7 @@ class PulsarReader(TopicReader):
                 d = json.loads(m[1])
                 if "messageId" not in d:
                     continue
-                out.append(PulsarRecord(name, d))
+                out.append(PulsarRecord(name, d, self.schema.get()))
                 self.ids[name] = d["messageId"]
                 w.send_text(json.dumps({"messageId": d["messageId"]}))
                 timeout = 0.001
@@ -310,6 +386,19 @@ class PulsarTopicConnectionsRuntime(TopicConnectionsRuntime):
                                    headers={"Content-Type": "application/json"})
             if r.status_code not in (200, 204, 409):
                 raise RuntimeError(f"creating pulsar topic {full}: {r.status_code} {r.text}")
+        for t in plan.topics.values():
+            # schema deploy (PulsarTopicConnectionsRuntimeProvider.java:256-289): only when
+            # the topic has no schema yet
+            ts = TopicSchema.from_definitions(_sd(t.definition.key_schema if t.definition else None),
+                                              _sd(t.definition.value_schema if t.definition else None))
+            if ts is None:
+                continue
+            full = self.cfg.full(t.name)
+            if self.cfg.get_schema(full) is None:
+                log.info("deploying schema %s for pulsar topic %s", ts.rest_payload()["type"], full)
+                self.cfg.post_schema(full, ts)
+            else:
+                log.info("pulsar topic %s already has a schema, skipping", full)
 
     def delete(self, plan) -> None:
         for t in plan.topics.values():
@@ -329,7 +418,9 @@ class PulsarTopicConnectionsRuntime(TopicConnectionsRuntime):
                               float(configuration.get("poll.timeout.ms", 1000)) / 1000.0)
 
     def create_producer(self, agent_id, streaming_cluster, configuration) -> TopicProducer:
-        return PulsarProducer(self.cfg, configuration["topic"])
+        return PulsarProducer(self.cfg, configuration["topic"],
+                              TopicSchema.from_definitions(configuration.get("keySchema"),
+                                                           configuration.get("valueSchema")))
 
     def create_reader(self, streaming_cluster, configuration, initial_position) -> TopicReader:
         return PulsarReader(self.cfg, configuration["topic"], initial_position,
@@ -337,6 +428,10 @@ class PulsarTopicConnectionsRuntime(TopicConnectionsRuntime):
 
     def create_topic_admin(self, agent_id, streaming_cluster, configuration) -> TopicAdmin:
         return TopicAdmin()
+
+
+def _sd(s) -> Optional[Dict[str, Any]]:
+    return None if s is None else {"type": s.type, "schema": s.schema, "name": s.name}
 
 
 TopicConnectionsRuntimeRegistry.register("pulsar", PulsarTopicConnectionsRuntime)

@@ -17,6 +17,12 @@ Endpoints (same paths and JSON bodies as a Pulsar broker with the WebSocket serv
   explicit id, like ``Reader.startMessageId``).
 * admin ``/admin/v2/persistent/{t}/{ns}/{topic}`` PUT/DELETE, ``.../partitions`` PUT (body =
   count) / GET / DELETE, ``/admin/v2/persistent/{t}/{ns}`` GET (topic list).
+* schema registry ``/admin/v2/schemas/{t}/{ns}/{topic}/schema`` GET (``{"version", "type",
+  "timestamp", "data", "properties"}``, 404 without one) / POST (``{"type", "schema",
+  "properties"}``) / DELETE.  With ``schema_enforced`` (the namespace policy
+  ``schemaValidationEnforced``) a produced message must decode under the topic's schema
+  (a KeyValue message: its key too), else the send fails -- what a broker does for a
+  producer whose schema does not match.
 Topics are auto-created on first produce/subscribe (``allowAutoTopicCreation``).
 Message ids are opaque base64 tokens (``partition:entry``).
 """
@@ -87,14 +93,17 @@ def _parse_mid(s: str):
 
 
 class PulsarStandalone:
-    def __init__(self, host: str = "127.0.0.1", port: int = 0):
+    def __init__(self, host: str = "127.0.0.1", port: int = 0, schema_enforced: bool = False):
         self.host, self.port = host, port
+        self.schema_enforced = schema_enforced
+        self.schemas: Dict[str, List[dict]] = {}     # base topic -> versions (GetSchemaResponse)
         self.topics: Dict[str, _Topic] = {}
         self.subs: Dict[tuple, _Sub] = {}
         self._loop: Optional[asyncio.AbstractEventLoop] = None
         self._runner: Optional[web.AppRunner] = None
         self._thread: Optional[threading.Thread] = None
         self._ready = threading.Event()
+        self._sockets: Set[web.WebSocketResponse] = set()
 
     # ------------------------------------------------------------------ lifecycle
     @property
@@ -124,9 +133,11 @@ class PulsarStandalone:
             self._thread.join(10)
 
     async def _shutdown(self):
-        for s in self.subs.values():
-            for c in list(s.consumers):
-                await c.ws.close()
+        for ws in list(self._sockets):        # every producer / consumer / reader socket
+            try:
+                await asyncio.wait_for(ws.close(), 2)
+            except Exception:  # noqa: BLE001
+                pass
         if self._runner is not None:
             await self._runner.cleanup()
 
@@ -142,6 +153,10 @@ class PulsarStandalone:
         app.router.add_put(base + "/{topic}/partitions", self._create_partitioned)
         app.router.add_get(base + "/{topic}/partitions", self._get_partitions)
         app.router.add_delete(base + "/{topic}/partitions", self._delete_topic)
+        sch = "/admin/v2/schemas/{tenant}/{ns}/{topic}/schema"
+        app.router.add_get(sch, self._get_schema)
+        app.router.add_post(sch, self._post_schema)
+        app.router.add_delete(sch, self._delete_schema)
         ws = "/ws/v2/{kind}/persistent/{tenant}/{ns}/{topic}"
         app.router.add_get(ws, self._ws)
         app.router.add_get(ws + "/{sub}", self._ws)
@@ -228,6 +243,60 @@ class PulsarStandalone:
         return web.json_response(sorted(t.name for t in self.topics.values()
                                         if t.name.startswith(pre) and t.partitions > 0))
 
+    # ------------------------------------------------------------------ schemas
+    async def _get_schema(self, req):
+        v = self.schemas.get(self._full(req))
+        if not v:
+            return web.json_response({"reason": "Schema not found"}, status=404)
+        return web.json_response(v[-1])
+
+    async def _post_schema(self, req):
+        from .schema import SchemaError, TopicSchema
+        body = await req.json()
+        name = self._full(req)
+        doc = {"version": len(self.schemas.get(name, [])), "type": str(body.get("type", "BYTES")).upper(),
+               "timestamp": int(time.time() * 1000), "data": body.get("schema") or "",
+               "properties": body.get("properties") or {}}
+        try:
+            ts = TopicSchema.from_rest(doc)
+        except (SchemaError, ValueError) as e:
+            return web.json_response({"reason": f"Invalid schema definition: {e}"}, status=422)
+        cur = self.schemas.get(name)
+        if cur and TopicSchema.from_rest(cur[-1]) == ts:
+            return web.json_response({"version": cur[-1]["version"]})
+        if cur and self.schema_enforced:
+            return web.json_response({"reason": "Schema not compatible with the existing one"}, status=409)
+        self.schemas.setdefault(name, []).append(doc)
+        return web.json_response({"version": doc["version"]})
+
+    async def _delete_schema(self, req):
+        if self.schemas.pop(self._full(req), None) is None:
+            return web.json_response({"reason": "Schema not found"}, status=404)
+        return web.json_response({"version": 0})
+
+    def _validate(self, topic: _Topic, key: Optional[str], payload: bytes) -> Optional[str]:
+        """None when the message decodes under the topic's schema (enforcement on)."""
+        if not self.schema_enforced:
+            return None
+        v = self.schemas.get(topic.name)
+        if not v:
+            return None
+        from .schema import TopicSchema
+        try:
+            ts = TopicSchema.from_rest(v[-1])
+            if payload or ts.value.type not in ("STRING", "BYTES", "NONE"):
+                ts.value.decode(payload)
+            if ts.is_kv and key is not None and ts.key.type != "STRING":
+                ts.key.decode(base64.b64decode(key))
+            if ts.value.type == "AVRO" and payload:
+                # the whole payload must be one Avro datum
+                from ...api import avro
+                if avro.encode(ts.value._avro, ts.value.decode(payload)) != payload:
+                    return "payload is not exactly one Avro datum of the topic's schema"
+        except Exception as e:  # noqa: BLE001
+            return f"message does not match the topic's {v[-1]['type']} schema: {e}"
+        return None
+
     # ------------------------------------------------------------------ websocket
     async def _ws(self, req):
         kind = req.match_info["kind"]
@@ -235,6 +304,7 @@ class PulsarStandalone:
             return web.Response(status=404)
         ws = web.WebSocketResponse(heartbeat=30)
         await ws.prepare(req)
+        self._sockets.add(ws)
         topic, pids = self._get_or_create(self._full(req))
         try:
             if kind == "producer":
@@ -244,6 +314,7 @@ class PulsarStandalone:
             else:
                 await self._reader(ws, topic, pids, req.query)
         finally:
+            self._sockets.discard(ws)
             await ws.close()
         return ws
 
@@ -258,6 +329,10 @@ class PulsarStandalone:
                 await ws.send_json({"result": "send-error:1", "errorMsg": str(e)})
                 continue
             key = d.get("key")
+            bad = self._validate(topic, key, payload)
+            if bad is not None:
+                await ws.send_json({"result": "send-error:2", "errorMsg": bad, "context": d.get("context")})
+                continue
             n = len(pids)
             if key is not None:
                 p = pids[zlib.crc32(str(key).encode()) % n]
@@ -397,8 +472,10 @@ def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description="Pulsar-compatible single-node broker (WebSocket API + admin)")
     ap.add_argument("--host", default="127.0.0.1")
     ap.add_argument("--port", type=int, default=8080)
+    ap.add_argument("--schema-enforced", action="store_true",
+                    help="reject messages that do not decode under the topic's schema")
     a = ap.parse_args(argv)
-    b = PulsarStandalone(a.host, a.port).start()
+    b = PulsarStandalone(a.host, a.port, schema_enforced=a.schema_enforced).start()
     print(f"pulsar standalone on {b.web_url}", flush=True)
     try:
         while True:

