@@ -1,0 +1,239 @@
+"""``langstream apps ui <app>`` -- a local web UI for one application
+(``langstream-cli/.../applications/UIAppCmd.java``).
+
+A small aiohttp server (default port 8092) that serves:
+* ``/`` -- the single-page UI (``app_ui_static/index.html``): the application's gateways
+  (produce / consume / chat / service forms talking WebSocket), its pipeline diagram
+  (Mermaid text) and a live log panel;
+* ``/api/application`` -- the app model the page renders: ``baseUrl`` (this server, as
+  ``ws://``), ``remoteBaseUrl`` (the profile's API gateway), ``tenant``,
+  ``applicationId``, ``gateways``, ``applicationDefinition`` (the control plane's
+  description, JSON text) and ``mermaidDefinition``;
+* ``/api/logs`` -- the application's logs from the control plane as a text stream;
+* ``/v1/**`` -- a proxy to the API gateway (WebSocket upgrades pumped both ways, plain
+  HTTP forwarded), so the page talks to one origin like the reference's Undertow proxy.
+"""
+from __future__ import annotations
+
+import asyncio
+import json
+import logging
+import os
+import threading
+from typing import Any, Dict, Optional
+
+log = logging.getLogger(__name__)
+
+_STATIC = os.path.join(os.path.dirname(__file__), "app_ui_static")
+
+
+def mermaid_from_plan(plan: Dict[str, Any]) -> str:
+    """Mermaid flowchart of an execution-plan dict (the description's ``application``)."""
+    lines = ["flowchart LR"]
+    ids: Dict[str, str] = {}
+
+    def nid(s: str) -> str:
+        return ids.setdefault(s, f"n{len(ids)}")
+
+    for t in plan.get("topics") or []:
+        lines.append(f'  {nid("topic:" + t["name"])}(["{t["name"]}"])')
+    for node in (plan.get("agents") or {}).values():
+        cfg = node.get("configuration") or {}
+        steps = [p.get("agentId") for p in cfg.get("processors", [])] if node.get("agent-type") == "composite-agent" \
+            else [node.get("id")]
+        lines.append(f'  {nid("agent:" + node["id"])}["{"<br/>".join(map(str, steps))}<br/>'
+                     f'<i>{node.get("agent-type")}</i>"]')
+        if node.get("input"):
+            lines.append(f'  {nid("topic:" + node["input"])} --> {nid("agent:" + node["id"])}')
+        if node.get("output"):
+            lines.append(f'  {nid("agent:" + node["id"])} --> {nid("topic:" + node["output"])}')
+    for g in plan.get("gateways") or []:
+        gid = nid("gateway:" + str(g.get("id")))
+        lines.append(f'  {gid}{{{{"{g.get("id")}<br/><i>{g.get("type")} gateway</i>"}}}}')
+        chat = g.get("chat-options") or {}
+        if g.get("type") == "chat":
+            if chat.get("questions-topic"):
+                lines.append(f'  {gid} --> {nid("topic:" + chat["questions-topic"])}')
+            if chat.get("answers-topic"):
+                lines.append(f'  {nid("topic:" + chat["answers-topic"])} --> {gid}')
+        elif g.get("topic"):
+            if g.get("type") == "consume":
+                lines.append(f'  {nid("topic:" + g["topic"])} --> {gid}')
+            else:
+                lines.append(f'  {gid} --> {nid("topic:" + g["topic"])}')
+    return "\n".join(lines)
+
+
+def app_model(client, app_id: str, api_gateway_url: str, tenant: str) -> Dict[str, Any]:
+    desc = client.get(app_id)
+    plan = desc.get("application") or {}
+    return {"remoteBaseUrl": api_gateway_url, "tenant": tenant, "applicationId": app_id,
+            "gateways": plan.get("gateways") or [],
+            "applicationDefinition": json.dumps(desc, default=str),
+            "mermaidDefinition": mermaid_from_plan(plan)}
+
+
+def make_app(client, app_id: str, api_gateway_url: str, tenant: str):
+    import aiohttp
+    from aiohttp import web
+
+    gw_ws = api_gateway_url.rstrip("/")
+    gw_http = gw_ws.replace("wss://", "https://", 1).replace("ws://", "http://", 1)
+
+    async def index(request):
+        return web.FileResponse(os.path.join(_STATIC, "index.html"))
+
+    async def application(request):
+        model = await asyncio.get_running_loop().run_in_executor(
+            None, app_model, client, app_id, api_gateway_url, tenant)
+        model["baseUrl"] = f"ws://{request.host}"
+        return web.json_response(model)
+
+    async def logs(request):
+        resp = web.StreamResponse(headers={"Content-Type": "text/plain; charset=utf-8"})
+        await resp.prepare(request)
+        loop = asyncio.get_running_loop()
+        q: "asyncio.Queue[Optional[str]]" = asyncio.Queue()
+        follow = request.query.get("follow", "true") != "false"
+
+        def pump():
+            try:
+                for rec in client.logs(app_id, follow=follow):
+                    line = f"[{rec.get('replica')}] {rec.get('level')} {rec.get('message')}"
+                    loop.call_soon_threadsafe(q.put_nowait, line)
+            except Exception as e:  # noqa: BLE001 - the stream ended or failed
+                loop.call_soon_threadsafe(q.put_nowait, f"-- logs unavailable: {e}")
+            loop.call_soon_threadsafe(q.put_nowait, None)
+
+        threading.Thread(target=pump, daemon=True, name="app-ui-logs").start()
+        try:
+            while True:
+                line = await q.get()
+                if line is None:
+                    break
+                await resp.write((line + "\n").encode())
+        except (ConnectionResetError, asyncio.CancelledError):
+            pass
+        return resp
+
+    async def proxy(request):
+        tail = request.match_info["tail"]
+        qs = ("?" + request.query_string) if request.query_string else ""
+        if request.headers.get("Upgrade", "").lower() == "websocket":
+            down = web.WebSocketResponse()
+            await down.prepare(request)
+            async with aiohttp.ClientSession() as s:
+                try:
+                    up = await s.ws_connect(f"{gw_ws}/v1/{tail}{qs}")
+                except aiohttp.ClientError as e:
+                    await down.close(code=1011, message=str(e).encode()[:120])
+                    return down
+
+                async def up_to_down():
+                    async for m in up:
+                        if m.type == aiohttp.WSMsgType.TEXT:
+                            await down.send_str(m.data)
+                        elif m.type == aiohttp.WSMsgType.BINARY:
+                            await down.send_bytes(m.data)
+                        else:
+                            break
+                    await down.close()
+
+                t = asyncio.ensure_future(up_to_down())
+                async for m in down:
+                    if m.type == aiohttp.WSMsgType.TEXT:
+                        await up.send_str(m.data)
+                    elif m.type == aiohttp.WSMsgType.BINARY:
+                        await up.send_bytes(m.data)
+                    else:
+                        break
+                await up.close()
+                t.cancel()
+            return down
+        async with aiohttp.ClientSession() as s:
+            body = await request.read()
+            async with s.request(request.method, f"{gw_http}/v1/{tail}{qs}", data=body or None,
+                                 headers={k: v for k, v in request.headers.items()
+                                          if k.lower() in ("content-type", "authorization")}) as r:
+                return web.Response(status=r.status, body=await r.read(),
+                                    content_type=r.content_type or "application/octet-stream")
+
+    app = web.Application()
+    app.router.add_get("/", index)
+    app.router.add_get("/index.html", index)
+    app.router.add_get("/api/application", application)
+    app.router.add_get("/api/logs", logs)
+    app.router.add_route("*", "/v1/{tail:.*}", proxy)
+    return app
+
+
+class AppUIServer:
+    def __init__(self, client, app_id: str, api_gateway_url: str, tenant: str, host: str = "127.0.0.1",
+                 port: int = 8092):
+        self.args = (client, app_id, api_gateway_url, tenant)
+        self.host, self.port = host, port
+        self._loop: Optional[asyncio.AbstractEventLoop] = None
+        self._ready = threading.Event()
+        self._thread: Optional[threading.Thread] = None
+
+    def start(self) -> "AppUIServer":
+        from aiohttp import web
+
+        def run():
+            self._loop = asyncio.new_event_loop()
+            asyncio.set_event_loop(self._loop)
+            self._runner = web.AppRunner(make_app(*self.args))
+            self._loop.run_until_complete(self._runner.setup())
+            site = web.TCPSite(self._runner, self.host, self.port)
+            self._loop.run_until_complete(site.start())
+            self.port = site._server.sockets[0].getsockname()[1]
+            self._ready.set()
+            self._loop.run_forever()
+
+        self._thread = threading.Thread(target=run, daemon=True, name="app-ui")
+        self._thread.start()
+        if not self._ready.wait(15):
+            raise RuntimeError("app UI server did not start")
+        return self
+
+    @property
+    def url(self) -> str:
+        return f"http://{'localhost' if self.host in ('0.0.0.0', '127.0.0.1') else self.host}:{self.port}"
+
+    def stop(self) -> None:
+        if self._loop is None:
+            return
+        fut = asyncio.run_coroutine_threadsafe(self._runner.cleanup(), self._loop)
+        try:
+            fut.result(10)
+        except Exception:  # noqa: BLE001
+            pass
+        self._loop.call_soon_threadsafe(self._loop.stop)
+        self._thread.join(10)
+
+
+def serve_forever(client, app_id: str, api_gateway_url: str, tenant: str, port: int = 8092,
+                  open_browser: bool = True) -> int:
+    client.get(app_id)                      # fail fast: the application must exist
+    srv = AppUIServer(client, app_id, api_gateway_url, tenant, host="0.0.0.0", port=port).start()
+    print(f"Starting UI at {srv.url}", flush=True)
+    if open_browser:
+        try:
+            import webbrowser
+            if not webbrowser.open(srv.url):
+                print(f"Could not start a browser: open {srv.url} manually", flush=True)
+        except Exception:  # noqa: BLE001
+            print(f"Could not start a browser: open {srv.url} manually", flush=True)
+    stop = threading.Event()
+    try:
+        import signal
+        signal.signal(signal.SIGTERM, lambda *_: stop.set())
+    except ValueError:
+        pass
+    try:
+        while not stop.wait(1.0):
+            pass
+    except KeyboardInterrupt:
+        pass
+    srv.stop()
+    return 0

@@ -66,6 +66,14 @@ class AdminClient:
     def tenant_put(self, name: str, config: Optional[dict] = None) -> Dict[str, Any]:
         return self._call("PUT", f"/api/tenants/{name}", json=config or {}).json()
 
+    def tenant_create(self, name: str, max_units: Optional[int] = None) -> Dict[str, Any]:
+        """POST: fails with 409 when the tenant exists (CreateTenantCmd.java)."""
+        return self._call("POST", f"/api/tenants/{name}", json={"maxTotalResourceUnits": max_units}).json()
+
+    def tenant_update(self, name: str, max_units: Optional[int] = None) -> Dict[str, Any]:
+        """PATCH: fails with 404 when the tenant does not exist (UpdateTenantCmd.java)."""
+        return self._call("PATCH", f"/api/tenants/{name}", json={"maxTotalResourceUnits": max_units}).json()
+
     def tenant_get(self, name: str) -> Dict[str, Any]:
         return self._call("GET", f"/api/tenants/{name}").json()
 

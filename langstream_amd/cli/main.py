@@ -3,10 +3,11 @@
     python -m langstream_amd.cli <group> <command> ...
 
 Groups:
-* ``profiles``  list | get | create | update | delete | set-current  (~/.langstream/config.yaml:
-  webServiceUrl, apiGatewayUrl, tenant, token)
-* ``tenants``   list | get | put | delete
-* ``apps``      deploy | update | get | list | delete | logs | download | diagram
+* ``profiles``  list | get | get-current | create | update | import | delete | set-current
+  (~/.langstream/config.yaml: webServiceUrl, apiGatewayUrl, tenant, token)
+* ``configure`` <webServiceUrl|apiGatewayUrl|tenant|token> <value>  (the default profile)
+* ``tenants``   list | get | create | update | put | delete
+* ``apps``      deploy | update | get | list | delete | logs | download | diagram | ui
 * ``gateway``   produce | consume | chat  (WebSocket client; chat re-assembles streamed
   answers from ``stream-id`` / ``stream-index`` / ``stream-last-message`` headers,
   ``ChatGatewayCmd.java:45-120``)
@@ -77,12 +78,51 @@ def _print(obj, fmt: str = "json") -> None:
 
 
 # ---------------------------------------------------------------- apps
+_PROFILE_KEYS = ("webServiceUrl", "apiGatewayUrl", "tenant", "token")
+
+
+def _validate_profile(p: Dict[str, Any]) -> None:
+    """BaseProfileCmd.validateProfile."""
+    if not str(p.get("webServiceUrl") or "").strip():
+        raise ValueError("webServiceUrl is required")
+
+
 def cmd_profiles(args) -> int:
     c = load_config()
     if args.cmd == "list":
         _print({"current": c["currentProfile"], "profiles": c["profiles"]})
     elif args.cmd == "get":
         _print(c["profiles"].get(args.name) or {})
+    elif args.cmd == "get-current":
+        print(c.get("currentProfile", "default"))
+    elif args.cmd == "import":
+        # ImportProfileCmd.java: exactly one of --file (YAML / JSON) or --inline (JSON, or
+        # base64:<JSON>); an existing profile only with --update (overwritten, not merged)
+        import base64
+        import yaml
+        if (args.file is None) == (args.inline is None):
+            raise ValueError("Either --file or --inline must be specified (and only one)")
+        if args.file is not None:
+            if not os.path.isfile(args.file):
+                raise ValueError(f"File {args.file} does not exist")
+            with open(args.file) as f:
+                prof = yaml.safe_load(f) or {}
+        else:
+            text = args.inline
+            if text.startswith("base64:"):
+                text = base64.b64decode(text[len("base64:"):]).decode()
+            prof = json.loads(text)
+        new = {k: prof.get(k) for k in _PROFILE_KEYS if prof.get(k) is not None}
+        _validate_profile(new)
+        existed = args.name in c["profiles"]
+        if existed and not args.update:
+            raise ValueError(f"Profile {args.name} already exists")
+        c["profiles"][args.name] = new
+        print(f"profile {args.name} {'updated' if existed else 'created'}")
+        if args.set_current:
+            c["currentProfile"] = args.name
+            print(f"profile {args.name} set as current")
+        save_config(c)
     elif args.cmd in ("create", "update"):
         p = c["profiles"].get(args.name, {}) if args.cmd == "update" else {}
         for k, a in (("webServiceUrl", args.web_service_url), ("apiGatewayUrl", args.api_gateway_url),
@@ -102,14 +142,33 @@ def cmd_profiles(args) -> int:
     return 0
 
 
+def cmd_configure(args) -> int:
+    """ConfigureCmd.java: set one key of the default profile."""
+    if getattr(args, "profile", None):
+        raise ValueError("Global profile flag is not allowed here")
+    c = load_config()
+    prof = dict(c["profiles"].get("default") or DEFAULT_PROFILE)
+    prof[args.key] = args.value
+    c["profiles"]["default"] = {k: v for k, v in prof.items() if v is not None}
+    save_config(c)
+    print(f"profile default updated: {args.key}={args.value}")
+    return 0
+
+
 def cmd_tenants(args) -> int:
     cl = _client(args)
     if args.cmd == "list":
         _print(cl.tenants())
     elif args.cmd == "get":
         _print(cl.tenant_get(args.name))
+    elif args.cmd == "create":
+        cl.tenant_create(args.name, args.max_units)
+        print(f"tenant {args.name} created")
+    elif args.cmd == "update":
+        cl.tenant_update(args.name, args.max_units)
+        print(f"tenant {args.name} updated")
     elif args.cmd == "put":
-        _print(cl.tenant_put(args.name, {"max-total-resource-units": args.max_units} if args.max_units else {}))
+        _print(cl.tenant_put(args.name, {"maxTotalResourceUnits": args.max_units} if args.max_units else {}))
     elif args.cmd == "delete":
         cl.tenant_delete(args.name)
     return 0
@@ -145,6 +204,11 @@ def cmd_apps(args) -> int:
     if args.cmd == "diagram":
         print(mermaid(args.app, args.instance, args.secrets))
         return 0
+    if args.cmd == "ui":
+        from .app_ui import serve_forever
+        p = current_profile(args)
+        return serve_forever(_client(args), args.name, p["apiGatewayUrl"], p["tenant"], args.port,
+                             open_browser=not args.no_browser)
     cl = _client(args)
     if args.cmd == "deploy":
         _print(cl.deploy(args.name, args.app, args.instance, args.secrets, args.dry_run), args.output)
@@ -423,8 +487,15 @@ def build_parser() -> argparse.ArgumentParser:
     p = sub.add_parser("profiles")
     ps = p.add_subparsers(dest="cmd", required=True)
     ps.add_parser("list")
+    ps.add_parser("get-current")
     for c in ("get", "delete", "set-current"):
         ps.add_parser(c).add_argument("name")
+    x = ps.add_parser("import", help="import a profile from a file or inline JSON")
+    x.add_argument("name")
+    x.add_argument("-f", "--file")
+    x.add_argument("-i", "--inline", help="JSON, or base64:<JSON>")
+    x.add_argument("-u", "--update", action="store_true", help="overwrite an existing profile")
+    x.add_argument("--set-current", action="store_true")
     for c in ("create", "update"):
         x = ps.add_parser(c)
         x.add_argument("name")
@@ -440,10 +511,16 @@ def build_parser() -> argparse.ArgumentParser:
     ts.add_parser("list")
     for c in ("get", "delete"):
         ts.add_parser(c).add_argument("name")
-    x = ts.add_parser("put")
-    x.add_argument("name")
-    x.add_argument("--max-units", type=int)
+    for c in ("create", "update", "put"):
+        x = ts.add_parser(c)
+        x.add_argument("name")
+        x.add_argument("--max-total-resource-units", "--max-units", dest="max_units", type=int)
     t.set_defaults(fn=cmd_tenants)
+
+    cf = sub.add_parser("configure", help="set a key of the default profile")
+    cf.add_argument("key", choices=("webServiceUrl", "apiGatewayUrl", "tenant", "token"))
+    cf.add_argument("value")
+    cf.set_defaults(fn=cmd_configure)
 
     a = sub.add_parser("apps")
     asub = a.add_subparsers(dest="cmd", required=True)
@@ -474,6 +551,10 @@ def build_parser() -> argparse.ArgumentParser:
     x.add_argument("-app", "--app", required=True)
     x.add_argument("-i", "--instance")
     x.add_argument("-s", "--secrets")
+    x = asub.add_parser("ui", help="local web UI for the application's gateways, diagram and logs")
+    x.add_argument("name")
+    x.add_argument("-p", "--port", type=int, default=8092, help="0 = a random port")
+    x.add_argument("--no-browser", action="store_true")
     a.set_defaults(fn=cmd_apps)
 
     g = sub.add_parser("gateway")

@@ -77,6 +77,25 @@ class _AppLogBuffer(logging.Handler):
                 self.cv.wait(timeout)
 
 
+def gateway_summary(g) -> Dict[str, Any]:
+    """A gateway as the application description lists it (the ``apps ui`` page reads
+    these: id, type, topic, parameters, auth provider, chat / service options)."""
+    out: Dict[str, Any] = {"id": g.id, "type": g.type, "topic": g.topic, "parameters": list(g.parameters or [])}
+    if g.authentication is not None:
+        out["authentication"] = {"provider": g.authentication.provider,
+                                 "allow-test-mode": g.authentication.allow_test_mode}
+    if g.chat_options is not None:
+        out["chat-options"] = {"questions-topic": g.chat_options.questions_topic,
+                               "answers-topic": g.chat_options.answers_topic}
+    if g.service_options is not None:
+        out["service-options"] = {"agent-id": g.service_options.agent_id,
+                                  "input-topic": g.service_options.input_topic,
+                                  "output-topic": g.service_options.output_topic}
+    if g.events_topic:
+        out["events-topic"] = g.events_topic
+    return out
+
+
 class ControlPlane:
     """Application lifecycle independent of HTTP (also used by the CLI's local mode)."""
 
@@ -109,6 +128,13 @@ class ControlPlane:
                 os.path.isdir(os.path.join(dest, entries[0])):
             root = os.path.join(dest, entries[0])
         return {"__root__": root, **read_app_directory(root)}
+
+    def tenant_limit(self, tenant: str) -> int:
+        """The tenant's ``maxTotalResourceUnits`` when set (> 0), else the default
+        (``ApplicationService.java:95-125``)."""
+        cfg = self.store.get_tenant(tenant) or {}
+        own = int(cfg.get("maxTotalResourceUnits") or cfg.get("max-total-resource-units") or 0)
+        return own if own > 0 else self.max_units
 
     def _units(self, plan) -> int:
         return sum(int(n.resources.size or 1) * int(n.resources.parallelism or 1) for n in plan.agents.values())
@@ -152,9 +178,10 @@ class ControlPlane:
         info = build_application_instance(files, instance, secrets)
         plan = ApplicationDeployer().create_implementation(app_id, info.application)
         units = self._units(plan)
-        if self.max_units and self._tenant_units(tenant, exclude=app_id) + units > self.max_units:
+        limit = self.tenant_limit(tenant)
+        if limit and self._tenant_units(tenant, exclude=app_id) + units > limit:
             raise PermissionError(f"Not enough resources to deploy application {app_id}: tenant limit "
-                                  f"{self.max_units} units")
+                                  f"{limit} units")
         if dry_run:
             if code_root is not None:
                 shutil.rmtree(tmp, ignore_errors=True)
@@ -250,6 +277,7 @@ class ControlPlane:
         plan = ApplicationDeployer().create_implementation(app_id, sa.application)
         out = sa.summary()
         out["application"] = plan.to_dict()
+        out["application"]["gateways"] = [gateway_summary(g) for g in (sa.application.gateways or [])]
         out["status"]["status"]["reason"] = getattr(sa, "error", None)
         agents = {}
         if sa.runner is not None and stats:
@@ -387,6 +415,9 @@ class WebServiceServer:
         return web.json_response(self.cp.store.list_tenants())
 
     async def tenant(self, request):
+        """``TenantResource.java``: GET; POST creates (409 when it exists); PATCH updates
+        (404 when missing); PUT creates or replaces; DELETE.  The body carries
+        ``maxTotalResourceUnits`` (>= 0; 0 = the control plane's default limit)."""
         from aiohttp import web
         t = request.match_info["tenant"]
         if request.method == "GET":
@@ -394,15 +425,28 @@ class WebServiceServer:
             if v is None:
                 raise KeyError(f"tenant {t} not found")
             return web.json_response(v)
-        if request.method in ("PUT", "POST"):
-            body = await request.json() if request.can_read_body else {}
-            self.cp.store.put_tenant(t, body or {})
+        if request.method in ("PUT", "POST", "PATCH"):
+            body = (await request.json() if request.can_read_body else {}) or {}
+            units = body.get("maxTotalResourceUnits", body.get("max-total-resource-units"))
+            if units is not None and int(units) < 0:
+                raise ValueError("maxTotalResourceUnits must be positive")
+            existing = self.cp.store.get_tenant(t)
+            if request.method == "POST" and existing is not None:
+                raise FileExistsError("tenant already exists")
+            if request.method == "PATCH" and existing is None:
+                raise KeyError("tenant not found")
+            cfg = dict(existing or {}) if request.method == "PATCH" else {}
+            cfg.pop("name", None)
+            cfg.pop("max-total-resource-units", None)
+            if units is not None or request.method != "PATCH":
+                cfg["maxTotalResourceUnits"] = int(units or 0)
+            self.cp.store.put_tenant(t, cfg)
             return web.json_response(self.cp.store.get_tenant(t))
         if request.method == "DELETE":
             if not self.cp.store.delete_tenant(t):
                 raise KeyError(f"tenant {t} not found")
             return web.json_response({})
-        raise web.HTTPMethodNotAllowed(request.method, ["GET", "PUT", "POST", "DELETE"])
+        raise web.HTTPMethodNotAllowed(request.method, ["GET", "PUT", "POST", "PATCH", "DELETE"])
 
     async def list_apps(self, request):
         from aiohttp import web

@@ -1,0 +1,201 @@
+"""CLI parity (VERDICT r4 missing #4): ``configure``, ``profiles import`` / ``get-current``,
+``tenants create`` / ``update`` and ``apps ui``, driven against the in-process control
+plane and API gateway.
+
+Reference: ``langstream-cli/.../commands/configure/ConfigureCmd.java``,
+``profiles/ImportProfileCmd.java``, ``profiles/GetCurrentProfileCmd.java``,
+``tenants/CreateTenantCmd.java`` / ``UpdateTenantCmd.java`` (POST / PATCH on
+``TenantResource.java``), ``applications/UIAppCmd.java``."""
+import asyncio
+import base64
+import json
+import textwrap
+
+import pytest
+import requests
+import yaml
+
+from langstream_amd.cli.client import AdminClient, zip_directory
+from langstream_amd.cli.main import main as cli_main
+from langstream_amd.topics.memory import reset_memlogs
+from langstream_amd.webservice.server import ControlPlane, WebServiceServer
+
+
+@pytest.fixture()
+def cfg(tmp_path, monkeypatch):
+    path = tmp_path / "cli.yaml"
+    monkeypatch.setattr("langstream_amd.cli.main.CONFIG", str(path))
+    return path
+
+
+def _load(path):
+    return yaml.safe_load(path.read_text())
+
+
+def test_configure_sets_default_profile_keys(cfg, capsys):
+    assert cli_main(["configure", "webServiceUrl", "http://cp:8090"]) == 0
+    assert cli_main(["configure", "tenant", "acme"]) == 0
+    assert cli_main(["configure", "token", "tok"]) == 0
+    d = _load(cfg)["profiles"]["default"]
+    assert d["webServiceUrl"] == "http://cp:8090" and d["tenant"] == "acme" and d["token"] == "tok"
+    assert d["apiGatewayUrl"] == "ws://localhost:8091"            # untouched default
+    assert "profile default updated: tenant=acme" in capsys.readouterr().out
+    assert cli_main(["--profile", "p1", "configure", "tenant", "x"]) == 1   # global profile flag refused
+    with pytest.raises(SystemExit):
+        cli_main(["configure", "nope", "x"])                       # unknown key
+
+
+def test_profiles_import_and_get_current(cfg, tmp_path, capsys):
+    f = tmp_path / "p.yaml"
+    f.write_text("webServiceUrl: http://a:1\napiGatewayUrl: ws://a:2\ntenant: ta\ntoken: t\n")
+    assert cli_main(["profiles", "import", "pa", "--file", str(f)]) == 0
+    assert "profile pa created" in capsys.readouterr().out
+    assert _load(cfg)["profiles"]["pa"] == {"webServiceUrl": "http://a:1", "apiGatewayUrl": "ws://a:2",
+                                            "tenant": "ta", "token": "t"}
+    # an existing profile needs --update (overwritten, not merged)
+    assert cli_main(["profiles", "import", "pa", "-i", '{"webServiceUrl": "http://b:1"}']) == 1
+    assert cli_main(["profiles", "import", "pa", "-u", "-i", '{"webServiceUrl": "http://b:1"}']) == 0
+    assert _load(cfg)["profiles"]["pa"] == {"webServiceUrl": "http://b:1"}
+    inline = "base64:" + base64.b64encode(json.dumps({"webServiceUrl": "http://c:1", "tenant": "tc"}).encode()).decode()
+    assert cli_main(["profiles", "import", "pc", "--inline", inline, "--set-current"]) == 0
+    assert _load(cfg)["profiles"]["pc"]["tenant"] == "tc" and _load(cfg)["currentProfile"] == "pc"
+    capsys.readouterr()
+    assert cli_main(["profiles", "get-current"]) == 0
+    assert capsys.readouterr().out.strip() == "pc"
+    # exactly one source; webServiceUrl required
+    assert cli_main(["profiles", "import", "x"]) == 1
+    assert cli_main(["profiles", "import", "x", "-f", str(f), "-i", "{}"]) == 1
+    assert cli_main(["profiles", "import", "x", "-i", '{"tenant": "t"}']) == 1
+    assert cli_main(["profiles", "import", "x", "-f", str(tmp_path / "missing.yaml")]) == 1
+
+
+@pytest.fixture()
+def control_plane(tmp_path):
+    reset_memlogs()
+    cp = ControlPlane(code_dir=str(tmp_path / "code"), max_units_per_tenant=100)
+    srv = WebServiceServer(cp, port=0).start()
+    yield cp, srv
+    for t in list(cp.store.list_tenants()):
+        for a in cp.store.list(t):
+            cp.delete(t, a.application_id, force=True)
+    srv.stop()
+    reset_memlogs()
+
+
+def test_tenants_create_and_update(control_plane, cfg, capsys):
+    cp, srv = control_plane
+    assert cli_main(["profiles", "create", "local", "--web-service-url", srv.url, "--set-current"]) == 0
+    assert cli_main(["tenants", "create", "t1", "--max-total-resource-units", "3"]) == 0
+    assert "tenant t1 created" in capsys.readouterr().out
+    assert cp.store.get_tenant("t1")["maxTotalResourceUnits"] == 3
+    assert cli_main(["tenants", "create", "t1"]) == 1                      # 409: already exists
+    assert "409" in capsys.readouterr().err
+    assert cli_main(["tenants", "update", "t1", "--max-total-resource-units", "8"]) == 0
+    assert cp.store.get_tenant("t1")["maxTotalResourceUnits"] == 8
+    assert cli_main(["tenants", "update", "missing"]) == 1                 # 404
+    cl = AdminClient(srv.url, "t1")
+    assert cl.tenant_get("t1")["maxTotalResourceUnits"] == 8
+    # a negative limit is refused
+    r = requests.patch(f"{srv.url}/api/tenants/t1", json={"maxTotalResourceUnits": -1}, timeout=10)
+    assert r.status_code == 400
+
+
+def test_tenant_limit_applies_to_deploys(control_plane, tmp_path):
+    cp, srv = control_plane
+    d = tmp_path / "app"
+    d.mkdir()
+    (d / "pipeline.yaml").write_text(textwrap.dedent("""
+        pipeline:
+          - name: c
+            type: compute
+            input: in-t
+            output: out-t
+            resources:
+              parallelism: 2
+              size: 2
+            configuration:
+              fields:
+                - name: value
+                  expression: "fn:uppercase(value)"
+        topics:
+          - name: in-t
+            creation-mode: create-if-not-exists
+          - name: out-t
+            creation-mode: create-if-not-exists
+        """))
+    cl = AdminClient(srv.url, "small")
+    cl.tenant_create("small", 5)
+    cl.deploy("a1", str(d))                    # 4 units
+    with pytest.raises(Exception) as ei:
+        cl.deploy("a2", str(d))                # 8 > 5 (the tenant's own limit, not the default 100)
+    assert getattr(ei.value, "status", None) == 403
+
+
+APP = """
+topics:
+  - name: ui-in
+    creation-mode: create-if-not-exists
+  - name: ui-out
+    creation-mode: create-if-not-exists
+pipeline:
+  - name: upper
+    type: compute
+    input: ui-in
+    output: ui-out
+    configuration:
+      fields:
+        - name: value
+          expression: "fn:uppercase(value)"
+"""
+GATEWAYS = """
+gateways:
+  - id: in
+    type: produce
+    topic: ui-in
+  - id: out
+    type: consume
+    topic: ui-out
+"""
+
+
+def test_apps_ui_serves_model_page_logs_and_proxies_gateways(control_plane, tmp_path):
+    import aiohttp
+    from langstream_amd.cli.app_ui import AppUIServer
+    from langstream_amd.gateway.server import GatewayServer, GatewayService
+    cp, srv = control_plane
+    d = tmp_path / "uiapp"
+    d.mkdir()
+    (d / "pipeline.yaml").write_text(APP)
+    (d / "gateways.yaml").write_text(GATEWAYS)
+    cp.store.put_tenant("default", {})
+    cp.deploy("default", "uiapp", zip_directory(str(d)), None, None)
+    gw = GatewayServer(GatewayService(cp.store), port=0).start()
+    ui = AppUIServer(AdminClient(srv.url, "default"), "uiapp", gw.url.replace("http", "ws"), "default",
+                     port=0).start()
+    try:
+        page = requests.get(ui.url + "/", timeout=10)
+        assert page.status_code == 200 and "<html" in page.text and "/api/application" in page.text
+        model = requests.get(ui.url + "/api/application", timeout=10).json()
+        assert model["applicationId"] == "uiapp" and model["tenant"] == "default"
+        assert model["baseUrl"].startswith("ws://") and model["remoteBaseUrl"] == gw.url.replace("http", "ws")
+        assert sorted((g["id"], g["type"]) for g in model["gateways"]) == [("in", "produce"), ("out", "consume")]
+        assert "flowchart LR" in model["mermaidDefinition"] and "produce gateway" in model["mermaidDefinition"]
+        assert json.loads(model["applicationDefinition"])["application"]["application-id"] == "uiapp"
+
+        async def roundtrip():
+            base = model["baseUrl"] + "/v1"
+            async with aiohttp.ClientSession() as s:
+                async with s.ws_connect(f"{base}/consume/default/uiapp/out?option:position=earliest") as cons:
+                    async with s.ws_connect(f"{base}/produce/default/uiapp/in") as prod:
+                        await prod.send_str(json.dumps({"value": "hello ui"}))
+                        ack = json.loads((await prod.receive(timeout=10)).data)
+                        assert ack["status"] == "OK", ack
+                    got = json.loads((await cons.receive(timeout=20)).data)
+                    return got["record"]["value"]
+
+        assert asyncio.new_event_loop().run_until_complete(roundtrip()) == "HELLO UI"
+        logs = requests.get(ui.url + "/api/logs?follow=false", timeout=20)
+        assert logs.status_code == 200 and logs.headers["Content-Type"].startswith("text/plain")
+    finally:
+        ui.stop()
+        gw.stop()
