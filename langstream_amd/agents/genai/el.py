@@ -321,7 +321,17 @@ def _fn_tostring(v) -> str:
 
 
 def _fn_to_json(v):
-    return json.dumps(v)
+    # Jackson's default writer: compact separators, non-ASCII as is (JstlFunctions.toJson)
+    return json.dumps(v, separators=(",", ":"), ensure_ascii=False, default=_json_default)
+
+
+def _json_default(o):
+    if isinstance(o, Decimal):
+        return float(o)
+    if isinstance(o, (bytes, bytearray)):
+        import base64
+        return base64.b64encode(bytes(o)).decode()
+    raise TypeError(f"{type(o).__name__} is not JSON serializable")
 
 
 def _fn_from_json(v):
@@ -329,7 +339,29 @@ def _fn_from_json(v):
         return None
     if isinstance(v, bytes):
         v = v.decode()
+    if isinstance(v, str) and not v.strip():
+        return None                     # JstlFunctions.fromJson: empty text -> null
     return json.loads(v) if isinstance(v, str) else v
+
+
+def _to_big_integer(v) -> int:
+    """BigInteger conversion of JstlTypeConverter: byte[] two's complement, text, numbers."""
+    if isinstance(v, (bytes, bytearray)):
+        return int.from_bytes(bytes(v), "big", signed=True)
+    if isinstance(v, str):
+        return int(v.strip())
+    return int(v)
+
+
+def _fn_to_big_decimal(v, scale=None):
+    """``toBigDecimal(value, scale)`` = new BigDecimal(BigInteger(value), scale) (exact);
+    ``toBigDecimal(value)`` = BigDecimal.valueOf(double): the value goes through a double."""
+    if v is None:
+        return None
+    if scale is None:
+        return Decimal(repr(_to_double(v)))
+    import decimal
+    return Decimal(_to_big_integer(v)).scaleb(-int(_fn_tostring(scale)), context=decimal.Context(prec=1000))
 
 
 def _fn_length(v):
@@ -378,6 +410,8 @@ def _fn_concat(*args):
 def _fn_replace(v, regex, repl):
     if v is None:
         return None
+    if regex is None or repl is None:      # JstlFunctions.replace: nothing to replace with
+        return _fn_tostring(v)
     return re.sub(_fn_tostring(regex), _fn_tostring(repl).replace("$", "\\"), _fn_tostring(v))
 
 
@@ -445,21 +479,45 @@ def _fn_list_to_list_of_structs(lst, field):
     return [{field: x} for x in lst]
 
 
+_EPOCH = _dt.datetime(1970, 1, 1, tzinfo=_dt.timezone.utc)
+
+
+def _dt_millis(d: "_dt.datetime") -> int:
+    # exact integer arithmetic (d.timestamp() * 1000 rounds .005 s down to 4 ms)
+    if d.tzinfo is None:
+        d = d.replace(tzinfo=_dt.timezone.utc)
+    return (d - _EPOCH) // _dt.timedelta(milliseconds=1)
+
+
 def _to_millis(v) -> int:
+    """Instant conversion of JstlTypeConverter: epoch millis, ISO-8601 text (an offset is
+    honoured, none means UTC), datetimes; byte / other types are refused."""
+    if isinstance(v, bool):
+        raise ValueError(f"Cannot convert [{v}] to an Instant")
     if isinstance(v, (int, float)):
         return int(v)
     if isinstance(v, _dt.datetime):
-        return int(v.timestamp() * 1000)
+        return _dt_millis(v)
+    if isinstance(v, (bytes, bytearray)):
+        v = v.decode()
     if isinstance(v, str):
-        s = v.replace("Z", "+00:00")
-        d = _dt.datetime.fromisoformat(s)
-        if d.tzinfo is None:
-            d = d.replace(tzinfo=_dt.timezone.utc)
-        return int(d.timestamp() * 1000)
-    raise ValueError(f"cannot coerce {v!r} to a timestamp")
+        return _dt_millis(_dt.datetime.fromisoformat(v.strip().replace("Z", "+00:00")))
+    raise ValueError(f"Cannot convert [{v}] of type [{type(v).__name__}] to an Instant")
 
 
 _UNIT_MS = {"days": 86400000, "hours": 3600000, "minutes": 60000, "seconds": 1000, "millis": 1}
+
+
+def _delta_long(d) -> int:
+    """The delta's long value (JstlTypeConverter): numbers, numeric text, and a
+    LocalTime as its millisecond of day."""
+    if isinstance(d, _dt.time):
+        return ((d.hour * 60 + d.minute) * 60 + d.second) * 1000 + d.microsecond // 1000
+    if isinstance(d, (bytes, bytearray)):
+        d = d.decode()
+    if isinstance(d, str):
+        return int(float(d)) if not d.strip().lstrip("-").isdigit() else int(d)
+    return int(d)
 
 
 def _fn_timestamp_add(v, delta, unit):
@@ -467,13 +525,16 @@ def _fn_timestamp_add(v, delta, unit):
         raise ValueError("timestampAdd requires input and unit")
     unit = _fn_tostring(unit)
     ms = _to_millis(v)
-    d = int(delta)
+    d = _delta_long(delta)
     if unit in ("years", "months"):
-        t = _dt.datetime.fromtimestamp(ms / 1000, tz=_dt.timezone.utc)
+        import calendar
+        t = _EPOCH + _dt.timedelta(milliseconds=ms)
         months = d * (12 if unit == "years" else 1)
         y, mth = divmod(t.month - 1 + months, 12)
-        t = t.replace(year=t.year + y, month=mth + 1)
-        return int(t.timestamp() * 1000)
+        # Instant.atZone(UTC).plusMonths: an out-of-range day clamps to the month's last day
+        day = min(t.day, calendar.monthrange(t.year + y, mth + 1)[1])
+        t = t.replace(year=t.year + y, month=mth + 1, day=day)
+        return _dt_millis(t)
     if unit == "nanos":
         return ms + d // 1_000_000
     if unit not in _UNIT_MS:
@@ -503,8 +564,7 @@ FUNCTIONS: Dict[str, Callable] = {
     "contains": _fn_contains, "trim": lambda v: None if v is None else _fn_tostring(v).strip(),
     "concat": _fn_concat, "concat3": _fn_concat, "coalesce": _fn_coalesce, "replace": _fn_replace,
     "str": _fn_tostring, "toString": _fn_tostring, "toDouble": _to_double, "toInt": _to_int, "toLong": _to_int,
-    "toBigDecimal": lambda v, scale=None: None if v is None else (
-        Decimal(_fn_tostring(v)) if scale is None else Decimal(int(v)).scaleb(-int(scale))),
+    "toBigDecimal": _fn_to_big_decimal,
     "decimalFromUnscaled": lambda v, scale: Decimal(int(v)).scaleb(-int(scale)),
     "decimalFromNumber": lambda v: Decimal(str(v)),
     "split": _fn_split, "unpack": _fn_unpack, "listOf": _fn_list_of, "emptyList": lambda: [],
