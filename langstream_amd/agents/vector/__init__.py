@@ -17,6 +17,7 @@ from typing import Any, Dict, List
 from ...api.agent import AgentProcessor, AgentSink, completed, failed
 from ...api.record import SourceRecordAndResult
 from ...engine.vector_store import VectorStoreRegistry
+from ...engine.vector_store import _safe as _safe_name
 from ...runtime.registry import register_agent
 from ..genai.el import eval_expression
 from ..genai.mutable import MutableRecord
@@ -252,11 +253,14 @@ class VectorDBSinkAgent(AgentSink):
         # in this agent's persistent state directory (the pod's PVC: the planner gives
         # every vector-db-sink a disk), so a pod restart never loses indexed rows whose
         # source offsets were committed.
+        # Only THIS sink's collection is bound to its directory; the process-wide default
+        # stays unset, so a later sink of another collection uses its own state dir.
+        self.writer = _LocalWriter(self.cfg)
         if VectorStoreRegistry.persist_dir is None:
             d = context.get_persistent_state_directory_for_agent(self.agent_id()) if context is not None else None
             if d:
-                VectorStoreRegistry.configure(persist_dir=os.path.join(d, "vector-store"))
-        self.writer = _LocalWriter(self.cfg)
+                VectorStoreRegistry.bind(self.writer.collection,
+                                         os.path.join(d, "vector-store", _safe_name(self.writer.collection)))
 
     def write(self, record) -> Future:
         self.processed(1, 0)

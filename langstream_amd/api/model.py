@@ -340,8 +340,8 @@ class KeyValueComparison:
         if n > 1:
             raise ValueError("Only one of 'value', 'valueFromParameters' or 'valueFromAuthentication' can be "
                              "specified for filter")
-        if self.key is None:
-            self.key = self.value or self.value_from_parameters or self.value_from_authentication
+        # no default for a missing key: the model keeps it null (ModelBuilderTest.testParseGateway)
+        # and the gateway refuses it when the gateway is used (ProduceGateway / ConsumeGateway)
 
     @staticmethod
     def from_dict(d: dict) -> "KeyValueComparison":

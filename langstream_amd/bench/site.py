@@ -58,11 +58,16 @@ class Site:
                 self._send(200, body.encode())
 
             def _send(self, code, body):
-                self.send_response(code)
-                self.send_header("Content-Type", "text/html; charset=utf-8")
-                self.send_header("Content-Length", str(len(body)))
-                self.end_headers()
-                self.wfile.write(body)
+                try:
+                    self.send_response(code)
+                    self.send_header("Content-Type", "text/html; charset=utf-8")
+                    self.send_header("Content-Length", str(len(body)))
+                    self.end_headers()
+                    self.wfile.write(body)
+                except (BrokenPipeError, ConnectionResetError):
+                    # the crawler gave up on a long-polled index (its http-timeout, or the
+                    # bench ending): nothing to answer, and no traceback on stderr
+                    self.close_connection = True
 
         self.httpd = http.server.ThreadingHTTPServer(("127.0.0.1", 0), H)
         self.httpd.daemon_threads = True

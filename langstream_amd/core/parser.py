@@ -287,19 +287,28 @@ def build_from_directory(app_dir: str, instance_file: Optional[str] = None,
 
 
 def directory_digest(path: str) -> Optional[str]:
-    """SHA-256 over every file (sorted relative paths + contents): 'code changed?' detection."""
+    """SHA-256 'code changed?' digest, ModelBuilder.java:275-361: a depth-first walk where
+    each directory's entries (files and sub-directories together) are visited in name
+    order, every file contributing its path relative to ``path`` and then its bytes;
+    None when there is no file."""
     if not os.path.isdir(path):
         return None
     h = hashlib.sha256()
-    for root, dirs, fns in os.walk(path):
-        dirs.sort()
-        dirs[:] = [d for d in dirs if d != "__pycache__"]
-        for fn in sorted(fns):
-            full = os.path.join(root, fn)
-            h.update(os.path.relpath(full, path).encode())
-            with open(full, "rb") as f:
-                h.update(f.read())
-    return h.hexdigest()
+    seen = [False]
+
+    def walk(cur: str) -> None:
+        for name in sorted(os.listdir(cur)):
+            full = os.path.join(cur, name)
+            if os.path.isdir(full):
+                walk(full)
+            elif os.path.isfile(full):
+                h.update(os.path.relpath(full, path).replace(os.sep, "/").encode())
+                with open(full, "rb") as f:
+                    h.update(f.read())
+                seen[0] = True
+
+    walk(path)
+    return h.hexdigest() if seen[0] else None
 
 
 # ---------------------------------------------------------------- archetypes

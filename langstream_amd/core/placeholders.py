@@ -53,7 +53,8 @@ def _to_str(v: Any) -> str:
         return ""
     if isinstance(v, str):
         return v
-    return json.dumps(v)
+    # Jackson's compact form: "123-[1,2]" (ApplicationPlaceholderResolverTest.testResolve)
+    return json.dumps(v, separators=(",", ":"), ensure_ascii=False)
 
 
 def resolve_in_string(template: str, context: Dict[str, Any]) -> str:

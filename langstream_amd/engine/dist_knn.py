@@ -186,6 +186,12 @@ class ShardedKnn:
 
     # ------------------------------------------------------------------ service loop
     def _loop(self) -> None:
+        import sys
+        # A round hands the GIL back and forth ~10 times (each gloo collective releases
+        # it); on a rank whose agents are busy in Python every hand-off waits up to the
+        # switch interval, and the OTHER ranks wait in the collective for it.  1 ms (the
+        # LLM engine's setting) bounds a slow rank's cost to the rest of the world.
+        sys.setswitchinterval(min(sys.getswitchinterval(), 0.001))
         try:
             if self.device.type == "cuda":
                 torch.cuda.set_device(self.device.index if self.device.index is not None

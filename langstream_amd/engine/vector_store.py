@@ -504,6 +504,37 @@ class VectorStoreRegistry:
     _lock = threading.Lock()
     persist_dir: Optional[str] = os.environ.get("LANGSTREAM_VECTOR_STORE_DIR") or None
     fsync: bool = False
+    # collection -> directory bound by the sink that owns it (``bind``): the zero-config
+    # default, each local vector-db-sink persisting ITS collection in ITS own state dir
+    _bound: Dict[str, str] = {}
+
+    @classmethod
+    def _dir_of(cls, name: str) -> Optional[str]:
+        """Where ``name`` persists: the process-wide directory when one is configured
+        (persist-directory / $LANGSTREAM_VECTOR_STORE_DIR), else its sink's binding."""
+        if cls.persist_dir:
+            return os.path.join(cls.persist_dir, _safe(name))
+        return cls._bound.get(name)
+
+    @classmethod
+    def bind(cls, name: str, directory: str) -> None:
+        """Persist collection ``name`` under ``directory`` (a sink's persistent state
+        directory) when no process-wide directory is configured.  Only that collection
+        is affected: a second sink of another collection binds its own directory, and
+        no sink's directory becomes a default for the others."""
+        with cls._lock:
+            if cls.persist_dir:
+                return
+            old = cls._bound.get(name)
+            if old and old != directory:
+                log.warning("vector collection %s is already persisted under %s; ignoring %s", name, old, directory)
+                return
+            cls._bound[name] = directory
+            s = cls._stores.get(name)
+            if s is not None and not s.persistent and not s.attach_persistence(directory, cls.fsync):
+                log.warning("vector collection %s was created without persistence and already holds "
+                            "%d rows: they are NOT durable (bind persistence before the first write)",
+                            name, len(s))
 
     @classmethod
     def configure(cls, persist_dir: Optional[str] = None, fsync: Optional[bool] = None) -> None:
@@ -529,9 +560,9 @@ class VectorStoreRegistry:
 
     @classmethod
     def _persisted_dim(cls, name: str) -> Optional[int]:
-        if not cls.persist_dir:
+        d = cls._dir_of(name)
+        if not d:
             return None
-        d = os.path.join(cls.persist_dir, _safe(name))
         meta = os.path.join(d, "snapshot.json")
         wal = os.path.join(d, "wal.log")
         hdr = _Persistence.read_snapshot_header(os.path.join(d, "snapshot.lsv"))
@@ -561,7 +592,7 @@ class VectorStoreRegistry:
                     raise KeyError(f"vector collection {name} does not exist")
                 if device is None:
                     device = "cuda" if torch.cuda.is_available() else "cpu"
-                pdir = os.path.join(cls.persist_dir, _safe(name)) if cls.persist_dir and persist else None
+                pdir = cls._dir_of(name) if persist else None
                 s = VectorStore(dim, device=device, name=name, persist_dir=pdir, fsync=cls.fsync)
                 cls._stores[name] = s
             return s
@@ -579,9 +610,10 @@ class VectorStoreRegistry:
             s = cls._stores.pop(name, None)
         if s is not None:
             s.close()
-        if purge and cls.persist_dir:
+        d = cls._dir_of(name) if purge else None
+        if d:
             import shutil
-            shutil.rmtree(os.path.join(cls.persist_dir, _safe(name)), ignore_errors=True)
+            shutil.rmtree(d, ignore_errors=True)
 
     @classmethod
     def reset(cls) -> None:
@@ -589,3 +621,4 @@ class VectorStoreRegistry:
             for s in cls._stores.values():
                 s.close()
             cls._stores.clear()
+            cls._bound.clear()

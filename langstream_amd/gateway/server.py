@@ -126,7 +126,16 @@ def message_filters(kvs: Optional[List[KeyValueComparison]], ctx: RequestContext
 
 
 def common_headers(kvs: Optional[List[KeyValueComparison]], ctx: RequestContext) -> List[Header]:
-    return [Header(kv.key, _kv_value(kv, ctx)) for kv in kvs or []]
+    """ProduceGateway.getProducerCommonHeaders: every mapping needs a key and a value."""
+    out = []
+    for kv in kvs or []:
+        if not kv.key:
+            raise GatewayError("Header key cannot be empty")
+        v = _kv_value(kv, ctx)
+        if v is None:
+            raise GatewayError(f"header {kv.key} cannot be empty")
+        out.append(Header(kv.key, v))
+    return out
 
 
 class _ProducerCache:

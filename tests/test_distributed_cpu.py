@@ -385,3 +385,76 @@ def test_sharded_knn_local_failure_keeps_collectives_in_step():
     assert g[0]["first"][0] == "ok" and g[0]["first"][2] == 5
     for r in range(2):
         assert g[r]["second"] == ("ok", [0, 1], 5)
+
+
+def _slow_rank_knn_worker(rank, world, port, q):
+    """A slow agent on one rank (blocked in a sleep, then busy in pure-Python work holding
+    the GIL for most of each switch interval) must not stall the other ranks' kNN
+    rounds: the service thread of the slow rank keeps taking part in every round."""
+    import time as _t
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from langstream_amd.engine import dist_knn
+        from langstream_amd.engine.vector_store import VectorStoreRegistry
+        vecs, queries = _knn_corpus()
+        rows = [i for i in range(vecs.shape[0]) if i % world == rank]
+        VectorStoreRegistry.get("docs", 48, device="cpu").upsert(
+            [f"d{i}" for i in rows], vecs[rows].tolist(), [{"text": f"t{i}"} for i in rows])
+        svc = dist_knn.start(device="cpu")
+        slow = world - 1
+        out = {}
+        for phase in ("none", "sleep", "busy"):
+            dist.barrier()
+            t0 = _t.time()
+            if rank == slow:
+                if phase == "none":
+                    pass
+                elif phase == "sleep":
+                    _t.sleep(_SLOW_S)                   # an agent blocked on a slow call
+                else:
+                    x = 0
+                    while _t.time() - t0 < _SLOW_S:     # an agent burning CPU in Python
+                        for i in range(1000):
+                            x += i * i
+                # the slow rank's own query still works once its agent comes back
+                assert len(svc.search("docs", queries[:1].tolist(), 5).result(60)[0]) == 5
+                out[phase] = {"end": _t.time()}
+            else:
+                lat = []
+                for j in range(_FAST_QUERIES):
+                    ts = _t.time()
+                    res = svc.search("docs", queries[(rank + j) % 10:(rank + j) % 10 + 1].tolist(), 5).result(60)
+                    lat.append(_t.time() - ts)
+                    assert len(res[0]) == 5
+                out[phase] = {"lat": lat, "done": _t.time()}
+        gathered = [None] * world
+        dist.all_gather_object(gathered, out)
+        dist_knn.stop()
+        if rank == 0:
+            q.put(gathered)
+    finally:
+        dist.destroy_process_group()
+
+
+_SLOW_S = 3.0
+_FAST_QUERIES = 10
+
+
+def test_sharded_knn_slow_rank_does_not_stall_others():
+    """world-8 gloo with one slow rank; every other rank's queries finish
+    while the slow rank's agent is still blocked / busy, with bounded per-query latency."""
+    world = 8
+    g = _spawn(_slow_rank_knn_worker, world)
+    slow = g[world - 1]
+    p50 = {}
+    for phase in ("none", "sleep", "busy"):
+        lats = sorted(x for r in g[:-1] for x in r[phase]["lat"])
+        p50[phase] = lats[len(lats) // 2]
+        print(phase, "p50 %.3f s  max %.3f s" % (p50[phase], lats[-1]))
+        assert lats[-1] < 1.5, (phase, lats[-5:])
+        if phase != "none":
+            # a slow agent costs the others at most a small factor of the unloaded latency
+            assert p50[phase] < 3 * p50["none"] + 0.1, (phase, p50)
+            # every fast rank finished its queries before the slow rank's agent came back
+            assert max(r[phase]["done"] for r in g[:-1]) < slow[phase]["end"], phase

@@ -276,3 +276,30 @@ def test_camel_github_pull_request_comments():
         a.close()
     finally:
         srv.shutdown()
+
+
+def test_webcrawler_sustains_bench_step_rate(tmp_path):
+    """at 8 GPUs the config-4 bench's single rank-0 crawler must deliver
+    256 pages per step (32 per GPU).  Crawl one published step of the bench's own site
+    (``langstream_amd.bench.site``, in its own process as in bench.py) with the bench's
+    crawler configuration and require >= 128 pages/s on this CPU box."""
+    from langstream_amd.bench.site import SiteProcess
+    site = SiteProcess(256, 2000)
+    try:
+        site.publish(0)
+        a = _crawler(site.url, tmp_path, **{
+            "seed-urls": [site.url + "/step/0/index.html"], "handle-robots-file": False,
+            "max-unflushed-pages": 1000, "http-timeout": 60000})
+        pages, t0 = 0, time.perf_counter()
+        deadline = t0 + 30
+        while pages < 256 and time.perf_counter() < deadline:
+            recs = a.read()
+            pages += sum(1 for r in recs if not r.key().endswith("index.html"))
+            a.commit(recs)
+        dt = time.perf_counter() - t0
+        a.close()
+        assert pages == 256, pages
+        assert pages / dt >= 128, f"{pages / dt:.1f} pages/s"
+        print(f"crawler: {pages / dt:.1f} pages/s")
+    finally:
+        site.close()

@@ -314,9 +314,11 @@ def test_vector_sink_is_durable_by_default_in_its_state_dir(tmp_path):
         for i in range(5):
             a.write(SimpleRecord.of(f"k{i}", {"vec": [1.0, float(i), 0.0], "text": f"t{i}"})).result(10)
         a.close()
-        assert VectorStoreRegistry.persist_dir.startswith(str(tmp_path))
+        # only this sink's collection is bound to its state dir; no process-wide default
+        assert VectorStoreRegistry.persist_dir is None
+        assert VectorStoreRegistry._dir_of("durable").startswith(str(tmp_path))
+        assert VectorStoreRegistry._dir_of("other") is None
         VectorStoreRegistry.reset()                  # pod restart: in-memory state gone
-        VectorStoreRegistry.persist_dir = None
         agent()
         s = VectorStoreRegistry.get("durable", device="cpu")
         assert len(s) == 5 and s.get("k3") == {"text": "t3"}
@@ -332,3 +334,40 @@ def test_planner_gives_local_vector_sinks_a_disk():
                                                  configuration={"datasource": "LocalVectors"}))
     assert not _vector_sink_disks(AgentConfiguration(id="w", type="vector-db-sink",
                                                      configuration={"datasource": {"service": "opensearch"}}))
+
+
+def test_two_sinks_persist_in_their_own_state_dirs(tmp_path):
+    """ADVICE r3 / VERDICT r4: the first sink's state directory must not become the
+    persistence default of every other collection in the process."""
+    from langstream_amd.agents.vector import VectorDBSinkAgent
+    from langstream_amd.api.agent import AgentContext
+    from langstream_amd.api.record import SimpleRecord
+    VectorStoreRegistry.reset()
+    VectorStoreRegistry.persist_dir = None
+
+    def sink(agent_id, coll):
+        a = VectorDBSinkAgent()
+        a.set_metadata(agent_id, "vector-db-sink", 0)
+        a.init({"datasource": {"service": "local"}, "collection-name": coll,
+                "fields": [{"name": "id", "expression": "key"}, {"name": "vector", "expression": "value.vec"}]})
+        a.set_context(AgentContext(agent_id=agent_id, global_agent_id=f"app-{agent_id}",
+                                   persistent_state_directory=str(tmp_path / agent_id)))
+        a.start()
+        return a
+    try:
+        a, b = sink("s1", "c1"), sink("s2", "c2")
+        a.write(SimpleRecord.of("x", {"vec": [1.0, 0.0]})).result(10)
+        b.write(SimpleRecord.of("y", {"vec": [0.0, 1.0]})).result(10)
+        a.close()
+        b.close()
+        assert VectorStoreRegistry._dir_of("c1").startswith(str(tmp_path / "s1"))
+        assert VectorStoreRegistry._dir_of("c2").startswith(str(tmp_path / "s2"))
+        # a collection no sink owns is not persisted anywhere
+        assert not VectorStoreRegistry.get("scratch", 2, device="cpu").persistent
+        assert os.listdir(tmp_path / "s1" / "s1" / "vector-store") == ["c1"]
+        VectorStoreRegistry.reset()
+        sink("s2", "c2")
+        assert VectorStoreRegistry.get("c2", device="cpu").get("y") is not None
+        assert not VectorStoreRegistry.exists("c1")       # s1 has not restarted yet
+    finally:
+        VectorStoreRegistry.reset()
