@@ -114,8 +114,51 @@ class GenAIToolKitAgent(AgentProcessor):
     def process(self, records, sink) -> None:
         if self.step is None:
             self.start()
+        many = getattr(sink, "many", None)
+        bulk = getattr(self.step, "process_bulk", None)
+        if many is not None and bulk is not None and self.step.bulk_ok():
+            self._process_bulk(records, many, bulk)
+            return
         for r in records:
             self._process_one(r, sink)
+
+    def _process_bulk(self, records, many, bulk) -> None:
+        """The runner takes results in batches (``sink.many``) and the step completes
+        records in batches (compute-ai-embeddings): one result batch per completed
+        embedding batch instead of a future and a callback chain per record."""
+        now, pend = [], []
+        for r in records:
+            try:
+                mr = MutableRecord.from_record(r)
+                if not self.step.applies(mr):
+                    now.append(SourceRecordAndResult(r, [r], None))
+                    continue
+                pend.append((r, mr))
+            except Exception as e:  # noqa: BLE001
+                now.append(SourceRecordAndResult(r, None, e))
+        if now:
+            self.processed(len(now), sum(1 for x in now if x.error is None))
+            many(now)
+        if pend:
+            bulk(pend, lambda done: self._emit_bulk(done, many))
+
+    def _emit_bulk(self, done, many) -> None:
+        out = []
+        n_out = 0
+        for r, mr, err in done:
+            if err is not None:
+                out.append(SourceRecordAndResult(r, None, err))
+                continue
+            try:
+                rec = mr.to_record()
+            except Exception as e:  # noqa: BLE001
+                out.append(SourceRecordAndResult(r, None, e))
+                continue
+            if rec is not None:
+                n_out += 1
+            out.append(SourceRecordAndResult(r, [rec] if rec is not None else [], None))
+        self.processed(len(done), n_out)
+        many(out)
 
     def _process_one(self, r, sink) -> None:
         try:

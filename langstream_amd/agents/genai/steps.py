@@ -281,31 +281,75 @@ class ComputeAIEmbeddingsStep(Step):
         self.executor.add((rec, text, fut))
         return fut
 
+    def bulk_ok(self) -> bool:
+        return self.loop_over is None
+
+    def process_bulk(self, pairs, emit) -> None:
+        """(source record, MutableRecord) pairs -> ``emit([(source, mutable, error)])``
+        once per completed embedding batch, for every pair of it that came through this
+        call.  The same ordered batch executor (per-key order, batch-size, flush-interval,
+        concurrency) as ``process_async``: only the completion is reported in bulk."""
+        add = self.executor.add
+        render = self.template.render
+        for src, mr in pairs:
+            try:
+                text = render(mr.json_context())
+            except Exception as e:  # noqa: BLE001
+                emit([(src, mr, e)])
+                continue
+            add((mr, text, (src, emit)))
+
+    @staticmethod
+    def _complete(batch, err, set_field) -> None:
+        """Resolve every item of a batch: per-record futures (process_async) and bulk
+        tokens (process_bulk, one emit call per distinct emit)."""
+        groups = {}
+        for rec, _, tok in batch:
+            e = err
+            if e is None:
+                try:
+                    set_field(rec)
+                except Exception as ex:  # noqa: BLE001
+                    e = ex
+            if isinstance(tok, Future):
+                if e is None:
+                    tok.set_result(None)
+                else:
+                    tok.set_exception(e)
+            else:
+                src, emit = tok
+                g = groups.get(id(emit))
+                if g is None:
+                    g = groups[id(emit)] = (emit, [])
+                g[1].append((src, rec, e))
+        for emit, items in groups.values():
+            emit(items)
+
     def _process_batch(self, batch, batch_fut: Future) -> None:
         texts = [t for _, t, _ in batch]
         try:
             f = self.service.compute_embeddings(texts)
         except Exception as e:  # noqa: BLE001
-            for _, _, fut in batch:
-                fut.set_exception(e)
+            self._complete(batch, e, None)
             batch_fut.set_exception(e)
             return
 
         def done(ff: Future):
             err = ff.exception()
             if err is not None:
-                for _, _, fut in batch:
-                    fut.set_exception(err)
+                self._complete(batch, err, None)
                 batch_fut.set_exception(err)
                 return
-            embs = ff.result()
-            for (rec, _, fut), e in zip(batch, embs):
-                try:
-                    rec.set_result_field(e if isinstance(e, list) else list(e), self.field)
-                    fut.set_result(None)
-                except Exception as ex:  # noqa: BLE001
-                    fut.set_exception(ex)
-            batch_fut.set_result(None)
+            embs = iter(ff.result())
+            field = self.field
+
+            def set_field(rec):
+                e = next(embs)
+                rec.set_result_field(e if isinstance(e, list) else list(e), field)
+            try:
+                self._complete(batch, None, set_field)
+            finally:
+                batch_fut.set_result(None)
 
         f.add_done_callback(done)
 

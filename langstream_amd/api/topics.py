@@ -55,10 +55,40 @@ class TopicConsumer:
     def get_native_consumer(self): return None
 
 
+def all_of(futures: List[Future]) -> Future:
+    """One future for many: done when all are, failed with the first failure (in list
+    order) if any failed."""
+    out: Future = Future()
+    if not futures:
+        out.set_result(None)
+        return out
+    left = [len(futures)]
+    lock = threading.Lock()
+
+    def one(_f: Future) -> None:
+        with lock:
+            left[0] -= 1
+            last = left[0] == 0
+        if last:
+            err = next((f.exception() for f in futures if f.exception() is not None), None)
+            if err is not None:
+                out.set_exception(err)
+            else:
+                out.set_result(None)
+    for f in futures:
+        f.add_done_callback(one)
+    return out
+
+
 class TopicProducer:
     def start(self) -> None: ...
     def close(self) -> None: ...
     def write(self, record: Record) -> Future: raise NotImplementedError
+
+    def write_many(self, records: List[Record]) -> Future:
+        """Write records in order; one future for all of them (a runtime with a batching
+        client overrides this to queue them as one unit)."""
+        return all_of([self.write(r) for r in records])
     def get_info(self) -> Dict[str, Any]: return {}
     def get_total_in(self) -> int: return 0
     def get_native_producer(self): return None

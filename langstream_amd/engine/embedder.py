@@ -18,6 +18,7 @@ from typing import List, Optional, Sequence
 import torch
 
 from ..models.bert import BertEncoder
+from ..utils.fastjson import f32_rows
 from ..utils.gpu import on_aux, to_host
 
 log = logging.getLogger(__name__)
@@ -44,7 +45,7 @@ class EmbeddingEngine:
     def embed(self, texts: Sequence[str]) -> List[List[float]]:
         """Blocking; runs inline on the caller's thread (no engine thread needed)."""
         out = self._embed_batch(list(texts))
-        return out.tolist() if isinstance(out, torch.Tensor) else out
+        return f32_rows(out) if isinstance(out, torch.Tensor) else out
 
     def embed_tensor(self, texts: Sequence[str]) -> torch.Tensor:
         """Device tensor, produced on the device's auxiliary stream (consume it there,
@@ -132,7 +133,8 @@ class EmbeddingEngine:
                 for p_texts, fut in pending:
                     part = out[k: k + len(p_texts)]
                     k += len(p_texts)
-                    fut.set_result(part if self.return_tensors else part.tolist())
+                    # float32 rows: serialised at float32 precision (utils/fastjson.py)
+                    fut.set_result(part if self.return_tensors else f32_rows(part))
             except Exception as e:  # noqa: BLE001
                 log.exception("embedding batch failed")
                 for _, fut in pending:

@@ -35,6 +35,21 @@ from .tracker import SourceRecordTracker
 log = logging.getLogger(__name__)
 
 
+class _ResultSink:
+    """The callback a processor reports results through: ``sink(result)`` per record, or
+    ``sink.many(results)`` for a batch completed together."""
+    __slots__ = ("runner", "errors")
+
+    def __init__(self, runner: "AgentRunner", errors: StandardErrorsHandler):
+        self.runner, self.errors = runner, errors
+
+    def __call__(self, res: SourceRecordAndResult) -> None:
+        self.runner._on_processor_result(res, self.errors)
+
+    def many(self, results: List[SourceRecordAndResult]) -> None:
+        self.runner._on_processor_results(results, self.errors)
+
+
 # ---------------------------------------------------------------- default adapters
 class TopicConsumerSource(AgentSource):
     """Source reading from the agent's input topic; permanent failures go to the DLQ
@@ -91,6 +106,10 @@ class TopicProducerSink(AgentSink):
     def write(self, record: Record) -> Future:
         self.processed(1, 0)
         return self.producer.write(record)
+
+    def write_many(self, records: List[Record]) -> Future:
+        self.processed(len(records), 0)
+        return self.producer.write_many(records)
 
     def build_additional_info(self) -> Dict[str, Any]:
         return {"producer": self.producer.get_info()}
@@ -307,7 +326,48 @@ class AgentRunner:
 
     # -- processor results
     def _run_processor(self, records: List[Record], errors: StandardErrorsHandler) -> None:
-        self.processor.process(records, lambda res: self._on_processor_result(res, errors))
+        self.processor.process(records, _ResultSink(self, errors))
+
+    def _on_processor_results(self, results: List[SourceRecordAndResult], errors: StandardErrorsHandler) -> None:
+        """A batch of results at once (a processor that completes records in batches,
+        e.g. compute-ai-embeddings): one tracker update, ONE sink write of all the
+        result records (``write_many``) and one commit pass when it is acknowledged.
+        Errors and empty results take the per-record path; a failed batch write hands
+        every record to the per-record write-error handling (retry / skip / DLQ)."""
+        writer = getattr(self.sink, "write_many", None)
+        if writer is None or self.sink.handles_commit():
+            for r in results:
+                self._on_processor_result(r, errors)
+            return
+        ok = []
+        for r in results:
+            if r.error is None and r.result_records:
+                ok.append(r)
+            else:
+                self._on_processor_result(r, errors)
+        if not ok:
+            return
+        try:
+            self.tracker.track(ok)
+            recs = [rec for r in ok for rec in r.result_records]
+            fut = writer(recs)
+        except BaseException as e:  # noqa: BLE001
+            log.exception("Error while processing record")
+            self._set_fatal(RuntimeError(f"Error while processing records: {e!r}"))
+            return
+
+        def done(f: Future) -> None:
+            err = f.exception()
+            if err is None:
+                self.records_out += len(recs)
+                self.metrics.counter("sink_records_out", self.pod.agent_id).inc(len(recs))
+                self.tracker.commit(recs)
+                return
+            for r in ok:
+                for rec in r.result_records:
+                    self._on_write_error(rec, r.source_record, err, errors)
+
+        fut.add_done_callback(done)
 
     def _on_processor_result(self, res: SourceRecordAndResult, errors: StandardErrorsHandler) -> None:
         src = res.source_record
@@ -362,24 +422,27 @@ class AgentRunner:
                 self.metrics.counter("sink_records_out", self.pod.agent_id).inc()
                 self.tracker.commit([rec])
                 return
-            action = errors.handle_errors(src, err)
-            if action == Outcome.SKIP:
-                self.tracker.commit([rec])
-            elif action == Outcome.RETRY:
-                self._write(rec, src, errors)
-            else:
-                pfe = PermanentFailureException(err)
-                try:
-                    self.source.permanent_failure(src, pfe)
-                except BaseException as e2:  # noqa: BLE001
-                    self._set_fatal(e2)
-                    return
-                if errors.fail_processing_on_permanent_errors():
-                    self._set_fatal(pfe)
-                else:
-                    self.tracker.commit([rec])
+            self._on_write_error(rec, src, err, errors)
 
         fut.add_done_callback(done)
+
+    def _on_write_error(self, rec: Record, src: Record, err: BaseException, errors: StandardErrorsHandler) -> None:
+        action = errors.handle_errors(src, err)
+        if action == Outcome.SKIP:
+            self.tracker.commit([rec])
+        elif action == Outcome.RETRY:
+            self._write(rec, src, errors)
+        else:
+            pfe = PermanentFailureException(err)
+            try:
+                self.source.permanent_failure(src, pfe)
+            except BaseException as e2:  # noqa: BLE001
+                self._set_fatal(e2)
+                return
+            if errors.fail_processing_on_permanent_errors():
+                self._set_fatal(pfe)
+            else:
+                self.tracker.commit([rec])
 
     # ------------------------------------------------------------------ introspection
     def agent_info(self) -> List[Dict[str, Any]]:

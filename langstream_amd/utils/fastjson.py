@@ -1,7 +1,13 @@
 """``dumps(obj)``: ``json.dumps(obj)`` (default options) through the native encoder
 (``native/jsonenc.cpp``), byte-identical output; objects outside its type set fall back
 to ``json.dumps``.  Used where records are serialised onto topics -- an embeddings
-record's float vector costs ~0.7 us per float through ``json.dumps``."""
+record's float vector costs ~0.7 us per float through ``json.dumps``.
+
+``Float32List``: a list of floats that hold float32 values (a local model's embedding
+row).  The native encoder writes each with its shortest float32 digits (~9 significant
+digits instead of the ~17 a widened double needs): half the record bytes, a quarter of
+the formatting time, and the same float32 after parsing.  Everywhere else it is a plain
+list (json.dumps, msgpack, EL, the vector stores)."""
 from __future__ import annotations
 
 import json
@@ -11,12 +17,24 @@ _native = None
 _unsupported = None
 
 
+class Float32List(list):
+    """A list whose float items are float32 values (see the module docstring)."""
+    __slots__ = ()
+
+
+def f32_rows(t) -> list:
+    """Host float tensor / array [n, d] -> n Float32Lists."""
+    return [Float32List(r) for r in t.tolist()]
+
+
 def _load():
     global _native, _unsupported
     try:
         from ..native import lib
         m = lib()
         _native, _unsupported = m.json_dumps, m.JsonUnsupported
+        if hasattr(m, "json_register_f32list"):
+            m.json_register_f32list(Float32List)
     except Exception:  # noqa: BLE001  (no toolchain: plain json)
         _native, _unsupported = False, None
 

@@ -59,3 +59,27 @@ def test_kafka_native_records_match_python():
     native = list(P.decode_batches(batch, verify_crc=True))
     assert native == list(P._records_py(batch, 61, len(recs), 100, recs[0][3]))
     assert [(x[2], x[3], x[4]) for x in native] == [(r[0], r[1], [tuple(h) for h in r[2]]) for r in recs]
+
+
+def test_float32_vectors_use_float32_digits():
+    """A Float32List (a local model's embedding row) is written with the shortest float32
+    digits: json.dumps of the doubles those digits parse to, byte for byte, and every
+    value parses back to the same float32."""
+    import numpy as np
+    from langstream_amd.utils.fastjson import Float32List, f32_rows
+    rng = np.random.default_rng(3)
+    for scale in (1e-30, 1e-6, 0.05, 1.0, 3e4, 1e15, 1e30):
+        v = (rng.standard_normal(512) * scale).astype(np.float32)
+        v[:6] = [0.0, -0.0, 1.0, -2.5, 1e-45, 123456790000000.0]
+        got = fastjson.dumps({"e": Float32List(v.astype(np.float64).tolist()), "k": 1})
+        want = json.dumps({"e": [float(str(np.float32(x))) for x in v], "k": 1})
+        assert got == want
+        assert np.array_equal(np.array(json.loads(got)["e"], dtype=np.float32), v)
+    rows = f32_rows(np.ones((2, 3), dtype=np.float32))
+    assert [type(r) for r in rows] == [Float32List, Float32List] and rows[0] == [1.0, 1.0, 1.0]
+    # anything but floats inside: the generic encoder, same bytes as json.dumps
+    mixed = Float32List([1, 0.5, None])
+    assert fastjson.dumps(mixed) == json.dumps(mixed)
+    # plain lists keep the double digits
+    x = float(np.float32(0.1))
+    assert fastjson.dumps([x]) == json.dumps([x]) and fastjson.dumps(Float32List([x])) == "[0.1]"

@@ -199,3 +199,43 @@ instance:
         app.stop(20)
         b.stop()
     assert all(p.proc.returncode == 0 for p in app.processes)
+
+
+def test_producer_write_many_one_future(broker):
+    """``KafkaProducer.write_many``: one future for a group of records spanning several
+    produce requests (> MAX_BATCH_RECORDS); order kept per partition; interleaves with
+    single writes; a serialisation error queues nothing."""
+    from langstream_amd.api.record import SimpleRecord
+    from langstream_amd.topics.kafka import KafkaProducer
+    c = KafkaClient(broker.bootstrap)
+    t = "wm-" + uuid.uuid4().hex[:6]
+    c.create_topic(t, 1)
+    prod = KafkaProducer(broker.bootstrap, t)
+    n = KafkaProducer.MAX_BATCH_RECORDS * 2 + 345
+    single = prod.write(SimpleRecord.of("s0", "first"))
+    f = prod.write_many([SimpleRecord.of(f"k{i}", json.dumps({"i": i, "pad": "x" * 300})) for i in range(n)])
+    last = prod.write(SimpleRecord.of("s1", "last"))
+    f.result(60)
+    single.result(60)
+    last.result(60)
+
+    class Bad:
+        def __init__(self):
+            pass
+    bad = prod.write_many([SimpleRecord.of("ok", "x"), SimpleRecord.of("bad", Bad())])
+    with pytest.raises(Exception):
+        bad.result(10)
+    assert prod.write_many([]).result(1) is None
+    prod.flush()
+    got = []
+    r = PartitionReader(c, t, start="earliest")
+    while len(got) < n + 2:
+        recs = r.read(500)
+        assert recs
+        got.extend(recs)
+    vals = [v.decode() for _, _, _, _, v, _ in got]
+    assert vals[0] == "first" and vals[-1] == "last" and len(got) == n + 2
+    assert [json.loads(v)["i"] for v in vals[1:-1]] == list(range(n))
+    prod.close()
+    c.delete_topic(t)
+    c.close()

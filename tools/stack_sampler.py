@@ -2,7 +2,10 @@
 stack every few ms (cProfile only sees the thread it runs in).  Prints the hottest leaf
 lines and inclusive functions.
 
-usage: python tools/stack_sampler.py [--every-ms 2] [--top 40] -- script.py args...
+usage: python tools/stack_sampler.py [--every-ms 2] [--top 40] [--thread PREFIX] -- script.py args...
+
+--thread PREFIX: only threads whose name starts with PREFIX, leaves keyed by their last
+three frames (where that thread spends its wall time, waits included).
 """
 import collections
 import os
@@ -16,7 +19,12 @@ import traceback
 def main():
     argv = sys.argv[1:]
     every, top = 0.002, 40
+    only = None
     while argv and argv[0] != "--":
+        if argv[0] == "--thread":
+            only = argv[1]
+            argv = argv[2:]
+            continue
         if argv[0] == "--every-ms":
             every = float(argv[1]) / 1000.0
             argv = argv[2:]
@@ -40,11 +48,15 @@ def main():
             for tid, fr in sys._current_frames().items():
                 if tid == me:
                     continue
+                if only is not None and not names.get(tid, "").startswith(only):
+                    continue
                 st = traceback.extract_stack(fr)
                 if not st:
                     continue
                 f = st[-1]
                 key = f"{os.path.basename(f.filename)}:{f.lineno}:{f.name}"
+                if only is not None:
+                    key = " < ".join(f"{os.path.basename(g.filename)}:{g.lineno}:{g.name}" for g in st[-3:][::-1])
                 leaf[key] += 1
                 # a thread parked in a wait / socket read / select is idle
                 if not any(s in key for s in ("wait", "_recv_exact", "select", "sleep", "get", "accept")):

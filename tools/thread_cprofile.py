@@ -2,7 +2,10 @@
 threading.Thread.run so each thread profiles itself, merges all threads' stats at
 exit and prints the top functions by own time and by cumulative time.
 
-usage: python tools/thread_cprofile.py [--top 50] -- script.py args...
+usage: python tools/thread_cprofile.py [--top 50] [--cpu] -- script.py args...
+
+--cpu times with each thread's CPU clock (time.thread_time) instead of wall time, so a
+thread waiting for the GIL or a lock is not charged for it.
 """
 import cProfile
 import os
@@ -20,12 +23,16 @@ def main():
     top = 50
     if argv[:1] == ["--top"]:
         top, argv = int(argv[1]), argv[2:]
+    timer = []
+    if argv[:1] == ["--cpu"]:
+        import time
+        timer, argv = [time.thread_time], argv[1:]
     if argv[:1] == ["--"]:
         argv = argv[1:]
     orig_run = threading.Thread.run
 
     def run(self):
-        pr = cProfile.Profile()
+        pr = cProfile.Profile(*timer)
         with _lock:
             _profiles.append(pr)
         pr.enable()
@@ -35,7 +42,7 @@ def main():
             pr.disable()
 
     threading.Thread.run = run
-    main_pr = cProfile.Profile()
+    main_pr = cProfile.Profile(*timer)
     _profiles.append(main_pr)
     sys.argv = argv
     sys.path.insert(0, os.path.dirname(os.path.abspath(argv[0])))
