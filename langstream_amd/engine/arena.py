@@ -22,8 +22,9 @@ from .. import ops
 from ..models.llama import AttnMeta
 
 # header words (must match enum Hdr in runner.hip)
-H_KIND, H_T, H_ND, H_NPS, H_NTILES, H_NROWS, H_NGATHER, H_NDELTA, H_NTOP, H_BUCKET, H_ROWS_ALL = range(11)
+H_KIND, H_T, H_ND, H_NPS, H_NTILES, H_NROWS, H_NGATHER, H_NDELTA, H_NTOP, H_BUCKET, H_ROWS_ALL, H_NCOPY = range(12)
 KIND_STEP, KIND_STOP, KIND_CAPTURE = 1, 3, 4
+MAX_KV_COPIES = 2048   # KV block copies a step can carry (kMaxKvCopies in runner.hip)
 MAX_TOP = 32
 _ALIGN = 256
 
@@ -49,7 +50,8 @@ class ArenaLayout:
                 ("ctx_len", np.int32, (S,)), ("tiles", np.int32, (max_tiles, 2)), ("rows", np.int64, (S,)),
                 ("gdst", np.int64, (S,)), ("gsrc", np.int64, (S,)), ("temp", np.float32, (S,)),
                 ("top_p", np.float32, (S,)), ("top_k", np.int32, (S,)), ("seeds", np.int64, (S,)),
-                ("steps", np.int64, (S,)), ("deltas", np.int32, (max_deltas, 3))]
+                ("steps", np.int64, (S,)), ("kvcopy", np.int32, (MAX_KV_COPIES, 2)),
+                ("deltas", np.int32, (max_deltas, 3))]
         off, fields, cur = {}, {}, 0
         for name, dt, shape in spec:
             cur = (cur + _ALIGN - 1) // _ALIGN * _ALIGN
@@ -182,6 +184,13 @@ class PyStepExecutor:
     def _run(self, out: Optional[Dict[str, np.ndarray]]) -> None:
         a = self._av
         h = a["hdr"]
+        nc = int(h[H_NCOPY])
+        if nc:   # prefix-cache KV block copies, ahead of the forward (runner.hip run())
+            src = torch.from_numpy(a["kvcopy"][:nc, 0].astype(np.int64)).to(self.device)
+            dst = torch.from_numpy(a["kvcopy"][:nc, 1].astype(np.int64)).to(self.device)
+            for kc, vc in self.kv:
+                kc[dst] = kc[src]
+                vc[dst] = vc[src]
         T, nd, nps, ntiles, nrows = (int(h[i]) for i in (H_T, H_ND, H_NPS, H_NTILES, H_NROWS))
         ng, ndl, ntop, bucket = int(h[H_NGATHER]), int(h[H_NDELTA]), int(h[H_NTOP]), int(h[H_BUCKET])
         ids = a["ids"][:T].copy()

@@ -25,6 +25,8 @@ engine:
 * sampling on device (temperature / top-k / top-p / seed / penalties / logit-bias,
   log-probs of the sampled token + top-n alternatives for FLARE);
 * recompute-preemption when KV blocks run out;
+* automatic prefix KV reuse (``engine/prefix_cache.py``): prompts that share a template
+  prefix start their prefill after it, its KV copied from a cached copy;
 * tensor parallel: rank 0 schedules; its executor broadcasts the device arena over
   RCCL and the other ranks' executors (``worker_loop``, pure C++) mirror every step.
 """
@@ -47,8 +49,9 @@ import torch.distributed as dist
 from .. import ops
 from ..models.llama import LlamaModel
 from ..native import lib
-from .arena import (H_BUCKET, H_KIND, H_ND, H_NDELTA, H_NGATHER, H_NPS, H_NROWS, H_NTILES, H_NTOP, H_ROWS_ALL,
-                    H_T, KIND_STEP, ArenaLayout, NativeStepExecutor, PyStepExecutor)
+from .prefix_cache import PrefixCache
+from .arena import (H_BUCKET, H_KIND, H_ND, H_NCOPY, H_NDELTA, H_NGATHER, H_NPS, H_NROWS, H_NTILES, H_NTOP,
+                    H_ROWS_ALL, H_T, KIND_STEP, MAX_KV_COPIES, ArenaLayout, NativeStepExecutor, PyStepExecutor)
 
 log = logging.getLogger(__name__)
 BLOCK = ops.KV_BLOCK
@@ -163,7 +166,7 @@ class LLMEngine:
     def __init__(self, model: LlamaModel, tokenizer=None, *, num_blocks: Optional[int] = None,
                  kv_fraction: float = 0.55, max_model_len: int = 4096, max_batch: int = 256,
                  max_prefill_tokens: int = 8192, use_graphs: bool = True, graph_buckets: Sequence[int] = (),
-                 lookahead: bool = True, device=None):
+                 lookahead: bool = True, device=None, prefix_cache: Optional[bool] = None):
         self.model = model
         self.cfg = model.cfg
         self.tok = tokenizer
@@ -197,6 +200,10 @@ class LLMEngine:
             self.kv_caches.append(ops.new_kv_cache(self.num_blocks, hkv, D, self.device, model.dtype))
         self.allocator = lib().BlockAllocator(self.num_blocks)
         self.nsplit, self.bps = ops.decode_splits(self.max_blocks_per_seq)
+        if prefix_cache is None:
+            prefix_cache = os.environ.get("LS_PREFIX_CACHE", "1") != "0"
+        self.prefix: Optional[PrefixCache] = (PrefixCache(self.allocator, BLOCK, max_copies=MAX_KV_COPIES)
+                                              if prefix_cache else None)
         # ---- step arena + executor
         G = model.hq // model.hkv
         max_tokens = max_prefill_tokens + max_batch
@@ -222,7 +229,7 @@ class LLMEngine:
         self.ttft_s: collections.deque = collections.deque(maxlen=4096)   # engine-side arrival -> first token
         self.stats = {"prefill_steps": 0, "decode_steps": 0, "mixed_steps": 0, "prefill_tokens": 0,
                       "decode_tokens": 0, "preemptions": 0, "requests": 0, "finished": 0, "graph_steps": 0,
-                      "host_ms": 0.0, "wait_ms": 0.0, "launch_ms": 0.0, "retire_ms": 0.0}
+                      "host_ms": 0.0, "wait_ms": 0.0, "launch_ms": 0.0, "retire_ms": 0.0, "prefix_hit_tokens": 0}
         # prompt lengths of the most recent requests (decode attention cost follows the longest context)
         self.prompt_lens: collections.deque = collections.deque(maxlen=8192)
         # wall-clock (time.time) times at which requests reached the scheduler
@@ -333,6 +340,8 @@ class LLMEngine:
             except queue.Empty:
                 break
             self.waiting.append(r)
+            if self.prefix is not None:
+                self.prefix.observe(r)
             self.stats["requests"] += 1
             self.prompt_lens.append(len(r.prompt_ids))
             self.arrival_log.append(time.time())
@@ -349,6 +358,9 @@ class LLMEngine:
         if not decode and not chunks:
             self._flush()
             return
+        if self.prefix is not None and self.prefix.pending:
+            # a capture's block copies make this step an eager one (graphs carry no copies)
+            self.prefix.collect_captures(self._step_id + 1)
         launched = self._launch(decode, chunks)
         prev, self._inflight = self._inflight, launched
         self.stats["host_ms"] += (time.perf_counter() - t0) * 1000
@@ -413,10 +425,28 @@ class LLMEngine:
                 self.waiting.pop(0)
                 continue
             total = r.num_tokens
-            remaining = total - r.num_computed
+            # a fresh prompt whose prefix is cached starts after it (KV copied in this step)
+            hit, entry = (self.prefix.hit(r, self._step_id + 1)
+                          if self.prefix is not None and r.num_computed == 0 and not r.blocks else (0, None))
+            base = r.num_computed + hit
+            remaining = total - base
             n = min(remaining, budget)
-            need = self._blocks_needed(r, r.num_computed + n)
+            need = self._blocks_needed(r, base + n)
             headroom = n_decode  # let every decoding sequence grow by one more block
+            if hit and self.allocator.can_allocate(need + headroom):
+                r.num_computed = base
+                r.blocks += self.allocator.allocate(need)
+                self.prefix.apply_hit(r, entry, self._step_id + 1)
+                chosen.append((r, n))
+                budget -= n
+                if n < remaining:
+                    break
+                self.waiting.pop(0)
+                continue
+            if hit:   # no room with the hit: the plain path decides (it may trim or stop)
+                remaining = total - r.num_computed
+                n = min(remaining, budget)
+                need = self._blocks_needed(r, r.num_computed + n)
             if not self.allocator.can_allocate(need + headroom):
                 if not chosen and not self.running:
                     fit = (self.allocator.num_free() + len(r.blocks)) * BLOCK - r.num_computed
@@ -485,7 +515,8 @@ class LLMEngine:
         nrows = len(sample_reqs)
         n_top = min(max((r.params.logprobs for r in sample_reqs), default=0), 20)
         B = 0
-        if npf == 0 and self.use_graphs and nd <= self.buckets[-1] and n_top == 0:
+        copies = self.prefix is not None and bool(self.prefix.copies)
+        if npf == 0 and self.use_graphs and nd <= self.buckets[-1] and n_top == 0 and not copies:
             B = self._bucket(nd)
             if not self.exec.has_graph(B):
                 self._flush()  # capture reuses the token-feedback buffer
@@ -578,6 +609,12 @@ class LLMEngine:
         h[H_NTOP] = n_top
         h[H_BUCKET] = B
         h[H_ROWS_ALL] = 1 if rows_all else 0
+        if self.prefix is not None and self.prefix.copies:
+            assert B == 0, "KV block copies ride with eager (prefill) steps"
+            cp = self.prefix.take_copies()
+            a["kvcopy"][: len(cp)] = cp
+            h[H_NCOPY] = len(cp)
+            self.stats["prefix_hit_tokens"] = self.prefix.stats["hit_tokens"]
         # ---- advance host state (KV of these tokens is being written by this step)
         for r in decode:
             r.num_computed += 1

@@ -1,0 +1,156 @@
+"""Automatic prefix KV reuse for the LLM engine (exact: the reused KV is bit-for-bit what
+the prompt's own prefill would write for those positions, up to kernel routing).
+
+Prompts built from one template share a token prefix -- the RAG chain's chat template
+and system message are ~45 of a ~350-token prompt in the config-4 bench (bench.py APP)
+-- and a prefix's KV depends only on the prefix (causal attention, absolute RoPE
+positions).  This cache keeps the KV of such prefixes in blocks of its own and starts a
+new prompt's prefill at the end of its longest cached prefix, after copying those
+blocks into the prompt's own blocks (copy, not share: the prompt's first partial block
+receives its own tokens after the prefix).
+
+* Discovery: a new prompt is compared with the heads of the last ``history`` prompts;
+  a common prefix of at least ``min_len`` tokens (and ``min_gain`` longer than what the
+  cache already holds for it) is captured from this request once its prefill has
+  passed it.
+* Capture and reuse are KV block copies that ride in the NEXT step's arena
+  (``kvcopy``, executed before that step's forward on the step stream --
+  ``StepExecutor::run`` / ``PyStepExecutor._run``), so they are ordered after the step
+  that computed the prefix and before any step that reads them, and under tensor
+  parallelism every rank performs them (the arena is broadcast).
+* At most ``max_entries`` prefixes (LRU); an entry is never evicted in a step that reads
+  it, so its blocks are never rewritten before the copies that read them ran.
+
+The vLLM / SGLang production engines do the same (block-hash / radix-tree prefix
+caching); the reference delegates generation to remote services (OpenAI prompt caching,
+OpenAICompletionService.java:122-404).  ``LS_PREFIX_CACHE=0`` disables it.
+"""
+from __future__ import annotations
+
+import collections
+from typing import Dict, List, Optional, Tuple
+
+import numpy as np
+
+
+class _Entry:
+    __slots__ = ("ids", "blocks", "last_step", "hits")
+
+    def __init__(self, ids: np.ndarray, blocks: List[int], step: int):
+        self.ids, self.blocks, self.last_step, self.hits = ids, blocks, step, 0
+
+
+class PrefixCache:
+    def __init__(self, allocator, block: int, max_entries: int = 8, min_len: int = 32, max_len: int = 512,
+                 history: int = 32, min_gain: int = 16, max_copies: int = 2048):
+        self.allocator, self.block = allocator, block
+        self.max_entries, self.min_len, self.max_len = max_entries, min_len, max_len
+        self.min_gain, self.max_copies = min_gain, max_copies
+        self.entries: List[_Entry] = []
+        self.recent: collections.deque = collections.deque(maxlen=history)
+        self.pending: List[Tuple[object, int]] = []      # (request, prefix length) to capture
+        self.copies: List[Tuple[int, int]] = []          # (src, dst) block pairs for the next step
+        self.stats: Dict[str, int] = {"hit_tokens": 0, "hits": 0, "captures": 0, "evictions": 0}
+
+    # -------------------------------------------------------------- lookups
+    def _head(self, r) -> np.ndarray:
+        h = getattr(r, "_prefix_head", None)
+        if h is None:
+            h = np.asarray(r.prompt_ids[: self.max_len], dtype=np.int64)
+            r._prefix_head = h
+        return h
+
+    def _best(self, head: np.ndarray, n_prompt: int) -> Optional[_Entry]:
+        best = None
+        for e in self.entries:
+            L = len(e.ids)
+            if L < n_prompt and L <= len(head) and (best is None or L > len(best.ids)) \
+                    and np.array_equal(head[:L], e.ids):
+                best = e
+        return best
+
+    def observe(self, r) -> None:
+        """A request reached the scheduler: look for a shared prefix worth capturing."""
+        head = self._head(r)
+        n = len(r.prompt_ids)
+        lcp = 0
+        for h in self.recent:
+            m = min(len(h), len(head), n - 1)
+            if m <= lcp:
+                continue
+            neq = np.flatnonzero(h[:m] != head[:m])
+            lcp = max(lcp, int(neq[0]) if len(neq) else m)
+        self.recent.append(head)
+        if lcp < self.min_len:
+            return
+        have = self._best(head, n)
+        if have is not None and lcp < len(have.ids) + self.min_gain:
+            return
+        if any(L >= lcp and np.array_equal(self._head(q)[:lcp], head[:lcp]) for q, L in self.pending):
+            return
+        self.pending.append((r, lcp))
+
+    def hit(self, r, step: int) -> Tuple[int, Optional[_Entry]]:
+        """Longest cached prefix of a fresh request's prompt: (length, entry) or (0, None)."""
+        e = self._best(self._head(r), len(r.prompt_ids))
+        if e is None:
+            return 0, None
+        nb = (len(e.ids) + self.block - 1) // self.block
+        if len(self.copies) + nb > self.max_copies:
+            return 0, None
+        return len(e.ids), e
+
+    def apply_hit(self, r, e: _Entry, step: int) -> None:
+        """The request took entry e (its blocks are allocated): queue the block copies."""
+        nb = (len(e.ids) + self.block - 1) // self.block
+        self.copies.extend(zip(e.blocks[:nb], r.blocks[:nb]))
+        e.last_step = step
+        e.hits += 1
+        self.stats["hits"] += 1
+        self.stats["hit_tokens"] += len(e.ids)
+
+    # -------------------------------------------------------------- captures
+    def collect_captures(self, step: int) -> None:
+        """Capture every pending prefix whose request has computed past it (its KV is
+        written by an earlier step); requests that finished or lost their blocks drop."""
+        keep = []
+        for r, L in self.pending:
+            if getattr(r, "finished", False):
+                continue
+            nb = (L + self.block - 1) // self.block
+            if r.num_computed < L or len(r.blocks) < nb:   # not there yet (or preempted)
+                keep.append((r, L))
+                continue
+            if len(self.copies) + nb > self.max_copies:
+                keep.append((r, L))
+                continue
+            if len(self.entries) >= self.max_entries and not self._evict(step):
+                continue
+            if not self.allocator.can_allocate(nb):
+                continue
+            dst = list(self.allocator.allocate(nb))
+            self.copies.extend(zip(r.blocks[:nb], dst))
+            self.entries.append(_Entry(self._head(r)[:L].copy(), dst, step))
+            self.stats["captures"] += 1
+        self.pending = keep
+
+    def _evict(self, step: int) -> bool:
+        cands = [e for e in self.entries if e.last_step != step]
+        if not cands:
+            return False
+        e = min(cands, key=lambda x: x.last_step)
+        self.entries.remove(e)
+        self.allocator.free(e.blocks)
+        self.stats["evictions"] += 1
+        return True
+
+    def take_copies(self) -> List[Tuple[int, int]]:
+        c, self.copies = self.copies, []
+        return c
+
+    def clear(self) -> None:
+        for e in self.entries:
+            self.allocator.free(e.blocks)
+        self.entries.clear()
+        self.pending.clear()
+        self.copies.clear()

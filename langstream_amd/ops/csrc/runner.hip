@@ -163,6 +163,20 @@ void rows_rms_scale(at::Tensor out, at::Tensor y, at::Tensor sumsq, double eps);
 
 namespace {
 
+// Prefix KV reuse (engine/llm_engine.py PrefixCache): copy whole KV blocks (src -> dst
+// pairs) in every layer's K and V cache.  grid = (pairs, 2 x layers); tab[t] is the base
+// of cache tensor t ([NB, ...], block_bytes per block).  Pairs outside [0, NB) are skipped.
+__global__ void __launch_bounds__(256) kv_block_copy_kernel(const int64_t* __restrict__ tab,
+                                                             const int32_t* __restrict__ pairs, int64_t nb,
+                                                             int64_t block_bytes) {
+  const int32_t s = pairs[2 * blockIdx.x], d = pairs[2 * blockIdx.x + 1];
+  if (s < 0 || d < 0 || s >= nb || d >= nb || s == d) return;
+  char* base = reinterpret_cast<char*>(tab[blockIdx.y]);
+  const uint4* src = reinterpret_cast<const uint4*>(base + (int64_t)s * block_bytes);
+  uint4* dst = reinterpret_cast<uint4*>(base + (int64_t)d * block_bytes);
+  for (int64_t i = threadIdx.x; i < block_bytes / 16; i += 256) dst[i] = src[i];
+}
+
 // ---------------------------------------------------------------------------- Llama
 class LlamaRunner {
  public:
@@ -233,6 +247,29 @@ class LlamaRunner {
         cnt_down_ = at::zeros({maxt}, dev.dtype(at::kLong));
       }
     }
+  }
+
+  // Copy `n` KV blocks (int32 (src, dst) pairs on the device) in every layer's K and V
+  // cache, on the current stream: the prefix-cache copies a step carries ahead of its
+  // forward (StepExecutor::run).
+  void copy_kv_blocks(const int32_t* pairs, int64_t n) {
+    if (n <= 0) return;
+    if (!kv_tab_.defined()) {
+      std::vector<int64_t> ptrs;
+      for (size_t l = 0; l < kc_.size(); ++l) {
+        TORCH_CHECK(kc_[l].is_contiguous() && vc_[l].is_contiguous() && kc_[l].size(0) == kc_[0].size(0) &&
+                    vc_[l].size(0) == kc_[0].size(0) && kc_[l][0].numel() == vc_[l][0].numel(),
+                    "KV caches: contiguous, one block count, K and V blocks of one size");
+        ptrs.push_back(reinterpret_cast<int64_t>(kc_[l].data_ptr()));
+        ptrs.push_back(reinterpret_cast<int64_t>(vc_[l].data_ptr()));
+      }
+      kv_tab_ = at::tensor(ptrs, at::TensorOptions().dtype(at::kLong)).to(embed_.device());
+      kv_block_bytes_ = kc_[0][0].numel() * kc_[0].element_size();
+      TORCH_CHECK(kv_block_bytes_ % 16 == 0);
+    }
+    kv_block_copy_kernel<<<dim3((unsigned)n, (unsigned)kv_tab_.numel()), 256, 0,
+                           at::hip::getCurrentHIPStream()>>>(kv_tab_.data_ptr<int64_t>(), pairs, kc_[0].size(0),
+                                                             kv_block_bytes_);
   }
 
   // Device int32 words that are 0 unless a step's results are invalid: [0] the gate_up
@@ -763,6 +800,8 @@ class LlamaRunner {
   std::vector<at::Tensor> qkv_w_, o_w_, gate_up_w_, down_w_, in_norm_, post_norm_;
   at::Tensor final_norm_, lm_head_;
   std::vector<at::Tensor> kc_, vc_;
+  at::Tensor kv_tab_;          // device [2 L] base pointers of the K / V caches (copy_kv_blocks)
+  int64_t kv_block_bytes_ = 0;
   at::Tensor cos_sin_;
   int64_t hq_, hkv_, d_;
   double eps_, scale_;
@@ -878,8 +917,10 @@ enum Hdr : int {
   H_NDELTA = 7,   // logit deltas (penalties / bias / min-tokens)
   H_NTOP = 8,     // top logprobs per row
   H_BUCKET = 9,   // >0: decode-only step replayed from the bucket's graph
-  H_ROWS_ALL = 10 // 1: sample every row (rows == arange(T))
+  H_ROWS_ALL = 10, // 1: sample every row (rows == arange(T))
+  H_NCOPY = 11    // KV block copies (prefix cache) ahead of the forward: kvcopy[0, n)
 };
+constexpr int kMaxKvCopies = 2048;   // must match MAX_KV_COPIES in engine/arena.py
 
 // ids[gdst[i]] = tok_prev[gsrc[i]] for i < hdr[H_NGATHER]; count read on the device.
 __global__ void gather_feedback_kernel(int32_t* __restrict__ ids, const int64_t* __restrict__ gdst,
@@ -916,7 +957,7 @@ class StepExecutor {
         nsplit_(nsplit), bps_(bps), use_graphs_(use_graphs) {
     static const char* need[] = {"hdr", "ids", "pos", "slots", "dbt", "dctx", "pbt", "q_start", "q_len", "ctx_len",
                                  "tiles", "rows", "gdst", "gsrc", "temp", "top_p", "top_k", "seeds", "steps",
-                                 "deltas"};
+                                 "kvcopy", "deltas"};
     for (const char* k : need) TORCH_CHECK(off_.count(k), "arena layout lacks ", k);
     auto dev = at::TensorOptions().device(at::kCUDA, device);
     auto pin = at::TensorOptions().dtype(at::kByte).pinned_memory(true);
@@ -1157,6 +1198,8 @@ class StepExecutor {
       TORCH_CHECK(h[H_T] == h[H_ND] && h[H_ND] <= h[H_BUCKET] && h[H_NPS] == 0 && h[H_NTOP] == 0,
                   "graph steps are decode-only");
     TORCH_CHECK(h[H_NPS] == 0 || h[H_T] > h[H_ND], "prefill sequences without prefill tokens");
+    TORCH_CHECK(h[H_NCOPY] >= 0 && h[H_NCOPY] <= kMaxKvCopies && (h[H_BUCKET] == 0 || h[H_NCOPY] == 0),
+                "KV block copies out of range (or on a graph step)");
   }
 
   void upload(int64_t slot) {
@@ -1246,6 +1289,8 @@ class StepExecutor {
   }
 
   void run(const int32_t* h) {
+    if (h[H_NCOPY] > 0)
+      r_->copy_kv_blocks(reinterpret_cast<const int32_t*>((char*)arena_.data_ptr() + off_.at("kvcopy")), h[H_NCOPY]);
     const int64_t B = h[H_BUCKET];
     if (B > 0) {
       auto it = graphs_.find(B);

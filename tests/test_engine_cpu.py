@@ -40,6 +40,10 @@ def _greedy_reference(model, prompt, n):
     return out
 
 
+def _prefix_blocks(eng):
+    return sum(len(e.blocks) for e in eng.prefix.entries) if eng.prefix is not None else 0
+
+
 def test_greedy_matches_full_recompute(model):
     prompts = [list(range(3, 3 + n)) for n in (5, 64, 65, 130)]
     sp = SamplingParams(max_tokens=8, temperature=0.0, ignore_eos=True)
@@ -48,7 +52,8 @@ def test_greedy_matches_full_recompute(model):
     for p, g in zip(prompts, got):
         assert g == _greedy_reference(model, p, 8)
     assert eng.stats["finished"] == 4
-    assert eng.allocator.num_free() == 64  # every block returned
+    # every block returned (the prefix cache keeps its captured prefixes' blocks)
+    assert eng.allocator.num_free() + _prefix_blocks(eng) == 64
 
 
 def test_lookahead_equals_synchronous(model):
@@ -149,3 +154,61 @@ def test_full_prefill_steps_are_256_aligned(model):
     assert full and all(t % 256 == 0 for t in full), list(eng.prefill_step_tokens)
     ref = LLMEngine(model, None, num_blocks=256, max_model_len=2048, max_batch=16, max_prefill_tokens=333)
     assert [r.output_ids for r in reqs] == [r.output_ids for r in ref.generate(prompts, sp)]
+
+
+def _shared_prefix_prompts(n=8, plen=70, seed=5):
+    rng = np.random.default_rng(seed)
+    head = rng.integers(3, 250, plen).tolist()
+    return [head + rng.integers(3, 250, int(rng.integers(8, 60))).tolist() for _ in range(n)]
+
+
+def test_prefix_cache_is_exact_and_hits(model):
+    """Prompts sharing a 70-token template prefix: with the prefix cache the later prompts
+    start their prefill after the cached prefix (KV block copies in the step arena) and
+    the greedy outputs equal both the cache-off engine and the full-recompute reference."""
+    prompts = _shared_prefix_prompts()
+    sp = SamplingParams(max_tokens=6, temperature=0.0, ignore_eos=True)
+    on = LLMEngine(model, None, num_blocks=96, max_model_len=512, max_batch=8, max_prefill_tokens=96,
+                   prefix_cache=True)
+    off = LLMEngine(model, None, num_blocks=96, max_model_len=512, max_batch=8, max_prefill_tokens=96,
+                    prefix_cache=False)
+    a = [r.output_ids for r in on.generate(prompts, sp)]
+    b = [r.output_ids for r in off.generate(prompts, sp)]
+    assert a == b
+    assert a[0] == _greedy_reference(model, prompts[0], 6) and a[-1] == _greedy_reference(model, prompts[-1], 6)
+    st = on.prefix.stats
+    assert st["captures"] >= 1 and st["hits"] >= 3 and on.stats["prefix_hit_tokens"] >= 3 * 64
+    # fewer tokens prefilled by exactly the reused ones
+    assert off.stats["prefill_tokens"] - on.stats["prefill_tokens"] == on.stats["prefix_hit_tokens"]
+    assert on.allocator.num_free() + _prefix_blocks(on) == 96 and off.allocator.num_free() == 96
+
+
+def test_prefix_cache_sampled_and_preempted(model):
+    """Seeded sampling and recompute-preemption under block pressure: the same tokens
+    with and without the cache (a preempted request re-enters through the cache)."""
+    prompts = _shared_prefix_prompts(n=10, plen=80, seed=9)
+    sp = SamplingParams(max_tokens=24, temperature=0.9, top_k=30, seed=4, ignore_eos=True)
+    kw = dict(num_blocks=24, max_model_len=512, max_batch=8, max_prefill_tokens=128)
+    on = LLMEngine(model, None, prefix_cache=True, **kw)
+    off = LLMEngine(model, None, prefix_cache=False, **kw)
+    assert [r.output_ids for r in on.generate(prompts, sp)] == [r.output_ids for r in off.generate(prompts, sp)]
+    assert on.prefix.stats["hits"] >= 1
+    assert on.allocator.num_free() + _prefix_blocks(on) == 24
+
+
+def test_prefix_cache_lru_bound(model):
+    """Many distinct template prefixes: at most max_entries are kept (LRU), the rest are
+    evicted and their blocks returned."""
+    rng = np.random.default_rng(2)
+    prompts = []
+    for g in range(12):
+        head = rng.integers(3, 250, 40).tolist()
+        prompts += [head + rng.integers(3, 250, 10).tolist() for _ in range(2)]
+    sp = SamplingParams(max_tokens=2, temperature=0.0, ignore_eos=True)
+    eng = LLMEngine(model, None, num_blocks=128, max_model_len=512, max_batch=4, max_prefill_tokens=64,
+                    prefix_cache=True)
+    eng.prefix.max_entries = 3
+    for i in range(0, len(prompts), 2):
+        eng.generate(prompts[i:i + 2], sp)
+    assert len(eng.prefix.entries) <= 3 and eng.prefix.stats["evictions"] >= 1
+    assert eng.allocator.num_free() + _prefix_blocks(eng) == 128
