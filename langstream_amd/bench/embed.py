@@ -115,9 +115,7 @@ def run(args, rank: int, world: int, barrier, bcast, gpu_init=None) -> None:
         if load is not None:
             load.produce(i)
             return
-        futs = [prod.write(r) for r in make_records(corpus, rank, world, B, i)]
-        for f in futs:
-            f.result(60)
+        prod.write_many(make_records(corpus, rank, world, B, i)).result(60)
 
     def wait_all(total):
         if rank != 0:

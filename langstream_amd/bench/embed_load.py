@@ -53,9 +53,9 @@ def main(argv=None) -> int:
         if cmd[0] == "quit":
             break
         if cmd[0] == "produce":
-            futs = [prod.write(r) for r in make_records(corpus, a.rank, a.world, a.batch, int(cmd[1]))]
-            for f in futs:
-                f.result(60)
+            # one queued unit behind one future (KafkaProducer.write_many), as a batching
+            # Kafka client application would send them
+            prod.write_many(make_records(corpus, a.rank, a.world, a.batch, int(cmd[1]))).result(60)
             print("ok", flush=True)
         elif cmd[0] == "wait":
             total = int(cmd[1])

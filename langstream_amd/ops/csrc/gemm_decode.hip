@@ -96,10 +96,6 @@ struct DgArgs {
   bf16* kc = nullptr;
   bf16* vc = nullptr;
   int Hq = 0, Hkv = 0, BS = 0;
-  // row blocks: the grid also walks ceil(M / BMT) blocks of BMT rows (plain / SwiGLU
-  // epilogues, S = 1); the blocks of one column tile are consecutive logical ids (one
-  // XCD, co-resident), so the tile's weights come from HBM once and from L2 after
-  int mblocks = 1;
 };
 
 // 1 / rms of one row from its npart partial sums of squares.  The partials were written by
@@ -188,15 +184,8 @@ __global__ void __launch_bounds__(LD ? 768 : 512) dgemm_kernel(const bf16* __res
   // split_outer: consecutive logical ids (one XCD) share the K split, i.e. the same X
   // slice, which then stays in that XCD's L2; otherwise the S splits of one tile are
   // adjacent (the gate_up exchange pairs sit on one XCD).
-  int logical = xcd_remap(blockIdx.x, gridDim.x);
-  if (ga.mblocks > 1) {
-    const int mb = logical % ga.mblocks;
-    logical /= ga.mblocks;
-    x += (int64_t)mb * BMT * ldx;
-    out += (int64_t)mb * BMT * ldo;
-    M = min(BMT, M - mb * BMT);
-  }
-  const int ntiles = gridDim.x / ga.mblocks / S;
+  const int logical = xcd_remap(blockIdx.x, gridDim.x);
+  const int ntiles = gridDim.x / S;
   const int tile = split_outer ? logical % ntiles : logical / S;
   const int split = split_outer ? logical / ntiles : logical - tile * S;
   const int nk = K / BK;
@@ -674,7 +663,7 @@ void dgemm_launch_bm(int S, int tiles, hipStream_t st, const at::Tensor& x, cons
   const int pol = LDW == 4 ? (wnt_default() ? 16 : 0) | (ntst_default() ? 128 : 0) : 0;
 #define POL_(A)                                                                                                  \
   case A:                                                                                                        \
-    dgemm_kernel<BN, XS, WS, EPI, A, LDW, BMT, SPB><<<dim3(tiles * S * ga.mblocks), 768, 0, st>>>(                                 \
+    dgemm_kernel<BN, XS, WS, EPI, A, LDW, BMT, SPB><<<dim3(tiles * S), 768, 0, st>>>(                                 \
         (const bf16*)x.data_ptr(), x.stride(0), (const bf16*)w.data_ptr(), M, N, K, S, out, ldo, part, F, tickets, \
         xchg, err, so, ga);                                                                                      \
     return;
@@ -684,7 +673,7 @@ void dgemm_launch_bm(int S, int tiles, hipStream_t st, const at::Tensor& x, cons
     switch (pol) { POL_(144) default: break; }
   }
 #undef POL_
-  dgemm_kernel<BN, XS, WS, EPI, 0, LDW, BMT, SPB><<<dim3(tiles * S * ga.mblocks), LDW ? 768 : 512, 0, st>>>(
+  dgemm_kernel<BN, XS, WS, EPI, 0, LDW, BMT, SPB><<<dim3(tiles * S), LDW ? 768 : 512, 0, st>>>(
       (const bf16*)x.data_ptr(), x.stride(0), (const bf16*)w.data_ptr(), M, N, K, S, out, ldo, part, F, tickets, xchg,
       err, so, ga);
 }
@@ -788,21 +777,6 @@ void decode_gemm(at::Tensor out, at::Tensor x, at::Tensor w, at::Tensor workspac
   const int S = splits_force > 0 ? (int)std::min<int64_t>(splits_force, K / BK) : pick_split(tiles, K, 4);
   auto st = at::hip::getCurrentHIPStream();
   if (S == 1 && !norm) {
-    // LS_DGEMM_ROWBLK=64|128 (read per call; A/B runs): row blocks instead of one 256-row
-    // tile -- no split-K slabs, each workgroup streams the full K of its column tile
-    const char* rbe = getenv("LS_DGEMM_ROWBLK");
-    const int rb = rbe ? atoi(rbe) : 0;
-    if ((rb == 64 || rb == 128) && bn == 128 && M > rb) {
-      DgArgs ga;
-      ga.mblocks = (M + rb - 1) / rb;
-      if (rb == 64)
-        dgemm_launch_bm<128, EPI_STORE, 64>(1, tiles, st, x, w, M, N, K, (bf16*)out.data_ptr(), out.stride(0), nullptr,
-                                            0, nullptr, nullptr, nullptr, ga);
-      else
-        dgemm_launch_bm<128, EPI_STORE, 128>(1, tiles, st, x, w, M, N, K, (bf16*)out.data_ptr(), out.stride(0),
-                                             nullptr, 0, nullptr, nullptr, nullptr, ga);
-      return;
-    }
     if (bn == 256)
       dgemm_launch<256, EPI_STORE>(1, tiles, st, x, w, M, N, K, (bf16*)out.data_ptr(), out.stride(0), nullptr, 0,
                                    nullptr, nullptr, nullptr);
@@ -996,15 +970,6 @@ void decode_gemm_silu(at::Tensor out, at::Tensor x, at::Tensor w, at::Tensor wor
   const int sp = splits > 0 ? (int)splits : split_env;
   auto st = at::hip::getCurrentHIPStream();
   if (sp != 2 || K / BK < 8) {
-    const char* rbe = getenv("LS_DGEMM_ROWBLK");
-    const int rb = rbe ? atoi(rbe) : 0;
-    if (rb == 128 && M > rb) {
-      DgArgs ga;
-      ga.mblocks = (M + rb - 1) / rb;
-      dgemm_launch_bm<128, EPI_SILU, 128>(1, F / 64, st, x, w, M, 2 * F, K, (bf16*)out.data_ptr(), out.stride(0),
-                                          nullptr, F, nullptr, nullptr, nullptr, ga);
-      return;
-    }
     // one launch, no combine: 128-column tiles (64 gate + 64 up), full K
     dgemm_launch<128, EPI_SILU>(1, F / 64, st, x, w, M, 2 * F, K, (bf16*)out.data_ptr(), out.stride(0), nullptr, F,
                            nullptr, nullptr, nullptr);

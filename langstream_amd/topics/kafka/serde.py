@@ -56,6 +56,11 @@ def deserializer_for_schema(schema: Optional[Dict[str, Any]]) -> str:
 
 def serialize_typed(v: Any, avro: Optional[Callable[[AvroRecord], bytes]] = None) -> Optional[bytes]:
     """Reflection-based serialisation (the BASE_SERIALIZERS table + JSON + Avro)."""
+    t = type(v)
+    if t is dict:   # the common cases first, by exact type (one check instead of ~10)
+        return fastjson.dumps(v).encode()
+    if t is str:
+        return v.encode("utf-8")
     if v is None:
         return None
     if isinstance(v, (bytes, bytearray, memoryview)):

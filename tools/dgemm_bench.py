@@ -35,17 +35,6 @@ def time_once(fn, n, iters):
     return s.elapsed_time(e) * 1000.0 / iters
 
 
-def _rowblk(rb, fn):
-    """Run ``fn`` with LS_DGEMM_ROWBLK=rb (row blocks of rb rows, no split-K)."""
-    def run(i):
-        os.environ["LS_DGEMM_ROWBLK"] = str(rb)
-        try:
-            fn(i)
-        finally:
-            os.environ.pop("LS_DGEMM_ROWBLK", None)
-    return run
-
-
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ms", default="256")
@@ -105,8 +94,6 @@ def main():
                 variants["skinny"] = lambda i: h.skinny_gemm_silu(out, x, ws[i])
                 variants["dgemm_s1"] = lambda i: h.decode_gemm_silu(out, x, ws[i], wsp, tickets, err, 1)
                 variants["dgemm_s2"] = lambda i: h.decode_gemm_silu(out, x, ws[i], wsp, tickets, err, 2)
-                variants["dgemm_s1_rb128"] = _rowblk(128, lambda i: h.decode_gemm_silu(out, x, ws[i], wsp, tickets,
-                                                                                        err, 1))
                 check = lambda: out.float()  # noqa: E731
             elif name in ("o", "down"):
                 out = torch.empty(M, N, device=dev, dtype=bf)
@@ -134,9 +121,6 @@ def main():
                     for sp in (0, 2, 4, 6, 8):
                         variants[f"dgemm_bn{bn}_s{sp}"] = (
                             lambda i, bn=bn, sp=sp: h.decode_gemm(out, x, ws[i], wsp, None, None, 1e-5, bn, sp))
-                for rb in (64, 128):
-                    variants[f"dgemm_bn128_s1_rb{rb}"] = _rowblk(
-                        rb, lambda i: h.decode_gemm(out, x, ws[i], wsp, None, None, 1e-5, 128, 1))
                 check = lambda: out.float()  # noqa: E731
                 if name == "qkv" and N % 128 == 0:
                     # decode-only step form: + RoPE + paged K/V write in the reduction pass; timed
