@@ -110,6 +110,7 @@ class Request:
     output_ids: List[int] = field(default_factory=list)
     output_logprobs: List[float] = field(default_factory=list)
     blocks: List[int] = field(default_factory=list)
+    shared_blocks: int = 0       # blocks[:shared_blocks] belong to a prefix-cache entry (read-only)
     num_computed: int = 0        # tokens whose KV is (or is being) written to the cache
     num_launched: int = 0        # output tokens launched (sampled or in flight)
     finished: bool = False
@@ -433,9 +434,15 @@ class LLMEngine:
             n = min(remaining, budget)
             need = self._blocks_needed(r, base + n)
             headroom = n_decode  # let every decoding sequence grow by one more block
+            # full blocks of the prefix are shared with the entry (read-only: this prompt
+            # writes from position `hit` on), the partial one is copied
+            nshared = hit // BLOCK
+            if hit:
+                need = (base + n + BLOCK - 1) // BLOCK - nshared
             if hit and self.allocator.can_allocate(need + headroom):
                 r.num_computed = base
-                r.blocks += self.allocator.allocate(need)
+                r.blocks = list(entry.blocks[:nshared]) + list(self.allocator.allocate(need))
+                r.shared_blocks = nshared
                 self.prefix.apply_hit(r, entry, self._step_id + 1)
                 chosen.append((r, n))
                 budget -= n
@@ -490,8 +497,7 @@ class LLMEngine:
             if victim is exclude or victim.finished:
                 continue
             self.running.remove(victim)
-            self.allocator.free(victim.blocks)
-            victim.blocks = []
+            self._free_blocks(victim)
             victim.num_computed = 0
             victim.pending_row = -1
             victim.pending_step = -1
@@ -759,12 +765,20 @@ class LLMEngine:
         r._text += s
         return s
 
+    def _free_blocks(self, r: Request) -> None:
+        """Return a request's own blocks; shared prefix blocks stay with their entry."""
+        own = r.blocks[r.shared_blocks:]
+        if own:
+            self.allocator.free(own)
+        if self.prefix is not None:
+            self.prefix.release(r)
+        r.blocks = []
+        r.shared_blocks = 0
+
     def _release(self, r: Request) -> None:
         if r in self.running:
             self.running.remove(r)
-        if r.blocks:
-            self.allocator.free(r.blocks)
-            r.blocks = []
+        self._free_blocks(r)
         r.finish_time = time.perf_counter()
         self.stats["finished"] += 1
         r._done_event.set()

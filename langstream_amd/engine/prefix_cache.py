@@ -18,8 +18,12 @@ receives its own tokens after the prefix).
   ``StepExecutor::run`` / ``PyStepExecutor._run``), so they are ordered after the step
   that computed the prefix and before any step that reads them, and under tensor
   parallelism every rank performs them (the arena is broadcast).
-* At most ``max_entries`` prefixes (LRU); an entry is never evicted in a step that reads
-  it, so its blocks are never rewritten before the copies that read them ran.
+* Full prefix blocks are SHARED: a hit's block table starts with the entry's blocks
+  (read-only -- the prompt writes from the prefix end on, which lies past them), so
+  only the partial last block is copied, and every sequence of the batch reads the same
+  physical prefix KV (cache hits in the decode attention instead of HBM reads).
+* At most ``max_entries`` prefixes (LRU); an entry is evicted only when no live request
+  shares its blocks and no copy of the step being built reads them.
 
 The vLLM / SGLang production engines do the same (block-hash / radix-tree prefix
 caching); the reference delegates generation to remote services (OpenAI prompt caching,
@@ -34,10 +38,11 @@ import numpy as np
 
 
 class _Entry:
-    __slots__ = ("ids", "blocks", "last_step", "hits")
+    __slots__ = ("ids", "blocks", "last_step", "hits", "refs")
 
     def __init__(self, ids: np.ndarray, blocks: List[int], step: int):
         self.ids, self.blocks, self.last_step, self.hits = ids, blocks, step, 0
+        self.refs = 0   # live requests whose block tables hold this entry's full blocks
 
 
 class PrefixCache:
@@ -101,9 +106,13 @@ class PrefixCache:
         return len(e.ids), e
 
     def apply_hit(self, r, e: _Entry, step: int) -> None:
-        """The request took entry e (its blocks are allocated): queue the block copies."""
+        """The request took entry e: its block table starts with the entry's full blocks
+        (shared, read-only); the partial last prefix block is copied into its own block."""
         nb = (len(e.ids) + self.block - 1) // self.block
-        self.copies.extend(zip(e.blocks[:nb], r.blocks[:nb]))
+        nfull = len(e.ids) // self.block
+        self.copies.extend(zip(e.blocks[nfull:nb], r.blocks[nfull:nb]))
+        e.refs += 1
+        r._prefix_entry = e
         e.last_step = step
         e.hits += 1
         self.stats["hits"] += 1
@@ -134,8 +143,17 @@ class PrefixCache:
             self.stats["captures"] += 1
         self.pending = keep
 
+    def release(self, r) -> None:
+        """A request gave its blocks back (finished or preempted)."""
+        e = getattr(r, "_prefix_entry", None)
+        if e is not None:
+            e.refs -= 1
+            r._prefix_entry = None
+
     def _evict(self, step: int) -> bool:
-        cands = [e for e in self.entries if e.last_step != step]
+        # an entry is evictable once no live request shares its blocks and no copy of
+        # this step reads them
+        cands = [e for e in self.entries if e.last_step != step and e.refs == 0]
         if not cands:
             return False
         e = min(cands, key=lambda x: x.last_step)
@@ -149,8 +167,9 @@ class PrefixCache:
         return c
 
     def clear(self) -> None:
-        for e in self.entries:
+        """Drop every entry no request shares (the rest stay until released)."""
+        for e in [e for e in self.entries if e.refs == 0]:
             self.allocator.free(e.blocks)
-        self.entries.clear()
+            self.entries.remove(e)
         self.pending.clear()
         self.copies.clear()

@@ -212,3 +212,29 @@ def test_prefix_cache_lru_bound(model):
         eng.generate(prompts[i:i + 2], sp)
     assert len(eng.prefix.entries) <= 3 and eng.prefix.stats["evictions"] >= 1
     assert eng.allocator.num_free() + _prefix_blocks(eng) == 128
+
+
+def test_prefix_cache_shares_full_blocks(model):
+    """A hit's block table starts with the entry's FULL prefix blocks (shared, never
+    written: the prompt writes from the prefix end on); only the partial block is
+    copied.  Refcounts keep a shared entry from eviction and return to 0 at release."""
+    prompts = _shared_prefix_prompts(n=6, plen=150, seed=12)
+    sp = SamplingParams(max_tokens=4, temperature=0.0, ignore_eos=True)
+    eng = LLMEngine(model, None, num_blocks=96, max_model_len=512, max_batch=8, max_prefill_tokens=128,
+                    prefix_cache=True)
+    reqs = [eng.submit(p, sp) for p in prompts]
+    seen = []
+    while not all(r.finished for r in reqs):
+        eng.step()
+        for r in reqs:
+            if r.shared_blocks and r.request_id not in [x[0] for x in seen]:
+                e = r._prefix_entry
+                seen.append((r.request_id, r.shared_blocks, list(r.blocks[:r.shared_blocks]) == e.blocks[:2],
+                             e.refs))
+    eng._flush()
+    assert seen and all(nb == 2 and same and refs >= 1 for _, nb, same, refs in seen)   # 150 // 64 = 2
+    assert all(e.refs == 0 for e in eng.prefix.entries)
+    assert eng.allocator.num_free() + _prefix_blocks(eng) == 96
+    off = LLMEngine(model, None, num_blocks=96, max_model_len=512, max_batch=8, max_prefill_tokens=128,
+                    prefix_cache=False)
+    assert [r.output_ids for r in reqs] == [r.output_ids for r in off.generate(prompts, sp)]
