@@ -31,7 +31,6 @@ OpenAICompletionService.java:122-404).  ``LS_PREFIX_CACHE=0`` disables it.
 """
 from __future__ import annotations
 
-import collections
 from typing import Dict, List, Optional, Tuple
 
 import numpy as np
@@ -52,7 +51,11 @@ class PrefixCache:
         self.max_entries, self.min_len, self.max_len = max_entries, min_len, max_len
         self.min_gain, self.max_copies = min_gain, max_copies
         self.entries: List[_Entry] = []
-        self.recent: collections.deque = collections.deque(maxlen=history)
+        # heads of the last `history` prompts, one row each (-1 padded), compared with a
+        # new prompt in one vectorised pass
+        self._heads = np.full((history, max_len), -1, dtype=np.int64)
+        self._nrecent = 0
+        self._next = 0
         self.pending: List[Tuple[object, int]] = []      # (request, prefix length) to capture
         self.copies: List[Tuple[int, int]] = []          # (src, dst) block pairs for the next step
         self.stats: Dict[str, int] = {"hit_tokens": 0, "hits": 0, "captures": 0, "evictions": 0}
@@ -79,20 +82,26 @@ class PrefixCache:
         head = self._head(r)
         n = len(r.prompt_ids)
         lcp = 0
-        for h in self.recent:
-            m = min(len(h), len(head), n - 1)
-            if m <= lcp:
-                continue
-            neq = np.flatnonzero(h[:m] != head[:m])
-            lcp = max(lcp, int(neq[0]) if len(neq) else m)
-        self.recent.append(head)
+        m = min(len(head), n - 1)
+        if self._nrecent and m > 0:
+            neq = self._heads[: self._nrecent, :m] != head[:m]       # padding (-1) never matches
+            first = np.where(neq.any(axis=1), neq.argmax(axis=1), m)
+            lcp = int(first.max())
+        row = self._heads[self._next]
+        row[:] = -1
+        row[: len(head)] = head
+        self._next = (self._next + 1) % len(self._heads)
+        self._nrecent = min(self._nrecent + 1, len(self._heads))
         if lcp < self.min_len:
             return
         have = self._best(head, n)
         if have is not None and lcp < len(have.ids) + self.min_gain:
             return
-        if any(L >= lcp and np.array_equal(self._head(q)[:lcp], head[:lcp]) for q, L in self.pending):
-            return
+        # one pending capture per prefix: a longer one only when it gains min_gain tokens
+        for q, L in self.pending:
+            k = min(L, lcp)
+            if lcp < L + self.min_gain and np.array_equal(self._head(q)[:k], head[:k]):
+                return
         self.pending.append((r, lcp))
 
     def hit(self, r, step: int) -> Tuple[int, Optional[_Entry]]:

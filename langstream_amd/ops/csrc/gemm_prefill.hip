@@ -385,22 +385,34 @@ constexpr int HT = 16384;
 constexpr int EPI_ROW = 256 + 8;          // staged row pitch in bf16 (528 B: 4-bank shift per row)
 constexpr int PP_LDS = 256 * EPI_ROW * 2 > 8 * HT ? 256 * EPI_ROW * 2 : 8 * HT;
 
+// Split-K (S > 1, plain GEMM only): the grid is S x the tile grid; split s takes K tiles
+// [2 floor(s P / S), 2 floor((s + 1) P / S)) of the P = K / 128 tile pairs and stores its
+// f32 partial tile to part[s][M][N] (a reduction kernel sums the S slabs into bf16).  For
+// mid-size steps whose tile grid leaves CUs idle: T = 1024 gives o / down 4 x 16 = 64
+// tiles on 256 CUs.  Consecutive logical ids share a split (one XCD streams one K range).
 template <int EPI, int EPS = 0>
 __global__ void __launch_bounds__(512) gemm_pp_kernel(const bf16* __restrict__ x, int64_t ldx,
                                                       const bf16* __restrict__ w, int M, int K,
                                                       bf16* __restrict__ out, int64_t ldo, int MT, int NTL, int F,
-                                                      int group_m) {
+                                                      int group_m, int S = 1, float* __restrict__ part = nullptr) {
   __shared__ __attribute__((aligned(1024))) char lds[EPS == 1 ? PP_LDS : 8 * HT];
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int logical = xcd_remap(blockIdx.x, gridDim.x);
+  int logical = xcd_remap(blockIdx.x, gridDim.x);
+  const int ntiles = gridDim.x / S;
+  const int split = logical / ntiles;
+  logical -= split * ntiles;
   const int per_group = group_m * NTL;
   const int grp = logical / per_group, first = grp * group_m;
   const int gsz = min(MT - first, group_m);
   const int rem = logical - grp * per_group;
   const int mt = first + rem % gsz, nt = rem / gsz;
   const int m0 = mt * TM;
-  const int nk = K / 64;
+  const int npairs = K / 128;
+  const int kt0 = 2 * (int)(((int64_t)split * npairs) / S);
+  const int nk = 2 * (int)(((int64_t)(split + 1) * npairs) / S) - kt0;
+  x += (int64_t)kt0 * 64;
+  w += (int64_t)kt0 * 64;
 
   // LDS-DMA sources: wave w fills LDS rows 16w..16w+15 of every half-tile (2 pieces of
   // 8 rows x 128 B); lane l loads row 8e + (l >> 3) of piece e, swizzled chunk l & 7.
@@ -565,6 +577,26 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(const bf16* __restrict__ x
 
   // acc[qm][qn][i][j][r] = C[128 wm + 64 qm + 16 i + 4 h + r][64 wn + 32 qn + 16 j + fr] (tile-local;
   // SILU: qn = 0 gate, qn = 1 up of feature nt*128 + 32 wn + 16 j + fr)
+  if constexpr (EPI == EPI_STORE) {
+    if (S > 1) {   // split-K: this split's f32 partial tile
+      const int64_t N = (int64_t)NTL * TN;
+#pragma unroll
+      for (int qm = 0; qm < 2; ++qm)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int m = m0 + 128 * wm + 64 * qm + 16 * i + 4 * h + r;
+            if (m >= M) continue;
+            float* prow = part + ((int64_t)split * M + m) * N;
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+              for (int qn = 0; qn < 2; ++qn) prow[nt * TN + 64 * wn + 32 * qn + 16 * j + fr] = acc[qm][qn][i][j][r];
+          }
+      return;
+    }
+  }
 #pragma unroll
   for (int qm = 0; qm < 2; ++qm)
 #pragma unroll
@@ -860,6 +892,8 @@ void launch(int variant, int ring, int nwv, bool sp, dim3 grid, hipStream_t st, 
 
 // Shapes the kernel takes: K % 32 == 0 and N % 256 == 0 (silu: the fused [2F, K] gate_up
 // weight with F % 128 == 0).
+void splitk_reduce_launch(const float* part, int S, int M, int N, bf16* out, int64_t ldo, hipStream_t st);
+
 bool gemm_prefill_supported(const at::Tensor& w, bool silu) {
   if (w.dim() != 2 || w.scalar_type() != at::kBFloat16 || !w.is_contiguous() || w.size(1) % GBK != 0) return false;
   return silu ? (w.size(0) % 256 == 0) : (w.size(0) % TN == 0);
@@ -895,6 +929,24 @@ void gemm_prefill(at::Tensor out, at::Tensor x, at::Tensor w, bool silu, int64_t
   // profiles/pgemm_ab_r3_pingpong_v1.log, pgemm_ab_r3_persistent_v2.log)
   static const int var_env = env_int("LS_PGEMM_KERNEL", 1);
   const int var = variant < 0 ? var_env : (int)variant;
+  // Split-K for under-filled plain GEMMs on the ping-pong kernel (LS_PGEMM_SPLITK=0: off):
+  // fewer than ~200 tiles on 256 CUs and a deep K (the f32 slabs cost 8 M N (S - 1) bytes
+  // more than the bf16 output; at K = 4096 that eats what the fuller grid wins)
+  static const int splitk_env = env_int("LS_PGEMM_SPLITK", 1);
+  static const int splitk_min_k = env_int("LS_PGEMM_SPLITK_MIN_K", 8192);
+  const int tiles = MT * NTL;
+  int S = 1;
+  if (!silu && var == 1 && splitk_env && K % 128 == 0 && K >= splitk_min_k && tiles < 200) {
+    S = std::max(1, std::min({4, 256 / tiles, (int)(K / 128) / 8}));
+  }
+  if (S > 1) {
+    at::Tensor part = at::empty({S, M, N}, x.options().dtype(at::kFloat));
+    gemm_pp_kernel<EPI_STORE, 0><<<dim3((unsigned)(tiles * S)), 512, 0, stream>>>(
+        (const bf16*)x.data_ptr(), x.stride(0), (const bf16*)w.data_ptr(), (int)M, (int)K, nullptr, 0, MT, NTL, 0, gm,
+        S, part.data_ptr<float>());
+    splitk_reduce_launch(part.data_ptr<float>(), S, (int)M, (int)N, (bf16*)out.data_ptr(), out.stride(0), stream);
+    return;
+  }
   if (silu) launch<EPI_SILU>(var, ring, nwv, sp, grid, stream, x, w, (int)M, (int)K, out, MT, NTL, (int)(N / 2), gm);
   else launch<EPI_STORE>(var, ring, nwv, sp, grid, stream, x, w, (int)M, (int)K, out, MT, NTL, 0, gm);
 }

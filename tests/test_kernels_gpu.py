@@ -484,6 +484,19 @@ def test_gemm_prefill_pingpong(M, N, K, variant):
     _close(out, x.float() @ w.float().t(), 0.02, 0.02)
 
 
+@pytest.mark.parametrize("M,N,K", [(300, 256, 8192), (1024, 256, 8320), (1024, 4096, 14336),
+                                   (2048, 4096, 14336), (3000, 512, 8192)])
+def test_gemm_prefill_pingpong_splitk(M, N, K):
+    """Split-K on the ping-pong kernel (under-filled tile grids with K >= 8192: the
+    Llama down projection at 1024-4095 tokens): S K-ranges of whole tile pairs, f32
+    partial slabs, then the reduction -- vs fp32, M tails included."""
+    torch.manual_seed(M + N + K + 7)
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=DEV) / K ** 0.5).to(torch.bfloat16)
+    out = ops.gemm_prefill(x, w, variant=1)
+    _close(out, x.float() @ w.float().t(), 0.02, 0.02)
+
+
 @pytest.mark.parametrize("variant", [1, 2])
 @pytest.mark.parametrize("M,F,K", [(77, 128, 256), (1000, 384, 1024), (4096, 256, 512), (40000, 640, 256)])
 def test_gemm_prefill_pingpong_silu(M, F, K, variant):
