@@ -930,10 +930,11 @@ void gemm_prefill(at::Tensor out, at::Tensor x, at::Tensor w, bool silu, int64_t
   static const int var_env = env_int("LS_PGEMM_KERNEL", 1);
   const int var = variant < 0 ? var_env : (int)variant;
   // Split-K for under-filled plain GEMMs on the ping-pong kernel (LS_PGEMM_SPLITK=0: off):
-  // fewer than ~200 tiles on 256 CUs and a deep K (the f32 slabs cost 8 M N (S - 1) bytes
-  // more than the bf16 output; at K = 4096 that eats what the fuller grid wins)
+  // fewer than ~200 tiles on 256 CUs, S = min(4, 256 / tiles) K ranges of >= 8 tile
+  // pairs.  Llama-3-8B at T = 1024 (profiles/r5/pgemm_midm_*): down 231 -> 102 us (S = 4,
+  // 1.18 PFLOP/s), o 78 -> 51, qkv 78 -> 62; T = 2048: down 236 -> 175, o 76 -> 71
   static const int splitk_env = env_int("LS_PGEMM_SPLITK", 1);
-  static const int splitk_min_k = env_int("LS_PGEMM_SPLITK_MIN_K", 8192);
+  static const int splitk_min_k = env_int("LS_PGEMM_SPLITK_MIN_K", 4096);
   const int tiles = MT * NTL;
   int S = 1;
   if (!silu && var == 1 && splitk_env && K % 128 == 0 && K >= splitk_min_k && tiles < 200) {
