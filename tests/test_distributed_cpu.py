@@ -437,8 +437,8 @@ def _slow_rank_knn_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-_SLOW_S = 3.0
-_FAST_QUERIES = 10
+_SLOW_S = 4.0
+_FAST_QUERIES = 8
 
 
 def test_sharded_knn_slow_rank_does_not_stall_others():
@@ -453,8 +453,13 @@ def test_sharded_knn_slow_rank_does_not_stall_others():
         p50[phase] = lats[len(lats) // 2]
         print(phase, "p50 %.3f s  max %.3f s" % (p50[phase], lats[-1]))
         assert lats[-1] < 1.5, (phase, lats[-5:])
-        if phase != "none":
-            # a slow agent costs the others at most a small factor of the unloaded latency
+        if phase == "sleep":
+            # an agent blocked outside the GIL costs the others nothing
             assert p50[phase] < 3 * p50["none"] + 0.1, (phase, p50)
+        if phase == "busy":
+            # an agent holding the GIL delays each of the slow rank's GIL hand-offs in a
+            # round by up to the 1 ms switch interval the service sets: bounded, not stalled
+            assert p50[phase] < 0.5, (phase, p50)
+        if phase != "none":
             # every fast rank finished its queries before the slow rank's agent came back
             assert max(r[phase]["done"] for r in g[:-1]) < slow[phase]["end"], phase
