@@ -120,10 +120,8 @@ class ShardedKnn:
     def search(self, collection: str, queries, k: int, with_vectors: bool = False) -> Future:
         """Global top-k for the rows of ``queries`` ([Q, d]) -> Future[List[List[dict]]]
         in the local store's result format (id, similarity, metadata[, vector])."""
-        q = torch.as_tensor(queries, dtype=torch.float32)
-        if q.dim() == 1:
-            q = q[None]
-        q = torch.nn.functional.normalize(q, dim=-1, eps=1e-12)
+        q = np.array(queries.cpu() if isinstance(queries, torch.Tensor) else queries, dtype=np.float32, ndmin=2)
+        q = q / np.maximum(np.linalg.norm(q, axis=-1, keepdims=True), 1e-12)
         r = _Req(collection, q, int(k), bool(with_vectors))
         if r.k < 1:
             r.fut.set_exception(ValueError("top-k must be >= 1"))
@@ -145,40 +143,42 @@ class ShardedKnn:
     # ------------------------------------------------------------------ collectives
     _SLOT = 2048   # round headers fit in one fixed-size all-gather slot almost always
 
+    # Host-side buffers are numpy arrays handed to the collectives through
+    # torch.from_numpy: a torch op releases and re-takes the GIL, and on a rank whose agents
+    # keep the GIL busy every re-take waits up to the switch interval while the other
+    # ranks wait in the next collective (tests/test_distributed_cpu.py slow-rank test).
     def _allgather_bytes(self, b: bytes) -> List[bytes]:
         """All-gather of variable-length byte strings over the gloo group: ONE collective
         with a fixed 2 KiB slot per rank (4-byte length + payload); only when some rank's
         payload is longer do all ranks (who all see every length) run a second round."""
-        slot = torch.zeros(self._SLOT, dtype=torch.uint8)
+        slot = np.zeros(self._SLOT, dtype=np.uint8)
         n = len(b)
-        slot[:4] = torch.tensor([n], dtype=torch.int32).view(torch.uint8)
+        slot[:4] = np.array([n], dtype=np.int32).view(np.uint8)
         if 0 < n <= self._SLOT - 4:
-            slot[4: 4 + n] = torch.frombuffer(bytearray(b), dtype=torch.uint8)
-        out = torch.empty(self.world * self._SLOT, dtype=torch.uint8)
-        dist.all_gather_into_tensor(out, slot, group=self.meta)
-        o = out.numpy()
-        lens = [int(np.frombuffer(o[i * self._SLOT: i * self._SLOT + 4].tobytes(), np.int32)[0])
-                for i in range(self.world)]
+            slot[4: 4 + n] = np.frombuffer(b, dtype=np.uint8)
+        o = np.empty(self.world * self._SLOT, dtype=np.uint8)
+        dist.all_gather_into_tensor(torch.from_numpy(o), torch.from_numpy(slot), group=self.meta)
+        lens = o.reshape(self.world, self._SLOT)[:, :4].copy().view(np.int32)[:, 0].tolist()
         if max(lens) <= self._SLOT - 4:
             return [o[i * self._SLOT + 4: i * self._SLOT + 4 + lens[i]].tobytes() for i in range(self.world)]
         m = max(lens)
-        buf = torch.zeros(m, dtype=torch.uint8)
+        buf = np.zeros(m, dtype=np.uint8)
         if b:
-            buf[:n] = torch.frombuffer(bytearray(b), dtype=torch.uint8)
-        out = torch.empty(self.world * m, dtype=torch.uint8)
-        dist.all_gather_into_tensor(out, buf, group=self.meta)
-        o = out.numpy()
+            buf[:n] = np.frombuffer(b, dtype=np.uint8)
+        o = np.empty(self.world * m, dtype=np.uint8)
+        dist.all_gather_into_tensor(torch.from_numpy(o), torch.from_numpy(buf), group=self.meta)
         return [o[i * m: i * m + lens[i]].tobytes() for i in range(self.world)]
 
     def _alltoall_bytes(self, per_dest: List[bytes]) -> List[bytes]:
-        send_n = torch.tensor([len(b) for b in per_dest], dtype=torch.int64)
-        recv_n = torch.empty(self.world, dtype=torch.int64)
-        dist.all_to_all_single(recv_n, send_n, group=self.meta)
+        send_n = np.array([len(b) for b in per_dest], dtype=np.int64)
+        recv_n = np.empty(self.world, dtype=np.int64)
+        dist.all_to_all_single(torch.from_numpy(recv_n), torch.from_numpy(send_n), group=self.meta)
         flat = b"".join(per_dest)
-        send = torch.frombuffer(bytearray(flat), dtype=torch.uint8) if flat else torch.zeros(0, dtype=torch.uint8)
-        recv = torch.empty(int(recv_n.sum()), dtype=torch.uint8)
-        dist.all_to_all_single(recv, send, recv_n.tolist(), send_n.tolist(), group=self.meta)
-        o, out, p = recv.numpy(), [], 0
+        send = np.frombuffer(flat, dtype=np.uint8).copy() if flat else np.zeros(0, dtype=np.uint8)
+        o = np.empty(int(recv_n.sum()), dtype=np.uint8)
+        dist.all_to_all_single(torch.from_numpy(o), torch.from_numpy(send), recv_n.tolist(), send_n.tolist(),
+                               group=self.meta)
+        out, p = [], 0
         for n in recv_n.tolist():
             out.append(o[p: p + n].tobytes())
             p += n
@@ -306,14 +306,22 @@ class ShardedKnn:
                     vec_colls.add(coll)
                 qmax = max(counts)
                 t_s = time.perf_counter()
-                pin = self.data_dev.type == "cuda"
-                qloc = torch.zeros(qmax, dim, dtype=torch.float32, pin_memory=pin)
-                if mine:
-                    torch.cat([r.q for r in mine], out=qloc[: counts[me]])
-                qloc = qloc.to(self.data_dev, non_blocking=pin)   # pinned: async, no staging copy
-                t_s = self._phase("upload_s", t_s)
-                qall = torch.empty(W * qmax, dim, dtype=torch.float32, device=self.data_dev)
-                dist.all_gather_into_tensor(qall, qloc, group=self.data)
+                host = self.data_dev.type == "cpu"
+                if host:
+                    qloc_np = np.zeros((qmax, dim), dtype=np.float32)
+                    if mine:
+                        qloc_np[: counts[me]] = np.concatenate([r.q for r in mine])
+                    qall_np = np.empty((W * qmax, dim), dtype=np.float32)
+                    dist.all_gather_into_tensor(torch.from_numpy(qall_np), torch.from_numpy(qloc_np), group=self.data)
+                    qall = torch.from_numpy(qall_np)
+                else:
+                    qloc = torch.zeros(qmax, dim, dtype=torch.float32, pin_memory=True)
+                    if mine:
+                        qloc[: counts[me]] = torch.from_numpy(np.concatenate([r.q for r in mine]))
+                    qloc = qloc.to(self.data_dev, non_blocking=True)   # pinned: async, no staging copy
+                    t_s = self._phase("upload_s", t_s)
+                    qall = torch.empty(W * qmax, dim, dtype=torch.float32, device=self.data_dev)
+                    dist.all_gather_into_tensor(qall, qloc, group=self.data)
                 t_s = self._phase("gather_s", t_s)
                 store = stores.get(coll)
                 s = idx = None
@@ -333,25 +341,42 @@ class ShardedKnn:
                         log.exception("sharded kNN: local search of %s failed", coll)
                         errs[coll] = e
                         s = idx = None
-                if s is None:
-                    s = torch.full((W * qmax, kmax), float("-inf"), device=self.data_dev)
-                    idx = torch.full((W * qmax, kmax), -1, dtype=torch.int32, device=self.data_dev)
-                send = torch.stack([s.float(), idx.int().view(torch.float32)], -1).contiguous()  # [W*qmax,k,2]
-                t_s = self._phase("topk_s", t_s)
-                recv = torch.empty_like(send)
-                dist.all_to_all_single(recv, send, group=self.data)
+                if host:
+                    # [W*qmax, k, 2] float32 pairs (score, row bits), exchanged in numpy
+                    send_np = np.empty((W * qmax, kmax, 2), dtype=np.float32)
+                    if s is None:
+                        send_np[..., 0] = -np.inf
+                        send_np[..., 1] = np.array([-1], dtype=np.int32).view(np.float32)[0]
+                    else:
+                        s_np = s.float().numpy() if isinstance(s, torch.Tensor) else np.asarray(s, np.float32)
+                        i_np = idx.int().numpy() if isinstance(idx, torch.Tensor) else np.asarray(idx, np.int32)
+                        send_np[..., 0] = s_np
+                        send_np[..., 1] = i_np.view(np.float32)
+                    t_s = self._phase("topk_s", t_s)
+                    recv_np = np.empty_like(send_np)
+                    dist.all_to_all_single(torch.from_numpy(recv_np), torch.from_numpy(send_np), group=self.data)
+                else:
+                    if s is None:
+                        s = torch.full((W * qmax, kmax), float("-inf"), device=self.data_dev)
+                        idx = torch.full((W * qmax, kmax), -1, dtype=torch.int32, device=self.data_dev)
+                    send = torch.stack([s.float(), idx.int().view(torch.float32)], -1).contiguous()  # [W*qmax,k,2]
+                    t_s = self._phase("topk_s", t_s)
+                    recv = torch.empty_like(send)
+                    dist.all_to_all_single(recv, send, group=self.data)
+                    recv_np = recv.cpu().numpy()
                 t_s = self._phase("a2a_s", t_s)
                 n_me = counts[me]
                 if n_me == 0:
                     continue
                 try:
-                    recv = recv.view(W, qmax, kmax, 2)[:, :n_me]                 # [W, n_me, k, 2]
-                    cs = recv[..., 0].permute(1, 0, 2).reshape(n_me, W * kmax)
-                    ci = recv[..., 1].contiguous().view(torch.int32).permute(1, 0, 2).reshape(n_me, W * kmax)
-                    top_s, sel = torch.topk(cs, kmax, dim=-1)
-                    rows = torch.gather(ci, 1, sel)
-                    owners = sel // kmax
-                    top_s, rows, owners = (t.tolist() for t in to_host(top_s, rows, owners.int()))
+                    # merge the W shards' candidates of this rank's queries on the host
+                    rv = recv_np.reshape(W, qmax, kmax, 2)[:, :n_me]            # [W, n_me, k, 2]
+                    cs = rv[..., 0].transpose(1, 0, 2).reshape(n_me, W * kmax)
+                    ci = np.ascontiguousarray(rv[..., 1]).view(np.int32).transpose(1, 0, 2).reshape(n_me, W * kmax)
+                    sel = np.argsort(-cs, axis=1, kind="stable")[:, :kmax]
+                    top_s = np.take_along_axis(cs, sel, 1).tolist()
+                    rows = np.take_along_axis(ci, sel, 1).tolist()
+                    owners = (sel // kmax).tolist()
                 except Exception as e:  # noqa: BLE001 - local merge only, no collective inside
                     log.exception("sharded kNN: merge of %s failed", coll)
                     errs.setdefault(coll, e)

@@ -145,7 +145,11 @@ __global__ void __launch_bounds__(64 * WPP) __attribute__((amdgpu_waves_per_eu(2
   // tools/attn_bench.py runs with a ring of pools.  LS_ATTN_NT=0 turns it off.
   const int kbyte = 8 * h * 2;
 
-  auto issue_k = [&](int bi, uint4(&kf)[4][KS]) {
+  // The FIRST block of a sequence is loaded with the default (cached) policy: prompts that
+  // share a template prefix share its full blocks (engine/prefix_cache.py), so a decode
+  // step's rows read the same physical block -- one HBM read, the rest cache hits.
+  auto issue_k_p = [&](int bi, uint4(&kf)[4][KS], auto polc) {
+    constexpr int POL = decltype(polc)::value;
     const int blk = __builtin_amdgcn_readfirstlane(block_of(bi));
     const int lim = __builtin_amdgcn_readfirstlane(min(ctx - bi * BS, BS));   // valid keys here (>= 1)
     const int64_t boff = ((int64_t)blk * Hkv + kvh) * BS * D;
@@ -156,10 +160,11 @@ __global__ void __launch_bounds__(64 * WPP) __attribute__((amdgpu_waves_per_eu(2
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks)
         kf[kt][ks] = __builtin_bit_cast(
-            uint4, __builtin_amdgcn_raw_buffer_load_b128(krs, key * D * 2 + 64 * ks + kbyte, 0, AUX));
+            uint4, __builtin_amdgcn_raw_buffer_load_b128(krs, key * D * 2 + 64 * ks + kbyte, 0, POL));
     }
   };
-  auto issue_v = [&](int bi, uint4(&vf)[2][DT]) {
+  auto issue_v_p = [&](int bi, uint4(&vf)[2][DT], auto polc) {
+    constexpr int POL = decltype(polc)::value;
     const int blk = __builtin_amdgcn_readfirstlane(block_of(bi));
     const int lim = __builtin_amdgcn_readfirstlane(min(ctx - bi * BS, BS));
     const int64_t boff = ((int64_t)blk * Hkv + kvh) * BS * D;
@@ -170,9 +175,20 @@ __global__ void __launch_bounds__(64 * WPP) __attribute__((amdgpu_waves_per_eu(2
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) {
         const int off = (int)vt_off(16 * dt + i16, 32 * kg + 8 * h, D) * 2;
-        vf[kg][dt] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(vrs, vok ? off : OOB, 0, AUX));
+        vf[kg][dt] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(vrs, vok ? off : OOB, 0, POL));
       }
     }
+  };
+  // AUX 3: nt loads except for a sequence's first block (cached)
+  constexpr bool FIRST_CACHED = AUX == 3;
+  constexpr int POLX = AUX == 3 ? 2 : AUX;
+  auto issue_k = [&](int bi, uint4(&kf)[4][KS]) {
+    if (FIRST_CACHED && bi == 0) issue_k_p(bi, kf, std::integral_constant<int, 0>());
+    else issue_k_p(bi, kf, std::integral_constant<int, POLX>());
+  };
+  auto issue_v = [&](int bi, uint4(&vf)[2][DT]) {
+    if (FIRST_CACHED && bi == 0) issue_v_p(bi, vf, std::integral_constant<int, 0>());
+    else issue_v_p(bi, vf, std::integral_constant<int, POLX>());
   };
 
   // K and V of block i are in flight together; with PIPE, block i+1's K loads are
@@ -489,14 +505,16 @@ static void decode_attention_launch(at::Tensor& out, const at::Tensor& q, const 
   static const int env_wpp = getenv("LS_ATTN_WPP") ? atoi(getenv("LS_ATTN_WPP")) : 0;
   static const bool pipe = getenv("LS_ATTN_PIPE") ? atoi(getenv("LS_ATTN_PIPE")) != 0 : true;
   const bool rope = ra != nullptr;
-  const char* ent = getenv("LS_ATTN_NT");   // read per launch (A/B inside one process)
-  const bool attn_nt = !ent || atoi(ent) != 0;
+  // LS_ATTN_NT (read per launch, A/B inside one process): 0 cached loads, 1 all nt,
+  // 2 (default) nt except each sequence's first block (shared template-prefix blocks)
+  const char* ent = getenv("LS_ATTN_NT");
+  const int attn_nt = ent ? atoi(ent) : 2;
   const RopeArgs rargs = rope ? *ra : RopeArgs{};
   const int wpp = env_wpp == 1 || env_wpp == 4 ? env_wpp : ((int64_t)B * Hkv >= WAVE_SLOTS && ns == 1 ? 1 : 4);
   dim3 grid(B * Hkv, ns);
   const float sl2 = (float)scale * LOG2E;
 #define LAUNCH_R(DD, W, P, R)                                                                                 \
-  if (attn_nt) LAUNCH_A(DD, W, P, R, 2); else LAUNCH_A(DD, W, P, R, 0)
+  if (attn_nt == 2) LAUNCH_A(DD, W, P, R, 3); else if (attn_nt) LAUNCH_A(DD, W, P, R, 2); else LAUNCH_A(DD, W, P, R, 0)
 #define LAUNCH_A(DD, W, P, R, A)                                                                              \
   decode_attn_kernel<DD, W, P, R, A><<<grid, 64 * W, 0, stream>>>(                                            \
       (bf16*)out.data_ptr(), (const bf16*)q.data_ptr(), q_stride, (const bf16*)k_cache.data_ptr(),            \
