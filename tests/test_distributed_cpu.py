@@ -463,3 +463,44 @@ def test_sharded_knn_slow_rank_does_not_stall_others():
         if phase != "none":
             # every fast rank finished its queries before the slow rank's agent came back
             assert max(r[phase]["done"] for r in g[:-1]) < slow[phase]["end"], phase
+
+
+def _prefix_prompts():
+    g = torch.Generator().manual_seed(21)
+    head = torch.randint(3, 250, (70,), generator=g).tolist()
+    return [head + torch.randint(3, 250, (int(n),), generator=g).tolist() for n in (9, 33, 21, 50, 14, 40)]
+
+
+def _tp_prefix_worker(rank, world, port, q):
+    """TP engine whose later prompts hit the prefix cache: the KV block copies ride in
+    the broadcast arena, so every rank copies its own KV shard."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from langstream_amd.engine.llm_engine import LLMEngine, SamplingParams
+        from langstream_amd.models.llama import LlamaModel, PRESETS, TPInfo
+        from langstream_amd.models.loader import shard_llama
+        cfg = PRESETS["llama-tiny"]
+        full = _full_model()
+        m = LlamaModel(cfg, device="cpu", dtype=torch.float32, tp=TPInfo(rank, world, None))
+        m.load_state_dict(shard_llama(full.state_dict(), cfg, rank, world))
+        eng = LLMEngine(m, None, num_blocks=64, max_model_len=512, max_prefill_tokens=96, prefix_cache=True)
+        if rank == 0:
+            sp = SamplingParams(max_tokens=MAXTOK, temperature=0.0, ignore_eos=True)
+            out = [r.output_ids for r in eng.generate(_prefix_prompts(), sp)]
+            hits = eng.prefix.stats["hits"]
+            eng.stop()
+            q.put((out, hits))
+        else:
+            eng.worker_loop()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_tensor_parallel_prefix_cache_matches_single():
+    from langstream_amd.engine.llm_engine import LLMEngine, SamplingParams
+    out, hits = _spawn(_tp_prefix_worker)
+    assert hits >= 2
+    eng = LLMEngine(_full_model(), None, num_blocks=64, max_model_len=512, prefix_cache=False)
+    sp = SamplingParams(max_tokens=MAXTOK, temperature=0.0, ignore_eos=True)
+    assert out == [r.output_ids for r in eng.generate(_prefix_prompts(), sp)]
