@@ -67,10 +67,11 @@ class MutableRecord:
         for h in r.headers():
             if h.key is not None and h.value is not None:
                 props[h.key] = h.value_as_string()
-        k, v = r.key(), r.value()
-        if attempt_json_conversion:
-            k, v = attempt_json(k), attempt_json(v)
-        m = MutableRecord(safe_clone(k), safe_clone(v), props, r.origin(), r.timestamp(), r)
+        k0, v0 = r.key(), r.value()
+        k, v = (attempt_json(k0), attempt_json(v0)) if attempt_json_conversion else (k0, v0)
+        # a value parsed from JSON text is already a fresh object: no copy needed
+        m = MutableRecord(k if k is not k0 else safe_clone(k), v if v is not v0 else safe_clone(v), props,
+                          r.origin(), r.timestamp(), r)
         return m
 
     def copy(self) -> "MutableRecord":

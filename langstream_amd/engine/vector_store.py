@@ -461,7 +461,10 @@ class VectorStore:
 
     def row_vectors(self, rows) -> Dict[int, List[float]]:
         flat, arr = self.row_vectors_array(rows)
-        return dict(zip(flat, arr.tolist())) if flat else {}
+        if not flat:
+            return {}
+        from ..utils.fastjson import f32_rows   # native rows of float32 values
+        return dict(zip(flat, f32_rows(arr)))
 
     def row_vectors_array(self, rows):
         """(sorted rows, float32 numpy [n, dim]): one device gather + one D2H copy, no
