@@ -426,16 +426,62 @@ class VectorStore:
             raise ValueError("top-k must be >= 1")
         tr = SEARCH_TRACE
         t_in = time.time() if tr is not None else 0.0
-        with on_search(self.device), self.lock:
-            t_lk = time.time() if tr is not None else 0.0
-            q = self._normalize(queries)
-            s, idx = self.topk_rows(q, k)
-            s, idx = (t.tolist() for t in to_host(s, idx))
-            t_gpu = time.time() if tr is not None else 0.0
-            out = self.rows_to_results(s, idx, with_vectors)
-            if tr is not None:
-                tr.append((t_in, t_lk, t_gpu, time.time(), len(out)))
-            return out
+        # host preparation outside the lock: numpy conversion + normalisation, then one
+        # pinned H2D copy on the search stream (the sharded service's path, which measured
+        # 26 ms per round in the RAG bench where this one took 30-170 ms per batch:
+        # profiles/r5/bench_stage_trace_r5j.log vs knn_w8load_r5o.log)
+        qn = self._normalize_host(queries)
+        with on_search(self.device):
+            with self.lock:
+                t_lk = time.time() if tr is not None else 0.0
+                q = self._to_device_query(qn)
+                s, idx = self.topk_rows(q, k)
+                s, idx = (t.tolist() for t in to_host(s, idx))
+                t_gpu = time.time() if tr is not None else 0.0
+                # what depends on the row numbering is read under the lock; the result
+                # objects are built after it is released
+                hits = [[(sc, r, self.row_payload(r)) for sc, r in zip(srow, irow) if 0 <= r < self._n]
+                        for srow, irow in zip(s, idx)]
+                vec_rows = (self.row_vectors_array({r for row in hits for _, r, _ in row})
+                            if with_vectors else None)
+        out = self._build_results(hits, vec_rows)
+        if tr is not None:
+            tr.append((t_in, t_lk, t_gpu, time.time(), len(out)))
+        return out
+
+    def _normalize_host(self, v) -> np.ndarray:
+        if isinstance(v, torch.Tensor):
+            a = v.detach().float().cpu().numpy()
+        else:
+            a = np.asarray(v, dtype=np.float32)
+        if a.ndim == 1:
+            a = a[None]
+        if a.shape[-1] != self.dim:
+            raise ValueError(f"vector dim {a.shape[-1]} != collection {self.name} dim {self.dim}")
+        return a / np.maximum(np.linalg.norm(a, axis=-1, keepdims=True), 1e-12)
+
+    def _to_device_query(self, a: np.ndarray) -> torch.Tensor:
+        t = torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32))
+        if self.device.type == "cuda":
+            t = t.pin_memory().to(self.device, non_blocking=True)
+        return t.to(self.dtype)
+
+    @staticmethod
+    def _build_results(hits, vec_rows) -> List[List[Dict[str, Any]]]:
+        vecs = {}
+        if vec_rows is not None and vec_rows[0]:
+            from ..utils.fastjson import f32_rows   # native rows of float32 values
+            vecs = dict(zip(vec_rows[0], f32_rows(vec_rows[1])))
+        out = []
+        for row in hits:
+            res = []
+            for sc, r, d in row:
+                d["similarity"] = sc
+                if vec_rows is not None:
+                    d["vector"] = vecs.get(r)
+                res.append(d)
+            out.append(res)
+        return out
 
     def rows_to_results(self, scores, rows, with_vectors: bool) -> List[List[Dict[str, Any]]]:
         """Host results for row indices (caller holds ``lock``)."""

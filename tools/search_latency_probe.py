@@ -32,17 +32,25 @@ def main() -> int:
     w = torch.randn(14336, 4096, device=dev, dtype=torch.bfloat16)
     q = torch.randn(64, 384)
 
+    from langstream_amd import ops
+    wg = torch.randn(2 * 14336, 4096, device=dev, dtype=torch.bfloat16)
+    kind = {"k": "matmul"}
+
     def load(stop):
         while not stop.is_set():
             for _ in range(40):
-                torch.matmul(a, w.t())
+                if kind["k"] == "matmul":
+                    torch.matmul(a, w.t())
+                else:   # the engine's prefill gate_up kernel: 160 KB of LDS per workgroup
+                    ops.gemm_prefill(a, wg, silu=True)
             torch.cuda.synchronize()
 
     res = {}
-    for mode in ("idle", "loaded"):
+    for mode in ("idle", "loaded", "loaded_pp"):
+        kind["k"] = "pp" if mode == "loaded_pp" else "matmul"
         stop = threading.Event()
         th = threading.Thread(target=load, args=(stop,), daemon=True)
-        if mode == "loaded":
+        if mode != "idle":
             th.start()
             time.sleep(0.5)
         for variant in ("default", "vectors"):
@@ -54,7 +62,7 @@ def main() -> int:
                 time.sleep(0.02)
             res[f"{mode}_{variant}_ms"] = [round(statistics.median(lat), 2), round(max(lat), 2)]
         stop.set()
-        if mode == "loaded":
+        if mode != "idle":
             th.join()
     # the raw copy paths under load
     stop = threading.Event()
