@@ -625,7 +625,13 @@ int split_outer_default() {
 // per-layer kernel times): W loads non-temporal (LS_DGEMM_WNT, gate_up 66.5 -> 64.5 us)
 // and the f32 split-K slabs stored non-temporally (LS_DGEMM_NTST); with the attention's
 // nt KV loads the layer drops 256.8 -> 240.6 us.  Both default on; read per launch.
-int wnt_default() { return env_int("LS_DGEMM_WNT", 1); }
+// LS_DGEMM_WNT = 2: nt only for weights past 64 MB (gate_up / down); qkv and o measured
+// faster with cached weight loads in isolation (M = 256, weights cold: 27.3 vs 28.8 and
+// 23.8 vs 26.5 us, profiles/r5/dgemm_cold_hot_r5q.log).
+int wnt_default(int64_t wbytes) {
+  const int v = env_int("LS_DGEMM_WNT", 1);
+  return v == 2 ? wbytes > (int64_t(64) << 20) : v;
+}
 int ntst_default() { return env_int("LS_DGEMM_NTST", 1); }
 
 // Host-side launch census per (BN, epilogue, tile rows, K splits): the tests read it to
@@ -660,7 +666,7 @@ void dgemm_launch_bm(int S, int tiles, hipStream_t st, const at::Tensor& x, cons
   // non-temporal hint -- 16 GB of weights per decode step have no reuse and should not
   // evict the activations and the split-K workspace -- and / or the f32 partial slabs
   // written non-temporally, so they do not sit dirty in L2 for the kernel-end write-back
-  const int pol = LDW == 4 ? (wnt_default() ? 16 : 0) | (ntst_default() ? 128 : 0) : 0;
+  const int pol = LDW == 4 ? (wnt_default(w.numel() * 2) ? 16 : 0) | (ntst_default() ? 128 : 0) : 0;
 #define POL_(A)                                                                                                  \
   case A:                                                                                                        \
     dgemm_kernel<BN, XS, WS, EPI, A, LDW, BMT, SPB><<<dim3(tiles * S), 768, 0, st>>>(                                 \

@@ -44,6 +44,9 @@ def main():
     ap.add_argument("--hidden", type=int, default=4096)
     ap.add_argument("--ffn", type=int, default=14336)
     ap.add_argument("--qkv", type=int, default=6144)
+    ap.add_argument("--ring", type=int, default=0,
+                    help="weight copies to rotate through (0: enough to exceed the Infinity Cache; "
+                         "1: the weights stay cache-resident -- the upper bound of a prefetch)")
     ap.add_argument("--ablate", action="store_true",
                     help="time the split-K kernel's ablation builds (no MFMA / no LDS reads / no DMA)")
     ap.add_argument("--env-ab", default="",
@@ -59,7 +62,7 @@ def main():
     for name, (N, K) in shapes.items():
         if a.only and name not in a.only.split(","):
             continue
-        ring = max(2, int(1.0e9 // (N * K * 2)))
+        ring = a.ring or max(2, int(1.0e9 // (N * K * 2)))
         ws = [(torch.randn(N, K, device=dev) * 0.02).to(bf) for _ in range(ring)]
         for M in (int(v) for v in a.ms.split(",")):
             x = torch.randn(M, K, device=dev).to(bf)
