@@ -498,9 +498,31 @@ def main():
                 i = (step * world + rank) * args.docs + d
                 doc_prod.write(_rec(balanced_key(f"doc-{i}", i % d_parts, d_parts), make_page(i, corpus)))
 
+    def thread_cpu():
+        out = {}
+        for th in threading.enumerate():
+            try:
+                out[th.name] = time.clock_gettime(time.pthread_getcpuclockid(th.ident))
+            except (OSError, TypeError, AttributeError):
+                pass
+        return out
+
+    def cpu_window(store, delay):
+        # per-thread CPU seconds over the step's first `delay` s (the question front:
+        # embed -> kNN -> MMR -> prompt), top threads -- who competes for the GIL there
+        a = thread_cpu()
+        time.sleep(delay)
+        b = thread_cpu()
+        d = sorted(((round(1e3 * (b[k] - a.get(k, 0.0)), 1), k) for k in b), reverse=True)[:10]
+        store.append(d)
+
+    cpu_front = []
+
     def run_step():
         step = steps_done[0]
         t0 = time.time()
+        if _composite.STAGE_TRACE is not None:
+            threading.Thread(target=cpu_window, args=(cpu_front, 0.6), daemon=True, name="cpu-window").start()
         publish_pages(step)
         step_keys = set()
         if args.load == "burst" or step == 0:
@@ -552,6 +574,9 @@ def main():
                                                 round(1e3 * (d - c), 1), n] for a, b, c, d, n in list(_vs.SEARCH_TRACE)
                                                if a >= t0]
                 _vs.SEARCH_TRACE.clear()
+            if cpu_front:
+                # per-thread CPU ms over the first 0.6 s of the step: [[ms, thread], ...]
+                stage_trace[-1]["thread_cpu_ms_front"] = cpu_front.pop()
         return t_end - t0, lats
 
     def run_window(k_steps):

@@ -39,7 +39,7 @@ import numpy as np
 import torch
 
 from .. import ops
-from ..utils.gpu import aux_stream, on_search, to_host
+from ..utils.gpu import aux_stream, on_search, to_host, to_host_async
 
 log = logging.getLogger(__name__)
 
@@ -84,15 +84,26 @@ class _Persistence:
             self._wal = open(self.wal_path, "ab")
 
     def _append(self, entry) -> None:
-        self._open_wal()
+        self.append_packed(self.pack(entry))
+
+    @staticmethod
+    def pack(entry) -> bytes:
         b = msgpack.packb(entry, use_bin_type=True)
-        self._wal.write(len(b).to_bytes(4, "little") + b)
+        return len(b).to_bytes(4, "little") + b
+
+    def append_packed(self, b: bytes) -> None:
+        self._open_wal()
+        self._wal.write(b)
         self._wal.flush()
         if self.fsync:
             os.fsync(self._wal.fileno())
 
+    @classmethod
+    def pack_upsert(cls, ids, vecs_f32: np.ndarray, metas) -> bytes:
+        return cls.pack(("u", list(ids), vecs_f32.astype(np.float32).tobytes(), list(metas)))
+
     def log_upsert(self, ids, vecs_f32: np.ndarray, metas) -> None:
-        self._append(("u", list(ids), vecs_f32.astype(np.float32).tobytes(), list(metas)))
+        self.append_packed(self.pack_upsert(ids, vecs_f32, metas))
 
     def log_delete(self, ids) -> None:
         self._append(("d", list(ids)))
@@ -217,6 +228,7 @@ class VectorStore:
         self._row: Dict[Any, int] = {}
         self.lock = threading.RLock()
         self._write_ev = None   # recorded on the store stream after every device write
+        self._gen = 0           # bumped when deletes renumber rows (search re-resolves)
         self._persist = _Persistence(persist_dir, fsync) if persist_dir else None
         if self._persist is not None:
             with on_search(self.device), self.lock:
@@ -268,10 +280,12 @@ class VectorStore:
         metadata = list(metadata) if metadata is not None else [{} for _ in ids]
         if len(metadata) != len(ids):
             raise ValueError("ids and metadata lengths differ")
+        if not (isinstance(vectors, torch.Tensor) and vectors.is_cuda):
+            self._upsert_host(ids, vectors, metadata)
+            return
         with on_search(self.device), self.lock:
-            if isinstance(vectors, torch.Tensor) and vectors.is_cuda:
-                # device vectors come from the embedding engine's auxiliary stream
-                torch.cuda.current_stream().wait_stream(aux_stream(self.device))
+            # device vectors come from the embedding engine's auxiliary stream
+            torch.cuda.current_stream().wait_stream(aux_stream(self.device))
             vecs = self._normalize(vectors)
             if vecs.shape[0] != len(ids):
                 raise ValueError("ids and vectors lengths differ")
@@ -280,6 +294,28 @@ class VectorStore:
             self._apply_upsert(ids, vecs, metadata)
             self._mark_written()
             self._maybe_compact()
+
+    def _upsert_host(self, ids, vectors, metadata) -> None:
+        """Host vectors (lists from records): normalisation, the store-dtype rounding, the
+        WAL entry and the pinned upload are prepared before the store lock is taken, so
+        the lock covers only the WAL append and the device scatter -- a search waits for
+        a few calls instead of the whole upsert (every torch call is a GIL hand-off, and
+        on a busy process each hand-off can wait behind other threads)."""
+        host = self._normalize_host(vectors)
+        if host.shape[0] != len(ids):
+            raise ValueError("ids and vectors lengths differ")
+        t = torch.from_numpy(np.ascontiguousarray(host, dtype=np.float32)).to(self.dtype)
+        entry = (_Persistence.pack_upsert(ids, t.float().numpy(), metadata)
+                 if self._persist is not None else None)
+        with on_search(self.device):
+            if self.device.type == "cuda":
+                t = t.pin_memory().to(self.device, non_blocking=True)
+            with self.lock:
+                if entry is not None:
+                    self._persist.append_packed(entry)
+                self._apply_upsert(ids, t, metadata)
+                self._mark_written()
+                self._maybe_compact()
 
     def _apply_upsert(self, ids, vecs: torch.Tensor, metadata) -> None:
         new_rows = {i for i in ids if i not in self._row}
@@ -319,6 +355,7 @@ class VectorStore:
 
     def _apply_delete(self, ids) -> int:
         """Remove rows in one device copy: the surviving tail rows fill the holes."""
+        self._gen += 1   # row numbers change: a search between its top-k and its payloads redoes
         dead = {self._row.pop(k) for k in ids}
         m = len(dead)
         keep_n = self._n - m
@@ -431,19 +468,37 @@ class VectorStore:
         # 26 ms per round in the RAG bench where this one took 30-170 ms per batch:
         # profiles/r5/bench_stage_trace_r5j.log vs knn_w8load_r5o.log)
         qn = self._normalize_host(queries)
+        # The lock is held while work is ENQUEUED, not while the GPU runs it: the top-k and
+        # its D2H copy are enqueued under the lock and waited for outside it; the row
+        # numbers are then resolved under the lock again, unless a delete renumbered the
+        # rows in between (generation check -> search again).  Writes go to the same
+        # search stream, so the device reads are ordered against them either way.
         with on_search(self.device):
-            with self.lock:
-                t_lk = time.time() if tr is not None else 0.0
-                q = self._to_device_query(qn)
-                s, idx = self.topk_rows(q, k)
-                s, idx = (t.tolist() for t in to_host(s, idx))
+            q = self._to_device_query(qn)
+            while True:
+                with self.lock:
+                    t_lk = time.time() if tr is not None else 0.0
+                    gen = self._gen
+                    (hs, hi), ev = to_host_async(*self.topk_rows(q, k))
+                if ev is not None:
+                    ev.synchronize()
+                s, idx = hs.tolist(), hi.tolist()
                 t_gpu = time.time() if tr is not None else 0.0
-                # what depends on the row numbering is read under the lock; the result
-                # objects are built after it is released
-                hits = [[(sc, r, self.row_payload(r)) for sc, r in zip(srow, irow) if 0 <= r < self._n]
-                        for srow, irow in zip(s, idx)]
-                vec_rows = (self.row_vectors_array({r for row in hits for _, r, _ in row})
+                with self.lock:
+                    if self._gen != gen:
+                        continue
+                    hits = [[(sc, r, self.row_payload(r)) for sc, r in zip(srow, irow) if 0 <= r < self._n]
+                            for srow, irow in zip(s, idx)]
+                    pend = (self._gather_rows_async({r for row in hits for _, r, _ in row})
                             if with_vectors else None)
+                break
+            vec_rows = None
+            if pend is not None:
+                flat, outs, ev = pend
+                if ev is not None:
+                    ev.synchronize()
+                vec_rows = (flat, outs[0].numpy() if flat else np.zeros((0, self.dim), np.float32))
+        # the result objects are built after the lock is released
         out = self._build_results(hits, vec_rows)
         if tr is not None:
             tr.append((t_in, t_lk, t_gpu, time.time(), len(out)))
@@ -511,6 +566,17 @@ class VectorStore:
             return {}
         from ..utils.fastjson import f32_rows   # native rows of float32 values
         return dict(zip(flat, f32_rows(arr)))
+
+    def _gather_rows_async(self, rows):
+        """(sorted rows, [pinned f32 copy], event) of the given rows: the device gather and
+        its D2H copy enqueued on the search stream (caller holds ``lock``)."""
+        flat = sorted(rows)
+        if not flat:
+            return flat, [], None
+        with on_search(self.device):
+            self._order_read()
+            outs, ev = to_host_async(self._vecs[torch.tensor(flat, device=self.device)].float())
+        return flat, outs, ev
 
     def row_vectors_array(self, rows):
         """(sorted rows, float32 numpy [n, dim]): one device gather + one D2H copy, no

@@ -68,6 +68,22 @@ def on_search(device):
         yield s
 
 
+def to_host_async(*tensors: torch.Tensor):
+    """(pinned host copies, event): the D2H copies enqueued on the current stream; the
+    caller synchronises the event before reading the copies (possibly after releasing a
+    lock).  CPU tensors pass through with event None."""
+    if not tensors or not tensors[0].is_cuda:
+        return list(tensors), None
+    outs = []
+    for t in tensors:
+        h = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+        h.copy_(t, non_blocking=True)
+        outs.append(h)
+    ev = torch.cuda.Event(blocking=True)
+    ev.record()
+    return outs, ev
+
+
 def to_host(*tensors: torch.Tensor) -> List[torch.Tensor]:
     """D2H copies of the given device tensors (enqueued on the current stream) into
     pinned buffers; waits with a blocking event.  CPU tensors pass through."""

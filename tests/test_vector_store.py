@@ -65,6 +65,41 @@ def test_batched_delete_keeps_dense_rows_consistent():
     assert s.get(1) == {"v": 6}
 
 
+def test_search_redoes_payloads_when_a_delete_renumbers_rows(monkeypatch):
+    """A search enqueues its top-k under the store lock and waits for it outside; a
+    delete landing in that window renumbers rows, so the search must resolve its row
+    numbers again instead of returning the payloads of the rows that moved in."""
+    import langstream_amd.engine.vector_store as vs
+    g = torch.Generator().manual_seed(3)
+    vecs = torch.randn(30, 32, generator=g)
+    s = VectorStore(32, device="cpu", dtype=torch.float32)
+    s.upsert(list(range(30)), vecs.tolist(), [{"i": i} for i in range(30)])
+    real = vs.to_host_async
+    calls = {"n": 0}
+
+    def racing(*t):
+        calls["n"] += 1
+        out = real(*t)
+        if calls["n"] == 1:
+            s.delete([0, 1, 2])   # another thread's delete between top-k and payloads
+        return out
+
+    topk = {"n": 0}
+    real_topk = s.topk_rows
+
+    def counted(*a):
+        topk["n"] += 1
+        return real_topk(*a)
+
+    monkeypatch.setattr(vs, "to_host_async", racing)
+    monkeypatch.setattr(s, "topk_rows", counted)
+    res = s.search([vecs[25].tolist(), vecs[0].tolist()], 3, with_vectors=True)
+    assert topk["n"] == 2   # the top-k ran again after the renumbering
+    assert res[0][0]["id"] == 25 and res[0][0]["i"] == 25
+    assert all(d["id"] == d["i"] and d["id"] not in (0, 1, 2) for r in res for d in r)
+    assert np.allclose(res[0][0]["vector"], torch.nn.functional.normalize(vecs[25], dim=0).numpy(), atol=1e-6)
+
+
 def test_wal_and_snapshot_restore(tmp_path):
     d = str(tmp_path / "coll")
     g = torch.Generator().manual_seed(3)

@@ -1,6 +1,6 @@
 """Search latency under LLM load: a vector-store search on the high-priority search
 stream while the default stream runs back-to-back large GEMMs (a prefill step's worth,
-~150 ms), with the D2H of results through freshly allocated pinned buffers
+~150 ms) -- or the high-priority auxiliary stream or a pool stream runs them -- with the D2H of results through freshly allocated pinned buffers
 (utils/gpu.to_host), through a reused pinned buffer, and through pageable memory.
 
 usage (GPU): python tools/search_latency_probe.py
@@ -36,18 +36,25 @@ def main() -> int:
     wg = torch.randn(2 * 14336, 4096, device=dev, dtype=torch.bfloat16)
     kind = {"k": "matmul"}
 
+    side = torch.cuda.Stream()
+
     def load(stop):
-        while not stop.is_set():
-            for _ in range(40):
-                if kind["k"] == "matmul":
-                    torch.matmul(a, w.t())
-                else:   # the engine's prefill gate_up kernel: 160 KB of LDS per workgroup
-                    ops.gemm_prefill(a, wg, silu=True)
-            torch.cuda.synchronize()
+        # the load's stream: the default stream (the LLM engine's), the high-priority
+        # auxiliary stream (ingest embeddings / upserts), or a pool stream
+        st = {"aux": gpu.aux_stream(dev), "side": side}.get(kind.get("stream"), torch.cuda.current_stream())
+        with torch.cuda.stream(st):
+            while not stop.is_set():
+                for _ in range(40):
+                    if kind["k"] == "matmul":
+                        torch.matmul(a, w.t())
+                    else:   # the engine's prefill gate_up kernel: 160 KB of LDS per workgroup
+                        ops.gemm_prefill(a, wg, silu=True)
+                torch.cuda.synchronize()
 
     res = {}
-    for mode in ("idle", "loaded", "loaded_pp"):
+    for mode in ("idle", "loaded", "loaded_pp", "loaded_aux", "loaded_side"):
         kind["k"] = "pp" if mode == "loaded_pp" else "matmul"
+        kind["stream"] = mode[len("loaded_"):] if mode in ("loaded_aux", "loaded_side") else None
         stop = threading.Event()
         th = threading.Thread(target=load, args=(stop,), daemon=True)
         if mode != "idle":
