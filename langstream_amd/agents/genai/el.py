@@ -22,6 +22,8 @@ import uuid
 from decimal import Decimal
 from typing import Any, Callable, Dict, List, Optional
 
+from ...api import temporal as _temporal
+
 # ---------------------------------------------------------------- lexer
 _TOKEN = re.compile(r"""
     (?P<ws>\s+)
@@ -309,6 +311,8 @@ def eval_predicate(expr: Optional[str], ctx: Dict[str, Any]) -> bool:
 def _fn_tostring(v) -> str:
     if v is None:
         return ""
+    if isinstance(v, _TEMPORAL_TYPES):
+        return _temporal.to_java_string(v)
     if isinstance(v, bytes):
         return v.decode("utf-8", errors="replace")
     if isinstance(v, bool):
@@ -480,6 +484,8 @@ def _fn_list_to_list_of_structs(lst, field):
 
 
 _EPOCH = _dt.datetime(1970, 1, 1, tzinfo=_dt.timezone.utc)
+_TEMPORAL_TYPES = (_temporal.JDate, _temporal.Timestamp, _temporal.Time, _temporal.Instant, _temporal.LocalTime,
+                   _temporal.LocalDateTime, _temporal.OffsetDateTime)
 
 
 def _dt_millis(d: "_dt.datetime") -> int:
@@ -498,6 +504,9 @@ def _to_millis(v) -> int:
         return int(v)
     if isinstance(v, _dt.datetime):
         return _dt_millis(v)
+    if isinstance(v, (_temporal.JDate, _temporal.Timestamp, _temporal.Instant, _temporal.LocalDateTime,
+                      _temporal.OffsetDateTime)) or (isinstance(v, _dt.date) and not isinstance(v, _dt.datetime)):
+        return _temporal.coerce(v, "instant").to_epoch_milli()   # the cast step's date-time values
     if isinstance(v, (bytes, bytearray)):
         v = v.decode()
     if isinstance(v, str):

@@ -19,6 +19,7 @@ from concurrent.futures import Future
 from typing import Any, Callable, Dict, List, Optional
 
 from ...api.util import OrderedAsyncBatchExecutor
+from ...api import temporal as _temporal
 from ...api.types import Float32, Int8, Int16, Int32
 from .el import eval_expression, eval_predicate
 from .mustache import compile_template
@@ -102,12 +103,27 @@ _CASTS: Dict[str, Callable[[Any], Any]] = {
 }
 
 
+# cast's schema types (config-schema.yaml Cast.schema-type) -> JstlTypeConverter targets
+_CAST_TYPES = ("bytes", "string", "int8", "int16", "int32", "int64", "float", "double", "boolean", "date",
+               "timestamp", "time", "local_date_time", "local_date", "local_time", "instant")
+
+
+def _cast_value(v, st: str):
+    """CastStep.convertValue: JstlTypeConverter.coerceToType to the schema type's Java
+    class (api/temporal.py); a struct value cast to STRING is its JSON text."""
+    if st == "string" and isinstance(v, (dict, list)):
+        return json.dumps(v)
+    return _temporal.coerce(v, st)
+
+
 class CastStep(Step):
     def process(self, rec):
-        st = str(self.cfg.get("schema-type", "string")).lower()
-        fn = _CASTS.get(st)
-        if fn is None:
+        st = str(self.cfg.get("schema-type", "string")).strip().lower().replace("-", "_")
+        if st not in _CAST_TYPES:
             raise ValueError(f"Unsupported schema-type {st}")
+
+        def fn(v, st=st):
+            return _cast_value(v, st)
         part = self.cfg.get("part")
         if part in (None, "key") and rec.key is not None:
             rec.key = fn(rec.key)

@@ -27,9 +27,13 @@ import json
 import struct
 from typing import Any, Dict, Optional, Tuple
 
-from ...api import avro
+import datetime as _dt
 
-PRIMITIVE_TYPES = ("STRING", "BYTES", "BOOLEAN", "INT8", "INT16", "INT32", "INT64", "FLOAT", "DOUBLE")
+from ...api import avro, temporal
+from ...api.types import Float32, Int8, Int16, Int32
+
+TEMPORAL_TYPES = ("DATE", "TIME", "TIMESTAMP", "INSTANT", "LOCAL_DATE", "LOCAL_TIME", "LOCAL_DATE_TIME")
+PRIMITIVE_TYPES = ("STRING", "BYTES", "BOOLEAN", "INT8", "INT16", "INT32", "INT64", "FLOAT", "DOUBLE") + TEMPORAL_TYPES
 _FMT = {"INT8": ">b", "INT16": ">h", "INT32": ">i", "INT64": ">q", "FLOAT": ">f", "DOUBLE": ">d"}
 
 
@@ -91,6 +95,14 @@ class PulsarSchema:
                 return struct.pack(_FMT[t], x)
             except (TypeError, ValueError, struct.error) as e:
                 raise SchemaError(f"cannot encode {v!r} as {t}: {e}") from e
+        if t in TEMPORAL_TYPES:
+            # Pulsar's DateSchema / TimeSchema / TimestampSchema (int64 millis), InstantSchema
+            # (int64 s + int32 nanos), LocalDate / LocalTime / LocalDateTime schemas (epoch
+            # day, nano of day) -- the value converted to the type first (JstlTypeConverter)
+            try:
+                return temporal.encode_bytes(temporal.coerce(v, t))
+            except ValueError as e:
+                raise SchemaError(f"cannot encode {v!r} as {t}: {e}") from e
         if t == "JSON":
             if isinstance(v, (bytes, bytearray)):
                 v = v.decode()
@@ -123,6 +135,11 @@ class PulsarSchema:
             if len(b) != struct.calcsize(_FMT[t]):
                 raise SchemaError(f"{t} payload of {len(b)} bytes")
             return struct.unpack(_FMT[t], b)[0]
+        if t in TEMPORAL_TYPES:
+            try:
+                return temporal.decode_bytes(b, t.lower())
+            except ValueError as e:
+                raise SchemaError(f"{t} payload: {e}") from e
         if t == "JSON":
             return json.loads(b.decode())
         if t == "AVRO":
@@ -209,6 +226,14 @@ class TopicSchema:
         return key, value
 
 
+# Java classes of BASE_SCHEMAS that Python values carry as tags (api/types.py,
+# api/temporal.py): Byte / Short / Integer / Float and the date-time classes
+_TAGGED = ((Int8, "INT8"), (Int16, "INT16"), (Int32, "INT32"), (Float32, "FLOAT"),
+           (temporal.JDate, "DATE"), (temporal.Timestamp, "TIMESTAMP"), (temporal.Time, "TIME"),
+           (temporal.Instant, "INSTANT"), (temporal.LocalTime, "LOCAL_TIME"),
+           (temporal.LocalDateTime, "LOCAL_DATE_TIME"))
+
+
 def infer(key: Any, value: Any) -> TopicSchema:
     """``BASE_SCHEMAS`` by the record's Python types (JSON-ish values: a str schema with
     JSON text -- the reference's ``getSchema`` has no entry for maps)."""
@@ -217,10 +242,15 @@ def infer(key: Any, value: Any) -> TopicSchema:
             return PulsarSchema("BYTES")
         if isinstance(v, bool):
             return PulsarSchema("BOOLEAN")
+        for cls, name in _TAGGED:
+            if isinstance(v, cls):
+                return PulsarSchema(name)
         if isinstance(v, int):
             return PulsarSchema("INT32" if -(1 << 31) <= v < (1 << 31) else "INT64")
         if isinstance(v, float):
             return PulsarSchema("DOUBLE")
+        if isinstance(v, _dt.date) and not isinstance(v, _dt.datetime):
+            return PulsarSchema("LOCAL_DATE")
         return PulsarSchema("STRING")
     if key is None:
         return TopicSchema(one(value))

@@ -10,6 +10,7 @@ the formatting time, and the same float32 after parsing.  Everywhere else it is 
 list (json.dumps, msgpack, EL, the vector stores)."""
 from __future__ import annotations
 
+import datetime as _dt
 import json
 from typing import Any
 
@@ -53,6 +54,20 @@ def _load():
         _native, _unsupported = False, None
 
 
+def _default(o: Any) -> Any:
+    """Values the JSON writer has no form for: the Java date-time types of
+    api/temporal.py -- java.util.Date / Timestamp / Time as epoch millis (Jackson's default
+    for Date), the java.time ones as their ISO text."""
+    from ..api import temporal
+    if isinstance(o, (temporal.JDate, temporal.Timestamp, temporal.Time)):
+        return o.get_time()
+    if isinstance(o, (temporal.Instant, temporal.LocalTime, temporal.LocalDateTime, temporal.OffsetDateTime)):
+        return str(o)
+    if isinstance(o, (_dt.date, _dt.time)):
+        return o.isoformat()
+    raise TypeError(f"Object of type {type(o).__name__} is not JSON serializable")
+
+
 def dumps(obj: Any) -> str:
     if _native is None:
         _load()
@@ -61,4 +76,4 @@ def dumps(obj: Any) -> str:
             return _native(obj)
         except _unsupported:
             pass
-    return json.dumps(obj)
+    return json.dumps(obj, default=_default)

@@ -1,0 +1,399 @@
+"""Type-converter parity vectors ported from the reference's own tests.
+
+* ``JstlTypeConverterTest.java`` (langstream-ai-agents/src/test/.../jstl/): every
+  (input, target class, expected) row of ``conversions()`` plus ``testNullConversion``,
+  against ``api/temporal.coerce`` -- the converter the cast step uses.  Java classes map to
+  Python types as api/temporal.py's table says; ``Utf8`` rows use ``str`` (Python has no
+  separate Avro string type).
+* ``CastStepTest.java``: ``testPrimitiveSchemaTypes`` (a STRING value cast to each schema
+  type) and ``testKeyValueAvroToString`` through the ``cast`` step itself.
+
+Schema.X.encode(...) expectations are written out as the big-endian layouts of
+``BytesConverter`` (= Pulsar's schema encodings)."""
+import datetime as dt
+import struct
+from decimal import Decimal
+
+import numpy as np
+import pytest
+
+from langstream_amd.api.record import SimpleRecord
+from langstream_amd.api.temporal import (Instant, JDate, LocalDateTime, LocalTime, OffsetDateTime, Time,
+                                         Timestamp, coerce)
+from langstream_amd.api.types import Float32, Int8, Int16, Int32
+
+# JstlTypeConverterTest.conversions(): the fixture values (TimeZone UTC)
+BYTE, SHORT, INT, LONG = Int8(42), Int16(42), Int32(42), 42
+FLOAT, DOUBLE = Float32(float(np.float32(42.8))), 42.8
+DATE_TIME_MILLIS, MIDNIGHT_MILLIS, NUMBER_OF_DAYS = 1672700645000, 1672617600000, 19359
+TIME_MILLIS, TIME_MILLIS_WITH_NANOS = 83045000, 83045000.000006
+DATE = JDate(DATE_TIME_MILLIS)
+INSTANT = Instant(1672700645, 6)
+TIMESTAMP = Timestamp(1672700645, 6)
+LOCAL_DATE = dt.date(2023, 1, 2)
+LOCAL_TIME = LocalTime.of(23, 4, 5, 6)
+LOCAL_DATE_TIME = LocalDateTime(LOCAL_DATE, LOCAL_TIME)
+OFFSET_DATE_TIME = OffsetDateTime(LOCAL_DATE_TIME, 0)
+TIME = Time(TIME_MILLIS)
+LOCAL_DATE_TIME_WITHOUT_NANOS = LocalDateTime(LOCAL_DATE, LocalTime.of(23, 4, 5))
+BIG_INTEGER = 345781342432523452345
+BIG_DECIMAL = Decimal("435897983457.83421")
+INT_MAX, LONG_MAX = Int32(2**31 - 1), 2**63 - 1
+FLOAT_MAX = Float32(float(np.finfo(np.float32).max))
+DOUBLE_MAX = float(np.finfo(np.float64).max)
+
+
+def i64(v):
+    return struct.pack(">q", v)
+
+
+LDT_BYTES = struct.pack(">qq", NUMBER_OF_DAYS, LOCAL_TIME.nano_of_day)
+INSTANT_BYTES = struct.pack(">qi", 1672700645, 6)
+
+# (input, target, expected, java class name of the target)
+CONVERSIONS = [
+    # Bytes
+    (b"\x01\x02\x03", "bytes", b"\x01\x02\x03"),
+    ("test", "bytes", b"test"),
+    (True, "bytes", b"\x01"),
+    (BYTE, "bytes", b"\x2a"),
+    (SHORT, "bytes", struct.pack(">h", 42)),
+    (INT, "bytes", struct.pack(">i", 42)),
+    (LONG, "bytes", i64(42)),
+    (FLOAT, "bytes", struct.pack(">f", 42.8)),
+    (DOUBLE, "bytes", struct.pack(">d", 42.8)),
+    (DATE, "bytes", i64(DATE_TIME_MILLIS)),
+    (TIMESTAMP, "bytes", i64(DATE_TIME_MILLIS)),
+    (TIME, "bytes", i64(TIME_MILLIS)),
+    (LOCAL_DATE_TIME, "bytes", LDT_BYTES),
+    (INSTANT, "bytes", INSTANT_BYTES),
+    (OFFSET_DATE_TIME, "bytes", INSTANT_BYTES),
+    (LOCAL_DATE, "bytes", i64(NUMBER_OF_DAYS)),
+    (LOCAL_TIME, "bytes", i64(LOCAL_TIME.nano_of_day)),
+    # String
+    (b"test", "string", "test"),
+    ("test", "string", "test"),
+    (True, "string", "true"),
+    (BYTE, "string", "42"),
+    (SHORT, "string", "42"),
+    (INT, "string", "42"),
+    (LONG, "string", "42"),
+    (FLOAT, "string", "42.8"),
+    (DOUBLE, "string", "42.8"),
+    (DATE, "string", "2023-01-02T23:04:05Z"),
+    (TIMESTAMP, "string", "2023-01-02T23:04:05.000000006Z"),
+    (TIME, "string", "23:04:05"),
+    (LOCAL_DATE_TIME, "string", "2023-01-02T23:04:05.000000006"),
+    (INSTANT, "string", "2023-01-02T23:04:05.000000006Z"),
+    (OFFSET_DATE_TIME, "string", "2023-01-02T23:04:05.000000006Z"),
+    (LOCAL_DATE, "string", "2023-01-02"),
+    (LOCAL_TIME, "string", "23:04:05.000000006"),
+    # Utf8String (Avro Utf8 -> str here)
+    ("test", "string", "test"),
+    ("1", "int32", Int32(1)),
+    # Boolean
+    (b"\x2a", "boolean", True),
+    ("true", "boolean", True),
+    (True, "boolean", True),
+    # Byte
+    (b"\x2a", "int8", BYTE),
+    ("42", "int8", BYTE),
+    (BYTE, "int8", BYTE),
+    (SHORT, "int8", BYTE),
+    (INT, "int8", BYTE),
+    (LONG, "int8", BYTE),
+    (FLOAT, "int8", BYTE),
+    (DOUBLE, "int8", BYTE),
+    # Short
+    (struct.pack(">h", 42), "int16", SHORT),
+    ("42", "int16", SHORT),
+    (BYTE, "int16", SHORT),
+    (SHORT, "int16", SHORT),
+    (INT, "int16", SHORT),
+    (LONG, "int16", SHORT),
+    (FLOAT, "int16", SHORT),
+    (DOUBLE, "int16", SHORT),
+    # Integer
+    (struct.pack(">i", 42), "int32", INT),
+    ("42", "int32", INT),
+    (BYTE, "int32", INT),
+    (SHORT, "int32", INT),
+    (INT, "int32", INT),
+    (LONG, "int32", INT),
+    (FLOAT, "int32", INT),
+    (DOUBLE, "int32", INT),
+    (LOCAL_DATE, "int32", Int32(NUMBER_OF_DAYS)),
+    # Long
+    (i64(42), "int64", LONG),
+    ("42", "int64", LONG),
+    (BYTE, "int64", LONG),
+    (SHORT, "int64", LONG),
+    (INT, "int64", LONG),
+    (LONG, "int64", LONG),
+    (FLOAT, "int64", LONG),
+    (DOUBLE, "int64", LONG),
+    (DATE, "int64", DATE_TIME_MILLIS),
+    (TIMESTAMP, "int64", DATE_TIME_MILLIS),
+    (TIME, "int64", TIME_MILLIS),
+    (LOCAL_DATE_TIME, "int64", DATE_TIME_MILLIS),
+    (INSTANT, "int64", DATE_TIME_MILLIS),
+    (OFFSET_DATE_TIME, "int64", DATE_TIME_MILLIS),
+    (LOCAL_TIME, "int64", TIME_MILLIS),
+    (LOCAL_DATE, "int64", NUMBER_OF_DAYS),
+    # Float
+    (struct.pack(">f", 42.8), "float", FLOAT),
+    ("42.8", "float", FLOAT),
+    (BYTE, "float", Float32(42.0)),
+    (SHORT, "float", Float32(42.0)),
+    (INT, "float", Float32(42.0)),
+    (LONG, "float", Float32(42.0)),
+    (FLOAT, "float", FLOAT),
+    (DOUBLE, "float", FLOAT),
+    (LOCAL_DATE, "float", Float32(float(NUMBER_OF_DAYS))),
+    # Double
+    (struct.pack(">d", 42.8), "double", DOUBLE),
+    ("42.8", "double", DOUBLE),
+    (BYTE, "double", 42.0),
+    (SHORT, "double", 42.0),
+    (INT, "double", 42.0),
+    (LONG, "double", 42.0),
+    (FLOAT, "double", float(FLOAT)),
+    (DOUBLE, "double", DOUBLE),
+    (DATE, "double", float(DATE_TIME_MILLIS)),
+    (TIMESTAMP, "double", float(DATE_TIME_MILLIS)),
+    (TIME, "double", float(TIME_MILLIS)),
+    (LOCAL_DATE_TIME, "double", float(DATE_TIME_MILLIS)),
+    (INSTANT, "double", float(DATE_TIME_MILLIS)),
+    (OFFSET_DATE_TIME, "double", float(DATE_TIME_MILLIS)),
+    (LOCAL_TIME, "double", TIME_MILLIS_WITH_NANOS),
+    (LOCAL_DATE, "double", float(NUMBER_OF_DAYS)),
+    # Date
+    (i64(DATE_TIME_MILLIS), "date", DATE),
+    ("2023-01-02T23:04:05.000000006Z", "date", DATE),
+    (DATE_TIME_MILLIS, "date", DATE),
+    (float(DATE_TIME_MILLIS), "date", DATE),
+    (DATE, "date", DATE),
+    (TIMESTAMP, "date", DATE),
+    (LOCAL_DATE_TIME, "date", DATE),
+    (INSTANT, "date", DATE),
+    (OFFSET_DATE_TIME, "date", DATE),
+    (LOCAL_DATE, "date", JDate(MIDNIGHT_MILLIS)),
+    # Timestamp
+    (i64(DATE_TIME_MILLIS), "timestamp", Timestamp.of_millis(DATE_TIME_MILLIS)),
+    ("2023-01-02T23:04:05.000000006Z", "timestamp", TIMESTAMP),
+    (DATE_TIME_MILLIS, "timestamp", Timestamp.of_millis(DATE_TIME_MILLIS)),
+    (float(DATE_TIME_MILLIS), "timestamp", Timestamp.of_millis(DATE_TIME_MILLIS)),
+    (DATE, "timestamp", Timestamp.of_millis(DATE_TIME_MILLIS)),
+    (TIMESTAMP, "timestamp", TIMESTAMP),
+    (LOCAL_DATE_TIME, "timestamp", TIMESTAMP),
+    (INSTANT, "timestamp", TIMESTAMP),
+    (OFFSET_DATE_TIME, "timestamp", TIMESTAMP),
+    (OFFSET_DATE_TIME, "timestamp", TIMESTAMP),
+    (LOCAL_DATE, "timestamp", Timestamp.of_millis(MIDNIGHT_MILLIS)),
+    # Time
+    (i64(TIME_MILLIS), "time", TIME),
+    ("23:04:05.000000006", "time", TIME),
+    (DATE_TIME_MILLIS, "time", Time(DATE_TIME_MILLIS)),
+    (float(DATE_TIME_MILLIS), "time", Time(DATE_TIME_MILLIS)),
+    (DATE, "time", Time(DATE_TIME_MILLIS)),
+    (TIMESTAMP, "time", TIME),
+    (LOCAL_DATE_TIME, "time", TIME),
+    (INSTANT, "time", TIME),
+    (OFFSET_DATE_TIME, "time", TIME),
+    (LOCAL_DATE, "time", Time(MIDNIGHT_MILLIS)),
+    (TIME, "time", TIME),
+    (LOCAL_TIME, "time", TIME),
+    # LocalTime
+    (i64(LOCAL_TIME.nano_of_day), "local_time", LOCAL_TIME),
+    ("23:04:05.000000006", "local_time", LOCAL_TIME),
+    (DATE_TIME_MILLIS, "local_time", LocalTime.of(23, 4, 5)),
+    (TIME_MILLIS_WITH_NANOS, "local_time", LOCAL_TIME),
+    (DATE, "local_time", LocalTime.of(23, 4, 5)),
+    (TIMESTAMP, "local_time", LOCAL_TIME),
+    (LOCAL_DATE_TIME, "local_time", LOCAL_TIME),
+    (INSTANT, "local_time", LOCAL_TIME),
+    (OFFSET_DATE_TIME, "local_time", LOCAL_TIME),
+    (LOCAL_DATE, "local_time", LocalTime(0)),
+    (TIME, "local_time", LocalTime.of(23, 4, 5)),
+    (LOCAL_TIME, "local_time", LOCAL_TIME),
+    # LocalDate
+    (i64(NUMBER_OF_DAYS), "local_date", LOCAL_DATE),
+    ("2023-01-02", "local_date", LOCAL_DATE),
+    (Int32(NUMBER_OF_DAYS), "local_date", LOCAL_DATE),
+    (NUMBER_OF_DAYS, "local_date", LOCAL_DATE),
+    (Float32(float(NUMBER_OF_DAYS)), "local_date", LOCAL_DATE),
+    (float(NUMBER_OF_DAYS), "local_date", LOCAL_DATE),
+    (DATE, "local_date", LOCAL_DATE),
+    (TIMESTAMP, "local_date", LOCAL_DATE),
+    (LOCAL_DATE_TIME, "local_date", LOCAL_DATE),
+    (INSTANT, "local_date", LOCAL_DATE),
+    (OFFSET_DATE_TIME, "local_date", LOCAL_DATE),
+    (LOCAL_DATE, "local_date", LOCAL_DATE),
+    # LocalDateTime
+    (LDT_BYTES, "local_date_time", LOCAL_DATE_TIME),
+    ("2023-01-02T23:04:05.000000006", "local_date_time", LOCAL_DATE_TIME),
+    (float(DATE_TIME_MILLIS), "local_date_time", LOCAL_DATE_TIME_WITHOUT_NANOS),
+    (DATE, "local_date_time", LOCAL_DATE_TIME_WITHOUT_NANOS),
+    (TIMESTAMP, "local_date_time", LOCAL_DATE_TIME),
+    (LOCAL_DATE_TIME, "local_date_time", LOCAL_DATE_TIME),
+    (INSTANT, "local_date_time", LOCAL_DATE_TIME),
+    (OFFSET_DATE_TIME, "local_date_time", LOCAL_DATE_TIME),
+    (LOCAL_DATE, "local_date_time", LocalDateTime(LOCAL_DATE, LocalTime(0))),
+    # Instant
+    (INSTANT_BYTES, "instant", INSTANT),
+    ("2023-01-02T23:04:05.000000006Z", "instant", INSTANT),
+    ("2023-01-02", "instant", Instant(1672617600)),
+    (DATE_TIME_MILLIS, "instant", Instant.of_epoch_milli(DATE_TIME_MILLIS)),
+    (float(DATE_TIME_MILLIS), "instant", Instant.of_epoch_milli(DATE_TIME_MILLIS)),
+    (DATE, "instant", Instant.of_epoch_milli(DATE_TIME_MILLIS)),
+    (TIMESTAMP, "instant", INSTANT),
+    (LOCAL_DATE_TIME, "instant", INSTANT),
+    (INSTANT, "instant", INSTANT),
+    (OFFSET_DATE_TIME, "instant", INSTANT),
+    (LOCAL_DATE, "instant", Instant(1672617600)),   # instant.truncatedTo(DAYS)
+    # OffsetDateTime
+    (INSTANT_BYTES, "offset_date_time", OFFSET_DATE_TIME),
+    ("2023-01-02T23:04:05.000000006Z", "offset_date_time", OFFSET_DATE_TIME),
+    ("2023-01-02", "offset_date_time", OffsetDateTime(LocalDateTime(LOCAL_DATE, LocalTime(0)), 0)),
+    (DATE_TIME_MILLIS, "offset_date_time", OffsetDateTime(LOCAL_DATE_TIME_WITHOUT_NANOS, 0)),
+    (float(DATE_TIME_MILLIS), "offset_date_time", OffsetDateTime(LOCAL_DATE_TIME_WITHOUT_NANOS, 0)),
+    (DATE, "offset_date_time", OffsetDateTime(LOCAL_DATE_TIME_WITHOUT_NANOS, 0)),
+    (TIMESTAMP, "offset_date_time", OFFSET_DATE_TIME),
+    (LOCAL_DATE_TIME, "offset_date_time", OFFSET_DATE_TIME),
+    (OFFSET_DATE_TIME, "offset_date_time", OFFSET_DATE_TIME),
+    (LOCAL_DATE, "offset_date_time", OffsetDateTime(LocalDateTime(LOCAL_DATE, LocalTime(0)), 0)),
+    (INSTANT, "offset_date_time", OFFSET_DATE_TIME),
+    # BigInteger
+    (BIG_INTEGER, "big_integer", BIG_INTEGER),
+    ("345781342432523452345", "big_integer", BIG_INTEGER),
+    (INT_MAX, "big_integer", 2**31 - 1),
+    (LONG_MAX, "big_integer", LONG_MAX),
+    # BigDecimal
+    (BIG_DECIMAL, "big_decimal", BIG_DECIMAL),
+    ("435897983457.83421", "big_decimal", BIG_DECIMAL),
+    (INT_MAX, "big_decimal", Decimal(2**31 - 1)),
+    (LONG_MAX, "big_decimal", Decimal(LONG_MAX)),
+    (FLOAT_MAX, "big_decimal", Decimal("3.4028234663852886E+38")),   # BigDecimal.valueOf(double)
+    (DOUBLE_MAX, "big_decimal", Decimal("1.7976931348623157E+308")),
+]
+
+# the Java class of each target, as Python types (JstlTypeConverterTest asserts
+# converted.getClass() == type)
+TYPE_OF = {"bytes": bytes, "string": str, "boolean": bool, "int8": Int8, "int16": Int16, "int32": Int32,
+           "int64": int, "float": Float32, "double": float, "date": JDate, "timestamp": Timestamp, "time": Time,
+           "local_time": LocalTime, "local_date": dt.date, "local_date_time": LocalDateTime, "instant": Instant,
+           "offset_date_time": OffsetDateTime, "big_integer": int, "big_decimal": Decimal}
+
+
+def test_null_conversion():
+    """JstlTypeConverterTest.testNullConversion."""
+    for t in TYPE_OF:
+        assert coerce(None, t) is None
+
+
+@pytest.mark.parametrize("value,target,expected", CONVERSIONS,
+                         ids=[f"{i}-{type(c[0]).__name__}-{c[1]}" for i, c in enumerate(CONVERSIONS)])
+def test_non_null_conversions(value, target, expected):
+    """JstlTypeConverterTest.testNonNullConversions."""
+    out = coerce(value, target)
+    assert type(out) is TYPE_OF[target]
+    if target == "time":   # "j.s.Time equality is weird": compared as LocalTime
+        assert out.to_local_time() == expected.to_local_time()
+    else:
+        assert out == expected, (out, expected)
+
+
+# ---------------------------------------------------------------- CastStepTest
+CAST_PRIMITIVES = [
+    ("test", "BYTES", b"test"),
+    ("true", "BOOLEAN", True),
+    ("42", "INT8", Int8(42)),
+    ("42", "INT32", Int32(42)),
+    ("42", "INT64", 42),
+    ("42.8", "FLOAT", FLOAT),
+    ("42.8", "DOUBLE", 42.8),
+    ("2023-01-02T22:04:05.000000006-01:00", "DATE", JDate(1672700645000)),
+    ("2023-01-02T22:04:05.000000006-01:00", "TIMESTAMP", Timestamp(1672700645, 6)),
+    ("23:04:05.000000006", "TIME", Time(83045000)),
+    ("2023-01-02T23:04:05.000000006", "LOCAL_DATE_TIME", LOCAL_DATE_TIME),
+    ("2023-01-02T22:04:05.000000006-01:00", "INSTANT", Instant(1672700645, 6)),
+    ("2023-01-02", "LOCAL_DATE", LOCAL_DATE),
+    ("23:04:05.000000006", "LOCAL_TIME", LOCAL_TIME),
+]
+
+
+def _cast(cfg, rec):
+    from langstream_amd.agents.genai.steps import CastStep
+    from langstream_amd.agents.genai.mutable import MutableRecord
+    mr = MutableRecord.from_record(rec)
+    CastStep(cfg).process(mr)
+    return mr
+
+
+@pytest.mark.parametrize("value,schema_type,expected", CAST_PRIMITIVES, ids=[c[1] for c in CAST_PRIMITIVES])
+def test_cast_primitive_schema_types(value, schema_type, expected):
+    """CastStepTest.testPrimitiveSchemaTypes: a STRING value cast to each schema type."""
+    out = _cast({"schema-type": schema_type}, SimpleRecord.of(None, value)).value
+    assert type(out) is type(expected)
+    assert out == expected
+
+
+def test_cast_key_value_struct_to_string():
+    """CastStepTest.testKeyValueAvroToString: both parts of a KeyValue record to STRING --
+    the struct's JSON text, as GenericRecord.toString writes it."""
+    key = {"keyField1": "key1", "keyField2": "key2", "keyField3": "key3"}
+    value = {"valueField1": "value1", "valueField2": "value2", "valueField3": "value3"}
+    mr = _cast({"schema-type": "STRING"}, SimpleRecord.of(key, value))
+    assert mr.key == '{"keyField1": "key1", "keyField2": "key2", "keyField3": "key3"}'
+    assert mr.value == '{"valueField1": "value1", "valueField2": "value2", "valueField3": "value3"}'
+
+
+def test_cast_rejects_struct_schema_types():
+    """CastStep.CastStepBuilder: AVRO / JSON / PROTOBUF / MAP are not cast targets."""
+    from langstream_amd.agents.genai.steps import CastStep
+    from langstream_amd.agents.genai.mutable import MutableRecord
+    for st in ("AVRO", "JSON", "MAP"):
+        with pytest.raises(ValueError):
+            CastStep({"schema-type": st}).process(MutableRecord(None, "x"))
+
+
+# ---------------------------------------------------------------- Pulsar schemas
+@pytest.mark.parametrize("stype,value,wire", [
+    ("DATE", DATE, i64(DATE_TIME_MILLIS)),
+    ("TIMESTAMP", TIMESTAMP, i64(DATE_TIME_MILLIS)),
+    ("TIME", TIME, i64(TIME_MILLIS)),
+    ("INSTANT", INSTANT, INSTANT_BYTES),
+    ("LOCAL_DATE", LOCAL_DATE, i64(NUMBER_OF_DAYS)),
+    ("LOCAL_TIME", LOCAL_TIME, i64(LOCAL_TIME.nano_of_day)),
+    ("LOCAL_DATE_TIME", LOCAL_DATE_TIME, LDT_BYTES),
+])
+def test_pulsar_temporal_schema_wire_forms(stype, value, wire):
+    """Pulsar's DATE / TIME / TIMESTAMP / INSTANT / LOCAL_* schemas carry the
+    BytesConverter layouts; the producer infers them from the value's Java type
+    (PulsarTopicConnectionsRuntimeProvider BASE_SCHEMAS)."""
+    from langstream_amd.topics.pulsar.schema import PulsarSchema, infer
+    s = PulsarSchema(stype)
+    assert s.encode(value) == wire
+    back = s.decode(wire)
+    if stype == "TIMESTAMP":   # Pulsar's TimestampSchema keeps millis
+        assert back == Timestamp.of_millis(DATE_TIME_MILLIS)
+    else:
+        assert back == value
+    assert infer(None, value).value.type == stype
+    # text is converted on the way in (a STRING field cast by the schema)
+    if stype in ("INSTANT", "LOCAL_DATE_TIME", "LOCAL_DATE", "LOCAL_TIME"):
+        assert s.encode(str(value)) == wire
+
+
+def test_pulsar_infers_tagged_numbers():
+    from langstream_amd.topics.pulsar.schema import infer
+    assert [infer(None, v).value.type for v in (BYTE, SHORT, INT, FLOAT, 42, 42.8)] == \
+        ["INT8", "INT16", "INT32", "FLOAT", "INT32", "DOUBLE"]
+
+
+def test_cast_then_expression_uses_the_date_time_value():
+    """A cast TIMESTAMP value feeds the expression language (fn:timestampAdd / toString)."""
+    from langstream_amd.agents.genai.el import eval_expression
+    mr = _cast({"schema-type": "TIMESTAMP"}, SimpleRecord.of(None, "2023-01-02T23:04:05.000000006Z"))
+    assert eval_expression("fn:timestampAdd(value, 1, 'seconds')", {"value": mr.value}) == DATE_TIME_MILLIS + 1000
+    assert eval_expression("fn:str(value)", {"value": mr.value}) == "2023-01-02T23:04:05.000000006Z"
