@@ -236,7 +236,15 @@ def _get(obj, key):
             if isinstance(parsed, dict):
                 return parsed.get(key)
         except ValueError:
-            return None
+            pass
+        # String's bean properties through the EL's BeanELResolver: 'x'.bytes (getBytes,
+        # UTF-8), 'x'.empty (isEmpty), 'x'.blank (isBlank)
+        if key == "bytes":
+            return obj.encode("utf-8")
+        if key == "empty":
+            return obj == ""
+        if key == "blank":
+            return obj.strip() == ""
         return None
     return getattr(obj, str(key), None)
 

@@ -157,33 +157,45 @@ class DropStep(Step):
         rec.drop = True
 
 
-_COMPUTE_TYPES = {
-    "STRING": lambda v: None if v is None else _CASTS["string"](v),
-    # width-tagged (api/types.py): a topic receives them as 1 / 2 / 4 / 8-byte and 4 / 8-byte
-    # Java-serialised numbers, like the reference's Byte / Short / Integer / Long / Float / Double
-    "INT8": lambda v: None if v is None else Int8(int(v)), "INT16": lambda v: None if v is None else Int16(int(v)),
-    "INT32": lambda v: None if v is None else Int32(int(v)), "INT64": lambda v: None if v is None else int(v),
-    "FLOAT": lambda v: None if v is None else Float32(float(v)), "DOUBLE": lambda v: None if v is None else float(v),
-    "BOOLEAN": lambda v: None if v is None else _CASTS["boolean"](v),
-    "BYTES": lambda v: None if v is None else _CASTS["bytes"](v),
-    "DATE": lambda v: None if v is None else _to_date(v), "TIME": lambda v: v,
-    "TIMESTAMP": lambda v: None if v is None else _to_ts(v), "INSTANT": lambda v: None if v is None else _to_ts(v),
-    "LOCAL_DATE": lambda v: None if v is None else _to_date(v), "LOCAL_TIME": lambda v: v,
-    "LOCAL_DATE_TIME": lambda v: None if v is None else _to_ts(v), "DATETIME": lambda v: None if v is None else
-    _to_ts(v), "DECIMAL": lambda v: v, "ARRAY": lambda v: v, "MAP": lambda v: v,
+# compute field type -> the Java class its expression is coerced to (ComputeField
+# .getJavaType: DATE is a LocalDate, DATETIME an Instant) as a JstlTypeConverter target
+_COMPUTE_TARGETS = {
+    "STRING": "string", "INT8": "int8", "INT16": "int16", "INT32": "int32", "INT64": "int64", "FLOAT": "float",
+    "DOUBLE": "double", "BOOLEAN": "boolean", "DATE": "local_date", "LOCAL_DATE": "local_date", "TIME": "time",
+    "LOCAL_TIME": "local_time", "LOCAL_DATE_TIME": "local_date_time", "DATETIME": "instant", "INSTANT": "instant",
+    "TIMESTAMP": "timestamp", "BYTES": "bytes", "DECIMAL": "big_decimal", "ARRAY": None, "MAP": None,
 }
+_COMPUTE_TYPES = _COMPUTE_TARGETS   # (the names a compute field may declare)
 
 
-def _to_ts(v):
-    if isinstance(v, (int, float)):
-        return _dt.datetime.fromtimestamp(v / 1000, tz=_dt.timezone.utc).isoformat()
-    return str(v)
+def _compute_value(v, t: Optional[str]):
+    """The field's value as the JstlEvaluator typed by the field returns it."""
+    if v is None or t is None:
+        return v
+    target = _COMPUTE_TARGETS[t]
+    if target is None:
+        return v
+    if target == "string" and isinstance(v, (dict, list)):
+        return json.dumps(v)
+    return _temporal.coerce(v, target)
 
 
-def _to_date(v):
-    if isinstance(v, (int, float)):
-        return _dt.datetime.fromtimestamp(v / 1000, tz=_dt.timezone.utc).date().isoformat()
-    return str(v)[:10]
+def _struct_value(v):
+    """A computed field written into a struct (key.x / value.x): the value in its Avro
+    form (ComputeStep.getAvroValue) -- Byte / Short as int, LocalDate / Date as epoch
+    days (date), Time / LocalTime as millis of day (time-millis), Timestamp / Instant /
+    LocalDateTime as epoch millis (timestamp-millis); other values as they are."""
+    if isinstance(v, (Int8, Int16)):
+        return int(v)
+    if isinstance(v, _dt.date) and not isinstance(v, _dt.datetime):
+        return Int32((v - _dt.date(1970, 1, 1)).days)
+    if isinstance(v, _temporal.JDate):
+        return Int32(v.millis // 86_400_000)
+    if isinstance(v, (_temporal.Time, _temporal.LocalTime)):
+        return _temporal.coerce(v, "int32")
+    if isinstance(v, (_temporal.Timestamp, _temporal.Instant, _temporal.LocalDateTime, _temporal.OffsetDateTime)):
+        return _temporal.coerce(v, "int64")
+    return v
 
 
 class ComputeStep(Step):
@@ -204,10 +216,11 @@ class ComputeStep(Step):
         results = []
         for name, expr, t, optional in self.fields:
             v = eval_expression(expr, ctx) if expr is not None else None
-            if t is not None:
-                v = _COMPUTE_TYPES[t](v)
+            v = _compute_value(v, t)
             if v is None and not optional:
                 raise ValueError(f"Field {name} is not optional but the expression evaluated to null")
+            if name.startswith(("value.", "key.")):
+                v = _struct_value(v)
             results.append((name, v))
         for name, v in results:
             if name in ("value", "key", "destinationTopic", "messageKey") or name.startswith(

@@ -57,7 +57,8 @@ def _load():
 def _default(o: Any) -> Any:
     """Values the JSON writer has no form for: the Java date-time types of
     api/temporal.py -- java.util.Date / Timestamp / Time as epoch millis (Jackson's default
-    for Date), the java.time ones as their ISO text."""
+    for Date), the java.time ones as their ISO text; bytes as base64 (Jackson's byte[]),
+    decimals as numbers."""
     from ..api import temporal
     if isinstance(o, (temporal.JDate, temporal.Timestamp, temporal.Time)):
         return o.get_time()
@@ -65,6 +66,12 @@ def _default(o: Any) -> Any:
         return str(o)
     if isinstance(o, (_dt.date, _dt.time)):
         return o.isoformat()
+    if isinstance(o, (bytes, bytearray, memoryview)):   # Jackson: byte[] / ByteBuffer as base64
+        import base64
+        return base64.b64encode(bytes(o)).decode()
+    from decimal import Decimal
+    if isinstance(o, Decimal):
+        return float(o)
     raise TypeError(f"Object of type {type(o).__name__} is not JSON serializable")
 
 

@@ -144,10 +144,10 @@ def test_serde_selection_from_schemas():
 
 
 def test_compute_step_int32_is_four_bytes_on_kafka():
-    from langstream_amd.agents.genai.steps import _COMPUTE_TYPES
-    v = _COMPUTE_TYPES["INT32"]("12")
+    from langstream_amd.agents.genai.steps import _compute_value
+    v = _compute_value("12", "INT32")
     assert v == 12 and serde.serialize_typed(v) == b"\x00\x00\x00\x0c"
-    assert serde.serialize_typed(_COMPUTE_TYPES["INT64"]("12")) == (12).to_bytes(8, "big")
+    assert serde.serialize_typed(_compute_value("12", "INT64")) == (12).to_bytes(8, "big")
 
 
 PROC = textwrap.dedent('''

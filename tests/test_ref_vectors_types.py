@@ -397,3 +397,93 @@ def test_cast_then_expression_uses_the_date_time_value():
     mr = _cast({"schema-type": "TIMESTAMP"}, SimpleRecord.of(None, "2023-01-02T23:04:05.000000006Z"))
     assert eval_expression("fn:timestampAdd(value, 1, 'seconds')", {"value": mr.value}) == DATE_TIME_MILLIS + 1000
     assert eval_expression("fn:str(value)", {"value": mr.value}) == "2023-01-02T23:04:05.000000006Z"
+
+
+# ---------------------------------------------------------------- ComputeStepTest
+def _compute(fields, value, key=None):
+    from langstream_amd.agents.genai.steps import ComputeStep
+    from langstream_amd.agents.genai.mutable import MutableRecord
+    mr = MutableRecord.from_record(SimpleRecord.of(key, value))
+    ComputeStep({"fields": fields}).process(mr)
+    return mr
+
+
+def _build_compute_fields(scope, optional=True, nullify=False, infer=False):
+    """ComputeStepTest.buildComputeFields(scope, optional, nullify, inferType)."""
+    rows = [("newStringField", "'Hotaru'", "STRING"), ("newInt8Field", "127", "INT8"),
+            ("newInt16Field", "32767", "INT16"), ("newInt32Field", "2147483647", "INT32"),
+            ("newInt64Field", "9223372036854775807", "INT64"),
+            ("newFloatField", "340282346638528859999999999999999999999.999999", "FLOAT"),
+            ("newDoubleField", "1.79769313486231570e+308", "DOUBLE"), ("newBooleanField", "1 == 1", "BOOLEAN"),
+            ("newDateField", "'2007-12-03'", "DATE"), ("newDateField2", "13850", "DATE"),
+            ("newLocalDateField", "'2007-12-03'", "LOCAL_DATE"), ("newLocalDateField2", "13850", "DATE"),
+            ("newTimeField", "'10:15:30'", "TIME"), ("newTimeField2", "36930000", "TIME"),
+            ("newLocalTimeField", "'10:15:30'", "LOCAL_TIME"), ("newLocalTimeField2", "36930000", "TIME"),
+            ("newTimestampField", "'2007-12-03T10:15:30+00:00'", "INSTANT"),
+            ("newTimestampField2", "1196676930000", "INSTANT"),
+            ("newInstantField", "'2007-12-03T10:15:30+00:00'", "TIMESTAMP"),
+            ("newInstantField2", "1196676930000", "INSTANT"),
+            ("newLocalDateTimeField", "'2007-12-03T10:15:30'", "LOCAL_DATE_TIME"),
+            ("newLocalDateTimeField2", "1196676930000", "INSTANT"),
+            ("newDateTimeField", "'2007-12-03T10:15:30+00:00'", "DATETIME"),
+            ("newBytesField", "'Hotaru'.bytes", "BYTES")]
+    return [{"name": f"{scope}.{n}", "expression": "null" if nullify else e, "optional": optional,
+             **({} if infer else {"type": t})} for n, e, t in rows]
+
+
+def test_compute_json_value_fields():
+    """ComputeStepTest.testJson, on a schemaless JSON value: typed fields land in the map
+    in their Avro forms (date = epoch days, time-millis = millis of day, timestamp-millis
+    = epoch millis, bytes -> base64 on the wire).  (The dateStr / timestampStr / timeStr
+    rows need the JSON schema's DATE / TIMESTAMP / TIME field types, which a schemaless
+    value does not carry -- unpinned here.)"""
+    from langstream_amd.utils import fastjson
+    import json as _json
+    value = {"firstName": "Jane", "lastName": "Doe", "age": 42, "integerStr": "13360"}
+    fields = _build_compute_fields("value") + [
+        {"name": "value.age", "expression": "value.age + 1", "type": "STRING"},
+        {"name": "value.integer", "expression": "value.integerStr", "type": "INT32"}]
+    v = _compute(fields, value, "test-key").value
+    read = _json.loads(fastjson.dumps(v))
+    assert read["firstName"] == "Jane" and read["integer"] == 13360 and read["age"] == "43"
+    assert read["newStringField"] == "Hotaru"
+    assert (read["newInt8Field"], read["newInt16Field"], read["newInt32Field"]) == (127, 32767, 2147483647)
+    assert read["newInt64Field"] == 9223372036854775807
+    assert read["newFloatField"] == pytest.approx(float(np.finfo(np.float32).max), rel=1e-7)
+    assert read["newDoubleField"] == 1.7976931348623157e308
+    assert read["newBooleanField"] is True
+    assert read["newBytesField"] == "SG90YXJ1"   # base64("Hotaru")
+    for f in ("newDateField", "newDateField2", "newLocalDateField", "newLocalDateField2"):
+        assert read[f] == 13850, f              # days since 1970-01-01
+    for f in ("newTimeField", "newTimeField2", "newLocalTimeField", "newLocalTimeField2"):
+        assert read[f] == 36930000, f           # millis since 00:00:00
+    for f in ("newDateTimeField", "newInstantField", "newInstantField2", "newTimestampField", "newTimestampField2",
+              "newLocalDateTimeField", "newLocalDateTimeField2"):
+        assert read[f] == 1196676930000, f
+
+
+@pytest.mark.parametrize("as_bytes", [False, True])
+def test_compute_string_json(as_bytes):
+    """ComputeStepTest.testStringJson: a STRING / BYTES JSON value is computed as a map."""
+    text = ('{"name":"Jane","age":42,"date":18999,"timestamp":1672525445006,"time":83085006,'
+            '"integerStr":"13360"}')
+    v = _compute([{"name": "value.age", "expression": "value.age + 1", "type": "STRING"}],
+                 text.encode() if as_bytes else text, "test-key").value
+    assert v == {"name": "Jane", "age": "43", "date": 18999, "timestamp": 1672525445006, "time": 83085006,
+                 "integerStr": "13360"}
+
+
+def test_compute_primitive_schema_types():
+    """ComputeStepTest.testPrimitiveSchemaTypes (the value itself computed): each type's
+    Java object -- a DATE is a LocalDate, a TIMESTAMP a Timestamp, an INSTANT an Instant."""
+    cases = [("'2007-12-03'", "DATE", dt.date(2007, 12, 3)), ("'10:15:30'", "TIME", Time(36930000)),
+             ("'10:15:30'", "LOCAL_TIME", LocalTime.of(10, 15, 30)),
+             ("'2007-12-03T10:15:30+00:00'", "INSTANT", Instant(1196676930)),
+             ("'2007-12-03T10:15:30+00:00'", "TIMESTAMP", Timestamp(1196676930)),
+             ("'2007-12-03T10:15:30'", "LOCAL_DATE_TIME", LocalDateTime(dt.date(2007, 12, 3), LocalTime.of(10, 15, 30))),
+             ("1", "INT8", Int8(1)), ("1", "INT16", Int16(1)), ("1", "INT32", Int32(1)), ("1", "INT64", 1),
+             ("1.5", "FLOAT", Float32(1.5)), ("1.5", "DOUBLE", 1.5), ("'Hotaru'.bytes", "BYTES", b"Hotaru"),
+             ("1 == 1", "BOOLEAN", True), ("42", "STRING", "42")]
+    for expr, t, expected in cases:
+        v = _compute([{"name": "value", "expression": expr, "type": t}], "x").value
+        assert type(v) is type(expected) and v == expected, (t, v)
