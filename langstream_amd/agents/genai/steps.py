@@ -76,17 +76,24 @@ class DropFieldsStep(Step):
 
 
 class MergeKeyValueStep(Step):
+    """MergeKeyValueStep.java: the key's fields are added to the value where the value has
+    no field of that name (``putIfAbsent``: the value's fields first, in their order)."""
+
     def process(self, rec):
         if isinstance(rec.key, dict) and isinstance(rec.value, dict):
-            merged = dict(rec.key)
-            merged.update(rec.value)
+            merged = dict(rec.value)
+            for k, v in rec.key.items():
+                merged.setdefault(k, v)
             rec.value = merged
-        elif isinstance(rec.key, dict) and rec.value is None:
-            rec.value = dict(rec.key)
 
 
 class UnwrapKeyValueStep(Step):
+    """UnwrapKeyValueStep.java: a record with a key becomes its value (or, with
+    ``unwrapKey``, its key) alone; a record without a key is untouched."""
+
     def process(self, rec):
+        if rec.key is None:
+            return
         if bool(self.cfg.get("unwrapKey", self.cfg.get("unwrap-key", False))):
             rec.value = rec.key
         rec.key = None
@@ -143,12 +150,22 @@ def _flatten(d: dict, delim: str, prefix: str = "") -> dict:
 
 
 class FlattenStep(Step):
+    """FlattenStep.java: nested struct fields become top-level ``a<delim>b`` fields.  The
+    reference flattens Avro records only; maps (JSON values) are flattened here too.  A
+    value with no struct to flatten fails as there (``Unsupported schema type``)."""
+
     def process(self, rec):
         delim = self.cfg.get("delimiter", "_")
         part = self.cfg.get("part")
+        if part not in (None, "key", "value"):
+            raise ValueError(f"Unsupported part for Flatten: {part}")
         if part in (None, "key") and isinstance(rec.key, dict):
             rec.key = _flatten(rec.key, delim)
-        if part in (None, "value") and isinstance(rec.value, dict):
+        if part in (None, "value"):
+            if rec.value is None:
+                raise ValueError("Flatten requires non-null schemas!")
+            if not isinstance(rec.value, dict):
+                raise ValueError(f"Unsupported schema type for Flatten: {type(rec.value).__name__}")
             rec.value = _flatten(rec.value, delim)
 
 

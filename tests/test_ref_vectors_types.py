@@ -487,3 +487,102 @@ def test_compute_primitive_schema_types():
     for expr, t, expected in cases:
         v = _compute([{"name": "value", "expression": expr, "type": t}], "x").value
         assert type(v) is type(expected) and v == expected, (t, v)
+
+
+# ---------------------------------------------------------------- FlattenStepTest
+def test_flatten_nested_value_with_custom_delimiter():
+    """FlattenStepTest.testNestedKeyValueFlattenedWithCustomDelimiter (values level)."""
+    from langstream_amd.agents.genai.steps import FlattenStep
+    from langstream_amd.agents.genai.mutable import MutableRecord
+    nested = {"level1String": "level1_1", "level1Record": {"level2String": "level2_1",
+              "level2Record": {"level3String": "level3_1", "level3Record": {"level4String": "level4_1"}}}}
+    mr = MutableRecord({"k": {"a": 1}}, nested)
+    FlattenStep({"delimiter": "__"}).process(mr)
+    assert mr.value == {"level1String": "level1_1", "level1Record__level2String": "level2_1",
+                        "level1Record__level2Record__level3String": "level3_1",
+                        "level1Record__level2Record__level3Record__level4String": "level4_1"}
+    assert mr.key == {"k__a": 1}
+
+
+def test_flatten_rejects_what_it_cannot_flatten():
+    """FlattenStepTest.testNestedSchemalessValue / testNestedKeyValueInvalidType: a
+    primitive value and an unknown part fail."""
+    from langstream_amd.agents.genai.steps import FlattenStep
+    from langstream_amd.agents.genai.mutable import MutableRecord
+    with pytest.raises(ValueError, match="Unsupported schema type"):
+        FlattenStep({"part": "value"}).process(MutableRecord("myKey", "value"))
+    with pytest.raises(ValueError, match="Unsupported part"):
+        FlattenStep({"part": "something"}).process(MutableRecord(None, {"a": {"b": 1}}))
+
+
+# ---------------------------------------------------------------- Merge / DropField / Unwrap
+_KEY_JSON = '{"keyField1": "key1", "keyField2": "key2", "keyField3": "key3"}'
+_VALUE_JSON = '{"valueField1": "value1", "valueField2": "value2", "valueField3": "value3"}'
+
+
+def _step(step_cls, cfg, key, value):
+    from langstream_amd.agents.genai.mutable import MutableRecord
+    mr = MutableRecord.from_record(SimpleRecord.of(key, value))
+    step_cls(cfg).process(mr)
+    return mr
+
+
+def test_merge_key_value_string_json():
+    """MergeKeyValueStepTest.testKeyValueStringJson: value fields first, then the key's
+    (the output text, compact as Jackson writes it)."""
+    import json as _json
+    from langstream_amd.agents.genai.steps import MergeKeyValueStep
+    mr = _step(MergeKeyValueStep, {}, _KEY_JSON, _VALUE_JSON)
+    assert _json.dumps(mr.value, separators=(",", ":")) == (
+        '{"valueField1":"value1","valueField2":"value2","valueField3":"value3",'
+        '"keyField1":"key1","keyField2":"key2","keyField3":"key3"}')
+    assert mr.key == {"keyField1": "key1", "keyField2": "key2", "keyField3": "key3"}
+
+
+def test_merge_key_value_primitive_untouched():
+    """MergeKeyValueStepTest.testPrimitive / testKeyValuePrimitives."""
+    from langstream_amd.agents.genai.steps import MergeKeyValueStep
+    mr = _step(MergeKeyValueStep, {}, "test-key", "test-message")
+    assert (mr.key, mr.value) == ("test-key", "test-message")
+    mr = _step(MergeKeyValueStep, {}, "key", Int32(42))
+    assert (mr.key, mr.value) == ("key", 42)
+
+
+def test_drop_fields_string_json():
+    """DropFieldStepTest.testStringJson / testKeyValueStringJson / testKeyValueBytesJson."""
+    import json as _json
+    from langstream_amd.agents.genai.steps import DropFieldsStep
+    mr = _step(DropFieldsStep, {"fields": ["value1"], "part": "value"}, "test-key", _VALUE_JSON)
+    assert _json.dumps(mr.value, separators=(",", ":")) == \
+        '{"valueField1":"value1","valueField2":"value2","valueField3":"value3"}'
+    for enc in (str, str.encode):
+        mr = _step(DropFieldsStep, {"fields": ["keyField1", "keyField2"], "part": "key"}, enc(_KEY_JSON),
+                   enc(_VALUE_JSON))
+        mr2 = _step(DropFieldsStep, {"fields": ["valueField1", "valueField2"], "part": "value"}, enc(_KEY_JSON),
+                    enc(_VALUE_JSON))
+        assert _json.dumps(mr.key, separators=(",", ":")) == '{"keyField3":"key3"}'
+        assert _json.dumps(mr2.value, separators=(",", ":")) == '{"valueField3":"value3"}'
+
+
+def test_drop_fields_primitives_untouched():
+    """DropFieldStepTest.testPrimitives."""
+    from langstream_amd.agents.genai.steps import DropFieldsStep
+    mr = _step(DropFieldsStep, {"fields": ["value"]}, "test-key", "value")
+    assert (mr.key, mr.value) == ("test-key", "value")
+
+
+def test_unwrap_key_value():
+    """UnwrapKeyValueStepTest: the value (or the key with unwrapKey) becomes the record;
+    a primitive record is untouched."""
+    from langstream_amd.agents.genai.steps import UnwrapKeyValueStep
+    assert _step(UnwrapKeyValueStep, {}, _KEY_JSON, _VALUE_JSON).value == \
+        {"valueField1": "value1", "valueField2": "value2", "valueField3": "value3"}
+    assert _step(UnwrapKeyValueStep, {"unwrapKey": True}, _KEY_JSON, _VALUE_JSON).value == \
+        {"keyField1": "key1", "keyField2": "key2", "keyField3": "key3"}
+
+
+def test_unwrap_without_key_is_untouched():
+    """UnwrapKeyValueStep: no key (keySchemaType null) -> nothing changes, even with unwrapKey."""
+    from langstream_amd.agents.genai.steps import UnwrapKeyValueStep
+    mr = _step(UnwrapKeyValueStep, {"unwrapKey": True}, None, "test-message")
+    assert (mr.key, mr.value) == (None, "test-message")
