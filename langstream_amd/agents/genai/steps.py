@@ -432,10 +432,11 @@ class QueryStep(Step):
         params = self._params(ctx)
         if self.mode == "execute":
             return self.ds.execute_statement(self.query, self.generated_keys, params)
-        rows = self.ds.fetch_data(self.query, params)
-        if self.only_first:
-            return rows[0] if rows else None
-        return rows
+        return self.ds.fetch_data(self.query, params) or []
+
+    def _first(self, rows):
+        # only-first: the first row, or an empty map when there is none (QueryStep.java:95-100)
+        return (rows[0] if rows else {}) if self.only_first else rows
 
     def process_async(self, rec) -> Future:
         fut: Future = Future()
@@ -448,8 +449,7 @@ class QueryStep(Step):
 
             def done(f):
                 try:
-                    rows = f.result()
-                    r = (rows[0] if rows else None) if self.only_first else rows
+                    r = self._first(f.result() or [])
                     rec.set_result_field(r, self.output_field)
                     fut.set_result(None)
                 except BaseException as e:  # noqa: BLE001
@@ -462,14 +462,24 @@ class QueryStep(Step):
             try:
                 items = _LoopOver.items(rec, self.loop_over)
                 if items is not None:
+                    # per item ("record" in the expressions): a query's rows are concatenated,
+                    # an execute's results listed (QueryStep.processQuery / processExecute)
                     res = []
                     for it in items:
                         c = rec.el_context()
                         c["record"] = it
-                        res.append(self._run_one(c))
+                        out = self._run_one(c)
+                        if self.mode == "execute":
+                            res.append(out)
+                        else:
+                            res.extend(out)
+                    if self.mode != "execute":
+                        res = self._first(res)
                     rec.set_result_field(res, self.output_field)
                 else:
                     r = self._run_one(rec.el_context())
+                    if self.mode != "execute":
+                        r = self._first(r)
                     if self.output_field:
                         rec.set_result_field(r, self.output_field)
                 fut.set_result(None)

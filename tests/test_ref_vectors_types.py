@@ -586,3 +586,85 @@ def test_unwrap_without_key_is_untouched():
     from langstream_amd.agents.genai.steps import UnwrapKeyValueStep
     mr = _step(UnwrapKeyValueStep, {"unwrapKey": True}, None, "test-message")
     assert (mr.key, mr.value) == (None, "test-message")
+
+
+# ---------------------------------------------------------------- QueryStepTest
+class _FakeDS:
+    """A QueryStepDataSource stub: fetch / execute callables."""
+
+    def __init__(self, fetch=None, execute=None):
+        self.fetch, self.execute = fetch, execute
+
+    def fetch_data(self, query, params):
+        return self.fetch(query, params)
+
+    def execute_statement(self, query, keys, params):
+        return self.execute(query, keys, params)
+
+
+def _query(cfg, ds, value, key=None):
+    from langstream_amd.agents.genai.steps import QueryStep
+    from langstream_amd.agents.genai.mutable import MutableRecord
+    mr = MutableRecord.from_record(SimpleRecord.of(key, value))
+    QueryStep(cfg, ds).process_async(mr).result(timeout=10)
+    return mr
+
+
+def test_query_primitive_and_dash_field():
+    """QueryStepTest.testPrimitive / testSetFieldWithDash."""
+    ds = _FakeDS(fetch=lambda q, p: [{"foo": "bar"}] if (q, p) == ("select 1", []) else 1 / 0)
+    assert _query({"query": "select 1", "output-field": "value"}, ds, "test-message").value == [{"foo": "bar"}]
+    assert _query({"query": "select 1", "output-field": "value.command-results"}, ds, "{}").value == \
+        {"command-results": [{"foo": "bar"}]}
+
+
+def test_query_only_first():
+    """QueryStepTest.testOnlyFirst: the first row, an empty map when nothing matched."""
+    def fetch(q, p):
+        return {"select a,b from test": [{"a": "10", "b": "foo"}, {"a": "20", "b": "bar"}],
+                "select a,b from test where 1=0": [{}]}[q]
+    ds = _FakeDS(fetch=fetch)
+    v = _query({"query": "select a,b from test", "output-field": "value.result", "only-first": True}, ds,
+               _VALUE_JSON, _KEY_JSON).value
+    assert v == {"valueField1": "value1", "valueField2": "value2", "valueField3": "value3",
+                 "result": {"a": "10", "b": "foo"}}
+    v = _query({"query": "select a,b from test where 1=0", "output-field": "value.result", "only-first": True}, ds,
+               _VALUE_JSON, _KEY_JSON).value
+    assert v["result"] == {}
+    v = _query({"query": "q", "output-field": "value.result", "only-first": True}, _FakeDS(fetch=lambda q, p: []),
+               _VALUE_JSON).value
+    assert v["result"] == {}
+
+
+_DOCS = ('{"documents_to_retrieve": [{"text": "text 1", "embeddings": [1,2,3,4,5]},'
+         '{"text": "text 2", "embeddings": [2,2,3,4,5]}]}')
+
+
+def test_query_loop_over_concatenates_rows():
+    """QueryStepTest.testLoopOver: each item's rows, concatenated."""
+    def fetch(q, p):
+        return {(1, 2, 3, 4, 5): [{"text": "retrieved-similar-to-1-1"}, {"text": "retrieved-similar-to-1-2"}],
+                (2, 2, 3, 4, 5): [{"text": "retrieved-similar-to-2"}]}[tuple(p[0])]
+    v = _query({"query": "select 1 where vector near ?", "loop-over": "value.documents_to_retrieve",
+                "output-field": "value.retrieved_documents", "fields": ["record.embeddings"]},
+               _FakeDS(fetch=fetch), _DOCS).value
+    assert v["retrieved_documents"] == [{"text": "retrieved-similar-to-1-1"}, {"text": "retrieved-similar-to-1-2"},
+                                        {"text": "retrieved-similar-to-2"}]
+
+
+def test_query_execute_and_loop_over_execute():
+    """QueryStepTest.testExecute / testLoopOverWithExecute."""
+    def execute(q, keys, p):
+        assert keys == ["pk"]
+        return {str(i): p[0] for i in range(len(p))}
+    v = _query({"query": "update something set a=1 WHERE value=?", "mode": "execute", "generated-keys": ["pk"],
+                "output-field": "value.command_results", "fields": ["value.question"]},
+               _FakeDS(execute=execute), '{"question":"really?"}').value
+    assert v["command_results"] == {"0": "really?"}
+
+    def execute2(q, keys, p):
+        return {(1, 2, 3, 4, 5): {"foo": "bar"}, (2, 2, 3, 4, 5): {"foo": "bar2"}}[tuple(p[0])]
+    v = _query({"query": "update something set a=1 WHERE value=?", "mode": "execute", "generated-keys": ["pk"],
+                "loop-over": "value.documents_to_retrieve", "output-field": "value.command_results",
+                "fields": ["record.embeddings"]}, _FakeDS(execute=execute2), _DOCS).value
+    assert v["command_results"] == [{"foo": "bar"}, {"foo": "bar2"}]
