@@ -113,9 +113,12 @@ class MutableRecord:
                 {"key": self.key, "value": self.value}}
 
     def json_context(self) -> Dict[str, Any]:
-        """Context for mustache templates (JsonRecord: key, value, origin, timestamp, properties)."""
-        return {"key": self.key, "value": self.value, "origin": self.input_topic, "timestamp": self.event_time,
-                "properties": self.properties, "messageKey": self.message_key or self.key}
+        """Context for mustache templates: MutableRecord.toJsonRecord's JsonRecord (topicName,
+        destinationTopic, key, value, properties, eventTime), plus origin / timestamp /
+        messageKey aliases."""
+        return {"key": self.key, "value": self.value, "topicName": self.input_topic,
+                "destinationTopic": self.output_topic, "eventTime": self.event_time, "properties": self.properties,
+                "origin": self.input_topic, "timestamp": self.event_time, "messageKey": self.message_key or self.key}
 
     def set_result_field(self, content: Any, field: Optional[str]) -> None:
         if field is None or field == "value":

@@ -668,3 +668,91 @@ def test_query_execute_and_loop_over_execute():
                 "loop-over": "value.documents_to_retrieve", "output-field": "value.command_results",
                 "fields": ["record.embeddings"]}, _FakeDS(execute=execute2), _DOCS).value
     assert v["command_results"] == [{"foo": "bar"}, {"foo": "bar2"}]
+
+
+# ---------------------------------------------------------------- ChatCompletionsStepTest
+class _FakeChat:
+    """OpenAICompletionService with a mocked client: captures the rendered messages and
+    answers 'result' (ChatCompletionsStepTest.setup)."""
+
+    def __init__(self):
+        self.calls = []
+
+    def get_chat_completions(self, messages, consumer, options):
+        from concurrent.futures import Future
+        from langstream_amd.agents.genai.services import CompletionResult
+        self.calls.append(([m.content for m in messages], dict(options)))
+        f = Future()
+        f.set_result(CompletionResult("result"))
+        return f
+
+
+def _chat(cfg, key, value, *, props=None, origin=None, ts=None, dest=None):
+    from langstream_amd.agents.genai.steps import ChatCompletionsStep
+    from langstream_amd.agents.genai.mutable import MutableRecord
+    from langstream_amd.api.record import Header
+    svc = _FakeChat()
+    step = ChatCompletionsStep({"model": "test-model", **cfg}, svc, lambda topic: None)
+    rec = SimpleRecord.of(key, value, [Header(k, v) for k, v in (props or {}).items()], origin=origin, timestamp=ts)
+    mr = MutableRecord.from_record(rec)
+    if dest is not None:
+        mr.output_topic = dest
+    step.process_async(mr).result(timeout=10)
+    return svc, mr
+
+
+def test_chat_template_sees_the_json_record():
+    """ChatCompletionsStepTest.testPrimitive / testPrimitiveNoStream: value, key, eventTime,
+    topicName, destinationTopic, properties.x in the message templates."""
+    tpl = "{{ value }} {{ key}} {{ eventTime }} {{ topicName }} {{ destinationTopic }} {{ properties.test-key }}"
+    for stream in (True, False):
+        svc, _ = _chat({"messages": [{"role": "user", "content": tpl}], "stream": stream}, "test-key", "test-message",
+                       props={"test-key": "test-value"}, origin="test-input-topic", ts=42, dest="test-output-topic")
+        assert svc.calls[0][0] == ["test-message test-key 42 test-input-topic test-output-topic test-value"]
+
+
+@pytest.mark.parametrize("as_bytes", [False, True])
+def test_chat_template_json_string_value(as_bytes):
+    """ChatCompletionsStepTest.testJsonString (STRING and BYTES JSON values)."""
+    text = ('{"firstName":"Jane","lastName":"Doe","age":42,"date":19359,"timestamp":1672700645006,'
+            '"time":83045006}')
+    tpl = ("{{ value.firstName }} {{ value.lastName }} {{ value.age }} {{ value.date }} {{ value.timestamp }} "
+           "{{ value.time }} {{ key }}")
+    svc, _ = _chat({"messages": [{"role": "user", "content": tpl}]}, "test-key", text.encode() if as_bytes else text)
+    assert svc.calls[0][0] == ["Jane Doe 42 19359 1672700645006 83045006 test-key"]
+
+
+def test_chat_kv_json_string():
+    """ChatCompletionsStepTest.testKVJsonString: key and value fields in one template."""
+    svc, _ = _chat({"messages": [{"role": "user", "content": "{{ value.valueField1 }} {{ key.keyField2 }}"}]},
+                   _KEY_JSON, _VALUE_JSON)
+    assert svc.calls[0][0] == ["value1 key2"]
+
+
+@pytest.mark.parametrize("field,check", [
+    ("value", lambda mr: mr.value == "result"),
+    ("key", lambda mr: mr.key == "result"),
+    ("destinationTopic", lambda mr: mr.output_topic == "result"),
+    ("messageKey", lambda mr: mr.to_record().key() == "result"),
+    ("properties.chat", lambda mr: mr.properties["chat"] == "result"),
+])
+def test_chat_completion_field_targets(field, check):
+    """ChatCompletionsStepTest.testValueOutput / testKeyOutput / testDestinationTopicOutput /
+    testMessageKeyOutput / testPropertyOutput."""
+    _, mr = _chat({"messages": [{"role": "user", "content": "content"}], "completion-field": field}, "test-key",
+                  "test-message")
+    assert check(mr)
+
+
+@pytest.mark.parametrize("value,expected", [
+    ('{"name":"Jane"}', {"name": "Jane", "chat": "result"}),
+    (b'{"name":"Jane"}', {"name": "Jane", "chat": "result"}),
+])
+def test_chat_completion_into_json_string_value(value, expected):
+    """ChatCompletionsStepTest.testJsonStringValueFieldOutput / testJsonValueFieldOutput."""
+    _, mr = _chat({"messages": [{"role": "user", "content": "content"}], "completion-field": "value.chat"},
+                  "test-key", value)
+    assert mr.value == expected
+    _, mr = _chat({"messages": [{"role": "user", "content": "content"}], "completion-field": "key.chat"},
+                  '{"name":"Jane"}', "v")
+    assert mr.key == {"name": "Jane", "chat": "result"}
