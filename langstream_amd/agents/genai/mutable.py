@@ -32,6 +32,32 @@ def attempt_json(v: Any) -> Any:
     return v
 
 
+def _text_origin(r: Record, i: int):
+    """str / bytes when the record's key (i = 0) or value (i = 1) is, or was before an
+    upstream agent parsed it, JSON text; else None."""
+    v = r.key() if i == 0 else r.value()
+    if type(v) in (str, bytes):
+        return type(v)
+    ref = getattr(r, "_source_ref", None)
+    if isinstance(ref, dict) and "json_origin" in ref:
+        return ref["json_origin"][i]
+    return None
+
+
+def text_form(v: Any, origin) -> Any:
+    """A map in the text form it came in: compact JSON (Jackson's writeValueAsString /
+    writeValueAsBytes); anything else unchanged."""
+    if isinstance(v, dict) and origin in (str, bytes):
+        t = json.dumps(v, separators=(",", ":"), ensure_ascii=False, default=_json_default)
+        return t if origin is str else t.encode("utf-8")
+    return v
+
+
+def _json_default(o):
+    from ...utils.fastjson import _default
+    return _default(o)
+
+
 def safe_clone(v: Any) -> Any:
     """Copy the top level of a map/list value.  Enough for isolation: every mutation a
     step performs replaces a top-level entry (``set_result_field`` writes flat keys,
@@ -101,8 +127,19 @@ class MutableRecord:
         headers = [Header(k, v) for k, v in self.properties.items()]
         key = self.message_key if self.message_key is not None else self.key
         r = SimpleRecord(key, self.value, self.input_topic, self.event_time, headers)
+        ref = None
         if self.output_topic is not None:
-            r._source_ref = {"destination_topic": self.output_topic}
+            ref = {"destination_topic": self.output_topic}
+        if self.source is not None and (isinstance(key, dict) or isinstance(self.value, dict)):
+            # maps parsed from JSON text stay maps on the way downstream (the next agent would
+            # parse them again), but remember the text form they came in: the reference hands
+            # them on as compact JSON strings / bytes (MutableRecord.convertMapToStringOrBytes),
+            # which is what a Python agent then receives (python_agents._to_user)
+            origin = (_text_origin(self.source, 0), _text_origin(self.source, 1))
+            if origin != (None, None):
+                ref = dict(ref or {}, json_origin=origin)
+        if ref is not None:
+            r._source_ref = ref
         return r
 
     def el_context(self) -> Dict[str, Any]:

@@ -62,10 +62,21 @@ class _UserRecord:
         self._r = r
 
     def key(self):
-        return _to_user(self._r.key())
+        return _to_user(self._text_form(self._r.key(), 0))
 
     def value(self):
-        return _to_user(self._r.value())
+        return _to_user(self._text_form(self._r.value(), 1))
+
+    def _text_form(self, v, i):
+        # a map an upstream agent parsed from JSON text reaches user code as that text,
+        # compact, as the reference's Java agents hand it to the Python runtime
+        # (MutableRecord.convertMapToStringOrBytes -> gRPC string / bytes value)
+        if isinstance(v, dict):
+            from .genai.mutable import _text_origin, text_form
+            ref = getattr(self._r, "_source_ref", None)
+            if isinstance(ref, dict) and "json_origin" in ref:
+                return text_form(v, ref["json_origin"][i])
+        return v
 
     def origin(self):
         return self._r.origin()

@@ -756,3 +756,25 @@ def test_chat_completion_into_json_string_value(value, expected):
     _, mr = _chat({"messages": [{"role": "user", "content": "content"}], "completion-field": "key.chat"},
                   '{"name":"Jane"}', "v")
     assert mr.key == {"name": "Jane", "chat": "result"}
+
+
+def test_python_agent_receives_json_text_like_the_reference():
+    """A map an agent parsed from JSON text is handed to Python user code as that text,
+    compact (MutableRecord.convertMapToStringOrBytes -> the gRPC string / bytes value the
+    reference's Python runtime receives), across several agents; a map that never was text
+    stays a map."""
+    from langstream_amd.agents.genai.mutable import MutableRecord
+    from langstream_amd.agents.python_agents import _UserRecord
+    for src, form in (('{"a": 1}', str), (b'{"a": 1}', bytes)):
+        mr = MutableRecord.from_record(SimpleRecord.of(None, src))
+        mr.set_result_field(2, "value.b")
+        r = mr.to_record()
+        assert r.value() == {"a": 1, "b": 2}                     # downstream agents keep the map
+        mr2 = MutableRecord.from_record(r)                        # a second agent
+        mr2.set_result_field("é", "value.c")
+        out = _UserRecord(mr2.to_record()).value()
+        assert type(out) is form
+        assert (out if form is str else out.decode()) == '{"a":1,"b":2,"c":"é"}'
+    mr = MutableRecord.from_record(SimpleRecord.of(None, {"a": 1}))
+    mr.set_result_field(2, "value.b")
+    assert _UserRecord(mr.to_record()).value() == {"a": 1, "b": 2}
