@@ -57,6 +57,9 @@ def main():
                          "block allocator) instead of scattered over the pool")
     ap.add_argument("--sorted", action="store_true",
                     help="rows ordered by context length, longest first (as the engine schedules them)")
+    ap.add_argument("--shared-first", type=int, default=0,
+                    help="the first N blocks of every sequence are the SAME physical blocks (a template "
+                         "prefix shared through the prefix cache)")
     ap.add_argument("--rope", action="store_true",
                     help="time the decode-only variant with RoPE + the KV write fused in "
                          "(paged_decode_attention_rope over an un-rotated qkv buffer, as the engine runs it)")
@@ -81,7 +84,10 @@ def main():
         blk_bytes = Hkv * 64 * D * 2 * 2
         pool = max(2 * B * nb, int(a.pool_gb * 1e9 // blk_bytes))
         perm = (torch.arange(B * nb) if a.seq_blocks else torch.randperm(pool, generator=g)[: B * nb]).to(torch.int32)
-        bt = perm.view(B, nb).to(dev)
+        bt = perm.view(B, nb).clone()
+        if a.shared_first:
+            bt[:, : a.shared_first] = bt[0, : a.shared_first]
+        bt = bt.to(dev)
         if pool > 2 * B * nb:
             kc = torch.zeros(pool, Hkv, 64, D, device=dev, dtype=bf)
             vc = torch.zeros(pool, Hkv, 8, D, 8, device=dev, dtype=bf)
@@ -137,6 +143,7 @@ def main():
                "pipe": os.environ.get("LS_ATTN_PIPE", "1"),
                "ragged": a.ragged, "pool_gb": a.pool_gb, "ring": a.ring, "rope": a.rope,
                "uniform_lo": a.uniform_lo, "sorted": a.sorted, "seq_blocks": a.seq_blocks,
+               "shared_first": a.shared_first, "nt": os.environ.get("LS_ATTN_NT", "2"),
                "interleave_gemm": a.interleave_gemm}
         if not a.rope and (B <= 16 or (a.check_all and B * ctx <= 512 * 1024)) and a.pool_gb == 0:
             exp = ref.paged_decode_attention(q.float().cpu().reshape(B, Hq, D), kc.float().cpu(), vc.float().cpu(),
