@@ -317,18 +317,28 @@ def eval_predicate(expr: Optional[str], ctx: Dict[str, Any]) -> bool:
 
 # ---------------------------------------------------------------- fn: library
 def _fn_tostring(v) -> str:
+    """JstlFunctions.toString: String.valueOf semantics -- a map prints as Java's
+    ``{k=v, ...}``, a list as ``[a, b]``, doubles as Double.toString."""
     if v is None:
         return ""
-    if isinstance(v, _TEMPORAL_TYPES):
-        return _temporal.to_java_string(v)
     if isinstance(v, bytes):
         return v.decode("utf-8", errors="replace")
+    return _java_str(v)
+
+
+def _java_str(v) -> str:
+    if v is None:
+        return "null"
+    if isinstance(v, _TEMPORAL_TYPES):
+        return _temporal.to_java_string(v)
     if isinstance(v, bool):
         return "true" if v else "false"
-    if isinstance(v, (dict, list)):
-        return json.dumps(v)
-    if isinstance(v, float) and v.is_integer():
-        return repr(v)
+    if isinstance(v, float):
+        return _temporal.java_float_str(v) if isinstance(v, _temporal.Float32) else _temporal.java_double_str(v)
+    if isinstance(v, dict):
+        return "{" + ", ".join(f"{_java_str(k)}={_java_str(x)}" for k, x in v.items()) + "}"
+    if isinstance(v, (list, tuple)):
+        return "[" + ", ".join(_java_str(x) for x in v) + "]"
     return str(v)
 
 

@@ -778,3 +778,20 @@ def test_python_agent_receives_json_text_like_the_reference():
     mr = MutableRecord.from_record(SimpleRecord.of(None, {"a": 1}))
     mr.set_result_field(2, "value.b")
     assert _UserRecord(mr.to_record()).value() == {"a": 1, "b": 2}
+
+
+# ---------------------------------------------------------------- GenAIToolKitAgentTest
+def test_genai_toolkit_compute_expressions():
+    """GenAIToolKitAgentTest.testCompute: what a compute field holds for each expression
+    (a map through fn:str prints as Java's Map.toString)."""
+    import json as _json
+    value = _json.dumps({"fieldInt": 1, "fieldText": "text", "fieldCsv": "a,b,c", "fieldJson": '{"this":"that"}'})
+
+    def compute(expr):
+        return _compute([{"name": "value.computedField", "expression": expr}], value).value["computedField"]
+    assert compute("value.fieldInt") == 1
+    assert compute("value.fieldText") == "text"
+    assert compute("fn:split(value.fieldCsv,',')") == ["a", "b", "c"]
+    assert compute("fn:str(fn:fromJson(value.fieldJson))") == "{this=that}"
+    assert _json.loads(compute("fn:toJson(fn:unpack(value.fieldCsv, 'f1,f2,f3'))")) == {"f1": "a", "f2": "b", "f3": "c"}
+    assert compute("fn:str(1.0E7)") == "1.0E7" and compute("fn:str(0.5)") == "0.5"
