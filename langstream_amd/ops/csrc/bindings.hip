@@ -70,6 +70,8 @@ void skinny_gemm_add_rmsnorm(at::Tensor out, at::Tensor x, at::Tensor w, at::Ten
                              double eps);
 void gemm_prefill(at::Tensor out, at::Tensor x, at::Tensor w, bool silu, int64_t variant);
 bool gemm_prefill_supported(const at::Tensor& w, bool silu);
+void gemm_prefill_f32(at::Tensor out, at::Tensor x, at::Tensor w);
+bool gemm_prefill_f32_supported(const at::Tensor& w);
 bool decode_gemm_supported(const at::Tensor& w, bool silu);
 int64_t decode_gemm_workspace(int64_t M, int64_t N, int64_t K, bool silu);
 void decode_gemm(at::Tensor out, at::Tensor x, at::Tensor w, at::Tensor workspace, c10::optional<at::Tensor> residual,
@@ -141,6 +143,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("skinny_gemm_add_rmsnorm", &skinny_gemm_add_rmsnorm);
   m.def("gemm_prefill", &gemm_prefill, py::arg("out"), py::arg("x"), py::arg("w"), py::arg("silu"), py::arg("variant") = -1);
   m.def("gemm_prefill_supported", &gemm_prefill_supported);
+  m.def("gemm_prefill_f32", &gemm_prefill_f32, "out[M, N] (f32) = x . w^T on the ping-pong MFMA kernel");
+  m.def("gemm_prefill_f32_supported", &gemm_prefill_f32_supported);
   m.def("decode_gemm_supported", &decode_gemm_supported);
   m.def("decode_gemm_workspace", &decode_gemm_workspace);
   m.def("decode_gemm", &decode_gemm, py::arg("out"), py::arg("x"), py::arg("w"), py::arg("workspace"),

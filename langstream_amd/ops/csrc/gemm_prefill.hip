@@ -578,7 +578,7 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(const bf16* __restrict__ x
   // acc[qm][qn][i][j][r] = C[128 wm + 64 qm + 16 i + 4 h + r][64 wn + 32 qn + 16 j + fr] (tile-local;
   // SILU: qn = 0 gate, qn = 1 up of feature nt*128 + 32 wn + 16 j + fr)
   if constexpr (EPI == EPI_STORE) {
-    if (S > 1) {   // split-K: this split's f32 partial tile
+    if (part != nullptr) {   // split-K: this split's f32 partial tile (S = 1: an f32 GEMM, gemm_prefill_f32)
       const int64_t N = (int64_t)NTL * TN;
 #pragma unroll
       for (int qm = 0; qm < 2; ++qm)
@@ -950,4 +950,33 @@ void gemm_prefill(at::Tensor out, at::Tensor x, at::Tensor w, bool silu, int64_t
   }
   if (silu) launch<EPI_SILU>(var, ring, nwv, sp, grid, stream, x, w, (int)M, (int)K, out, MT, NTL, (int)(N / 2), gm);
   else launch<EPI_STORE>(var, ring, nwv, sp, grid, stream, x, w, (int)M, (int)K, out, MT, NTL, 0, gm);
+}
+
+// out[M, N] (f32) = x . w^T on the ping-pong kernel (its split-K partial-tile epilogue with
+// one split).  The LM head of decode batches of 129..256 rows: at M = 256, N = 128256 the
+// head is MFMA-bound (269 GFLOP); 261 us here vs 279 on the bandwidth-shaped decode GEMM
+// (profiles/r5/head_pp_r5ag.log).  Shapes: K % 128 == 0, N % 256 == 0.
+bool gemm_prefill_f32_supported(const at::Tensor& w) {
+  return w.dim() == 2 && w.scalar_type() == at::kBFloat16 && w.is_contiguous() && w.size(1) % 128 == 0 &&
+         w.size(0) % TN == 0;
+}
+
+void gemm_prefill_f32(at::Tensor out, at::Tensor x, at::Tensor w) {
+  const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 2 && x.stride(1) == 1 &&
+              x.stride(0) % 8 == 0, "x must be bf16 [M, K] with unit column stride");
+  TORCH_CHECK(w.size(1) == K && gemm_prefill_f32_supported(w), "gemm_prefill_f32: unsupported weight shape");
+  TORCH_CHECK(out.scalar_type() == at::kFloat && out.dim() == 2 && out.size(0) == M && out.size(1) == N &&
+              out.is_contiguous(), "out must be a contiguous f32 [M, N]");
+  TORCH_CHECK(x.device() == w.device() && out.device() == x.device(), "gemm_prefill_f32: tensors on different devices");
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(x.data_ptr()) & 15) == 0 && (reinterpret_cast<uintptr_t>(w.data_ptr()) & 15) == 0,
+              "gemm_prefill_f32: x and w must be 16-byte aligned");
+  TORCH_CHECK(M < (1LL << 31) / TM);
+  if (M == 0) return;
+  const int MT = (int)((M + TM - 1) / TM), NTL = (int)(N / TN);
+  static const int gm_env = env_int("LS_PGEMM_GROUP", 8);
+  const int gm = std::max(1, std::min(gm_env, MT));
+  gemm_pp_kernel<EPI_STORE, 0><<<dim3((unsigned)(MT * NTL)), 512, 0, at::hip::getCurrentHIPStream()>>>(
+      (const bf16*)x.data_ptr(), x.stride(0), (const bf16*)w.data_ptr(), (int)M, (int)K, nullptr, 0, MT, NTL, 0, gm,
+      1, out.data_ptr<float>());
 }

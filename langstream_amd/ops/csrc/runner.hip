@@ -133,6 +133,8 @@ void skinny_gemm_add_rmsnorm(at::Tensor out, at::Tensor x, at::Tensor w, at::Ten
                              double eps);
 void gemm_prefill(at::Tensor out, at::Tensor x, at::Tensor w, bool silu, int64_t variant);
 bool gemm_prefill_supported(const at::Tensor& w, bool silu);
+void gemm_prefill_f32(at::Tensor out, at::Tensor x, at::Tensor w);
+bool gemm_prefill_f32_supported(const at::Tensor& w);
 bool decode_gemm_supported(const at::Tensor& w, bool silu);
 int64_t decode_gemm_workspace(int64_t M, int64_t N, int64_t K, bool silu);
 void decode_gemm_qkv_rope(at::Tensor qkv, at::Tensor x, at::Tensor w, at::Tensor workspace, at::Tensor pos,
@@ -295,6 +297,20 @@ class LlamaRunner {
       return e == nullptr || e[0] != '0';
     }();
     const int64_t R = x.size(0);
+    // batches from LS_HEAD_PP_MIN_T rows (default 129): the head is MFMA-bound there, so
+    // the ping-pong prefill kernel with an f32 epilogue: 261 vs 279 us at M = 256, 247 vs
+    // 268 at 192 (profiles/r5/head_pp_r5ag.log; its scattered f32 stores of 131 MB of
+    // logits keep it off the MFMA rate); smaller batches stay on the decode GEMM
+    static const int64_t pp_min = [] {
+      const char* e = getenv("LS_HEAD_PP_MIN_T");
+      return e ? atoll(e) : 129;
+    }();
+    if (pp_min > 0 && R >= pp_min && gemm_prefill_f32_supported(lm_head_) &&
+        (reinterpret_cast<uintptr_t>(x.data_ptr()) & 15) == 0 && x.stride(1) == 1 && x.stride(0) % 8 == 0) {
+      at::Tensor out = at::empty({R, lm_head_.size(0)}, x.options().dtype(at::kFloat));
+      gemm_prefill_f32(out, x, lm_head_);
+      return out;
+    }
     if (dg_head && dgemm_enabled() && R >= 1 && decode_gemm_f32_supported(lm_head_, std::min<int64_t>(R, kDgemmMaxM))) {
       at::Tensor xc = x.contiguous();
       at::Tensor out = at::empty({R, lm_head_.size(0)}, x.options().dtype(at::kFloat));

@@ -497,6 +497,21 @@ def test_gemm_prefill_pingpong_splitk(M, N, K):
     _close(out, x.float() @ w.float().t(), 0.02, 0.02)
 
 
+@pytest.mark.parametrize("M,N,K", [(1, 512, 256), (129, 2048, 1024), (200, 768, 4096), (256, 128256, 4096),
+                                   (300, 1024, 512)])
+def test_gemm_prefill_f32_output(M, N, K):
+    """The ping-pong kernel's f32-output form (the LM head of 129..256-row decode batches)
+    vs fp32, M tails included; N = 128256 is the Llama-3 vocabulary."""
+    torch.manual_seed(M + N + K + 11)
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=DEV) / K ** 0.5).to(torch.bfloat16)
+    out = torch.empty(M, N, device=DEV, dtype=torch.float32)
+    ops.hip().gemm_prefill_f32(out, x, w)
+    torch.cuda.synchronize()
+    ref = x.float() @ w.float().t()
+    assert torch.allclose(out, ref, atol=2e-3, rtol=2e-3), float((out - ref).abs().max())
+
+
 @pytest.mark.parametrize("variant", [1, 2])
 @pytest.mark.parametrize("M,F,K", [(77, 128, 256), (1000, 384, 1024), (4096, 256, 512), (40000, 640, 256)])
 def test_gemm_prefill_pingpong_silu(M, F, K, variant):
