@@ -795,3 +795,32 @@ def test_genai_toolkit_compute_expressions():
     assert compute("fn:str(fn:fromJson(value.fieldJson))") == "{this=that}"
     assert _json.loads(compute("fn:toJson(fn:unpack(value.fieldCsv, 'f1,f2,f3'))")) == {"f1": "a", "f2": "b", "f3": "c"}
     assert compute("fn:str(1.0E7)") == "1.0E7" and compute("fn:str(0.5)") == "0.5"
+
+
+# ---------------------------------------------------------------- WebCrawlerConfigurationTest
+def test_webcrawler_allowed_domains_and_forbidden_paths():
+    """WebCrawlerConfigurationTest.testAllowedDomains / testForbiddenPaths."""
+    from langstream_amd.agents.webcrawler import CrawlerConfig
+
+    def dom(url, allowed):
+        return CrawlerConfig(set(allowed), set()).is_allowed_url(url)
+
+    def fp(url, forbidden):
+        return CrawlerConfig({"domain"}, set(forbidden)).is_allowed_url(url)
+    assert dom("http://domain/something/....", {"domain"})
+    assert dom("https://domain/something/....", {"domain"})
+    assert dom("https://domain/something/....", {"https://domain"})
+    assert not dom("https://domain/something/....", {"https://domain/else"})
+    assert not dom("not-an-url", {"domain"})
+    assert not dom("http://domain/something/....", set())
+    assert fp("http://domain/something/something", set())
+    assert fp("https://domain/something", {"/something/"})
+    assert fp("https://domain/something/secondlevel", {"/something-else"})
+    assert fp("https://domain/something/secondlevel", {"/secondlevel"})
+    assert not fp("https://domain/something/", {"/something/"})
+    assert not fp("https://domain/something/secondlevel", {"/something"})
+    assert not fp("https://domain/something/secondlevel", {"/something/sec"})
+    assert not fp("not-an-url", {"/something"})
+    assert not fp("something:somewhere", {"/something"})
+    assert fp("https://domain", {"/something"}) and fp("https://domain/", {"/something"})
+    assert not fp("https://domain", {"/"}) and not fp("https://domain/", {"/"})
