@@ -178,12 +178,27 @@ class TextNormaliserAgent(SingleRecordAgentProcessor):
 
     def process_record(self, record):
         t = to_text(record.value())
+        if self.trim:
+            t = trim_spaces(t)
         if self.lower:
             t = t.lower()
-        if self.trim:
-            t = re.sub(r"[ \t]+", " ", t)
-            t = re.sub(r"\n\s*\n+", "\n\n", t).strip()
         return [SimpleRecord.copy_from(record, value=t)]
+
+
+def trim_spaces(s: str) -> str:
+    """TextNormaliserAgent.trimSpaces: the same replacement chain, in order -- tabs to a
+    space, space runs to one, one pass of triple newlines to double, (space + blank line)
+    runs to one, (space + newline) runs to a newline, newline + space to a newline, trim."""
+    s = re.sub(r"\t+", " ", s)
+    s = re.sub(r" +", " ", s)
+    s = s.replace("\n\n\n", "\n\n")
+    s = re.sub(r"( \n\n)+", " \n\n", s)
+    s = re.sub(r"( \n)+", "\n", s)
+    s = s.replace("\n ", "\n")
+    return s.strip(_JAVA_TRIM)   # String.trim: code points <= U+0020 only
+
+
+_JAVA_TRIM = "".join(chr(c) for c in range(33))
 
 
 @register_agent("document-to-json")

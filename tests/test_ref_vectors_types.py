@@ -824,3 +824,12 @@ def test_webcrawler_allowed_domains_and_forbidden_paths():
     assert not fp("something:somewhere", {"/something"})
     assert fp("https://domain", {"/something"}) and fp("https://domain/", {"/something"})
     assert not fp("https://domain", {"/"}) and not fp("https://domain/", {"/"})
+
+
+def test_text_normaliser_trim_spaces():
+    """TextNormaliserAgentTest.testTrimSpaces (and Java's trim: a leading NBSP stays)."""
+    from langstream_amd.agents.text import trim_spaces
+    text = ("  some  \n\n text with \t \tspaces \n\n\n this is a new line. \n \n \n     \n then two new lines. "
+            "\n\n  \n\n  \n\n  \n\n end")
+    assert trim_spaces(text) == ("some\n\ntext with spaces\n\nthis is a new line.\nthen two new lines.\n\nend")
+    assert trim_spaces(" x ") == " x"
