@@ -208,11 +208,14 @@ class DocumentToJsonAgent(SingleRecordAgentProcessor):
         self.copy_props = str(configuration.get("copy-properties", "true")).lower() == "true"
 
     def process_record(self, record):
+        # DocumentToJsonAgent.java: the value becomes the JSON TEXT of {text-field: text,
+        # header: value...} (compact, as Jackson writes it); byte header values as UTF-8 text
         out = {self.field: to_text(record.value())}
         if self.copy_props:
             for h in record.headers():
-                out[h.key] = h.value_as_string()
-        return [SimpleRecord.copy_from(record, value=out)]
+                v = h.value
+                out[h.key] = v.decode("utf-8", errors="replace") if isinstance(v, (bytes, bytearray)) else v
+        return [SimpleRecord.copy_from(record, value=json.dumps(out, separators=(",", ":"), ensure_ascii=False))]
 
 
 # ---------------------------------------------------------------- extraction

@@ -833,3 +833,21 @@ def test_text_normaliser_trim_spaces():
             "\n\n  \n\n  \n\n  \n\n end")
     assert trim_spaces(text) == ("some\n\ntext with spaces\n\nthis is a new line.\nthen two new lines.\n\nend")
     assert trim_spaces(" x ") == " x"
+
+
+def test_document_to_json():
+    """DocumentToJsonTest.textConvertToJson: the value becomes compact JSON text; byte
+    header values as UTF-8 text; copy-properties false keeps only the text field."""
+    import json as _json
+    from langstream_amd.agents.text import DocumentToJsonAgent
+    from langstream_amd.api.record import Header
+    rec = SimpleRecord.of("filename.txt", "This is a English".encode(),
+                          [Header("detected-language", "en"), Header("other-header", b"bytearray-value")], "origin")
+    a = DocumentToJsonAgent()
+    a.init({"text-field": "document", "copy-properties": "true"})
+    out = a.process_record(rec)[0].value()
+    assert isinstance(out, str) and _json.loads(out) == {"detected-language": "en", "document": "This is a English",
+                                                         "other-header": "bytearray-value"}
+    assert ": " not in out and ", " not in out
+    a.init({"text-field": "document", "copy-properties": "false"})
+    assert a.process_record(rec)[0].value() == '{"document":"This is a English"}'
