@@ -145,10 +145,9 @@ __global__ void __launch_bounds__(64 * WPP) __attribute__((amdgpu_waves_per_eu(2
   // tools/attn_bench.py runs with a ring of pools.  LS_ATTN_NT=0 turns it off.
   const int kbyte = 8 * h * 2;
 
-  // AUX 3 (LS_ATTN_NT=2, off by default): the FIRST block of a sequence loaded with the
+  // AUX 3 (LS_ATTN_NT=2, the default): the FIRST block of a sequence loaded with the
   // cached policy, for template-prefix blocks shared by every prompt (engine/
-  // prefix_cache.py).  Measured slower than all-nt even with shared blocks (the shared
-  // block's re-reads hit with nt loads as well; see the launch site).
+  // prefix_cache.py); see the launch site for the measurements behind the default.
   auto issue_k_p = [&](int bi, uint4(&kf)[4][KS], auto polc) {
     constexpr int POL = decltype(polc)::value;
     const int blk = __builtin_amdgcn_readfirstlane(block_of(bi));
@@ -506,13 +505,16 @@ static void decode_attention_launch(at::Tensor& out, const at::Tensor& q, const 
   static const int env_wpp = getenv("LS_ATTN_WPP") ? atoi(getenv("LS_ATTN_WPP")) : 0;
   static const bool pipe = getenv("LS_ATTN_PIPE") ? atoi(getenv("LS_ATTN_PIPE")) != 0 : true;
   const bool rope = ra != nullptr;
-  // LS_ATTN_NT (read per launch, A/B inside one process): 0 cached loads, 1 (default) all
-  // nt, 2 nt except each sequence's first block.  All-nt wins with shared template-prefix
-  // blocks too: B = 256 ctx 270..550, one shared first block, cold caches: 67.2 / 72.2 /
-  // 73.5 us for 1 / 2 / 0 (profiles/r5/attn_shared_first_block_r5ab.log); in the RAG bench
-  // timeline 67.7 vs 70.7 us per layer (attn_nt_ab_r5ac).
+  // LS_ATTN_NT (read per launch, A/B inside one process): 0 cached loads, 1 all nt, 2
+  // (default) nt except each sequence's first block (the shared template-prefix block).
+  // The attention kernel alone is faster all-nt (B = 256 ctx 270..550, one shared first
+  // block, cold caches: 67.2 / 72.2 / 73.5 us for 1 / 2 / 0,
+  // profiles/r5/attn_shared_first_block_r5ab.log; bench timeline 67.7 vs 70.7 us), but the
+  // whole RAG bench ran less GPU time with 2 in both rounds of a same-box A/B (16.55 /
+  // 16.63 s vs 16.74 / 17.25 s, ab_head_attn_r5ai.log): the decode GEMMs that follow
+  // lose more than the attention gains.
   const char* ent = getenv("LS_ATTN_NT");
-  const int attn_nt = ent ? atoi(ent) : 1;
+  const int attn_nt = ent ? atoi(ent) : 2;
   const RopeArgs rargs = rope ? *ra : RopeArgs{};
   const int wpp = env_wpp == 1 || env_wpp == 4 ? env_wpp : ((int64_t)B * Hkv >= WAVE_SLOTS && ns == 1 ? 1 : 4);
   dim3 grid(B * Hkv, ns);
