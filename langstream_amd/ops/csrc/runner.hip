@@ -297,13 +297,15 @@ class LlamaRunner {
       return e == nullptr || e[0] != '0';
     }();
     const int64_t R = x.size(0);
-    // batches from LS_HEAD_PP_MIN_T rows (default 129): the head is MFMA-bound there, so
-    // the ping-pong prefill kernel with an f32 epilogue: 261 vs 279 us at M = 256, 247 vs
-    // 268 at 192 (profiles/r5/head_pp_r5ag.log; its scattered f32 stores of 131 MB of
-    // logits keep it off the MFMA rate); smaller batches stay on the decode GEMM
+    // LS_HEAD_PP_MIN_T = n > 0: batches of n+ rows on the ping-pong prefill kernel with an
+    // f32 epilogue -- faster alone (261 vs 279 us at M = 256, 247 vs 268 at 192:
+    // profiles/r5/head_pp_r5ag.log) but slower end to end: the RAG bench's closed-loop rate
+    // was 1.8 % lower with it in all three rounds of a same-box A/B (ab_head_r5ak.log; it
+    // streams the 1 GB head through the caches, where the decode GEMM's loads are
+    // non-temporal).  Off by default.
     static const int64_t pp_min = [] {
       const char* e = getenv("LS_HEAD_PP_MIN_T");
-      return e ? atoll(e) : 129;
+      return e ? atoll(e) : 0;
     }();
     if (pp_min > 0 && R >= pp_min && gemm_prefill_f32_supported(lm_head_) &&
         (reinterpret_cast<uintptr_t>(x.data_ptr()) & 15) == 0 && x.stride(1) == 1 && x.stride(0) % 8 == 0) {
