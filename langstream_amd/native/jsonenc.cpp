@@ -22,6 +22,7 @@
 // lost (float32(parsed value) is the original float32).
 #include <Python.h>
 #include <pybind11/pybind11.h>
+#include <pybind11/numpy.h>
 
 #include <charconv>
 #include <cmath>
@@ -382,6 +383,41 @@ void bind_jsonenc(py::module_& m) {
       if (!row) throw py::error_already_set();
       PyList_SET_ITEM(out.ptr(), i, row);
     }
+    return out;
+  }, py::arg("rows"));
+  // the inverse: a sequence of equal-length number lists (e.g. the retrieved documents'
+  // Float32List vectors the re-rank agent scores) -> a float32 [n, d] array, reading the
+  // PyFloats directly (np.asarray over Python floats cost ~0.2 ms for 20 x 384)
+  m.def("f32_matrix", [](py::sequence rows) {
+    const py::ssize_t n = (py::ssize_t)py::len(rows);
+    py::ssize_t d = -1;
+    std::vector<float> buf;
+    for (py::ssize_t i = 0; i < n; ++i) {
+      PyObject* r = PySequence_GetItem(rows.ptr(), i);
+      if (!r) throw py::error_already_set();
+      PyObject* fast = PySequence_Fast(r, "f32_matrix: rows must be sequences");
+      Py_DECREF(r);
+      if (!fast) throw py::error_already_set();
+      const py::ssize_t m = PySequence_Fast_GET_SIZE(fast);
+      if (d < 0) { d = m; buf.reserve((size_t)(n * d)); }
+      if (m != d) { Py_DECREF(fast); throw py::value_error("f32_matrix: ragged rows"); }
+      PyObject** items = PySequence_Fast_ITEMS(fast);
+      for (py::ssize_t j = 0; j < m; ++j) {
+        PyObject* o = items[j];
+        double v;
+        if (PyFloat_CheckExact(o)) v = PyFloat_AS_DOUBLE(o);
+        else {
+          if (PyBool_Check(o) || !PyNumber_Check(o)) { Py_DECREF(fast); throw py::value_error("f32_matrix: non-numeric entry"); }
+          v = PyFloat_AsDouble(o);
+          if (v == -1.0 && PyErr_Occurred()) { Py_DECREF(fast); throw py::error_already_set(); }
+        }
+        buf.push_back((float)v);
+      }
+      Py_DECREF(fast);
+    }
+    if (d < 0) d = 0;
+    py::array_t<float> out({n, d});
+    if (n * d) std::memcpy(out.mutable_data(), buf.data(), sizeof(float) * (size_t)(n * d));
     return out;
   }, py::arg("rows"));
   m.def("json_register_f32list", [](py::handle t) {

@@ -40,6 +40,21 @@ def f32_rows(t) -> list:
     return [Float32List(r) for r in t.tolist()]
 
 
+def f32_matrix(rows):
+    """A list of equal-length number lists -> float32 [n, d] ndarray (native when built;
+    numpy otherwise).  Raises ValueError on ragged or non-numeric rows."""
+    import numpy as np
+    if _native is None:
+        _load()
+    fn = _f32_matrix_native
+    if fn is not None:
+        return fn(rows)
+    return np.asarray(rows, dtype=np.float32).reshape(len(rows), -1)
+
+
+_f32_matrix_native = None
+
+
 def _load():
     global _native, _unsupported
     try:
@@ -50,6 +65,8 @@ def _load():
             m.json_register_f32list(Float32List)
             global _f32_rows_native
             _f32_rows_native = getattr(m, "f32_rows", None)
+        global _f32_matrix_native
+        _f32_matrix_native = getattr(m, "f32_matrix", None)
     except Exception:  # noqa: BLE001  (no toolchain: plain json)
         _native, _unsupported = False, None
 
