@@ -83,3 +83,16 @@ def test_float32_vectors_use_float32_digits():
     # plain lists keep the double digits
     x = float(np.float32(0.1))
     assert fastjson.dumps([x]) == json.dumps([x]) and fastjson.dumps(Float32List([x])) == "[0.1]"
+
+
+def test_f32_matrix_matches_numpy():
+    rng = random.Random(3)
+    rows = [[rng.uniform(-2, 2) for _ in range(17)] for _ in range(5)]
+    rows[2][3] = 7                                     # ints convert too
+    got = fastjson.f32_matrix(rows)
+    assert got.dtype == np.float32 and got.shape == (5, 17)
+    np.testing.assert_array_equal(got, np.asarray(rows, dtype=np.float32))
+    with pytest.raises(ValueError):
+        fastjson.f32_matrix([[1.0, 2.0], [3.0]])       # ragged
+    with pytest.raises((TypeError, ValueError)):
+        fastjson.f32_matrix([[1.0, "x"]])              # non-numeric
