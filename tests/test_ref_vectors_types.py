@@ -851,3 +851,86 @@ def test_document_to_json():
     assert ": " not in out and ", " not in out
     a.init({"text-field": "document", "copy-properties": "false"})
     assert a.process_record(rec)[0].value() == '{"document":"This is a English"}'
+
+
+# ---------------------------------------------------------------------------------------
+# TextChunkerAgentTest (langstream-agents-text-processing/src/test/.../TextChunkerAgentTest.java:34-171)
+# ---------------------------------------------------------------------------------------
+
+def _chunks(cfg, text):
+    from langstream_amd.agents.text import TextSplitterAgent
+    a = TextSplitterAgent()
+    a.init(cfg)
+    out = a.process_record(SimpleRecord.of("filename.txt", text.encode(), [], "origin"))
+    return [r.value() if isinstance(r.value(), str) else r.value().decode() for r in out]
+
+
+@pytest.mark.parametrize("size,overlap,text,lf,expected", [
+    (20, 5, "Hello world", "length", ["Hello world"]),
+    (15, 5, "Hello world. This is a great day", "length", ["Hello world.", "This is a great", "great day"]),
+    (20, 5, "", "length", []),
+    (20, 5, " ", "length", []),
+    (20, 5, "Hello world", "cl100k_base", ["Hello world"]),
+    (10, 2, "Hello world, I would like to see some overlap here", "cl100k_base",
+     ["Hello world, I would like", "like to see some overlap", "overlap here"]),
+])
+def test_text_chunker(size, overlap, text, lf, expected, monkeypatch):
+    if lf == "cl100k_base":
+        # no cl100k_base vocabulary offline: every word of these texts is ONE cl100k token,
+        # so counting the pre-tokenizer's pieces is exact here (the vectors pin the
+        # splitter's token-window logic; the BPE counter itself: test_text_fixtures)
+        import regex
+        from langstream_amd import tokenizers
+        pat = regex.compile(r"""'(?i:[sdmt]|ll|ve|re)|[^\r\n\p{L}\p{N}]?+\p{L}+|\p{N}{1,3}| ?[^\s\p{L}\p{N}]++[\r\n]*|\s*[\r\n]|\s+(?!\S)|\s+""")
+        monkeypatch.setattr(tokenizers, "cl100k_counter", lambda: (lambda t: len(pat.findall(t))))
+    cfg = {"splitter_type": "RecursiveCharacterTextSplitter", "separators": ["\n\n", "\n", " ", ""],
+           "keep_separator": False, "chunk_size": size, "chunk_overlap": overlap, "length_function": lf}
+    assert _chunks(cfg, text) == expected
+
+
+def test_text_chunker_keep_separator():
+    cfg = {"splitter_type": "RecursiveCharacterTextSplitter", "separators": ["\n\n", "\n", " ", ""],
+           "keep_separator": True, "chunk_size": 15, "chunk_overlap": 5, "length_function": "length"}
+    assert _chunks(cfg, "Hello world. This is a great day") == ["Hello world.", "This is a", "is a great day"]
+
+
+def test_text_chunker_regex_separator():
+    cfg = {"splitter_type": "RecursiveCharacterTextSplitter", "separators": ["\\d+"],
+           "keep_separator": True, "chunk_size": 15, "chunk_overlap": 5, "length_function": "length"}
+    assert _chunks(cfg, "Hello1world.2This3is4a5great6day") == ["Hello1world.", "2This3is4a", "3is4a5great6day"]
+
+
+# ---------------------------------------------------------------------------------------
+# ReRankAgentTest (langstream-ai-agents/src/test/.../rerank/ReRankAgentTest.java:31-118)
+# ---------------------------------------------------------------------------------------
+
+_RERANK_CFG = {"output-field": "value.output_field", "query-text": "value.query",
+               "query-embeddings": "value.query_embeddings", "text-field": "record.text",
+               "embeddings-field": "record.embeddings"}
+
+
+def test_rerank_none_compact_json():
+    """testNone: algorithm none copies the (empty) list; a JSON-text value stays JSON text."""
+    from langstream_amd.agents.rerank import ReRankAgent
+    a = ReRankAgent()
+    a.init(dict(_RERANK_CFG, field="value.field", algorithm="none"))
+    from langstream_amd.agents.genai.mutable import _text_origin, text_form
+    r = a.process_record(SimpleRecord.of("key", '{\n    "field": [\n    ]\n}\n'))[0]
+    # the map stays a map in-process; its hand-off form is the compact JSON text
+    assert text_form(r.value(), _text_origin(r, 1)) == '{"field":[],"output_field":[]}'
+
+
+def test_rerank_mmr():
+    """testMMR: lambda 0.7 puts the query-identical document first; inputs unchanged."""
+    from langstream_amd.agents.rerank import ReRankAgent
+    a = ReRankAgent()
+    a.init(dict(_RERANK_CFG, field="value.query_results", algorithm="MMR", **{"lambda": 0.7}))
+    one = {"text": "one", "embeddings": [1.0, 2.0]}
+    two = {"text": "two", "embeddings": [3.0, 4.0]}
+    v = {"query": "tell my a number, for instance two", "query_embeddings": [3.0, 4.0],
+         "query_results": [dict(one), dict(two)]}
+    out = a.process_record(SimpleRecord.of("key", v))[0].value()
+    assert out["query_embeddings"] == [3.0, 4.0]
+    assert out["query_results"] == [one, two]
+    assert out["output_field"] == [two, one]
+    assert out["query"] == "tell my a number, for instance two"
