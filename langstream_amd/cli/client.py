@@ -13,12 +13,19 @@ from typing import Any, Dict, Iterator, Optional
 
 
 def zip_directory(path: str) -> bytes:
+    """The application directory as a zip, minus ``.langstreamignore`` matches (ignored
+    directories are not descended into; ``ApplicationPackager.java:44-80``)."""
+    from .ignore import load_ignore
+    ign = load_ignore(path)
     buf = io.BytesIO()
     with zipfile.ZipFile(buf, "w", zipfile.ZIP_DEFLATED) as z:
         for root, dirs, files in os.walk(path):
-            dirs[:] = sorted(d for d in dirs if d not in ("__pycache__", ".git"))
+            dirs[:] = sorted(d for d in dirs if d not in ("__pycache__", ".git")
+                             and not (ign and ign.matches(os.path.join(root, d), True)))
             for fn in sorted(files):
                 full = os.path.join(root, fn)
+                if ign and ign.matches(full, False):
+                    continue
                 z.write(full, os.path.relpath(full, path))
     return buf.getvalue()
 

@@ -934,3 +934,75 @@ def test_rerank_mmr():
     assert out["query_results"] == [one, two]
     assert out["output_field"] == [two, one]
     assert out["query"] == "tell my a number, for instance two"
+
+
+# ---------------------------------------------------------------------------------------
+# GitIgnoreParserTest (langstream-cli/src/test/.../GitIgnoreParserTest.java:27-77, fixture
+# src/test/resources/.langstreamignore reproduced below)
+# ---------------------------------------------------------------------------------------
+
+_LANGSTREAMIGNORE = ("aaa\n\n#comment\n\\#\nbbb/\n/ccc\nddd/eee\nfff/ggg/\nhhh/*\n!hhh/hh\n*/iii\njjj/*/kkk\n"
+                     "lll*\nmmm?\nnnn[op-r]sss\n**/ttt\nuuu/**\nvvv/**/www\n")
+
+
+@pytest.mark.parametrize("path,is_dir,expected", [
+    ("aaa", False, True), ("a/aaa", False, True), ("a/a/aaa", False, True), ("#comment", False, False),
+    ("#", False, True), ("bbb", True, True), ("b/bbb", True, True), ("bbb", False, False),
+    ("b/bbb", False, False), ("ccc", False, True), ("c/ccc", False, False), ("ddd/eee", False, True),
+    ("d/ddd/eee", False, False), ("fff/ggg", True, True), ("fff/ggg", False, False), ("hhh/h", False, True),
+    ("hhh/hh", False, False), ("i/iii", False, True), ("i/i/iii", False, False), ("jjj/j/kkk", False, True),
+    ("jjj/j/k/kkk", False, False), ("lllm", False, True), ("lll", False, True), ("lllmm", False, True),
+    ("lll/m", False, False), ("mmml", False, True), ("mmm", False, False), ("mmmll", False, False),
+    ("mmm/l", False, False), ("nnnsss", False, False), ("nnnosss", False, True), ("nnnpsss", False, True),
+    ("nnnqsss", False, True), ("nnnrsss", False, True), ("ttt", False, True), ("t/ttt", False, True),
+    ("t/t/ttt", False, True), ("uuu", False, False), ("uuu", True, False), ("uuu/u", False, True),
+    ("uuu/u/u", False, True), ("vvv/www", False, False), ("vvv/v/www", False, True),
+    ("vvv/v/v/www", False, True),
+])
+def test_langstreamignore(tmp_path, path, is_dir, expected):
+    from langstream_amd.cli.ignore import IgnoreRules
+    f = tmp_path / ".langstreamignore"
+    f.write_text(_LANGSTREAMIGNORE)
+    assert IgnoreRules.from_file(str(f)).matches(str(tmp_path / path), is_dir) is expected
+
+
+def test_langstreamignore_app_zip(tmp_path):
+    """ApplicationPackager: matched files and directories stay out of the deploy zip."""
+    import io
+    import zipfile
+    from langstream_amd.cli.client import zip_directory
+    (tmp_path / ".langstreamignore").write_text("*.log\nbuild/\n!keep.log\n")
+    for rel in ("pipeline.yaml", "x.log", "keep.log", "build/out.bin", "python/agent.py", "python/y.log"):
+        p = tmp_path / rel
+        p.parent.mkdir(parents=True, exist_ok=True)
+        p.write_text("x")
+    names = set(zipfile.ZipFile(io.BytesIO(zip_directory(str(tmp_path)))).namelist())
+    assert names == {".langstreamignore", "pipeline.yaml", "keep.log", "python/agent.py"}
+
+
+# ---------------------------------------------------------------------------------------
+# LanguageDetectorTest (langstream-agents-text-processing/src/test/.../LanguageDetectorTest.java:30-55)
+# ---------------------------------------------------------------------------------------
+
+def test_language_detector():
+    from langstream_amd.agents.text import LanguageDetectorAgent
+    a = LanguageDetectorAgent()
+    a.init({"property": "detected-language"})
+
+    def detect(text):
+        r = a.process_record(SimpleRecord.of("filename.txt", text.encode(), [], "origin"))[0]
+        return {h.key: h.value for h in r.headers()}["detected-language"]
+    assert detect("This is a English") == "en"
+    assert detect("Questo é italiano") == "it"
+    assert detect("Parlez-vous français?") == "fr"
+
+
+# DropTest (langstream-ai-agents/src/test/.../DropTest.java:33-90): every record form dropped
+@pytest.mark.parametrize("key,value", [("test-key", {"firstName": "Jane"}), ({"k": 1}, {"v": 2}),
+                                       ("test-key", b""), ("key", 42)])
+def test_drop_step(key, value):
+    from langstream_amd.agents.genai.steps import DropStep
+    from langstream_amd.agents.genai.mutable import MutableRecord
+    m = MutableRecord.from_record(SimpleRecord.of(key, value))
+    DropStep({}).process(m)
+    assert m.to_record() is None
