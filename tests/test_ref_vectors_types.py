@@ -1006,3 +1006,190 @@ def test_drop_step(key, value):
     m = MutableRecord.from_record(SimpleRecord.of(key, value))
     DropStep({}).process(m)
     assert m.to_record() is None
+
+
+# ---------------------------------------------------------------------------------------
+# FlowControlAgentsTest (langstream-agents-flow-control/src/test/.../FlowControlAgentsTest.java:45-260)
+# ---------------------------------------------------------------------------------------
+
+class _SideProducer:
+    def __init__(self, fail_on=None):
+        self.records, self.fail_on = [], fail_on
+
+    def start(self):
+        pass
+
+    def close(self):
+        pass
+
+    def write(self, record):
+        from concurrent.futures import Future
+        f = Future()
+        if self.fail_on and self.fail_on in str(record.value()):
+            f.set_exception(IOError("Simulated error"))
+        else:
+            self.records.append(record)
+            f.set_result(None)
+        return f
+
+
+def _with_side_producer(agent, producer):
+    from types import SimpleNamespace
+    provider = SimpleNamespace(create_producer=lambda agent_id, topic, *a, **k: producer)
+    agent.context = SimpleNamespace(topic_connection_provider=provider, global_agent_id="app-agent")
+
+
+def test_timer_source():
+    from langstream_amd.agents.flow import TimerSource
+    t = TimerSource()
+    t.init({"period-seconds": 0.01, "fields": [
+        {"name": "value.now", "expression": "fn:now()"}, {"name": "key.someid", "expression": "fn:uuid()"},
+        {"name": "properties.someprop", "expression": "fn:random(1000)"}]})
+    got = []
+    while len(got) < 10:
+        read = t.read()
+        assert len(read) <= 1
+        got += read
+    for r in got:
+        assert r.value()["now"] is not None and r.key()["someid"]
+        assert {h.key: h.value for h in r.headers()}["someprop"] is not None
+
+
+def test_trigger_event_processor():
+    from langstream_amd.api.record import Header
+    from langstream_amd.agents.flow import TriggerEventAgent
+    p = TriggerEventAgent()
+    p.init({"when": "value.activator > 5", "destination": "other-topic", "fields": [
+        {"name": "value.computed", "expression": "fn:uppercase(value.original)"},
+        {"name": "key.computed", "expression": "fn:lowercase(key.original)"},
+        {"name": "properties.computed", "expression": "fn:lowercase(properties.original)"}]})
+    side = _SideProducer()
+    _with_side_producer(p, side)
+    p.start()
+    for i in range(10):
+        rec = SimpleRecord.of('{"original": "Hello World %d"}\n' % i, '{"original": "Hello Folks %d", "activator": %d}\n'
+                              % (i, i), [Header("original", "Some session id %d" % i)])
+        out = []
+        p.process([rec], out.append)
+        assert len(out) == 1 and out[0].result_records[0] is rec     # the source record continues
+        if i > 5:
+            r = side.records.pop(0)
+            assert r.value()["computed"] == ("Hello Folks %d" % i).upper()
+            assert r.key()["computed"] == ("Hello World %d" % i).lower()
+            assert {h.key: h.value for h in r.headers()}["computed"] == ("Some session id %d" % i).lower()
+        assert not side.records
+
+
+def test_trigger_event_processor_producer_errors():
+    from langstream_amd.agents.flow import TriggerEventAgent
+    p = TriggerEventAgent()
+    p.init({"destination": "other-topic", "fields": [{"name": "value", "expression": "fn:uppercase(value)"}]})
+    side = _SideProducer(fail_on="FAIL-ME")
+    _with_side_producer(p, side)
+    p.start()
+    for i in range(10):
+        fail = i % 2 == 0
+        content = ("fail-me" if fail else "keep-me") + " %d" % i
+        rec = SimpleRecord.of(None, content)
+        out = []
+        p.process([rec], out.append)
+        assert len(out) == 1 and out[0].source_record is rec
+        if fail:
+            assert out[0].error is not None
+        else:
+            assert out[0].error is None
+            assert side.records.pop(0).value() == content.upper()
+
+
+# ---------------------------------------------------------------------------------------
+# WebCrawlerStatusTest (langstream-agent-webcrawler/src/test/.../WebCrawlerStatusTest.java:32-175)
+# ---------------------------------------------------------------------------------------
+
+_U = ["https://site/page%d" % i for i in range(6)]
+
+
+def _verify(st, visited, pending, remaining):
+    assert (len(st.urls), len(st.pending), len(st.remaining)) == (visited, pending, remaining)
+
+
+@pytest.mark.parametrize("first,again", [(_U[1], _U[1]), (_U[2], _U[2] + "#anchor")])
+def test_crawler_status_prevents_cycles(first, again):
+    from langstream_amd.agents.webcrawler import CrawlerStatus
+    st = CrawlerStatus()
+    st.add_url(first, "page", 0, True)
+    _verify(st, 1, 1, 1)
+    st.add_url(again, "page", 0, True)
+    _verify(st, 1, 1, 1)
+    url = st.next_url()
+    _verify(st, 1, 0, 1)
+    st.url_processed(url)
+    _verify(st, 1, 0, 0)
+    st.add_url(first, "page", 0, True)
+    st.add_url(again, "page", 0, False)
+    _verify(st, 1, 0, 0)
+
+
+def _crawler(**kw):
+    from langstream_amd.agents.webcrawler import CrawlerConfig, CrawlerStatus, WebCrawler
+    st = CrawlerStatus()
+    return WebCrawler(CrawlerConfig({"site"}, set(), **kw), st, lambda *a: None), st
+
+
+def test_crawler_max_urls():
+    c, st = _crawler(max_urls=2)
+    assert c._add_page(_U[1], None) and c._add_page(_U[2], None)
+    assert not c._add_page(_U[3], None)
+    _verify(st, 2, 2, 2)
+
+
+def test_crawler_max_depth():
+    c, st = _crawler(max_depth=2)
+    depth = lambda u: st.urls[u][1]   # noqa: E731
+    assert c._add_page(_U[1], None)
+    assert c._add_page(_U[2], depth(_U[1]))
+    assert c._add_page(_U[3], depth(_U[2]))
+    assert not c._add_page(_U[4], depth(_U[3]))      # coming from page 3: too deep
+    assert c._add_page(_U[5], depth(_U[2]))
+    assert c._add_page(_U[4], depth(_U[2]))
+    assert depth(_U[5]) == 2
+    assert c._add_page(_U[5], depth(_U[1]))          # found from page 1: depth updated
+    assert depth(_U[5]) == 1
+    _verify(st, 5, 5, 5)
+
+
+def test_crawler_status_reload():
+    import json as _json
+    from langstream_amd.agents.webcrawler import CrawlerStatus
+    storage = {}
+
+    def persist(st):
+        storage["s"] = _json.loads(_json.dumps(st.to_json()))
+
+    def reload():
+        st = CrawlerStatus()
+        st.reload(storage.get("s"))
+        return st
+    st = CrawlerStatus()
+    st.add_url(_U[1], "page", 0, True)
+    st.add_url(_U[2], "page", 0, True)
+    _verify(st, 2, 2, 2)
+    persist(st)
+    st = reload()
+    _verify(st, 2, 2, 2)
+    url = st.next_url()
+    _verify(st, 2, 1, 2)
+    persist(st)
+    st = reload()                                     # a crash: one page was not committed
+    _verify(st, 2, 2, 2)
+    assert st.next_url() == url                       # restarts from the same point
+    _verify(st, 2, 1, 2)
+    persist(st)
+    st.url_processed(url)
+    _verify(st, 2, 1, 1)
+    persist(st)
+    st = reload()
+    _verify(st, 2, 1, 1)
+    st.url_processed(st.next_url())
+    _verify(st, 2, 0, 0)
+    persist(st)
+    _verify(reload(), 2, 0, 0)
