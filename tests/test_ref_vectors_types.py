@@ -1193,3 +1193,109 @@ def test_crawler_status_reload():
     _verify(st, 2, 0, 0)
     persist(st)
     _verify(reload(), 2, 0, 0)
+
+
+# ---------------------------------------------------------------------------------------
+# OrderedAsyncBatchExecutorTest (langstream-api/src/test/.../OrderedAsyncBatchExecutorTest.java:37-303)
+# ---------------------------------------------------------------------------------------
+
+def _await(cond, timeout=10.0):
+    import time as _t
+    end = _t.time() + timeout
+    while not cond():
+        assert _t.time() < end, "condition not reached"
+        _t.sleep(0.005)
+
+
+_BATCH_SIZES = [(0, 1), (1, 1), (1, 2), (2, 1), (2, 2), (3, 5), (5, 3)]
+
+
+@pytest.mark.parametrize("n,bs", _BATCH_SIZES)
+def test_ordered_batches_flush_interval(n, bs):
+    from langstream_amd.api.util import OrderedAsyncBatchExecutor
+    recs = ["text %d" % i for i in range(n)]
+    got = []
+
+    def proc(batch, fut):
+        got.extend(batch)
+        fut.set_result(None)
+    ex = OrderedAsyncBatchExecutor(bs, proc, 100, 4, hash)
+    ex.start()
+    for r in recs:
+        ex.add(r)
+    _await(lambda: sorted(got) == sorted(recs))     # the partial batches come with the timer
+    ex.stop()
+
+
+@pytest.mark.parametrize("n,bs", _BATCH_SIZES)
+def test_ordered_batches_no_flush_interval(n, bs):
+    from langstream_amd.api.util import OrderedAsyncBatchExecutor
+    recs = ["text %d" % i for i in range(n)]
+    got = []
+
+    def proc(batch, fut):
+        assert len(batch) == 1            # no flush interval: every item runs at once
+        got.extend(batch)
+        fut.set_result(None)
+    ex = OrderedAsyncBatchExecutor(bs, proc, 0, 4, hash)
+    ex.start()
+    for r in recs:
+        ex.add(r)
+    assert got == recs
+    ex.stop()
+
+
+@pytest.mark.parametrize("n,bs,delay_ms", [(n, bs, d) for d in (0, 200) for n, bs in
+                                           _BATCH_SIZES + [(37, 5), (50, 3)]])
+def test_ordered_batches_key_ordering(n, bs, delay_ms):
+    """Per-key order survives batches completing later on other threads."""
+    import random as _r
+    import threading
+    from langstream_amd.api.util import OrderedAsyncBatchExecutor
+    recs = [(i % 7, "text %d" % i) for i in range(n)]
+    results, lock = {}, threading.Lock()
+
+    def proc(batch, fut):
+        with lock:
+            for kv in batch:
+                results.setdefault(kv[0], []).append(kv)
+        if delay_ms == 0:
+            fut.set_result(None)
+        else:
+            threading.Timer(_r.uniform(0, delay_ms) / 1000.0, fut.set_result, (None,)).start()
+    ex = OrderedAsyncBatchExecutor(bs, proc, 100, 4, lambda kv: kv[0])
+    ex.start()
+    for kv in recs:
+        ex.add(kv)
+    expected = {}
+    for kv in recs:
+        expected.setdefault(kv[0], []).append(kv)
+    _await(lambda: sum(map(len, results.values())) == n)
+    assert results == expected
+    ex.stop()
+
+
+def test_compute_embeddings_loop_over():
+    """ComputeAIEmbeddingsTest.testLoopOver: one embedding per list item, written into a
+    copy of each item; the value's Java Map.toString as the reference prints it."""
+    from concurrent.futures import Future
+    from langstream_amd.agents.genai.el import _java_str
+    from langstream_amd.agents.genai.mutable import MutableRecord
+    from langstream_amd.agents.genai.steps import ComputeAIEmbeddingsStep
+    table = {"Jane The Princess": [1.0, 2.0, 3.0], "George The Prince": [1.0, 5.0, 3.0]}
+
+    class Svc:
+        def compute_embeddings(self, texts):
+            f = Future()
+            f.set_result([table[t] for t in texts])
+            return f
+    step = ComputeAIEmbeddingsStep({"text": "{{ record.firstName }} {{ record.lastName }}",
+                                    "embeddings-field": "record.newField", "loop-over": "value.documents_to_retrieve",
+                                    "batch-size": 1, "flush-interval": 0, "concurrency": 1}, Svc())
+    src = SimpleRecord.of(None, '{"documents_to_retrieve": [{"firstName": "Jane", "lastName": "The Princess"},'
+                                ' {"firstName": "George", "lastName": "The Prince"}]}')
+    m = MutableRecord.from_record(src)
+    step.process_async(m).result(timeout=5)
+    assert _java_str(m.to_record().value()) == (
+        "{documents_to_retrieve=[{firstName=Jane, lastName=The Princess, newField=[1.0, 2.0, 3.0]}, "
+        "{firstName=George, lastName=The Prince, newField=[1.0, 5.0, 3.0]}]}")
