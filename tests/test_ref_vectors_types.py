@@ -1299,3 +1299,32 @@ def test_compute_embeddings_loop_over():
     assert _java_str(m.to_record().value()) == (
         "{documents_to_retrieve=[{firstName=Jane, lastName=The Princess, newField=[1.0, 2.0, 3.0]}, "
         "{firstName=George, lastName=The Prince, newField=[1.0, 5.0, 3.0]}]}")
+
+
+# ---------------------------------------------------------------------------------------
+# AgentRecordTrackerTest (langstream-runtime-impl/src/test/.../AgentRecordTrackerTest.java:37-125)
+# ---------------------------------------------------------------------------------------
+
+@pytest.mark.parametrize("sinks,commits", [
+    (1, [[0]]),            # testTracker
+    (2, [[0], [1]]),       # testChunking: the source commits after the second chunk only
+    (0, [["other"]]),      # testSkippedRecord: no sink record; any commit releases it
+])
+def test_source_record_tracker(sinks, commits):
+    from langstream_amd.api.record import SourceRecordAndResult
+    from langstream_amd.runtime.tracker import SourceRecordTracker
+
+    class Src:
+        committed = []
+
+        def commit(self, recs):
+            self.committed.extend(recs)
+    src = Src()
+    tr = SourceRecordTracker(src)
+    source = SimpleRecord.of("key", "sourceValue")
+    out = [SimpleRecord.of("key", "sinkValue%d" % i) for i in range(sinks)]
+    tr.track([SourceRecordAndResult(source, out, None)])
+    for n, c in enumerate(commits):
+        tr.commit([out[i] if isinstance(i, int) else SimpleRecord.of("key", "sinkValue") for i in c])
+        assert src.committed == ([source] if n == len(commits) - 1 else [])
+    assert not tr._remaining and not tr._sink_to_source and tr.pending() == 0     # no leaks
