@@ -9,7 +9,6 @@ key, value, messageKey, topicName, destinationTopic, eventTime, properties, reco
 """
 from __future__ import annotations
 
-import copy
 import json
 from typing import Any, Dict, List, Optional
 
@@ -65,7 +64,12 @@ def safe_clone(v: Any) -> Any:
     e.g. retrieved documents with 384-float vectors -- are shared, never written.
     A deep copy per step dominated the per-record host cost of the RAG pipeline."""
     if isinstance(v, dict):
-        return dict(v)
+        if type(v) is dict:
+            return dict(v)
+        # a decoded Avro record stays one (cast prints it differently) but without its
+        # schema: steps add / drop fields, so the writer re-derives the schema as for a map
+        from ...api.avro import AvroRecord
+        return AvroRecord(v) if isinstance(v, AvroRecord) else dict(v)
     if isinstance(v, list):
         return list(v)
     return v

@@ -23,6 +23,7 @@ from ...api import temporal as _temporal
 from ...api.types import Float32, Int8, Int16, Int32
 from .el import eval_expression, eval_predicate
 from .mustache import compile_template
+from ...api.avro import AvroRecord
 from .mutable import MutableRecord
 
 log = logging.getLogger(__name__)
@@ -117,9 +118,13 @@ _CAST_TYPES = ("bytes", "string", "int8", "int16", "int32", "int64", "float", "d
 
 def _cast_value(v, st: str):
     """CastStep.convertValue: JstlTypeConverter.coerceToType to the schema type's Java
-    class (api/temporal.py); a struct value cast to STRING is its JSON text."""
+    class (api/temporal.py); a struct value cast to STRING is its JSON text: an Avro
+    record as GenericRecord.toString prints it (``{"a": 1, "b": 2}``, CastStepTest), a
+    map as Jackson writes it (compact, TransformFunctionTest.testMixedPredicate)."""
     if st == "string" and isinstance(v, (dict, list)):
-        return json.dumps(v)
+        if isinstance(v, AvroRecord):
+            return json.dumps(v)
+        return json.dumps(v, separators=(",", ":"), ensure_ascii=False)
     return _temporal.coerce(v, st)
 
 

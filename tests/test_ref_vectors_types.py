@@ -341,8 +341,9 @@ def test_cast_primitive_schema_types(value, schema_type, expected):
 def test_cast_key_value_struct_to_string():
     """CastStepTest.testKeyValueAvroToString: both parts of a KeyValue record to STRING --
     the struct's JSON text, as GenericRecord.toString writes it."""
-    key = {"keyField1": "key1", "keyField2": "key2", "keyField3": "key3"}
-    value = {"valueField1": "value1", "valueField2": "value2", "valueField3": "value3"}
+    from langstream_amd.api.avro import AvroRecord      # Utils.createTestAvroKeyValueRecord
+    key = AvroRecord({"keyField1": "key1", "keyField2": "key2", "keyField3": "key3"})
+    value = AvroRecord({"valueField1": "value1", "valueField2": "value2", "valueField3": "value3"})
     mr = _cast({"schema-type": "STRING"}, SimpleRecord.of(key, value))
     assert mr.key == '{"keyField1": "key1", "keyField2": "key2", "keyField3": "key3"}'
     assert mr.value == '{"valueField1": "value1", "valueField2": "value2", "valueField3": "value3"}'
@@ -1328,3 +1329,91 @@ def test_source_record_tracker(sinks, commits):
         tr.commit([out[i] if isinstance(i, int) else SimpleRecord.of("key", "sinkValue") for i in c])
         assert src.committed == ([source] if n == len(commits) - 1 else [])
     assert not tr._remaining and not tr._sink_to_source and tr.pending() == 0     # no leaks
+
+
+# ---------------------------------------------------------------------------------------
+# TransformFunctionTest's step chains (langstream-ai-agents/src/test/.../TransformFunctionTest.java:
+# 187-470) on the test key-value record (Utils.createTestAvroKeyValueRecord)
+# ---------------------------------------------------------------------------------------
+
+def _run_chain(steps, key, value):
+    from langstream_amd.agents.genai import steps as S
+    from langstream_amd.agents.genai.mutable import MutableRecord
+    kinds = {"drop-fields": S.DropFieldsStep, "merge-key-value": S.MergeKeyValueStep,
+             "unwrap-key-value": S.UnwrapKeyValueStep, "cast": S.CastStep, "flatten": S.FlattenStep,
+             "drop": S.DropStep, "compute": S.ComputeStep}
+    m = MutableRecord.from_record(SimpleRecord.of(key, value))
+    for cfg in steps:
+        st = kinds[cfg["type"]](cfg)
+        if m.drop:
+            break
+        if st.applies(m):
+            st.process(m)
+    return m.to_record()
+
+
+def _kv():
+    return ({"keyField1": "key1", "keyField2": "key2", "keyField3": "key3"},
+            {"valueField1": "value1", "valueField2": "value2", "valueField3": "value3"})
+
+
+def test_transform_drop_fields_chain():
+    r = _run_chain([{"type": "drop-fields", "fields": ["keyField1"]},
+                    {"type": "drop-fields", "fields": ["keyField2"], "part": "key"},
+                    {"type": "drop-fields", "fields": ["keyField3"], "part": "value"},
+                    {"type": "drop-fields", "fields": ["valueField1"]},
+                    {"type": "drop-fields", "fields": ["valueField2"], "part": "key"},
+                    {"type": "drop-fields", "fields": ["valueField3"], "part": "value"}], *_kv())
+    assert r.key() == {"keyField3": "key3"} and r.value() == {"valueField2": "value2"}
+
+
+def test_transform_compute_fields():
+    r = _run_chain([{"type": "compute", "fields": [
+        {"name": "key.newField1", "expression": "5*3", "type": "INT32"},
+        {"name": "key.newField2", "expression": "value.valueField1", "type": "STRING", "optional": False},
+        {"name": "value.newField1", "expression": "5+3", "type": "INT32"},
+        {"name": "value.newField2", "expression": "value.valueField1", "type": "STRING", "optional": False}]}], *_kv())
+    k, v = _kv()
+    assert r.key() == dict(k, newField1=15, newField2="value1")
+    assert r.value() == dict(v, newField1=8, newField2="value1")
+
+
+def test_transform_compute_without_type():
+    r = _run_chain([{"type": "compute", "fields": [
+        {"name": "destinationTopic", "expression": "'routed'"}, {"name": "messageKey", "expression": "'newKey'"},
+        {"name": "properties.foo", "expression": "'bar'"}]}],
+        "", {"level1String": "level1_1"})
+    assert r._source_ref["destination_topic"] == "routed"
+    assert r.key() == "newKey"
+    assert {h.key: h.value for h in r.headers()}["foo"] == "bar"
+
+
+@pytest.mark.parametrize("when1,when2,kept", [("key.keyField1 == 'key1'", "key.keyField2 == 'key2'", {"keyField3"}),
+                                              ("key.keyField1 == 'key100'", "key.keyField2 == 'key100'",
+                                               {"keyField1", "keyField2"})])
+def test_transform_predicates(when1, when2, kept):
+    steps = [{"type": "drop-fields", "fields": ["keyField1"], "when": when1},
+             {"type": "drop-fields", "fields": ["keyField2"], "when": when2}]
+    if "key100" in when1:
+        steps.append({"type": "drop-fields", "fields": ["keyField3"]})
+    assert set(_run_chain(steps, *_kv()).key()) == kept
+
+
+def test_transform_mixed_predicates():
+    r = _run_chain([{"type": "drop-fields", "fields": ["keyField1"], "when": "key.keyField1 == 'key1'"},
+                    {"type": "merge-key-value", "when": "key.keyField2 == 'key100'"},
+                    {"type": "unwrap-key-value", "when": "key.keyField3 == 'key100'"},
+                    {"type": "cast", "schema-type": "STRING", "when": "value.valueField1 == 'value1'"}], *_kv())
+    assert r.key() == '{"keyField2":"key2","keyField3":"key3"}'
+    assert r.value() == '{"valueField1":"value1","valueField2":"value2","valueField3":"value3"}'
+
+
+_DROP_WHEN = {"type": "drop", "when": "value.firstName=='Jane' || value.lastName=='Doe'"}
+
+
+@pytest.mark.parametrize("at,dropped", [(0, True), (1, True), (2, False)])
+def test_transform_drop_on_predicate(at, dropped):
+    steps = [{"type": "drop-fields", "fields": ["firstName"]}, {"type": "drop-fields", "fields": ["lastName"]}]
+    steps.insert(at, _DROP_WHEN)
+    r = _run_chain(steps, "test-key", {"firstName": "Jane", "lastName": "Doe", "age": 42})
+    assert (r is None) if dropped else (r.value() == {"age": 42})
