@@ -64,13 +64,126 @@ def mermaid_from_plan(plan: Dict[str, Any]) -> str:
     return "\n".join(lines)
 
 
+_AI_CONFIGS = ("vertex-configuration", "open-ai-configuration", "hugging-face-configuration",
+               "bedrock-configuration", "ollama-configuration")
+
+
+def mermaid_from_description(desc: Dict[str, Any]) -> str:
+    """Mermaid flowchart of an application DESCRIPTION (the control plane's ``apps get``
+    JSON: ``application.{resources, modules[].topics / pipelines[].agents, gateways}``),
+    laid out as ``MermaidAppDiagramGenerator.java:37-504`` lays it out: external systems,
+    then Resources / Topics / Gateways / one subgraph per pipeline, then the links --
+    agent inputs (dotted, green), gateway topics, client -> gateways, agent outputs (to a
+    topic / external sink / lone resource: yellow; agent to agent: blue; to a resource
+    beside another output: dotted blue)."""
+    app = desc.get("application") or {}
+
+    def rid(kind: str, name: str) -> str:
+        return f"{kind}-" + str(name).replace(" ", "___").lower()
+
+    gateways = []
+    for g in (app.get("gateways") or {}).get("gateways") or []:
+        prod, cons = [], []
+        chat = g.get("chat-options")
+        if chat is not None:
+            if chat.get("questions-topic") is not None:
+                prod.append(rid("topic", chat["questions-topic"]))
+            if chat.get("answers-topic") is not None:
+                cons.append(rid("topic", chat["answers-topic"]))
+        elif g.get("topic") is not None:
+            (prod if g.get("type") == "produce" else cons).append(rid("topic", g["topic"]))
+        gateways.append((rid("gateway", g.get("id")), g.get("id"), prod, cons))
+    resources = [(k, r.get("name"), r.get("type")) for k, r in (app.get("resources") or {}).items()]
+    topics, pipelines, ext_src, ext_sink = [], [], [], []
+    for mod in app.get("modules") or []:
+        topics += [(rid("topic", t.get("name")), t.get("name")) for t in mod.get("topics") or []]
+        for p in mod.get("pipelines") or []:
+            agents = []
+            for a in p.get("agents") or []:
+                aid = rid("agent", a.get("id"))
+                inp = a.get("input")
+                if inp is None:
+                    src = "external-source-" + aid
+                    ext_src.append(src)
+                    inp_id = src
+                else:
+                    inp_id = rid("topic", inp.get("definition")) if inp.get("connectionType") == "TOPIC" else None
+                outs = []
+                out = a.get("output")
+                if out is None:
+                    ext_sink.append("external-sink-" + aid)
+                    outs.append("external-sink-" + aid)
+                else:
+                    outs.append(rid("topic" if out.get("connectionType") == "TOPIC" else "agent", out.get("definition")))
+                cfg = a.get("configuration") or {}
+                if isinstance(cfg.get("datasource"), str):
+                    outs.append(rid("resource", cfg["datasource"]))
+                if isinstance(cfg.get("stream-to-topic"), str):
+                    outs.append(rid("topic", cfg["stream-to-topic"]))
+                if a.get("type") in ("ai-text-completions", "ai-chat-completions", "compute-ai-embeddings"):
+                    if "ai-service" in cfg:
+                        outs.append(rid("resource", cfg["ai-service"]))
+                    else:
+                        svc = next((r for r in resources if r[2] in _AI_CONFIGS), None)
+                        if svc is not None:
+                            outs.append(rid("resource", svc[0]))
+                agents.append((aid, a.get("name"), inp_id, outs))
+            pipelines.append((p.get("id"), agents))
+
+    m = ["flowchart LR", ""]
+    if gateways:
+        m += ["external-client((Client))", ""]
+    for e in list(dict.fromkeys(ext_sink)) + list(dict.fromkeys(ext_src)):
+        m += [f'{e}(["External system"])', ""]
+    m.append('subgraph resources["Resources"]')
+    for k, name, typ in resources:
+        m.append(rid("resource", k) + (f'[("{name}")]' if typ == "datasource" else f'("{name}")'))
+    m += ["end", "", 'subgraph streaming-cluster["Topics"]']
+    m += [f'{t}(["{label}"])' for t, label in topics]
+    m += ["end", "", 'subgraph gateways["Gateways"]']
+    m += [f'{g}[/"{label}"\\]' for g, label, _, _ in gateways]
+    m += ["end", ""]
+    for pid, agents in pipelines:
+        m.append(f'subgraph pipeline-{pid}["Pipeline: <b>{pid}</b>"]')
+        m += [f'{aid}("{label}")' for aid, label, _, _ in agents]
+        m += ["end", ""]
+    n = 0
+
+    def link(a: str, b: str, dotted: bool, style: Optional[str]) -> None:
+        nonlocal n
+        m.append(a + ("-.->" if dotted else "-->") + b)
+        if style:
+            m.append(f"linkStyle {n} {style}")
+        n += 1
+
+    for _, agents in pipelines:
+        for aid, _, inp, _ in agents:
+            if inp is not None:
+                link(aid, inp, True, "stroke:#82E0AA")
+    for g, _, prod, cons in gateways:
+        for t in cons:
+            link(g, t, True, None)
+        for t in prod:
+            link(g, t, False, None)
+    link("external-client", "gateways", False, None)
+    for _, agents in pipelines:
+        for aid, _, _, outs in agents:
+            ends = [o for o in outs if o.startswith(("topic-", "external-sink-"))]
+            for o in outs:
+                if o in ends or (not ends and o.startswith("resource-")):
+                    link(aid, o, False, "stroke:#F4D03F")
+                else:
+                    link(aid, o, o.startswith("resource-"), "stroke:#5DADE2")
+    return "\n".join(m) + "\n"
+
+
 def app_model(client, app_id: str, api_gateway_url: str, tenant: str) -> Dict[str, Any]:
     desc = client.get(app_id)
     plan = desc.get("application") or {}
     return {"remoteBaseUrl": api_gateway_url, "tenant": tenant, "applicationId": app_id,
             "gateways": plan.get("gateways") or [],
             "applicationDefinition": json.dumps(desc, default=str),
-            "mermaidDefinition": mermaid_from_plan(plan)}
+            "mermaidDefinition": mermaid_from_description(desc) if "modules" in plan else mermaid_from_plan(plan)}
 
 
 def make_app(client, app_id: str, api_gateway_url: str, tenant: str):

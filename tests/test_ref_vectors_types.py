@@ -1417,3 +1417,80 @@ def test_transform_drop_on_predicate(at, dropped):
     steps.insert(at, _DROP_WHEN)
     r = _run_chain(steps, "test-key", {"firstName": "Jane", "lastName": "Doe", "age": 42})
     assert (r is None) if dropped else (r.value() == {"age": 42})
+
+
+# ---------------------------------------------------------------------------------------
+# MermaidAppDiagramGeneratorTest (langstream-cli/src/test/.../MermaidAppDiagramGeneratorTest.java:27-105;
+# fixture src/test/resources/expected-get.json copied to tests/fixtures/)
+# ---------------------------------------------------------------------------------------
+
+def test_mermaid_from_description():
+    import json as _json
+    import os
+    from langstream_amd.cli.app_ui import mermaid_from_description
+    with open(os.path.join(os.path.dirname(__file__), "fixtures", "expected-get.json")) as f:
+        desc = _json.load(f)
+    assert mermaid_from_description(desc) == (
+        'flowchart LR\n'
+        '\n'
+        'external-client((Client))\n'
+        '\n'
+        'external-sink-agent-write-to-astra-sink-1(["External system"])\n'
+        '\n'
+        'external-source-agent-extract-text-s3-source-1(["External system"])\n'
+        '\n'
+        'subgraph resources["Resources"]\n'
+        'resource-openai___azure___configuration("OpenAI Azure configuration")\n'
+        'end\n'
+        '\n'
+        'subgraph streaming-cluster["Topics"]\n'
+        'topic-chunks-topic(["chunks-topic"])\n'
+        'end\n'
+        '\n'
+        'subgraph gateways["Gateways"]\n'
+        'gateway-consume-chunks[/"consume-chunks"\\]\n'
+        'end\n'
+        '\n'
+        'subgraph pipeline-extract-text["Pipeline: <b>extract-text</b>"]\n'
+        'agent-extract-text-s3-source-1("Read from S3")\n'
+        'agent-extract-text-text-extractor-2("Extract text")\n'
+        'agent-extract-text-text-normaliser-3("Normalise text")\n'
+        'agent-extract-text-language-detector-4("Detect language")\n'
+        'agent-extract-text-text-splitter-5("Split into chunks")\n'
+        'agent-extract-text-document-to-json-6("Convert to structured data")\n'
+        'agent-extract-text-compute-7("prepare-structure")\n'
+        'agent-step1("compute-embeddings")\n'
+        'end\n'
+        '\n'
+        'subgraph pipeline-write-to-astra["Pipeline: <b>write-to-astra</b>"]\n'
+        'agent-write-to-astra-sink-1("Write to AstraDB")\n'
+        'end\n'
+        '\n'
+        'agent-extract-text-s3-source-1-.->external-source-agent-extract-text-s3-source-1\n'
+        'linkStyle 0 stroke:#82E0AA\n'
+        'agent-write-to-astra-sink-1-.->topic-chunks-topic\n'
+        'linkStyle 1 stroke:#82E0AA\n'
+        'gateway-consume-chunks-.->topic-chunks-topic\n'
+        'external-client-->gateways\n'
+        'agent-extract-text-s3-source-1-->agent-extract-text-text-extractor-2\n'
+        'linkStyle 4 stroke:#5DADE2\n'
+        'agent-extract-text-text-extractor-2-->agent-extract-text-text-normaliser-3\n'
+        'linkStyle 5 stroke:#5DADE2\n'
+        'agent-extract-text-text-normaliser-3-->agent-extract-text-language-detector-4\n'
+        'linkStyle 6 stroke:#5DADE2\n'
+        'agent-extract-text-language-detector-4-->agent-extract-text-text-splitter-5\n'
+        'linkStyle 7 stroke:#5DADE2\n'
+        'agent-extract-text-text-splitter-5-->agent-extract-text-document-to-json-6\n'
+        'linkStyle 8 stroke:#5DADE2\n'
+        'agent-extract-text-document-to-json-6-->agent-extract-text-compute-7\n'
+        'linkStyle 9 stroke:#5DADE2\n'
+        'agent-extract-text-compute-7-->agent-step1\n'
+        'linkStyle 10 stroke:#5DADE2\n'
+        'agent-step1-->topic-chunks-topic\n'
+        'linkStyle 11 stroke:#F4D03F\n'
+        'agent-step1-.->resource-openai___azure___configuration\n'
+        'linkStyle 12 stroke:#5DADE2\n'
+        'agent-write-to-astra-sink-1-->external-sink-agent-write-to-astra-sink-1\n'
+        'linkStyle 13 stroke:#F4D03F\n')
+    assert mermaid_from_description({"application": {}}) is not None
+    assert mermaid_from_description({"application": {"gateways": {}}}) is not None
