@@ -215,7 +215,12 @@ def cmd_apps(args) -> int:
     elif args.cmd == "update":
         _print(cl.update(args.name, args.app, args.instance, args.secrets), args.output)
     elif args.cmd == "get":
-        _print(cl.get(args.name, stats=True), args.output)
+        desc = cl.get(args.name, stats=True)
+        if args.output == "mermaid":   # AbstractGetApplicationCmd: -o mermaid
+            from .app_ui import mermaid_from_description
+            print(mermaid_from_description(desc), end="")
+        else:
+            _print(desc, args.output)
     elif args.cmd == "list":
         _print(cl.list(), args.output)
     elif args.cmd == "delete":
@@ -535,7 +540,7 @@ def build_parser() -> argparse.ArgumentParser:
     for c in ("get",):
         x = asub.add_parser(c)
         x.add_argument("name")
-        x.add_argument("-o", "--output", default="json", choices=["json", "yaml"])
+        x.add_argument("-o", "--output", default="json", choices=["json", "yaml", "mermaid"])
     x = asub.add_parser("list")
     x.add_argument("-o", "--output", default="json", choices=["json", "yaml"])
     x = asub.add_parser("delete")

@@ -1494,3 +1494,17 @@ def test_mermaid_from_description():
         'linkStyle 13 stroke:#F4D03F\n')
     assert mermaid_from_description({"application": {}}) is not None
     assert mermaid_from_description({"application": {"gateways": {}}}) is not None
+
+
+def test_apps_get_mermaid_output(capsys, monkeypatch):
+    """``apps get <id> -o mermaid`` prints the description's diagram (AbstractGetApplicationCmd)."""
+    import json as _json
+    import os
+    from types import SimpleNamespace
+    from langstream_amd.cli import main as cli
+    from langstream_amd.cli.app_ui import mermaid_from_description
+    with open(os.path.join(os.path.dirname(__file__), "fixtures", "expected-get.json")) as f:
+        desc = _json.load(f)
+    monkeypatch.setattr(cli, "_client", lambda args: SimpleNamespace(get=lambda name, stats=True: desc))
+    assert cli.cmd_apps(SimpleNamespace(cmd="get", name="app", output="mermaid")) in (0, None)
+    assert capsys.readouterr().out == mermaid_from_description(desc)
