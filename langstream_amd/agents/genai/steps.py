@@ -65,7 +65,20 @@ class Step:
 
 
 # ---------------------------------------------------------------- host transforms
+def _check_part(cfg) -> None:
+    """``part``: absent / null, ``key`` or ``value`` (TransformFunctionUtil's step configs)."""
+    if cfg.get("part") not in (None, "key", "value"):
+        raise ValueError(f"Invalid part {cfg.get('part')!r}: expected key or value")
+
+
 class DropFieldsStep(Step):
+    def __init__(self, cfg):
+        super().__init__(cfg)
+        fields = cfg.get("fields")
+        if not isinstance(fields, list) or not fields or not all(isinstance(f, str) and f for f in fields):
+            raise ValueError("drop-fields needs a non-empty list of non-empty field names")
+        _check_part(cfg)
+
     def process(self, rec):
         fields = self.cfg.get("fields") or []
         part = self.cfg.get("part")
@@ -129,6 +142,13 @@ def _cast_value(v, st: str):
 
 
 class CastStep(Step):
+    def __init__(self, cfg):
+        super().__init__(cfg)
+        st = cfg.get("schema-type", "string")
+        if not isinstance(st, str) or st.strip().lower().replace("-", "_") not in _CAST_TYPES:
+            raise ValueError(f"Unsupported schema-type {st!r}")
+        _check_part(cfg)
+
     def process(self, rec):
         st = str(self.cfg.get("schema-type", "string")).strip().lower().replace("-", "_")
         if st not in _CAST_TYPES:
@@ -158,6 +178,11 @@ class FlattenStep(Step):
     """FlattenStep.java: nested struct fields become top-level ``a<delim>b`` fields.  The
     reference flattens Avro records only; maps (JSON values) are flattened here too.  A
     value with no struct to flatten fails as there (``Unsupported schema type``)."""
+
+    def __init__(self, cfg):
+        super().__init__(cfg)
+        if cfg.get("part") not in (None, "key", "value"):
+            raise ValueError(f"Unsupported part for Flatten: {cfg.get('part')}")
 
     def process(self, rec):
         delim = self.cfg.get("delimiter", "_")
@@ -224,14 +249,26 @@ class ComputeStep(Step):
     def __init__(self, cfg):
         super().__init__(cfg)
         self.fields = []
-        for f in cfg.get("fields") or []:
+        if not cfg.get("fields"):
+            raise ValueError("compute needs at least one field")
+        seen = set()
+        for f in cfg.get("fields"):
             name = f.get("name")
             if not name:
                 raise ValueError("compute field name is required")
+            if not (name in ("value", "key", "destinationTopic", "messageKey", "topicName")
+                    or name.startswith(("value.", "key.", "properties."))):
+                raise ValueError(f"Invalid compute field name {name}")
+            if name in seen:
+                raise ValueError(f"Duplicate compute field name {name}")
+            seen.add(name)
             t = str(f.get("type") or "").upper() or None
             if t and t not in _COMPUTE_TYPES:
                 raise ValueError(f"Unsupported compute type {t}")
-            self.fields.append((name, f.get("expression"), t, bool(f.get("optional", True))))
+            opt = f.get("optional", True)
+            if not isinstance(opt, bool):
+                raise ValueError(f"optional must be a boolean, got {opt!r}")
+            self.fields.append((name, f.get("expression"), t, opt))
 
     def process(self, rec):
         ctx = rec.el_context()

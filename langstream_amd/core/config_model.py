@@ -125,7 +125,8 @@ AGENT_MODELS: Dict[str, Model] = {
         "fields": L("Fields to drop.", True, S()), "part": S("key or value (default: both)."), **_COMPOSABLE}),
     "merge-key-value": Model("Merge key-value format", "Merges the key fields into the value.", {**_COMPOSABLE}),
     "unwrap-key-value": Model("Unwrap key-value format", "Replaces the record by its key or its value.", {
-        "unwrapKey": B("Unwrap the key instead of the value.", default=False), **_COMPOSABLE}),
+        "unwrapKey": B("Unwrap the key instead of the value.", default=False),
+        "unwrap-key": B("Alias of unwrapKey (the transform-function spelling)."), **_COMPOSABLE}),
     "cast": Model("Cast record to another schema", "Converts key/value to another schema type.", {
         "schema-type": S("Target schema type (STRING, BYTES, INT32, ...).", True), "part": S("key or value."),
         **_COMPOSABLE}),
