@@ -16,9 +16,12 @@ MI355X-native services:
     (the reference example ``EX/docker-chatbot/chatbot.yaml:36`` runs that query on HerdDB);
   - ``jdbc:herddb:local`` (HerdDB's embedded, in-process mode) -> an in-process SQLite
     database shared by the process's agents;
-  - any other URL (``jdbc:herddb:server:...``, ``jdbc:mysql:...``) fails at init: no
-    driver for it ships in this build, and a silent stand-in would not share data
-    between pods.
+  - ``jdbc:herddb:server:<host>:<port>`` -> the local database service that ``langstream
+    run --start-database`` starts (the HerdDB of the reference's docker image; herddb.py):
+    in its own process straight on its SQLite database (GPU kNN mirror included), from
+    other processes over its PostgreSQL-protocol endpoint;
+  - any other URL (``jdbc:mysql:...``) fails at init: no driver for it ships in this
+    build, and a silent stand-in would not share data between pods.
 * cassandra / astra / astra-vector-db / milvus / opensearch / pinecone / solr: the REST /
   CQL clients of ``remote.py`` / ``cql.py``.
 """
@@ -209,12 +212,16 @@ _dbs_lock = threading.Lock()
 class SqliteDataSource(DataSource):
     """JDBC-compatible SQL on SQLite with GPU kNN for cosine-similarity ORDER BY."""
 
-    def __init__(self, cfg: Dict[str, Any]):
+    def __init__(self, cfg: Dict[str, Any], uri: Optional[str] = None, lock: Optional[Any] = None):
+        """``uri`` / ``lock``: open that SQLite URI and serialise on that lock (a database
+        this process also serves to other processes: herddb.py)."""
         url = str(cfg.get("url") or cfg.get("path") or "memory")
         m = re.match(r"^jdbc:sqlite:(.+)$", url)
         self.path = m.group(1) if m else (url if cfg.get("path") else None)
         self.name = url
-        if self.path is None or self.path == ":memory:":
+        if uri is not None:
+            self.conn = sqlite3.connect(uri, uri=True, check_same_thread=False)
+        elif self.path is None or self.path == ":memory:":
             # an in-process database shared by this process's agents (jdbc:herddb:local,
             # jdbc:sqlite::memory:, service sqlite without a path)
             self.conn = sqlite3.connect(f"file:{re.sub(r'[^A-Za-z0-9]', '_', url)}?mode=memory&cache=shared",
@@ -223,7 +230,7 @@ class SqliteDataSource(DataSource):
             self.conn = sqlite3.connect(self.path, check_same_thread=False)
         self.conn.create_function("cosine_similarity", 2, _cosine, deterministic=True)
         self.conn.row_factory = sqlite3.Row
-        self.lock = threading.RLock()
+        self.lock = lock if lock is not None else threading.RLock()
         self.vector_cols: Dict[tuple, str] = {}  # (table, column) -> store name
 
     @staticmethod
@@ -359,6 +366,9 @@ def jdbc_datasource(cfg: Dict[str, Any]):
     if svc == "sqlite" or url.startswith("jdbc:sqlite:") or url.startswith("jdbc:herddb:local") or \
             (not url and cfg.get("path")):
         return SqliteDataSource.shared(cfg)
+    if url.startswith("jdbc:herddb:server:"):
+        from .herddb import herddb_datasource
+        return herddb_datasource(cfg)
     if url.startswith("jdbc:postgresql:"):
         from .pgwire import PostgresDataSource
         key = (url, str(cfg.get("user")), str(cfg.get("password")))
@@ -368,8 +378,9 @@ def jdbc_datasource(cfg: Dict[str, Any]):
                 ds = _pg[key] = PostgresDataSource(cfg)
             return ds
     raise ValueError(f"JDBC URL {url or '(none)'!r} is not supported by this build: it speaks "
-                     f"jdbc:postgresql:// (wire protocol), jdbc:sqlite:<path> and jdbc:herddb:local "
-                     f"(in-process); set one of those")
+                     f"jdbc:postgresql:// (wire protocol), jdbc:sqlite:<path>, jdbc:herddb:local "
+                     f"(in-process) and jdbc:herddb:server: (the local database service, herddb.py); "
+                     f"set one of those")
 
 
 def reset_jdbc_datasources() -> None:

@@ -23,7 +23,7 @@ import socket
 import sqlite3
 import struct
 import threading
-from typing import Any, Dict, List, Optional, Tuple
+from typing import Any, Callable, Dict, List, Optional, Tuple
 
 _TS = re.compile(r"^\d{4}-\d{2}-\d{2}[T ]\d{2}:\d{2}(:\d{2}(\.\d+)?)?(Z|[+-]\d{2}(:?\d{2})?)?$")
 
@@ -81,6 +81,8 @@ def _text(v: Any) -> Optional[bytes]:
 
 def _decl_oid(decl: str) -> int:
     d = decl.upper()
+    if d.startswith("FLOATA") or "ARRAY" in d or d.endswith("[]"):   # HerdDB FLOATA / arrays: JSON text
+        return 114
     if "INT" in d:
         return 20
     if any(x in d for x in ("REAL", "FLOA", "DOUB", "NUMERIC", "DECIMAL")):
@@ -118,12 +120,23 @@ class PgStandalone:
     """``auth``: 'trust' | 'password' | 'md5' | 'scram-sha-256'."""
 
     def __init__(self, host: str = "127.0.0.1", port: int = 0, users: Optional[Dict[str, str]] = None,
-                 auth: str = "scram-sha-256", db_path: Optional[str] = None):
+                 auth: str = "scram-sha-256", db_path: Optional[str] = None, db_uri: Optional[str] = None,
+                 functions: Optional[Dict[str, Tuple[int, Callable[..., Any]]]] = None,
+                 rewrite: Optional[Callable[[str], str]] = None, on_write: Optional[Callable[[str], None]] = None,
+                 db_lock: Optional[Any] = None, server_version: str = "16.0 (langstream pg-standalone)"):
+        """``db_uri`` / ``db_lock``: serve a SQLite database (and its writer lock) that this
+        process shares with in-process users; ``functions``: SQL UDFs per session;
+        ``rewrite``: a dialect rewrite applied before the PostgreSQL -> SQLite one;
+        ``on_write``: called with every statement that is not a SELECT."""
         self.users = dict(users or {"postgres": "password"})
         self.auth = auth
-        self.db_path = f"file:{db_path}" if db_path else f"file:pgstandalone{id(self)}?mode=memory&cache=shared"
+        self.db_path = db_uri or (f"file:{db_path}" if db_path else f"file:pgstandalone{id(self)}?mode=memory&cache=shared")
         self._keep = sqlite3.connect(self.db_path, uri=True, check_same_thread=False)   # keeps a memory db alive
-        self.db_lock = threading.Lock()
+        self.db_lock = db_lock if db_lock is not None else threading.Lock()
+        self.functions = dict(functions or {})
+        self.rewrite = rewrite
+        self.on_write = on_write
+        self.server_version = server_version
         self.sock = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
         self.sock.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
         self.sock.bind((host, port))
@@ -178,6 +191,8 @@ class _Session:
         self.db = sqlite3.connect(srv.db_path, uri=True, check_same_thread=False, isolation_level=None)
         self.db.create_function("pg_now", 0, _pg_now)
         self.db.create_function("current_timestamp_pg", 0, _pg_now)
+        for fname, (nargs, fn) in srv.functions.items():
+            self.db.create_function(fname, nargs, fn, deterministic=True)
         self.stmts: Dict[str, Tuple[str, int]] = {}
         self.portals: Dict[str, Tuple[str, List[Optional[str]]]] = {}
         self.skip_to_sync = False
@@ -222,7 +237,7 @@ class _Session:
         if not self._auth(user):
             return
         self._send(b"R", struct.pack("!i", 0))
-        for k, v in (("server_version", "16.0 (langstream pg-standalone)"), ("client_encoding", "UTF8"),
+        for k, v in (("server_version", self.srv.server_version), ("client_encoding", "UTF8"),
                      ("DateStyle", "ISO, MDY"), ("integer_datetimes", "on"), ("standard_conforming_strings", "on")):
             self._send(b"S", k.encode() + b"\0" + v.encode() + b"\0")
         self._send(b"K", struct.pack("!ii", os.getpid(), 1))
@@ -317,12 +332,18 @@ class _Session:
     def _nparams(self, sql: str) -> int:
         return max([int(x) for x in re.findall(r"\$(\d+)", sql)] or [0])
 
+    def _sql(self, sql: str) -> str:
+        return _to_sqlite(self.srv.rewrite(sql) if self.srv.rewrite else sql)
+
     def _run(self, sql: str, params: List[Optional[str]]):
         with self.srv.db_lock:
-            cur = self.db.execute(_to_sqlite(sql), [_norm_param(p) for p in params])
+            cur = self.db.execute(self._sql(sql), [_norm_param(p) for p in params])
             rows = cur.fetchall() if cur.description else []
             cols = [d[0] for d in cur.description] if cur.description else None
-            return cols, rows, cur.rowcount
+            rc = cur.rowcount
+        if self.srv.on_write is not None and cols is None:
+            self.srv.on_write(sql)
+        return cols, rows, rc
 
     def _declared_types(self) -> Dict[str, int]:
         """column name -> type OID from the tables' declared types (the stand-in's answer
@@ -370,7 +391,7 @@ class _Session:
             # validate now, like the server's parse step
             with self.srv.db_lock:
                 try:
-                    self.db.execute("EXPLAIN " + _to_sqlite(sql_s), [None] * self._nparams(sql_s))
+                    self.db.execute("EXPLAIN " + self._sql(sql_s), [None] * self._nparams(sql_s))
                 except sqlite3.Error as e:
                     raise sqlite3.OperationalError(str(e)) from e
             self.stmts[name.decode()] = (sql_s, self._nparams(sql_s))
@@ -435,7 +456,7 @@ class _Session:
         with self.srv.db_lock:
             self.db.execute("SAVEPOINT pgdescribe")
             try:
-                cur = self.db.execute(_to_sqlite(sql), [None] * n)
+                cur = self.db.execute(self._sql(sql), [None] * n)
                 cols = [d[0] for d in cur.description] if cur.description else None
                 rows = cur.fetchmany(16) if cols else []
             except sqlite3.Error:

@@ -11,9 +11,11 @@ Groups:
 * ``gateway``   produce | consume | chat  (WebSocket client; chat re-assembles streamed
   answers from ``stream-id`` / ``stream-index`` / ``stream-last-message`` headers,
   ``ChatGatewayCmd.java:45-120``)
-* ``run``       the ``docker run`` equivalent (``LocalRunApplicationCmd.java``): control
-  plane (8090), gateway (8091) and agent control API (8790) in-process, the app
-  deployed on memory topics and the local GPU services
+* ``run`` / ``docker run``  the ``docker run`` equivalent (``LocalRunApplicationCmd.java``):
+  the bundled broker / S3 / database services (``--start-broker/-s3/-database``), control
+  plane (8090), gateway (8091), agent control API (8790) and the UI (``-up`` 8092)
+  in-process, ``--only-agent``, ``--watch-files`` hot reload, and the local GPU services
+* app / instance / secrets paths may be ``file://``, ``https://`` or GitHub URLs (sources.py)
 * ``archetypes`` list | get | deploy
 * ``python``    load-pip-requirements | run-tests
 * ``code-download`` (k8s init container: fetch + unzip the app code archive)
@@ -210,6 +212,9 @@ def cmd_apps(args) -> int:
         return serve_forever(_client(args), args.name, p["apiGatewayUrl"], p["tenant"], args.port,
                              open_browser=not args.no_browser)
     cl = _client(args)
+    if args.cmd in ("deploy", "update"):
+        # https:// / GitHub / file:// sources (BaseCmd.checkFileExistsOrDownload)
+        args.app, args.instance, args.secrets = _resolve_sources(args)
     if args.cmd == "deploy":
         _print(cl.deploy(args.name, args.app, args.instance, args.secrets, args.dry_run), args.output)
     elif args.cmd == "update":
@@ -315,50 +320,136 @@ def cmd_gateway(args) -> int:
 
 
 # ---------------------------------------------------------------- local run (docker run)
+LOCAL_RUN_PROFILE = "local-docker-run"
+
+
+def _resolve_sources(args):
+    """app / instance / secrets through ``BaseCmd.checkFileExistsOrDownload`` (sources.py)."""
+    from .sources import as_app_directory, check_file_exists_or_download
+    cache = not getattr(args, "disable_local_repositories_cache", False)
+    app = check_file_exists_or_download(getattr(args, "app", None), cache)
+    inst = check_file_exists_or_download(getattr(args, "instance", None), cache)
+    sec = check_file_exists_or_download(getattr(args, "secrets", None), cache)
+    return (as_app_directory(app) if app else None), inst, sec
+
+
 def cmd_run(args) -> int:
+    """``langstream docker run`` (``LocalRunApplicationCmd.java:165-440``) without the
+    container: the bundled services (broker / S3 / database, runtime/local_services.py),
+    the control plane (8090), the gateway (8091), the agent-control API (8790) and the
+    application's agents all run in this process; ``--watch-files`` hot-reloads python/,
+    ``--start-ui`` serves the application UI on ``-up`` (8092)."""
     import logging
     logging.basicConfig(level=logging.INFO, format="%(asctime)s %(levelname)s %(threadName)s %(message)s")
     from ..core.store import InMemoryApplicationStore
     from ..gateway.server import GatewayServer, GatewayService
+    from ..runtime.local_services import ApplicationWatcher, LocalServices, restart_agents
     from ..runtime.pod import AgentAPIServer
     from ..webservice.server import ControlPlane, WebServiceServer
-    from .client import zip_directory
-    store = InMemoryApplicationStore()
-    cp = ControlPlane(store)
-    store.put_tenant(args.tenant)
     from ..core.file_refs import read_yaml_with_references
-    instance = read_yaml_with_references(args.instance) if args.instance else None
-    secrets = read_yaml_with_references(args.secrets) if args.secrets else None
-    res = cp.deploy(args.tenant, args.name, zip_directory(args.app), instance, secrets, dry_run=args.dry_run)
-    if args.dry_run:
-        _print(res, "yaml")
-        return 0
-    ws = WebServiceServer(cp, host=args.host, port=args.web_port).start()
-    gw = GatewayServer(GatewayService(store), host=args.host, port=args.gateway_port).start()
-    sa = store.get(args.tenant, args.name)
-    api = AgentAPIServer(sa.runner.runners if sa.runner else [], host=args.host, port=args.agents_port).start()
-    print(f"application {args.name} running: webservice {ws.url}  gateway {gw.url.replace('http', 'ws')}  "
-          f"agents http://{args.host}:{api.port}", flush=True)
+    from .client import zip_directory
+    dry = args.dry_run
+    app_dir, inst_path, sec_path = _resolve_sources(args)
+    tenant = args.tenant or "default"
+    print(f"Tenant: {tenant}\nApplication: {args.name}\nApplication directory: {os.path.abspath(app_dir)}", flush=True)
+    print(f"Filter agent: {args.only_agent}" if args.only_agent else "Running all the agents in the application",
+          flush=True)
+    for flag in ("memory", "cpus", "docker_command", "langstream_runtime_version", "langstream_runtime_docker_image"):
+        if getattr(args, flag, None):
+            print(f"--{flag.replace('_', '-')} ignored: the application runs in this process, not in a container",
+                  flush=True)
+    services = LocalServices(broker=args.start_broker and not dry, s3=args.start_s3 and not dry,
+                             database=args.start_database and not dry, host=args.host,
+                             # LANGSTREAM_LOCAL_SERVICES_PORTS=random: free ports + aliases (tests)
+                             well_known_ports=os.environ.get("LANGSTREAM_LOCAL_SERVICES_PORTS") != "random").start()
+    print(f"Start broker: {services.broker is not None}" +
+          (f" (kafka bootstrap {services.broker.bootstrap})" if services.broker else ""), flush=True)
+    print(f"Start S3: {services.s3 is not None}" + (f" ({services.s3.endpoint})" if services.s3 else ""), flush=True)
+    print(f"Start Database: {services.database is not None}" +
+          (f" ({services.database.url})" if services.database else ""), flush=True)
     stop = threading.Event()
+    started: list = []
     try:
-        import signal
-        signal.signal(signal.SIGTERM, lambda *_: stop.set())
-    except ValueError:
-        pass
-    try:
-        while not stop.is_set():
-            stop.wait(1.0)
-            if sa.runner is not None and sa.runner.errors:
-                print(f"agent failure: {sa.runner.errors[0]!r}", file=sys.stderr)
-                return 1
-    except KeyboardInterrupt:
-        pass
+        if inst_path:
+            instance = read_yaml_with_references(inst_path)
+        else:
+            instance = services.default_instance()
+            print("Using default instance file that connects to the Kafka broker started here" if services.broker
+                  else "The broker is disabled: using the in-process memory streaming cluster", flush=True)
+        secrets = read_yaml_with_references(sec_path) if sec_path else None
+        store = InMemoryApplicationStore()
+        cp = ControlPlane(store)
+        cp.only_agents = [args.only_agent] if args.only_agent else None
+        cp.local_runs = True
+        store.put_tenant(tenant)
+        res = cp.deploy(tenant, args.name, zip_directory(app_dir), instance, secrets, dry_run=dry)
+        if dry:
+            _print(res, "yaml")
+            return 0
+        sa = store.get(tenant, args.name)
+        if sa.status != "DEPLOYED":
+            print(f"application {args.name} failed to start: {sa.error}", file=sys.stderr, flush=True)
+            return 1
+        ws = gw = None
+        if args.start_webservices:
+            ws = WebServiceServer(cp, host=args.host, port=args.web_port).start()
+            gw = GatewayServer(GatewayService(store), host=args.host, port=args.gateway_port).start()
+            started += [gw, ws]
+            _update_local_run_profile(tenant, ws.url, gw.url.replace("http", "ws"))
+        api = AgentAPIServer(sa.runner.runners if sa.runner else [], host=args.host, port=args.agents_port).start()
+        started.insert(0, api)
+        agents_url = f"http://{args.host}:{api.port}"
+        print(f"application {args.name} running: webservice {ws.url if ws else '-'}  "
+              f"gateway {gw.url.replace('http', 'ws') if gw else '-'}  agents {agents_url}", flush=True)
+        if args.watch_files:
+            if os.path.isdir(os.path.join(app_dir, "python")):
+                code = cp.local_code(sa) if sa.code_archive_id else None
+                started.insert(0, ApplicationWatcher(app_dir, code, lambda _c: restart_agents(agents_url)).start())
+            else:
+                print(f"Python directory {os.path.join(app_dir, 'python')} not found, not watching files", flush=True)
+        if args.start_ui and ws is not None:
+            from .app_ui import AppUIServer
+            from .client import AdminClient
+            ui = AppUIServer(AdminClient(ws.url, tenant), args.name, gw.url.replace("http", "ws"), tenant,
+                             host=args.host, port=args.ui_port).start()
+            started.insert(0, ui)
+            print(f"Started UI at {ui.url}", flush=True)
+        try:
+            import signal
+            signal.signal(signal.SIGTERM, lambda *_: stop.set())
+        except ValueError:
+            pass
+        try:
+            while not stop.is_set():
+                stop.wait(1.0)
+                if sa.runner is not None and sa.runner.errors:
+                    print(f"agent failure: {sa.runner.errors[0]!r}", file=sys.stderr)
+                    return 1
+        except KeyboardInterrupt:
+            pass
+        finally:
+            for srv in started:
+                try:
+                    srv.stop()
+                except Exception:  # noqa: BLE001
+                    pass
+            cp.delete(tenant, args.name, force=True)
+        return 0
     finally:
-        api.stop()
-        gw.stop()
-        ws.stop()
-        cp.delete(args.tenant, args.name, force=True)
-    return 0
+        services.stop()
+
+
+def _update_local_run_profile(tenant: str, web: str, gateway: str) -> None:
+    """``LocalRunApplicationCmd.updateLocalDockerRunProfile``: a ``local-docker-run``
+    profile pointing at this run."""
+    try:
+        c = load_config()
+        c["profiles"][LOCAL_RUN_PROFILE] = {"webServiceUrl": web, "apiGatewayUrl": gateway, "tenant": tenant,
+                                            "token": None}
+        save_config(c)
+        print(f"profile {LOCAL_RUN_PROFILE} updated", flush=True)
+    except OSError as e:
+        print(f"could not update the {LOCAL_RUN_PROFILE} profile: {e}", flush=True)
 
 
 def cmd_archetypes(args) -> int:
@@ -487,6 +578,8 @@ def build_parser() -> argparse.ArgumentParser:
     ap = argparse.ArgumentParser(prog="langstream", description="LangStream (MI355X-native) command line")
     ap.add_argument("--profile")
     ap.add_argument("--tenant")
+    ap.add_argument("--disable-local-repositories-cache", action="store_true",
+                    help="clone GitHub application sources afresh instead of updating the local cache")
     sub = ap.add_subparsers(dest="group", required=True)
 
     p = sub.add_parser("profiles")
@@ -582,17 +675,36 @@ def build_parser() -> argparse.ArgumentParser:
             x.add_argument("--position")
     g.set_defaults(fn=cmd_gateway)
 
-    r = sub.add_parser("run", help="run an application locally (the `docker run` equivalent)")
-    r.add_argument("name")
-    r.add_argument("-app", "--app", required=True)
-    r.add_argument("-i", "--instance")
-    r.add_argument("-s", "--secrets")
-    r.add_argument("--dry-run", action="store_true")
-    r.add_argument("--host", default="127.0.0.1")
-    r.add_argument("--web-port", type=int, default=8090)
-    r.add_argument("--gateway-port", type=int, default=8091)
-    r.add_argument("--agents-port", type=int, default=8790)
-    r.set_defaults(fn=cmd_run, tenant="default")
+    def run_args(r):
+        b = argparse.BooleanOptionalAction
+        r.add_argument("name")
+        r.add_argument("-app", "--app", "--application", dest="app", required=True,
+                       help="application directory, zip, file:// path, https:// URL or GitHub URL")
+        r.add_argument("-i", "--instance")
+        r.add_argument("-s", "--secrets")
+        r.add_argument("--dry-run", action="store_true")
+        r.add_argument("--start-broker", action=b, default=True, help="start the Kafka-protocol broker (9092)")
+        r.add_argument("--start-s3", action=b, default=True, help="start the S3 service (9000)")
+        r.add_argument("--start-database", action=b, default=True, help="start the database service (7000)")
+        r.add_argument("--start-webservices", action=b, default=True, help="start the control plane and gateway")
+        r.add_argument("--start-ui", action=b, default=True, help="start the application UI")
+        r.add_argument("--watch-files", action=b, default=True, help="hot-reload python/ changes")
+        r.add_argument("-up", "--ui-port", type=int, default=8092, help="UI port (0: a random port)")
+        r.add_argument("--only-agent", help="run only this agent")
+        r.add_argument("--host", default="127.0.0.1")
+        r.add_argument("--web-port", type=int, default=8090)
+        r.add_argument("--gateway-port", type=int, default=8091)
+        r.add_argument("--agents-port", type=int, default=8790)
+        for opt in ("--memory", "--cpus", "--docker-command", "--langstream-runtime-version",
+                    "--langstream-runtime-docker-image"):
+            r.add_argument(opt, help="accepted for compatibility (no container)")
+        r.add_argument("--docker-args", action="append", help="accepted for compatibility (no container)")
+        r.set_defaults(fn=cmd_run)
+
+    run_args(sub.add_parser("run", help="run an application locally (the `docker run` equivalent)"))
+    dk = sub.add_parser("docker", help="local runs (`langstream docker run`)")
+    dks = dk.add_subparsers(dest="cmd", required=True)
+    run_args(dks.add_parser("run", help="run an application locally with the bundled services"))
 
     ar = sub.add_parser("archetypes")
     ars = ar.add_subparsers(dest="cmd", required=True)
@@ -627,6 +739,13 @@ def build_parser() -> argparse.ArgumentParser:
     pv.add_argument("--host", default="127.0.0.1")
     pv.add_argument("--port", type=int, default=9090)
     pv.set_defaults(fn=cmd_pravega_standalone)
+
+    s3 = sub.add_parser("s3-standalone", help="run the S3-protocol object store (the docker image's MinIO)")
+    s3.add_argument("--host", default="127.0.0.1")
+    s3.add_argument("--port", type=int, default=9000)
+    s3.add_argument("--data-dir", default=None)
+    s3.set_defaults(fn=lambda a: __import__("langstream_amd.agents.s3_standalone", fromlist=["main"]).main(
+        ["--host", a.host, "--port", str(a.port)] + (["--data-dir", a.data_dir] if a.data_dir else [])))
 
     pg = sub.add_parser("pg-standalone",
                         help="run the in-tree PostgreSQL wire-protocol stand-in (SQL on SQLite) for jdbc:postgresql://")
@@ -754,8 +873,18 @@ def cmd_docs(args) -> int:
     return 0
 
 
+def _picocli_booleans(argv: List[str]) -> List[str]:
+    """picocli's ``--start-broker=false`` form of the boolean options -> ``--no-start-broker``."""
+    import re
+    out = []
+    for a in argv:
+        m = re.match(r"^--((?:start-[\w-]+)|watch-files)=(true|false)$", a, re.I)
+        out.append(a if not m else (f"--{m.group(1)}" if m.group(2).lower() == "true" else f"--no-{m.group(1)}"))
+    return out
+
+
 def main(argv: Optional[List[str]] = None) -> int:
-    args = build_parser().parse_args(argv)
+    args = build_parser().parse_args(_picocli_booleans(list(sys.argv[1:] if argv is None else argv)))
     try:
         return args.fn(args) or 0
     except Exception as e:  # noqa: BLE001

@@ -631,15 +631,24 @@ class GatewayServer:
             self._runner = web.AppRunner(self.make_app())
             self._loop.run_until_complete(self._runner.setup())
             site = web.TCPSite(self._runner, self.host, self.port)
-            self._loop.run_until_complete(site.start())
+            try:
+                self._loop.run_until_complete(site.start())
+            except OSError as e:      # e.g. the port is taken: start() raises it
+                self._start_error = e
+                self._started.set()
+                return
             if self.port == 0:
                 self.port = site._server.sockets[0].getsockname()[1]
             self._started.set()
             self._loop.run_forever()
 
         self._thread = threading.Thread(target=run, daemon=True, name="api-gateway")
+        self._start_error = None
         self._thread.start()
         self._started.wait(30)
+        if self._start_error is not None:
+            self._loop = None
+            raise self._start_error
         return self
 
     def stop(self) -> None:

@@ -88,7 +88,10 @@ class ServiceRegistry:
     def default(cls) -> "ServiceRegistry":
         with cls._dlock:
             if cls._default is None:
-                cls._default = ServiceRegistry()
+                # LANGSTREAM_SERVICES_CONFIG: JSON overrides of the local-gpu configuration
+                # (e.g. {"local-ai": true, "force-chat-model": "llama-tiny", "device": "cpu"})
+                import json
+                cls._default = ServiceRegistry(json.loads(os.environ.get("LANGSTREAM_SERVICES_CONFIG") or "{}"))
             return cls._default
 
     @classmethod

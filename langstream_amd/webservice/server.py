@@ -111,6 +111,11 @@ class ControlPlane:
         self.max_units = max_units_per_tenant
         self._logs: Dict[tuple, _AppLogBuffer] = {}
         self.archetypes_dir: Optional[str] = None
+        self.only_agents: Optional[List[str]] = None   # `run --only-agent`: local runners start only these
+        # `run`: agents always run here, whatever the instance's compute cluster (the
+        # runtime-tester deploys through the k8s path into a mock API server, then runs
+        # every agent pod as a thread: TESTER/LocalApplicationRunner.java:214-272)
+        self.local_runs = False
 
     # ---------------------------------------------------------------- helpers
     @staticmethod
@@ -212,7 +217,7 @@ class ControlPlane:
     def _start(self, sa: StoredApplication, plan) -> None:
         cc = sa.application.instance.compute_cluster.type if sa.application.instance and \
             sa.application.instance.compute_cluster else "local"
-        if cc == "kubernetes":
+        if cc == "kubernetes" and not self.local_runs:
             from ..core.k8s import render_manifests
             sa.manifests = render_manifests(plan, sa.tenant, sa.code_archive_id)
             sa.status = "DEPLOYED"
@@ -221,7 +226,7 @@ class ControlPlane:
         from ..runtime.local import LocalApplicationRunner
         code = self.local_code(sa) if sa.code_archive_id else ""
         runner = LocalApplicationRunner(sa.application, application_id=sa.application_id, tenant=sa.tenant,
-                                        code_directory=code, services=self.services)
+                                        code_directory=code, services=self.services, agents=self.only_agents)
         buf = _AppLogBuffer()
         buf.setFormatter(logging.Formatter("%(name)s %(message)s"))
         logging.getLogger().addHandler(buf)
@@ -557,15 +562,24 @@ class WebServiceServer:
             self._runner = web.AppRunner(self.make_app())
             self._loop.run_until_complete(self._runner.setup())
             site = web.TCPSite(self._runner, self.host, self.port)
-            self._loop.run_until_complete(site.start())
+            try:
+                self._loop.run_until_complete(site.start())
+            except OSError as e:      # e.g. the port is taken: start() raises it
+                self._start_error = e
+                self._started.set()
+                return
             if self.port == 0:
                 self.port = site._server.sockets[0].getsockname()[1]
             self._started.set()
             self._loop.run_forever()
 
         self._thread = threading.Thread(target=run, daemon=True, name="webservice")
+        self._start_error = None
         self._thread.start()
         self._started.wait(30)
+        if self._start_error is not None:
+            self._loop = None
+            raise self._start_error
         return self
 
     def stop(self) -> None:

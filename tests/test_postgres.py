@@ -113,9 +113,12 @@ def test_query_and_execute_through_the_datasource(pg):
 
 
 def test_unsupported_jdbc_urls_fail_at_init():
-    for url in ("jdbc:herddb:server:herddb:7000", "jdbc:mysql://db/app", ""):
+    for url in ("jdbc:mysql://db/app", ""):
         with pytest.raises(ValueError, match="not supported"):
             jdbc_datasource({"service": "jdbc", "url": url})
+    # a HerdDB server URL with no local database service behind it (herddb.py)
+    with pytest.raises(ConnectionError, match="--start-database"):
+        jdbc_datasource({"service": "jdbc", "url": "jdbc:herddb:server:herddb.invalid:7000"})
     # HerdDB's embedded mode is an in-process database: served by SQLite
     ds = jdbc_datasource({"service": "jdbc", "url": "jdbc:herddb:local"})
     ds.execute_statement("CREATE TABLE IF NOT EXISTS t (a INT)", [], [])
@@ -129,7 +132,7 @@ def test_query_agent_start_fails_on_unreachable_or_unsupported_jdbc():
                          "password": "p"})
     a = GenAIToolKitAgent()
     a.init({"steps": [{"type": "query", "query": "SELECT 1", "fields": [], "output-field": "value.x"}],
-            "datasource": {"service": "jdbc", "url": "jdbc:herddb:server:localhost:7000"}})
+            "datasource": {"service": "jdbc", "url": "jdbc:mysql://localhost:3306/app"}})
     with pytest.raises(ValueError, match="not supported"):
         a.start()
 
