@@ -670,6 +670,7 @@ def main():
         stream_res = {"elapsed": time.time() - ts0, "lats": s_lats}
     mine = {"elapsed": elapsed, "lats": my_lats, "chunks": chunks, "assign": assign, "stream": stream_res,
             "prefill_tokens": stats.get("prefill_tokens", 0), "requests": stats.get("requests", 0),
+            "prompt_tokens": stats.get("prompt_tokens", 0),
             "phases": phases, "stage_trace": stage_trace, "gc": {"pause_ms": round(gc_t["ms"], 1), "collections_by_gen": gc_t["n"]},
             "knn_rounds": dist_knn.active().rounds if dist_knn.active() else 0,
             "knn_stats": ({k: (round(v, 3) if isinstance(v, float) else v) for k, v in dist_knn.active().stats.items()}
@@ -683,7 +684,12 @@ def main():
     all_lats = [x for g in gathered for x in g["lats"]]
     p50 = statistics.median(all_lats) if all_lats else 0.0
     reqs = sum(g["requests"] for g in gathered)
-    mean_prompt = sum(g["prefill_tokens"] for g in gathered) / reqs if reqs else 0.0
+    # seq_len: the mean prompt length of a request (what the model attends over); the
+    # prefill tokens actually computed are fewer by the prefix-KV hits, reported beside it
+    prompt_toks = sum(g["prompt_tokens"] for g in gathered)
+    prefill_toks = sum(g["prefill_tokens"] for g in gathered)
+    mean_prompt = prompt_toks / reqs if reqs else 0.0
+    hit_frac = (prompt_toks - prefill_toks) / prompt_toks if prompt_toks else 0.0
     total = args.batch * args.steps * world
     value = total / elapsed
     if rank == 0:
@@ -696,6 +702,8 @@ def main():
             "data": "synthetic questions + synthetic crawled pages + synthetic corpus, random-init weights",
             "config": {"model": chat_model, "embedding_model": embed_model, "global_batch": args.batch * world,
                        "seq_len": round(mean_prompt, 1), "max_model_len": 4096,
+                       "prefix_hit_tokens_frac": round(hit_frac, 4),
+                       "prefill_tokens_per_request": round(prefill_toks / reqs, 1) if reqs else 0.0,
                        "prefill_chunk": args.prefill_chunk, "max_new_tokens": args.max_tokens,
                        "corpus_docs_per_gpu": args.corpus, "top_k": 20, "rerank": 5,
                        "crawled_pages_per_gpu_per_step": args.docs, "crawl": crawl,

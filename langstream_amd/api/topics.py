@@ -55,6 +55,41 @@ class TopicConsumer:
     def get_native_consumer(self): return None
 
 
+class BatchWriteError(Exception):
+    """A ``write_many`` where some records failed: ``errors[i]`` is record i's error, or
+    None when record i was delivered (only the failed ones go to retry / skip / DLQ)."""
+
+    def __init__(self, errors: List[Optional[BaseException]]):
+        first = next(e for e in errors if e is not None)
+        super().__init__(f"{sum(e is not None for e in errors)} of {len(errors)} records failed: {first!r}")
+        self.errors = errors
+
+
+def per_item(futures: List[Future]) -> Future:
+    """One future for a batch of record writes: its result is None when every write
+    succeeded, else it fails with a ``BatchWriteError`` listing each record's error."""
+    out: Future = Future()
+    if not futures:
+        out.set_result(None)
+        return out
+    left = [len(futures)]
+    lock = threading.Lock()
+
+    def one(_f: Future) -> None:
+        with lock:
+            left[0] -= 1
+            last = left[0] == 0
+        if last:
+            errs = [f.exception() for f in futures]
+            if any(e is not None for e in errs):
+                out.set_exception(BatchWriteError(errs))
+            else:
+                out.set_result(None)
+    for f in futures:
+        f.add_done_callback(one)
+    return out
+
+
 def all_of(futures: List[Future]) -> Future:
     """One future for many: done when all are, failed with the first failure (in list
     order) if any failed."""
@@ -86,9 +121,10 @@ class TopicProducer:
     def write(self, record: Record) -> Future: raise NotImplementedError
 
     def write_many(self, records: List[Record]) -> Future:
-        """Write records in order; one future for all of them (a runtime with a batching
-        client overrides this to queue them as one unit)."""
-        return all_of([self.write(r) for r in records])
+        """Write records in order; one future for all of them, failing with a
+        ``BatchWriteError`` (per-record errors) if any write failed (a runtime with a
+        batching client overrides this to queue them as one unit)."""
+        return per_item([self.write(r) for r in records])
     def get_info(self) -> Dict[str, Any]: return {}
     def get_total_in(self) -> int: return 0
     def get_native_producer(self): return None

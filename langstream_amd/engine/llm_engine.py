@@ -230,7 +230,8 @@ class LLMEngine:
         self.ttft_s: collections.deque = collections.deque(maxlen=4096)   # engine-side arrival -> first token
         self.stats = {"prefill_steps": 0, "decode_steps": 0, "mixed_steps": 0, "prefill_tokens": 0,
                       "decode_tokens": 0, "preemptions": 0, "requests": 0, "finished": 0, "graph_steps": 0,
-                      "host_ms": 0.0, "wait_ms": 0.0, "launch_ms": 0.0, "retire_ms": 0.0, "prefix_hit_tokens": 0}
+                      "host_ms": 0.0, "wait_ms": 0.0, "launch_ms": 0.0, "retire_ms": 0.0, "prefix_hit_tokens": 0,
+                      "prompt_tokens": 0}
         # prompt lengths of the most recent requests (decode attention cost follows the longest context)
         self.prompt_lens: collections.deque = collections.deque(maxlen=8192)
         # wall-clock (time.time) times at which requests reached the scheduler
@@ -344,6 +345,7 @@ class LLMEngine:
             if self.prefix is not None:
                 self.prefix.observe(r)
             self.stats["requests"] += 1
+            self.stats["prompt_tokens"] += len(r.prompt_ids)
             self.prompt_lens.append(len(r.prompt_ids))
             self.arrival_log.append(time.time())
 
@@ -361,7 +363,7 @@ class LLMEngine:
             return
         if self.prefix is not None and self.prefix.pending:
             # a capture's block copies make this step an eager one (graphs carry no copies)
-            self.prefix.collect_captures(self._step_id + 1)
+            self.prefix.collect_captures(self._step_id + 1, headroom=len(decode))
         launched = self._launch(decode, chunks)
         prev, self._inflight = self._inflight, launched
         self.stats["host_ms"] += (time.perf_counter() - t0) * 1000
@@ -391,10 +393,15 @@ class LLMEngine:
         in-flight step and preempting the newest sequences when the pool is short)."""
         cands = self._decode_candidates()[: self.max_batch]
         need = sum(self._blocks_needed(r, r.num_computed + 1) for r in cands)
+        sid = self._step_id + 1
+        if need > self.allocator.num_free() and self.prefix is not None:
+            self.prefix.reclaim(need, sid)   # idle cached prefixes go before any sequence does
         if need > self.allocator.num_free():
             self._flush()  # exact host state before preempting
             cands = self._decode_candidates()[: self.max_batch]
             need = sum(self._blocks_needed(r, r.num_computed + 1) for r in cands)
+            if self.prefix is not None:
+                self.prefix.reclaim(need, sid)
             while need > self.allocator.num_free() and len(cands) > 1 and self._preempt_one():
                 cands = self._decode_candidates()[: self.max_batch]
                 need = sum(self._blocks_needed(r, r.num_computed + 1) for r in cands)
@@ -402,6 +409,8 @@ class LLMEngine:
         for r in cands:
             n = self._blocks_needed(r, r.num_computed + 1)
             if n:
+                if not self.allocator.can_allocate(n) and self.prefix is not None:
+                    self.prefix.reclaim(n, sid)
                 if not self.allocator.can_allocate(n):
                     continue
                 r.blocks += self.allocator.allocate(n)
@@ -439,6 +448,8 @@ class LLMEngine:
             nshared = hit // BLOCK
             if hit:
                 need = (base + n + BLOCK - 1) // BLOCK - nshared
+            if hit and not self.allocator.can_allocate(need + headroom):
+                self.prefix.reclaim(need + headroom, self._step_id + 1, keep=entry)
             if hit and self.allocator.can_allocate(need + headroom):
                 r.num_computed = base
                 r.blocks = list(entry.blocks[:nshared]) + list(self.allocator.allocate(need))
@@ -454,6 +465,8 @@ class LLMEngine:
                 remaining = total - r.num_computed
                 n = min(remaining, budget)
                 need = self._blocks_needed(r, r.num_computed + n)
+            if not self.allocator.can_allocate(need + headroom) and self.prefix is not None:
+                self.prefix.reclaim(need + headroom, self._step_id + 1)
             if not self.allocator.can_allocate(need + headroom):
                 if not chosen and not self.running:
                     fit = (self.allocator.num_free() + len(r.blocks)) * BLOCK - r.num_computed

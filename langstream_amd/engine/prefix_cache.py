@@ -128,9 +128,11 @@ class PrefixCache:
         self.stats["hit_tokens"] += len(e.ids)
 
     # -------------------------------------------------------------- captures
-    def collect_captures(self, step: int) -> None:
+    def collect_captures(self, step: int, headroom: int = 0) -> None:
         """Capture every pending prefix whose request has computed past it (its KV is
-        written by an earlier step); requests that finished or lost their blocks drop."""
+        written by an earlier step); requests that finished or lost their blocks drop.
+        ``headroom``: blocks a capture may not take (one per decoding sequence of the
+        step being built, so a capture never starves decoding)."""
         keep = []
         for r, L in self.pending:
             if getattr(r, "finished", False):
@@ -144,7 +146,8 @@ class PrefixCache:
                 continue
             if len(self.entries) >= self.max_entries and not self._evict(step):
                 continue
-            if not self.allocator.can_allocate(nb):
+            if self.allocator.num_free() - headroom < nb:
+                keep.append((r, L))            # the pool is short now: retry at a later step
                 continue
             dst = list(self.allocator.allocate(nb))
             self.copies.extend(zip(r.blocks[:nb], dst))
@@ -170,6 +173,32 @@ class PrefixCache:
         self.allocator.free(e.blocks)
         self.stats["evictions"] += 1
         return True
+
+    def _idle(self, step: int, keep: Optional[_Entry] = None) -> List[_Entry]:
+        return [e for e in self.entries if e.refs == 0 and e.last_step != step and e is not keep]
+
+    def reclaimable(self, step: int, keep: Optional[_Entry] = None) -> int:
+        """Blocks that ``reclaim`` could give back for the step being built."""
+        return sum(len(e.blocks) for e in self._idle(step, keep))
+
+    def reclaim(self, want_free: int, step: int, keep: Optional[_Entry] = None) -> int:
+        """KV pool pressure: evict idle entries (no request shares their blocks, no copy of
+        step ``step`` reads them), least recently used first, until ``want_free`` blocks
+        are free or none is left.  The scheduler calls this before it preempts a sequence,
+        skips a decode row or ends a prompt with 'length' -- cached prefixes are an
+        optimisation and never hold blocks a sequence needs.  Returns the blocks freed."""
+        freed = 0
+        while self.allocator.num_free() < want_free:
+            cands = self._idle(step, keep)
+            if not cands:
+                break
+            e = min(cands, key=lambda x: x.last_step)
+            self.entries.remove(e)
+            self.allocator.free(e.blocks)
+            freed += len(e.blocks)
+            self.stats["evictions"] += 1
+            self.stats["reclaimed_blocks"] = self.stats.get("reclaimed_blocks", 0) + len(e.blocks)
+        return freed
 
     def take_copies(self) -> List[Tuple[int, int]]:
         c, self.copies = self.copies, []

@@ -207,6 +207,7 @@ class _Persistence:
 # Optional search tracer (benchmarks): when a list, every search appends (enter, lock
 # taken, top-k on the host, results built, number of queries) as time.time() stamps.
 SEARCH_TRACE: Optional[list] = None
+SEARCH_RETRIES = 3   # lock-free top-k attempts a renumbering delete may invalidate before one under the lock
 
 
 class VectorStore:
@@ -229,6 +230,7 @@ class VectorStore:
         self.lock = threading.RLock()
         self._write_ev = None   # recorded on the store stream after every device write
         self._gen = 0           # bumped when deletes renumber rows (search re-resolves)
+        self.search_retries = 0
         self._persist = _Persistence(persist_dir, fsync) if persist_dir else None
         if self._persist is not None:
             with on_search(self.device), self.lock:
@@ -475,7 +477,23 @@ class VectorStore:
         # search stream, so the device reads are ordered against them either way.
         with on_search(self.device):
             q = self._to_device_query(qn)
-            while True:
+            for attempt in range(SEARCH_RETRIES + 1):
+                if attempt == SEARCH_RETRIES:
+                    # a steady stream of deletes kept renumbering rows: the last attempt
+                    # holds the lock from the top-k through the row resolution, so the
+                    # search always finishes
+                    with self.lock:
+                        t_lk = time.time() if tr is not None else 0.0
+                        (hs, hi), ev = to_host_async(*self.topk_rows(q, k))
+                        if ev is not None:
+                            ev.synchronize()
+                        s, idx = hs.tolist(), hi.tolist()
+                        t_gpu = time.time() if tr is not None else 0.0
+                        hits = [[(sc, r, self.row_payload(r)) for sc, r in zip(srow, irow) if 0 <= r < self._n]
+                                for srow, irow in zip(s, idx)]
+                        pend = (self._gather_rows_async({r for row in hits for _, r, _ in row})
+                                if with_vectors else None)
+                    break
                 with self.lock:
                     t_lk = time.time() if tr is not None else 0.0
                     gen = self._gen
@@ -486,6 +504,7 @@ class VectorStore:
                 t_gpu = time.time() if tr is not None else 0.0
                 with self.lock:
                     if self._gen != gen:
+                        self.search_retries += 1
                         continue
                     hits = [[(sc, r, self.row_payload(r)) for sc, r in zip(srow, irow) if 0 <= r < self._n]
                             for srow, irow in zip(s, idx)]

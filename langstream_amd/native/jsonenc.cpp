@@ -174,8 +174,15 @@ void put_float(std::string& o, double x) {
 // a Float32List: every item a float (anything else: the generic path)
 bool put_f32_list(std::string& o, PyObject* seq) {
   const Py_ssize_t n = PyList_GET_SIZE(seq);
-  for (Py_ssize_t i = 0; i < n; ++i)
-    if (!PyFloat_CheckExact(PyList_GET_ITEM(seq, i))) return false;
+  // Float32List is a mutable list: user or EL code may have stored doubles in it.  Only
+  // when every item is exactly a float32 value are float32 shortest digits the same
+  // number; otherwise the generic path writes doubles (json.dumps' digits).
+  for (Py_ssize_t i = 0; i < n; ++i) {
+    PyObject* it = PyList_GET_ITEM(seq, i);
+    if (!PyFloat_CheckExact(it)) return false;
+    const double d = PyFloat_AS_DOUBLE(it);
+    if ((double)(float)d != d && d == d) return false;
+  }
   const size_t at = o.size();
   o.resize(at + size_t(n) * 24 + 2);   // ", " + at most 18 chars per float32, + brackets
   char* w = &o[at];

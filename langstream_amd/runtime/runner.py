@@ -26,7 +26,7 @@ from typing import Any, Callable, Dict, List, Optional
 from ..api.agent import (AgentCode, AgentContext, AgentProcessor, AgentService, AgentSink, AgentSource,
                          BadRecordHandler, ComponentType, completed)
 from ..api.record import Record, SourceRecordAndResult
-from ..api.topics import TopicConnectionProvider, TopicConnectionsRuntimeRegistry
+from ..api.topics import BatchWriteError, TopicConnectionProvider, TopicConnectionsRuntimeRegistry
 from .composite import CompositeAgentProcessor
 from .errors import Outcome, PermanentFailureException, StandardErrorsHandler
 from .metrics import MetricsReporter
@@ -363,9 +363,23 @@ class AgentRunner:
                 self.metrics.counter("sink_records_out", self.pod.agent_id).inc(len(recs))
                 self.tracker.commit(recs)
                 return
+            # a BatchWriteError names the records that failed: the delivered ones commit,
+            # only the failed ones go to retry / skip / dead-letter
+            per = err.errors if isinstance(err, BatchWriteError) and len(err.errors) == len(recs) else None
+            i = 0
+            delivered = []
             for r in ok:
                 for rec in r.result_records:
-                    self._on_write_error(rec, r.source_record, err, errors)
+                    e = err if per is None else per[i]
+                    i += 1
+                    if e is None:
+                        delivered.append(rec)
+                    else:
+                        self._on_write_error(rec, r.source_record, e, errors)
+            if delivered:
+                self.records_out += len(delivered)
+                self.metrics.counter("sink_records_out", self.pod.agent_id).inc(len(delivered))
+                self.tracker.commit(delivered)
 
         fut.add_done_callback(done)
 

@@ -39,7 +39,7 @@ from concurrent.futures import Future
 from typing import Any, Dict, List, Optional, Tuple
 
 from ...api.record import Header, Record
-from ...api.topics import (TopicAdmin, TopicConnectionsRuntime, TopicConnectionsRuntimeRegistry, TopicConsumer,
+from ...api.topics import (BatchWriteError, TopicAdmin, TopicConnectionsRuntime, TopicConnectionsRuntimeRegistry, TopicConsumer,
                            TopicOffsetPosition, TopicProducer, TopicReader, TopicReadResult, decode_offsets,
                            encode_offsets)
 from . import codecs, serde
@@ -140,22 +140,29 @@ class KafkaConsumer(TopicConsumer):
 
 
 class _Group:
-    """The future behind ``n`` queued records (one record for ``write``)."""
-    __slots__ = ("fut", "left", "err")
+    """The future behind ``n`` queued records (one record for ``write``).  A failed
+    ``write_many`` group fails with a ``BatchWriteError`` naming the records whose produce
+    request failed: records of the batch acknowledged in another request are not
+    retried, skipped or dead-lettered."""
+    __slots__ = ("fut", "n", "left", "errs")
 
-    def __init__(self, fut: Future, n: int):
-        self.fut, self.left, self.err = fut, n, None
+    def __init__(self, fut: Future, n: int, batch: bool = False):
+        self.fut, self.n, self.left, self.errs = fut, (n if batch else 0), n, None
 
-    def one_done(self, err) -> None:
+    def one_done(self, err, idx: int) -> None:
         # only the sender thread calls this: no lock needed
-        if err is not None and self.err is None:
-            self.err = err
+        if err is not None:
+            if self.errs is None:
+                self.errs = {}
+            self.errs[idx] = err
         self.left -= 1
         if self.left == 0:
-            if self.err is not None:
-                self.fut.set_exception(self.err)
-            else:
+            if not self.errs:
                 self.fut.set_result(None)
+            elif self.n == 0:
+                self.fut.set_exception(next(iter(self.errs.values())))
+            else:
+                self.fut.set_exception(BatchWriteError([self.errs.get(i) for i in range(self.n)]))
 
 
 class KafkaProducer(TopicProducer):
@@ -177,7 +184,7 @@ class KafkaProducer(TopicProducer):
         self.topic = topic
         self._in = 0
         self._cv = threading.Condition()
-        self._q: List[Tuple[tuple, "_Group", int]] = []
+        self._q: List[Tuple[tuple, "_Group", int, int]] = []   # (item, group, bytes, index in group)
         self._closed = False
         self._thread: Optional[threading.Thread] = None
         self._last: Optional[Future] = None
@@ -217,12 +224,13 @@ class KafkaProducer(TopicProducer):
         except Exception as e:  # noqa: BLE001
             f.set_exception(e)
             return f
-        return self._enqueue([(item, _Group(f, 1), size)], f)
+        return self._enqueue([(item, _Group(f, 1), size, 0)], f)
 
     def write_many(self, records: List[Record]) -> Future:
         """Queue the records as one unit (same order, same batching into produce requests
         as ``write``) behind ONE future: resolved when the last of them is acknowledged,
-        failed if any produce request carrying them failed.  Per-record futures and their
+        failed with a ``BatchWriteError`` (which records failed) if any produce request
+        carrying them failed.  Per-record futures and their
         callbacks were a third of an embeddings agent's per-record host time."""
         f: Future = Future()
         if not records:
@@ -233,8 +241,8 @@ class KafkaProducer(TopicProducer):
         except Exception as e:  # noqa: BLE001  (nothing queued: all or none)
             f.set_exception(e)
             return f
-        g = _Group(f, len(items))
-        return self._enqueue([(it, g, size) for it, size in items], f)
+        g = _Group(f, len(items), batch=True)
+        return self._enqueue([(it, g, size, i) for i, (it, size) in enumerate(items)], f)
 
     def _sender(self) -> None:
         while True:
@@ -249,13 +257,13 @@ class KafkaProducer(TopicProducer):
                     n += 1
                 batch, self._q = self._q[:n], self._q[n:]
             try:
-                self.p.send_many([it for it, _, _ in batch])
+                self.p.send_many([it for it, _, _, _ in batch])
                 self._in += len(batch)
                 err = None
             except Exception as e:  # noqa: BLE001
                 err = e
-            for _, g, _ in batch:
-                g.one_done(err)
+            for _, g, _, i in batch:
+                g.one_done(err, i)
 
     def flush(self, timeout: float = 30.0) -> None:
         """Wait until every record written so far is acknowledged (one sender thread

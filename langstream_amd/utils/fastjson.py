@@ -6,8 +6,11 @@ record's float vector costs ~0.7 us per float through ``json.dumps``.
 ``Float32List``: a list of floats that hold float32 values (a local model's embedding
 row).  The native encoder writes each with its shortest float32 digits (~9 significant
 digits instead of the ~17 a widened double needs): half the record bytes, a quarter of
-the formatting time, and the same float32 after parsing.  Everywhere else it is a plain
-list (json.dumps, msgpack, EL, the vector stores)."""
+the formatting time, and the same float32 after parsing -- the one place the output
+differs from ``json.dumps`` text (not in value).  It is a mutable list: when any item is
+not exactly a float32 value (user or EL code stored a double in it), the whole list is
+written with double digits, byte-identical to ``json.dumps``.  Everywhere else it is a
+plain list (json.dumps, msgpack, EL, the vector stores)."""
 from __future__ import annotations
 
 import datetime as _dt

@@ -174,3 +174,33 @@ def test_bulk_failed_write_retries_per_record(fake, monkeypatch):
         out = app.consume(tout, 50, timeout=30)
     assert state["failed"] > 0
     assert sorted(json.loads(r.value())["i"] for r in out) == list(range(50))
+
+
+def test_bulk_partially_failed_write_retries_only_failed_records(fake, monkeypatch):
+    """a write_many whose middle produce request failed reports per-record
+    errors (BatchWriteError); the runner commits the delivered records and retries only
+    the failed ones -- no record is written twice."""
+    from langstream_amd.api.topics import BatchWriteError
+    tin, tout = _t(), _t()
+    state = {"failed": 0}
+    orig = MemoryProducer.write_many
+
+    def partial(self, records):
+        if self.topic == tout and state["failed"] == 0 and len(records) >= 3:
+            mid = len(records) // 2
+            state["failed"] = 1
+            orig(self, records[:mid] + records[mid + 1:]).result(10)     # all but the middle record land
+            f: Future = Future()
+            f.set_exception(BatchWriteError([None] * mid + [ConnectionError("request failed")] +
+                                            [None] * (len(records) - mid - 1)))
+            return f
+        return orig(self, records)
+    monkeypatch.setattr(MemoryProducer, "write_many", partial, raising=False)
+    extra = "    errors:\n      on-failure: fail\n      retries: 1000"
+    with LocalApplicationRunner.from_yaml(_files(_pipe(tin, tout, extra=extra))) as app:
+        for i in range(50):
+            app.produce(tin, json.dumps({"text": "t", "i": i}))
+        out = app.consume(tout, 51, timeout=5)    # a 51st record would be a duplicate
+    assert state["failed"] == 1
+    got = sorted(json.loads(r.value())["i"] for r in out)
+    assert got == list(range(50))             # each exactly once

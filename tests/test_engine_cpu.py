@@ -238,3 +238,72 @@ def test_prefix_cache_shares_full_blocks(model):
     off = LLMEngine(model, None, num_blocks=96, max_model_len=512, max_batch=8, max_prefill_tokens=128,
                     prefix_cache=False)
     assert [r.output_ids for r in reqs] == [r.output_ids for r in off.generate(prompts, sp)]
+
+
+def test_prefix_cache_yields_blocks_under_pool_pressure(model):
+    """idle cached prefixes never hold blocks a sequence needs.  A pool of
+    max_model_len / BLOCK + 1 blocks, mostly held by captured prefixes, then one long
+    request that needs nearly the whole pool: the scheduler reclaims the idle entries
+    (LRU) instead of truncating the prompt with 'length', skipping its decode rows or
+    preempting, and the tokens equal a cache-off engine's."""
+    from langstream_amd.engine.llm_engine import BLOCK
+    rng = np.random.default_rng(21)
+    max_len = 8 * BLOCK
+    nb = max_len // BLOCK + 1
+    kw = dict(num_blocks=nb, max_model_len=max_len, max_batch=4, max_prefill_tokens=128)
+    eng = LLMEngine(model, None, prefix_cache=True, **kw)
+    sp2 = SamplingParams(max_tokens=2, temperature=0.0, ignore_eos=True)
+    for _ in range(3):
+        head = rng.integers(3, 250, 100).tolist()
+        eng.generate([head + rng.integers(3, 250, 8).tolist() for _ in range(2)], sp2)
+    held = _prefix_blocks(eng)
+    assert held >= 4 and eng.allocator.num_free() + held == nb
+    long_prompt = rng.integers(3, 250, 5 * BLOCK - 10).tolist()
+    sp = SamplingParams(max_tokens=max_len - len(long_prompt) - 1, temperature=0.0, ignore_eos=True)
+    r = eng.generate([long_prompt], sp)[0]
+    off = LLMEngine(model, None, prefix_cache=False, **kw).generate([long_prompt], sp)[0]
+    assert len(r.output_ids) == sp.max_tokens and r.output_ids == off.output_ids
+    assert eng.prefix.stats.get("reclaimed_blocks", 0) >= 1 and eng.stats["preemptions"] == 0
+    assert eng.allocator.num_free() + _prefix_blocks(eng) == nb
+
+
+def test_prefix_capture_leaves_decode_headroom(model):
+    """collect_captures(headroom=n_decode): a capture never takes the blocks the step's
+    decoding sequences may need."""
+    from langstream_amd.engine.prefix_cache import PrefixCache
+
+    class Alloc:
+        def __init__(self, n):
+            self.free_ = list(range(n))
+
+        def num_free(self):
+            return len(self.free_)
+
+        def can_allocate(self, n):
+            return n <= len(self.free_)
+
+        def allocate(self, n):
+            out, self.free_ = self.free_[:n], self.free_[n:]
+            return out
+
+        def free(self, bl):
+            self.free_ += list(bl)
+
+    class R:
+        def __init__(self, ids):
+            self.prompt_ids, self.num_computed, self.finished = ids, len(ids), False
+            self.blocks = [100, 101]
+
+    a = Alloc(3)
+    pc = PrefixCache(a, 64, min_len=32)
+    head = list(range(3, 103))
+    pc.observe(R(head + [1]))
+    r2 = R(head + [2])
+    pc.observe(r2)
+    assert pc.pending
+    pc.collect_captures(step=1, headroom=2)   # 3 free - 2 headroom < 2 blocks: no capture
+    assert not pc.entries
+    pc.collect_captures(step=1, headroom=1)
+    assert len(pc.entries) == 1 and a.num_free() == 1
+    assert pc.reclaimable(step=1) == 0          # captured this step: its copy reads it
+    assert pc.reclaim(3, step=2) == 2 and a.num_free() == 3 and not pc.entries

@@ -83,6 +83,12 @@ def test_float32_vectors_use_float32_digits():
     # plain lists keep the double digits
     x = float(np.float32(0.1))
     assert fastjson.dumps([x]) == json.dumps([x]) and fastjson.dumps(Float32List([x])) == "[0.1]"
+    # user / EL code stored a double in a Float32List: no silent float32 rounding
+    row = f32_rows(np.full((1, 4), 0.5, dtype=np.float32))[0]
+    row[1] = 0.1                                    # not a float32 value
+    row.append(1 / 3)
+    assert fastjson.dumps(row) == json.dumps(row) == "[0.5, 0.1, 0.5, 0.5, 0.3333333333333333]"
+    assert fastjson.dumps(Float32List([float("nan"), 2.0])) == json.dumps([float("nan"), 2.0])
 
 
 def test_f32_matrix_matches_numpy():

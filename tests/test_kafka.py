@@ -239,3 +239,37 @@ def test_producer_write_many_one_future(broker):
     prod.close()
     c.delete_topic(t)
     c.close()
+
+
+def test_producer_write_many_reports_per_record_errors(broker):
+    """the middle produce request of a write_many fails -> BatchWriteError
+    whose errors name exactly that request's records; the others were delivered."""
+    from langstream_amd.api.record import SimpleRecord
+    from langstream_amd.api.topics import BatchWriteError
+    from langstream_amd.topics.kafka import KafkaProducer
+    c = KafkaClient(broker.bootstrap)
+    t = "wmerr-" + uuid.uuid4().hex[:6]
+    c.create_topic(t, 1)
+    prod = KafkaProducer(broker.bootstrap, t)
+    prod.MAX_BATCH_RECORDS = 2
+    real = prod.p.send_many
+    calls = {"n": 0}
+
+    def flaky(items):
+        calls["n"] += 1
+        if calls["n"] == 2:
+            raise ConnectionError("produce request failed")
+        return real(items)
+    prod.p.send_many = flaky
+    with prod._cv:      # queue the whole group before the sender wakes
+        f = prod.write_many([SimpleRecord.of(f"k{i}", f"v{i}") for i in range(6)])
+    with pytest.raises(BatchWriteError) as ei:
+        f.result(30)
+    errs = ei.value.errors
+    assert [e is not None for e in errs] == [False, False, True, True, False, False]
+    one = prod.write(SimpleRecord.of("x", "y"))
+    one.result(30)
+    got = PartitionReader(c, t, start="earliest").read(100)
+    assert [v.decode() for _, _, _, _, v, _ in got] == ["v0", "v1", "v4", "v5", "y"]
+    prod.close()
+    c.delete_topic(t)

@@ -406,3 +406,28 @@ def test_two_sinks_persist_in_their_own_state_dirs(tmp_path):
         assert not VectorStoreRegistry.exists("c1")       # s1 has not restarted yet
     finally:
         VectorStoreRegistry.reset()
+
+
+def test_search_finishes_under_a_stream_of_deletes(monkeypatch):
+    """a delete between every lock-free top-k and its row resolution cannot
+    make a search repeat forever -- after SEARCH_RETRIES invalidated attempts the search
+    holds the lock from the top-k through the resolution."""
+    import langstream_amd.engine.vector_store as vs
+    g = torch.Generator().manual_seed(4)
+    vecs = torch.randn(40, 32, generator=g)
+    s = VectorStore(32, device="cpu", dtype=torch.float32)
+    s.upsert(list(range(40)), vecs.tolist(), [{"i": i} for i in range(40)])
+    real = vs.to_host_async
+    calls = {"n": 0}
+
+    def racing(*t):
+        calls["n"] += 1
+        out = real(*t)
+        if calls["n"] <= vs.SEARCH_RETRIES:
+            s.delete([calls["n"]])     # every lock-free attempt loses its rows
+        return out
+
+    monkeypatch.setattr(vs, "to_host_async", racing)
+    res = s.search([vecs[30].tolist()], 2)
+    assert calls["n"] == vs.SEARCH_RETRIES + 1 and s.search_retries == vs.SEARCH_RETRIES
+    assert res[0][0]["id"] == 30 and res[0][0]["i"] == 30
