@@ -296,6 +296,41 @@ def _stream_summary(gathered, args, world):
 from langstream_amd.bench.site import Site, SiteProcess, make_page  # noqa: E402
 
 
+def _bringup(rank: int, world: int, use_gpu: bool, args):
+    """Multi-rank bring-up: a per-rank watchdog (a rank that stops making progress ends
+    every rank with exit 3 and one JSON line naming the stalled phase and the suspect
+    rank) and the collective self-check on the job's group (a wrong RCCL / gloo sum ends
+    the run with exit 2 and the failing phase, before any timing)."""
+    from langstream_amd.parallel.bringup import CollectiveCheckError, check_collectives
+    from langstream_amd.parallel.watchdog import RankWatchdog
+    wd = RankWatchdog(rank, world, prefix="bench-watchdog").start()
+    try:
+        res = check_collectives(device=f"cuda:{torch_current_device()}" if use_gpu else "cpu", graphs=False,
+                                watchdog=wd, limit_s=_env_int("LS_BRINGUP_LIMIT_S", 300))
+    except CollectiveCheckError as e:
+        print(json.dumps({"error": "collective self-check failed", "rank": rank, "detail": str(e)}),
+              file=sys.stderr, flush=True)
+        os._exit(2)
+    if rank == 0:
+        print(json.dumps({"bringup": res, "world": world}), file=sys.stderr, flush=True)
+    return wd
+
+
+def torch_current_device() -> int:
+    import torch
+    return torch.cuda.current_device()
+
+
+def _phase(wd, name: str, limit_s: float) -> None:
+    if wd is not None:
+        wd.phase(name, _env_int("LS_WATCHDOG_LIMIT_S", 0) or limit_s)
+
+
+def _beat(wd) -> None:
+    if wd is not None:
+        wd.beat()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -379,12 +414,16 @@ def main():
     # LS_BENCH_FORCE_DIST=1 (under torchrun): take the multi-rank code path even at world
     # size 1 -- RCCL/gloo groups, barriers, the sharded kNN service -- to rehearse it on one GPU
     multi = world > 1 or os.environ.get("LS_BENCH_FORCE_DIST") == "1" and "WORLD_SIZE" in os.environ
+    wd = None
     if multi:
         dist.init_process_group("nccl" if use_gpu else "gloo")
         ctrl = dist.new_group(backend="gloo")   # barriers / small host exchanges
+        wd = _bringup(rank, world, use_gpu, args)
 
     def barrier():
         if multi:
+            if wd is not None:
+                wd.arrive("barrier")
             dist.barrier(group=ctrl)
         if use_gpu:
             torch.cuda.synchronize()
@@ -424,6 +463,7 @@ def main():
 
     # ---- untimed setup: engines, corpus ingest into this rank's HBM shard
     t_setup = time.time()
+    _phase(wd, "setup", 1800)
     persist_dir = None
     if not args.no_persist:
         import tempfile
@@ -609,6 +649,7 @@ def main():
                 raise runner.errors[0]
             if time.time() > deadline:
                 raise TimeoutError(f"rank {rank}: {quota - len(lats)} window answers missing")
+            _beat(wd)
             for r in reader.read().records:
                 t = sent.pop(r.key(), None)
                 if t is None:
@@ -621,9 +662,12 @@ def main():
         steps_done[0] += k_steps
         return lats
 
+    _phase(wd, "warmup", args.timeout + 300)
     for _ in range(args.warmup):
         run_step()
+        _beat(wd)
     chunks0 = len(store)
+    _phase(wd, "timed", args.timeout + 300)
     barrier()
     from langstream_amd.utils import threads as _threads
     cpu0 = _threads.snapshot()
@@ -647,6 +691,7 @@ def main():
         for _ in range(args.steps):
             _, lats = run_step()
             my_lats.extend(lats)
+            _beat(wd)
     barrier()
     elapsed = time.time() - t0
     gc.callbacks.remove(_gc_cb)
@@ -675,6 +720,7 @@ def main():
             "knn_rounds": dist_knn.active().rounds if dist_knn.active() else 0,
             "knn_stats": ({k: (round(v, 3) if isinstance(v, float) else v) for k, v in dist_knn.active().stats.items()}
                           if dist_knn.active() else None)}
+    _phase(wd, "report", 600)
     if multi:
         gathered = [None] * world
         dist.all_gather_object(gathered, mine, group=ctrl)

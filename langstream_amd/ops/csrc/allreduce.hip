@@ -235,44 +235,68 @@ class OneShotAllReduce {
     W_ = pg_->getSize();
     rank_ = pg_->getRank();
     TORCH_CHECK(W_ >= 1 && W_ <= kMaxRanks, "one-shot all-reduce supports up to ", kMaxRanks, " ranks");
-    const int64_t bytes = region_bytes(cap_);
-    AR_OK(hipMalloc(&base_, bytes));
-    AR_OK(hipMemset(base_, 0, bytes));
+    // Data halves: plain device memory (written once by the owner, read once per call by
+    // each peer over xGMI).  Flags: UNCACHED device memory -- peers on other GPUs spin on
+    // them with system-scope acquires, and a coarse-grained allocation gives no coherence
+    // guarantee for a remote writer's stores into a line this GPU's L2 may hold.  A driver
+    // that cannot export uncached memory over IPC falls back to plain memory (warned).
+    const int64_t dbytes = 2 * cap_ * (int64_t)sizeof(bf16);
+    const int64_t fbytes = kMaxRanks * kBlocks * (int64_t)sizeof(int);
+    AR_OK(hipMalloc(&base_, dbytes));
+    AR_OK(hipMemset(base_, 0, dbytes));
+    hipIpcMemHandle_t h[2];
+    AR_OK(hipIpcGetMemHandle(&h[0], base_));
+    if (hipExtMallocWithFlags(&flags_, fbytes, hipDeviceMallocUncached) == hipSuccess &&
+        hipIpcGetMemHandle(&h[1], flags_) == hipSuccess) {
+      flags_uncached_ = true;
+    } else {
+      if (flags_ != nullptr) (void)hipFree(flags_);
+      (void)hipGetLastError();
+      flags_ = nullptr;
+      AR_OK(hipMalloc(&flags_, fbytes));
+      AR_OK(hipIpcGetMemHandle(&h[1], flags_));
+      TORCH_WARN_ONCE("one-shot all-reduce: uncached flag memory not exportable over IPC; using plain device memory");
+    }
+    AR_OK(hipMemset(flags_, 0, fbytes));
     AR_OK(hipMalloc(&epoch_, kBlocks * sizeof(int) + sizeof(int)));
     AR_OK(hipMemset(epoch_, 0, kBlocks * sizeof(int) + sizeof(int)));
     err_ = epoch_ + kBlocks;
-    hipIpcMemHandle_t h;
-    AR_OK(hipIpcGetMemHandle(&h, base_));
+    AR_OK(hipDeviceSynchronize());
     auto opts = at::TensorOptions().dtype(at::kByte).device(at::kCUDA, at::hip::current_device());
-    at::Tensor mine = at::from_blob(&h, {(int64_t)sizeof(h)}, at::kByte).to(opts);
+    at::Tensor mine = at::from_blob(h, {(int64_t)sizeof(h)}, at::kByte).to(opts);
     std::vector<at::Tensor> parts;
     for (int w = 0; w < W_; ++w) parts.push_back(at::empty({(int64_t)sizeof(h)}, opts));
     std::vector<std::vector<at::Tensor>> outs{parts};
     std::vector<at::Tensor> ins{mine};
     pg_->allgather(outs, ins)->wait();
     for (int w = 0; w < W_; ++w) {
-      char* p = nullptr;
       if (w == rank_) {
-        p = (char*)base_;
-      } else {
-        hipIpcMemHandle_t hw;
-        at::Tensor hb = parts[w].cpu();
-        memcpy(&hw, hb.data_ptr(), sizeof(hw));
-        void* q = nullptr;
-        AR_OK(hipIpcOpenMemHandle(&q, hw, hipIpcMemLazyEnablePeerAccess));
-        opened_.push_back(q);
-        p = (char*)q;
+        tbl_.data[w] = (bf16*)base_;
+        tbl_.flags[w] = (int*)flags_;
+        continue;
       }
-      tbl_.data[w] = (bf16*)p;
-      tbl_.flags[w] = (int*)(p + 2 * cap_ * sizeof(bf16));
+      hipIpcMemHandle_t hw[2];
+      at::Tensor hb = parts[w].cpu();
+      memcpy(hw, hb.data_ptr(), sizeof(hw));
+      void* q = nullptr;
+      AR_OK(hipIpcOpenMemHandle(&q, hw[0], hipIpcMemLazyEnablePeerAccess));
+      opened_.push_back(q);
+      tbl_.data[w] = (bf16*)q;
+      q = nullptr;
+      AR_OK(hipIpcOpenMemHandle(&q, hw[1], hipIpcMemLazyEnablePeerAccess));
+      opened_.push_back(q);
+      tbl_.flags[w] = (int*)q;
     }
   }
 
   ~OneShotAllReduce() {
     for (void* q : opened_) (void)hipIpcCloseMemHandle(q);
     (void)hipFree(base_);
+    (void)hipFree(flags_);
     (void)hipFree(epoch_);
   }
+
+  bool flags_uncached() const { return flags_uncached_; }
 
   int64_t capacity() const { return cap_; }
 
@@ -320,6 +344,8 @@ class OneShotAllReduce {
   int64_t cap_;
   int W_ = 1, rank_ = 0;
   void* base_ = nullptr;
+  void* flags_ = nullptr;
+  bool flags_uncached_ = false;
   int* epoch_ = nullptr;
   int* err_ = nullptr;
   PeerTable tbl_{};
@@ -406,6 +432,12 @@ std::vector<at::Tensor> oneshot_allreduce_sim(std::vector<at::Tensor> inputs, in
   AR_OK(hipStreamSynchronize(stream));
   outs.push_back(epochs.select(1, kBlocks).contiguous());
   return outs;
+}
+
+// Whether an instance built on this group got uncached (fine-grained) flag memory.
+bool oneshot_flags_uncached(py::object process_group) {
+  auto pg = py::cast<c10::intrusive_ptr<::c10d::ProcessGroup>>(process_group);
+  return make_oneshot_allreduce(pg, 1024)->flags_uncached();
 }
 
 // World-size-agnostic self test over a real process group: build the instance, run one

@@ -39,6 +39,7 @@ void tp_sample_final(at::Tensor stats_all, at::Tensor cand_all, int64_t world, i
                      int64_t n_top, at::Tensor out_tok, at::Tensor out_lp, at::Tensor top_ids, at::Tensor top_lps);
 std::vector<at::Tensor> oneshot_allreduce_sim(std::vector<at::Tensor> inputs, int64_t calls, int64_t stall_rank);
 int64_t oneshot_allreduce_selftest(py::object process_group, at::Tensor t);
+bool oneshot_flags_uncached(py::object process_group);
 std::vector<at::Tensor> oneshot_collectives_selftest(py::object process_group, at::Tensor bf, at::Tensor g32,
                                                      at::Tensor i64, int64_t cap);
 std::vector<at::Tensor> oneshot_route_selftest(py::object process_group, at::Tensor g32, at::Tensor i64, int64_t cap);
@@ -118,6 +119,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("oneshot_allreduce_sim", &oneshot_allreduce_sim, py::arg("inputs"), py::arg("calls"),
         py::arg("stall_rank") = -1);
   m.def("oneshot_allreduce_selftest", &oneshot_allreduce_selftest);
+  m.def("oneshot_flags_uncached", &oneshot_flags_uncached);
   m.def("oneshot_collectives_selftest", &oneshot_collectives_selftest);
   m.def("oneshot_route_selftest", &oneshot_route_selftest);
   m.def("tp_sample_stats", &tp_sample_stats);

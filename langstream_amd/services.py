@@ -121,6 +121,16 @@ class ServiceRegistry:
             device = c.get("device") or default_device()
             mcfg = PRESETS[name]
             dtype = torch.bfloat16 if device.startswith("cuda") else torch.float32
+            if self.tp is not None and self.tp.world > 1:
+                # bring-up self-check of the TP collectives before any weight is loaded: a
+                # wrong RCCL / one-shot sum raises (the pod exits non-zero with the phase);
+                # a graph-captured all-reduce that fails only turns decode graphs off
+                from .parallel.bringup import check_collectives
+                chk = check_collectives(group=self.tp.group, device=device,
+                                        graphs=str(c.get("use-graphs", "true")).lower() == "true")
+                log.info("TP collective self-check: %s", chk)
+                if device.startswith("cuda") and not chk["graph"]:
+                    c["use-graphs"] = "false"
             log.info("starting LLM engine %s on %s", name, device)
             model_ = LlamaModel(mcfg, device=device, dtype=dtype, tp=self.tp)
             if c.get("weights-path"):

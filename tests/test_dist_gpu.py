@@ -115,6 +115,7 @@ def _oneshot_rank(rank, world, port, q):
         ts = [(torch.arange(n, dtype=torch.float32) % 61 - 30.0 + 0.25 * r) for r in range(world)]
         t = ts[rank].to("cuda", torch.bfloat16)
         errs = [ops.hip().oneshot_allreduce_selftest(dist.group.WORLD, t) for _ in range(3)]
+        uncached = bool(ops.hip().oneshot_flags_uncached(dist.group.WORLD))
         # after each in-place call every rank holds bf16(f32 sum over ranks, rank order)
         ref = [x.to(torch.bfloat16) for x in ts]
         for _ in range(3):
@@ -123,7 +124,7 @@ def _oneshot_rank(rank, world, port, q):
                 acc = acc + x.float()
             s = acc.to(torch.bfloat16)
             ref = [s] * world
-        q.put((rank, errs, float((t.float().cpu() - ref[0].float()).abs().max())))
+        q.put((rank, errs, float((t.float().cpu() - ref[0].float()).abs().max()), uncached))
     finally:
         dist.destroy_process_group()
 
@@ -151,9 +152,10 @@ def test_oneshot_allreduce_processes_sharing_one_gpu(W):
             if p.is_alive():
                 p.kill()
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
-    for rank, errs, diff in res:
+    for rank, errs, diff, uncached in res:
         assert errs == [0, 0, 0], (rank, errs)
         assert diff == 0.0, (rank, diff)
+        assert uncached, "the flag region fell back to coarse-grained memory (IPC export of uncached memory failed)"
 
 
 def _collectives_rank(rank, world, port, q):
@@ -251,3 +253,20 @@ def test_oneshot_routing_falls_back_to_c10d_past_one_call(n_i64, n_g32, want_use
         assert used == want_used + [0], (rank, used)
         assert i64 == want_i.tolist(), rank
         assert g == want_g.tolist(), rank
+
+
+def test_bringup_selfcheck_rccl_world1(rccl_world1, monkeypatch):
+    """parallel/bringup.py over RCCL: eager all-reduce + all-gather, a graph-captured
+    all-reduce replayed, and the one-shot IPC all-reduce, each against the host sum."""
+    from langstream_amd.parallel.bringup import check_collectives
+    monkeypatch.setenv("LS_ONESHOT_AR", "1")
+    res = check_collectives(device="cuda:0")
+    assert res == {"eager": True, "graph": True, "oneshot": True}
+
+
+def test_bringup_selfcheck_wrong_oneshot_sum_raises(rccl_world1, monkeypatch):
+    from langstream_amd.parallel.bringup import CollectiveCheckError, check_collectives
+    monkeypatch.setenv("LS_ONESHOT_AR", "1")
+    monkeypatch.setenv("LS_BRINGUP_FAULT", "wrong-sum@0")
+    with pytest.raises(CollectiveCheckError, match="eager all-reduce"):
+        check_collectives(device="cuda:0")
