@@ -248,6 +248,29 @@ class AgentRunner:
         self._topic_rt = topic_rt
 
     # ------------------------------------------------------------------ run
+    @classmethod
+    def run_main_loop(cls, source: AgentSource, processor: AgentProcessor, sink: AgentSink,
+                      errors: Optional[Dict[str, Any]] = None, has_more=None, context: Optional[AgentContext] = None,
+                      agent_id: str = "agent", max_loops: Optional[int] = None) -> "AgentRunner":
+        """``AgentRunner.runMainLoop(source, processor, sink, context, errorsHandler,
+        continueLoop)`` (RT/agent/AgentRunner.java:651-730) for already-built components:
+        the loop runs while ``has_more()`` is true (then drains in-flight records) and
+        raises the fatal error -- a ``PermanentFailureException`` under ``fail`` -- like
+        the reference's static entry point.  Returns the runner (tracker, counters)."""
+        pod = RuntimePodConfiguration(agent_id=agent_id, agent_type="custom", component_type="PROCESSOR",
+                                      application_id="app", tenant="default", configuration={},
+                                      errors=dict(errors or {"retries": 0, "onFailure": "fail"}))
+        r = cls(pod)
+        r.source, r.processor, r.sink = source, processor, sink
+        r.main_code = processor
+        r.context = context or r._make_context(None, None, None, BadRecordHandler(lambda rec, err, cleanup: None))
+        try:
+            r._main_loop(max_loops, has_more)
+        finally:
+            r._close()
+            r.stopped.set()
+        return r
+
     def stop(self) -> None:
         self._continue.clear()
 
@@ -283,7 +306,7 @@ class AgentRunner:
             except Exception:  # noqa: BLE001
                 log.exception("error closing %s", c)
 
-    def _main_loop(self, max_loops: Optional[int]) -> None:
+    def _main_loop(self, max_loops: Optional[int], continue_fn: Optional[Callable[[], bool]] = None) -> None:
         source, processor, sink = self.source, self.processor, self.sink
         for c in (source, sink, processor):
             c.set_context(self.context)
@@ -294,7 +317,7 @@ class AgentRunner:
         errors = StandardErrorsHandler(self.pod.errors)
         self.started.set()
         loops = 0
-        while self._continue.is_set():
+        while self._continue.is_set() and (continue_fn is None or continue_fn()):
             records = source.read()
             if records:
                 self.records_in += len(records)
