@@ -45,6 +45,11 @@ class _Group:
         self.rebalance_task: Optional[asyncio.Task] = None
 
 
+# what DescribeConfigs reports for a topic setting the creator did not pass (Kafka defaults)
+TOPIC_CONFIG_DEFAULTS = {"cleanup.policy": "delete", "retention.ms": "604800000", "retention.bytes": "-1",
+                         "max.message.bytes": "1048588", "segment.bytes": "1073741824"}
+
+
 class KafkaBroker:
     def __init__(self, host: str = "127.0.0.1", port: int = 0, auto_create_topics: bool = True,
                  default_partitions: int = 1, node_id: int = 0, ssl_context=None,
@@ -60,6 +65,7 @@ class KafkaBroker:
         self.auto_create = auto_create_topics
         self.default_partitions = default_partitions
         self.topics: Dict[str, List[_Partition]] = {}
+        self.topic_configs: Dict[str, Dict[str, Optional[str]]] = {}   # CreateTopics configs (DescribeConfigs)
         self.groups: Dict[str, _Group] = {}
         self.offsets: Dict[Tuple[str, str, int], int] = {}
         self._loop: Optional[asyncio.AbstractEventLoop] = None
@@ -172,12 +178,30 @@ class KafkaBroker:
                     out.append({"name": t["name"], "error": P.TOPIC_ALREADY_EXISTS})
                 else:
                     self.topics[t["name"]] = [_Partition() for _ in range(max(1, t["num_partitions"]))]
+                    self.topic_configs[t["name"]] = {c["name"]: c["value"] for c in t.get("configs") or []}
                     out.append({"name": t["name"], "error": P.NONE})
             return {"topics": out}
+        if api == P.DESCRIBE_CONFIGS:
+            res = []
+            for r in b["resources"]:
+                if r["type"] != P.RESOURCE_TOPIC or r["name"] not in self.topics:
+                    res.append({"error": P.UNKNOWN_TOPIC_OR_PARTITION, "error_message": f"unknown {r['name']}",
+                                "type": r["type"], "name": r["name"], "configs": []})
+                    continue
+                conf = dict(TOPIC_CONFIG_DEFAULTS)
+                conf.update(self.topic_configs.get(r["name"], {}))
+                want = r.get("config_names")
+                res.append({"error": P.NONE, "error_message": None, "type": r["type"], "name": r["name"],
+                            "configs": [{"name": k, "value": v, "read_only": False,
+                                         "is_default": k not in self.topic_configs.get(r["name"], {}),
+                                         "sensitive": False} for k, v in sorted(conf.items())
+                                        if not want or k in want]})
+            return {"throttle": 0, "resources": res}
         if api == P.DELETE_TOPICS:
             out = []
             for name in b["topics"]:
                 ok = self.topics.pop(name, None) is not None
+                self.topic_configs.pop(name, None)
                 out.append({"name": name, "error": P.NONE if ok else P.UNKNOWN_TOPIC_OR_PARTITION})
             return {"topics": out}
         if api == P.PRODUCE:

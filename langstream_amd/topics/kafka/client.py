@@ -169,6 +169,20 @@ class KafkaClient:
         self.refresh_metadata([name])
         return err == P.NONE
 
+    def describe_topic_configs(self, name: str) -> Dict[str, Optional[str]]:
+        """DescribeConfigs (v0) of a topic: {config name: value} (Admin.describeConfigs)."""
+        r = self.any_conn().request(P.DESCRIBE_CONFIGS, {"resources": [
+            {"type": P.RESOURCE_TOPIC, "name": name, "config_names": None}]})
+        res = r["resources"][0]
+        if res["error"] != P.NONE:
+            raise KafkaError(res["error"], f"describe configs {name}: {res.get('error_message')}")
+        return {c["name"]: c["value"] for c in res["configs"]}
+
+    def list_topics(self) -> List[str]:
+        """Admin.listTopics: every topic the cluster's metadata names."""
+        r = self.any_conn().request(P.METADATA, {"topics": None})
+        return sorted(t["name"] for t in r["topics"] if t["error"] == P.NONE)
+
     def delete_topic(self, name: str) -> None:
         self.any_conn().request(P.DELETE_TOPICS, {"topics": [name], "timeout": 30000})
         with self._lock:

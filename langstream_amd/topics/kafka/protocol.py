@@ -23,10 +23,12 @@ OFFSET_COMMIT, OFFSET_FETCH, FIND_COORDINATOR = 8, 9, 10
 JOIN_GROUP, HEARTBEAT, LEAVE_GROUP, SYNC_GROUP = 11, 12, 13, 14
 API_VERSIONS, CREATE_TOPICS, DELETE_TOPICS = 18, 19, 20
 SASL_HANDSHAKE, SASL_AUTHENTICATE = 17, 36
+DESCRIBE_CONFIGS = 32
+RESOURCE_TOPIC = 2
 
 VERSIONS = {PRODUCE: 3, FETCH: 4, LIST_OFFSETS: 1, METADATA: 1, OFFSET_COMMIT: 2, OFFSET_FETCH: 1,
             FIND_COORDINATOR: 0, JOIN_GROUP: 1, HEARTBEAT: 0, LEAVE_GROUP: 0, SYNC_GROUP: 0, API_VERSIONS: 0,
-            CREATE_TOPICS: 0, DELETE_TOPICS: 0, SASL_HANDSHAKE: 1, SASL_AUTHENTICATE: 0}
+            CREATE_TOPICS: 0, DELETE_TOPICS: 0, SASL_HANDSHAKE: 1, SASL_AUTHENTICATE: 0, DESCRIBE_CONFIGS: 0}
 
 # error codes
 NONE, OFFSET_OUT_OF_RANGE, UNKNOWN_TOPIC_OR_PARTITION = 0, 1, 3
@@ -71,6 +73,7 @@ REQ = {
                                   ("assignments", A([("partition", I32), ("brokers", A(I32))])),
                                   ("configs", A([("name", STR), ("value", NSTR)]))])), ("timeout", I32)],
     DELETE_TOPICS: [("topics", A(STR)), ("timeout", I32)],
+    DESCRIBE_CONFIGS: [("resources", A([("type", I8), ("name", STR), ("config_names", A(STR))]))],
 }
 
 RESP = {
@@ -103,6 +106,10 @@ RESP = {
                                                                   ("metadata", NSTR), ("error", I16)]))]))],
     CREATE_TOPICS: [("topics", A([("name", STR), ("error", I16)]))],
     DELETE_TOPICS: [("topics", A([("name", STR), ("error", I16)]))],
+    DESCRIBE_CONFIGS: [("throttle", I32),
+                       ("resources", A([("error", I16), ("error_message", NSTR), ("type", I8), ("name", STR),
+                                        ("configs", A([("name", STR), ("value", NSTR), ("read_only", BOOL),
+                                                       ("is_default", BOOL), ("sensitive", BOOL)]))]))],
 }
 
 # embedded consumer-protocol blobs (JoinGroup metadata / SyncGroup assignment)
