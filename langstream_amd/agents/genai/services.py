@@ -203,12 +203,28 @@ def _run_async(fn) -> Future:
 
 
 class OpenAIService(CompletionsService, EmbeddingsService):
-    """OpenAI / Azure OpenAI REST (streaming SSE for chat)."""
+    """OpenAI / Azure OpenAI REST with the reference client's wire behaviour
+    (``TransformFunctionUtil.java:95-135`` builds the Azure OpenAI SDK client;
+    ``OpenAICompletionService.java:122-498`` streams):
+
+    * with a ``url`` the deployment route ``{url}/openai/deployments/{model}/{op}
+      ?api-version=2023-08-01-preview`` is used whatever the provider (``azure`` sends the
+      key as ``api-key``, ``openai`` as a bearer token) and the body carries no model;
+      without one, ``https://api.openai.com/v1/{op}`` with ``model`` in the body;
+    * request bodies list only the options that are set, in the SDK's field order;
+    * streamed chat: role-only deltas are not chunks, chunks coalesce 1, 2, 4 ... up to
+      ``min-chunks-per-message`` and carry the stream's own completion id;
+    * streamed text completions: a blank first chunk is dropped (some models open with
+      line breaks), every other chunk -- empty ones included -- counts, and the logprobs
+      of the kept chunks are collected ({tokens[], logprobs[]}).
+    """
+
+    API_VERSION = "2023-08-01-preview"
 
     def __init__(self, cfg: Dict[str, Any], model: Optional[str] = None):
         self.cfg = cfg
         self.model = model
-        self.url = (cfg.get("url") or "https://api.openai.com/v1").rstrip("/")
+        self.url = (cfg.get("url") or "").rstrip("/")
         self.key = cfg.get("access-key")
         self.provider = cfg.get("provider", "openai")
 
@@ -218,57 +234,132 @@ class OpenAIService(CompletionsService, EmbeddingsService):
         return {"Authorization": f"Bearer {self.key}"}
 
     def _endpoint(self, kind: str, model: str) -> str:
-        if self.provider == "azure":
-            return f"{self.url}/openai/deployments/{model}/{kind}?api-version=2023-05-15"
-        return f"{self.url}/{kind}"
+        if self.url:
+            return f"{self.url}/openai/deployments/{model}/{kind}?api-version={self.API_VERSION}"
+        return f"https://api.openai.com/v1/{kind}"
+
+    def _body(self, first: Dict[str, Any], options: Dict[str, Any], fields, model: str, stream: bool):
+        body = dict(first)
+        conv = {"max-tokens": int, "temperature": float, "top-p": float, "presence-penalty": float,
+                "frequency-penalty": float, "logprobs": int}
+        for k in fields:
+            v = options.get(k)
+            if v is None:
+                continue
+            body[k.replace("-", "_")] = conv[k](v) if k in conv else v
+        if stream:
+            body["stream"] = True
+        if not self.url:
+            body["model"] = model
+        return body
+
+    def _post(self, url: str, body: Dict[str, Any], stream: bool):
+        import requests
+        data = json.dumps(body, separators=(",", ":"))
+        r = requests.post(url, data=data.encode(), headers={**self._headers(), "Content-Type": "application/json"},
+                          stream=stream, timeout=300)
+        r.raise_for_status()
+        return r
+
+    @staticmethod
+    def _events(r):
+        for line in r.iter_lines():
+            if not line or not line.startswith(b"data:"):
+                continue
+            data = line[5:].strip()
+            if data == b"[DONE]":
+                return
+            yield json.loads(data)
 
     def compute_embeddings(self, texts):
         model = self.model or "text-embedding-ada-002"
-        return _run_async(lambda: [d["embedding"] for d in _http_json(
-            self._endpoint("embeddings", model), {"model": model, "input": texts}, self._headers())["data"]])
+        # the SDK keeps the response's list order (it does not re-sort by "index")
+        return _run_async(lambda: [d["embedding"] for d in self._post(
+            self._endpoint("embeddings", model), self._body({"input": list(texts)}, {}, (), model, False),
+            False).json()["data"]])
+
+    CHAT_FIELDS = ("max-tokens", "temperature", "top-p", "logit-bias", "user", "stop", "presence-penalty",
+                   "frequency-penalty")
+    TEXT_FIELDS = ("max-tokens", "temperature", "top-p", "logit-bias", "user", "logprobs", "stop",
+                   "presence-penalty", "frequency-penalty")
 
     def get_chat_completions(self, messages, consumer, options):
         model = options.get("model") or self.model
+        stream = bool(options.get("stream", True))
 
         def run():
-            import requests
-            payload = {"model": model, "messages": [m.to_dict() for m in messages], "stream": True}
-            for k in ("max-tokens", "temperature", "top-p", "presence-penalty", "frequency-penalty", "stop", "user"):
-                if options.get(k) is not None:
-                    payload[k.replace("-", "_")] = options[k]
-            aid = f"chatcmpl-{uuid.uuid4().hex[:24]}"
-            co = ChunkCoalescer(consumer, int(options.get("min-chunks-per-message", 20)), aid)
-            parts = []
-            with requests.post(self._endpoint("chat/completions", model), json=payload, headers=self._headers(),
-                               stream=True, timeout=300) as r:
-                r.raise_for_status()
-                for line in r.iter_lines():
-                    if not line or not line.startswith(b"data:"):
+            body = self._body({"messages": [m.to_dict() for m in messages]}, options, self.CHAT_FIELDS, model, stream)
+            r = self._post(self._endpoint("chat/completions", model), body, stream)
+            if not stream:
+                res = r.json()
+                ch = res["choices"][0]
+                return CompletionResult((ch.get("message") or {}).get("content") or "", res.get("id", ""),
+                                        ch.get("finish_reason"))
+            co, parts, aid, reason = None, [], "", None
+            with r:
+                for ev in self._events(r):
+                    choices = ev.get("choices") or []
+                    if not choices:
                         continue
-                    data = line[5:].strip()
-                    if data == b"[DONE]":
-                        break
-                    ev = json.loads(data)
-                    ch = (ev.get("choices") or [{}])[0]
+                    aid = ev.get("id") or aid
+                    if co is None:
+                        co = ChunkCoalescer(consumer, int(options.get("min-chunks-per-message", 20)), aid)
+                    ch = choices[0]
                     d = (ch.get("delta") or {}).get("content") or ""
                     parts.append(d)
+                    reason = ch.get("finish_reason") or reason
                     co.accept(d, ch.get("finish_reason") is not None)
-            return CompletionResult("".join(parts), aid)
+            return CompletionResult("".join(parts), aid, reason)
 
         return _run_async(run)
 
     def get_text_completions(self, prompts, consumer, options):
         model = options.get("model") or self.model
+        stream = bool(options.get("stream", True))
 
         def run():
-            payload = {"model": model, "prompt": prompts, "max_tokens": options.get("max-tokens", 256)}
-            if options.get("logprobs"):
-                payload["logprobs"] = 1
-            res = _http_json(self._endpoint("completions", model), payload, self._headers())
-            ch = res["choices"][0]
-            lp = ch.get("logprobs") or {}
-            return CompletionResult(ch.get("text", ""), res.get("id", ""), ch.get("finish_reason"),
-                                    lp.get("tokens") or [], lp.get("token_logprobs") or [])
+            body = self._body({"prompt": list(prompts)}, options, self.TEXT_FIELDS, model, stream)
+            r = self._post(self._endpoint("completions", model), body, stream)
+            if not stream:
+                res = r.json()
+                ch = res["choices"][0]
+                lp = ch.get("logprobs") or {}
+                return CompletionResult(ch.get("text", ""), res.get("id", ""), ch.get("finish_reason"),
+                                        lp.get("tokens") or [], lp.get("token_logprobs") or [])
+            minc = max(1, int(options.get("min-chunks-per-message", 20)))
+            state = {"first": True, "cur": 1, "n": 0, "idx": 0, "buf": [], "total": [], "toks": [], "lps": []}
+            aid, reason = "", None
+            with r:
+                for ev in self._events(r):
+                    choices = ev.get("choices") or []
+                    if not choices:
+                        continue
+                    aid = ev.get("id") or aid
+                    ch = choices[0]
+                    last = ch.get("finish_reason") is not None
+                    reason = ch.get("finish_reason") or reason
+                    content = ch.get("text")
+                    if content is None:
+                        continue
+                    if state["first"]:
+                        state["first"] = False
+                        if not content.strip():
+                            continue
+                    state["buf"].append(content)
+                    state["total"].append(content)
+                    lp = ch.get("logprobs") or {}
+                    state["toks"] += lp.get("tokens") or []
+                    state["lps"] += lp.get("token_logprobs") or []
+                    state["n"] += 1
+                    if state["n"] >= state["cur"] or last:
+                        state["cur"] = min(state["cur"] * 2, minc)
+                        state["idx"] += 1
+                        text = "".join(state["buf"])
+                        state["buf"].clear()
+                        state["n"] = 0
+                        if consumer is not None:
+                            consumer(aid, state["idx"], text, last)
+            return CompletionResult("".join(state["total"]), aid, reason, state["toks"], state["lps"])
 
         return _run_async(run)
 

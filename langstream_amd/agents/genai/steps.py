@@ -18,7 +18,7 @@ import threading
 from concurrent.futures import Future
 from typing import Any, Callable, Dict, List, Optional
 
-from ...api.util import OrderedAsyncBatchExecutor
+from ...api.util import java_hash, OrderedAsyncBatchExecutor
 from ...api import temporal as _temporal
 from ...api.types import Float32, Int8, Int16, Int32
 from .el import eval_expression, eval_predicate
@@ -325,7 +325,7 @@ class ComputeAIEmbeddingsStep(Step):
         self.loop_over = cfg.get("loop-over")
         self.executor = OrderedAsyncBatchExecutor(
             int(cfg.get("batch-size", 10)), self._process_batch, int(cfg.get("flush-interval", 0)),
-            int(cfg.get("concurrency", 4)), lambda item: hash(str(item[0].key)))
+            int(cfg.get("concurrency", 4)), lambda item: java_hash(item[0].key))
 
     def start(self):
         self.executor.start()
@@ -535,6 +535,40 @@ class QueryStep(Step):
         return fut
 
 
+# The step configuration as the reference logs it (convertToMap of ChatCompletionsConfig /
+# TextCompletionsConfig: every field in declaration order, unset ones as null, Integer /
+# Double / boolean typed).  name -> (type, default)
+CHAT_LOG_FIELDS = (("model", str, None), ("messages", list, None), ("stream-to-topic", str, None),
+                   ("stream-response-completion-field", str, None), ("min-chunks-per-message", int, 20),
+                   ("completion-field", str, None), ("stream", bool, True), ("log-field", str, None),
+                   ("max-tokens", int, None), ("temperature", float, None), ("top-p", float, None),
+                   ("logit-bias", dict, None), ("user", str, None), ("stop", list, None),
+                   ("presence-penalty", float, None), ("frequency-penalty", float, None), ("options", dict, None))
+TEXT_LOG_FIELDS = (("model", str, None), ("prompt", list, None), ("stream-to-topic", str, None),
+                   ("stream-response-completion-field", str, None), ("min-chunks-per-message", int, 20),
+                   ("completion-field", str, None), ("stream", bool, True), ("log-field", str, None),
+                   ("logprobs-field", str, None), ("logprobs", float, None), ("max-tokens", int, None),
+                   ("temperature", float, None), ("top-p", float, None), ("logit-bias", dict, None),
+                   ("user", str, None), ("stop", list, None), ("presence-penalty", float, None),
+                   ("frequency-penalty", float, None), ("options", dict, None))
+
+
+def log_options(cfg: Dict[str, Any], fields, step_type: str) -> Dict[str, Any]:
+    out: Dict[str, Any] = {"type": cfg.get("type", step_type), "when": cfg.get("when")}
+    for name, typ, dflt in fields:
+        v = cfg.get(name, dflt)
+        if typ is bool and isinstance(v, str):
+            v = v.strip().lower() == "true"
+        elif v is not None and typ in (int, float, bool) and not isinstance(v, typ):
+            v = typ(v)
+        elif v is not None and typ is float:
+            v = float(v)
+        if name == "messages" and v is not None:
+            v = [{"role": m.get("role"), "content": m.get("content")} for m in v]
+        out[name] = v
+    return out
+
+
 class ChatCompletionsStep(Step):
     """ai-chat-completions (ChatCompletionsStep.java:77-196)."""
     is_async = True
@@ -558,6 +592,7 @@ class ChatCompletionsStep(Step):
         self.options.update(cfg.get("options") or {})
         self.options["min-chunks-per-message"] = int(cfg.get("min-chunks-per-message", 20))
         self.options["stream"] = bool(cfg.get("stream", True))
+        self.log_options = log_options(cfg, CHAT_LOG_FIELDS, "ai-chat-completions")
 
     def start(self):
         if self.stream_to:
@@ -606,8 +641,11 @@ class ChatCompletionsStep(Step):
                 res = f.result()
                 self._apply(rec, res.content, False)
                 if self.log_field:
-                    rec.set_result_field(json.dumps({"model": self.options.get("model"), "options": self.options,
-                                                     "messages": [m.to_dict() for m in messages]}), self.log_field)
+                    # ChatCompletionsStep.java:162-170: {options: the step config (every
+                    # field, nulls included), messages: the rendered messages, model}
+                    rec.set_result_field(json.dumps({"options": self.log_options, "messages": [m.to_dict() for m in messages],
+                                                     "model": self.log_options.get("model")}, separators=(",", ":")),
+                                         self.log_field)
                 fut.set_result(None)
             except BaseException as e:  # noqa: BLE001
                 fut.set_exception(e)
@@ -641,6 +679,7 @@ class TextCompletionsStep(ChatCompletionsStep):
         self.options.update(cfg.get("options") or {})
         self.options["min-chunks-per-message"] = int(cfg.get("min-chunks-per-message", 20))
         self.options["stream"] = bool(cfg.get("stream", True))
+        self.log_options = log_options(cfg, TEXT_LOG_FIELDS, "ai-text-completions")
 
     def process_async(self, rec) -> Future:
         fut: Future = Future()
@@ -659,8 +698,9 @@ class TextCompletionsStep(ChatCompletionsStep):
                 if self.logprobs_field:
                     rec.set_result_field({"tokens": res.tokens, "logprobs": res.logprobs}, self.logprobs_field)
                 if self.log_field:
-                    rec.set_result_field(json.dumps({"model": self.options.get("model"), "options": self.options,
-                                                     "prompt": prompts}), self.log_field)
+                    rec.set_result_field(json.dumps({"options": self.log_options, "messages": prompts,
+                                                     "model": self.log_options.get("model")}, separators=(",", ":")),
+                                         self.log_field)
                 fut.set_result(None)
             except BaseException as e:  # noqa: BLE001
                 fut.set_exception(e)

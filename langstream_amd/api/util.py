@@ -111,6 +111,37 @@ def redact_secrets(v: Any) -> Any:
 
 
 # ---------------------------------------------------------------- batch executors
+def java_hash(v: Any) -> int:
+    """``java.util.Objects.hashCode`` of a record key as the JVM computes it: String ->
+    String.hashCode over UTF-16 code units, Integer / Long / Boolean / Double per their
+    hashCode, null -> 0; byte[] keys hash by content (Arrays.hashCode).  Bucket choices of
+    the ordered batch executors depend on it (OrderedAsyncBatchExecutor.java:94-105)."""
+    def s32(h: int) -> int:
+        h &= 0xFFFFFFFF
+        return h - (1 << 32) if h >= 1 << 31 else h
+    if v is None:
+        return 0
+    if isinstance(v, bool):
+        return 1231 if v else 1237
+    if isinstance(v, int):
+        return s32(v) if -(1 << 31) <= v < (1 << 31) else s32(v ^ (v >> 32))
+    if isinstance(v, float):
+        import struct
+        bits = struct.unpack(">q", struct.pack(">d", v))[0]
+        return s32(bits ^ (bits >> 32))
+    if isinstance(v, (bytes, bytearray)):
+        h = 1
+        for b in v:
+            h = (31 * h + (b - 256 if b > 127 else b)) & 0xFFFFFFFF
+        return s32(h)
+    s = v if isinstance(v, str) else str(v)
+    h = 0
+    data = s.encode("utf-16-be")
+    for i in range(0, len(data), 2):
+        h = (31 * h + ((data[i] << 8) | data[i + 1])) & 0xFFFFFFFF
+    return s32(h)
+
+
 class _Scheduler:
     """A tiny shared timer thread (ScheduledExecutorService analogue)."""
 

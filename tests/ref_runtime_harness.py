@@ -238,3 +238,65 @@ def as_json(v):
 
 
 _lock = threading.Lock()
+
+
+# ---------------------------------------------------------------- WireMock stand-in
+class FakeHTTP:
+    """Stub server for the reference's @WireMockTest cases: ``stub(method, path, body,
+    status=200, json_body=..., text=...)`` where ``path`` includes the query string and
+    ``body`` (optional) must equal the request body exactly; unmatched requests get 404."""
+
+    def __init__(self):
+        import http.server
+        import socketserver
+        self.stubs = []
+        self.requests = []
+        outer = self
+
+        class H(http.server.BaseHTTPRequestHandler):
+            protocol_version = "HTTP/1.1"
+
+            def log_message(self, *a):
+                pass
+
+            def _do(self):
+                n = int(self.headers.get("Content-Length") or 0)
+                body = self.rfile.read(n).decode() if n else ""
+                outer.requests.append((self.command, self.path, body, dict(self.headers)))
+                for m, path, want, status, ctype, payload in outer.stubs:
+                    if m == self.command and path == self.path and (want is None or want == body):
+                        data = payload.encode()
+                        self.send_response(status)
+                        self.send_header("Content-Type", ctype)
+                        self.send_header("Content-Length", str(len(data)))
+                        self.end_headers()
+                        self.wfile.write(data)
+                        return
+                data = f"no stub for {self.command} {self.path} {body}".encode()
+                self.send_response(404)
+                self.send_header("Content-Length", str(len(data)))
+                self.end_headers()
+                self.wfile.write(data)
+
+            do_GET = do_POST = do_PUT = do_DELETE = _do
+
+        class S(socketserver.ThreadingMixIn, http.server.HTTPServer):
+            daemon_threads = True
+        self.srv = S(("127.0.0.1", 0), H)
+        self.url = f"http://127.0.0.1:{self.srv.server_address[1]}"
+        threading.Thread(target=self.srv.serve_forever, daemon=True).start()
+
+    def stub(self, method, path, body=None, status=200, json_body=None, text=None, ctype=None):
+        if json_body is not None:
+            payload, ct = json.dumps(json_body), "application/json"
+        else:
+            payload, ct = text or "", "application/json"
+        self.stubs.append((method, path, body, status, ctype or ct, payload))
+
+    def reset(self):
+        self.stubs.clear()
+        self.requests.clear()
+
+    def close(self):
+        self.srv.shutdown()
+        self.srv.server_close()
