@@ -11,7 +11,11 @@ Deliberate fixes of reference bugs (documented, behaviour otherwise identical):
 ``retrieve-documents-field`` is read from its own key (the reference reads
 ``loop-topic``: FlareControllerAgent.java:73-75), a token counts as a word when it
 CONTAINS a word character (the reference's ``matches("\\w")`` requires a 1-char token),
-and span ends are clamped to the token count (the reference can overrun).
+span ends are clamped to the token count (the reference can overrun), and every pass
+through the loop increments ``num-iterations-field`` (the reference reads the counter but
+never writes it, so ``max-iterations`` could not stop a record whose answer keeps a
+low-confidence span: with the word-token fix above, FlareControllerAgentRunnerIT's stubbed
+completion is such an answer and now loops ``max-iterations`` + 1 times, then passes).
 """
 from __future__ import annotations
 
@@ -89,6 +93,7 @@ class FlareControllerAgent(AgentProcessor):
                     sink(SourceRecordAndResult(r, [r], None))
                     continue
                 mr.set_result_field(spans, self.retrieve_field)
+                mr.set_result_field(int(it) + 1, self.iter_field)
                 f = self.producer.write(mr.to_record())
                 f.add_done_callback(lambda ff, r=r: sink(
                     SourceRecordAndResult(r, None, ff.exception()) if ff.exception() else

@@ -191,3 +191,14 @@ class GenAIToolKitAgent(AgentProcessor):
 
     def build_additional_info(self) -> Dict[str, Any]:
         return {"step": self.step_cfg.get("type")}
+
+    def get_agent_status(self):
+        # the reference reports a toolkit agent under its declared type ("drop-fields",
+        # "compute", ...: the NAR index maps every step type to GenAIToolKitAgent), not
+        # the shared runtime type (GenIAgentsRunnerIT.testRunAIToolsComposite)
+        st = super().get_agent_status()
+        step = self.step_cfg.get("type") if getattr(self, "step_cfg", None) else None
+        if step:
+            for s in st:
+                s.agent_type = step
+        return st

@@ -5,7 +5,8 @@ CMN/jstl/JstlFunctions.java:49-537, CMN/jstl/predicate/JstlPredicate.java):
 literals (numbers, 'str', "str", true/false/null), property access ``a.b``,
 ``a['b']``, ``a[0]``, arithmetic ``+ - * / div % mod``, comparisons
 (``== != < > <= >= eq ne lt gt le ge``), logic (``&& || ! and or not``), ``empty``,
-ternary ``? :``, string concatenation ``+=``, and the ``fn:`` function library.
+ternary ``? :``, string concatenation ``+=``, EL 3.0 collection literals (``[a, b]`` list,
+``{a, b}`` set, ``{k: v}`` map) and the ``fn:`` function library.
 Expressions may be wrapped in ``${...}``.  Compiled ASTs are cached.
 """
 from __future__ import annotations
@@ -29,7 +30,7 @@ _TOKEN = re.compile(r"""
     (?P<ws>\s+)
   | (?P<num>\d+\.\d*(?:[eE][+-]?\d+)?|\.\d+(?:[eE][+-]?\d+)?|\d+(?:[eE][+-]?\d+)?)
   | (?P<str>'(?:[^'\\]|\\.)*'|"(?:[^"\\]|\\.)*")
-  | (?P<op>\+=|==|!=|<=|>=|&&|\|\||[-+*/%<>!?:.,()\[\]])
+  | (?P<op>\+=|==|!=|<=|>=|&&|\|\||[-+*/%<>!?:.,()\[\]{}])
   | (?P<name>[A-Za-z_][A-Za-z0-9_]*)
 """, re.VERBOSE)
 
@@ -123,6 +124,31 @@ class _Parser:
             e = self.parse(0)
             self.expect(")")
             return self.postfix(e)
+        if kind == "op" and v == "[":
+            # EL 3.0 collection construction: [a, b, ...] is a List
+            return self.postfix(("list", self._items("]")))
+        if kind == "op" and v == "{":
+            # {a, b} is a Set, {k: v, ...} a Map
+            if self.peek() == ("op", "}"):
+                self.next()
+                return self.postfix(("set", []))
+            first = self.parse(0)
+            if self.peek() == ("op", ":"):
+                self.next()
+                pairs = [(first, self.parse(0))]
+                while self.peek() == ("op", ","):
+                    self.next()
+                    k = self.parse(0)
+                    self.expect(":")
+                    pairs.append((k, self.parse(0)))
+                self.expect("}")
+                return self.postfix(("map", pairs))
+            items = [first]
+            while self.peek() == ("op", ","):
+                self.next()
+                items.append(self.parse(0))
+            self.expect("}")
+            return self.postfix(("set", items))
         if kind == "op" and v == "!":
             return ("not", self.parse(8))
         if kind == "op" and v == "-":
@@ -147,6 +173,18 @@ class _Parser:
                 return self.postfix(("call", v, fname, args))
             return self.postfix(("var", v))
         raise ValueError(f"unexpected token {v!r}")
+
+    def _items(self, close):
+        items = []
+        if self.peek() != ("op", close):
+            while True:
+                items.append(self.parse(0))
+                if self.peek() == ("op", ","):
+                    self.next()
+                    continue
+                break
+        self.expect(close)
+        return items
 
     def postfix(self, e):
         while True:
@@ -257,6 +295,17 @@ def evaluate(ast, ctx: Dict[str, Any]) -> Any:
         return ctx.get(ast[1])
     if t == "get":
         return _get(evaluate(ast[1], ctx), evaluate(ast[2], ctx))
+    if t == "list":
+        return [evaluate(x, ctx) for x in ast[1]]
+    if t == "set":
+        out = []
+        for x in ast[1]:
+            v = evaluate(x, ctx)
+            if v not in out:
+                out.append(v)
+        return out
+    if t == "map":
+        return {evaluate(k, ctx): evaluate(v, ctx) for k, v in ast[1]}
     if t == "not":
         return not _truthy(evaluate(ast[1], ctx))
     if t == "neg":
