@@ -75,9 +75,31 @@ def safe_clone(v: Any) -> Any:
     return v
 
 
+def java_hashmap_order(d: dict) -> dict:
+    """``d`` with its keys in the iteration order of a ``java.util.HashMap`` the same
+    entries were put into (default capacity 16, load factor 0.75): buckets in index order
+    (``hash ^ hash >>> 16`` masked to the table size), insertion order within a bucket --
+    resizes split buckets without reordering them.  MutableRecord.copy() in the reference
+    clones maps into HashMaps (``MutableRecord.safeClone``), so a copied record's JSON
+    fields come out in this order (LangServeInvokeAgentRunnerIT's ``{"answer":..,"topic":..}``)."""
+    n = len(d)
+    if n < 2 or type(d) is not dict:
+        return d
+    from ...api.util import java_hash
+    cap = 16
+    while n > cap * 3 // 4:
+        cap *= 2
+    mask = cap - 1
+
+    def bucket(k):
+        h = java_hash(k) & 0xFFFFFFFF
+        return (h ^ (h >> 16)) & mask
+    return {k: d[k] for k in sorted(d, key=bucket)}
+
+
 class MutableRecord:
     __slots__ = ("key", "value", "properties", "input_topic", "output_topic", "event_time", "drop",
-                 "message_key", "record_object", "source")
+                 "message_key", "record_object", "source", "hashmap")
 
     def __init__(self, key=None, value=None, properties=None, input_topic=None, event_time=None, source=None):
         self.key = key
@@ -90,6 +112,9 @@ class MutableRecord:
         self.message_key = None
         self.record_object = None
         self.source = source
+        # a copy(): its maps are java.util.HashMaps in the reference, so fields added later
+        # also land in hash order (see java_hashmap_order); applied when leaving as a record
+        self.hashmap = False
 
     @staticmethod
     def from_record(r: Record, attempt_json_conversion: bool = True) -> "MutableRecord":
@@ -107,6 +132,7 @@ class MutableRecord:
     def copy(self) -> "MutableRecord":
         m = MutableRecord(safe_clone(self.key), safe_clone(self.value), dict(self.properties), self.input_topic,
                           self.event_time, self.source)
+        m.hashmap = True
         m.output_topic = self.output_topic
         m.drop = self.drop
         m.message_key = self.message_key
@@ -123,6 +149,7 @@ class MutableRecord:
         m.output_topic = self.output_topic
         m.drop = self.drop
         m.message_key = self.message_key
+        m.hashmap = True
         return m
 
     def to_record(self) -> Optional[Record]:
@@ -130,7 +157,11 @@ class MutableRecord:
             return None
         headers = [Header(k, v) for k, v in self.properties.items()]
         key = self.message_key if self.message_key is not None else self.key
-        r = SimpleRecord(key, self.value, self.input_topic, self.event_time, headers)
+        value = self.value
+        if self.hashmap:
+            key, value = java_hashmap_order(key) if isinstance(key, dict) else key, \
+                java_hashmap_order(value) if isinstance(value, dict) else value
+        r = SimpleRecord(key, value, self.input_topic, self.event_time, headers)
         ref = None
         if self.output_topic is not None:
             ref = {"destination_topic": self.output_topic}

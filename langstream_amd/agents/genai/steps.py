@@ -14,7 +14,6 @@ from __future__ import annotations
 import datetime as _dt
 import json
 import logging
-import threading
 from concurrent.futures import Future
 from typing import Any, Callable, Dict, List, Optional
 
@@ -528,10 +527,10 @@ class QueryStep(Step):
             except BaseException as e:  # noqa: BLE001
                 fut.set_exception(e)
 
-        if getattr(self.ds, "is_async_friendly", False):
-            run()
-        else:
-            threading.Thread(target=run, daemon=True).start()
+        # on the agent thread, as the reference's QueryStep.process: results stay in input
+        # order (JdbcDatabaseIT reads each written key back in sequence).  GPU vector
+        # queries take the micro-batched path above instead.
+        run()
         return fut
 
 

@@ -209,7 +209,8 @@ class LangServeInvokeAgent(AgentProcessor):
         try:
             mr = MutableRecord.from_record(record)
             el = mr.el_context()
-            body = json.dumps({"input": {n: eval_expression(e, el) for n, e in self.fields}})
+            body = json.dumps({"input": {n: eval_expression(e, el) for n, e in self.fields}}, separators=(",", ":"),
+                              ensure_ascii=False, default=str)
             jctx = mr.json_context()
             headers = {"Content-Type": "application/json"}
             headers.update({k: t.render(jctx) for k, t in self.header_t.items()})

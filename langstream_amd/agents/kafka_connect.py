@@ -342,6 +342,10 @@ class KafkaConnectSinkAgent(AgentSink):
         self._lock = threading.Lock()
         self._last_flush = time.time()
         self.task: Optional[SinkTask] = None
+        # the reference's test hook (KafkaConnectSinkAgent.java:429-431): the first N records
+        # fail conversion and go through the bad-record handler (errors.on-failure)
+        self._inject_errors = int(self.adapter.get("__test_inject_conversion_error", 0) or 0)
+        self._stopped = False
 
     def set_context(self, context) -> None:
         super().set_context(context)
@@ -357,18 +361,44 @@ class KafkaConnectSinkAgent(AgentSink):
     def handles_commit(self) -> bool:
         return True
 
+    def _stop_on_failure(self) -> None:
+        """errors.on-failure=fail: the sink stops before the error propagates; records not
+        yet handed to the task are dropped (they stay uncommitted, so they are redelivered)
+        -- the reference's close() from the bad-record handler."""
+        with self._lock:
+            self._stopped = True
+            self._buf.clear()
+
     def write(self, record: Record) -> Future:
-        part = getattr(record, "partition", None)
-        off = getattr(record, "offset", None)
-        cr = ConnectRecord(record.origin(), part, off, record.key(), record.value(),
-                           {h.key: h.value for h in record.headers()}, record.timestamp())
+        self.processed(1, 0)
+        if self._stopped:
+            raise RuntimeError("Sink is stopped. Cannot send the records")
+        try:
+            if self._inject_errors > 0:
+                self._inject_errors -= 1
+                raise RuntimeError("Injected record conversion error")
+            cr = self._to_connect(record)
+        except Exception as e:  # noqa: BLE001
+            # a record that cannot be converted: skip / dead-letter / fail by errors.on-failure
+            # (the handler raises for "fail"; the runner then stops with this cause)
+            handler = getattr(getattr(self, "ctx", None), "bad_record_handler", None)
+            if handler is None:
+                raise
+            handler.handle(record, e, self._stop_on_failure)
+            return completed(None)
         with self._lock:
             self._buf.append((cr, record))
             full = len(self._buf) >= self.max_batch
-        self.processed(1, 0)
         if full:
             self._put()
         return completed(None)
+
+    @staticmethod
+    def _to_connect(record: Record) -> "ConnectRecord":
+        part = getattr(record, "partition", None)
+        off = getattr(record, "offset", None)
+        return ConnectRecord(record.origin(), part, off, record.key(), record.value(),
+                             {h.key: h.value for h in record.headers()}, record.timestamp())
 
     def _put(self) -> None:
         with self._lock:
@@ -409,7 +439,8 @@ class KafkaConnectSinkAgent(AgentSink):
     def close(self) -> None:
         if self.task is not None:
             try:
-                self.flush()
+                if not self._stopped:
+                    self.flush()
             finally:
                 self.task.stop()
                 self.connector.stop()

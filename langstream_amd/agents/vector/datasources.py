@@ -41,7 +41,6 @@ log = logging.getLogger(__name__)
 
 
 class DataSource:
-    is_async_friendly = False
 
     def fetch_data(self, query: str, params: List[Any]) -> List[Dict[str, Any]]:
         raise NotImplementedError
@@ -126,7 +125,6 @@ def _bind_text(query: str, params: Optional[List[Any]], sent) -> str:
 
 
 class LocalVectorDataSource(DataSource):
-    is_async_friendly = True
 
     def __init__(self, cfg: Dict[str, Any]):
         self.cfg = cfg

@@ -39,10 +39,28 @@ _lock = threading.Lock()
 _servers: Dict[Tuple[str, int], "HerdDBServer"] = {}
 
 
+_AUTO_PK = re.compile(r"\b(integer|int|long|bigint)\s+auto_increment\s+primary\s+key\b", re.I)
+_AUTO = re.compile(r"\s+auto_increment\b", re.I)
+
+
 def herddb_sql(sql: str) -> str:
     """HerdDB dialect -> SQLite: ``CAST(? AS FLOAT ARRAY)`` binds the JSON vector as is
-    (``FLOATA`` columns hold JSON arrays; SQLite keeps any declared type name)."""
-    return _CAST.sub(r"\1", sql)
+    (``FLOATA`` columns hold JSON arrays; SQLite keeps any declared type name), and an
+    ``integer auto_increment primary key`` column becomes SQLite's rowid alias
+    (``INTEGER PRIMARY KEY AUTOINCREMENT``: keys 1, 2, ... as HerdDB generates them)."""
+    sql = _CAST.sub(r"\1", sql)
+    if "auto_increment" in sql.lower():
+        sql = _AUTO.sub("", _AUTO_PK.sub("INTEGER PRIMARY KEY AUTOINCREMENT", sql))
+    return sql
+
+
+def herddb_keys(res: Dict[str, Any]) -> Dict[str, Any]:
+    """HerdDB's JDBC driver names the generated-keys column ``key`` whatever the table's
+    column is called (JdbcDatabaseIT.testSimpleQueries expects ``{"key": 1}``)."""
+    keys = res.get("generatedKeys")
+    if isinstance(keys, dict) and keys:
+        res["generatedKeys"] = {"key": next(iter(keys.values()))}
+    return res
 
 
 def parse_url(url: str) -> Tuple[str, int]:
@@ -106,7 +124,7 @@ class _HerdDBDataSource(SqliteDataSource):
         return super().fetch_data(herddb_sql(query), params)
 
     def execute_statement(self, query, generated_keys, params):
-        return super().execute_statement(herddb_sql(query), generated_keys, params)
+        return herddb_keys(super().execute_statement(herddb_sql(query), generated_keys, params))
 
     def script(self, statements):
         return super().script([herddb_sql(s) for s in statements])
@@ -155,7 +173,7 @@ def _remote_class():
             return super().fetch_data(herddb_sql(query), params)
 
         def execute_statement(self, query, generated_keys, params):
-            return super().execute_statement(herddb_sql(query), generated_keys, params)
+            return herddb_keys(super().execute_statement(herddb_sql(query), generated_keys, params))
 
         def script(self, statements):
             return super().script([herddb_sql(x) for x in statements])

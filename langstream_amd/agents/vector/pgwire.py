@@ -582,7 +582,6 @@ class PgConnection:
 # ---------------------------------------------------------------- datasource
 class PostgresDataSource:
     """``query`` / ``vector-db-sink`` / ``jdbc-table`` over a PostgreSQL server."""
-    is_async_friendly = False
 
     def __init__(self, cfg: Dict[str, Any]):
         self.url = str(cfg.get("url"))

@@ -15,8 +15,10 @@ Parity: ``WebCrawlerSource.java:95-461``, ``crawler/WebCrawler.java``,
   fragments are stripped; 3xx redirects are followed by enqueueing the Location (unless
   it is forbidden); 4xx drops the URL, 5xx/IO errors re-queue it up to
   ``max-error-count`` times.
-* each page is ONE record: key = url, value = raw bytes, headers ``url`` and
-  ``content_type``.  ``commit()`` marks the URL processed (it leaves ``remainingUrls``);
+* each page is ONE record: key = url, value = the page re-serialised from its parsed
+  tree (``agents/htmlnorm.py``, the reference's ``document.html()``) for ``text/*``
+  pages, the raw bytes for XML and -- with ``allow-non-html-contents`` -- other types;
+  headers ``url`` and ``content_type``.  ``commit()`` marks the URL processed (it leaves ``remainingUrls``);
   status (remaining urls, every seen url with type/depth, robots files, index
   timestamps) is flushed every ``max-unflushed-pages`` commits and at the end of a pass,
   so a restarted agent resumes where it stopped.  After a full pass the source idles
@@ -24,10 +26,10 @@ Parity: ``WebCrawlerSource.java:95-461``, ``crawler/WebCrawler.java``,
 """
 from __future__ import annotations
 
-import html.parser
 import json
 import logging
 import os
+import re
 import threading
 import time
 import urllib.parse
@@ -39,10 +41,12 @@ from ..api.agent import AgentSource
 from ..api.record import Header, Record, SimpleRecord
 from ..api.util import get_boolean, get_int, get_list, get_string
 from ..runtime.registry import register_agent
+from . import htmlnorm
 
 log = logging.getLogger(__name__)
 DEFAULT_USER_AGENT = "Mozilla/5.0 (compatible; LangStream.ai/0.1; +https://langstream.ai)"
 PAGE, ROBOTS, SITEMAP = "PAGE", "ROBOTS", "SITEMAP"
+_XML_TYPE = re.compile(r"(application|text)/\w*\+?xml")
 
 
 def remove_fragment(url: str) -> str:
@@ -136,18 +140,6 @@ class CrawlerStatus:
         self.robots = dict(st.get("robotFiles") or {})
 
 
-class _Links(html.parser.HTMLParser):
-    def __init__(self):
-        super().__init__(convert_charrefs=True)
-        self.hrefs: List[str] = []
-
-    def handle_starttag(self, tag, attrs):
-        if tag.lower() == "a":
-            for k, v in attrs:
-                if k == "href" and v:
-                    self.hrefs.append(v)
-
-
 class WebCrawler:
     def __init__(self, cfg: CrawlerConfig, status: CrawlerStatus, visitor: Callable[[str, bytes, str], None]):
         import requests
@@ -233,7 +225,6 @@ class WebCrawler:
                 for sm in rp.site_maps() or []:
                     self.status.add_url(sm, SITEMAP, 0, True)
             else:
-                import re
                 for loc in re.findall(r"<loc>\s*([^<\s]+)\s*</loc>", body):
                     if not self._forbidden(loc):
                         self._add_page(loc, depth)
@@ -261,7 +252,14 @@ class WebCrawler:
             self._throttle(cur)
             return True
         ctype = r.headers.get("Content-Type", "text/html")
-        is_html = "html" in ctype.lower() or "xml" in ctype.lower()
+        low = ctype.lower()
+        # what the reference's HTML fetch accepts (text/*, XML types); XML is passed through
+        is_xml = bool(_XML_TYPE.match(low))
+        is_html = low.startswith("text/") and not is_xml
+        if is_xml:
+            self.visitor(cur, r.content, ctype)
+            self._throttle(cur)
+            return True
         if not is_html:
             if self.cfg.allow_non_html:
                 self.visitor(cur, r.content, ctype)
@@ -269,13 +267,13 @@ class WebCrawler:
                 self.status.add_url(cur, typ, depth, False)
             self._throttle(cur)
             return True
+        try:
+            page, hrefs = htmlnorm.normalize(r.text)
+            content = page.encode("utf-8")
+        except Exception:  # noqa: BLE001
+            content, hrefs = r.content, []
         if self.cfg.scan_html:
-            p = _Links()
-            try:
-                p.feed(r.text)
-            except Exception:  # noqa: BLE001
-                pass
-            for href in p.hrefs:
+            for href in hrefs:
                 u = remove_fragment(urllib.parse.urljoin(cur, href))
                 if not u.startswith(("http://", "https://")):
                     continue
@@ -283,7 +281,7 @@ class WebCrawler:
                     self.status.add_url(u, PAGE, depth + 1, False)
                 else:
                     self._add_page(u, depth)
-        self.visitor(cur, r.content, ctype)
+        self.visitor(cur, content, ctype)
         self._throttle(cur)
         return True
 

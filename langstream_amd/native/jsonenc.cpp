@@ -1,6 +1,9 @@
-// json_dumps(obj) -> str: byte-identical to Python's json.dumps(obj) with its default
-// options (", " / ": " separators, ensure_ascii, allow_nan, insertion-ordered keys),
-// for dict / list / tuple / str / int / float / bool / None trees.
+// json_dumps(obj) -> str: the text the reference runtime puts on a topic for a map /
+// list value (Jackson's ObjectMapper.writeValueAsString: compact "," / ":" separators,
+// non-ASCII characters written as themselves, control characters escaped), which is
+// byte-identical to Python's json.dumps(obj, separators=(",", ":"), ensure_ascii=False)
+// (allow_nan, insertion-ordered keys) for dict / list / tuple / str / int / float /
+// bool / None trees.  Numbers keep Python's repr digits.
 //
 // Why native: records leaving an embeddings agent carry a 384..1024-float vector, and
 // json.dumps spends ~0.7 us per float in float.__repr__ + str building (263 us for one
@@ -10,8 +13,9 @@
 // decimal exponents -4..15 with a ".0" for integral values, else d.ddde+XX.
 //
 // Anything else (numpy scalars, objects with a `default`, cycles deeper than the
-// limit) raises _lsnative.JsonUnsupported and the Python wrapper falls back to
-// json.dumps, so errors and extensions behave exactly as before.
+// limit, strings with lone surrogates) raises _lsnative.JsonUnsupported and the Python
+// wrapper falls back to json.dumps with the same options, so errors and extensions
+// behave exactly as before.
 //
 // Float32 vectors: a list of the registered float32-vector type (utils/fastjson.py
 // Float32List: the embeddings of a local float32 / bf16 model) is written with each
@@ -47,58 +51,62 @@ void put_u16(std::string& o, unsigned c) {
   o.append(b, 6);
 }
 
+inline void put_utf8(std::string& o, Py_UCS4 c) {
+  if (c < 0x80) {
+    o.push_back((char)c);
+  } else if (c < 0x800) {
+    o.push_back((char)(0xc0 | (c >> 6)));
+    o.push_back((char)(0x80 | (c & 0x3f)));
+  } else if (c < 0x10000) {
+    if (c >= 0xd800 && c <= 0xdfff) throw Unsupported{};   // lone surrogate: json's own path
+    o.push_back((char)(0xe0 | (c >> 12)));
+    o.push_back((char)(0x80 | ((c >> 6) & 0x3f)));
+    o.push_back((char)(0x80 | (c & 0x3f)));
+  } else {
+    o.push_back((char)(0xf0 | (c >> 18)));
+    o.push_back((char)(0x80 | ((c >> 12) & 0x3f)));
+    o.push_back((char)(0x80 | ((c >> 6) & 0x3f)));
+    o.push_back((char)(0x80 | (c & 0x3f)));
+  }
+}
+
+inline bool put_escape(std::string& o, Py_UCS4 c) {
+  switch (c) {
+    case '"': o.append("\\\""); return true;
+    case '\\': o.append("\\\\"); return true;
+    case '\n': o.append("\\n"); return true;
+    case '\r': o.append("\\r"); return true;
+    case '\t': o.append("\\t"); return true;
+    case '\b': o.append("\\b"); return true;
+    case '\f': o.append("\\f"); return true;
+    default:
+      if (c < 0x20) { put_u16(o, c); return true; }
+      return false;
+  }
+}
+
 void put_str(std::string& o, PyObject* s) {
   if (PyUnicode_READY(s) < 0) throw Unsupported{};
   const Py_ssize_t n = PyUnicode_GET_LENGTH(s);
   const int kind = PyUnicode_KIND(s);
   const void* d = PyUnicode_DATA(s);
   o.push_back('"');
-  if (kind == PyUnicode_1BYTE_KIND) {
+  if (PyUnicode_IS_ASCII(s)) {
     const unsigned char* p = (const unsigned char*)d;
     Py_ssize_t i = 0;
     while (i < n) {
       // copy the run of characters that need no escape in one append
       Py_ssize_t j = i;
-      while (j < n && p[j] >= 0x20 && p[j] < 0x7f && p[j] != '"' && p[j] != '\\') ++j;
+      while (j < n && p[j] >= 0x20 && p[j] != '"' && p[j] != '\\') ++j;
       if (j > i) o.append((const char*)p + i, j - i);
       if (j >= n) break;
-      unsigned c = p[j];
-      switch (c) {
-        case '"': o.append("\\\""); break;
-        case '\\': o.append("\\\\"); break;
-        case '\n': o.append("\\n"); break;
-        case '\r': o.append("\\r"); break;
-        case '\t': o.append("\\t"); break;
-        case '\b': o.append("\\b"); break;
-        case '\f': o.append("\\f"); break;
-        default: put_u16(o, c);
-      }
+      put_escape(o, p[j]);
       i = j + 1;
     }
   } else {
     for (Py_ssize_t i = 0; i < n; ++i) {
-      Py_UCS4 c = PyUnicode_READ(kind, d, i);
-      if (c >= 0x20 && c < 0x7f && c != '"' && c != '\\') {
-        o.push_back((char)c);
-        continue;
-      }
-      switch (c) {
-        case '"': o.append("\\\""); break;
-        case '\\': o.append("\\\\"); break;
-        case '\n': o.append("\\n"); break;
-        case '\r': o.append("\\r"); break;
-        case '\t': o.append("\\t"); break;
-        case '\b': o.append("\\b"); break;
-        case '\f': o.append("\\f"); break;
-        default:
-          if (c >= 0x10000) {
-            Py_UCS4 v = c - 0x10000;
-            put_u16(o, 0xd800 | ((v >> 10) & 0x3ff));
-            put_u16(o, 0xdc00 | (v & 0x3ff));
-          } else {
-            put_u16(o, c);
-          }
-      }
+      const Py_UCS4 c = PyUnicode_READ(kind, d, i);
+      if (!put_escape(o, c)) put_utf8(o, c);
     }
   }
   o.push_back('"');
@@ -184,12 +192,12 @@ bool put_f32_list(std::string& o, PyObject* seq) {
     if ((double)(float)d != d && d == d) return false;
   }
   const size_t at = o.size();
-  o.resize(at + size_t(n) * 24 + 2);   // ", " + at most 18 chars per float32, + brackets
+  o.resize(at + size_t(n) * 24 + 2);   // "," + at most 18 chars per float32, + brackets
   char* w = &o[at];
   char* const w0 = w;
   *w++ = '[';
   for (Py_ssize_t i = 0; i < n; ++i) {
-    if (i) { *w++ = ','; *w++ = ' '; }
+    if (i) *w++ = ',';
     w += format_float(w, (float)PyFloat_AS_DOUBLE(PyList_GET_ITEM(seq, i)));
   }
   *w++ = ']';
@@ -243,7 +251,7 @@ bool put_float_run(std::string& o, PyObject* seq, bool lst, Py_ssize_t n) {
     if (!PyFloat_CheckExact(it)) return false;
     xs[i] = PyFloat_AS_DOUBLE(it);
   }
-  // ", " + at most 25 chars per float, + brackets
+  // "," + at most 25 chars per float, + brackets
   tmp.resize(size_t(n) * 28 + 2);
   size_t len = 0;
   bool ok = true;
@@ -252,7 +260,7 @@ bool put_float_run(std::string& o, PyObject* seq, bool lst, Py_ssize_t n) {
     char* w = &tmp[0];
     *w++ = '[';
     for (Py_ssize_t i = 0; i < n; ++i) {
-      if (i) { *w++ = ','; *w++ = ' '; }
+      if (i) *w++ = ',';
       w += format_float(w, xs[i]);
     }
     *w++ = ']';
@@ -303,7 +311,7 @@ void put(std::string& o, PyObject* v, int depth) {
     if (n >= kFloatRunMin && float_run_enabled() && put_float_run(o, seq, lst, n)) return;
     o.push_back('[');
     for (Py_ssize_t i = 0; i < n; ++i) {
-      if (i) o.append(", ");
+      if (i) o.push_back(',');
       PyObject* it = lst ? PyList_GET_ITEM(seq, i) : PyTuple_GET_ITEM(seq, i);
       Py_INCREF(it);
       try {
@@ -325,10 +333,10 @@ void put(std::string& o, PyObject* v, int depth) {
     PyObject *k, *x;
     bool first = true;
     while (PyDict_Next(v, &pos, &k, &x)) {
-      if (!first) o.append(", ");
+      if (!first) o.push_back(',');
       first = false;
       put_key(o, k);
-      o.append(": ");
+      o.push_back(':');
       Py_INCREF(x);
       try {
         put(o, x, depth + 1);
@@ -353,7 +361,7 @@ py::object json_dumps(py::handle obj) {
     PyErr_SetString(g_unsupported, "json_dumps: type outside the native encoder");
     throw py::error_already_set();
   }
-  // output is pure ASCII (ensure_ascii)
+  // output is UTF-8
   PyObject* s = PyUnicode_FromStringAndSize(o.data(), (Py_ssize_t)o.size());
   if (!s) throw py::error_already_set();
   return py::reinterpret_steal<py::object>(s);
@@ -365,7 +373,7 @@ void bind_jsonenc(py::module_& m) {
   g_unsupported = PyErr_NewException("_lsnative.JsonUnsupported", PyExc_TypeError, nullptr);
   m.attr("JsonUnsupported") = py::handle(g_unsupported);
   m.def("json_dumps", &json_dumps, py::arg("obj"),
-        "json.dumps(obj) with default options; raises JsonUnsupported for other types");
+        "json.dumps(obj, separators=(',', ':'), ensure_ascii=False); raises JsonUnsupported for other types");
   // rows of a C-contiguous float32 [n, d] buffer -> n Float32Lists (the embedding engine's
   // results): the PyFloats are made here, ~10x cheaper than ndarray.tolist() + a copy
   m.def("f32_rows", [](py::buffer b) {

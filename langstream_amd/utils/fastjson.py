@@ -1,7 +1,10 @@
-"""``dumps(obj)``: ``json.dumps(obj)`` (default options) through the native encoder
-(``native/jsonenc.cpp``), byte-identical output; objects outside its type set fall back
-to ``json.dumps``.  Used where records are serialised onto topics -- an embeddings
-record's float vector costs ~0.7 us per float through ``json.dumps``.
+"""``dumps(obj)``: the JSON text of a map / list record value as the reference runtime
+writes it onto a topic (Jackson: compact separators, non-ASCII as itself) --
+``json.dumps(obj, separators=(",", ":"), ensure_ascii=False)`` -- through the native
+encoder (``native/jsonenc.cpp``), byte-identical output; objects outside its type set
+fall back to ``json.dumps`` with the same options.  Used where records are serialised
+onto topics -- an embeddings record's float vector costs ~0.7 us per float through
+``json.dumps``.
 
 ``Float32List``: a list of floats that hold float32 values (a local model's embedding
 row).  The native encoder writes each with its shortest float32 digits (~9 significant
@@ -19,6 +22,7 @@ from typing import Any
 
 _native = None
 _unsupported = None
+SEPARATORS = (",", ":")
 
 
 class Float32List(list):
@@ -103,4 +107,9 @@ def dumps(obj: Any) -> str:
             return _native(obj)
         except _unsupported:
             pass
-    return json.dumps(obj, default=_default)
+    s = json.dumps(obj, default=_default, separators=SEPARATORS, ensure_ascii=False)
+    try:
+        s.encode("utf-8")
+    except UnicodeEncodeError:   # lone surrogates: \u escapes keep the text encodable
+        s = json.dumps(obj, default=_default, separators=SEPARATORS)
+    return s

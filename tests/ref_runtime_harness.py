@@ -244,7 +244,8 @@ _lock = threading.Lock()
 class FakeHTTP:
     """Stub server for the reference's @WireMockTest cases: ``stub(method, path, body,
     status=200, json_body=..., text=...)`` where ``path`` includes the query string and
-    ``body`` (optional) must equal the request body exactly; unmatched requests get 404."""
+    ``body`` (optional) must equal the request body exactly and ``headers`` (optional) must
+    all be present with these values; unmatched requests get 404."""
 
     def __init__(self):
         import http.server
@@ -263,8 +264,9 @@ class FakeHTTP:
                 n = int(self.headers.get("Content-Length") or 0)
                 body = self.rfile.read(n).decode() if n else ""
                 outer.requests.append((self.command, self.path, body, dict(self.headers)))
-                for m, path, want, status, ctype, payload in outer.stubs:
-                    if m == self.command and path == self.path and (want is None or want == body):
+                for m, path, want, status, ctype, payload, hdrs in outer.stubs:
+                    if m == self.command and path == self.path and (want is None or want == body) and \
+                            all(self.headers.get(k) == v for k, v in hdrs.items()):
                         data = payload.encode()
                         self.send_response(status)
                         self.send_header("Content-Type", ctype)
@@ -286,12 +288,12 @@ class FakeHTTP:
         self.url = f"http://127.0.0.1:{self.srv.server_address[1]}"
         threading.Thread(target=self.srv.serve_forever, daemon=True).start()
 
-    def stub(self, method, path, body=None, status=200, json_body=None, text=None, ctype=None):
+    def stub(self, method, path, body=None, status=200, json_body=None, text=None, ctype=None, headers=None):
         if json_body is not None:
             payload, ct = json.dumps(json_body), "application/json"
         else:
             payload, ct = text or "", "application/json"
-        self.stubs.append((method, path, body, status, ctype or ct, payload))
+        self.stubs.append((method, path, body, status, ctype or ct, payload, dict(headers or {})))
 
     def reset(self):
         self.stubs.clear()

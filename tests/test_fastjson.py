@@ -1,5 +1,8 @@
-"""Native JSON encoder (native/jsonenc.cpp) is byte-identical to json.dumps."""
+"""Native JSON encoder (native/jsonenc.cpp) is byte-identical to
+jdumps(separators=(",", ":"), ensure_ascii=False) -- the compact, UTF-8 text the
+reference's Jackson writes for map values on topics."""
 import collections
+import functools
 import json
 import random
 import struct
@@ -8,6 +11,8 @@ import numpy as np
 import pytest
 
 from langstream_amd.utils import fastjson
+
+jdumps = functools.partial(json.dumps, separators=(",", ":"), ensure_ascii=False)
 
 
 def test_floats_match_repr():
@@ -18,7 +23,7 @@ def test_floats_match_repr():
         vals.append(rnd.uniform(-1, 1) * 10 ** rnd.randint(-30, 30))
         vals.append(float(np.float32(rnd.gauss(0, 1))))
         vals.append(struct.unpack("d", struct.pack("Q", rnd.getrandbits(64)))[0])
-    assert [fastjson.dumps(v) for v in vals] == [json.dumps(v) for v in vals]
+    assert [fastjson.dumps(v) for v in vals] == [jdumps(v) for v in vals]
 
 
 def test_structures_and_strings():
@@ -27,8 +32,8 @@ def test_structures_and_strings():
             [], {}, (1, 2), [10 ** 30, -10 ** 30, -5, 0], "x" * 1000, {"k": [[[]]]}, "汉字",
             {"embeddings": np.random.default_rng(0).standard_normal(384).astype(np.float32).tolist()}]
     for o in objs:
-        assert fastjson.dumps(o) == json.dumps(o)
-    assert fastjson.dumps(collections.OrderedDict(a=1, b=[1.5])) == json.dumps(collections.OrderedDict(a=1, b=[1.5]))
+        assert fastjson.dumps(o) == jdumps(o)
+    assert fastjson.dumps(collections.OrderedDict(a=1, b=[1.5])) == jdumps(collections.OrderedDict(a=1, b=[1.5]))
 
 
 def test_unsupported_falls_back_to_json_errors():
@@ -72,23 +77,23 @@ def test_float32_vectors_use_float32_digits():
         v = (rng.standard_normal(512) * scale).astype(np.float32)
         v[:6] = [0.0, -0.0, 1.0, -2.5, 1e-45, 123456790000000.0]
         got = fastjson.dumps({"e": Float32List(v.astype(np.float64).tolist()), "k": 1})
-        want = json.dumps({"e": [float(str(np.float32(x))) for x in v], "k": 1})
+        want = jdumps({"e": [float(str(np.float32(x))) for x in v], "k": 1})
         assert got == want
         assert np.array_equal(np.array(json.loads(got)["e"], dtype=np.float32), v)
     rows = f32_rows(np.ones((2, 3), dtype=np.float32))
     assert [type(r) for r in rows] == [Float32List, Float32List] and rows[0] == [1.0, 1.0, 1.0]
     # anything but floats inside: the generic encoder, same bytes as json.dumps
     mixed = Float32List([1, 0.5, None])
-    assert fastjson.dumps(mixed) == json.dumps(mixed)
+    assert fastjson.dumps(mixed) == jdumps(mixed)
     # plain lists keep the double digits
     x = float(np.float32(0.1))
-    assert fastjson.dumps([x]) == json.dumps([x]) and fastjson.dumps(Float32List([x])) == "[0.1]"
+    assert fastjson.dumps([x]) == jdumps([x]) and fastjson.dumps(Float32List([x])) == "[0.1]"
     # user / EL code stored a double in a Float32List: no silent float32 rounding
     row = f32_rows(np.full((1, 4), 0.5, dtype=np.float32))[0]
     row[1] = 0.1                                    # not a float32 value
     row.append(1 / 3)
-    assert fastjson.dumps(row) == json.dumps(row) == "[0.5, 0.1, 0.5, 0.5, 0.3333333333333333]"
-    assert fastjson.dumps(Float32List([float("nan"), 2.0])) == json.dumps([float("nan"), 2.0])
+    assert fastjson.dumps(row) == jdumps(row) == "[0.5,0.1,0.5,0.5,0.3333333333333333]"
+    assert fastjson.dumps(Float32List([float("nan"), 2.0])) == jdumps([float("nan"), 2.0])
 
 
 def test_f32_matrix_matches_numpy():

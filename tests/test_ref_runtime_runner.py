@@ -335,6 +335,22 @@ def test_async_composite_failure_and_dead_letter(streaming, retries):
         r.wait_any_order(tin + "-deadletter", dlq)
 
 
+@pytest.mark.parametrize("content", ["fail-this-message-in-the-beginning", "fail-this-message-in-the-middle",
+                                     "fail-this-message-in-the-end"])
+@pytest.mark.parametrize("retries", [0, 1, 2])
+def test_async_composite_with_fail(content, retries):
+    """AsyncProcessingIT.testCompositeMultiStepProcessMultiThreadOutOfOrderWithFail: with
+    on-failure: fail, the message that fails at the beginning, middle or end of the async
+    composite stops the agent with the injected failure as cause (every retry count)."""
+    tin, tout = uniq("input-topic"), uniq("output-topic")
+    files = _async_files(tin, tout, FAILING_COMPOSITE, f"errors:\n   on-failure: fail\n   retries: {retries}\n")
+    with Run("memory", None, files) as r:
+        r.produce(tin, content)
+        err = r.wait_failure()
+        assert isinstance(err, PermanentFailureException)
+        assert isinstance(err.__cause__, InjectedFailure), repr(err.__cause__)
+
+
 # ---------------------------------------------------------------- state/StatefulAgentsTest.java
 def test_single_stateful_agent(streaming, tmp_path):
     """StatefulAgentsTest.testSingleStatefulAgent: the agent's disk state survives a

@@ -49,7 +49,7 @@ def test_roundtrip_types_headers_and_reader_positions(logname):
         got += res.records
         tok = res.offset
     by_key = {r.key(): r for r in got}
-    assert by_key["k0"].value() == '{"a": 1, "b": [1, 2]}'  # maps are JSON-encoded like Kafka
+    assert by_key["k0"].value() == '{"a":1,"b":[1,2]}'  # maps are JSON-encoded as on Kafka (compact)
     assert by_key["k2"].value() == b"\x00\x01" and by_key["k3"].value() == 42 and by_key["k5"].value() is None
     assert by_key["k1"].header_value("n") == 7
     # resume from the returned absolute position: only new records
