@@ -97,6 +97,8 @@ def main():
                 variants["skinny"] = lambda i: h.skinny_gemm_silu(out, x, ws[i])
                 variants["dgemm_s1"] = lambda i: h.decode_gemm_silu(out, x, ws[i], wsp, tickets, err, 1)
                 variants["dgemm_s2"] = lambda i: h.decode_gemm_silu(out, x, ws[i], wsp, tickets, err, 2)
+                # the prefill 256x256 ping-pong kernel (ops.gemm_prefill) on the decode shape
+                variants["pgemm"] = lambda i: h.gemm_prefill(out, x, ws[i], True, -1)
                 check = lambda: out.float()  # noqa: E731
             elif name in ("o", "down"):
                 out = torch.empty(M, N, device=dev, dtype=bf)
@@ -110,6 +112,10 @@ def main():
                     out.copy_(o)
                 variants["hipblaslt+norm"] = base
                 variants["skinny"] = lambda i: h.skinny_gemm_add_rmsnorm(out, x, ws[i], res, g, 1e-5)
+                def pg_norm(i):
+                    h.gemm_prefill(out, x, ws[i], False, -1)
+                    h.fused_add_rmsnorm(out, res, g, 1e-5)
+                variants["pgemm+norm"] = pg_norm
                 for bn in (64, 128, 256):
                     for sp in (0, 4, 8, 16):
                         variants[f"dgemm_bn{bn}_s{sp}"] = (
@@ -120,6 +126,7 @@ def main():
                 ref = x.float() @ ws[0].float().t()
                 variants["hipblaslt"] = lambda i: out.copy_(F.linear(x, ws[i]))
                 variants["skinny"] = lambda i: h.skinny_gemm(out, x, ws[i])
+                variants["pgemm"] = lambda i: h.gemm_prefill(out, x, ws[i], False, -1)
                 for bn in (64, 128, 256):
                     for sp in (0, 2, 4, 6, 8):
                         variants[f"dgemm_bn{bn}_s{sp}"] = (
