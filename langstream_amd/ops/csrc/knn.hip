@@ -551,9 +551,8 @@ __global__ void __launch_bounds__(NW * 64, 1) knn_filter_q256_kernel(const bf16*
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) f[ks] = __builtin_bit_cast(bf16x8, ld16(st + i * 16 * RB + aoff[ks]));
     };
-    if constexpr (DIM > 384 || NW == 4) {
-      // one fragment set: two of them beside the query fragments exceed 256 VGPRs (DIM > 384,
-      // or 4 waves holding 64 queries each)
+    if constexpr (DIM > 384) {
+      // one fragment set: two of them beside the query fragments exceed 256 VGPRs
       rd(0, fa);
       mm(fa, accA);
       if (pend >= 0) epi(pend, accB);
@@ -569,7 +568,7 @@ __global__ void __launch_bounds__(NW * 64, 1) knn_filter_q256_kernel(const bf16*
       pend = tl0 + 48;
       continue;
     }
-    if constexpr (DIM <= 384 && NW == 8) {
+    if constexpr (DIM <= 384) {
       // instruction-level interleave: the next subtile's fragment reads ride between this
       // subtile's MFMAs (per k-step one ds_read, QGW MFMAs), so a wave is never in an
       // all-read or all-MFMA phase (sched_group_barrier, one sync group).  Q = 2048: 1.585
@@ -684,14 +683,6 @@ void launch_q256(int abl, dim3 grid, hipStream_t stream, const bf16* X, int64_t 
       default:
         break;
     }
-  }
-  // LS_KNN_NW=4: 4 waves of 64 queries each (twice the MFMAs per LDS fragment read, one
-  // wave per SIMD) instead of 8 waves of 32
-  static const int nw = getenv("LS_KNN_NW") ? atoi(getenv("LS_KNN_NW")) : 8;
-  if (nw == 4) {
-    knn_filter_q256_kernel<DD, MM, 4><<<grid, 256, 0, stream>>>(X, N, Q, Qn, ws_s, ws_i, ctrl, cap, row_begin, rpw,
-                                                                nqb, ws_s, G, prio);
-    return;
   }
   knn_filter_q256_kernel<DD, MM, 8><<<grid, 512, 0, stream>>>(X, N, Q, Qn, ws_s, ws_i, ctrl, cap, row_begin, rpw, nqb,
                                                               ws_s, G, prio);
