@@ -120,18 +120,31 @@ def test_s3_source_example_runs_unmodified(tmp_path):
     _s3_source_example(tmp_path, None, 128)
 
 
-@needs_ref
 @pytest.mark.gpu
 def test_s3_source_example_runs_unmodified_on_gpu(tmp_path):
     """The same, on the GPU engines behind the hosted model names: gpt-3.5-turbo ->
-    Llama-3-8B (bf16, HIP kernels, random init), text-embedding-ada-002 -> bge-small-en."""
-    _s3_source_example(tmp_path, {"local-ai": True, "max-model-len": 2048, "max-batch": 16, "kv-fraction": 0.1},
-                       384, timeout=600.0)
+    Llama-3-8B (bf16, HIP kernels, random init), text-embedding-ada-002 -> bge-small-en.
+    Where the reference checkout is absent (the GPU box gets only this repository) the
+    in-tree app of the same shape runs instead (tests/apps/s3_rag: s3-source on the
+    bundled S3 service -> text pipeline -> embeddings -> vector-db-sink on the HerdDB-URL
+    database, and the chatbot over the produce / consume gateways)."""
+    gpu = {"local-ai": True, "max-model-len": 2048, "max-batch": 16, "kv-fraction": 0.1}
+    if os.path.isdir(f"{EX}/applications/s3-source"):
+        _s3_source_example(tmp_path, gpu, 384, timeout=600.0)
+    else:
+        _s3_source_example(tmp_path, gpu, 384, timeout=600.0, app=os.path.join(REPO, "tests", "apps", "s3_rag"),
+                           secrets=os.path.join(REPO, "tests", "apps", "s3_rag_secrets.yaml"))
 
 
-def _s3_source_example(tmp_path, services, dim, timeout=90.0):
+def test_in_tree_s3_rag_app_runs(tmp_path):
+    """tests/apps/s3_rag (the GPU variant's fallback app) on the tiny CPU models."""
+    _s3_source_example(tmp_path, None, 128, app=os.path.join(REPO, "tests", "apps", "s3_rag"),
+                       secrets=os.path.join(REPO, "tests", "apps", "s3_rag_secrets.yaml"))
+
+
+def _s3_source_example(tmp_path, services, dim, timeout=90.0, app=f"{EX}/applications/s3-source", secrets=SECRETS):
     from langstream_amd.agents.storage import S3Client
-    r = _Run(tmp_path, "s3test", f"{EX}/applications/s3-source", services=services, timeout=timeout)
+    r = _Run(tmp_path, "s3test", app, services=services, timeout=timeout, secrets=secrets)
     try:
         assert "Using default instance file that connects to the Kafka broker" in r.output()
         c = S3Client(r.info["s3"], "minioadmin", "minioadmin")
