@@ -341,6 +341,8 @@ class LlamaRunner {
     at::Tensor out = at::empty({T, w.size(0)}, x.options());
     if (pgemm(T, w, false)) {
       gemm_prefill(out, x, w, false, -1);
+    } else if (plib(T, w)) {
+      at::linear_out(out, x, w);
     } else if (dgemm_blocks_ok(w, false) && x.stride(1) == 1) {
       for (int64_t r0 = 0; r0 < T; r0 += kDgemmMaxM) {
         const int64_t n = std::min<int64_t>(kDgemmMaxM, T - r0);
@@ -722,9 +724,16 @@ class LlamaRunner {
   // Prefill-sized steps (T >= LS_PGEMM_MIN_T, default 1024) run all four projections on
   // the 256 x 256-tile ping-pong GEMM (ops/csrc/gemm_prefill.hip), gate_up with SwiGLU in
   // its epilogue (no [T, 2F] round trip).  LS_PGEMM=lib: the library GEMM instead (A/B
-  // switch); LS_PGEMM=route: qkv / o / down by the measured per-M-bucket table of round 3
-  // (ops/pgemm_route_gfx950.csv), gate_up always here.
-  static bool pgemm(int64_t T, const at::Tensor& w, bool silu) {
+  // switch); LS_PGEMM=route: qkv / o / down by the measured per-M-bucket table
+  // (ops/pgemm_route_gfx950.csv, tools/pgemm_route_tune.py) between this kernel and the
+  // library GEMM, gate_up always here.  (Until round 6 a "library" bucket fell through to
+  // the 256-row decode GEMM blocks, so route-mode A/Bs before then measured those.)
+  static bool pgemm(int64_t T, const at::Tensor& w, bool silu) { return prefill_route(T, w, silu) == 1; }
+  // LS_PGEMM=route and the table says the library GEMM for this plain projection's M bucket
+  static bool plib(int64_t T, const at::Tensor& w) { return prefill_route(T, w, false) == 2; }
+  // 0: not a prefill-sized step (decode GEMM blocks / library below), 1: gemm_prefill,
+  // 2: the library GEMM (route mode, where the table measured it faster)
+  static int prefill_route(int64_t T, const at::Tensor& w, bool silu) {
     static const int mode = [] {
       const char* e = getenv("LS_PGEMM");
       if (e == nullptr) return 2;
@@ -737,9 +746,9 @@ class LlamaRunner {
       const char* e = getenv("LS_PGEMM_MIN_T");
       return e ? (int64_t)atoll(e) : (int64_t)1024;
     }();
-    if (mode == 0 || !gemm_prefill_supported(w, silu) || T < min_t) return false;
-    if (silu || mode == 2) return true;
-    return pgemm_route::use_pp(T, w.size(0), w.size(1));
+    if (mode == 0 || !gemm_prefill_supported(w, silu) || T < min_t) return 0;
+    if (silu || mode == 2) return 1;
+    return pgemm_route::use_pp(T, w.size(0), w.size(1)) ? 1 : 2;
   }
   // rows below the prefill threshold: the decode GEMM in 256-row blocks
   bool dgemm_blocks_ok(const at::Tensor& w, bool silu) const {

@@ -38,6 +38,7 @@ def main():
     ap.add_argument("--m-min", type=int, default=1024)
     ap.add_argument("--m-max", type=int, default=16640)
     ap.add_argument("--iters", type=int, default=6)
+    ap.add_argument("--reps", type=int, default=3)
     a = ap.parse_args()
     os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
     dev = "cuda"
@@ -51,8 +52,12 @@ def main():
             for M in range(a.m_min, a.m_max + 1, 256):
                 x = xa[:M]
                 o = out[:M]
-                t_lib = timeit(lambda: torch.matmul(x, w.t(), out=o), a.iters)
-                t_pp = timeit(lambda: ops.gemm_prefill(x, w, out=o), a.iters)
+                # interleaved repeats, median: single timings jitter by up to 40 % at some M
+                libs, pps = [], []
+                for _ in range(a.reps):
+                    libs.append(timeit(lambda: torch.matmul(x, w.t(), out=o), a.iters))
+                    pps.append(timeit(lambda: ops.gemm_prefill(x, w, out=o), a.iters))
+                t_lib, t_pp = sorted(libs)[len(libs) // 2], sorted(pps)[len(pps) // 2]
                 wr.writerow([N, K, M, round(t_lib, 2), round(t_pp, 2)])
                 print(name, M, round(t_lib, 1), round(t_pp, 1), flush=True)
 
