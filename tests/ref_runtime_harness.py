@@ -245,7 +245,8 @@ class FakeHTTP:
     """Stub server for the reference's @WireMockTest cases: ``stub(method, path, body,
     status=200, json_body=..., text=...)`` where ``path`` includes the query string and
     ``body`` (optional) must equal the request body exactly and ``headers`` (optional) must
-    all be present with these values; unmatched requests get 404."""
+    all be present with these values; the latest matching stub answers (``data``: a bytes
+    body, ``status=FakeHTTP.RESET``: the connection is reset); unmatched requests get 404."""
 
     def __init__(self):
         import http.server
@@ -264,12 +265,20 @@ class FakeHTTP:
                 n = int(self.headers.get("Content-Length") or 0)
                 body = self.rfile.read(n).decode() if n else ""
                 outer.requests.append((self.command, self.path, body, dict(self.headers)))
-                for m, path, want, status, ctype, payload, hdrs in outer.stubs:
+                for m, path, want, status, ctype, payload, hdrs, rhdrs in outer.stubs:
                     if m == self.command and path == self.path and (want is None or want == body) and \
                             all(self.headers.get(k) == v for k, v in hdrs.items()):
-                        data = payload.encode()
+                        if status == FakeHTTP.RESET:   # WireMock's Fault.CONNECTION_RESET_BY_PEER
+                            import socket
+                            import struct
+                            self.connection.setsockopt(socket.SOL_SOCKET, socket.SO_LINGER, struct.pack("ii", 1, 0))
+                            self.close_connection = True
+                            return
+                        data = payload if isinstance(payload, bytes) else payload.encode()
                         self.send_response(status)
                         self.send_header("Content-Type", ctype)
+                        for k, v in rhdrs.items():
+                            self.send_header(k, v)
                         self.send_header("Content-Length", str(len(data)))
                         self.end_headers()
                         self.wfile.write(data)
@@ -288,12 +297,19 @@ class FakeHTTP:
         self.url = f"http://127.0.0.1:{self.srv.server_address[1]}"
         threading.Thread(target=self.srv.serve_forever, daemon=True).start()
 
-    def stub(self, method, path, body=None, status=200, json_body=None, text=None, ctype=None, headers=None):
+    RESET = -1   # status: reset the connection instead of answering
+
+    def stub(self, method, path, body=None, status=200, json_body=None, text=None, ctype=None, headers=None,
+             data=None, response_headers=None):
         if json_body is not None:
             payload, ct = json.dumps(json_body), "application/json"
+        elif data is not None:
+            payload, ct = bytes(data), "application/octet-stream"
         else:
             payload, ct = text or "", "application/json"
-        self.stubs.append((method, path, body, status, ctype or ct, payload, dict(headers or {})))
+        # the most recent stub for a request wins (as in WireMock)
+        self.stubs.insert(0, (method, path, body, status, ctype or ct, payload, dict(headers or {}),
+                              dict(response_headers or {})))
 
     def reset(self):
         self.stubs.clear()
