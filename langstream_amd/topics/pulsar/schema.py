@@ -30,6 +30,7 @@ from typing import Any, Dict, Optional, Tuple
 import datetime as _dt
 
 from ...api import avro, temporal
+from ...utils import fastjson
 from ...api.types import Float32, Int8, Int16, Int32
 
 TEMPORAL_TYPES = ("DATE", "TIME", "TIMESTAMP", "INSTANT", "LOCAL_DATE", "LOCAL_TIME", "LOCAL_DATE_TIME")
@@ -80,11 +81,11 @@ class PulsarSchema:
         if t in ("BYTES", "NONE"):
             if isinstance(v, (bytes, bytearray)):
                 return bytes(v)
-            return (v if isinstance(v, str) else json.dumps(v)).encode()
+            return (v if isinstance(v, str) else fastjson.dumps(v)).encode()
         if t == "STRING":
             if isinstance(v, (bytes, bytearray)):
                 return bytes(v)
-            return (v if isinstance(v, str) else json.dumps(v)).encode()
+            return (v if isinstance(v, str) else fastjson.dumps(v)).encode()
         if t == "BOOLEAN":
             if isinstance(v, str):
                 v = v.strip().lower() == "true"
@@ -109,7 +110,7 @@ class PulsarSchema:
             if isinstance(v, str):
                 json.loads(v)                      # must be a JSON document already
                 return v.encode()
-            return json.dumps(v).encode()
+            return fastjson.dumps(v).encode()
         if t == "AVRO":
             if isinstance(v, (bytes, bytearray)):
                 return bytes(v)

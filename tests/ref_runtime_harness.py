@@ -144,10 +144,20 @@ register_agent_type(AgentSpec(("mock-service",), ComponentType.SERVICE))
 
 
 # ---------------------------------------------------------------- runs
-def instance_yaml(streaming: str, bootstrap: Optional[str], globals_: Optional[Dict[str, str]] = None,
+def instance_yaml(streaming: str, bootstrap, globals_: Optional[Dict[str, str]] = None,
                   extra_admin: Optional[Dict[str, str]] = None) -> str:
+    """``bootstrap``: the Kafka bootstrap servers; for ``pulsar`` (web url, service url,
+    tenant, namespace); for ``pravega`` the controller URI."""
     g = "".join(f"    {k}: {v}\n" for k, v in (globals_ or {}).items())
-    if streaming == "kafka":
+    if streaming == "pulsar":
+        web, svc, tenant, ns = bootstrap
+        sc = (f"  streamingCluster:\n    type: \"pulsar\"\n    configuration:\n      admin:\n"
+              f"        serviceUrl: \"{web}\"\n      service:\n        serviceUrl: \"{svc}\"\n"
+              f"      default-tenant: \"{tenant}\"\n      default-namespace: \"{ns}\"\n")
+    elif streaming == "pravega":
+        sc = (f"  streamingCluster:\n    type: \"pravega\"\n    configuration:\n      client:\n"
+              f"        controller-uri: \"{bootstrap}\"\n        scope: \"langstream\"\n")
+    elif streaming == "kafka":
         admin = {"bootstrap.servers": bootstrap, **(extra_admin or {})}
         conf = "".join(f"        {k}: \"{v}\"\n" for k, v in admin.items())
         sc = f"  streamingCluster:\n    type: \"kafka\"\n    configuration:\n      admin:\n{conf}"
