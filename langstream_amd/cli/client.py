@@ -66,6 +66,14 @@ class AdminClient:
             return r
         raise last  # type: ignore[misc]
 
+    def raw(self, method: str, path: str, **kw) -> str:
+        """The response body as text (the reference CLI prints some bodies as sent)."""
+        return self._call(method, path, idempotent=method in ("GET", "PUT", "DELETE"), **kw).text
+
+    @staticmethod
+    def _json(r) -> Any:
+        return r.json() if r.content and r.content.strip() else {}
+
     # tenants
     def tenants(self) -> Dict[str, Any]:
         return self._call("GET", "/api/tenants").json()
@@ -75,11 +83,11 @@ class AdminClient:
 
     def tenant_create(self, name: str, max_units: Optional[int] = None) -> Dict[str, Any]:
         """POST: fails with 409 when the tenant exists (CreateTenantCmd.java)."""
-        return self._call("POST", f"/api/tenants/{name}", json={"maxTotalResourceUnits": max_units}).json()
+        return self._json(self._call("POST", f"/api/tenants/{name}", json={"maxTotalResourceUnits": max_units}))
 
     def tenant_update(self, name: str, max_units: Optional[int] = None) -> Dict[str, Any]:
         """PATCH: fails with 404 when the tenant does not exist (UpdateTenantCmd.java)."""
-        return self._call("PATCH", f"/api/tenants/{name}", json={"maxTotalResourceUnits": max_units}).json()
+        return self._json(self._call("PATCH", f"/api/tenants/{name}", json={"maxTotalResourceUnits": max_units}))
 
     def tenant_get(self, name: str) -> Dict[str, Any]:
         return self._call("GET", f"/api/tenants/{name}").json()
@@ -104,15 +112,21 @@ class AdminClient:
         return files
 
     def deploy(self, app_id: str, app: Optional[str], instance: Optional[str] = None, secrets: Optional[str] = None,
-               dry_run: bool = False) -> Dict[str, Any]:
+               dry_run: bool = False, auto_upgrade: bool = False) -> Dict[str, Any]:
+        return self._json(self.deploy_raw(app_id, app, instance, secrets, dry_run, auto_upgrade))
+
+    def deploy_raw(self, app_id, app, instance=None, secrets=None, dry_run=False, auto_upgrade=False):
         return self._call("POST", f"/api/applications/{self.tenant}/{app_id}", idempotent=False,
-                          params={"dry-run": str(dry_run).lower()},
-                          files=self._files(app, instance, secrets)).json()
+                          params={"dry-run": str(dry_run).lower(), "auto-upgrade": str(auto_upgrade).lower()},
+                          files=self._files(app, instance, secrets))
 
     def update(self, app_id: str, app: Optional[str], instance: Optional[str] = None,
-               secrets: Optional[str] = None) -> Dict[str, Any]:
-        return self._call("PATCH", f"/api/applications/{self.tenant}/{app_id}", idempotent=False,
-                          files=self._files(app, instance, secrets)).json()
+               secrets: Optional[str] = None, auto_upgrade: bool = False,
+               force_restart: bool = False) -> Dict[str, Any]:
+        return self._json(self._call("PATCH", f"/api/applications/{self.tenant}/{app_id}", idempotent=False,
+                                     params={"auto-upgrade": str(auto_upgrade).lower(),
+                                             "force-restart": str(force_restart).lower()},
+                                     files=self._files(app, instance, secrets)))
 
     def get(self, app_id: str, stats: bool = False) -> Dict[str, Any]:
         return self._call("GET", f"/api/applications/{self.tenant}/{app_id}",
@@ -125,11 +139,25 @@ class AdminClient:
         self._call("DELETE", f"/api/applications/{self.tenant}/{app_id}", params={"force": str(force).lower()})
 
     def logs(self, app_id: str, follow: bool = False) -> Iterator[Dict[str, Any]]:
+        """The application's log records (NDJSON: timestamp, replica, message)."""
         r = self._call("GET", f"/api/applications/{self.tenant}/{app_id}/logs",
-                       params={"follow": str(follow).lower()}, stream=True)
+                       params={"follow": str(follow).lower(), "format": "json"}, stream=True)
         for line in r.iter_lines():
             if line:
-                yield json.loads(line)
+                rec = json.loads(line)
+                if not rec.get("heartbeat"):
+                    yield rec
+
+    def log_lines(self, app_id: str, fmt: str = "text", filters=None, follow: bool = True) -> Iterator[str]:
+        """GetApplicationLogsCmd: the raw lines in ``text`` or ``json`` format."""
+        params = [("format", fmt), ("follow", str(follow).lower())] + [("filter", f) for f in filters or []]
+        r = self._call("GET", f"/api/applications/{self.tenant}/{app_id}/logs", params=params, stream=True)
+        for line in r.iter_lines(decode_unicode=True):
+            if line is not None:
+                yield line
+
+    def download_response(self, app_id: str):
+        return self._call("GET", f"/api/applications/{self.tenant}/{app_id}/code")
 
     def download(self, app_id: str) -> bytes:
         return self._call("GET", f"/api/applications/{self.tenant}/{app_id}/code").content

@@ -33,33 +33,77 @@ from typing import Any, Dict, List, Optional
 CONFIG = os.path.expanduser(os.environ.get("LANGSTREAM_CLI_CONFIG", "~/.langstream/config.yaml"))
 DEFAULT_PROFILE = {"webServiceUrl": "http://localhost:8090", "apiGatewayUrl": "ws://localhost:8091",
                    "tenant": "default", "token": None}
+DEFAULT_PROFILE_NAME = "default"
+_PROFILE_KEYS = ("webServiceUrl", "apiGatewayUrl", "tenant", "token")
+
+
+class CliError(Exception):
+    """A command failure reported as its message alone, exit code 1 (LangStreamCLI.execute)."""
 
 
 # ---------------------------------------------------------------- profiles
 def load_config() -> Dict[str, Any]:
+    """The CLI config file in the reference's layout (LangStreamCLIConfig): the default
+    profile's keys at the top level, named profiles under ``profiles``, ``currentProfile``.
+    A ``profiles.default`` entry written by earlier versions moves to the top level."""
     import yaml
     if os.path.exists(CONFIG):
         with open(CONFIG) as f:
             c = yaml.safe_load(f) or {}
     else:
         c = {}
-    c.setdefault("profiles", {})
-    c.setdefault("currentProfile", "default")
+    c["profiles"] = dict(c.get("profiles") or {})
+    old = c["profiles"].pop(DEFAULT_PROFILE_NAME, None)
+    if isinstance(old, dict):
+        for k in _PROFILE_KEYS:
+            if c.get(k) is None and old.get(k) is not None:
+                c[k] = old[k]
+    for name, prof in c["profiles"].items():
+        prof["name"] = name
+    c.setdefault("currentProfile", DEFAULT_PROFILE_NAME)
     return c
 
 
 def save_config(c: Dict[str, Any]) -> None:
     import yaml
-    os.makedirs(os.path.dirname(CONFIG), exist_ok=True)
+    os.makedirs(os.path.dirname(CONFIG) or ".", exist_ok=True)
+    out = {k: c.get(k) for k in _PROFILE_KEYS if c.get(k) is not None}
+    out["profiles"] = {n: {k: v for k, v in p.items() if v is not None} for n, p in sorted(c["profiles"].items())}
+    out["currentProfile"] = c.get("currentProfile", DEFAULT_PROFILE_NAME)
     with open(CONFIG, "w") as f:
-        yaml.safe_dump(c, f)
+        yaml.safe_dump(out, f, sort_keys=False)
+
+
+def default_profile(c: Dict[str, Any]) -> Dict[str, Any]:
+    """BaseCmd.getDefaultProfile: the top-level keys with the local defaults filled in."""
+    return {"webServiceUrl": c.get("webServiceUrl") or DEFAULT_PROFILE["webServiceUrl"],
+            "apiGatewayUrl": c.get("apiGatewayUrl") or DEFAULT_PROFILE["apiGatewayUrl"],
+            "tenant": c.get("tenant") or DEFAULT_PROFILE["tenant"], "token": c.get("token"),
+            "name": DEFAULT_PROFILE_NAME}
+
+
+def named_profile(c: Dict[str, Any], name: str) -> Optional[Dict[str, Any]]:
+    if name == DEFAULT_PROFILE_NAME:
+        return default_profile(c)
+    p = c["profiles"].get(name)
+    if p is None:
+        return None
+    return {"webServiceUrl": p.get("webServiceUrl"), "apiGatewayUrl": p.get("apiGatewayUrl"),
+            "tenant": p.get("tenant"), "token": p.get("token"), "name": name}
 
 
 def current_profile(args) -> Dict[str, Any]:
+    """BaseCmd.getCurrentProfile: ``-p`` / ``--profile``, else the current one; the
+    LANGSTREAM_<key> environment variables override it (overrideFromEnv)."""
     c = load_config()
-    name = getattr(args, "profile", None) or c.get("currentProfile", "default")
-    p = dict(DEFAULT_PROFILE)
-    p.update(c["profiles"].get(name) or {})
+    name = getattr(args, "profile", None) or c.get("currentProfile", DEFAULT_PROFILE_NAME)
+    p = named_profile(c, name)
+    if p is None:
+        raise CliError(f"No profile '{name}' defined in configuration")
+    for k in _PROFILE_KEYS:
+        v = os.environ.get(f"LANGSTREAM_{k}")
+        if v is not None:
+            p[k] = v
     if getattr(args, "tenant", None):
         p["tenant"] = args.tenant
     return p
@@ -68,79 +112,146 @@ def current_profile(args) -> Dict[str, Any]:
 def _client(args):
     from .client import AdminClient
     p = current_profile(args)
-    return AdminClient(p["webServiceUrl"], p["tenant"], p.get("token"))
+    if not p.get("webServiceUrl"):
+        raise CliError(f"No webServiceUrl defined for profile '{p.get('name')}'")
+    return AdminClient(p["webServiceUrl"], p.get("tenant"), p.get("token"))
+
+
+def _tenant_client(args):
+    cl = _client(args)
+    if not cl.tenant:
+        raise CliError("Tenant not set. Please set the tenant in the configuration.")
+    return cl
 
 
 def _print(obj, fmt: str = "json") -> None:
-    if fmt == "yaml":
-        import yaml
-        print(yaml.safe_dump(obj, sort_keys=False))
-    else:
-        print(json.dumps(obj, indent=2, default=str))
-
-
-# ---------------------------------------------------------------- apps
-_PROFILE_KEYS = ("webServiceUrl", "apiGatewayUrl", "tenant", "token")
+    from .printer import jackson_json, jackson_yaml
+    print(jackson_yaml(obj) if fmt == "yaml" else jackson_json(obj))
 
 
 def _validate_profile(p: Dict[str, Any]) -> None:
     """BaseProfileCmd.validateProfile."""
     if not str(p.get("webServiceUrl") or "").strip():
-        raise ValueError("webServiceUrl is required")
+        raise CliError("webServiceUrl is required")
+
+
+PROFILE_COLUMNS = ("profile", "webServiceUrl", "tenant", "token", "current")
+
+
+def _profile_cell(c: Dict[str, Any]):
+    """ListProfileCmd.rawMapping: the token masked, ``*`` on the current profile."""
+    def value(p, col):
+        if col == "profile":
+            return p.get("name")
+        if col == "token":
+            return None if p.get("token") is None else "********"
+        if col == "current":
+            return "*" if p.get("name") == c.get("currentProfile") else ""
+        return p.get(col)
+    return value
+
+
+def _profile_not_found(c: Dict[str, Any], name: str) -> CliError:
+    names = [DEFAULT_PROFILE_NAME] + list(c["profiles"])
+    return CliError(f"Profile {name} not found, maybe you meant one of these: {', '.join(names)}")
+
+
+def _check_formats(fmt: str, allowed) -> None:
+    if fmt not in allowed:
+        raise CliError(f"Format {fmt} is not allowed. Allowed formats are: {', '.join(allowed)}")
 
 
 def cmd_profiles(args) -> int:
+    """``profiles`` (commands/profiles/*.java): messages, errors and output formats as the
+    reference CLI prints them; the default profile lives in the config's top-level keys."""
+    from .printer import render
+    if getattr(args, "profile", None):
+        raise CliError("Global profile flag is not allowed for profiles commands")
     c = load_config()
-    if args.cmd == "list":
-        _print({"current": c["currentProfile"], "profiles": c["profiles"]})
-    elif args.cmd == "get":
-        _print(c["profiles"].get(args.name) or {})
-    elif args.cmd == "get-current":
-        print(c.get("currentProfile", "default"))
-    elif args.cmd == "import":
-        # ImportProfileCmd.java: exactly one of --file (YAML / JSON) or --inline (JSON, or
-        # base64:<JSON>); an existing profile only with --update (overwritten, not merged)
-        import base64
-        import yaml
-        if (args.file is None) == (args.inline is None):
-            raise ValueError("Either --file or --inline must be specified (and only one)")
-        if args.file is not None:
-            if not os.path.isfile(args.file):
-                raise ValueError(f"File {args.file} does not exist")
-            with open(args.file) as f:
-                prof = yaml.safe_load(f) or {}
+    if args.cmd in ("list", "get"):
+        fmt = args.output or "raw"
+        _check_formats(fmt, ("raw", "json", "yaml"))
+        if args.cmd == "get":
+            prof = named_profile(c, args.name)
+            if prof is None:
+                raise _profile_not_found(c, args.name)
+            body: Any = [prof] if fmt == "raw" else prof
         else:
-            text = args.inline
-            if text.startswith("base64:"):
-                text = base64.b64decode(text[len("base64:"):]).decode()
-            prof = json.loads(text)
-        new = {k: prof.get(k) for k in _PROFILE_KEYS if prof.get(k) is not None}
-        _validate_profile(new)
-        existed = args.name in c["profiles"]
-        if existed and not args.update:
-            raise ValueError(f"Profile {args.name} already exists")
-        c["profiles"][args.name] = new
-        print(f"profile {args.name} {'updated' if existed else 'created'}")
+            profs = [default_profile(c)] + [named_profile(c, n) for n in c["profiles"]]
+            body = profs if fmt == "raw" else {
+                **{k: c.get(k) for k in _PROFILE_KEYS}, "profiles": {n: named_profile(c, n) for n in c["profiles"]},
+                "currentProfile": c.get("currentProfile")}
+        print(render(fmt, body, PROFILE_COLUMNS, _profile_cell(c)))
+    elif args.cmd == "get-current":
+        print(c.get("currentProfile", DEFAULT_PROFILE_NAME))
+    elif args.cmd in ("create", "update", "import"):
+        if args.cmd == "import":
+            # ImportProfileCmd.java: exactly one of --file (YAML / JSON) or --inline (JSON, or
+            # base64:<JSON>); an existing profile only with --update (overwritten, not merged)
+            import base64
+            import yaml
+            if args.file is None and args.inline is None:
+                raise CliError("Either --file or --inline must be specified")
+            if args.file is not None and args.inline is not None:
+                raise CliError("Only one of --file or --inline must be specified")
+            if args.file is not None:
+                if not os.path.isfile(args.file):
+                    raise CliError(f"File {args.file} does not exist")
+                with open(args.file) as f:
+                    src = yaml.safe_load(f) or {}
+            else:
+                text = args.inline
+                if text.startswith("base64:"):
+                    text = base64.b64decode(text[len("base64:"):]).decode()
+                src = json.loads(text)
+            prof = {k: src.get(k) for k in _PROFILE_KEYS}
+            _validate_profile(prof)
+            existed = named_profile(c, args.name) is not None
+            if existed and not args.update:
+                raise CliError(f"Profile {args.name} already exists")
+            created = not existed
+        else:
+            existing = named_profile(c, args.name)
+            if args.cmd == "create" and existing is not None:
+                raise CliError(f"Profile {args.name} already exists")
+            if args.cmd == "update" and existing is None:
+                raise _profile_not_found(c, args.name)
+            prof = dict(existing or {})
+            if args.name == DEFAULT_PROFILE_NAME:
+                # the stored keys, not the filled-in defaults
+                prof = {k: c.get(k) for k in _PROFILE_KEYS}
+            for k, a in (("webServiceUrl", args.web_service_url), ("apiGatewayUrl", args.api_gateway_url),
+                         ("tenant", args.tenant_name), ("token", args.token)):
+                if a is not None:
+                    prof[k] = a
+            _validate_profile(prof)
+            created = args.cmd == "create"
+        if args.name == DEFAULT_PROFILE_NAME:
+            for k in _PROFILE_KEYS:
+                c[k] = prof.get(k)
+        else:
+            c["profiles"][args.name] = {**{k: prof.get(k) for k in _PROFILE_KEYS}, "name": args.name}
+        print(f"profile {args.name} {'created' if created else 'updated'}")
         if args.set_current:
             c["currentProfile"] = args.name
             print(f"profile {args.name} set as current")
         save_config(c)
-    elif args.cmd in ("create", "update"):
-        p = c["profiles"].get(args.name, {}) if args.cmd == "update" else {}
-        for k, a in (("webServiceUrl", args.web_service_url), ("apiGatewayUrl", args.api_gateway_url),
-                     ("tenant", args.tenant_name), ("token", args.token)):
-            if a is not None:
-                p[k] = a
-        c["profiles"][args.name] = p
-        if args.set_current:
-            c["currentProfile"] = args.name
-        save_config(c)
     elif args.cmd == "delete":
+        if args.name == DEFAULT_PROFILE_NAME:
+            raise CliError(f"Profile name {args.name} can't be deleted")
+        if named_profile(c, args.name) is None:
+            raise _profile_not_found(c, args.name)
+        if c.get("currentProfile") == args.name:
+            raise CliError("Cannot delete the current profile")
         c["profiles"].pop(args.name, None)
         save_config(c)
+        print(f"profile {args.name} deleted")
     elif args.cmd == "set-current":
+        if named_profile(c, args.name) is None:
+            raise _profile_not_found(c, args.name)
         c["currentProfile"] = args.name
         save_config(c)
+        print(f"profile {args.name} set as current")
     return 0
 
 
@@ -149,20 +260,19 @@ def cmd_configure(args) -> int:
     if getattr(args, "profile", None):
         raise ValueError("Global profile flag is not allowed here")
     c = load_config()
-    prof = dict(c["profiles"].get("default") or DEFAULT_PROFILE)
-    prof[args.key] = args.value
-    c["profiles"]["default"] = {k: v for k, v in prof.items() if v is not None}
+    c[args.key] = args.value
     save_config(c)
     print(f"profile default updated: {args.key}={args.value}")
     return 0
 
 
 def cmd_tenants(args) -> int:
+    """``tenants`` (commands/tenants/*.java): get / list print the server's body as sent."""
     cl = _client(args)
     if args.cmd == "list":
-        _print(cl.tenants())
+        print(cl.raw("GET", "/api/tenants"))
     elif args.cmd == "get":
-        _print(cl.tenant_get(args.name))
+        print(cl.raw("GET", f"/api/tenants/{args.name}"))
     elif args.cmd == "create":
         cl.tenant_create(args.name, args.max_units)
         print(f"tenant {args.name} created")
@@ -170,9 +280,11 @@ def cmd_tenants(args) -> int:
         cl.tenant_update(args.name, args.max_units)
         print(f"tenant {args.name} updated")
     elif args.cmd == "put":
-        _print(cl.tenant_put(args.name, {"maxTotalResourceUnits": args.max_units} if args.max_units else {}))
+        cl.raw("PUT", f"/api/tenants/{args.name}", data="{}", headers={"Content-Type": "application/json"})
+        print(f"tenant {args.name} created/updated")
     elif args.cmd == "delete":
         cl.tenant_delete(args.name)
+        print(f"Tenant {args.name} deleted")
     return 0
 
 
@@ -202,7 +314,43 @@ def mermaid(app_dir: str, instance: Optional[str] = None, secrets: Optional[str]
     return "\n".join(lines)
 
 
+APP_COLUMNS = ("id", "streaming", "compute", "status", "executors", "replicas")
+
+
+def _path(d, path: str):
+    for part in path.split("."):
+        if not isinstance(d, dict):
+            return None
+        d = d.get(part)
+    return d
+
+
+def _app_cell(app, col):
+    """ListApplicationCmd.getRawFormatValuesSupplier: executors DEPLOYED / all, replicas
+    RUNNING / all (empty when no executor reports replicas)."""
+    if col == "id":
+        return _path(app, "application-id")
+    if col == "streaming":
+        return _path(app, "application.instance.streamingCluster.type")
+    if col == "compute":
+        return _path(app, "application.instance.computeCluster.type")
+    if col == "status":
+        return _path(app, "status.status.status")
+    executors = _path(app, "status.executors") or []
+    if col == "executors":
+        ok = sum(1 for e in executors if str(_path(e, "status.status")) == "DEPLOYED")
+        return f"{ok}/{len(executors)}"
+    if col == "replicas":
+        reps = [r for e in executors for r in (e.get("replicas") or [])]
+        if not reps:
+            return ""
+        return f"{sum(1 for r in reps if str(r.get('status')) == 'RUNNING')}/{len(reps)}"
+    return app.get(col) if isinstance(app, dict) else None
+
+
 def cmd_apps(args) -> int:
+    """``apps`` (commands/applications/*.java): the reference CLI's messages and formats."""
+    from .printer import render
     if args.cmd == "diagram":
         print(mermaid(args.app, args.instance, args.secrets))
         return 0
@@ -211,35 +359,64 @@ def cmd_apps(args) -> int:
         p = current_profile(args)
         return serve_forever(_client(args), args.name, p["apiGatewayUrl"], p["tenant"], args.port,
                              open_browser=not args.no_browser)
-    cl = _client(args)
+    cl = _tenant_client(args)
     if args.cmd in ("deploy", "update"):
         # https:// / GitHub / file:// sources (BaseCmd.checkFileExistsOrDownload)
         args.app, args.instance, args.secrets = _resolve_sources(args)
+        size = len(_zip_size_probe(args.app)) // 1024 if args.app else 0
     if args.cmd == "deploy":
-        _print(cl.deploy(args.name, args.app, args.instance, args.secrets, args.dry_run), args.output)
-    elif args.cmd == "update":
-        _print(cl.update(args.name, args.app, args.instance, args.secrets), args.output)
-    elif args.cmd == "get":
-        desc = cl.get(args.name, stats=True)
-        if args.output == "mermaid":   # AbstractGetApplicationCmd: -o mermaid
-            from .app_ui import mermaid_from_description
-            print(mermaid_from_description(desc), end="")
+        if args.dry_run:
+            print(f"resolving application: {args.name}. Dry run mode is enabled, the application will NOT be "
+                  f"deployed")
         else:
-            _print(desc, args.output)
+            print(f"deploying application: {args.name} ({size} KB)")
+        r = cl.deploy_raw(args.name, args.app, args.instance, args.secrets, args.dry_run, args.auto_upgrade)
+        if args.dry_run:
+            fmt = args.output or "yaml"
+            _check_formats(fmt, ("json", "yaml"))
+            print(render(fmt, r.text))
+        else:
+            print(f"application {args.name} deployed")
+    elif args.cmd == "update":
+        print(f"updating application: {args.name} ({size} KB)")
+        cl.update(args.name, args.app, args.instance, args.secrets, args.auto_upgrade, args.force_restart)
+        print(f"application {args.name} updated")
+    elif args.cmd == "get":
+        fmt = args.output or "raw"
+        _check_formats(fmt, ("raw", "json", "yaml", "mermaid"))
+        body = cl.raw("GET", f"/api/applications/{cl.tenant}/{args.name}", params={"stats": str(args.stats).lower()})
+        if fmt == "mermaid":   # GetApplicationCmd: -o mermaid
+            from .app_ui import mermaid_from_description
+            print(mermaid_from_description(json.loads(body)), end="")
+        else:
+            print(render(fmt, body, APP_COLUMNS, _app_cell))
     elif args.cmd == "list":
-        _print(cl.list(), args.output)
+        fmt = args.output or "raw"
+        _check_formats(fmt, ("raw", "json", "yaml"))
+        print(render(fmt, cl.raw("GET", f"/api/applications/{cl.tenant}"), APP_COLUMNS, _app_cell))
     elif args.cmd == "delete":
         cl.delete(args.name, args.force)
+        print(f"Application '{args.name}' marked for deletion" + (" (forced)" if args.force else ""))
     elif args.cmd == "logs":
-        for rec in cl.logs(args.name, follow=args.follow):
-            print(f"[{rec.get('replica')}] {rec.get('level')} {rec.get('message')}")
+        for line in cl.log_lines(args.name, args.output or "text", args.filter, follow=not args.no_follow):
+            if line != "Heartbeat":
+                print(line, flush=True)
     elif args.cmd == "download":
-        data = cl.download(args.name)
-        out = args.output_file or f"{args.name}.zip"
+        import re
+        r = cl.download_response(args.name)
+        out = args.output_file
+        if out is None:
+            m = re.search(r"""filename=["']?([^"'\r\n]+)["']?""", r.headers.get("Content-Disposition") or "")
+            out = m.group(1) if m else f"{cl.tenant}-{args.name}.zip"
         with open(out, "wb") as f:
-            f.write(data)
-        print(out)
+            f.write(r.content)
+        print(f"Downloaded application code to {os.path.abspath(out)}")
     return 0
+
+
+def _zip_size_probe(app: str) -> bytes:
+    from .client import zip_directory
+    return zip_directory(app) if os.path.isdir(app) else open(app, "rb").read()
 
 
 # ---------------------------------------------------------------- gateway
@@ -576,18 +753,23 @@ def cmd_code_download(args) -> int:
 # ---------------------------------------------------------------- parser
 def build_parser() -> argparse.ArgumentParser:
     ap = argparse.ArgumentParser(prog="langstream", description="LangStream (MI355X-native) command line")
-    ap.add_argument("--profile")
+    ap.add_argument("-p", "--profile")
     ap.add_argument("--tenant")
+    ap.add_argument("--conf", help="CLI configuration file (default ~/.langstream/config.yaml, or "
+                                   "$LANGSTREAM_CLI_CONFIG)")
     ap.add_argument("--disable-local-repositories-cache", action="store_true",
                     help="clone GitHub application sources afresh instead of updating the local cache")
     sub = ap.add_subparsers(dest="group", required=True)
 
     p = sub.add_parser("profiles")
     ps = p.add_subparsers(dest="cmd", required=True)
-    ps.add_parser("list")
+    ps.add_parser("list").add_argument("-o", dest="output", help="raw (default), json or yaml")
     ps.add_parser("get-current")
     for c in ("get", "delete", "set-current"):
-        ps.add_parser(c).add_argument("name")
+        x = ps.add_parser(c)
+        x.add_argument("name")
+        if c == "get":
+            x.add_argument("-o", dest="output", help="raw (default), json or yaml")
     x = ps.add_parser("import", help="import a profile from a file or inline JSON")
     x.add_argument("name")
     x.add_argument("-f", "--file")
@@ -628,20 +810,26 @@ def build_parser() -> argparse.ArgumentParser:
         x.add_argument("-app", "--app", required=(c == "deploy"))
         x.add_argument("-i", "--instance")
         x.add_argument("-s", "--secrets")
-        x.add_argument("--dry-run", action="store_true")
-        x.add_argument("-o", "--output", default="json", choices=["json", "yaml"])
-    for c in ("get",):
-        x = asub.add_parser(c)
-        x.add_argument("name")
-        x.add_argument("-o", "--output", default="json", choices=["json", "yaml", "mermaid"])
+        x.add_argument("--auto-upgrade", action="store_true")
+        if c == "deploy":
+            x.add_argument("--dry-run", action="store_true")
+            x.add_argument("-o", "--output", help="dry-run output: yaml (default) or json")
+        else:
+            x.add_argument("--force-restart", action="store_true")
+    x = asub.add_parser("get")
+    x.add_argument("name")
+    x.add_argument("-o", "--output", help="raw (default), json, yaml or mermaid")
+    x.add_argument("-s", "--stats", action="store_true", help="include agent metrics")
     x = asub.add_parser("list")
-    x.add_argument("-o", "--output", default="json", choices=["json", "yaml"])
+    x.add_argument("-o", "--output", help="raw (default), json or yaml")
     x = asub.add_parser("delete")
     x.add_argument("name")
-    x.add_argument("--force", action="store_true")
+    x.add_argument("-f", "--force", action="store_true")
     x = asub.add_parser("logs")
     x.add_argument("name")
-    x.add_argument("-f", "--follow", action="store_true")
+    x.add_argument("-f", "--filter", action="append", help="only these replicas (repeatable)")
+    x.add_argument("-o", "--output", help="text (default) or json")
+    x.add_argument("--no-follow", action="store_true", help="print the logs so far and exit")
     x = asub.add_parser("download")
     x.add_argument("name")
     x.add_argument("-o", "--output-file")
@@ -885,10 +1073,14 @@ def _picocli_booleans(argv: List[str]) -> List[str]:
 
 def main(argv: Optional[List[str]] = None) -> int:
     args = build_parser().parse_args(_picocli_booleans(list(sys.argv[1:] if argv is None else argv)))
+    global CONFIG
+    if getattr(args, "conf", None):
+        CONFIG = os.path.abspath(os.path.expanduser(args.conf))
     try:
         return args.fn(args) or 0
     except Exception as e:  # noqa: BLE001
-        print(f"error: {e}", file=sys.stderr)
+        # the message alone, exit code 1 (LangStreamCLI.execute)
+        print(str(e) or type(e).__name__, file=sys.stderr)
         return 1
 
 

@@ -288,6 +288,16 @@ class ControlPlane:
         if sa.runner is not None and stats:
             agents = sa.runner.agent_info()
         out["status"]["agents"] = agents
+        # ApplicationStatus.executors (the CLI's EXECUTORS / REPLICAS columns): one executor
+        # per planned agent, its replicas RUNNING while this control plane runs them
+        running = sa.runner is not None and sa.status == "DEPLOYED"
+        execs = []
+        for node in plan.agents.values():
+            n = max(1, int(getattr(node.resources, "parallelism", 1) or 1))
+            execs.append({"id": node.id, "status": {"status": sa.status, "reason": None},
+                          "replicas": [{"id": f"{app_id}-{node.id}-{r}", "status": "RUNNING" if running else "UNKNOWN",
+                                        "reason": None} for r in range(n)]})
+        out["status"]["executors"] = execs
         if getattr(sa, "manifests", None):
             out["manifests"] = sa.manifests
         return out
@@ -493,12 +503,27 @@ class WebServiceServer:
         if self.cp.store.get(t, i) is None:
             raise KeyError(f"application {i} not found")
         buf = self.cp.logs(t, i)
-        resp = web.StreamResponse(headers={"Content-Type": "application/x-ndjson"})
+        # ApplicationResource.getApplicationLogs: format=text (default: "[replica] message"
+        # lines, coloured per replica) or json (NDJSON {timestamp, replica, message}); filter=
+        # replica names (repeatable); follow=false (this server's extension) ends the stream
+        fmt = request.query.get("format", "text")
+        wanted = set(request.query.getall("filter", []))
+        resp = web.StreamResponse(headers={"Content-Type": "application/x-ndjson" if fmt == "json"
+                                           else "text/plain"})
         await resp.prepare(request)
         if buf is None:
             await resp.write_eof()
             return resp
         follow = request.query.get("follow", "true") != "false"
+        colors = ("32", "33", "34", "35", "36", "37", "38")
+
+        def line(r) -> str:
+            if fmt == "json":
+                return json.dumps({"timestamp": r["timestamp"], "replica": r["replica"], "message": r["message"]},
+                                  separators=(",", ":"), ensure_ascii=False) + "\n"
+            digits = "".join(ch for ch in str(r["replica"]).rsplit("-", 1)[-1] if ch.isdigit())
+            color = colors[(int(digits) if digits else 0) % len(colors)]
+            return f"\x1b[{color}m[{r['replica']}] {r['message']}\x1b[0m\n"
         last = 0
         loop = asyncio.get_running_loop()
         while True:
@@ -506,7 +531,9 @@ class WebServiceServer:
                 batch = [r for s, r in buf.records if s > last]
                 last = buf.seq
             for r in batch:
-                await resp.write((json.dumps(r) + "\n").encode())
+                if wanted and r["replica"] not in wanted:
+                    continue
+                await resp.write(line(r).encode())
             if not follow:
                 break
             await loop.run_in_executor(None, buf.wait_new, last, 1.0)
@@ -520,7 +547,8 @@ class WebServiceServer:
         if sa is None or not sa.code_archive_id:
             raise KeyError("code not found")
         data = await self._off(self.cp.code_storage.download_application_code, sa.tenant, sa.code_archive_id)
-        return web.Response(body=data, content_type="application/zip")
+        return web.Response(body=data, content_type="application/zip", headers={
+            "Content-Disposition": f'attachment; filename="{sa.tenant}-{sa.application_id}.zip"'})
 
     async def app_code_info(self, request):
         from aiohttp import web

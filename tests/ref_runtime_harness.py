@@ -273,7 +273,7 @@ class FakeHTTP:
 
             def _do(self):
                 n = int(self.headers.get("Content-Length") or 0)
-                body = self.rfile.read(n).decode() if n else ""
+                body = self.rfile.read(n).decode("latin-1") if n else ""
                 outer.requests.append((self.command, self.path, body, dict(self.headers)))
                 for m, path, want, status, ctype, payload, hdrs, rhdrs in outer.stubs:
                     if m == self.command and path == self.path and (want is None or want == body) and \
@@ -299,7 +299,7 @@ class FakeHTTP:
                 self.end_headers()
                 self.wfile.write(data)
 
-            do_GET = do_POST = do_PUT = do_DELETE = _do
+            do_GET = do_POST = do_PUT = do_PATCH = do_DELETE = _do
 
         class S(socketserver.ThreadingMixIn, http.server.HTTPServer):
             daemon_threads = True

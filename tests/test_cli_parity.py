@@ -36,9 +36,9 @@ def test_configure_sets_default_profile_keys(cfg, capsys):
     assert cli_main(["configure", "webServiceUrl", "http://cp:8090"]) == 0
     assert cli_main(["configure", "tenant", "acme"]) == 0
     assert cli_main(["configure", "token", "tok"]) == 0
-    d = _load(cfg)["profiles"]["default"]
+    d = _load(cfg)   # the default profile is the config's top-level keys (LangStreamCLIConfig)
     assert d["webServiceUrl"] == "http://cp:8090" and d["tenant"] == "acme" and d["token"] == "tok"
-    assert d["apiGatewayUrl"] == "ws://localhost:8091"            # untouched default
+    assert "apiGatewayUrl" not in d                               # untouched: the local default applies
     assert "profile default updated: tenant=acme" in capsys.readouterr().out
     assert cli_main(["--profile", "p1", "configure", "tenant", "x"]) == 1   # global profile flag refused
     with pytest.raises(SystemExit):
@@ -51,11 +51,11 @@ def test_profiles_import_and_get_current(cfg, tmp_path, capsys):
     assert cli_main(["profiles", "import", "pa", "--file", str(f)]) == 0
     assert "profile pa created" in capsys.readouterr().out
     assert _load(cfg)["profiles"]["pa"] == {"webServiceUrl": "http://a:1", "apiGatewayUrl": "ws://a:2",
-                                            "tenant": "ta", "token": "t"}
+                                            "tenant": "ta", "token": "t", "name": "pa"}
     # an existing profile needs --update (overwritten, not merged)
     assert cli_main(["profiles", "import", "pa", "-i", '{"webServiceUrl": "http://b:1"}']) == 1
     assert cli_main(["profiles", "import", "pa", "-u", "-i", '{"webServiceUrl": "http://b:1"}']) == 0
-    assert _load(cfg)["profiles"]["pa"] == {"webServiceUrl": "http://b:1"}
+    assert _load(cfg)["profiles"]["pa"] == {"webServiceUrl": "http://b:1", "name": "pa"}
     inline = "base64:" + base64.b64encode(json.dumps({"webServiceUrl": "http://c:1", "tenant": "tc"}).encode()).decode()
     assert cli_main(["profiles", "import", "pc", "--inline", inline, "--set-current"]) == 0
     assert _load(cfg)["profiles"]["pc"]["tenant"] == "tc" and _load(cfg)["currentProfile"] == "pc"

@@ -139,9 +139,10 @@ def test_cli_profiles_and_diagram(tmp_path, app_dir, monkeypatch, capsys):
     monkeypatch.setattr("langstream_amd.cli.main.CONFIG", str(tmp_path / "cfg.yaml"))
     assert cli_main(["profiles", "create", "p1", "--web-service-url", "http://x:1", "--tenant", "tt",
                      "--set-current"]) == 0
-    assert cli_main(["profiles", "list"]) == 0
+    capsys.readouterr()
+    assert cli_main(["profiles", "list", "-o", "json"]) == 0     # ListProfileCmd: the whole config
     out = json.loads(capsys.readouterr().out)
-    assert out["current"] == "p1" and out["profiles"]["p1"]["tenant"] == "tt"
+    assert out["currentProfile"] == "p1" and out["profiles"]["p1"]["tenant"] == "tt"
     assert cli_main(["apps", "diagram", "-app", app_dir]) == 0
     assert "flowchart" in capsys.readouterr().out
 
