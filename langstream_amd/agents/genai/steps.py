@@ -244,6 +244,24 @@ def _struct_value(v):
     return v
 
 
+def compute_field_scope(scoped: str):
+    """(name, scope) of a compute field (``ComputeField.java:96-121``): ``key`` / ``value``
+    are the primitive scope, ``key.x`` / ``value.x`` a struct field, ``properties.x`` a
+    header property, ``destinationTopic`` / ``messageKey`` (and this runtime's
+    ``topicName``) a header."""
+    if scoped in ("key", "value"):
+        return scoped, "primitive"
+    if scoped.startswith(("key.", "value.")):
+        scope, name = scoped.split(".", 1)
+        return name, scope
+    if scoped.startswith("properties."):
+        return scoped.split(".", 1)[1], "header.properties"
+    if scoped in ("destinationTopic", "messageKey", "topicName"):
+        return scoped, "header"
+    raise ValueError(f"Invalid compute field name: {scoped}. It should be prefixed with 'key.' or 'value.' or "
+                     f"'properties.' or be one of [key, value, destinationTopic, messageKey]")
+
+
 class ComputeStep(Step):
     def __init__(self, cfg):
         super().__init__(cfg)
@@ -255,9 +273,7 @@ class ComputeStep(Step):
             name = f.get("name")
             if not name:
                 raise ValueError("compute field name is required")
-            if not (name in ("value", "key", "destinationTopic", "messageKey", "topicName")
-                    or name.startswith(("value.", "key.", "properties."))):
-                raise ValueError(f"Invalid compute field name {name}")
+            compute_field_scope(name)
             if name in seen:
                 raise ValueError(f"Duplicate compute field name {name}")
             seen.add(name)

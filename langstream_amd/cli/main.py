@@ -363,6 +363,13 @@ def cmd_apps(args) -> int:
     if args.cmd in ("deploy", "update"):
         # https:// / GitHub / file:// sources (BaseCmd.checkFileExistsOrDownload)
         args.app, args.instance, args.secrets = _resolve_sources(args)
+        if args.cmd == "update" and not (args.app or args.instance or args.secrets):
+            raise CliError("no application, instance or secrets file provided")
+        if args.cmd == "deploy" and not (args.app and args.instance):
+            raise CliError("application and instance files are required")
+        if args.app:
+            from .sources import download_dependencies
+            download_dependencies(args.app, print)
         size = len(_zip_size_probe(args.app)) // 1024 if args.app else 0
     if args.cmd == "deploy":
         if args.dry_run:
@@ -500,6 +507,16 @@ def cmd_gateway(args) -> int:
 LOCAL_RUN_PROFILE = "local-docker-run"
 
 
+def _java_dependencies(app_dir: str):
+    import yaml
+    path = os.path.join(app_dir, "configuration.yaml")
+    if not os.path.exists(path):
+        return []
+    with open(path, encoding="utf-8") as f:
+        data = yaml.safe_load(f) or {}
+    return (data.get("configuration") or {}).get("dependencies") or []
+
+
 def _resolve_sources(args):
     """app / instance / secrets through ``BaseCmd.checkFileExistsOrDownload`` (sources.py)."""
     from .sources import as_app_directory, check_file_exists_or_download
@@ -527,6 +544,12 @@ def cmd_run(args) -> int:
     from .client import zip_directory
     dry = args.dry_run
     app_dir, inst_path, sec_path = _resolve_sources(args)
+    # LocalRunApplicationCmd.java:210 fetches configuration.dependencies into java/lib for the
+    # container's JVM; the agents run in this process and no JVM loads them, so the
+    # application directory is left as it is
+    for dep in _java_dependencies(app_dir):
+        print(f"Dependency {dep.get('name')} ({dep.get('url')}): not needed, the agents run without a JVM",
+              flush=True)
     tenant = args.tenant or "default"
     print(f"Tenant: {tenant}\nApplication: {args.name}\nApplication directory: {os.path.abspath(app_dir)}", flush=True)
     print(f"Filter agent: {args.only_agent}" if args.only_agent else "Running all the agents in the application",

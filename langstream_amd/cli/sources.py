@@ -159,3 +159,73 @@ def as_app_directory(path: str) -> str:
             os.path.isdir(os.path.join(dest, entries[0])):
         return os.path.join(dest, entries[0])
     return dest
+
+
+def _sha512_hex(path: str) -> str:
+    import hashlib
+    h = hashlib.sha512()
+    with open(path, "rb") as f:
+        for block in iter(lambda: f.read(1 << 20), b""):
+            h.update(block)
+    return h.hexdigest()
+
+
+def _checksum_ok(path: str, sha512sum: Optional[str], logger: Callable[[str], None]) -> bool:
+    got = _sha512_hex(path)
+    if got != sha512sum:
+        logger(f"Computed checksum: {got}")
+        logger(f"Expected checksum: {sha512sum}")
+    return got == sha512sum
+
+
+def download_dependencies(directory: str, logger: Callable[[str], None] = log,
+                          fetch: Optional[Callable[[str], Tuple[int, bytes]]] = None) -> None:
+    """``configuration.dependencies`` of an application directory (``BaseCmd.downloadDependencies``,
+    BaseCmd.java:502-582): each ``java-library`` goes to ``java/lib/<file name of the url>``;
+    a present file with the right SHA-512 is kept, a corrupted one is replaced, and a
+    download that still does not match is deleted and fails the command.  An unreachable
+    host only logs: no agent of this runtime loads a java library."""
+    import yaml
+    conf = os.path.join(directory, "configuration.yaml")
+    if not os.path.exists(conf):
+        return
+    with open(conf, encoding="utf-8") as f:
+        data = yaml.safe_load(f) or {}
+    deps = (data.get("configuration") or {}).get("dependencies")
+    for dep in deps or []:
+        url, kind, sha = dep.get("url"), dep.get("type"), dep.get("sha512sum")
+        if kind is None:
+            raise RuntimeError("dependency type must be set")
+        if kind != "java-library":
+            raise RuntimeError(f"unsupported dependency type: {kind}")
+        out = os.path.join(directory, "java", "lib")
+        os.makedirs(out, exist_ok=True)
+        target = os.path.join(out, urllib.parse.urlparse(url).path.rsplit("/", 1)[-1])
+        if os.path.isfile(target):
+            if _checksum_ok(target, sha, logger):
+                logger(f"Dependency: {target} at {os.path.abspath(target)}")
+                continue
+            logger("File seems corrupted, deleting it")
+            os.remove(target)
+        logger(f"downloading dependency: {target} to {os.path.abspath(target)}")
+        try:
+            if fetch is None:
+                import requests
+                r = requests.get(url, timeout=300)
+                status, body = r.status_code, r.content
+            else:
+                status, body = fetch(url)
+        except (OSError, IOError) as e:
+            # this runtime has no JVM, so no agent loads a java-library: an unreachable
+            # repository (offline hosts) leaves the jar out instead of failing the command
+            logger(f"dependency not downloaded ({e}); java libraries are not loaded by this runtime")
+            continue
+        if status >= 400:
+            raise IOError(f"Failed to download dependency {url}: HTTP {status}")
+        with open(target, "wb") as f:
+            f.write(body)
+        if not _checksum_ok(target, sha, logger):
+            logger("File still seems corrupted. Please double check the checksum and try again.")
+            os.remove(target)
+            raise IOError(f"File at {url}, seems corrupted")
+        logger("dependency downloaded")

@@ -116,7 +116,9 @@ def resolve_file_references(content: str, base_dir: str, env: Optional[Mapping[s
     if data is None:
         return content
     resolved = _walk(data, lambda fn: read_file_reference(base_dir, fn), env)
-    return yaml.safe_dump(resolved, sort_keys=False, allow_unicode=True, width=1 << 30)
+    # re-serialised as the reference's YAML printer writes it (AppsCmdTest.testDeployWithFilePlaceholders)
+    from ..cli.printer import jackson_yaml
+    return jackson_yaml(resolved) + "\n"
 
 
 def read_yaml_with_references(path: str, env: Optional[Mapping[str, str]] = None) -> str:

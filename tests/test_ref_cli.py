@@ -219,10 +219,29 @@ def _app(tmp_path):
     return str(d), str(inst), str(sec)
 
 
+def _multipart(req):
+    """name -> bytes of each part of a recorded multipart request."""
+    boundary = req[3]["Content-Type"].split("boundary=", 1)[1].encode()
+    out = {}
+    for chunk in req[2].encode("latin-1").split(b"--" + boundary)[1:-1]:
+        head, _, body = chunk[2:].partition(b"\r\n\r\n")
+        name = head.split(b'name="', 1)[1].split(b'"', 1)[0].decode()
+        out[name] = body[:-2]
+    return out
+
+
 def _parts(req):
-    body = req[2]
-    return {n: ("instance: {}" in body if n == "instance" else "secrets: []" in body if n == "secrets" else True)
-            for n in ("app", "instance", "secrets") if f'name="{n}"' in body}
+    """Which parts were sent, and whether instance / secrets carry the files' text."""
+    mp = _multipart(req)
+    return {n: (mp[n] == b"instance: {}" if n == "instance" else mp[n] == b"secrets: []" if n == "secrets" else True)
+            for n in mp}
+
+
+def _zip_names(data):
+    import io
+    import zipfile
+    with zipfile.ZipFile(io.BytesIO(data)) as z:
+        return {n: z.read(n) for n in z.namelist()}
 
 
 @pytest.mark.parametrize("extra,query", [([], "dry-run=false&auto-upgrade=false"),
@@ -260,10 +279,65 @@ def test_apps_update(cli, tmp_path, extra, query):
     assert r.exit_code == 0 and r.err == "" and r.out.endswith("application my-app updated")
     assert _parts(cli.mock.requests[-1]) == {"app": True, "instance": True, "secrets": True}
     if not extra:
-        assert cli.run("apps", "update", "my-app", "-i", inst).exit_code == 0
-        assert _parts(cli.mock.requests[-1]) == {"instance": True}
-        assert cli.run("apps", "update", "my-app", "-s", sec).exit_code == 0
-        assert _parts(cli.mock.requests[-1]) == {"secrets": True}
+        for flags, parts in ((["-i", inst], {"instance"}), (["-s", sec], {"secrets"}),
+                             (["-app", app], {"app"}), (["-app", app, "-i", inst], {"app", "instance"})):
+            assert cli.run("apps", "update", "my-app", *flags).exit_code == 0
+            assert set(_parts(cli.mock.requests[-1])) == parts
+        assert cli.run("apps", "update", "my-app") == (1, "", "no application, instance or secrets file provided")
+
+
+def test_apps_deploy_with_dependencies(cli, tmp_path):
+    """AppsCmdTest.testDeployWithDependencies: a java-library already in java/lib with the
+    right SHA-512 is kept (not downloaded again) and zipped with the application; a
+    corrupted one is replaced by the download."""
+    import hashlib
+    content = b"dep-content"
+    sha = hashlib.sha512(content).hexdigest()
+    assert sha.startswith("e1ebfd0f4e4a624e")      # the reference test's constant
+    cli.mock.stub("GET", "/local/get-dependency.jar", text="dep-content")
+    app, inst, sec = _app(tmp_path)
+    os.makedirs(os.path.join(app, "java", "lib"))
+    with open(os.path.join(app, "configuration.yaml"), "w") as f:
+        f.write(f'configuration:\n  dependencies:\n    - name: "PostGRES JDBC Driver"\n'
+                f'      url: "{cli.url}/local/get-dependency.jar"\n      sha512sum: "{sha}"\n'
+                f'      type: "java-library"\n')
+    jar = os.path.join(app, "java", "lib", "get-dependency.jar")
+    with open(jar, "wb") as f:
+        f.write(content)
+    cli.mock.stub("POST", f"/api/applications/{TENANT}/my-app?dry-run=false&auto-upgrade=false",
+                  text='{ "name": "my-app" }')
+    r = cli.run("apps", "deploy", "my-app", "-s", sec, "-app", app, "-i", inst)
+    assert r.err == "" and r.exit_code == 0
+    assert not any(q[1] == "/local/get-dependency.jar" for q in cli.mock.requests)
+    assert _zip_names(_multipart(cli.mock.requests[-1])["app"])["java/lib/get-dependency.jar"] == content
+    with open(jar, "wb") as f:
+        f.write(b"corrupted")
+    r = cli.run("apps", "deploy", "my-app", "-s", sec, "-app", app, "-i", inst)
+    assert r.err == "" and r.exit_code == 0 and "File seems corrupted, deleting it" in r.out
+    assert "dependency downloaded" in r.out and open(jar, "rb").read() == content
+
+
+def test_apps_deploy_with_file_placeholders(cli, tmp_path):
+    """AppsCmdTest.testDeployWithFilePlaceholders: a ``<file:...>`` reference in the secrets
+    is inlined and the file re-sent as the reference's YAML printer writes it."""
+    app, inst, _ = _app(tmp_path)
+    (tmp_path / "sa.json").write_text('{"client-id":"xxx"}')
+    sec = tmp_path / "secrets-ph.yaml"
+    sec.write_text("secrets:\n     - name: vertex-ai\n       id: vertex-ai\n       data:\n"
+                   "         url: https://us-central1-aiplatform.googleapis.com\n         token: xxx\n"
+                   '         serviceAccountJson: "<file:sa.json>"\n         region: us-central1\n'
+                   "         project: myproject\n")
+    cli.mock.stub("POST", f"/api/applications/{TENANT}/my-app?dry-run=false&auto-upgrade=false",
+                  text='{ "name": "my-app" }')
+    r = cli.run("apps", "deploy", "my-app", "-s", str(sec), "-app", app, "-i", inst)
+    assert r.exit_code == 0 and r.err == ""
+    mp = _multipart(cli.mock.requests[-1])
+    assert mp["instance"] == b"instance: {}"
+    assert mp["secrets"].decode() == (
+        '---\nsecrets:\n- name: "vertex-ai"\n  id: "vertex-ai"\n  data:\n'
+        '    url: "https://us-central1-aiplatform.googleapis.com"\n    token: "xxx"\n'
+        '    serviceAccountJson: "{\\"client-id\\":\\"xxx\\"}"\n    region: "us-central1"\n'
+        '    project: "myproject"\n')
 
 
 def _yaml12_floats(v):
