@@ -353,12 +353,11 @@ def _yaml12_floats(v):
     return v
 
 
-EXPECTED_GET = "/root/reference/langstream-cli/src/test/resources/expected-get.json"
+EXPECTED_GET = os.path.join(os.path.dirname(__file__), "fixtures", "expected-get.json")
 
 
-@pytest.mark.skipif(not os.path.exists(EXPECTED_GET), reason="the reference checkout's expected-get.json is absent")
 def test_apps_get(cli):
-    """AppsCmdTest.testGet on the reference's own fixture (read in place): the raw table,
+    """AppsCmdTest.testGet on the reference's fixture (tests/fixtures/expected-get.json): the raw table,
     JSON re-printed in the reference's layout, YAML, and a mermaid diagram."""
     text = open(EXPECTED_GET).read()
     cli.mock.stub("GET", f"/api/applications/{TENANT}/my-app?stats=false", text=text)

@@ -1505,8 +1505,9 @@ def test_apps_get_mermaid_output(capsys, monkeypatch):
     from langstream_amd.cli.app_ui import mermaid_from_description
     with open(os.path.join(os.path.dirname(__file__), "fixtures", "expected-get.json")) as f:
         desc = _json.load(f)
-    monkeypatch.setattr(cli, "_client", lambda args: SimpleNamespace(get=lambda name, stats=True: desc))
-    assert cli.cmd_apps(SimpleNamespace(cmd="get", name="app", output="mermaid")) in (0, None)
+    monkeypatch.setattr(cli, "_client", lambda args: SimpleNamespace(
+        tenant="t", raw=lambda method, path, **kw: _json.dumps(desc)))
+    assert cli.cmd_apps(SimpleNamespace(cmd="get", name="app", output="mermaid", stats=False)) in (0, None)
     assert capsys.readouterr().out == mermaid_from_description(desc)
 
 
