@@ -96,6 +96,54 @@ def gateway_summary(g) -> Dict[str, Any]:
     return out
 
 
+def _topic_key(td) -> Dict[str, Any]:
+    """What makes two topic definitions the same topic (``TopicDefinition`` equality)."""
+    def sch(x):
+        return None if x is None else (x.type, x.schema, x.name)
+    return {"name": td.name, "creation-mode": td.creation_mode, "deletion-mode": td.deletion_mode,
+            "implicit": td.implicit, "partitions": td.partitions, "key-schema": sch(td.key_schema),
+            "value-schema": sch(td.value_schema), "options": td.options, "config": td.config}
+
+
+def validate_topics_update(existing_plan, new_plan) -> None:
+    """An update may not add, remove, rename or redefine a topic
+    (``ApplicationService.validateTopicsUpdate``, ApplicationService.java:303-336)."""
+    old = {t.name: t.definition for t in existing_plan.topics.values()}
+    new = {t.name: t.definition for t in new_plan.topics.values()}
+    if len(old) != len(new):
+        raise ValueError(f"Detected a change in the topics which is not supported. New topics: {len(new)}. "
+                         f"Existing topics: {len(old)}")
+    for name, td in new.items():
+        if name not in old:
+            raise ValueError(f"Detected a change in the topics which is not supported. Topic {name} is not "
+                             f"present in the existing application. Rename or adding new topics is not supported.")
+        if _topic_key(td) != _topic_key(old[name]):
+            raise ValueError(f"Detected a change in the topics which is not supported. Topic {name} has changed "
+                             f"from: {_topic_key(old[name])} to: {_topic_key(td)}")
+
+
+def validate_agents_update(existing_plan, new_plan) -> None:
+    """An update keeps the same agents with the same type and connections; configuration,
+    names and resources may change (``ApplicationService.validateAgentsUpdate``,
+    ApplicationService.java:232-301)."""
+    old, new = existing_plan.agents, new_plan.agents
+    if len(old) != len(new):
+        raise ValueError(f"Detected a change in the agents which is not supported. New agents: {len(new)}. "
+                         f"Existing agents: {len(old)}")
+    for key, n in new.items():
+        o = old.get(key)
+        if o is None:
+            raise ValueError(f"Detected a change in the agents which is not supported. Agent {key} is not present "
+                             f"in the existing application. Rename or adding new agents is not supported.")
+        for field, a, b in (("type", o.agent_type, n.agent_type), ("type", o.component_type, n.component_type),
+                            ("type", (o.metadata or {}).get("declared-type"), (n.metadata or {}).get("declared-type")),
+                            ("input", o.input.name if o.input else None, n.input.name if n.input else None),
+                            ("output", o.output.name if o.output else None, n.output.name if n.output else None)):
+            if a != b:
+                raise ValueError(f"Detected a change in the agents which is not supported. For agent {n.id} field "
+                                 f"{field} changed from {getattr(a, 'value', a)} to {getattr(b, 'value', b)}")
+
+
 class ControlPlane:
     """Application lifecycle independent of HTTP (also used by the CLI's local mode)."""
 
@@ -182,6 +230,10 @@ class ControlPlane:
         secrets = secrets if secrets is not None else (existing.secrets if existing else None)
         info = build_application_instance(files, instance, secrets)
         plan = ApplicationDeployer().create_implementation(app_id, info.application)
+        if update and existing is not None:
+            old_plan = ApplicationDeployer().create_implementation(app_id, existing.application)
+            validate_topics_update(old_plan, plan)
+            validate_agents_update(old_plan, plan)
         units = self._units(plan)
         limit = self.tenant_limit(tenant)
         if limit and self._tenant_units(tenant, exclude=app_id) + units > limit:
