@@ -22,6 +22,7 @@ from __future__ import annotations
 import base64
 import hashlib
 import json
+import re
 import shutil
 import subprocess
 from typing import Any, Dict, List, Optional
@@ -40,6 +41,43 @@ def _uses_gpu(node: AgentNode) -> bool:
         return any(t in txt for t in ("compute-ai-embeddings", "ai-chat-completions", "ai-text-completions",
                                       "query", "vector"))
     return node.agent_type in GPU_AGENT_TYPES
+
+
+MAX_APPLICATION_ID_LENGTH = 20
+MAX_AGENT_ID_LENGTH = 37
+_RESOURCE_NAME = re.compile(r"^([a-z])[-a-z0-9]+$")
+
+
+def validate_application_id(app_id: str) -> None:
+    """``AppResourcesFactory.validateApplicationId`` (AppResourcesFactory.java:588-606):
+    the id names the Application resource and every agent's."""
+    if len(app_id) <= 1:
+        raise ValueError(f"Application id '{app_id}' is too short. Must be at least 2 characters long.")
+    if not _RESOURCE_NAME.match(app_id):
+        raise ValueError(f"Application id '{app_id}' contains illegal characters. Allowed characters are "
+                         f"alphanumeric and dash.")
+    if len(app_id) > MAX_APPLICATION_ID_LENGTH:
+        raise ValueError(f"Application id '{app_id}' is too long, max length is {MAX_APPLICATION_ID_LENGTH}")
+
+
+def validate_agent_id(agent_id: str, app_id: str) -> None:
+    """``AgentResourcesFactory.validateAgentId`` (AgentResourcesFactory.java:859-873): the
+    custom resource ``<app>-<agent>`` must be a valid resource name."""
+    full = f"{app_id}-{agent_id}"
+    if not _RESOURCE_NAME.match(full):
+        raise ValueError(f"Agent id '{agent_id}' (computed as '{full}') contains illegal characters. Allowed "
+                         f"characters are alphanumeric and dash. To fully control the agent id, you can set the "
+                         f"'id' field.")
+    if len(agent_id) > MAX_AGENT_ID_LENGTH:
+        raise ValueError(f"Agent id '{agent_id}' is too long, max length is {MAX_AGENT_ID_LENGTH}. To fully control "
+                         f"the agent id, you can set the 'id' field.")
+
+
+def validate_execution_plan(plan: ExecutionPlan) -> None:
+    """``KubernetesClusterRuntime.validateExecutionPlan`` (KubernetesClusterRuntime.java:381-391)."""
+    validate_application_id(plan.application_id)
+    for node in plan.agents.values():
+        validate_agent_id(node.id, plan.application_id)
 
 
 def _name(s: str) -> str:

@@ -154,7 +154,7 @@ def parse_pipeline_file(filename: str, content: str, app: Application) -> None:
     auto_id = 1
     for raw in doc.get("pipeline") or []:
         ag = AgentConfiguration(
-            id=raw.get("id"), name=raw.get("name"), type=raw.get("type"),
+            id=None if raw.get("id") is None else str(raw.get("id")), name=raw.get("name"), type=raw.get("type"),
             configuration=dict(raw.get("configuration") or {}),
             resources=(ResourcesSpec.from_dict(raw.get("resources")) or ResourcesSpec()).with_defaults_from(
                 pipeline.resources),

@@ -197,6 +197,10 @@ class Planner:
                 prev: Optional[AgentNode] = None
                 for ac in pipeline.agents:
                     prev = self._build_agent(module, pipeline, ac, plan, prev)
+        inst = application.instance
+        if inst is not None and inst.compute_cluster is not None and inst.compute_cluster.type == "kubernetes":
+            from .k8s import validate_execution_plan
+            validate_execution_plan(plan)
         return plan
 
     # ------------------------------------------------------------------ connections
