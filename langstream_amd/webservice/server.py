@@ -192,6 +192,20 @@ class ControlPlane:
     def _units(self, plan) -> int:
         return sum(int(n.resources.size or 1) * int(n.resources.parallelism or 1) for n in plan.agents.values())
 
+    def check_resource_usage(self, tenant: str, app_id: str, plan,
+                             usage: Optional[Dict[str, int]] = None) -> None:
+        """``ApplicationService.checkResourceUsage`` (ApplicationService.java:98-119): the
+        plan's units (size x parallelism per agent) plus the tenant's other applications'
+        must fit the tenant limit; ``usage`` (application id -> units) defaults to what
+        the stored applications request."""
+        limit = self.tenant_limit(tenant)
+        if limit <= 0:
+            return
+        current = (sum(u for a, u in usage.items() if a != app_id) if usage is not None
+                   else self._tenant_units(tenant, exclude=app_id))
+        if limit < current + self._units(plan):
+            raise PermissionError(f"Not enough resources to deploy application {app_id}")
+
     def _tenant_units(self, tenant: str, exclude: Optional[str] = None) -> int:
         from ..core.deployer import ApplicationDeployer
         tot = 0
@@ -234,11 +248,7 @@ class ControlPlane:
             old_plan = ApplicationDeployer().create_implementation(app_id, existing.application)
             validate_topics_update(old_plan, plan)
             validate_agents_update(old_plan, plan)
-        units = self._units(plan)
-        limit = self.tenant_limit(tenant)
-        if limit and self._tenant_units(tenant, exclude=app_id) + units > limit:
-            raise PermissionError(f"Not enough resources to deploy application {app_id}: tenant limit "
-                                  f"{limit} units")
+        self.check_resource_usage(tenant, app_id, plan)
         if dry_run:
             if code_root is not None:
                 shutil.rmtree(tmp, ignore_errors=True)
