@@ -180,8 +180,11 @@ def mermaid_from_description(desc: Dict[str, Any]) -> str:
 def app_model(client, app_id: str, api_gateway_url: str, tenant: str) -> Dict[str, Any]:
     desc = client.get(app_id)
     plan = desc.get("application") or {}
+    gws = plan.get("gateways") or []
+    if isinstance(gws, dict):   # the reference description: {"gateways": [...]}
+        gws = gws.get("gateways") or []
     return {"remoteBaseUrl": api_gateway_url, "tenant": tenant, "applicationId": app_id,
-            "gateways": plan.get("gateways") or [],
+            "gateways": gws,
             "applicationDefinition": json.dumps(desc, default=str),
             "mermaidDefinition": mermaid_from_description(desc) if "modules" in plan else mermaid_from_plan(plan)}
 

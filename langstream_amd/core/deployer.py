@@ -19,16 +19,64 @@ from .planner import AgentNode, ExecutionPlan, Planner
 log = logging.getLogger(__name__)
 
 
+def referenced_resources(app: Application) -> set:
+    """Ids / names of the resources the application's agents and assets use: any string in
+    an agent's or asset's configuration naming a resource (``datasource``, ``ai-service``,
+    step fields), plus the default AI service of agents that call a model without naming
+    one (the first AI resource, as GenAIToolKitFunctionAgentProvider.java:210-290 picks)."""
+    from .genai import AI_SERVICE_KEYS, AI_STEPS
+    names = {k for k in app.resources} | {r.name for r in app.resources.values() if r.name} | \
+            {r.id for r in app.resources.values() if r.id}
+    used: set = set()
+
+    def walk(v):
+        if isinstance(v, str):
+            if v in names:
+                used.add(v)
+        elif isinstance(v, dict):
+            for x in v.values():
+                walk(x)
+        elif isinstance(v, (list, tuple)):
+            for x in v:
+                walk(x)
+    needs_ai = False
+    for m in app.modules.values():
+        for p in m.pipelines.values():
+            for a in p.agents:
+                cfg = a.configuration or {}
+                walk(cfg)
+                steps = cfg.get("steps") if isinstance(cfg.get("steps"), list) else []
+                kinds = [a.type] + [s.get("type") for s in steps if isinstance(s, dict)]
+                if any(k in AI_STEPS for k in kinds) and "ai-service" not in cfg:
+                    needs_ai = True
+        for asset in m.assets:
+            walk(asset.config)
+    if needs_ai:
+        for k, r in app.resources.items():
+            if r.type in AI_SERVICE_KEYS:
+                used.add(k)
+                break
+    return used
+
+
 class ApplicationDeployer:
     def __init__(self, compute_cluster=None, planner: Optional[Planner] = None):
         self.compute_cluster = compute_cluster
         self.planner = planner or Planner()
 
     def create_implementation(self, application_id: str, application: Application) -> ExecutionPlan:
+        """Resources are validated when an agent or asset uses them (the reference builds a
+        resource's configuration only through ``getResourceImplementation``, called by the
+        agent / asset providers: BasicClusterRuntime.java:150-157); an unused resource only
+        needs a known type."""
+        from .resources import RESOURCE_TYPES, validate_resource
         resolved = resolve_placeholders(application)
-        for r in resolved.resources.values():
-            from .resources import validate_resource
-            validate_resource(r)
+        used = referenced_resources(resolved)
+        for key, r in resolved.resources.items():
+            if key in used or r.id in used or r.name in used:
+                validate_resource(r)
+            elif r.type not in RESOURCE_TYPES:
+                raise ValueError(f"Resource type {r.type} is not supported; known: {sorted(RESOURCE_TYPES)}")
         return self.planner.build_execution_plan(application_id, resolved)
 
     def setup(self, tenant: str, plan: ExecutionPlan) -> None:

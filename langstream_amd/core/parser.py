@@ -313,31 +313,54 @@ def directory_digest(path: str) -> Optional[str]:
 
 # ---------------------------------------------------------------- archetypes
 def build_from_archetype(archetype_dir: str, parameters: Dict[str, Any]) -> ApplicationWithPackageInfo:
-    """An archetype is an app directory plus ``archetype.yaml`` declaring parameters bound
-    to ``globals.*`` or ``secrets.<id>.<key>`` (ModelBuilder.java:78-184)."""
+    files, inst, sec = archetype_application_files(archetype_dir, parameters)
+    return build_application_instance(files, inst, sec, from_archetype=True)
+
+
+def archetype_application_files(archetype_dir: str, parameters: Dict[str, Any]):
+    """(application files, instance.yaml text, secrets.yaml text) of an archetype with its
+    parameters applied.  An archetype is an app directory plus ``archetype.yaml`` declaring parameters bound
+    to ``globals.<path>`` or ``secrets.<id>.<path>`` (``ModelBuilder.java:78-190``): the
+    archetype's own instance.yaml and secrets.yaml (both required) are kept, and each
+    parameter's value is set at its binding path, creating nested maps on the way
+    (``nested-map.key2.key2-1`` replaces one leaf of a map the instance declares)."""
+    import copy
     files = read_app_directory(archetype_dir)
     spec = _load_yaml(files.get("archetype.yaml", "")) or {}
     arche = spec.get("archetype") or {}
-    globals_: Dict[str, Any] = {}
-    secrets: Dict[str, Dict[str, Any]] = {}
+    if "instance.yaml" not in files:
+        raise ValueError("An archetype must always contain an instance.yaml file")
+    if "secrets.yaml" not in files:
+        raise ValueError("An archetype must always contain an secrets.yaml file")
+    instance = (_load_yaml(files.pop("instance.yaml")) or {}).get("instance") or {}
+    secret_list = (_load_yaml(files.pop("secrets.yaml")) or {}).get("secrets") or []
+    globals_: Dict[str, Any] = copy.deepcopy(instance.get("globals") or {})
+    secrets: Dict[str, Any] = {s.get("id"): copy.deepcopy(s.get("data") or {}) for s in secret_list}
     for section in arche.get("sections") or []:
         for p in section.get("parameters") or []:
-            name = p.get("name")
-            binding = p.get("binding")
-            if name is None or binding is None:
+            name, binding = p.get("name"), p.get("binding")
+            if binding is None:
                 continue
-            value = parameters.get(name, p.get("default"))
+            value = parameters[name] if name in parameters else p.get("default")
             if p.get("required") and value is None:
                 raise ValueError(f"Missing required archetype parameter {name}")
-            parts = binding.split(".")
-            if parts[0] == "globals":
-                globals_[".".join(parts[1:])] = value
-            elif parts[0] == "secrets" and len(parts) >= 3:
-                secrets.setdefault(parts[1], {})[".".join(parts[2:])] = value
+            path = binding.split(".")
+            if path[0] == "globals":
+                ctx = globals_
+            elif path[0] == "secrets":
+                ctx = secrets
             else:
-                raise ValueError(f"Invalid archetype binding {binding}")
-    inst = yaml.safe_dump({"instance": {"globals": globals_}})
-    sec = yaml.safe_dump({"secrets": [{"id": k, "data": v} for k, v in secrets.items()]})
-    files.pop("instance.yaml", None)
-    files.pop("secrets.yaml", None)
-    return build_application_instance(files, inst, sec, from_archetype=True)
+                raise ValueError(f"Invalid binding {binding}")
+            for key in path[1:-1]:
+                nxt = ctx.get(key)
+                if not isinstance(nxt, dict):
+                    nxt = ctx[key] = {}
+                ctx = nxt
+            ctx[path[-1]] = value
+    new_instance = {k: v for k, v in instance.items() if k != "globals"}
+    new_instance["globals"] = globals_
+    inst = yaml.safe_dump({"instance": new_instance})
+    sec = yaml.safe_dump({"secrets": [{**{k: v for k, v in s.items() if k != "data"}, "data": secrets.get(s.get("id"))}
+                                      for s in secret_list]})
+    files.pop("archetype.yaml", None)
+    return files, inst, sec

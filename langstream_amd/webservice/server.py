@@ -45,7 +45,7 @@ import time
 import zipfile
 from typing import Any, Dict, List, Optional
 
-from ..core.parser import build_application_instance, build_from_archetype, directory_digest, read_app_directory
+from ..core.parser import build_application_instance, archetype_application_files, directory_digest, read_app_directory
 from ..core.store import ApplicationStore, InMemoryApplicationStore, StoredApplication
 
 log = logging.getLogger(__name__)
@@ -94,6 +94,71 @@ def gateway_summary(g) -> Dict[str, Any]:
     if g.events_topic:
         out["events-topic"] = g.events_topic
     return out
+
+
+def _kv_list(items):
+    if items is None:
+        return None
+    return [{"key": h.key, "value": h.value, "valueFromParameters": h.value_from_parameters,
+             "valueFromAuthentication": h.value_from_authentication} for h in items]
+
+
+def application_definition(app) -> Dict[str, Any]:
+    """The application as the reference's description carries it
+    (``ApplicationDescription.ApplicationDefinition``, ApplicationDescription.java:65-110):
+    resources by id, modules with their topics and pipelines (agents with their
+    connections, configuration as declared), gateways and the instance.  Placeholders stay
+    as written; a dry run passes the resolved application."""
+    def res(r):
+        return None if r is None else {"parallelism": r.parallelism, "size": r.size}
+
+    def err(e):
+        return None if e is None else {"retries": e.retries, "on-failure": e.on_failure}
+
+    def conn(c):
+        return None if c is None else {"connectionType": c.connection_type, "definition": c.definition,
+                                       "enableDeadletterQueue": bool(c.enable_dead_letter_queue)}
+
+    def sch(x):
+        return None if x is None else {"type": x.type, "schema": x.schema, "name": x.name}
+
+    modules = []
+    for m in app.modules.values():
+        md: Dict[str, Any] = {"id": m.id}
+        if m.pipelines:
+            md["pipelines"] = [{
+                "id": p.id, "module": p.module, "name": p.name, "resources": res(p.resources),
+                "errors": err(p.errors),
+                "agents": [{"id": a.id, "name": a.name, "type": a.type, "input": conn(a.input),
+                            "output": conn(a.output), "configuration": a.configuration,
+                            "resources": res(a.resources), "errors": err(a.errors)} for a in p.agents]}
+                for p in m.pipelines.values()]
+        if m.topics:
+            md["topics"] = [{"name": t.name, "config": t.config or None, "options": t.options or None,
+                             "keySchema": sch(t.key_schema), "valueSchema": sch(t.value_schema),
+                             "partitions": t.partitions, "implicit": t.implicit, "creation-mode": t.creation_mode}
+                            for t in m.topics.values()]
+        modules.append(md)
+    gws = []
+    for g in app.gateways or []:
+        d = gateway_summary(g)
+        d["produceOptions"] = None if g.produce_options is None else {"headers": _kv_list(g.produce_options)}
+        d["consumeOptions"] = None if g.consume_options is None else {
+            "filters": {"headers": _kv_list(g.consume_options)}}
+        gws.append(d)
+    inst = app.instance
+    return {
+        "resources": {k: {"id": r.id, "name": r.name, "type": r.type, "configuration": r.configuration}
+                      for k, r in app.resources.items()},
+        "modules": modules,
+        "gateways": {"gateways": gws} if app.gateways else None,
+        "instance": None if inst is None else {
+            "streamingCluster": None if inst.streaming_cluster is None else {
+                "type": inst.streaming_cluster.type, "configuration": inst.streaming_cluster.configuration},
+            "computeCluster": None if inst.compute_cluster is None else {
+                "type": inst.compute_cluster.type, "configuration": inst.compute_cluster.configuration},
+            "globals": inst.globals or None},
+    }
 
 
 def _topic_key(td) -> Dict[str, Any]:
@@ -233,8 +298,10 @@ class ControlPlane:
         code_root, digest, archive = None, None, None
         if app_zip is not None:
             tmp = tempfile.mkdtemp(prefix="app-", dir=self.code_dir)
-            files = self.unzip(app_zip, tmp)
-            code_root = files.pop("__root__")
+            unzipped = self.unzip(app_zip, tmp)
+            code_root = unzipped.pop("__root__")
+            if files is None:       # an archetype passes its own files beside its code archive
+                files = unzipped
             digest = directory_digest(os.path.join(code_root, "python"))
         elif files is None:
             if existing is None:
@@ -252,7 +319,8 @@ class ControlPlane:
         if dry_run:
             if code_root is not None:
                 shutil.rmtree(tmp, ignore_errors=True)
-            return {"application": plan.to_dict(), "dry-run": True}
+            from ..core.placeholders import resolve_placeholders
+            return application_definition(resolve_placeholders(info.application))
         if update and existing is not None and existing.code_archive_id and digest is not None:
             md = self.code_storage.describe_application_code(tenant, existing.code_archive_id)
             if md is not None and md.py_binaries_digest == digest:
@@ -343,8 +411,7 @@ class ControlPlane:
         from ..core.deployer import ApplicationDeployer
         plan = ApplicationDeployer().create_implementation(app_id, sa.application)
         out = sa.summary()
-        out["application"] = plan.to_dict()
-        out["application"]["gateways"] = [gateway_summary(g) for g in (sa.application.gateways or [])]
+        out["application"] = application_definition(sa.application)
         out["status"]["status"]["reason"] = getattr(sa, "error", None)
         agents = {}
         if sa.runner is not None and stats:
@@ -368,34 +435,55 @@ class ControlPlane:
         return self._logs.get((tenant, app_id))
 
     # ---------------------------------------------------------------- archetypes
-    def list_archetypes(self) -> List[Dict[str, Any]]:
+    def get_archetype(self, archetype: str) -> Optional[Dict[str, Any]]:
+        """``ArchetypeDefinition`` (ArchetypeDefinition.java): the archetype.yaml with every
+        field of the reference's records present (null when unset)."""
         import yaml
+        if not self.archetypes_dir:
+            return None
+        p = os.path.join(self.archetypes_dir, archetype, "archetype.yaml")
+        if not os.path.exists(p):
+            return None
+        with open(p) as f:
+            spec = (yaml.safe_load(f) or {}).get("archetype") or {}
+        sections = [{"title": sec.get("title"), "description": sec.get("description"),
+                     "parameters": [{"default": par.get("default"), "name": par.get("name"),
+                                     "label": par.get("label"), "description": par.get("description"),
+                                     "type": par.get("type"), "subtype": par.get("subtype"),
+                                     "binding": par.get("binding"), "required": bool(par.get("required", False))}
+                                    for par in sec.get("parameters") or []]}
+                    for sec in spec.get("sections") or []]
+        return {"archetype": {"id": spec.get("id", archetype), "title": spec.get("title"),
+                              "labels": spec.get("labels"), "description": spec.get("description"),
+                              "icon": spec.get("icon"), "sections": sections}}
+
+    def list_archetypes(self) -> List[Dict[str, Any]]:
+        """``ArchetypeBasicInfo`` of every archetype: id, title, labels, description, icon."""
         out = []
         if not self.archetypes_dir or not os.path.isdir(self.archetypes_dir):
             return out
         for d in sorted(os.listdir(self.archetypes_dir)):
-            p = os.path.join(self.archetypes_dir, d, "archetype.yaml")
-            if os.path.exists(p):
-                with open(p) as f:
-                    spec = (yaml.safe_load(f) or {}).get("archetype") or {}
-                out.append({"id": d, "title": spec.get("title"), "labels": spec.get("labels"),
-                            "description": spec.get("description"), "sections": spec.get("sections")})
+            a = self.get_archetype(d)
+            if a is not None:
+                a = a["archetype"]
+                out.append({"id": a["id"], "title": a["title"], "labels": a["labels"],
+                            "description": a["description"], "icon": a["icon"]})
         return out
 
-    def deploy_archetype(self, tenant: str, archetype: str, app_id: str, params: Dict[str, Any]) -> Dict[str, Any]:
+    def deploy_archetype(self, tenant: str, archetype: str, app_id: str, params: Dict[str, Any],
+                         dry_run: bool = False) -> Dict[str, Any]:
+        """ArchetypeResource.deployApplication: the deployed application's definition
+        (placeholders resolved on a dry run, which deploys nothing)."""
         d = os.path.join(self.archetypes_dir or "", archetype)
         if not os.path.isdir(d):
             raise KeyError(f"archetype {archetype} not found")
-        info = build_from_archetype(d, params)
-        files = read_app_directory(d)
-        files.pop("archetype.yaml", None)
-        import yaml
-        inst = yaml.safe_dump({"instance": {"globals": dict(info.application.instance.globals)
-                                            if info.application.instance else {}}})
-        sec = yaml.safe_dump({"secrets": [{"id": s.id, "data": s.data}
-                                          for s in (info.application.secrets.secrets.values()
-                                                    if info.application.secrets else [])]})
-        return self.deploy(tenant, app_id, None, inst, sec, files=files)
+        files, inst, sec = archetype_application_files(d, params)
+        from ..cli.client import zip_directory   # ArchetypeService.buildArchetypeZip
+        res = self.deploy(tenant, app_id, None if dry_run else zip_directory(d), inst, sec, files=files,
+                          dry_run=dry_run)
+        if dry_run:
+            return res
+        return application_definition(self.store.get(tenant, app_id).application)
 
 
 # ---------------------------------------------------------------- HTTP layer
@@ -631,17 +719,18 @@ class WebServiceServer:
     async def archetype(self, request):
         from aiohttp import web
         self._authorize(request)
-        for a in self.cp.list_archetypes():
-            if a["id"] == request.match_info["id"]:
-                return web.json_response(a)
-        raise KeyError("archetype not found")
+        a = self.cp.get_archetype(request.match_info["id"])
+        if a is None:
+            raise KeyError("archetype not found")
+        return web.json_response(a)
 
     async def archetype_deploy(self, request):
         from aiohttp import web
         self._authorize(request)
         params = await request.json() if request.can_read_body else {}
         res = await self._off(self.cp.deploy_archetype, request.match_info["tenant"], request.match_info["id"],
-                              request.match_info["app"], params or {})
+                              request.match_info["app"], params or {},
+                              request.query.get("dry-run", "false").lower() == "true")
         return web.json_response(res, dumps=lambda o: json.dumps(o, default=str))
 
     def start(self) -> "WebServiceServer":

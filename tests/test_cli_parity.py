@@ -179,8 +179,8 @@ def test_apps_ui_serves_model_page_logs_and_proxies_gateways(control_plane, tmp_
         assert model["applicationId"] == "uiapp" and model["tenant"] == "default"
         assert model["baseUrl"].startswith("ws://") and model["remoteBaseUrl"] == gw.url.replace("http", "ws")
         assert sorted((g["id"], g["type"]) for g in model["gateways"]) == [("in", "produce"), ("out", "consume")]
-        assert "flowchart LR" in model["mermaidDefinition"] and "produce gateway" in model["mermaidDefinition"]
-        assert json.loads(model["applicationDefinition"])["application"]["application-id"] == "uiapp"
+        assert "flowchart LR" in model["mermaidDefinition"] and 'gateway-in[/"in"\\]' in model["mermaidDefinition"]
+        assert json.loads(model["applicationDefinition"])["application-id"] == "uiapp"
 
         async def roundtrip():
             base = model["baseUrl"] + "/v1"

@@ -81,7 +81,7 @@ def test_tenants_and_app_lifecycle(server, app_dir):
     cl.tenant_put("t1")
     assert "t1" in cl.tenants()
     plan = cl.deploy("app", app_dir, dry_run=True)
-    assert plan["dry-run"] and "in-topic" in [t["name"] for t in plan["application"]["topics"]]
+    assert "in-topic" in [t["name"] for m in plan["modules"] for t in m.get("topics") or []]
     assert cl.list() == []
     res = cl.deploy("app", app_dir)
     assert res["status"]["status"]["status"] == "DEPLOYED"
