@@ -522,14 +522,17 @@ class WebServiceServer:
             request["principal"] = None
             policy = route_policy(request.path, request.method)
             if self.auth is not None and policy != "public":
+                # a missing or bad token leaves the request unauthenticated, which the
+                # reference's security chain answers with 403 (TokenAuthFilter.java:66-108,
+                # SecurityConfigurationTest.shouldBeForbiddenIfTokenIsInvalid)
                 h = request.headers.get("Authorization", "")
                 if not h.startswith("Bearer ") or len(h) <= len("Bearer "):
-                    raise web.HTTPUnauthorized(text="Missing token")
+                    raise web.HTTPForbidden(text="Missing token")
                 try:
                     # JWKS / issuer fetches may block: off the event loop
                     name = await self._off(self.auth.authenticate, h[len("Bearer "):])
                 except AuthenticationError as e:
-                    raise web.HTTPUnauthorized(text=str(e))
+                    raise web.HTTPForbidden(text=str(e))
                 principal = Principal(name, self.auth.is_admin(name))
                 if policy == "admin" and not principal.admin:
                     raise web.HTTPForbidden(text="ROLE_ADMIN required")
@@ -554,6 +557,8 @@ class WebServiceServer:
         r.add_get("/api/applications/{tenant}/{id}/logs", self.app_logs)
         r.add_get("/api/applications/{tenant}/{id}/code", self.app_code)
         r.add_get("/api/applications/{tenant}/{id}/code/info", self.app_code_info)
+        r.add_get("/api/applications/{tenant}/{id}/code/{ref}", self.app_code)
+        r.add_get("/api/applications/{tenant}/{id}/code/{ref}/info", self.app_code_info)
         r.add_get("/api/archetypes/{tenant}", self.archetypes)
         r.add_get("/api/archetypes/{tenant}/{id}", self.archetype)
         r.add_post("/api/archetypes/{tenant}/{id}/applications/{app}", self.archetype_deploy)
@@ -694,9 +699,12 @@ class WebServiceServer:
         from aiohttp import web
         self._authorize(request)
         sa = self.cp.store.get(request.match_info["tenant"], request.match_info["id"])
-        if sa is None or not sa.code_archive_id:
+        if sa is None:
+            raise KeyError("application not found")
+        ref = request.match_info.get("ref") or sa.code_archive_id   # /code/{codeArchiveReference}
+        if not ref or ref.startswith(".") or "/" in ref or "\\" in ref:
             raise KeyError("code not found")
-        data = await self._off(self.cp.code_storage.download_application_code, sa.tenant, sa.code_archive_id)
+        data = await self._off(self.cp.code_storage.download_application_code, sa.tenant, ref)
         return web.Response(body=data, content_type="application/zip", headers={
             "Content-Disposition": f'attachment; filename="{sa.tenant}-{sa.application_id}.zip"'})
 
@@ -706,9 +714,9 @@ class WebServiceServer:
         sa = self.cp.store.get(request.match_info["tenant"], request.match_info["id"])
         if sa is None:
             raise KeyError("application not found")
-        md = self.cp.code_storage.describe_application_code(sa.tenant, sa.code_archive_id) \
-            if sa.code_archive_id else None
-        return web.json_response({"code-archive-id": sa.code_archive_id,
+        ref = request.match_info.get("ref") or sa.code_archive_id
+        md = self.cp.code_storage.describe_application_code(sa.tenant, ref) if ref else None
+        return web.json_response({"code-archive-id": ref,
                                   "python-digest": md.py_binaries_digest if md else None})
 
     async def archetypes(self, request):

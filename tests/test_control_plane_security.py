@@ -201,8 +201,8 @@ def test_tenants_are_admin_only_and_apps_are_per_tenant(tmp_path):
     try:
         admin = sign({"alg": "HS256"}, {"sub": "super"}, hs=SECRET)
         t1 = sign({"alg": "HS256"}, {"sub": "t1"}, hs=SECRET)
-        assert _get(srv, "/api/tenants").status_code == 401                   # no token
-        assert _get(srv, "/api/tenants", "x.y.z").status_code == 401          # garbage
+        assert _get(srv, "/api/tenants").status_code == 403                   # no token
+        assert _get(srv, "/api/tenants", "x.y.z").status_code == 403          # garbage
         assert _get(srv, "/api/tenants", t1).status_code == 403               # not ROLE_ADMIN
         assert _get(srv, "/api/tenants/t1", t1).status_code == 403
         r = _get(srv, "/api/tenants", admin)
@@ -227,17 +227,17 @@ def test_tenants_are_admin_only_and_apps_are_per_tenant(tmp_path):
         assert _get(srv, "/management/health").status_code == 200
         assert _get(srv, "/api/docs").status_code == 200
         # wrong secret / expired / not yet valid
-        assert _get(srv, "/api/applications/t1", sign({"alg": "HS256"}, {"sub": "t1"}, hs=b"x" * 40)).status_code == 401
+        assert _get(srv, "/api/applications/t1", sign({"alg": "HS256"}, {"sub": "t1"}, hs=b"x" * 40)).status_code == 403
         exp = sign({"alg": "HS256"}, {"sub": "t1", "exp": int(time.time()) - 10}, hs=SECRET)
-        assert _get(srv, "/api/applications/t1", exp).status_code == 401
+        assert _get(srv, "/api/applications/t1", exp).status_code == 403
         nbf = sign({"alg": "HS256"}, {"sub": "t1", "nbf": int(time.time()) + 600}, hs=SECRET)
-        assert _get(srv, "/api/applications/t1", nbf).status_code == 401
+        assert _get(srv, "/api/applications/t1", nbf).status_code == 403
         # a token without the principal claim
-        assert _get(srv, "/api/applications/t1", sign({"alg": "HS256"}, {"x": 1}, hs=SECRET)).status_code == 401
+        assert _get(srv, "/api/applications/t1", sign({"alg": "HS256"}, {"x": 1}, hs=SECRET)).status_code == 403
         # alg confusion: an RS256 token against an HMAC-only configuration
-        assert _get(srv, "/api/applications/t1", sign({"alg": "RS256"}, {"sub": "t1"}, rsa=RSA_A)).status_code == 401
+        assert _get(srv, "/api/applications/t1", sign({"alg": "RS256"}, {"sub": "t1"}, rsa=RSA_A)).status_code == 403
         assert _get(srv, "/api/applications/t1", _b64u(b'{"alg":"none"}') + "." + _b64u(b'{"sub":"t1"}') + ".")\
-            .status_code == 401
+            .status_code == 403
     finally:
         srv.stop()
 
@@ -261,10 +261,10 @@ def test_rsa_public_key_tokens(tmp_path, alg):
     try:
         ok = sign({"alg": alg}, {"sub": "t1"}, rsa=RSA_A)
         assert _get(srv, "/api/applications/t1", ok).status_code == 200
-        assert _get(srv, "/api/applications/t1", sign({"alg": alg}, {"sub": "t1"}, rsa=RSA_B)).status_code == 401
+        assert _get(srv, "/api/applications/t1", sign({"alg": alg}, {"sub": "t1"}, rsa=RSA_B)).status_code == 403
         assert _get(srv, "/api/tenants", sign({"alg": alg}, {"sub": "root"}, rsa=RSA_A)).status_code == 200
         # an HS256 token "signed" with the public key bytes must not pass (key confusion)
-        assert _get(srv, "/api/applications/t1", sign({"alg": "HS256"}, {"sub": "t1"}, hs=pem)).status_code == 401
+        assert _get(srv, "/api/applications/t1", sign({"alg": "HS256"}, {"sub": "t1"}, hs=pem)).status_code == 403
     finally:
         srv.stop()
 
@@ -276,7 +276,7 @@ def test_ec_public_key_es256(tmp_path):
     try:
         assert _get(srv, "/api/applications/t1", sign({"alg": "ES256"}, {"sub": "t1"}, ec=EC_PRIV)).status_code == 200
         bad = sign({"alg": "ES256"}, {"sub": "t1"}, ec=EC_PRIV + 1)
-        assert _get(srv, "/api/applications/t1", bad).status_code == 401
+        assert _get(srv, "/api/applications/t1", bad).status_code == 403
     finally:
         srv.stop()
     with pytest.raises(ValueError):   # an EC key with an RSA public-alg
@@ -295,18 +295,18 @@ def test_jwks_uri_claim_needs_an_allowlisted_host(tmp_path, fake_http):
         assert _get(srv, "/api/applications/t1", tok).status_code == 200
         # kid a is RSA_A's key: a token signed with RSA_B and kid a fails
         tok = sign({"alg": "RS256", "kid": "a"}, {"sub": "t1", "jwks_uri": base + "/jwks.json"}, rsa=RSA_B)
-        assert _get(srv, "/api/applications/t1", tok).status_code == 401
+        assert _get(srv, "/api/applications/t1", tok).status_code == 403
         # keys are filtered by alg == public-alg (RS256): the RS384 entry is never used
         tok = sign({"alg": "RS384", "kid": "b384"}, {"sub": "t1", "jwks_uri": base + "/jwks.json"}, rsa=RSA_B)
-        assert _get(srv, "/api/applications/t1", tok).status_code == 401
+        assert _get(srv, "/api/applications/t1", tok).status_code == 403
         # a host outside the allowlist (localhost != 127.0.0.1) is never fetched
         port = base.rsplit(":", 1)[1]
         tok = sign({"alg": "RS256", "kid": "b"}, {"sub": "t1", "jwks_uri": f"http://localhost:{port}/jwks.json"},
                    rsa=RSA_B)
-        assert _get(srv, "/api/applications/t1", tok).status_code == 401
+        assert _get(srv, "/api/applications/t1", tok).status_code == 403
         evil = sign({"alg": "RS256", "kid": "b"}, {"sub": "t1", "jwks_uri": f"http://127.0.0.1.evil:{port}/j"},
                     rsa=RSA_B)
-        assert _get(srv, "/api/applications/t1", evil).status_code == 401
+        assert _get(srv, "/api/applications/t1", evil).status_code == 403
     finally:
         srv.stop()
     # no allowlist: a jwks_uri claim is untrusted
@@ -327,10 +327,10 @@ def test_audience_and_auth_claim(tmp_path):
         assert _get(srv, "/api/applications/t1", tok({"roles": "t1", "aud": "langstream"})).status_code == 200
         assert _get(srv, "/api/applications/t1", tok({"roles": ["t1", "x"], "aud": ["a", "langstream"]})) \
             .status_code == 200
-        assert _get(srv, "/api/applications/t1", tok({"roles": "t1", "aud": "other"})).status_code == 401
-        assert _get(srv, "/api/applications/t1", tok({"roles": "t1", "aud": ["other"]})).status_code == 401
-        assert _get(srv, "/api/applications/t1", tok({"roles": "t1"})).status_code == 401          # no audience
-        assert _get(srv, "/api/applications/t1", tok({"sub": "t1", "aud": "langstream"})).status_code == 401
+        assert _get(srv, "/api/applications/t1", tok({"roles": "t1", "aud": "other"})).status_code == 403
+        assert _get(srv, "/api/applications/t1", tok({"roles": "t1", "aud": ["other"]})).status_code == 403
+        assert _get(srv, "/api/applications/t1", tok({"roles": "t1"})).status_code == 403          # no audience
+        assert _get(srv, "/api/applications/t1", tok({"sub": "t1", "aud": "langstream"})).status_code == 403
         assert _get(srv, "/api/tenants", tok({"roles": ["ops"], "aud": "langstream"})).status_code == 200
     finally:
         srv.stop()
@@ -361,11 +361,11 @@ def test_kubernetes_service_account_tokens(tmp_path, fake_http):
         # the same claims signed by another key
         forged = sign({"alg": "RS256", "kid": "sa"},
                       {"iss": issuer, "kubernetes.io": {"namespace": "langstream-t2"}}, rsa=RSA_B)
-        assert _get(srv, "/api/applications/t2", forged).status_code == 401
+        assert _get(srv, "/api/applications/t2", forged).status_code == 403
         # a foreign issuer falls back to the secret key: an RS256 token then fails
         other = sign({"alg": "RS256", "kid": "sa"},
                      {"iss": "https://elsewhere", "kubernetes.io": {"namespace": "langstream-t1"}}, rsa=RSA_A)
-        assert _get(srv, "/api/applications/t1", other).status_code == 401
+        assert _get(srv, "/api/applications/t1", other).status_code == 403
         assert ("/k8s/keys", "Bearer pod-sa-token") in fake.seen_auth
     finally:
         srv.stop()
