@@ -1014,6 +1014,10 @@ def build_parser() -> argparse.ArgumentParser:
                          "allow-kubernetes-service-accounts, kubernetes-namespace-prefix")
     cp.add_argument("--admin-roles", default=None, help="comma-separated principals granted ROLE_ADMIN")
     cp.add_argument("--max-units-per-tenant", type=int, default=0)
+    cp.add_argument("--max-units-limit", type=int, default=0,
+                    help="cap on a tenant's maxTotalResourceUnits (0: none)")
+    cp.add_argument("--default-tenant", default="default", help="tenant created at start when missing")
+    cp.add_argument("--no-default-tenant", action="store_true")
     cp.set_defaults(fn=cmd_control_plane)
     return ap
 
@@ -1031,7 +1035,9 @@ def cmd_control_plane(args) -> int:
         store = KubernetesApplicationStore(KubeClient(args.api_server))
     cs = _json_arg(args.code_storage or os.environ.get("LANGSTREAM_CODE_STORAGE"))
     cp = ControlPlane(store, code_dir=args.code_dir, max_units_per_tenant=args.max_units_per_tenant,
-                      code_storage=code_storage_for(cs) if cs else None)
+                      code_storage=code_storage_for(cs) if cs else None,
+                      default_tenant=None if args.no_default_tenant else args.default_tenant,
+                      max_units_limit=args.max_units_limit)
     sec = dict(_json_arg(args.security or os.environ.get("LANGSTREAM_SECURITY_TOKEN")) or {})
     if args.admin_roles:
         sec["admin-roles"] = [r.strip() for r in args.admin_roles.split(",") if r.strip()]

@@ -57,9 +57,9 @@ class ApplicationStore:
 
 
 class InMemoryApplicationStore(ApplicationStore):
-    def __init__(self):
+    def __init__(self, default_tenant: Optional[str] = "default"):
         self._apps: Dict[tuple, StoredApplication] = {}
-        self._tenants: Dict[str, dict] = {"default": {"name": "default"}}
+        self._tenants: Dict[str, dict] = {default_tenant: {"name": default_tenant}} if default_tenant else {}
         self._lock = threading.RLock()
 
     def put(self, app: StoredApplication) -> None:

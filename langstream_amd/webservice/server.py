@@ -213,15 +213,24 @@ class ControlPlane:
     """Application lifecycle independent of HTTP (also used by the CLI's local mode)."""
 
     def __init__(self, store: Optional[ApplicationStore] = None, code_dir: Optional[str] = None,
-                 services=None, max_units_per_tenant: int = 0, code_storage=None):
+                 services=None, max_units_per_tenant: int = 0, code_storage=None,
+                 default_tenant: Optional[str] = "default", max_units_limit: int = 0):
+        """``default_tenant``: created at start when missing (``application.tenants.
+        default-tenant.{create,name}``, LangStreamEventListener.java:35-45); ``max_units_limit``:
+        the largest ``maxTotalResourceUnits`` a tenant may ask for (0 = no cap,
+        ``maxTotalResourceUnitsLimit``); ``max_units_per_tenant``: the limit of a tenant that
+        sets none (``defaultMaxTotalResourceUnits``)."""
         from ..core.codestorage import LocalDiskCodeStorage
-        self.store = store or InMemoryApplicationStore()
+        self.store = store or InMemoryApplicationStore(default_tenant)
         self.code_dir = code_dir or tempfile.mkdtemp(prefix="langstream-code-")
         os.makedirs(self.code_dir, exist_ok=True)
         # archives live in the code storage; code_dir only caches unpacked copies for local runners
         self.code_storage = code_storage or LocalDiskCodeStorage({"path": os.path.join(self.code_dir, "archives")})
         self.services = services
         self.max_units = max_units_per_tenant
+        self.max_units_limit = max_units_limit
+        if default_tenant and self.store.get_tenant(default_tenant) is None:
+            self.store.put_tenant(default_tenant, {})
         self._logs: Dict[tuple, _AppLogBuffer] = {}
         self.archetypes_dir: Optional[str] = None
         self.only_agents: Optional[List[str]] = None   # `run --only-agent`: local runners start only these
@@ -600,6 +609,9 @@ class WebServiceServer:
             units = body.get("maxTotalResourceUnits", body.get("max-total-resource-units"))
             if units is not None and int(units) < 0:
                 raise ValueError("maxTotalResourceUnits must be positive")
+            lim = self.cp.max_units_limit   # GlobalMetadataService.validateMaxTotalResourceUnits
+            if lim > 0 and units is not None and int(units) > lim:
+                raise ValueError(f"Max total resource units limit is {lim}")
             existing = self.cp.store.get_tenant(t)
             if request.method == "POST" and existing is not None:
                 raise FileExistsError("tenant already exists")

@@ -290,7 +290,7 @@ def test_run_dry_run_and_picocli_boolean_syntax(tmp_path):
     out = subprocess.run([sys.executable, "-m", "langstream_amd.cli", "docker", "run", "py", "-app", str(app),
                           "--dry-run", "--start-broker=false"], env=env, capture_output=True, text=True, timeout=120)
     assert out.returncode == 0, out.stderr
-    assert "Start broker: False" in out.stdout and "application:" in out.stdout
+    assert "Start broker: False" in out.stdout and "modules:" in out.stdout
     assert "upper" in out.stdout
 
 
