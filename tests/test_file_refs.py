@@ -76,9 +76,9 @@ def test_reference_example_apps_plan(app, monkeypatch):
         with pytest.raises(ValueError, match=REF_REJECTS[app]):
             info = build_from_directory(d, os.path.join(REF, "instances", "kafka-docker.yaml"),
                                         os.path.join(REF, "secrets", "secrets.yaml"))
-            ApplicationDeployer().create_implementation(app, info.application)
+            ApplicationDeployer().create_implementation("app", info.application)
         return
     info = build_from_directory(d, os.path.join(REF, "instances", "kafka-docker.yaml"),
                                 os.path.join(REF, "secrets", "secrets.yaml"))
-    plan = ApplicationDeployer().create_implementation(app, info.application)
+    plan = ApplicationDeployer().create_implementation("app", info.application)
     assert plan.agents or plan.application.gateways is not None
