@@ -200,10 +200,10 @@ class GatewayService:
         leftover = set(params)
         for p in required:
             if not (params.get(p) or "").strip():
-                raise err(f"missing required parameter {p}. Required parameters: {required}")
+                raise err(f"missing required parameter {p}. Required parameters: [{', '.join(required)}]")
             leftover.discard(p)
         if leftover:
-            raise err(f"unknown parameters: {sorted(leftover)}")
+            raise err(f"unknown parameters: [{', '.join(sorted(leftover))}]")
         for k, v in options.items():
             if gtype in ("consume", "chat") and k == "position":
                 if not v.strip():
@@ -671,6 +671,11 @@ class GatewayServer:
 
 
 def _http_error(e: GatewayError):
+    """An RFC 7807 problem body, as the reference's HTTP gateway answers
+    (GatewayResourceTest.produceJsonAndExpectBadRequest reads ``detail``)."""
     from aiohttp import web
     cls = {401: web.HTTPUnauthorized, 404: web.HTTPNotFound}.get(e.status, web.HTTPBadRequest)
-    return cls(text=str(e))
+    import http
+    code = cls.status_code
+    body = json.dumps({"type": "about:blank", "title": http.HTTPStatus(code).phrase, "status": code, "detail": str(e)})
+    return cls(text=body, content_type="application/problem+json")

@@ -1,0 +1,253 @@
+"""The reference's gateway handler tests, ported (``langstream-api-gateway/src/test/java/ai/
+langstream/apigateway/``: ``websocket/handlers/ProduceConsumeHandlerTest`` and
+``http/GatewayResourceTest``), on the memory streaming cluster.  Each case builds the
+application the Java test builds (one module, the case's topics, the case's gateways) and
+talks to the gateway over WebSockets / HTTP.
+
+Deliberate difference: a WebSocket handshake the gateway refuses (bad parameters) answers
+HTTP 400 with the reason, where the reference's servlet container answers 500."""
+import asyncio
+import json
+import uuid
+
+import pytest
+import requests
+import yaml
+
+from langstream_amd.core.parser import build_application_instance
+from langstream_amd.core.store import InMemoryApplicationStore, StoredApplication
+from langstream_amd.gateway.server import GatewayServer, GatewayService
+from langstream_amd.topics.memory import reset_memlogs
+
+INSTANCE = "instance:\n  streamingCluster:\n    type: memory\n  computeCluster:\n    type: none\n"
+
+
+class GW:
+    def __init__(self, topics, gateways):
+        reset_memlogs()
+        module = {"module": "mod1", "id": "p",
+                  "topics": [{"name": t, "creation-mode": "create-if-not-exists"} for t in topics]}
+        files = {"module.yaml": yaml.safe_dump(module), "gateways.yaml": yaml.safe_dump({"gateways": gateways})}
+        app = build_application_instance(files, INSTANCE, None).application
+        store = InMemoryApplicationStore()
+        store.put(StoredApplication("application1", "tenant1", app, files))
+        self.srv = GatewayServer(GatewayService(store), port=0).start()
+        self.ws = self.srv.url.replace("http", "ws")
+        self.http = self.srv.url
+
+    def close(self):
+        self.srv.stop()
+        reset_memlogs()
+
+
+@pytest.fixture()
+def gw():
+    made = []
+
+    def make(topics, gateways):
+        g = GW(topics, gateways)
+        made.append(g)
+        return g
+    yield make
+    for g in made:
+        g.close()
+
+
+def _topic():
+    return "topic" + uuid.uuid4().hex[:8]
+
+
+def _run(coro):
+    return asyncio.new_event_loop().run_until_complete(coro)
+
+
+async def _produce(s, url, req):
+    ws = await s.ws_connect(url)
+    await ws.send_str(req if isinstance(req, str) else json.dumps(req))
+    resp = json.loads((await ws.receive(timeout=10)).data)
+    await ws.close()
+    return resp
+
+
+class _Collector:
+    def __init__(self):
+        self.msgs = []
+
+    async def start(self, s, url):
+        self.ws = await s.ws_connect(url)
+        self.task = asyncio.ensure_future(self._loop())
+        await asyncio.sleep(0.3)     # the reader is positioned before anything is produced
+        return self
+
+    async def _loop(self):
+        async for m in self.ws:
+            self.msgs.append(json.loads(m.data))
+
+    def records(self):
+        return [(m["record"]["key"], m["record"]["value"], m["record"]["headers"]) for m in self.msgs]
+
+    async def wait(self, n, timeout=10.0):
+        for _ in range(int(timeout / 0.05)):
+            if len(self.msgs) >= n:
+                return
+            await asyncio.sleep(0.05)
+
+    async def close(self):
+        await self.ws.close()
+        self.task.cancel()
+
+
+def test_simple_produce_consume(gw):
+    """ProduceConsumeHandlerTest.testSimpleProduceConsume"""
+    import aiohttp
+    t = _topic()
+    g = gw([t], [{"id": "produce", "type": "produce", "topic": t}, {"id": "consume", "type": "consume", "topic": t}])
+
+    async def go():
+        async with aiohttp.ClientSession() as s:
+            c = await _Collector().start(s, f"{g.ws}/v1/consume/tenant1/application1/consume")
+            r = await _produce(s, f"{g.ws}/v1/produce/tenant1/application1/produce", {"value": "this is a message"})
+            assert r["status"] == "OK"
+            await c.wait(1)
+            assert c.records() == [(None, "this is a message", {})]
+            await c.close()
+    _run(go())
+
+
+@pytest.mark.parametrize("kind", ["consume", "produce"])
+def test_parameters_required(gw, kind):
+    """ProduceConsumeHandlerTest.testParametersRequired"""
+    import aiohttp
+    t = _topic()
+    g = gw([t], [{"id": "gw", "type": kind, "topic": t, "parameters": ["session-id"]}])
+
+    async def go():
+        async with aiohttp.ClientSession() as s:
+            base = f"{g.ws}/v1/{kind}/tenant1/application1/gw"
+            for q in ("", "?param:otherparam=1", "?param:session-id=", "?param:session-id=ok&param:another-non-declared=y"):
+                with pytest.raises(aiohttp.WSServerHandshakeError) as e:
+                    await s.ws_connect(base + q)
+                assert e.value.status == 400
+            for q in ("?param:session-id=1", "?param:session-id=string-value"):
+                ws = await s.ws_connect(base + q)
+                await ws.close()
+    _run(go())
+
+
+def test_filter_out_messages_by_fixed_value(gw):
+    """ProduceConsumeHandlerTest.testFilterOutMessagesByFixedValue"""
+    import aiohttp
+    t = _topic()
+    g = gw([t], [
+        {"id": "produce", "type": "produce", "topic": t, "parameters": ["session-id"],
+         "produce-options": {"headers": [{"key": "header1", "value": "langstream"}]}},
+        {"id": "produce-non-langstream", "type": "produce", "topic": t, "parameters": ["session-id"]},
+        {"id": "consume", "type": "consume", "topic": t, "parameters": ["session-id"],
+         "consume-options": {"filters": {"headers": [{"key": "header1", "value": "langstream"}]}}}])
+
+    async def go():
+        async with aiohttp.ClientSession() as s:
+            base = f"{g.ws}/v1/consume/tenant1/application1/consume?param:session-id="
+            u1 = await _Collector().start(s, base + "user1")
+            u2 = await _Collector().start(s, base + "user2")
+            await _produce(s, f"{g.ws}/v1/produce/tenant1/application1/produce-non-langstream?param:session-id=user1",
+                           {"value": "this is a message non from langstream"})
+            await _produce(s, f"{g.ws}/v1/produce/tenant1/application1/produce?param:session-id=user1",
+                           {"value": "this is a message for everyone"})
+            await u1.wait(1)
+            await u2.wait(1)
+            await asyncio.sleep(0.3)
+            for c in (u1, u2):
+                assert c.records() == [(None, "this is a message for everyone", {"header1": "langstream"})]
+                await c.close()
+    _run(go())
+
+
+def test_produce(gw):
+    """ProduceConsumeHandlerTest.testProduce: reasons for a parameter-level header set by
+    the client, an empty request and bad JSON (the parser's own message follows the
+    prefix: Python's here, Jackson's there)."""
+    import aiohttp
+    t = _topic()
+    g = gw([t], [{"id": "gw", "type": "produce", "topic": t, "parameters": ["session-id"],
+                  "produce-options": {"headers": [{"key": "header1", "value-from-parameters": "session-id"}]}}])
+
+    async def go():
+        async with aiohttp.ClientSession() as s:
+            url = f"{g.ws}/v1/produce/tenant1/application1/gw?param:session-id=s"
+            r = await _produce(s, url, {"value": "hello", "headers": {"header0": "value0", "header2": "value2"}})
+            assert r["status"] == "OK"
+            r = await _produce(s, url, {"value": "hello", "headers": {"header1": "value1"}})
+            assert (r["status"], r["reason"]) == ("BAD_REQUEST", "Header header1 is configured as parameter-level header.")
+            r = await _produce(s, url, "{}")
+            assert (r["status"], r["reason"]) == ("BAD_REQUEST", "Either key or value must be set.")
+            r = await _produce(s, url, "invalid-json")
+            assert r["status"] == "BAD_REQUEST" and r["reason"].startswith("Error while parsing JSON payload: ")
+    _run(go())
+
+
+def test_start_from_offsets(gw):
+    """ProduceConsumeHandlerTest.testStartFromOffsets: ``option:position`` = an offset a
+    consumer was handed (resume after it), ``earliest`` or ``latest``."""
+    import aiohttp
+    t = _topic()
+    g = gw([t], [{"id": "produce", "type": "produce", "topic": t}, {"id": "consume", "type": "consume", "topic": t}])
+
+    async def go():
+        async with aiohttp.ClientSession() as s:
+            cons = f"{g.ws}/v1/consume/tenant1/application1/consume"
+            prod = f"{g.ws}/v1/produce/tenant1/application1/produce"
+            c1 = await _Collector().start(s, cons)
+            await _produce(s, prod, {"value": "msg1"})
+            await c1.wait(1)
+            assert c1.records() == [(None, "msg1", {})]
+            off1 = c1.msgs[0]["offset"]
+            await _produce(s, prod, {"value": "msg2"})
+            c_off = await _Collector().start(s, f"{cons}?option:position={off1}")
+            await c_off.wait(1)
+            assert c_off.records() == [(None, "msg2", {})]
+            c_early = await _Collector().start(s, f"{cons}?option:position=earliest")
+            await c_early.wait(2)
+            assert [v for _, v, _ in c_early.records()] == ["msg1", "msg2"]
+            c_late = await _Collector().start(s, f"{cons}?option:position=latest")
+            await _produce(s, prod, {"value": "msg3"})
+            for c, want in ((c1, ["msg1", "msg2", "msg3"]), (c_off, ["msg2", "msg3"]),
+                            (c_early, ["msg1", "msg2", "msg3"]), (c_late, ["msg3"])):
+                await c.wait(len(want))
+                assert [v for _, v, _ in c.records()] == want
+            for c in (c1, c_off, c_early, c_late):
+                await c.close()
+    _run(go())
+
+
+def test_http_parameters_required(gw):
+    """GatewayResourceTest.testParametersRequired: problem-detail 400s naming the parameter."""
+    t = _topic()
+    g = gw([t], [{"id": "gw", "type": "produce", "topic": t, "parameters": ["session-id"]}])
+    base = f"{g.http}/api/gateways/produce/tenant1/application1/gw"
+    body = '{"value": "my-value"}'
+    hdr = {"Content-Type": "application/json"}
+    for q, msg in (("", "missing required parameter session-id"),
+                   ("?param:otherparam=1", "missing required parameter session-id"),
+                   ("?param:session-id=", "missing required parameter session-id"),
+                   ("?param:session-id=ok&param:another-non-declared=y", "unknown parameters: [another-non-declared]")):
+        r = requests.post(base + q, data=body, headers=hdr, timeout=30)
+        assert r.status_code == 400 and msg in r.json()["detail"]
+    for q in ("?param:session-id=1", "?param:session-id=string-value"):
+        r = requests.post(base + q, data=body, headers=hdr, timeout=30)
+        assert r.status_code == 200 and r.json()["status"] == "OK"
+
+
+def test_http_simple_produce(gw):
+    """GatewayResourceTest.testSimpleProduce: JSON bodies as produce requests, other
+    content types as the record value."""
+    t = _topic()
+    g = gw([t], [{"id": "produce", "type": "produce", "topic": t}])
+    url = f"{g.http}/api/gateways/produce/tenant1/application1/produce"
+    r = requests.post(url, data='{"value": "my-value"}', headers={"Content-Type": "application/json"}, timeout=30)
+    assert r.status_code == 200 and r.json() == {"status": "OK", "reason": None}
+    r = requests.post(url, data='{"key": "my-key", "value": "my-value", "headers": {"header1": "value1"}}',
+                      headers={"Content-Type": "application/json"}, timeout=30)
+    assert r.status_code == 200 and r.json()["status"] == "OK"
+    r = requests.post(url, data="my-value", headers={"Content-Type": "text/plain"}, timeout=30)
+    assert r.status_code == 200 and r.json()["status"] == "OK"
