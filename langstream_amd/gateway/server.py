@@ -298,9 +298,12 @@ class GatewayService:
         if not topic:
             return
         ev = {"category": "Gateway", "type": typ, "timestamp": int(time.time() * 1000),
-              "source": {"tenant": ctx.tenant, "applicationId": ctx.application_id, "gateway": ctx.gateway.id},
+              "source": {"tenant": ctx.tenant, "applicationId": ctx.application_id,
+                         "gateway": {"id": ctx.gateway.id, "type": ctx.gateway.type, "topic": ctx.gateway.topic,
+                                     "parameters": list(ctx.gateway.parameters or []),
+                                     "events-topic": ctx.gateway.events_topic}},
               "data": {"userParameters": ctx.user_parameters, "options": ctx.options,
-                       "httpRequestHeaders": ctx.http_headers}}
+                       "httpRequestHeaders": {k.lower(): v for k, v in (ctx.http_headers or {}).items()}}}
         try:
             self.producer(ctx, topic).write(SimpleRecord.of(None, json.dumps(ev))).result(10)
         except Exception as e:  # noqa: BLE001
@@ -524,8 +527,10 @@ class GatewayServer:
         from aiohttp import WSMsgType
         ctx, ws = await self._prepare(request, "consume")
         loop = asyncio.get_running_loop()
-        await loop.run_in_executor(None, self.service.send_event, ctx, "ClientConnected")
+        # the reader is positioned first: a consumer of its own gateway's events topic sees
+        # its ClientConnected event (ProduceConsumeHandlerTest.testSendEvents)
         pump, task = await self._pump_to_ws(ws, ctx, ctx.gateway.topic, ctx.gateway.consume_options)
+        await loop.run_in_executor(None, self.service.send_event, ctx, "ClientConnected")
         try:
             async for msg in ws:
                 if msg.type in (WSMsgType.ERROR, WSMsgType.CLOSE):

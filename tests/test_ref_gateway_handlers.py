@@ -251,3 +251,33 @@ def test_http_simple_produce(gw):
     assert r.status_code == 200 and r.json()["status"] == "OK"
     r = requests.post(url, data="my-value", headers={"Content-Type": "text/plain"}, timeout=30)
     assert r.status_code == 200 and r.json()["status"] == "OK"
+
+
+def test_send_events(gw):
+    """ProduceConsumeHandlerTest.testSendEvents: ClientConnected / ClientDisconnected
+    events on the gateways' events topic, the consumer's own connection first."""
+    import aiohttp
+    t, ev = _topic(), _topic()
+    g = gw([t, ev], [{"id": "produce", "type": "produce", "topic": t, "parameters": ["p"], "events-topic": ev},
+                     {"id": "consume", "type": "consume", "topic": ev, "parameters": ["p"], "events-topic": ev}])
+
+    async def go():
+        async with aiohttp.ClientSession() as s:
+            c = await _Collector().start(s, f"{g.ws}/v1/consume/tenant1/application1/consume?param:p=consumer")
+            await _produce(s, f"{g.ws}/v1/produce/tenant1/application1/produce?param:p=producer",
+                           {"value": "this is a message"})
+            other = await s.ws_connect(f"{g.ws}/v1/consume/tenant1/application1/consume?param:p=consumer1")
+            await asyncio.sleep(0.3)
+            await other.close()
+            await c.wait(5)
+            await c.close()
+            return [json.loads(m["record"]["value"]) for m in c.msgs]
+    events = _run(go())
+    want = [("ClientConnected", "consume", "consumer"), ("ClientConnected", "produce", "producer"),
+            ("ClientDisconnected", "produce", "producer"), ("ClientConnected", "consume", "consumer1"),
+            ("ClientDisconnected", "consume", "consumer1")]
+    assert [(e["type"], e["source"]["gateway"]["id"], e["data"]["userParameters"]["p"]) for e in events[:5]] == want
+    for e in events[:5]:
+        assert e["category"] == "Gateway" and e["timestamp"] > 0
+        assert (e["source"]["tenant"], e["source"]["applicationId"]) == ("tenant1", "application1")
+        assert e["data"]["options"] == {} and e["data"]["httpRequestHeaders"].get("host")
