@@ -1,6 +1,6 @@
 """The reference's gateway handler tests, ported (``langstream-api-gateway/src/test/java/ai/
 langstream/apigateway/``: ``websocket/handlers/ProduceConsumeHandlerTest`` and
-``http/GatewayResourceTest``), on the memory streaming cluster.  Each case builds the
+``http/GatewayResourceTest``), on the memory streaming cluster and the in-tree Kafka broker.  Each case builds the
 application the Java test builds (one module, the case's topics, the case's gateways) and
 talks to the gateway over WebSockets / HTTP.
 
@@ -14,21 +14,24 @@ import pytest
 import requests
 import yaml
 
+from ref_runtime_harness import instance_yaml
+from langstream_amd.core.deployer import ApplicationDeployer
 from langstream_amd.core.parser import build_application_instance
 from langstream_amd.core.store import InMemoryApplicationStore, StoredApplication
 from langstream_amd.gateway.server import GatewayServer, GatewayService
+from langstream_amd.topics.kafka.broker import KafkaBroker
 from langstream_amd.topics.memory import reset_memlogs
 
-INSTANCE = "instance:\n  streamingCluster:\n    type: memory\n  computeCluster:\n    type: none\n"
-
-
 class GW:
-    def __init__(self, topics, gateways):
+    def __init__(self, topics, gateways, streaming="memory", bootstrap=None):
         reset_memlogs()
         module = {"module": "mod1", "id": "p",
                   "topics": [{"name": t, "creation-mode": "create-if-not-exists"} for t in topics]}
         files = {"module.yaml": yaml.safe_dump(module), "gateways.yaml": yaml.safe_dump({"gateways": gateways})}
-        app = build_application_instance(files, INSTANCE, None).application
+        app = build_application_instance(files, instance_yaml(streaming, bootstrap), None).application
+        # prepareTopicsForTest: the topics exist before any client connects
+        dep = ApplicationDeployer()
+        dep.setup("tenant1", dep.create_implementation("application1", app))
         store = InMemoryApplicationStore()
         store.put(StoredApplication("application1", "tenant1", app, files))
         self.srv = GatewayServer(GatewayService(store), port=0).start()
@@ -40,12 +43,21 @@ class GW:
         reset_memlogs()
 
 
-@pytest.fixture()
-def gw():
+@pytest.fixture(scope="module")
+def kafka():
+    b = KafkaBroker(default_partitions=1).start()
+    yield b
+    b.stop()
+
+
+@pytest.fixture(params=["memory", "kafka"])
+def gw(request, kafka):
+    """Every case on the memory streaming cluster and on the in-tree Kafka broker (the
+    Java suite's KafkaProduceConsumeHandlerTest / KafkaGatewayResourceTest subclasses)."""
     made = []
 
     def make(topics, gateways):
-        g = GW(topics, gateways)
+        g = GW(topics, gateways, request.param, kafka.bootstrap if request.param == "kafka" else None)
         made.append(g)
         return g
     yield make
@@ -281,3 +293,39 @@ def test_send_events(gw):
         assert e["category"] == "Gateway" and e["timestamp"] > 0
         assert (e["source"]["tenant"], e["source"]["applicationId"]) == ("tenant1", "application1")
         assert e["data"]["options"] == {} and e["data"]["httpRequestHeaders"].get("host")
+
+
+def test_filter_out_messages_by_param_value(gw):
+    """ProduceConsumeHandlerTest.testFilterOutMessagesByParamValue: the producer stamps its
+    session id as header1, each consumer sees only its own session's records (one from
+    the earliest position, one from the latest)."""
+    import aiohttp
+    t = _topic()
+    g = gw([t], [
+        {"id": "produce", "type": "produce", "topic": t, "parameters": ["session-id"],
+         "produce-options": {"headers": [{"key": "header1", "value-from-parameters": "session-id"}]}},
+        {"id": "consume", "type": "consume", "topic": t, "parameters": ["session-id"],
+         "consume-options": {"filters": {"headers": [{"key": "header1", "value-from-parameters": "session-id"}]}}}])
+
+    async def go():
+        async with aiohttp.ClientSession() as s:
+            cons = f"{g.ws}/v1/consume/tenant1/application1/consume?param:session-id="
+            prod = f"{g.ws}/v1/produce/tenant1/application1/produce?param:session-id="
+            u1 = await _Collector().start(s, cons + "user1&option:position=earliest")
+            u2 = await _Collector().start(s, cons + "user2")
+            await _produce(s, prod + "user1", {"value": "this is a message for user1"})
+            await u1.wait(1)
+            assert u1.records() == [(None, "this is a message for user1", {"header1": "user1"})] and u2.msgs == []
+            await _produce(s, prod + "user1", {"value": "this is a message for user1, again"})
+            await u1.wait(2)
+            assert [v for _, v, _ in u1.records()] == ["this is a message for user1",
+                                                       "this is a message for user1, again"]
+            assert u2.msgs == []
+            await _produce(s, prod + "user2", {"value": "this is a message for user2"})
+            await u2.wait(1)
+            await asyncio.sleep(0.3)
+            assert u2.records() == [(None, "this is a message for user2", {"header1": "user2"})]
+            assert len(u1.msgs) == 2
+            for c in (u1, u2):
+                await c.close()
+    _run(go())
