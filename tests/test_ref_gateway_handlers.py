@@ -23,7 +23,7 @@ from langstream_amd.topics.kafka.broker import KafkaBroker
 from langstream_amd.topics.memory import reset_memlogs
 
 class GW:
-    def __init__(self, topics, gateways, streaming="memory", bootstrap=None):
+    def __init__(self, topics, gateways, streaming="memory", bootstrap=None, test_auth=None):
         reset_memlogs()
         module = {"module": "mod1", "id": "p",
                   "topics": [{"name": t, "creation-mode": "create-if-not-exists"} for t in topics]}
@@ -34,7 +34,7 @@ class GW:
         dep.setup("tenant1", dep.create_implementation("application1", app))
         store = InMemoryApplicationStore()
         store.put(StoredApplication("application1", "tenant1", app, files))
-        self.srv = GatewayServer(GatewayService(store), port=0).start()
+        self.srv = GatewayServer(GatewayService(store, test_auth=test_auth), port=0).start()
         self.ws = self.srv.url.replace("http", "ws")
         self.http = self.srv.url
 
@@ -56,8 +56,8 @@ def gw(request, kafka):
     Java suite's KafkaProduceConsumeHandlerTest / KafkaGatewayResourceTest subclasses)."""
     made = []
 
-    def make(topics, gateways):
-        g = GW(topics, gateways, request.param, kafka.bootstrap if request.param == "kafka" else None)
+    def make(topics, gateways, test_auth=None):
+        g = GW(topics, gateways, request.param, kafka.bootstrap if request.param == "kafka" else None, test_auth)
         made.append(g)
         return g
     yield make
@@ -329,3 +329,97 @@ def test_filter_out_messages_by_param_value(gw):
             for c in (u1, u2):
                 await c.close()
     _run(go())
+
+
+class _TestAuth:
+    """The Java suite's TestGatewayAuthenticationProvider (``test-auth``): credentials
+    starting with ``test-user-password`` log in as themselves."""
+
+    def __init__(self, configuration):
+        pass
+
+    def authenticate(self, ctx):
+        from langstream_amd.gateway.auth import AuthResult
+        c = ctx.credentials
+        if c is not None and c.startswith("test-user-password"):
+            return AuthResult(True, None, {"login": c})
+        return AuthResult(False, "Invalid credentials")
+
+
+def _auth_gateways(t, extra=()):
+    auth = {"provider": "test-auth", "allow-test-mode": True}
+    return [{"id": "produce", "type": "produce", "topic": t, "authentication": auth,
+             "produce-options": {"headers": [{"key": "header1", "value-from-authentication": "login"}]}},
+            {"id": "consume", "type": "consume", "topic": t, "authentication": auth,
+             "consume-options": {"filters": {"headers": [{"key": "header1", "value-from-authentication": "login"}]}}},
+            *extra]
+
+
+def test_authentication(gw, monkeypatch):
+    """ProduceConsumeHandlerTest.testAuthentication: 401 without / with bad credentials;
+    the login becomes the produced header and the consumer's filter."""
+    import aiohttp
+    from langstream_amd.gateway import auth
+    monkeypatch.setitem(auth.PROVIDERS, "test-auth", _TestAuth)
+    t = _topic()
+    g = gw([t], _auth_gateways(t))
+
+    async def go():
+        async with aiohttp.ClientSession() as s:
+            prod = f"{g.ws}/v1/produce/tenant1/application1/produce"
+            for q in ("", "?credentials=", "?credentials=error"):
+                with pytest.raises(aiohttp.WSServerHandshakeError) as e:
+                    await s.ws_connect(prod + q)
+                assert e.value.status == 401
+            ws = await s.ws_connect(prod + "?credentials=test-user-password")
+            await ws.close()
+            cons = f"{g.ws}/v1/consume/tenant1/application1/consume?option:position=earliest&credentials="
+            u1 = await _Collector().start(s, cons + "test-user-password")
+            u2 = await _Collector().start(s, cons + "test-user-password-2")
+            r = await _produce(s, prod + "?credentials=test-user-password", {"value": "hello user"})
+            assert r["status"] == "OK"
+            await u1.wait(1)
+            await asyncio.sleep(0.3)
+            assert u1.records() == [(None, "hello user", {"header1": "test-user-password"})] and u2.msgs == []
+            for c in (u1, u2):
+                await c.close()
+    _run(go())
+
+
+def test_test_credentials(gw, monkeypatch):
+    """ProduceConsumeHandlerTest.testTestCredentials: ``test-credentials`` go to the
+    gateway's test-mode provider (an HTTP check here, as in the Java suite); the principal
+    is the SHA-256 of the credentials; gateways without test mode and credentials the
+    provider rejects get 401."""
+    import aiohttp
+    from ref_runtime_harness import FakeHTTP
+    from langstream_amd.gateway import auth
+    monkeypatch.setitem(auth.PROVIDERS, "test-auth", _TestAuth)
+    fake = FakeHTTP()
+    fake.stub("GET", "/auth/tenant1", text="", headers={"Authorization": "Bearer test-user-password", "h1": "v1"})
+    t = _topic()
+    no_test = {"id": "consume-no-test", "type": "consume", "topic": t,
+               "authentication": {"provider": "test-auth", "allow-test-mode": False}}
+    g = gw([t], _auth_gateways(t, [no_test]),
+           test_auth=("http", {"base-url": fake.url, "path-template": "/auth/{tenant}", "headers": {"h1": "v1"}}))
+
+    async def go():
+        async with aiohttp.ClientSession() as s:
+            u1 = await _Collector().start(
+                s, f"{g.ws}/v1/consume/tenant1/application1/consume?test-credentials=test-user-password")
+            r = await _produce(s, f"{g.ws}/v1/produce/tenant1/application1/produce?test-credentials=test-user-password",
+                               {"value": "hello user"})
+            assert r["status"] == "OK"
+            await u1.wait(1)
+            assert u1.records() == [(None, "hello user", {
+                "header1": "9d75ff199d33e051209b59702de27d1e470eafb58ac6d8865788bf23b48e6818"})]
+            await u1.close()
+            for url in (f"{g.ws}/v1/consume/tenant1/application1/consume-no-test?test-credentials=test-user-password",
+                        f"{g.ws}/v1/produce/tenant1/application1/produce?test-credentials=test-user-password-but-wrong"):
+                with pytest.raises(aiohttp.WSServerHandshakeError) as e:
+                    await s.ws_connect(url)
+                assert e.value.status == 401
+    try:
+        _run(go())
+    finally:
+        fake.close()
