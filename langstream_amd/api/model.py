@@ -340,8 +340,13 @@ class KeyValueComparison:
         if n > 1:
             raise ValueError("Only one of 'value', 'valueFromParameters' or 'valueFromAuthentication' can be "
                              "specified for filter")
-        # no default for a missing key: the model keeps it null (ModelBuilderTest.testParseGateway)
-        # and the gateway refuses it when the gateway is used (ProduceGateway / ConsumeGateway)
+        # a missing key is named after the value / parameter / authentication field
+        # (Gateway.KeyValueComparison's canonical constructor, Gateway.java:97-108; the
+        # ModelBuilderTest expectations go through the same constructor)
+        if self.key is None:
+            self.key = self.value if self.value is not None else (
+                self.value_from_parameters if self.value_from_parameters is not None
+                else self.value_from_authentication)
 
     @staticmethod
     def from_dict(d: dict) -> "KeyValueComparison":

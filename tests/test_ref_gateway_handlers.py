@@ -423,3 +423,28 @@ def test_test_credentials(gw, monkeypatch):
         _run(go())
     finally:
         fake.close()
+
+
+def test_chat_gateway(gw):
+    """ProduceConsumeHandlerTest.testChatGateway: questions and answers on one topic; a
+    header comparison without a key is named after its parameter."""
+    import aiohttp
+    t = _topic()
+    g = gw([t], [{"id": "chat", "type": "chat", "chat-options": {
+        "questions-topic": t, "answers-topic": t, "headers": [{"value-from-parameters": "session"}]}}])
+
+    async def go():
+        async with aiohttp.ClientSession() as s:
+            ws = await s.ws_connect(f"{g.ws}/v1/chat/tenant1/application1/chat?param:session=s1")
+            await asyncio.sleep(0.3)
+            await ws.send_str(json.dumps({"value": "this is a message"}))
+            records = []
+            for _ in range(4):
+                m = json.loads((await ws.receive(timeout=10)).data)
+                if "record" in m:
+                    records.append((m["record"]["key"], m["record"]["value"], m["record"]["headers"]))
+                    break
+                assert m["status"] == "OK"      # the produce acknowledgement
+            await ws.close()
+            assert records == [(None, "this is a message", {"session": "s1"})]
+    _run(go())
