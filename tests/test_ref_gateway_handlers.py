@@ -28,7 +28,7 @@ class GW:
         module = {"module": "mod1", "id": "p",
                   "topics": [{"name": t, "creation-mode": "create-if-not-exists"} for t in topics]}
         files = {"module.yaml": yaml.safe_dump(module), "gateways.yaml": yaml.safe_dump({"gateways": gateways})}
-        app = build_application_instance(files, instance_yaml(streaming, bootstrap), None).application
+        app = self.app = build_application_instance(files, instance_yaml(streaming, bootstrap), None).application
         # prepareTopicsForTest: the topics exist before any client connects
         dep = ApplicationDeployer()
         dep.setup("tenant1", dep.create_implementation("application1", app))
@@ -448,3 +448,58 @@ def test_chat_gateway(gw):
             await ws.close()
             assert records == [(None, "this is a message", {"session": "s1"})]
     _run(go())
+
+
+def test_http_service(gw):
+    """GatewayResourceTest.testService: a service gateway writes the request to the input
+    topic and answers with the record that comes back on the output topic (an echo
+    exchange between the two topics here, as in the Java test), key / value / headers as
+    sent plus the gateway's correlation header; 100 requests from 10 threads."""
+    import threading
+    from concurrent.futures import ThreadPoolExecutor
+    from langstream_amd.api.topics import TopicConnectionsRuntimeRegistry
+    tin, tout = _topic(), _topic()
+    g = gw([tin, tout], [{"id": "svc", "type": "service",
+                          "service-options": {"input-topic": tin, "output-topic": tout}}])
+    sc = g.app.instance.streaming_cluster
+    rt = TopicConnectionsRuntimeRegistry.get(sc)
+    stop = threading.Event()
+
+    def exchange():
+        cons = rt.create_consumer("exchange", sc, {"topic": tin, "subscriptionName": "s"})
+        prod = rt.create_producer("exchange", sc, {"topic": tout})
+        cons.start()
+        prod.start()
+        try:
+            while not stop.is_set():
+                recs = cons.read()
+                for r in recs:
+                    prod.write(r).result(10)
+                if recs:
+                    cons.commit(recs)
+        finally:
+            cons.close()
+            prod.close()
+    th = threading.Thread(target=exchange, daemon=True)
+    th.start()
+    url = f"{g.http}/api/gateways/service/tenant1/application1/svc"
+
+    def call(body, ctype="application/json"):
+        r = requests.post(url, data=body, headers={"Content-Type": ctype}, timeout=60)
+        assert r.status_code == 200, r.text
+        rec = r.json()["record"]
+        hs = dict(rec["headers"])
+        assert hs.pop("langstream-service-request-id")      # the correlation header comes back
+        return rec["key"], rec["value"], hs
+    try:
+        assert call('{"key": "my-key", "value": "my-value"}') == ("my-key", "my-value", {})
+        assert call('{"key": "my-key2", "value": "my-value"}') == ("my-key2", "my-value", {})
+        assert call("my-text", "text/plain") == (None, "my-text", {})
+        assert call('{"key": "my-key2", "value": "my-value", "headers": {"header1": "value1"}}') == \
+            ("my-key2", "my-value", {"header1": "value1"})
+        with ThreadPoolExecutor(10) as ex:
+            outs = list(ex.map(lambda _: call('{"key": "my-key", "value": "my-value"}'), range(100)))
+        assert outs == [("my-key", "my-value", {})] * 100
+    finally:
+        stop.set()
+        th.join(10)
