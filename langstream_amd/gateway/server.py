@@ -138,26 +138,83 @@ def common_headers(kvs: Optional[List[KeyValueComparison]], ctx: RequestContext)
     return out
 
 
+class _SharedProducer:
+    """A cached topic producer that sessions keep using after the cache evicts it
+    (``LRUTopicProducerCache``'s reference-counted handles, LRUTopicProducerCacheTest):
+    an evicted producer closes once its in-flight writes finish, and a session that writes
+    through it later reopens it for that write instead of failing on a closed producer."""
+
+    def __init__(self, factory):
+        self._factory = factory
+        self._lock = threading.Lock()
+        self._p = factory()
+        self._inflight = 0
+        self._evicted = False
+
+    def write(self, record):
+        with self._lock:
+            if self._p is None:
+                self._p = self._factory()
+            self._inflight += 1
+            p = self._p
+        try:
+            fut = p.write(record)
+        except BaseException:
+            self._done(None)
+            raise
+        fut.add_done_callback(self._done)
+        return fut
+
+    def _done(self, _f) -> None:
+        close = None
+        with self._lock:
+            self._inflight -= 1
+            if self._evicted and self._inflight == 0 and self._p is not None:
+                close, self._p = self._p, None
+        if close is not None:
+            _close_quietly(close)
+
+    def evict(self) -> None:
+        close = None
+        with self._lock:
+            self._evicted = True
+            if self._inflight == 0 and self._p is not None:
+                close, self._p = self._p, None
+        if close is not None:
+            _close_quietly(close)
+
+    @property
+    def closed(self) -> bool:
+        return self._p is None
+
+    def __getattr__(self, name):
+        return getattr(self._p, name)
+
+
+def _close_quietly(p) -> None:
+    try:
+        p.close()
+    except Exception:  # noqa: BLE001
+        pass
+
+
 class _ProducerCache:
     def __init__(self, size: int = 100):
         self.size = size
-        self._d: "OrderedDict[tuple, Any]" = OrderedDict()
+        self._d: "OrderedDict[tuple, _SharedProducer]" = OrderedDict()
         self._lock = threading.Lock()
 
-    def get_or_create(self, key: tuple, factory):
+    def get_or_create(self, key: tuple, factory) -> _SharedProducer:
         with self._lock:
             p = self._d.get(key)
             if p is not None:
                 self._d.move_to_end(key)
                 return p
-            p = factory()
+            p = _SharedProducer(factory)
             self._d[key] = p
             while len(self._d) > self.size:
                 _, old = self._d.popitem(last=False)
-                try:
-                    old.close()
-                except Exception:  # noqa: BLE001
-                    pass
+                old.evict()
             return p
 
 

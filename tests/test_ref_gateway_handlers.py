@@ -503,3 +503,53 @@ def test_http_service(gw):
     finally:
         stop.set()
         th.join(10)
+
+
+def test_producer_cache_eviction_keeps_sessions_working():
+    """LRUTopicProducerCacheTest (testGetOrCreate / testConcurrency): producers are shared
+    per key, at most ``size`` stay cached, and an evicted producer still serves the
+    sessions holding it -- it closes when idle and reopens for a later write."""
+    import threading
+    from concurrent.futures import Future, ThreadPoolExecutor
+    from langstream_amd.gateway.server import _ProducerCache
+    opened, closed = [], []
+
+    class P:
+        def __init__(self):
+            self.closed = False
+            opened.append(self)
+
+        def write(self, rec):
+            assert not self.closed, "write on a closed producer"
+            f = Future()
+            f.set_result(None)
+            return f
+
+        def close(self):
+            self.closed = True
+            closed.append(self)
+    cache = _ProducerCache(2)
+    first = cache.get_or_create(("t", "a", "g"), P)
+    assert cache.get_or_create(("t", "a", "g"), P) is first and len(opened) == 1
+    second = cache.get_or_create(("t", "a", "g2"), P)
+    assert len(opened) == 2 and not closed
+    cache.get_or_create(("t", "a", "g3"), P)             # evicts "g" (idle): closed now
+    assert len(opened) == 3 and len(closed) == 1 and first.closed
+    first.write("x").result(1)                           # a session still holding it: reopened
+    assert len(opened) == 4 and len(closed) == 2 and first.closed   # ... and closed once idle
+    assert cache.get_or_create(("t", "a", "g"), P) is not first and len(cache._d) == 2
+    assert second.closed and len(closed) == 3          # "g2" was evicted in turn
+
+    cache = _ProducerCache(2)
+    errors = []
+
+    def worker(i):
+        try:
+            for j in range(50):
+                cache.get_or_create(("t", "a", f"g{(i + j) % 5}"), P).write(j).result(1)
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+    with ThreadPoolExecutor(50) as ex:
+        list(ex.map(worker, range(50)))
+    assert not errors and len(cache._d) == 2
+    _ = threading
