@@ -23,7 +23,7 @@ from langstream_amd.topics.kafka.broker import KafkaBroker
 from langstream_amd.topics.memory import reset_memlogs
 
 class GW:
-    def __init__(self, topics, gateways, streaming="memory", bootstrap=None, test_auth=None):
+    def __init__(self, topics, gateways, streaming="memory", bootstrap=None, test_auth=None, resolver=None):
         reset_memlogs()
         module = {"module": "mod1", "id": "p",
                   "topics": [{"name": t, "creation-mode": "create-if-not-exists"} for t in topics]}
@@ -34,7 +34,8 @@ class GW:
         dep.setup("tenant1", dep.create_implementation("application1", app))
         store = InMemoryApplicationStore()
         store.put(StoredApplication("application1", "tenant1", app, files))
-        self.srv = GatewayServer(GatewayService(store, test_auth=test_auth), port=0).start()
+        self.srv = GatewayServer(GatewayService(store, test_auth=test_auth, service_url_resolver=resolver),
+                                 port=0).start()
         self.ws = self.srv.url.replace("http", "ws")
         self.http = self.srv.url
 
@@ -553,3 +554,36 @@ def test_producer_cache_eviction_keeps_sessions_working():
         list(ex.map(worker, range(50)))
     assert not errors and len(cache._d) == 2
     _ = threading
+
+
+def test_service_agent(tmp_path):
+    """ServiceAgentGatewayResourceTest.testServiceAgent: a service gateway naming an agent
+    proxies method, path, query, headers and body to the agent's service endpoint."""
+    from ref_runtime_harness import FakeHTTP
+    fake = FakeHTTP()
+    fake.stub("POST", "/agent-endpoint/custom-path", text="agent response")
+    fake.stub("POST", "/agent-endpoint/custom-path-json?q=v", text="agent response",
+              headers={"X-Custom-Header": "XXX", "Content-Type": "application/json"})
+    fake.stub("POST", "/", body="hello", text="agent response ROOT")
+    for m in ("GET", "PUT", "DELETE"):
+        fake.stub(m, "/", text="agent response ROOT")
+    g = GW([], [{"id": "svc", "type": "service", "service-options": {"agent-id": "my-agent"}}],
+           resolver=lambda tenant, app, agent: fake.url)
+    try:
+        url = f"{g.http}/api/gateways/service/tenant1/application1/svc"
+        r = requests.post(url, data="hello", headers={"Content-Type": "text/plain"}, timeout=30)
+        assert (r.status_code, r.text) == (200, "agent response ROOT")
+        for m in ("GET", "PUT", "DELETE"):
+            r = requests.request(m, url, data="hello", headers={"Content-Type": "text/plain"}, timeout=30)
+            assert (r.status_code, r.text) == (200, "agent response ROOT")
+        r = requests.post(url + "/not-found", data="hello", headers={"Content-Type": "text/plain"}, timeout=30)
+        assert r.status_code == 404
+        r = requests.post(url + "/agent-endpoint/custom-path", data="hello",
+                          headers={"Content-Type": "text/plain"}, timeout=30)
+        assert (r.status_code, r.text) == (200, "agent response")
+        r = requests.post(url + "/agent-endpoint/custom-path-json?q=v", data="hello",
+                          headers={"Content-Type": "application/json", "X-Custom-Header": "XXX"}, timeout=30)
+        assert (r.status_code, r.text) == (200, "agent response")
+    finally:
+        g.close()
+        fake.close()
