@@ -86,10 +86,11 @@ class _Collector:
     def __init__(self):
         self.msgs = []
 
-    async def start(self, s, url):
+    async def start(self, s, url, settle=True):
         self.ws = await s.ws_connect(url)
         self.task = asyncio.ensure_future(self._loop())
-        await asyncio.sleep(0.3)     # the reader is positioned before anything is produced
+        if settle:
+            await asyncio.sleep(0.3)     # the reader is positioned before anything is produced
         return self
 
     async def _loop(self):
@@ -587,3 +588,29 @@ def test_service_agent(tmp_path):
     finally:
         g.close()
         fake.close()
+
+
+def test_concurrent_consume(gw):
+    """ProduceConsumeHandlerTest.testConcurrentConsume: 50 consumers from the earliest
+    position each get every record, in order."""
+    import aiohttp
+    t = _topic()
+    g = gw([t], [{"id": "produce", "type": "produce", "topic": t}, {"id": "consume", "type": "consume", "topic": t}])
+
+    async def go():
+        async with aiohttp.ClientSession() as s:
+            cons = f"{g.ws}/v1/consume/tenant1/application1/consume?option:position=earliest"
+            clients = [await _Collector().start(s, cons, settle=False) for _ in range(50)]
+            await asyncio.sleep(0.5)
+            prod = f"{g.ws}/v1/produce/tenant1/application1/produce"
+            await _produce(s, prod, {"value": "msg1"})
+            for c in clients:
+                await c.wait(1)
+                assert c.records() == [(None, "msg1", {})]
+            await _produce(s, prod, {"value": "msg2"})
+            for c in clients:
+                await c.wait(2)
+                assert c.records() == [(None, "msg1", {}), (None, "msg2", {})]
+            for c in clients:
+                await c.close()
+    _run(go())
