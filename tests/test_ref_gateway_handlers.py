@@ -1,6 +1,7 @@
 """The reference's gateway handler tests, ported (``langstream-api-gateway/src/test/java/ai/
 langstream/apigateway/``: ``websocket/handlers/ProduceConsumeHandlerTest`` and
-``http/GatewayResourceTest``), on the memory streaming cluster and the in-tree Kafka broker.  Each case builds the
+``http/GatewayResourceTest``), on the memory streaming cluster, the in-tree Kafka broker and the Pulsar stand-in (the Java
+suite's Kafka and Pulsar subclasses).  Each case builds the
 application the Java test builds (one module, the case's topics, the case's gateways) and
 talks to the gateway over WebSockets / HTTP.
 
@@ -51,14 +52,24 @@ def kafka():
     b.stop()
 
 
-@pytest.fixture(params=["memory", "kafka"])
-def gw(request, kafka):
-    """Every case on the memory streaming cluster and on the in-tree Kafka broker (the
-    Java suite's KafkaProduceConsumeHandlerTest / KafkaGatewayResourceTest subclasses)."""
+@pytest.fixture(scope="module")
+def pulsar():
+    from langstream_amd.topics.pulsar.standalone import PulsarStandalone
+    b = PulsarStandalone().start()
+    yield b
+    b.stop()
+
+
+@pytest.fixture(params=["memory", "kafka", "pulsar"])
+def gw(request, kafka, pulsar):
+    """Every case on the memory streaming cluster, the in-tree Kafka broker and the Pulsar
+    stand-in (the Java suite's Kafka* / Pulsar* ProduceConsumeHandlerTest and
+    GatewayResourceTest subclasses)."""
     made = []
 
     def make(topics, gateways, test_auth=None):
-        g = GW(topics, gateways, request.param, kafka.bootstrap if request.param == "kafka" else None, test_auth)
+        boot = {"kafka": kafka.bootstrap, "pulsar": (pulsar.web_url, pulsar.service_url, "public", "default")}
+        g = GW(topics, gateways, request.param, boot.get(request.param), test_auth)
         made.append(g)
         return g
     yield make
