@@ -464,3 +464,47 @@ def test_github_download_cache_update_and_fallback(tmp_path, monkeypatch):
     monkeypatch.setattr(sources, "_cloned", {})
     d = sources.download_github("https://localhost/LangStream/langstream2/tree/main/examples", use_cache=True)
     assert content(d) == "content! main" and not (home / "ghrepos").exists()
+
+
+# ---------------------------------------------------------------- AbstractDeployApplicationCmdTest
+def test_remote_file():
+    """AbstractDeployApplicationCmdTest.testRemoteFile"""
+    from ref_runtime_harness import FakeHTTP
+    fake = FakeHTTP()
+    fake.stub("GET", "/my-remote-dir/my-remote-file", text="content!")
+    try:
+        assert open(sources.download_https(fake.url + "/my-remote-dir/my-remote-file")).read() == "content!"
+        with pytest.raises(RuntimeError, match="Received status code: 404"):
+            sources.download_https(fake.url + "/unknown")
+    finally:
+        fake.close()
+
+
+def test_dependencies(tmp_path):
+    """AbstractDeployApplicationCmdTest.testDependencies: a wrong or empty checksum fails
+    after the download, a missing type fails, two dependencies with the right SHA-512
+    download (the second finds the first's file already there)."""
+    from ref_runtime_harness import FakeHTTP
+    fake = FakeHTTP()
+    fake.stub("GET", "/the-dep.jar", text="content!")
+    sha = ("bed0f8673c13f8431d5e4f5e4a0e496b2eddc4a18e03cff19256964a6132521a485afa59ace702b76c2832274d1c3914e3fec0221"
+           "fee9d698eaedc7f5810a284")
+    url = fake.url + "/the-dep.jar"
+
+    def run(deps):
+        d = tmp_path / f"app{len(list(tmp_path.iterdir()))}"
+        d.mkdir()
+        (d / "configuration.yaml").write_text(yaml.safe_dump({"configuration": {"dependencies": deps}}))
+        sources.download_dependencies(str(d), lambda m: None)
+        return d
+    try:
+        for bad in ("-", ""):
+            with pytest.raises(IOError, match=f"File at {url}, seems corrupted"):
+                run([{"name": "My dep", "url": url, "sha512sum": bad, "type": "java-library"}])
+        with pytest.raises(RuntimeError, match="dependency type must be set"):
+            run([{"name": "My dep", "url": url}])
+        d = run([{"name": "My dep", "url": url, "sha512sum": sha, "type": "java-library"},
+                 {"name": "My dep2", "url": url, "sha512sum": sha, "type": "java-library"}])
+        assert (d / "java" / "lib" / "the-dep.jar").read_text() == "content!"
+    finally:
+        fake.close()
