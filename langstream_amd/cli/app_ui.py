@@ -328,18 +328,41 @@ class AppUIServer:
         self._thread.join(10)
 
 
+def check_and_launch(open_command: str, port: int) -> bool:
+    """``UIAppCmd.checkAndLaunch``: run ``<open_command> http://localhost:<port>`` when the
+    command exists on disk; False when it does not or cannot start."""
+    import subprocess
+    if not os.path.exists(open_command):
+        return False
+    try:
+        subprocess.Popen([open_command, f"http://localhost:{port}"], stdout=subprocess.DEVNULL,
+                         stderr=subprocess.DEVNULL, start_new_session=True)
+        return True
+    except OSError:
+        return False
+
+
+def open_browser_at_port(port: int) -> bool:
+    """``UIAppCmd.openBrowserAtPort``: xdg-open on Linux, the platform browser elsewhere."""
+    import sys
+    if sys.platform.startswith("linux"):
+        return check_and_launch("/usr/bin/xdg-open", port)
+    try:
+        import webbrowser
+        return bool(webbrowser.open(f"http://localhost:{port}"))
+    except Exception:  # noqa: BLE001
+        return False
+
+
 def serve_forever(client, app_id: str, api_gateway_url: str, tenant: str, port: int = 8092,
                   open_browser: bool = True) -> int:
     client.get(app_id)                      # fail fast: the application must exist
     srv = AppUIServer(client, app_id, api_gateway_url, tenant, host="0.0.0.0", port=port).start()
-    print(f"Starting UI at {srv.url}", flush=True)
-    if open_browser:
-        try:
-            import webbrowser
-            if not webbrowser.open(srv.url):
-                print(f"Could not start a browser: open {srv.url} manually", flush=True)
-        except Exception:  # noqa: BLE001
-            print(f"Could not start a browser: open {srv.url} manually", flush=True)
+    if open_browser and open_browser_at_port(srv.port):
+        print(f"Started UI at http://localhost:{srv.port}", flush=True)
+    else:
+        print("Could not Start browser.  Either add the proper command to your OS (open for mac or xdg-open for "
+              f"linux) or start a browser manually at http://localhost:{srv.port}", flush=True)
     stop = threading.Event()
     try:
         import signal

@@ -508,3 +508,15 @@ def test_dependencies(tmp_path):
         assert (d / "java" / "lib" / "the-dep.jar").read_text() == "content!"
     finally:
         fake.close()
+
+
+# ---------------------------------------------------------------- UIAppCmdTest
+def test_open_browser(tmp_path):
+    """UIAppCmdTest.openBrowser: an open command that exists is launched, one that does
+    not is reported as not launched."""
+    from langstream_amd.cli.app_ui import check_and_launch
+    exe = tmp_path / "open-cmd"
+    exe.write_text("#!/bin/sh\necho hello\n")
+    exe.chmod(0o500)
+    assert check_and_launch(str(exe), 80) is True
+    assert check_and_launch("_no_such_command_", 80) is False
