@@ -67,16 +67,14 @@ class ApplicationDeployer:
     def create_implementation(self, application_id: str, application: Application) -> ExecutionPlan:
         """Resources are validated when an agent or asset uses them (the reference builds a
         resource's configuration only through ``getResourceImplementation``, called by the
-        agent / asset providers: BasicClusterRuntime.java:150-157); an unused resource only
-        needs a known type."""
-        from .resources import RESOURCE_TYPES, validate_resource
+        agent / asset providers: BasicClusterRuntime.java:150-157); an unused resource is not
+        looked at, whatever its type (ApplicationDeployerTest.testDeploy)."""
+        from .resources import validate_resource
         resolved = resolve_placeholders(application)
         used = referenced_resources(resolved)
         for key, r in resolved.resources.items():
             if key in used or r.id in used or r.name in used:
                 validate_resource(r)
-            elif r.type not in RESOURCE_TYPES:
-                raise ValueError(f"Resource type {r.type} is not supported; known: {sorted(RESOURCE_TYPES)}")
         return self.planner.build_execution_plan(application_id, resolved)
 
     def setup(self, tenant: str, plan: ExecutionPlan) -> None:
