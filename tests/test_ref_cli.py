@@ -1,6 +1,7 @@
 """The reference CLI's command tests, ported
 (``langstream-cli/src/test/java/ai/langstream/cli/commands/applications/``:
-``ProfilesCmdTest``, ``TenantsCmdTest``, ``AppsCmdTest``, ``GithubRepositoryDownloaderTest``).
+``ProfilesCmdTest``, ``TenantsCmdTest``, ``AppsCmdTest``, ``GithubRepositoryDownloaderTest``,
+``AbstractDeployApplicationCmdTest``, ``UIAppCmdTest``).
 
 Each case runs the CLI in-process as ``CommandTestBase.executeCommand`` does: ``--conf`` a
 fresh ``cli.yaml`` whose default profile points at a stub control plane (WireMock there,
